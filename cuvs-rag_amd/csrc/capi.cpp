@@ -1,0 +1,767 @@
+// mivs C-ABI (include/mivs.h): index objects and the build / search pipelines.
+//
+// Build  (replaces cuvs ivf_flat::build, index_building_coordinator.py:392-396):
+//   trainset rows -> strided init -> n_iters x {pack centroids, K4 assign (scan
+//   k=1), stable counting sort, K5 fp64 update} -> K4 assign of every row ->
+//   stable counting sort -> K6 pack of the interleaved lists.
+// Search (replaces cuvs ivf_flat::search, improved_multi_gpu_rag.py:225-227):
+//   query norms -> coarse scan over the centroid list (k = n_probes) -> probe
+//   map (list -> query buckets, work items, output slots) -> K3 fine scan ->
+//   K7 merge of the per-(probe, chunk) partials.
+// Everything is enqueued on the caller's stream; the only host syncs are in
+// build (list sizes) and in stats collection when profiling is on.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <memory>
+#include <cstring>
+#include <mutex>
+#include <numeric>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/mivs.h"
+#include "mivs_common.hpp"
+
+using namespace mivs;
+
+namespace {
+
+thread_local std::string g_err;
+std::atomic<int> g_profiling{0};
+
+struct MivsError : std::runtime_error {
+  int code;
+  MivsError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+void hipchk(hipError_t e, const char* what) {
+  if (e == hipSuccess) return;
+  (void)hipGetLastError();
+  const int code = e == hipErrorOutOfMemory ? MIVS_ERR_OOM : MIVS_ERR_HIP;
+  int dev = -1;
+  (void)hipGetDevice(&dev);
+  throw MivsError(code, std::string(what) + ": " + hipGetErrorString(e) + " (device " + std::to_string(dev) + ")");
+}
+#define HIPCHK(x) hipchk((x), #x)
+
+void require(bool ok, const std::string& msg, int code = MIVS_ERR_INVALID) {
+  if (!ok) throw MivsError(code, msg);
+}
+
+template <class F>
+int32_t guarded(F&& f) {
+  try {
+    f();
+    return MIVS_OK;
+  } catch (const MivsError& e) {
+    g_err = e.what();
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    g_err = "host allocation failed";
+    return MIVS_ERR_OOM;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return MIVS_ERR_HIP;
+  }
+}
+
+// owning device buffer (grow-only when reused as workspace)
+struct Buf {
+  void* p = nullptr;
+  size_t n = 0;
+  Buf() = default;
+  Buf(const Buf&) = delete;
+  Buf& operator=(const Buf&) = delete;
+  ~Buf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  void reserve(size_t bytes) {
+    if (bytes <= n && p) return;
+    if (p) HIPCHK(hipDeviceSynchronize());  // in-flight work may still use the old workspace
+    release();
+    HIPCHK(hipMalloc(&p, bytes > 0 ? bytes : 16));
+    n = bytes;
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+int cu_count(int device) {
+  static std::mutex mu;
+  static std::vector<int> cache;
+  std::lock_guard<std::mutex> g(mu);
+  if ((int)cache.size() <= device) cache.resize(device + 1, 0);
+  if (cache[device] == 0) {
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    cache[device] = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  }
+  return cache[device];
+}
+
+// A set of inverted lists in the interleaved group layout.
+struct ListSet {
+  int n_lists = 0;
+  int64_t n_rows = 0, n_groups = 0;
+  Buf groups, norms, ids, off, goff;
+  std::vector<int64_t> h_off, h_goff;
+  std::vector<int64_t> top_chunks_prefix;  // prefix sums of chunk counts sorted descending
+
+  int64_t chunks_of(int l, int G) const { return ceil_div(h_goff[l + 1] - h_goff[l], G); }
+  void finalize_host(int G) {
+    std::vector<int64_t> c(n_lists);
+    for (int l = 0; l < n_lists; ++l) c[l] = chunks_of(l, G);
+    std::sort(c.begin(), c.end(), std::greater<int64_t>());
+    top_chunks_prefix.assign(n_lists + 1, 0);
+    for (int l = 0; l < n_lists; ++l) top_chunks_prefix[l + 1] = top_chunks_prefix[l] + c[l];
+  }
+};
+
+// Pack rows into `ls` given list row offsets (host) and an optional permutation.
+void pack_lists(ListSet& ls, const float* src, int d, int dp, const int64_t* perm_d, const std::vector<int64_t>& h_off,
+                int64_t id_offset, const int64_t* id_map, int G, hipStream_t s) {
+  ls.n_lists = (int)h_off.size() - 1;
+  ls.n_rows = h_off.back();
+  ls.h_off = h_off;
+  ls.h_goff.assign(ls.n_lists + 1, 0);
+  for (int l = 0; l < ls.n_lists; ++l)
+    ls.h_goff[l + 1] = ls.h_goff[l] + ceil_div(h_off[l + 1] - h_off[l], kGroupRows);
+  ls.n_groups = ls.h_goff.back();
+  require(ls.n_groups * (int64_t)kGroupRows < (int64_t)INT32_MAX, "index too large for 32-bit row positions",
+          MIVS_ERR_UNSUPPORTED);
+  const int64_t nslot = std::max<int64_t>(ls.n_groups, 1) * kGroupRows;
+  ls.groups.reserve(sizeof(float) * (size_t)nslot * dp);
+  ls.norms.reserve(sizeof(float) * (size_t)nslot);
+  ls.ids.reserve(sizeof(int64_t) * (size_t)nslot);
+  ls.off.reserve(sizeof(int64_t) * (ls.n_lists + 1));
+  ls.goff.reserve(sizeof(int64_t) * (ls.n_lists + 1));
+  HIPCHK(hipMemcpyAsync(ls.off.p, h_off.data(), sizeof(int64_t) * (ls.n_lists + 1), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(ls.goff.p, ls.h_goff.data(), sizeof(int64_t) * (ls.n_lists + 1), hipMemcpyHostToDevice, s));
+  Buf group_list;
+  if (ls.n_lists > 1) {
+    group_list.reserve(sizeof(int) * (size_t)std::max<int64_t>(ls.n_groups, 1));
+    HIPCHK(launch_group_list(ls.goff.as<int64_t>(), ls.n_lists, ls.n_groups, group_list.as<int>(), s));
+  }
+  HIPCHK(launch_pack_groups(src, 0, d, dp, perm_d, ls.off.as<int64_t>(), ls.goff.as<int64_t>(),
+                            ls.n_lists > 1 ? group_list.as<int>() : nullptr, ls.n_groups, ls.groups.as<float>(),
+                            ls.norms.as<float>(), ls.ids.as<int64_t>(), id_map, id_offset, s));
+  ls.finalize_host(G);
+  HIPCHK(hipStreamSynchronize(s));  // host vectors above are referenced by the async copies
+}
+
+struct Workspace {
+  Buf qn, bucket_q, bucket_slot, bucket_off, work_off, counter, part_d, part_i, slot_begin, probes_d, probes_i,
+      counts, fill, qp_slots, scan_tmp, gmerge;
+};
+
+struct Events {
+  hipEvent_t e[6] = {};
+  bool ok = false;
+  void create() {
+    if (ok) return;
+    for (auto& x : e) HIPCHK(hipEventCreate(&x));
+    ok = true;
+  }
+  ~Events() {
+    if (ok)
+      for (auto& x : e) (void)hipEventDestroy(x);
+  }
+};
+
+}  // namespace
+
+struct mivs_index_s {
+  int kind = 0;  // 0 = ivf_flat, 1 = brute force
+  int device = 0, d = 0, dp = 0, metric = 0, G = kDefaultChunkGroups;
+  int64_t id_offset = 0;
+  ListSet lists;  // data
+  ListSet cents;  // IVF: the centroid "list"
+  Buf centroids_rm;
+  std::mutex mu;
+  Workspace ws;
+  Events ev;
+  mivs_search_stats stats{};
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    HIPCHK(hipGetDevice(&prev));
+    if (prev != dev) HIPCHK(hipSetDevice(dev));
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur != prev && prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// ---- one scan job: lists x buckets -> partial slots ----
+struct ScanJob {
+  const ListSet* ls;
+  int G;
+  const float* queries;
+  const float* qnorms;
+  int d, dp, k, metric;
+  const int64_t* bucket_q;
+  const int64_t* bucket_slot;
+  const int* bucket_off;
+  const int* work_off;
+  float* out_d;
+  int64_t* out_i;
+};
+
+void run_scan(const ScanJob& j, int device, Workspace& ws, hipStream_t s) {
+  const int kcap = scan_kcap(j.k);
+  require(kcap > 0, "k must be in [1, " + std::to_string(kMaxK) + "]", MIVS_ERR_UNSUPPORTED);
+  require(j.dp <= 1024, "dim > 1024 is not supported by this build", MIVS_ERR_UNSUPPORTED);
+  const size_t lds = scan_lds_bytes(j.dp, kcap);
+  const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / lds)));
+  const int grid = cu_count(device) * per_cu;
+  float* gmerge = nullptr;
+  if (!scan_merge_in_lds(j.dp, kcap)) {
+    ws.gmerge.reserve(scan_gmerge_bytes(grid, kcap));
+    gmerge = ws.gmerge.as<float>();
+  }
+  ws.counter.reserve(16);
+  HIPCHK(hipMemsetAsync(ws.counter.p, 0, sizeof(int), s));
+  ScanArgs a{};
+  a.groups = j.ls->groups.as<float>();
+  a.row_norms = j.ls->norms.as<float>();
+  a.row_ids = j.ls->ids.as<int64_t>();
+  a.list_goff = j.ls->goff.as<int64_t>();
+  a.n_lists = j.ls->n_lists;
+  a.chunk_groups = j.G;
+  a.queries = j.queries;
+  a.qnorms = j.qnorms;
+  a.bucket_q = j.bucket_q;
+  a.bucket_slot = j.bucket_slot;
+  a.bucket_off = j.bucket_off;
+  a.work_off = j.work_off;
+  a.work_counter = ws.counter.as<int>();
+  a.out_d = j.out_d;
+  a.out_i = j.out_i;
+  a.d = j.d;
+  a.dp = j.dp;
+  a.k = j.k;
+  a.metric = j.metric;
+  HIPCHK(launch_scan_ex(a, kcap, grid, lds, gmerge, s));
+}
+
+// single-list job (brute force, coarse probe selection, k-means assign):
+// every query (or every row id of `rows`) against every row of `ls`.
+// Writes [nq][k] results into (out_d, out_i) (merging chunk partials if needed).
+void single_list_topk(const ListSet& ls, int G, const float* queries, const float* qnorms, const int64_t* rows,
+                      int64_t nq, int d, int dp, int k, int metric, float* out_d, int64_t* out_i, int device,
+                      Workspace& ws, hipStream_t s) {
+  const int64_t chunks = std::max<int64_t>(1, ceil_div(ls.n_groups, G));
+  require(ceil_div(nq, kQTile) * chunks < (int64_t)INT32_MAX, "too many work items", MIVS_ERR_UNSUPPORTED);
+  ws.bucket_q.reserve(sizeof(int64_t) * nq);
+  ws.bucket_slot.reserve(sizeof(int64_t) * nq);
+  ws.bucket_off.reserve(sizeof(int) * 2);
+  ws.work_off.reserve(sizeof(int) * 2);
+  HIPCHK(launch_single_list_job(nq, chunks, ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(),
+                                ws.bucket_off.as<int>(), ws.work_off.as<int>(), nullptr, s));
+  if (rows) HIPCHK(hipMemcpyAsync(ws.bucket_q.p, rows, sizeof(int64_t) * nq, hipMemcpyDeviceToDevice, s));
+  float* pd = out_d;
+  int64_t* pi = out_i;
+  if (chunks > 1) {
+    ws.part_d.reserve(sizeof(float) * (size_t)(nq * chunks * k));
+    ws.part_i.reserve(sizeof(int64_t) * (size_t)(nq * chunks * k));
+    pd = ws.part_d.as<float>();
+    pi = ws.part_i.as<int64_t>();
+  }
+  ScanJob j{&ls, G, queries, qnorms, d, dp, k, metric, ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(),
+            ws.bucket_off.as<int>(), ws.work_off.as<int>(), pd, pi};
+  run_scan(j, device, ws, s);
+  if (chunks > 1) {
+    MergeArgs m{};
+    m.in_d = pd;
+    m.in_i = pi;
+    m.slot_begin = nullptr;
+    m.slots_per_q = chunks;
+    m.nq = nq;
+    m.k_in = k;
+    m.k = k;
+    m.metric = metric;
+    m.out_d = out_d;
+    m.out_i = out_i;
+    HIPCHK(launch_merge(m, s));
+  }
+}
+
+void make_single_list(ListSet& ls, const float* src, int64_t n, int d, int dp, int64_t id_offset, int G,
+                      hipStream_t s) {
+  std::vector<int64_t> off = {0, n};
+  pack_lists(ls, src, d, dp, nullptr, off, id_offset, nullptr, G, s);
+}
+
+// K4 assign of rows (rows == nullptr: all n rows) to centroids -> labels
+void assign_rows(const float* data, const float* data_norms, const int64_t* rows, int64_t nr, int d, int dp,
+                 const ListSet& cents, int G, int metric, int64_t* labels, int device, Workspace& ws,
+                 hipStream_t s) {
+  Buf dist;
+  dist.reserve(sizeof(float) * (size_t)std::max<int64_t>(nr, 1));
+  single_list_topk(cents, G, data, data_norms, rows, nr, d, dp, 1, metric, dist.as<float>(), labels, device, ws, s);
+  HIPCHK(hipStreamSynchronize(s));  // `dist` is freed on return
+}
+
+// n_iters Lloyd iterations on trainset rows; centroids_rm in/out [nc][d]
+void kmeans_fit_impl(const float* data, const float* data_norms, const int64_t* rows, int64_t n_train, int d, int dp,
+                     int nc, int iters, float* centroids_rm, int G, int device, Workspace& ws, hipStream_t s) {
+  if (iters <= 0) return;
+  Buf labels, perm, off, partial, chunk_off, tmp, ctmp;
+  labels.reserve(sizeof(int64_t) * n_train);
+  perm.reserve(sizeof(int64_t) * n_train);
+  off.reserve(sizeof(int64_t) * (nc + 1));
+  partial.reserve(sizeof(double) * km_partial_rows(n_train, nc) * d);
+  chunk_off.reserve(sizeof(int64_t) * (nc + 1));
+  tmp.reserve(sizeof(int64_t) * (nc + 1) + scan_tmp_bytes(nc + 1));
+  const size_t cb = csort_tmp_bytes(n_train, nc);
+  ctmp.reserve(cb);
+  for (int it = 0; it < iters; ++it) {
+    ListSet cents;
+    make_single_list(cents, centroids_rm, nc, d, dp, 0, G, s);
+    assign_rows(data, data_norms, rows, n_train, d, dp, cents, G, kL2, labels.as<int64_t>(), device, ws, s);
+    HIPCHK(launch_counting_sort(labels.as<int64_t>(), n_train, nc, perm.as<int64_t>(), off.as<int64_t>(), ctmp.p,
+                                cb, s));
+    HIPCHK(launch_km_update(data, d, rows, perm.as<int64_t>(), off.as<int64_t>(), nc, n_train,
+                            partial.as<double>(), chunk_off.as<int64_t>(), tmp.p, centroids_rm, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+}
+
+// lists of `idx` from final centroids: assign every row, stable sort, pack
+void build_lists(mivs_index_s* idx, const float* data, const float* data_norms, int64_t n, hipStream_t s) {
+  const int nl = idx->cents.n_lists == 1 ? (int)idx->cents.n_rows : idx->cents.n_lists;
+  Buf labels, perm, off, ctmp;
+  labels.reserve(sizeof(int64_t) * std::max<int64_t>(n, 1));
+  perm.reserve(sizeof(int64_t) * std::max<int64_t>(n, 1));
+  off.reserve(sizeof(int64_t) * (nl + 1));
+  if (n > 0)
+    assign_rows(data, data_norms, nullptr, n, idx->d, idx->dp, idx->cents, idx->G, idx->metric,
+                labels.as<int64_t>(), idx->device, idx->ws, s);
+  const size_t cb = csort_tmp_bytes(n, nl);
+  ctmp.reserve(cb);
+  HIPCHK(launch_counting_sort(labels.as<int64_t>(), n, nl, perm.as<int64_t>(), off.as<int64_t>(), ctmp.p, cb, s));
+  std::vector<int64_t> h_off(nl + 1);
+  HIPCHK(hipMemcpyAsync(h_off.data(), off.p, sizeof(int64_t) * (nl + 1), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  pack_lists(idx->lists, data, idx->d, idx->dp, perm.as<int64_t>(), h_off, idx->id_offset, nullptr, idx->G, s);
+}
+
+int chunk_groups_from_rows(int32_t chunk_rows) {
+  if (chunk_rows <= 0) return kDefaultChunkGroups;
+  return (int)std::max<int64_t>(1, ceil_div(chunk_rows, kGroupRows));
+}
+
+void check_common(int device, const void* data, int64_t n, int32_t dim) {
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  require(device >= 0 && device < ndev, "invalid device " + std::to_string(device));
+  require(dim >= 1, "dim must be >= 1");
+  require(dim_pad(dim) <= 1024, "dim > 1024 is not supported by this build", MIVS_ERR_UNSUPPORTED);
+  require(n >= 0, "n must be >= 0");
+  require(n == 0 || data != nullptr, "data is NULL");
+}
+
+
+void ivf_search_impl(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
+                     int64_t* out_i, int32_t* out_probes) {
+  Workspace& ws = idx->ws;
+  const bool prof = g_profiling.load() != 0;
+  if (prof) idx->ev.create();
+  if (prof) HIPCHK(hipEventRecord(idx->ev.e[0], s));
+  ws.qn.reserve(sizeof(float) * nq);
+  HIPCHK(launch_row_norms(q, nq, idx->d, ws.qn.as<float>(), s));
+  // coarse: top-n_probes centroids per query
+  ws.probes_d.reserve(sizeof(float) * nq * np);
+  ws.probes_i.reserve(sizeof(int64_t) * nq * np);
+  if (prof) HIPCHK(hipEventRecord(idx->ev.e[1], s));
+  single_list_topk(idx->cents, idx->G, q, ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, np, idx->metric,
+                   ws.probes_d.as<float>(), ws.probes_i.as<int64_t>(), idx->device, ws, s);
+  if (prof) HIPCHK(hipEventRecord(idx->ev.e[2], s));
+  if (out_probes) HIPCHK(launch_i64_to_i32(ws.probes_i.as<int64_t>(), nq * np, out_probes, s));
+  // probe map
+  const ListSet& L = idx->lists;
+  const int64_t ne = nq * np;
+  ws.counts.reserve(sizeof(int) * L.n_lists);
+  ws.fill.reserve(sizeof(int) * L.n_lists);
+  ws.bucket_off.reserve(sizeof(int) * (L.n_lists + 1));
+  ws.work_off.reserve(sizeof(int) * (L.n_lists + 1));
+  ws.bucket_q.reserve(sizeof(int64_t) * ne);
+  ws.bucket_slot.reserve(sizeof(int64_t) * ne);
+  ws.qp_slots.reserve(sizeof(int64_t) * ne);
+  ws.slot_begin.reserve(sizeof(int64_t) * (nq + 1));
+  const size_t stb = scan_tmp_bytes(ne) + sizeof(int64_t) * (size_t)ne;
+  ws.scan_tmp.reserve(stb);
+  HIPCHK(launch_probe_map(ws.probes_i.as<int64_t>(), nq, np, L.n_lists, L.goff.as<int64_t>(), idx->G,
+                          ws.counts.as<int>(), ws.fill.as<int>(), ws.bucket_off.as<int>(), ws.work_off.as<int>(),
+                          ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(), ws.qp_slots.as<int64_t>(),
+                          ws.slot_begin.as<int64_t>(), ws.scan_tmp.p, stb, s));
+  // fine scan into per-(query, probe, chunk) slots
+  const int64_t max_slots = nq * L.top_chunks_prefix[std::min<int64_t>(np, L.n_lists)];
+  require(max_slots * k < ((int64_t)1 << 40), "search workspace too large", MIVS_ERR_UNSUPPORTED);
+  ws.part_d.reserve(sizeof(float) * (size_t)std::max<int64_t>(max_slots * k, 1));
+  ws.part_i.reserve(sizeof(int64_t) * (size_t)std::max<int64_t>(max_slots * k, 1));
+  ScanJob j{&L, idx->G, q, ws.qn.as<float>(), idx->d, idx->dp, k, idx->metric, ws.bucket_q.as<int64_t>(),
+            ws.bucket_slot.as<int64_t>(), ws.bucket_off.as<int>(), ws.work_off.as<int>(), ws.part_d.as<float>(),
+            ws.part_i.as<int64_t>()};
+  if (prof) HIPCHK(hipEventRecord(idx->ev.e[3], s));
+  run_scan(j, idx->device, ws, s);
+  if (prof) HIPCHK(hipEventRecord(idx->ev.e[4], s));
+  MergeArgs m{};
+  m.in_d = ws.part_d.as<float>();
+  m.in_i = ws.part_i.as<int64_t>();
+  m.slot_begin = ws.slot_begin.as<int64_t>();
+  m.nq = nq;
+  m.k_in = k;
+  m.k = k;
+  m.metric = idx->metric;
+  m.out_d = out_d;
+  m.out_i = out_i;
+  HIPCHK(launch_merge(m, s));
+  if (prof) {
+    HIPCHK(hipEventRecord(idx->ev.e[5], s));
+    HIPCHK(hipEventSynchronize(idx->ev.e[5]));
+    mivs_search_stats st{};
+    st.n_queries = nq;
+    st.n_probes = np;
+    st.k = k;
+    HIPCHK(hipEventElapsedTime(&st.coarse_ms, idx->ev.e[1], idx->ev.e[2]));
+    HIPCHK(hipEventElapsedTime(&st.scan_ms, idx->ev.e[3], idx->ev.e[4]));
+    HIPCHK(hipEventElapsedTime(&st.total_ms, idx->ev.e[0], idx->ev.e[5]));
+    std::vector<int> counts(L.n_lists), woff(L.n_lists + 1);
+    HIPCHK(hipMemcpy(counts.data(), ws.counts.p, sizeof(int) * L.n_lists, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(woff.data(), ws.work_off.p, sizeof(int) * (L.n_lists + 1), hipMemcpyDeviceToHost));
+    for (int l = 0; l < L.n_lists; ++l) {
+      const int64_t sz = L.h_off[l + 1] - L.h_off[l];
+      st.scanned_rows += (int64_t)counts[l] * sz;
+      st.streamed_groups += ceil_div(counts[l], kQTile) * (L.h_goff[l + 1] - L.h_goff[l]);
+    }
+    st.work_items = woff[L.n_lists];
+    idx->stats = st;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* mivs_last_error(void) { return g_err.c_str(); }
+int32_t mivs_version(void) { return 100; }
+void mivs_set_profiling(int32_t on) { g_profiling.store(on ? 1 : 0); }
+
+int32_t mivs_ivf_flat_build(int32_t device, void* stream, const float* d_data, int64_t n, int32_t dim,
+                            const mivs_ivf_flat_params* p, int64_t id_offset, mivs_index_t* out) {
+  return guarded([&] {
+    require(p != nullptr && out != nullptr, "params/out is NULL");
+    check_common(device, d_data, n, dim);
+    require(p->metric == MIVS_METRIC_L2 || p->metric == MIVS_METRIC_IP, "unknown metric");
+    require(p->n_lists >= 1, "n_lists must be >= 1");
+    require(n >= p->n_lists, "n_rows (" + std::to_string(n) + ") must be >= n_lists (" + std::to_string(p->n_lists) + ")");
+    require(p->n_lists <= 32768, "n_lists > 32768 is not supported by this build", MIVS_ERR_UNSUPPORTED);
+    require(p->kmeans_n_iters >= 0, "kmeans_n_iters must be >= 0");
+    require(p->kmeans_trainset_fraction > 0.0 && p->kmeans_trainset_fraction <= 1.0,
+            "kmeans_trainset_fraction must be in (0, 1]");
+    DeviceGuard dg(device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    auto idx = std::make_unique<mivs_index_s>();
+    idx->kind = 0;
+    idx->device = device;
+    idx->d = dim;
+    idx->dp = dim_pad(dim);
+    idx->metric = p->metric;
+    idx->G = chunk_groups_from_rows(p->chunk_rows);
+    idx->id_offset = id_offset;
+    const int nl = p->n_lists;
+    // trainset + strided init (oracle orc_train_count / orc_train_rows / orc_init_rows)
+    int64_t nt = (int64_t)((double)n * p->kmeans_trainset_fraction);
+    if (p->kmeans_max_train_per_list > 0 && nt > (int64_t)nl * p->kmeans_max_train_per_list)
+      nt = (int64_t)nl * p->kmeans_max_train_per_list;
+    nt = std::max<int64_t>(nt, nl);
+    nt = std::min<int64_t>(nt, n);
+    Buf rows, init_rows, norms;
+    rows.reserve(sizeof(int64_t) * nt);
+    HIPCHK(launch_train_rows(rows.as<int64_t>(), n, nt, s));
+    std::vector<int64_t> h_init(nl);
+    for (int j = 0; j < nl; ++j) h_init[j] = ((((int64_t)j * nt) / nl) * n) / nt;
+    init_rows.reserve(sizeof(int64_t) * nl);
+    HIPCHK(hipMemcpyAsync(init_rows.p, h_init.data(), sizeof(int64_t) * nl, hipMemcpyHostToDevice, s));
+    idx->centroids_rm.reserve(sizeof(float) * (size_t)nl * dim);
+    HIPCHK(launch_gather_rows(d_data, dim, init_rows.as<int64_t>(), nl, idx->centroids_rm.as<float>(), s));
+    norms.reserve(sizeof(float) * n);
+    HIPCHK(launch_row_norms(d_data, n, dim, norms.as<float>(), s));
+    HIPCHK(hipStreamSynchronize(s));
+    kmeans_fit_impl(d_data, norms.as<float>(), rows.as<int64_t>(), nt, dim, idx->dp, nl, p->kmeans_n_iters,
+                    idx->centroids_rm.as<float>(), idx->G, device, idx->ws, s);
+    make_single_list(idx->cents, idx->centroids_rm.as<float>(), nl, dim, idx->dp, 0, idx->G, s);
+    if (p->add_data_on_build) {
+      build_lists(idx.get(), d_data, norms.as<float>(), n, s);
+    } else {
+      build_lists(idx.get(), d_data, norms.as<float>(), 0, s);
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    *out = idx.release();
+  });
+}
+
+int32_t mivs_ivf_flat_build_from_centroids(int32_t device, void* stream, const float* d_data, int64_t n,
+                                           int32_t dim, const float* d_centroids, int32_t n_lists,
+                                           int32_t metric, int64_t id_offset, int32_t chunk_rows,
+                                           mivs_index_t* out) {
+  return guarded([&] {
+    require(out != nullptr && d_centroids != nullptr, "centroids/out is NULL");
+    check_common(device, d_data, n, dim);
+    require(metric == MIVS_METRIC_L2 || metric == MIVS_METRIC_IP, "unknown metric");
+    require(n_lists >= 1 && n_lists <= 32768, "n_lists must be in [1, 32768]");
+    DeviceGuard dg(device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    auto idx = std::make_unique<mivs_index_s>();
+    idx->kind = 0;
+    idx->device = device;
+    idx->d = dim;
+    idx->dp = dim_pad(dim);
+    idx->metric = metric;
+    idx->G = chunk_groups_from_rows(chunk_rows);
+    idx->id_offset = id_offset;
+    idx->centroids_rm.reserve(sizeof(float) * (size_t)n_lists * dim);
+    HIPCHK(hipMemcpyAsync(idx->centroids_rm.p, d_centroids, sizeof(float) * (size_t)n_lists * dim,
+                          hipMemcpyDeviceToDevice, s));
+    make_single_list(idx->cents, idx->centroids_rm.as<float>(), n_lists, dim, idx->dp, 0, idx->G, s);
+    Buf norms;
+    norms.reserve(sizeof(float) * std::max<int64_t>(n, 1));
+    HIPCHK(launch_row_norms(d_data, n, dim, norms.as<float>(), s));
+    build_lists(idx.get(), d_data, norms.as<float>(), n, s);
+    HIPCHK(hipStreamSynchronize(s));
+    *out = idx.release();
+  });
+}
+
+int32_t mivs_ivf_flat_search(mivs_index_t idx, void* stream, const float* d_q, int64_t nq, int32_t k,
+                             int32_t n_probes, float* d_dist, int64_t* d_ids, int32_t* d_probes) {
+  return guarded([&] {
+    require(idx != nullptr && idx->kind == 0, "not an ivf_flat index");
+    require(nq >= 0, "nq must be >= 0");
+    require(k >= 1 && k <= kMaxK, "k must be in [1, " + std::to_string(kMaxK) + "]", MIVS_ERR_UNSUPPORTED);
+    require(n_probes >= 1, "n_probes must be >= 1");
+    require(n_probes <= kMaxK, "n_probes must be <= " + std::to_string(kMaxK), MIVS_ERR_UNSUPPORTED);
+    require(nq == 0 || (d_q && d_dist && d_ids), "NULL query/output pointer");
+    if (nq == 0) return;
+    std::lock_guard<std::mutex> g(idx->mu);
+    DeviceGuard dg(idx->device);
+    const int np = std::min<int>(n_probes, idx->lists.n_lists);
+    require(np == n_probes || d_probes == nullptr, "n_probes > n_lists with a probes output");
+    ivf_search_impl(idx, static_cast<hipStream_t>(stream), d_q, nq, k, np, d_dist, d_ids, d_probes);
+  });
+}
+
+int32_t mivs_ivf_flat_get_centroids(mivs_index_t idx, void* stream, float* d_out) {
+  return guarded([&] {
+    require(idx != nullptr && idx->kind == 0, "not an ivf_flat index");
+    DeviceGuard dg(idx->device);
+    HIPCHK(hipMemcpyAsync(d_out, idx->centroids_rm.p, sizeof(float) * (size_t)idx->lists.n_lists * idx->d,
+                          hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
+  });
+}
+
+int32_t mivs_ivf_flat_get_list_sizes(mivs_index_t idx, int64_t* h_out) {
+  return guarded([&] {
+    require(idx != nullptr, "index is NULL");
+    for (int l = 0; l < idx->lists.n_lists; ++l) h_out[l] = idx->lists.h_off[l + 1] - idx->lists.h_off[l];
+  });
+}
+
+int32_t mivs_ivf_flat_get_list_ids(mivs_index_t idx, void* stream, int64_t* d_out) {
+  return guarded([&] {
+    require(idx != nullptr, "index is NULL");
+    DeviceGuard dg(idx->device);
+    const ListSet& L = idx->lists;
+    HIPCHK(launch_compact_ids(L.ids.as<int64_t>(), L.off.as<int64_t>(), L.goff.as<int64_t>(), L.n_lists, L.n_rows,
+                              d_out, static_cast<hipStream_t>(stream)));
+  });
+}
+
+int32_t mivs_ivf_flat_get_list_rows(mivs_index_t idx, void* stream, float* d_out) {
+  return guarded([&] {
+    require(idx != nullptr, "index is NULL");
+    DeviceGuard dg(idx->device);
+    const ListSet& L = idx->lists;
+    HIPCHK(launch_unpack_rows(L.groups.as<float>(), idx->dp, idx->d, L.off.as<int64_t>(), L.goff.as<int64_t>(),
+                              L.n_lists, L.n_rows, d_out, static_cast<hipStream_t>(stream)));
+  });
+}
+
+int32_t mivs_brute_force_build(int32_t device, void* stream, const float* d_data, int64_t n, int32_t dim,
+                               int32_t metric, int64_t id_offset, mivs_index_t* out) {
+  return guarded([&] {
+    require(out != nullptr, "out is NULL");
+    check_common(device, d_data, n, dim);
+    require(metric == MIVS_METRIC_L2 || metric == MIVS_METRIC_IP, "unknown metric");
+    DeviceGuard dg(device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    auto idx = std::make_unique<mivs_index_s>();
+    idx->kind = 1;
+    idx->device = device;
+    idx->d = dim;
+    idx->dp = dim_pad(dim);
+    idx->metric = metric;
+    idx->id_offset = id_offset;
+    make_single_list(idx->lists, d_data, n, dim, idx->dp, id_offset, idx->G, s);
+    *out = idx.release();
+  });
+}
+
+int32_t mivs_brute_force_search(mivs_index_t idx, void* stream, const float* d_q, int64_t nq, int32_t k,
+                                float* d_dist, int64_t* d_ids) {
+  return guarded([&] {
+    require(idx != nullptr && idx->kind == 1, "not a brute-force index");
+    require(nq >= 0, "nq must be >= 0");
+    require(k >= 1 && k <= kMaxK, "k must be in [1, " + std::to_string(kMaxK) + "]", MIVS_ERR_UNSUPPORTED);
+    require(nq == 0 || (d_q && d_dist && d_ids), "NULL query/output pointer");
+    if (nq == 0) return;
+    std::lock_guard<std::mutex> g(idx->mu);
+    DeviceGuard dg(idx->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const bool prof = g_profiling.load() != 0;
+    if (prof) {
+      idx->ev.create();
+      HIPCHK(hipEventRecord(idx->ev.e[0], s));
+    }
+    idx->ws.qn.reserve(sizeof(float) * nq);
+    HIPCHK(launch_row_norms(d_q, nq, idx->d, idx->ws.qn.as<float>(), s));
+    single_list_topk(idx->lists, idx->G, d_q, idx->ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, k, idx->metric,
+                     d_dist, d_ids, idx->device, idx->ws, s);
+    if (prof) {
+      HIPCHK(hipEventRecord(idx->ev.e[5], s));
+      HIPCHK(hipEventSynchronize(idx->ev.e[5]));
+      mivs_search_stats st{};
+      st.n_queries = nq;
+      st.k = k;
+      st.n_probes = 1;
+      st.scanned_rows = nq * idx->lists.n_rows;
+      st.streamed_groups = ceil_div(nq, kQTile) * idx->lists.n_groups;
+      HIPCHK(hipEventElapsedTime(&st.total_ms, idx->ev.e[0], idx->ev.e[5]));
+      st.scan_ms = st.total_ms;
+      idx->stats = st;
+    }
+  });
+}
+
+int32_t mivs_index_info(mivs_index_t idx, int64_t* n_rows, int32_t* dim, int32_t* n_lists, int32_t* metric,
+                        int32_t* device) {
+  return guarded([&] {
+    require(idx != nullptr, "index is NULL");
+    if (n_rows) *n_rows = idx->lists.n_rows;
+    if (dim) *dim = idx->d;
+    if (n_lists) *n_lists = idx->lists.n_lists;
+    if (metric) *metric = idx->metric;
+    if (device) *device = idx->device;
+  });
+}
+
+int32_t mivs_index_last_search_stats(mivs_index_t idx, mivs_search_stats* out) {
+  return guarded([&] {
+    require(idx != nullptr && out != nullptr, "NULL argument");
+    *out = idx->stats;
+  });
+}
+
+void mivs_index_free(mivs_index_t idx) {
+  if (!idx) return;
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(idx->device);
+  delete idx;
+  if (prev >= 0) (void)hipSetDevice(prev);
+}
+
+int32_t mivs_kmeans_fit(int32_t device, void* stream, const float* d_data, int64_t n, int32_t dim,
+                        const int64_t* d_rows, int64_t n_train, int32_t n_clusters, int32_t n_iters,
+                        float* d_centroids) {
+  return guarded([&] {
+    check_common(device, d_data, n, dim);
+    require(n_clusters >= 1 && n_clusters <= 32768, "n_clusters must be in [1, 32768]");
+    require(n_train >= 1 && (d_rows != nullptr || n_train <= n), "bad trainset");
+    DeviceGuard dg(device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    Workspace ws;
+    Buf norms;
+    norms.reserve(sizeof(float) * std::max<int64_t>(n, 1));
+    HIPCHK(launch_row_norms(d_data, n, dim, norms.as<float>(), s));
+    kmeans_fit_impl(d_data, norms.as<float>(), d_rows, n_train, dim, dim_pad(dim), n_clusters, n_iters, d_centroids,
+                    kDefaultChunkGroups, device, ws, s);
+  });
+}
+
+int32_t mivs_kmeans_predict(int32_t device, void* stream, const float* d_data, int64_t n, int32_t dim,
+                            const float* d_centroids, int32_t n_clusters, int32_t metric, int64_t* d_labels) {
+  return guarded([&] {
+    check_common(device, d_data, n, dim);
+    require(n_clusters >= 1, "n_clusters must be >= 1");
+    require(metric == MIVS_METRIC_L2 || metric == MIVS_METRIC_IP, "unknown metric");
+    if (n == 0) return;
+    DeviceGuard dg(device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    Workspace ws;
+    ListSet cents;
+    make_single_list(cents, d_centroids, n_clusters, dim, dim_pad(dim), 0, kDefaultChunkGroups, s);
+    Buf norms;
+    norms.reserve(sizeof(float) * n);
+    HIPCHK(launch_row_norms(d_data, n, dim, norms.as<float>(), s));
+    assign_rows(d_data, norms.as<float>(), nullptr, n, dim, dim_pad(dim), cents, kDefaultChunkGroups, metric,
+                d_labels, device, ws, s);
+  });
+}
+
+int32_t mivs_merge_topk(int32_t device, void* stream, const float* d_in_dist, const int64_t* d_in_ids, int64_t nq,
+                        int32_t m, int32_t k_in, int32_t k, int32_t metric, float* d_out_dist,
+                        int64_t* d_out_ids) {
+  return guarded([&] {
+    require(k >= 1 && k <= kMaxK, "k must be in [1, " + std::to_string(kMaxK) + "]", MIVS_ERR_UNSUPPORTED);
+    require(m >= 0 && k_in >= 0 && nq >= 0, "bad shape");
+    require(metric == MIVS_METRIC_L2 || metric == MIVS_METRIC_IP, "unknown metric");
+    if (nq == 0) return;
+    DeviceGuard dg(device);
+    MergeArgs a{};
+    a.in_d = d_in_dist;
+    a.in_i = d_in_ids;
+    a.slot_begin = nullptr;
+    a.slots_per_q = m;
+    a.nq = nq;
+    a.k_in = k_in;
+    a.k = k;
+    a.metric = metric;
+    a.out_d = d_out_dist;
+    a.out_i = d_out_ids;
+    HIPCHK(launch_merge(a, static_cast<hipStream_t>(stream)));
+  });
+}
+
+int32_t mivs_row_norms(int32_t device, void* stream, const float* d_x, int64_t n, int32_t dim, float* d_out) {
+  return guarded([&] {
+    check_common(device, d_x, n, dim);
+    DeviceGuard dg(device);
+    HIPCHK(launch_row_norms(d_x, n, dim, d_out, static_cast<hipStream_t>(stream)));
+  });
+}
+
+int32_t mivs_synth_mixture(int32_t device, void* stream, float* d_out, int64_t row_begin, int64_t n, int32_t dim,
+                           uint64_t seed, int32_t n_centers, float sigma, int32_t normalize) {
+  return guarded([&] {
+    require(n_centers >= 1, "n_centers must be >= 1");
+    require(dim >= 1 && n >= 0, "bad shape");
+    DeviceGuard dg(device);
+    HIPCHK(launch_synth_mixture(d_out, row_begin, n, dim, seed, n_centers, sigma, normalize,
+                                static_cast<hipStream_t>(stream)));
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,281 @@
+// K6 list fill + row norms, K5 deterministic k-means update, and the synthetic
+// corpus generator. All HBM-bound streaming kernels (DESIGN.md §"Kernels").
+#include "mivs_common.hpp"
+
+namespace mivs {
+
+namespace {
+
+__device__ __forceinline__ float4 ld4(const float* __restrict__ row, int c, int d) {
+  if ((d & 3) == 0 && c + 4 <= d) return *reinterpret_cast<const float4*>(row + c);
+  float4 v;
+  v.x = c + 0 < d ? row[c + 0] : 0.0f;
+  v.y = c + 1 < d ? row[c + 1] : 0.0f;
+  v.z = c + 2 < d ? row[c + 2] : 0.0f;
+  v.w = c + 3 < d ? row[c + 3] : 0.0f;
+  return v;
+}
+
+// One wave per destination group: gathers its 32 source rows (sorted list
+// order), writes the interleaved [dp/8][32][8] image (one contiguous 1 KiB wave
+// store per k-step) and the row norms in the mivs k-order
+// (k = 8s+j then 8s+4+j, i.e. this lane's dim then its lane^32 partner's).
+__global__ __launch_bounds__(256) void k_pack(const float* __restrict__ src, int d, int dp,
+                                              const int64_t* __restrict__ src_index,
+                                              const int64_t* __restrict__ list_off,
+                                              const int64_t* __restrict__ list_goff,
+                                              const int* __restrict__ group_list, int64_t n_groups,
+                                              float* __restrict__ groups, float* __restrict__ norms,
+                                              int64_t* __restrict__ ids_out, const int64_t* __restrict__ id_map,
+                                              int64_t id_offset) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= n_groups) return;
+  const int rr = lane & 31, h = lane >> 5;
+  const int l = group_list ? group_list[g] : 0;
+  const int64_t r = (g - list_goff[l]) * kGroupRows + rr;
+  const int64_t size = list_off[l + 1] - list_off[l];
+  const bool valid = r < size;
+  const int64_t sidx = list_off[l] + r;
+  const int64_t srow = valid ? (src_index ? src_index[sidx] : sidx) : 0;
+  const float* rowp = src + srow * (int64_t)d;
+  float* dst = groups + g * (int64_t)(kGroupRows * dp) + rr * 8 + 4 * h;
+  float acc = 0.0f;
+  const int S = dp >> 3;
+  for (int s = 0; s < S; ++s) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (valid) v = ld4(rowp, 8 * s + 4 * h, d);
+    *reinterpret_cast<float4*>(dst + s * 256) = v;
+    const float px = __shfl_xor(v.x, 32), py = __shfl_xor(v.y, 32);
+    const float pz = __shfl_xor(v.z, 32), pw = __shfl_xor(v.w, 32);
+    acc = fmaf(v.x, v.x, acc); acc = fmaf(px, px, acc);
+    acc = fmaf(v.y, v.y, acc); acc = fmaf(py, py, acc);
+    acc = fmaf(v.z, v.z, acc); acc = fmaf(pz, pz, acc);
+    acc = fmaf(v.w, v.w, acc); acc = fmaf(pw, pw, acc);
+  }
+  if (h == 0) {
+    const int64_t pos = g * kGroupRows + rr;
+    norms[pos] = valid ? acc : INFINITY;
+    if (ids_out) ids_out[pos] = valid ? (id_map ? id_map[srow] : srow + id_offset) : (int64_t)-1;
+  }
+}
+
+// ‖x‖² of plain row-major rows in the mivs k-order (one thread per row)
+__global__ void k_row_norms(const float* __restrict__ x, int64_t n, int d, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* row = x + i * (int64_t)d;
+  const int S = dim_pad(d) >> 3;
+  float acc = 0.0f;
+  for (int s = 0; s < S; ++s) {
+    const float4 a = ld4(row, 8 * s, d), b = ld4(row, 8 * s + 4, d);
+    acc = fmaf(a.x, a.x, acc); acc = fmaf(b.x, b.x, acc);
+    acc = fmaf(a.y, a.y, acc); acc = fmaf(b.y, b.y, acc);
+    acc = fmaf(a.z, a.z, acc); acc = fmaf(b.z, b.z, acc);
+    acc = fmaf(a.w, a.w, acc); acc = fmaf(b.w, b.w, acc);
+  }
+  out[i] = acc;
+}
+
+__device__ __forceinline__ int find_list(const int64_t* __restrict__ off, int n_lists, int64_t r) {
+  int lo = 0, hi = n_lists - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= r) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// interleaved groups -> row-major rows in list order (for parity tests / export)
+__global__ void k_unpack(const float* __restrict__ groups, int dp, int d, const int64_t* __restrict__ list_off,
+                         const int64_t* __restrict__ list_goff, int n_lists, int64_t n_rows,
+                         float* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_rows * (int64_t)d) return;
+  const int64_t row = t / d;
+  const int c = (int)(t - row * d);
+  const int l = find_list(list_off, n_lists, row);
+  const int64_t r = row - list_off[l];
+  const int64_t g = list_goff[l] + r / kGroupRows;
+  const int rr = (int)(r % kGroupRows);
+  out[t] = groups[g * (int64_t)(kGroupRows * dp) + (c >> 3) * 256 + rr * 8 + (c & 7)];
+}
+
+__global__ void k_compact_ids(const int64_t* __restrict__ row_ids, const int64_t* __restrict__ list_off,
+                              const int64_t* __restrict__ list_goff, int n_lists, int64_t n_rows,
+                              int64_t* __restrict__ out) {
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= n_rows) return;
+  const int l = find_list(list_off, n_lists, row);
+  out[row] = row_ids[list_goff[l] * kGroupRows + (row - list_off[l])];
+}
+
+__global__ void k_gather_rows(const float* __restrict__ src, int d, const int64_t* __restrict__ rows, int64_t n,
+                              float* __restrict__ dst) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * (int64_t)d) return;
+  const int64_t i = t / d;
+  const int c = (int)(t - i * d);
+  dst[t] = src[rows[i] * (int64_t)d + c];
+}
+
+// ---- k-means update (K5): fixed member order, fp64 partials over kKmChunk members ----
+__global__ void k_km_chunks(const int64_t* __restrict__ list_off, int nc, int64_t* __restrict__ cnt) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < nc) cnt[c] = ceil_div(list_off[c + 1] - list_off[c], kKmChunk);
+  if (c == nc) cnt[nc] = 0;
+}
+
+__global__ __launch_bounds__(256) void k_km_partial(const float* __restrict__ x, int d,
+                                                    const int64_t* __restrict__ rows,
+                                                    const int64_t* __restrict__ perm,
+                                                    const int64_t* __restrict__ list_off,
+                                                    const int64_t* __restrict__ chunk_off, int nc,
+                                                    double* __restrict__ partial) {
+  const int64_t b = blockIdx.x;
+  if (b >= chunk_off[nc]) return;
+  int lo = 0, hi = nc - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (chunk_off[mid] <= b) lo = mid; else hi = mid - 1;
+  }
+  const int c = lo;
+  const int64_t m0 = list_off[c] + (b - chunk_off[c]) * kKmChunk;
+  const int64_t m1 = m0 + kKmChunk < list_off[c + 1] ? m0 + kKmChunk : list_off[c + 1];
+  for (int dim = threadIdx.x; dim < d; dim += blockDim.x) {
+    double s = 0.0;
+    for (int64_t m = m0; m < m1; ++m) {
+      const int64_t t = perm[m];
+      const int64_t row = rows ? rows[t] : t;
+      s += (double)x[row * d + dim];
+    }
+    partial[b * d + dim] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_km_final(const double* __restrict__ partial,
+                                                  const int64_t* __restrict__ chunk_off,
+                                                  const int64_t* __restrict__ list_off, int d,
+                                                  float* __restrict__ cent) {
+  const int c = blockIdx.x;
+  const int64_t cnt = list_off[c + 1] - list_off[c];
+  if (cnt == 0) return;  // empty cluster keeps its centroid
+  for (int dim = threadIdx.x; dim < d; dim += blockDim.x) {
+    double tot = 0.0;
+    for (int64_t b = chunk_off[c]; b < chunk_off[c + 1]; ++b) tot += partial[b * d + dim];
+    cent[(int64_t)c * d + dim] = (float)(tot / (double)cnt);
+  }
+}
+
+// ---- synthetic clustered corpus (bench / large-scale tests) ----
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// Irwin-Hall(4) approximation of N(0,1) from one 64-bit hash (exact integer -> fp32 steps)
+__device__ __forceinline__ float gauss4(uint64_t h) {
+  float s = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) s += ((float)((h >> (16 * i)) & 0xFFFFull) + 0.5f) * (1.0f / 65536.0f);
+  return (s - 2.0f) * 1.7320508075688772f;
+}
+
+// row i: centre c = H(seed, i) mod n_centers; x = C[c] + sigma * e; optionally L2-normalised.
+__global__ __launch_bounds__(256) void k_synth(float* __restrict__ out, int64_t row_begin, int64_t n, int d,
+                                               uint64_t seed, int n_centers, float sigma, int normalize) {
+  const int lane = threadIdx.x & 63;
+  const int64_t li = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (li >= n) return;
+  const uint64_t gi = (uint64_t)(row_begin + li);
+  const uint64_t cs = splitmix64(seed ^ 0xC2B2AE3D27D4EB4Full);
+  const uint64_t es = splitmix64(seed ^ 0x165667B19E3779F9ull);
+  const uint64_t c = splitmix64(seed * 0xD1B54A32D192ED03ull + gi) % (uint64_t)n_centers;
+  float ss = 0.0f;
+  float* row = out + li * (int64_t)d;
+  for (int k = lane; k < d; k += 64) {
+    const float cv = gauss4(splitmix64(cs + c * 0x100000001B3ull * 1315423911ull + (uint64_t)k));
+    const float ev = gauss4(splitmix64(es + gi * 0x9E3779B97F4A7C15ull + (uint64_t)k * 0xBF58476D1CE4E5B9ull));
+    const float v = cv + sigma * ev;
+    row[k] = v;
+    ss = fmaf(v, v, ss);
+  }
+  if (normalize) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);
+    const float inv = ss > 0.0f ? 1.0f / sqrtf(ss) : 0.0f;
+    for (int k = lane; k < d; k += 64) row[k] *= inv;
+  }
+}
+
+inline dim3 grid1(int64_t n, int b) { return dim3((unsigned)ceil_div(n > 0 ? n : 1, b)); }
+
+}  // namespace
+
+hipError_t launch_pack_groups(const float* src, int64_t /*src_rows_total*/, int d, int dp, const int64_t* src_index,
+                              const int64_t* list_off, const int64_t* list_goff, const int* group_list,
+                              int64_t n_groups, float* groups, float* norms, int64_t* ids_out,
+                              const int64_t* id_map, int64_t id_offset, hipStream_t s) {
+  if (n_groups <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pack, grid1(n_groups, 4), dim3(256), 0, s, src, d, dp, src_index, list_off, list_goff,
+                     group_list, n_groups, groups, norms, ids_out, id_map, id_offset);
+  return hipGetLastError();
+}
+
+hipError_t launch_row_norms(const float* x, int64_t n, int d, float* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_row_norms, grid1(n, 256), dim3(256), 0, s, x, n, d, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_unpack_rows(const float* groups, int dp, int d, const int64_t* list_off, const int64_t* list_goff,
+                              int n_lists, int64_t n_rows, float* out, hipStream_t s) {
+  if (n_rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_unpack, grid1(n_rows * d, 256), dim3(256), 0, s, groups, dp, d, list_off, list_goff, n_lists,
+                     n_rows, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_compact_ids(const int64_t* row_ids, const int64_t* list_off, const int64_t* list_goff,
+                              int n_lists, int64_t n_rows, int64_t* out, hipStream_t s) {
+  if (n_rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_compact_ids, grid1(n_rows, 256), dim3(256), 0, s, row_ids, list_off, list_goff, n_lists,
+                     n_rows, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_rows(const float* src, int d, const int64_t* rows, int64_t n, float* dst, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_rows, grid1(n * d, 256), dim3(256), 0, s, src, d, rows, n, dst);
+  return hipGetLastError();
+}
+
+size_t km_partial_rows(int64_t n_members, int nc) { return (size_t)(ceil_div(n_members, kKmChunk) + nc); }
+
+hipError_t launch_km_update(const float* x, int d, const int64_t* rows, const int64_t* perm,
+                            const int64_t* list_off, int nc, int64_t n_members, double* partial,
+                            int64_t* chunk_off, void* tmp, float* centroids, hipStream_t s) {
+  hipLaunchKernelGGL(k_km_chunks, grid1(nc + 1, 256), dim3(256), 0, s, list_off, nc, chunk_off);
+  // in-place exclusive scan via tmp copy: chunk_off holds counts; scan into tmp area then copy back
+  int64_t* cnt_copy = static_cast<int64_t*>(tmp);
+  hipError_t e = hipMemcpyAsync(cnt_copy, chunk_off, sizeof(int64_t) * (nc + 1), hipMemcpyDeviceToDevice, s);
+  if (e != hipSuccess) return e;
+  e = launch_exclusive_scan_i64(cnt_copy, chunk_off, nc + 1, cnt_copy + (nc + 1), s);
+  if (e != hipSuccess) return e;
+  const int64_t bound = (int64_t)km_partial_rows(n_members, nc);
+  hipLaunchKernelGGL(k_km_partial, dim3((unsigned)bound), dim3(256), 0, s, x, d, rows, perm, list_off, chunk_off, nc,
+                     partial);
+  hipLaunchKernelGGL(k_km_final, dim3((unsigned)nc), dim3(256), 0, s, partial, chunk_off, list_off, d, centroids);
+  return hipGetLastError();
+}
+
+hipError_t launch_synth_mixture(float* out, int64_t row_begin, int64_t n, int d, uint64_t seed, int n_centers,
+                                float sigma, int normalize, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_synth, grid1(n, 4), dim3(256), 0, s, out, row_begin, n, d, seed, n_centers, sigma, normalize);
+  return hipGetLastError();
+}
+
+}  // namespace mivs

@@ -1,0 +1,128 @@
+// mivs — MI355X-native IVF-Flat / brute-force k-NN. Shared device/host definitions.
+//
+// Data layout in HBM (DESIGN.md §"Data layout"):
+//   * dims are zero-padded to dp = round_up(d, 32);
+//   * rows are stored in GROUPS of 32 rows; inside a group the row-major
+//     [32][dp] block is re-ordered as [dp/8][32 rows][8 floats] so that the
+//     32x32x2 f32 MFMA operand of one k-step (lane (r,h) needs dims
+//     8s+4h..8s+4h+3 of row r) is ONE contiguous 1 KiB wave load;
+//   * every inverted list starts on a group boundary; pad rows are zero with
+//     norm = +inf and id = -1, so they can never enter a top-k.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mivs {
+
+constexpr int kGroupRows = 32;     // rows per interleaved group (= MFMA M)
+constexpr int kQTile = 32;         // queries per work item (= MFMA N)
+constexpr int kDimAlign = 32;      // dp = round_up(d, 32)
+constexpr int kScanWaves = 8;      // waves per scan workgroup (2 per SIMD)
+constexpr int kScanThreads = kScanWaves * 64;
+constexpr int kKmChunk = 256;      // members per fp64 partial in the k-means update (== ORC_KM_CHUNK)
+constexpr int kDefaultChunkGroups = 32;  // groups (1024 rows) per scan work item
+constexpr int kMaxK = 64;          // register top-k capacity of scan + merge kernels
+
+enum Metric : int { kL2 = 0, kIP = 1 };
+
+__host__ __device__ inline int dim_pad(int d) { return (d + kDimAlign - 1) / kDimAlign * kDimAlign; }
+__host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// ---------------------------------------------------------------------------
+// Scan job: (lists of interleaved groups) x (buckets of queries probing them).
+// Work item w -> list l (binary search over work_off), then
+//   local = w - work_off[l], tiles_l = ceil(m_l / 32),
+//   chunk = local / tiles_l, tile = local % tiles_l     (tiles of one chunk adjacent)
+// Output slot of bucket entry e for chunk c = bucket_slot[e] + c; each slot
+// holds k (dist, id) pairs sorted ascending by (key, id).
+// ---------------------------------------------------------------------------
+struct ScanArgs {
+  const float* groups;        // interleaved rows
+  const float* row_norms;     // [total_groups*32]; +inf on pad rows
+  const int64_t* row_ids;     // [total_groups*32]; -1 on pad rows
+  const int64_t* list_goff;   // [n_lists+1] group offsets
+  int n_lists;
+  int chunk_groups;           // G
+  const float* queries;       // row-major [*, d]
+  const float* qnorms;        // indexed by query row id
+  const int64_t* bucket_q;    // query row id per bucket entry
+  const int64_t* bucket_slot; // output slot base per bucket entry
+  const int* bucket_off;      // [n_lists+1]
+  const int* work_off;        // [n_lists+1]; total = work_off[n_lists]
+  int* work_counter;          // zeroed before launch
+  float* out_d;               // [slots][k]
+  int64_t* out_i;             // [slots][k]
+  int d, dp, k, metric;
+};
+
+// Merge job: per query q, candidates = slots [slot_begin[q], slot_begin[q+1])
+// (or [q*slots_per_q, (q+1)*slots_per_q) when slot_begin == nullptr), each of
+// k_in sorted (dist, id) pairs -> top-k.
+struct MergeArgs {
+  const float* in_d;
+  const int64_t* in_i;
+  const int64_t* slot_begin;
+  int64_t slots_per_q;
+  int64_t nq;
+  int k_in, k, metric;
+  float* out_d;
+  int64_t* out_i;
+};
+
+// ---- host-side launchers (implemented in the .hip files) ----
+hipError_t launch_scan(const ScanArgs& a, int kcap, int grid, size_t lds_bytes, hipStream_t s);
+hipError_t launch_scan_ex(const ScanArgs& a, int kcap, int grid, size_t lds_bytes, float* gmerge, hipStream_t s);
+size_t scan_lds_bytes(int dp, int kcap);
+bool scan_merge_in_lds(int dp, int kcap);
+size_t scan_gmerge_bytes(int grid, int kcap);
+int scan_kcap(int k);
+hipError_t launch_train_rows(int64_t* rows, int64_t n, int64_t n_train, hipStream_t s);
+hipError_t launch_i64_to_i32(const int64_t* in, int64_t n, int32_t* out, hipStream_t s);
+hipError_t launch_merge(const MergeArgs& a, hipStream_t s);
+
+hipError_t launch_pack_groups(const float* src, int64_t src_rows_total, int d, int dp, const int64_t* src_index,
+                              const int64_t* list_off, const int64_t* list_goff, const int* group_list,
+                              int64_t n_groups, float* groups, float* norms, int64_t* ids_out,
+                              const int64_t* id_map, int64_t id_offset, hipStream_t s);
+hipError_t launch_row_norms(const float* x, int64_t n, int d, float* out, hipStream_t s);
+hipError_t launch_iota_i64(int64_t* out, int64_t n, int64_t start, int64_t step, hipStream_t s);
+hipError_t launch_fill_i32(int* out, int64_t n, int v, hipStream_t s);
+
+// single-list job prep: bucket = identity over nq queries, slot base = q * chunks
+hipError_t launch_single_list_job(int64_t nq, int64_t chunks, int64_t* bucket_q, int64_t* bucket_slot,
+                                  int* bucket_off, int* work_off, int64_t* slot_begin, hipStream_t s);
+// IVF probe map: probes [nq][np] (int64 list ids) -> buckets, work offsets, slot bases
+hipError_t launch_probe_map(const int64_t* probes, int64_t nq, int np, int n_lists, const int64_t* list_goff,
+                            int chunk_groups, int* counts, int* fill, int* bucket_off, int* work_off,
+                            int64_t* bucket_q, int64_t* bucket_slot, int64_t* qp_slots, int64_t* slot_begin,
+                            void* scan_tmp, size_t scan_tmp_bytes, hipStream_t s);
+
+// device-wide exclusive scan (int64) — tmp >= scan_tmp_bytes(n)
+size_t scan_tmp_bytes(int64_t n);
+hipError_t launch_exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, void* tmp, hipStream_t s);
+
+// stable counting sort of positions 0..n-1 by label (labels int64 in [0, nl))
+size_t csort_tmp_bytes(int64_t n, int nl);
+hipError_t launch_counting_sort(const int64_t* labels, int64_t n, int nl, int64_t* perm /*[n]*/,
+                                int64_t* list_off /*[nl+1]*/, void* tmp, size_t tmp_bytes, hipStream_t s);
+
+// k-means deterministic update
+hipError_t launch_km_update(const float* x, int d, const int64_t* rows, const int64_t* perm,
+                            const int64_t* list_off, int nc, int64_t n_members, double* partial,
+                            int64_t* chunk_off, void* tmp, float* centroids, hipStream_t s);
+size_t km_partial_rows(int64_t n_members, int nc);
+
+hipError_t launch_gather_rows(const float* src, int d, const int64_t* rows, int64_t n, float* dst, hipStream_t s);
+hipError_t launch_unpack_rows(const float* groups, int dp, int d, const int64_t* list_off, const int64_t* list_goff,
+                              int n_lists, int64_t n_rows, float* out, hipStream_t s);
+hipError_t launch_compact_ids(const int64_t* row_ids, const int64_t* list_off, const int64_t* list_goff,
+                              int n_lists, int64_t n_rows, int64_t* out, hipStream_t s);
+hipError_t launch_synth_mixture(float* out, int64_t row_begin, int64_t n, int d, uint64_t seed, int n_centers,
+                                float sigma, int normalize, hipStream_t s);
+hipError_t launch_group_list(const int64_t* list_goff, int n_lists, int64_t n_groups, int* group_list,
+                             hipStream_t s);
+hipError_t launch_labels_from_ids(const int64_t* ids, int64_t n, int64_t* labels, hipStream_t s);
+
+}  // namespace mivs

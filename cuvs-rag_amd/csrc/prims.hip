@@ -1,0 +1,354 @@
+// Integer primitives of the IVF pipeline: device-wide exclusive scan, stable
+// counting sort (list fill order / k-means member order), and the per-batch
+// probe map that turns coarse probes into (list -> query bucket) work items.
+// All HBM-bound integer work: plain coalesced loads/stores, LDS histograms, no
+// MFMA (DESIGN.md §"Kernels", K6).
+#include "mivs_common.hpp"
+
+namespace mivs {
+
+namespace {
+
+constexpr int kScanBlock = 1024;
+constexpr int kScanPerThread = 4;
+constexpr int kScanTile = kScanBlock * kScanPerThread;
+
+// block-wide exclusive scan of one value per thread (returns exclusive prefix, total via *tot)
+__device__ int64_t block_excl_scan(int64_t v, int64_t* sh, int64_t* tot) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  int64_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sh[wave] = x;
+  __syncthreads();
+  if (wave == 0) {
+    int64_t s = lane < nw ? sh[lane] : 0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t y = __shfl_up(s, o);
+      if (lane >= o) s += y;
+    }
+    if (lane < nw) sh[lane] = s;  // inclusive wave totals
+  }
+  __syncthreads();
+  const int64_t base = wave > 0 ? sh[wave - 1] : 0;
+  if (tot) *tot = sh[nw - 1];
+  __syncthreads();
+  return base + x - v;
+}
+
+__global__ __launch_bounds__(kScanBlock) void k_scan_reduce(const int64_t* __restrict__ in, int64_t n,
+                                                            int64_t* __restrict__ sums) {
+  __shared__ int64_t sh[16];
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanPerThread;
+  int64_t v = 0;
+#pragma unroll
+  for (int i = 0; i < kScanPerThread; ++i) v += base + i < n ? in[base + i] : 0;
+  int64_t tot;
+  block_excl_scan(v, sh, &tot);
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+// single block: exclusive scan of the block sums in place (any count, carried)
+__global__ __launch_bounds__(kScanBlock) void k_scan_sums(int64_t* __restrict__ sums, int64_t nb) {
+  __shared__ int64_t sh[16];
+  int64_t carry = 0;
+  for (int64_t b0 = 0; b0 < nb; b0 += kScanBlock) {
+    const int64_t i = b0 + threadIdx.x;
+    const int64_t v = i < nb ? sums[i] : 0;
+    int64_t tot;
+    const int64_t ex = block_excl_scan(v, sh, &tot);
+    if (i < nb) sums[i] = carry + ex;
+    carry += tot;
+  }
+}
+
+__global__ __launch_bounds__(kScanBlock) void k_scan_down(const int64_t* __restrict__ in, int64_t n,
+                                                          const int64_t* __restrict__ sums,
+                                                          int64_t* __restrict__ out) {
+  __shared__ int64_t sh[16];
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanPerThread;
+  int64_t vals[kScanPerThread];
+  int64_t v = 0;
+#pragma unroll
+  for (int i = 0; i < kScanPerThread; ++i) { vals[i] = base + i < n ? in[base + i] : 0; v += vals[i]; }
+  int64_t run = sums[blockIdx.x] + block_excl_scan(v, sh, nullptr);
+#pragma unroll
+  for (int i = 0; i < kScanPerThread; ++i) {
+    if (base + i < n) out[base + i] = run;
+    run += vals[i];
+  }
+}
+
+// ---------------- stable counting sort by label ----------------
+constexpr int kSortBlock = 1024;  // rows per histogram block (16 waves)
+
+__global__ __launch_bounds__(kSortBlock) void k_sort_hist(const int64_t* __restrict__ labels, int64_t n, int nl,
+                                                          int64_t nb, int64_t* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* hist = reinterpret_cast<int*>(smem);
+  for (int i = threadIdx.x; i < nl; i += kSortBlock) hist[i] = 0;
+  __syncthreads();
+  const int64_t r = (int64_t)blockIdx.x * kSortBlock + threadIdx.x;
+  if (r < n) atomicAdd(&hist[(int)labels[r]], 1);
+  __syncthreads();
+  for (int i = threadIdx.x; i < nl; i += kSortBlock) counts[(int64_t)i * nb + blockIdx.x] = hist[i];
+}
+
+// positions: offs[l*nb + b] = first output slot of block b's rows with label l
+__global__ __launch_bounds__(kSortBlock) void k_sort_scatter(const int64_t* __restrict__ labels, int64_t n, int nl,
+                                                             int64_t nb, const int64_t* __restrict__ offs,
+                                                             int64_t* __restrict__ perm) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* running = reinterpret_cast<int*>(smem);
+  for (int i = threadIdx.x; i < nl; i += kSortBlock) running[i] = 0;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t r = (int64_t)blockIdx.x * kSortBlock + threadIdx.x;
+  const int lab = r < n ? (int)labels[r] : -1;
+  // rank among earlier lanes of this wave with the same label, and the wave's count of it
+  int rank = 0, cnt = 0;
+  for (int t = 0; t < 64; ++t) {
+    const int o = __shfl(lab, t);
+    if (o == lab) { ++cnt; if (t < lane) ++rank; }
+  }
+  __syncthreads();
+  for (int wv = 0; wv < kSortBlock / 64; ++wv) {
+    if (wave == wv && lab >= 0) {
+      const int64_t pos = offs[(int64_t)lab * nb + blockIdx.x] + running[lab] + rank;
+      perm[pos] = r;
+    }
+    __syncthreads();
+    if (wave == wv && lab >= 0 && rank == cnt - 1) running[lab] += cnt;
+    __syncthreads();
+  }
+}
+
+__global__ void k_list_off_from_offs(const int64_t* __restrict__ offs, int nl, int64_t nb, int64_t n,
+                                     int64_t* __restrict__ list_off) {
+  const int l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l < nl) list_off[l] = offs[(int64_t)l * nb];
+  if (l == 0) list_off[nl] = n;
+}
+
+// ---------------- probe map ----------------
+__global__ void k_probe_count(const int64_t* __restrict__ probes, int64_t n, int* __restrict__ counts) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && probes[i] >= 0) atomicAdd(&counts[(int)probes[i]], 1);  // -1: query without probes (NaN)
+}
+
+__global__ __launch_bounds__(1024) void k_probe_prefix(const int* __restrict__ counts, int n_lists,
+                                                       const int64_t* __restrict__ list_goff, int G,
+                                                       int* __restrict__ bucket_off, int* __restrict__ work_off,
+                                                       int* __restrict__ fill) {
+  __shared__ int64_t sh[16];
+  int64_t cb = 0, cw = 0;
+  for (int l0 = 0; l0 < n_lists; l0 += 1024) {
+    const int l = l0 + threadIdx.x;
+    int64_t c = 0, wk = 0;
+    if (l < n_lists) {
+      c = counts[l];
+      const int64_t chunks = ceil_div(list_goff[l + 1] - list_goff[l], G);
+      wk = ceil_div(c, kQTile) * chunks;
+      fill[l] = 0;
+    }
+    int64_t tb, tw;
+    const int64_t eb = block_excl_scan(c, sh, &tb);
+    const int64_t ew = block_excl_scan(wk, sh, &tw);
+    if (l < n_lists) { bucket_off[l] = (int)(cb + eb); work_off[l] = (int)(cw + ew); }
+    cb += tb;
+    cw += tw;
+  }
+  if (threadIdx.x == 0) { bucket_off[n_lists] = (int)cb; work_off[n_lists] = (int)cw; }
+}
+
+__global__ void k_probe_fill(const int64_t* __restrict__ probes, int64_t n, int np, const int* __restrict__ bucket_off,
+                             int* __restrict__ fill, int64_t* __restrict__ bucket_q, int64_t* __restrict__ bucket_qp,
+                             const int64_t* __restrict__ list_goff, int G, int64_t* __restrict__ qp_slots) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int l = (int)probes[i];
+  if (l < 0) { qp_slots[i] = 0; return; }
+  const int e = bucket_off[l] + atomicAdd(&fill[l], 1);
+  bucket_q[e] = i / np;
+  bucket_qp[e] = i;
+  qp_slots[i] = ceil_div(list_goff[l + 1] - list_goff[l], G);
+}
+
+__global__ void k_bucket_slot(int64_t* __restrict__ bucket_slot, int64_t n, const int64_t* __restrict__ qp_base) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n) bucket_slot[e] = qp_base[bucket_slot[e]];
+}
+
+__global__ void k_slot_begin(const int64_t* __restrict__ qp_base, const int64_t* __restrict__ qp_slots, int64_t nq,
+                             int np, int64_t* __restrict__ slot_begin) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < nq) slot_begin[q] = qp_base[q * np];
+  if (q == nq) slot_begin[nq] = qp_base[nq * np - 1] + qp_slots[nq * np - 1];
+}
+
+__global__ void k_single_job(int64_t nq, int64_t chunks, int64_t* __restrict__ bucket_q,
+                             int64_t* __restrict__ bucket_slot, int* __restrict__ bucket_off,
+                             int* __restrict__ work_off, int64_t* __restrict__ slot_begin) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < nq) {
+    bucket_q[q] = q;
+    bucket_slot[q] = q * chunks;
+    if (slot_begin) slot_begin[q] = q * chunks;
+  }
+  if (q == 0) {
+    bucket_off[0] = 0;
+    bucket_off[1] = (int)nq;
+    work_off[0] = 0;
+    work_off[1] = (int)(ceil_div(nq, kQTile) * chunks);
+    if (slot_begin) slot_begin[nq] = nq * chunks;
+  }
+}
+
+__global__ void k_iota(int64_t* __restrict__ out, int64_t n, int64_t start, int64_t step) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = start + i * step;
+}
+
+__global__ void k_fill_i32(int* __restrict__ out, int64_t n, int v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = v;
+}
+
+__global__ void k_group_list(const int64_t* __restrict__ list_goff, int n_lists, int64_t n_groups,
+                             int* __restrict__ group_list) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_groups) return;
+  int lo = 0, hi = n_lists - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (list_goff[mid] <= g) lo = mid; else hi = mid - 1;
+  }
+  group_list[g] = lo;
+}
+
+// strided trainset row ids: rows[i] = floor(i * n / n_train) (oracle orc_train_rows)
+__global__ void k_train_rows(int64_t* __restrict__ rows, int64_t n, int64_t n_train) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_train) rows[i] = (i * n) / n_train;
+}
+
+__global__ void k_i64_to_i32(const int64_t* __restrict__ in, int64_t n, int32_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (int32_t)in[i];
+}
+
+inline dim3 grid1(int64_t n, int b) { return dim3((unsigned)ceil_div(n > 0 ? n : 1, b)); }
+
+}  // namespace
+
+hipError_t launch_train_rows(int64_t* rows, int64_t n, int64_t n_train, hipStream_t s) {
+  if (n_train <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_train_rows, grid1(n_train, 256), dim3(256), 0, s, rows, n, n_train);
+  return hipGetLastError();
+}
+
+hipError_t launch_i64_to_i32(const int64_t* in, int64_t n, int32_t* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_i64_to_i32, grid1(n, 256), dim3(256), 0, s, in, n, out);
+  return hipGetLastError();
+}
+
+size_t scan_tmp_bytes(int64_t n) { return (size_t)(ceil_div(n > 0 ? n : 1, kScanTile) + 1) * sizeof(int64_t); }
+
+hipError_t launch_exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, void* tmp, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int64_t nb = ceil_div(n, kScanTile);
+  int64_t* sums = static_cast<int64_t*>(tmp);
+  hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(kScanBlock), 0, s, in, n, sums);
+  hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kScanBlock), 0, s, sums, nb);
+  hipLaunchKernelGGL(k_scan_down, dim3((unsigned)nb), dim3(kScanBlock), 0, s, in, n, sums, out);
+  return hipGetLastError();
+}
+
+size_t csort_tmp_bytes(int64_t n, int nl) {
+  const int64_t nb = ceil_div(n > 0 ? n : 1, kSortBlock);
+  const int64_t m = nb * nl;
+  return (size_t)m * 2 * sizeof(int64_t) + scan_tmp_bytes(m) + 256;
+}
+
+hipError_t launch_counting_sort(const int64_t* labels, int64_t n, int nl, int64_t* perm, int64_t* list_off,
+                                void* tmp, size_t tmp_bytes, hipStream_t s) {
+  if (tmp_bytes < csort_tmp_bytes(n, nl)) return hipErrorInvalidValue;
+  if ((size_t)nl * sizeof(int) > 160 * 1024) return hipErrorInvalidValue;
+  const int64_t nb = ceil_div(n > 0 ? n : 1, kSortBlock);
+  const int64_t m = nb * nl;
+  int64_t* counts = static_cast<int64_t*>(tmp);
+  int64_t* offs = counts + m;
+  void* stmp = offs + m;
+  const size_t lds = (size_t)nl * sizeof(int);
+  static const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_hist),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  static const hipError_t a2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_scatter),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (a1 != hipSuccess) return a1;
+  if (a2 != hipSuccess) return a2;
+  if (n > 0) {
+    hipLaunchKernelGGL(k_sort_hist, dim3((unsigned)nb), dim3(kSortBlock), lds, s, labels, n, nl, nb, counts);
+    hipError_t e = launch_exclusive_scan_i64(counts, offs, m, stmp, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_sort_scatter, dim3((unsigned)nb), dim3(kSortBlock), lds, s, labels, n, nl, nb, offs, perm);
+    hipLaunchKernelGGL(k_list_off_from_offs, grid1(nl + 1, 256), dim3(256), 0, s, offs, nl, nb, n, list_off);
+  } else {
+    hipError_t e = hipMemsetAsync(list_off, 0, sizeof(int64_t) * (nl + 1), s);
+    if (e != hipSuccess) return e;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_probe_map(const int64_t* probes, int64_t nq, int np, int n_lists, const int64_t* list_goff,
+                            int chunk_groups, int* counts, int* fill, int* bucket_off, int* work_off,
+                            int64_t* bucket_q, int64_t* bucket_slot, int64_t* qp_slots, int64_t* slot_begin,
+                            void* scan_tmp, size_t scan_tmp_bytes_, hipStream_t s) {
+  const int64_t n = nq * np;
+  if (scan_tmp_bytes_ < scan_tmp_bytes(n) + sizeof(int64_t) * (size_t)n) return hipErrorInvalidValue;
+  int64_t* qp_base = static_cast<int64_t*>(scan_tmp);
+  void* stmp = qp_base + n;
+  hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * n_lists, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_probe_count, grid1(n, 256), dim3(256), 0, s, probes, n, counts);
+  hipLaunchKernelGGL(k_probe_prefix, dim3(1), dim3(1024), 0, s, counts, n_lists, list_goff, chunk_groups, bucket_off,
+                     work_off, fill);
+  hipLaunchKernelGGL(k_probe_fill, grid1(n, 256), dim3(256), 0, s, probes, n, np, bucket_off, fill, bucket_q,
+                     bucket_slot, list_goff, chunk_groups, qp_slots);
+  e = launch_exclusive_scan_i64(qp_slots, qp_base, n, stmp, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_bucket_slot, grid1(n, 256), dim3(256), 0, s, bucket_slot, n, qp_base);
+  hipLaunchKernelGGL(k_slot_begin, grid1(nq + 1, 256), dim3(256), 0, s, qp_base, qp_slots, nq, np, slot_begin);
+  return hipGetLastError();
+}
+
+hipError_t launch_single_list_job(int64_t nq, int64_t chunks, int64_t* bucket_q, int64_t* bucket_slot,
+                                  int* bucket_off, int* work_off, int64_t* slot_begin, hipStream_t s) {
+  hipLaunchKernelGGL(k_single_job, grid1(nq, 256), dim3(256), 0, s, nq, chunks, bucket_q, bucket_slot, bucket_off,
+                     work_off, slot_begin);
+  return hipGetLastError();
+}
+
+hipError_t launch_iota_i64(int64_t* out, int64_t n, int64_t start, int64_t step, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_iota, grid1(n, 256), dim3(256), 0, s, out, n, start, step);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_i32(int* out, int64_t n, int v, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fill_i32, grid1(n, 256), dim3(256), 0, s, out, n, v);
+  return hipGetLastError();
+}
+
+hipError_t launch_group_list(const int64_t* list_goff, int n_lists, int64_t n_groups, int* group_list,
+                             hipStream_t s) {
+  if (n_groups <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_group_list, grid1(n_groups, 256), dim3(256), 0, s, list_goff, n_lists, n_groups, group_list);
+  return hipGetLastError();
+}
+
+}  // namespace mivs

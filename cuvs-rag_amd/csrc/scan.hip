@@ -1,0 +1,287 @@
+// K1/K2/K3/K4 — the fused distance + top-k list-scan kernel (DESIGN.md §"Kernels").
+//
+// One workgroup (8 waves, 512 threads) takes a work item = (list l, one tile of
+// up to 32 queries probing l, one chunk of <= G row groups of l). The query
+// tile is staged once in LDS; each wave streams its row groups straight from
+// HBM (one contiguous 1 KiB dwordx4 wave load per k-step, thanks to the
+// interleaved group layout) into v_mfma_f32_32x32x2_f32 (A = 32 list rows,
+// B = 32 queries). The epilogue turns the 32x32 dot tile into ranking keys and
+// keeps a per-lane register top-K (lane = query, 16 rows per group per lane);
+// at the end of the work item the 16 lane lists of each query are merged in
+// LDS by 16-lane shuffle min-reductions and the chunk's top-k (dist, id) is
+// written to the query's output slot.
+//
+// Replaces the list scan inside cuVS ivf_flat::search (reached from
+// improved_multi_gpu_rag.py:227 / cuvs-2gpu-main.ipynb:1801), the exhaustive
+// scan of FAISS IndexFlatL2.search (colab_a100_test.ipynb:454) and the k-means
+// predict inside ivf_flat::build (index_building_coordinator.py:396).
+#include <climits>
+
+#include "mivs_common.hpp"
+
+namespace mivs {
+
+namespace {
+
+constexpr int kSmallBytes = 32 * 8 + 32 * 8 + 32 * 4 + 16;  // s_q, s_slot, s_qn, s_misc (16-B multiple)
+
+__device__ __forceinline__ float4 load_row4(const float* __restrict__ row, int c, int d) {
+  if ((d & 3) == 0 && c + 4 <= d) return *reinterpret_cast<const float4*>(row + c);
+  float4 v;
+  v.x = c + 0 < d ? row[c + 0] : 0.0f;
+  v.y = c + 1 < d ? row[c + 1] : 0.0f;
+  v.z = c + 2 < d ? row[c + 2] : 0.0f;
+  v.w = c + 3 < d ? row[c + 3] : 0.0f;
+  return v;
+}
+
+// Insert (key, pos) into an ascending register list; positions reach a lane in
+// increasing order, so an equal key lands after the existing ones (ties by id).
+template <int KCAP>
+__device__ __forceinline__ void lane_insert(float (&lk)[KCAP], int (&lp)[KCAP], float key, int pos) {
+#pragma unroll
+  for (int t = KCAP - 1; t >= 0; --t) {
+    const float prev = t > 0 ? lk[t > 0 ? t - 1 : 0] : -INFINITY;
+    const int prevp = t > 0 ? lp[t > 0 ? t - 1 : 0] : 0;
+    const bool shift = key < prev;
+    const bool place = !shift && key < lk[t];
+    lk[t] = shift ? prev : (place ? key : lk[t]);
+    lp[t] = shift ? prevp : (place ? pos : lp[t]);
+  }
+}
+
+template <int KCAP, int METRIC>
+__global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a, float* __restrict__ gmerge) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int64_t* s_q = reinterpret_cast<int64_t*>(smem);          // [32] query row ids (-1: empty lane)
+  int64_t* s_slot = s_q + 32;                                // [32] output slot (already + chunk)
+  float* s_qn = reinterpret_cast<float*>(s_slot + 32);       // [32]
+  int* s_misc = reinterpret_cast<int*>(s_qn + 32);           // [4]
+  float* qtile = reinterpret_cast<float*>(smem + kSmallBytes);
+  const int dp = a.dp;
+  const int qstride = dp + 4;  // +16 B per row: conflict-free ds_read_b128 of the B operand
+
+  // merge area: LDS after the scan when it fits, else this block's global scratch
+  float* mkey = gmerge ? gmerge + (size_t)blockIdx.x * (kQTile * 16 * KCAP * 2) : qtile;
+  int* mpos = reinterpret_cast<int*>(mkey + kQTile * 16 * KCAP);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int j = lane & 31;  // query column of this lane in the MFMA tile
+  const int h = lane >> 5;  // k-half / row-half of this lane
+  const int total = a.work_off[a.n_lists];
+  const int S = dp >> 3;    // k-steps of 8 dims (multiple of 4)
+
+  for (;;) {
+    if (tid == 0) s_misc[0] = atomicAdd(a.work_counter, 1);
+    __syncthreads();
+    const int w = s_misc[0];
+    if (w >= total) break;
+
+    // ---- decode the work item ----
+    int lo = 0, hi = a.n_lists - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (a.work_off[mid] <= w) lo = mid; else hi = mid - 1;
+    }
+    const int l = lo;
+    const int m = a.bucket_off[l + 1] - a.bucket_off[l];
+    const int tiles = (m + kQTile - 1) / kQTile;
+    const int local = w - a.work_off[l];
+    const int chunk = local / tiles;
+    const int tile = local - chunk * tiles;
+    const int64_t g_begin = a.list_goff[l] + (int64_t)chunk * a.chunk_groups;
+    const int64_t g_lim = a.list_goff[l + 1];
+    const int64_t g_end = g_begin + a.chunk_groups < g_lim ? g_begin + a.chunk_groups : g_lim;
+    const int e0 = a.bucket_off[l] + tile * kQTile;
+    const int nqt = m - tile * kQTile < kQTile ? m - tile * kQTile : kQTile;
+
+    if (tid < kQTile) {
+      if (tid < nqt) {
+        const int64_t q = a.bucket_q[e0 + tid];
+        s_q[tid] = q;
+        s_slot[tid] = a.bucket_slot[e0 + tid] + chunk;
+        s_qn[tid] = a.qnorms[q];
+      } else {
+        s_q[tid] = -1;
+        s_slot[tid] = -1;
+        s_qn[tid] = INFINITY;
+      }
+    }
+    __syncthreads();
+
+    // ---- stage the query tile in LDS (zero-padded dims, zero rows for empty lanes) ----
+    {
+      const int c4 = dp >> 2;
+      for (int i = tid; i < kQTile * c4; i += kScanThreads) {
+        const int r = i / c4;
+        const int c = (i - r * c4) << 2;
+        const int64_t q = s_q[r];
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (q >= 0) v = load_row4(a.queries + q * (int64_t)a.d, c, a.d);
+        *reinterpret_cast<float4*>(qtile + r * qstride + c) = v;
+      }
+    }
+    __syncthreads();
+
+    float lk[KCAP];
+    int lp[KCAP];
+#pragma unroll
+    for (int t = 0; t < KCAP; ++t) { lk[t] = INFINITY; lp[t] = INT_MAX; }
+    const float qn = s_qn[j];
+    const bool qvalid = s_q[j] >= 0;
+    const float* qrow = qtile + j * qstride + 4 * h;
+
+    for (int64_t g = g_begin + wave; g < g_end; g += kScanWaves) {
+      const float* gp = a.groups + g * (int64_t)(kGroupRows * dp) + j * 8 + 4 * h;
+      f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      float4 av[4], an[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) av[u] = *reinterpret_cast<const float4*>(gp + u * 256);
+      for (int s0 = 0; s0 < S; s0 += 4) {
+        if (s0 + 4 < S) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) an[u] = *reinterpret_cast<const float4*>(gp + (s0 + 4 + u) * 256);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float4 b = *reinterpret_cast<const float4*>(qrow + (s0 + u) * 8);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u].x, b.x, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u].y, b.y, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u].z, b.z, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u].w, b.w, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) av[u] = an[u];
+      }
+
+      // ---- epilogue: 16 rows of this lane's query ----
+      const int64_t rbase = g * kGroupRows;
+      float xn[16];
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const float4 t = *reinterpret_cast<const float4*>(a.row_norms + rbase + 8 * q4 + 4 * h);
+        xn[4 * q4 + 0] = t.x; xn[4 * q4 + 1] = t.y; xn[4 * q4 + 2] = t.z; xn[4 * q4 + 3] = t.w;
+      }
+      if (qvalid) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float key;
+          if (METRIC == kL2) {
+            const float v = fmaf(-2.0f, acc[r], xn[r] + qn);
+            key = v > 0.0f ? v : 0.0f;
+          } else {
+            key = xn[r] < INFINITY ? -acc[r] : INFINITY;
+          }
+          if (key < lk[KCAP - 1]) {
+            const int pos = (int)(rbase + (r & 3) + 8 * (r >> 2) + 4 * h);
+            lane_insert<KCAP>(lk, lp, key, pos);
+          }
+        }
+      }
+    }
+
+    // ---- merge the 16 lane lists (8 waves x 2 halves) of every query ----
+    __syncthreads();  // every wave is done with qtile (the merge area may alias it)
+    {
+      const int src = wave * 2 + h;
+#pragma unroll
+      for (int t = 0; t < KCAP; ++t) {
+        mkey[(j * 16 + src) * KCAP + t] = lk[t];
+        mpos[(j * 16 + src) * KCAP + t] = lp[t];
+      }
+    }
+    __syncthreads();
+    {
+      const int jj = tid >> 4;  // query of this 16-thread segment
+      const int ss = tid & 15;  // source list of this thread
+      const float* myk = mkey + (jj * 16 + ss) * KCAP;
+      const int* myp = mpos + (jj * 16 + ss) * KCAP;
+      const int64_t slot = s_slot[jj];
+      int head = 0;
+      float hk = myk[0];
+      int hp = myp[0];
+      for (int t = 0; t < a.k; ++t) {
+        float bk = hk;
+        int bp = hp;
+#pragma unroll
+        for (int off = 8; off >= 1; off >>= 1) {
+          const float ok = __shfl_xor(bk, off, 16);
+          const int op = __shfl_xor(bp, off, 16);
+          if (ok < bk || (ok == bk && op < bp)) { bk = ok; bp = op; }
+        }
+        if (ss == 0 && slot >= 0) {
+          const bool valid = bp != INT_MAX;
+          a.out_d[slot * a.k + t] = valid ? (METRIC == kIP ? -bk : bk) : (METRIC == kIP ? -INFINITY : INFINITY);
+          a.out_i[slot * a.k + t] = valid ? a.row_ids[bp] : (int64_t)-1;
+        }
+        if (hk == bk && hp == bp && head < KCAP) {
+          ++head;
+          hk = head < KCAP ? myk[head] : INFINITY;
+          hp = head < KCAP ? myp[head] : INT_MAX;
+        }
+      }
+    }
+    __syncthreads();  // LDS (s_*, merge area) reused by the next work item
+  }
+}
+
+template <int KCAP, int METRIC>
+hipError_t launch_km(const ScanArgs& a, int grid, size_t lds, float* gmerge, hipStream_t s) {
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<KCAP, METRIC>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL((k_scan<KCAP, METRIC>), dim3(grid), dim3(kScanThreads), lds, s, a, gmerge);
+  return hipGetLastError();
+}
+
+template <int KCAP>
+hipError_t launch_k(const ScanArgs& a, int grid, size_t lds, float* gmerge, hipStream_t s) {
+  return a.metric == kIP ? launch_km<KCAP, kIP>(a, grid, lds, gmerge, s) : launch_km<KCAP, kL2>(a, grid, lds, gmerge, s);
+}
+
+}  // namespace
+
+int scan_kcap(int k) {
+  if (k <= 1) return 1;
+  if (k <= 4) return 4;
+  if (k <= 8) return 8;
+  if (k <= 16) return 16;
+  if (k <= 32) return 32;
+  if (k <= 64) return 64;
+  return -1;
+}
+
+static size_t merge_bytes(int kcap) { return (size_t)kQTile * 16 * kcap * 8; }
+static size_t qtile_bytes(int dp) { return (size_t)kQTile * (dp + 4) * 4; }
+static constexpr size_t kLdsMax = 160 * 1024;
+
+// LDS request; the merge area moves to global scratch when it does not fit
+size_t scan_lds_bytes(int dp, int kcap) {
+  const size_t q = qtile_bytes(dp), m = merge_bytes(kcap);
+  const size_t both = kSmallBytes + (q > m ? q : m);
+  return both <= kLdsMax ? both : kSmallBytes + q;
+}
+
+bool scan_merge_in_lds(int dp, int kcap) { return kSmallBytes + merge_bytes(kcap) <= kLdsMax && kSmallBytes + qtile_bytes(dp) <= kLdsMax; }
+
+size_t scan_gmerge_bytes(int grid, int kcap) { return (size_t)grid * merge_bytes(kcap); }
+
+hipError_t launch_scan_ex(const ScanArgs& a, int kcap, int grid, size_t lds, float* gmerge, hipStream_t s) {
+  switch (kcap) {
+    case 1: return launch_k<1>(a, grid, lds, gmerge, s);
+    case 4: return launch_k<4>(a, grid, lds, gmerge, s);
+    case 8: return launch_k<8>(a, grid, lds, gmerge, s);
+    case 16: return launch_k<16>(a, grid, lds, gmerge, s);
+    case 32: return launch_k<32>(a, grid, lds, gmerge, s);
+    case 64: return launch_k<64>(a, grid, lds, gmerge, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_scan(const ScanArgs& a, int kcap, int grid, size_t lds_bytes, hipStream_t s) {
+  return launch_scan_ex(a, kcap, grid, lds_bytes, nullptr, s);
+}
+
+}  // namespace mivs

@@ -1,0 +1,160 @@
+"""ctypes binding of libmivs.so (the C-ABI declared in include/mivs.h).
+
+This module is the only place Python touches the native library. It loads the
+in-tree ``libmivs.so`` (built by ``__graft_entry__.build()`` /
+``make -C cuvs-rag_amd/csrc``) and fails LOUDLY when it is missing: there is no
+CPU or PyTorch fallback for any ANN operation.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from ctypes import POINTER, c_double, c_float, c_int32, c_int64, c_uint64, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MIVS_LIB", os.path.join(_HERE, "libmivs.so"))
+
+MIVS_OK = 0
+MIVS_ERR_INVALID = 1
+MIVS_ERR_OOM = 2
+MIVS_ERR_HIP = 3
+MIVS_ERR_UNSUPPORTED = 4
+
+METRIC_L2 = 0
+METRIC_IP = 1
+MAX_K = 64
+
+
+class MivsError(RuntimeError):
+    """Error raised by the native engine (carries the MIVS_ERR_* code)."""
+
+    def __init__(self, code: int, message: str):
+        super().__init__(message)
+        self.code = code
+
+
+class MivsOutOfMemoryError(MivsError, MemoryError):
+    """hipErrorOutOfMemory inside the engine (the reference's OOM paths catch MemoryError/RuntimeError)."""
+
+
+class NativeLibraryMissing(ImportError):
+    pass
+
+
+class IvfFlatParams(ctypes.Structure):
+    _fields_ = [
+        ("n_lists", c_int32),
+        ("metric", c_int32),
+        ("kmeans_n_iters", c_int32),
+        ("kmeans_trainset_fraction", c_double),
+        ("kmeans_max_train_per_list", c_int64),
+        ("add_data_on_build", c_int32),
+        ("chunk_rows", c_int32),
+    ]
+
+
+class SearchStats(ctypes.Structure):
+    _fields_ = [
+        ("n_queries", c_int64),
+        ("n_probes", c_int32),
+        ("k", c_int32),
+        ("scanned_rows", c_int64),
+        ("streamed_groups", c_int64),
+        ("work_items", c_int64),
+        ("scan_ms", c_float),
+        ("coarse_ms", c_float),
+        ("total_ms", c_float),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+_SIGS = {
+    "mivs_last_error": (ctypes.c_char_p, []),
+    "mivs_version": (c_int32, []),
+    "mivs_set_profiling": (None, [c_int32]),
+    "mivs_ivf_flat_build": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int32, POINTER(IvfFlatParams), c_int64,
+                                      POINTER(c_void_p)]),
+    "mivs_ivf_flat_build_from_centroids": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_int32,
+                                                     c_int32, c_int64, c_int32, POINTER(c_void_p)]),
+    "mivs_ivf_flat_search": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p,
+                                       c_void_p]),
+    "mivs_ivf_flat_get_centroids": (c_int32, [c_void_p, c_void_p, c_void_p]),
+    "mivs_ivf_flat_get_list_sizes": (c_int32, [c_void_p, c_void_p]),
+    "mivs_ivf_flat_get_list_ids": (c_int32, [c_void_p, c_void_p, c_void_p]),
+    "mivs_ivf_flat_get_list_rows": (c_int32, [c_void_p, c_void_p, c_void_p]),
+    "mivs_brute_force_build": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int64,
+                                         POINTER(c_void_p)]),
+    "mivs_brute_force_search": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
+    "mivs_index_info": (c_int32, [c_void_p, POINTER(c_int64), POINTER(c_int32), POINTER(c_int32), POINTER(c_int32),
+                                  POINTER(c_int32)]),
+    "mivs_index_last_search_stats": (c_int32, [c_void_p, POINTER(SearchStats)]),
+    "mivs_index_free": (None, [c_void_p]),
+    "mivs_kmeans_fit": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32, c_int32,
+                                  c_void_p]),
+    "mivs_kmeans_predict": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_int32, c_int32,
+                                      c_void_p]),
+    "mivs_merge_topk": (c_int32, [c_int32, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_int32,
+                                  c_void_p, c_void_p]),
+    "mivs_row_norms": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int32, c_void_p]),
+    "mivs_synth_mixture": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int64, c_int32, c_uint64, c_int32,
+                                     c_float, c_int32]),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+_lib = None
+_lock = threading.Lock()
+_load_error: str | None = None
+
+
+def load(path: str | None = None):
+    """Load libmivs.so (idempotent). Raises NativeLibraryMissing if it cannot be loaded."""
+    global _lib, _load_error
+    with _lock:
+        if _lib is not None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            _load_error = f"{p} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            raise NativeLibraryMissing(_load_error)
+        try:
+            lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+        except OSError as e:  # pragma: no cover - depends on the ROCm runtime install
+            _load_error = f"cannot load {p}: {e}"
+            raise NativeLibraryMissing(_load_error) from e
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def available() -> bool:
+    try:
+        load()
+        return True
+    except NativeLibraryMissing:
+        return False
+
+
+def lib():
+    return load()
+
+
+def check(rc: int) -> None:
+    if rc == MIVS_OK:
+        return
+    msg = load().mivs_last_error().decode(errors="replace")
+    if rc == MIVS_ERR_OOM:
+        raise MivsOutOfMemoryError(rc, msg)
+    if rc in (MIVS_ERR_INVALID, MIVS_ERR_UNSUPPORTED):
+        raise ValueError(msg)
+    raise MivsError(rc, msg)
+
+
+def set_profiling(on: bool) -> None:
+    load().mivs_set_profiling(1 if on else 0)

@@ -1,0 +1,233 @@
+"""IVF-Flat on MI355X — drop-in for ``cuvs.neighbors.ivf_flat`` (cuVS 25.6.0).
+
+The reference uses exactly these call shapes:
+  * ``ivf_flat.IndexParams(n_lists=...)``             index_building_coordinator.py:395
+  * ``ivf_flat.build(params, torch_cuda_tensor)``      index_building_coordinator.py:396
+  * ``ivf_flat.SearchParams()``                        improved_multi_gpu_rag.py:226
+  * ``ivf_flat.search(sp, index, q_2d, k)``            improved_multi_gpu_rag.py:227
+    -> ``(distances, neighbors)``
+
+Everything runs in libmivs.so (hand-written HIP for gfx950); this module only
+validates arguments and moves pointers. Defaults follow cuVS: 20 k-means
+iterations on a 0.5 trainset fraction, 20 probes.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+
+from .. import _native
+from .._tensors import as_device_f32, emit, out_tensor, ptr, stream_ptr
+
+_METRICS = {
+    "sqeuclidean": _native.METRIC_L2,
+    "l2": _native.METRIC_L2,
+    "L2Expanded": _native.METRIC_L2,
+    "euclidean": _native.METRIC_L2,  # same ranking; distances are sqrt'ed on output
+    "L2SqrtExpanded": _native.METRIC_L2,
+    "inner_product": _native.METRIC_IP,
+    "InnerProduct": _native.METRIC_IP,
+}
+_SQRT_METRICS = ("euclidean", "L2SqrtExpanded")
+
+
+def metric_code(metric: str) -> int:
+    try:
+        return _METRICS[metric]
+    except KeyError:
+        raise ValueError(f"unsupported metric {metric!r}; supported: {sorted(_METRICS)}") from None
+
+
+class IndexParams:
+    """cuvs.neighbors.ivf_flat.IndexParams."""
+
+    def __init__(self, n_lists: int = 1024, metric: str = "sqeuclidean", kmeans_n_iters: int = 20,
+                 kmeans_trainset_fraction: float = 0.5, add_data_on_build: bool = True,
+                 adaptive_centers: bool = False, conservative_memory_allocation: bool = False,
+                 kmeans_max_train_per_list: int = 0, chunk_rows: int = 0):
+        if int(n_lists) < 1:
+            raise ValueError(f"n_lists must be >= 1, got {n_lists}")
+        metric_code(metric)
+        if adaptive_centers:
+            raise NotImplementedError("adaptive_centers is not supported by mivs")
+        self.n_lists = int(n_lists)
+        self.metric = metric
+        self.kmeans_n_iters = int(kmeans_n_iters)
+        self.kmeans_trainset_fraction = float(kmeans_trainset_fraction)
+        self.add_data_on_build = bool(add_data_on_build)
+        self.adaptive_centers = bool(adaptive_centers)
+        self.conservative_memory_allocation = bool(conservative_memory_allocation)
+        self.kmeans_max_train_per_list = int(kmeans_max_train_per_list)
+        self.chunk_rows = int(chunk_rows)
+
+    def _c(self) -> _native.IvfFlatParams:
+        return _native.IvfFlatParams(self.n_lists, metric_code(self.metric), self.kmeans_n_iters,
+                                     self.kmeans_trainset_fraction, self.kmeans_max_train_per_list,
+                                     1 if self.add_data_on_build else 0, self.chunk_rows)
+
+    def __repr__(self):
+        return (f"IndexParams(n_lists={self.n_lists}, metric={self.metric!r}, kmeans_n_iters={self.kmeans_n_iters}, "
+                f"kmeans_trainset_fraction={self.kmeans_trainset_fraction})")
+
+
+class SearchParams:
+    """cuvs.neighbors.ivf_flat.SearchParams (cuVS default n_probes = 20)."""
+
+    def __init__(self, n_probes: int = 20):
+        if int(n_probes) < 1:
+            raise ValueError(f"n_probes must be >= 1, got {n_probes}")
+        self.n_probes = int(n_probes)
+
+    def __repr__(self):
+        return f"SearchParams(n_probes={self.n_probes})"
+
+
+class Index:
+    """Handle to an IVF-Flat index resident on one GPU (owned by libmivs)."""
+
+    def __init__(self, handle: int, metric: str):
+        self._h = ctypes.c_void_p(handle)
+        self.metric = metric
+        n, d, nl, m, dev = ctypes.c_int64(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        _native.check(_native.lib().mivs_index_info(self._h, ctypes.byref(n), ctypes.byref(d), ctypes.byref(nl),
+                                                    ctypes.byref(m), ctypes.byref(dev)))
+        self.size = int(n.value)
+        self.dim = int(d.value)
+        self.n_lists = int(nl.value)
+        self.device = int(dev.value)
+        self.trained = True
+
+    @property
+    def handle(self):
+        if self._h is None:
+            raise RuntimeError("index has been closed")
+        return self._h
+
+    def __len__(self):
+        return self.size
+
+    @property
+    def centers(self) -> torch.Tensor:
+        out = torch.empty((self.n_lists, self.dim), dtype=torch.float32, device=f"cuda:{self.device}")
+        _native.check(_native.lib().mivs_ivf_flat_get_centroids(self.handle, stream_ptr(self.device), ptr(out)))
+        return out
+
+    @property
+    def list_sizes(self) -> torch.Tensor:
+        out = torch.empty(self.n_lists, dtype=torch.int64)
+        _native.check(_native.lib().mivs_ivf_flat_get_list_sizes(self.handle, ptr(out)))
+        return out
+
+    def list_ids(self) -> torch.Tensor:
+        """ids of all lists concatenated in list order (each list ascending by id)."""
+        out = torch.empty(self.size, dtype=torch.int64, device=f"cuda:{self.device}")
+        _native.check(_native.lib().mivs_ivf_flat_get_list_ids(self.handle, stream_ptr(self.device), ptr(out)))
+        return out
+
+    def list_rows(self) -> torch.Tensor:
+        out = torch.empty((self.size, self.dim), dtype=torch.float32, device=f"cuda:{self.device}")
+        _native.check(_native.lib().mivs_ivf_flat_get_list_rows(self.handle, stream_ptr(self.device), ptr(out)))
+        return out
+
+    def last_search_stats(self) -> dict:
+        st = _native.SearchStats()
+        _native.check(_native.lib().mivs_index_last_search_stats(self.handle, ctypes.byref(st)))
+        return st.as_dict()
+
+    def close(self):
+        if self._h is not None and self._h.value:
+            lib = _native._lib
+            if lib is not None:
+                lib.mivs_index_free(self._h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __repr__(self):
+        return (f"ivf_flat.Index(size={self.size}, dim={self.dim}, n_lists={self.n_lists}, metric={self.metric!r}, "
+                f"device=cuda:{self.device})")
+
+
+def build(index_params: IndexParams, dataset, resources=None, ids_offset: int = 0) -> Index:
+    """Train k-means, assign every row, fill the inverted lists (all on the GPU holding `dataset`)."""
+    if not isinstance(index_params, IndexParams):
+        raise TypeError("index_params must be an ivf_flat.IndexParams")
+    x = as_device_f32(dataset, name="dataset")
+    dev = x.device.index
+    n, d = x.shape
+    if n < index_params.n_lists:
+        raise ValueError(f"dataset has {n} rows, fewer than n_lists={index_params.n_lists}")
+    h = ctypes.c_void_p()
+    p = index_params._c()
+    with torch.cuda.device(dev):
+        _native.check(_native.lib().mivs_ivf_flat_build(dev, stream_ptr(dev), ptr(x), n, d, ctypes.byref(p),
+                                                        int(ids_offset), ctypes.byref(h)))
+    return Index(h.value, index_params.metric)
+
+
+def build_from_centroids(centroids, dataset, metric: str = "sqeuclidean", ids_offset: int = 0,
+                         chunk_rows: int = 0) -> Index:
+    """IVF-Flat lists from given centroids (FAISS IndexIVFFlat with a pre-trained quantizer)."""
+    x = as_device_f32(dataset, name="dataset")
+    dev = x.device.index
+    c = as_device_f32(centroids, device=dev, name="centroids")
+    if c.shape[1] != x.shape[1]:
+        raise ValueError("centroids and dataset dims differ")
+    h = ctypes.c_void_p()
+    with torch.cuda.device(dev):
+        _native.check(_native.lib().mivs_ivf_flat_build_from_centroids(
+            dev, stream_ptr(dev), ptr(x), x.shape[0], x.shape[1], ptr(c), c.shape[0], metric_code(metric),
+            int(ids_offset), int(chunk_rows), ctypes.byref(h)))
+    return Index(h.value, metric)
+
+
+def search(search_params: SearchParams, index: Index, queries, k: int, neighbors=None, distances=None,
+           resources=None, probes_out: torch.Tensor | None = None):
+    """k-NN over the n_probes closest lists. Returns ``(distances, neighbors)`` ([nq, k] f32, [nq, k] i64)."""
+    if not isinstance(index, Index):
+        raise TypeError("index must be an ivf_flat.Index")
+    sp = search_params if search_params is not None else SearchParams()
+    k = int(k)
+    if k < 1:
+        raise ValueError(f"k must be >= 1, got {k}")
+    dev = index.device
+    q = as_device_f32(queries, device=dev, name="queries")
+    if q.shape[1] != index.dim:
+        raise ValueError(f"queries have dim {q.shape[1]}, index has {index.dim}")
+    nq = q.shape[0]
+    dist = out_tensor(distances, (nq, k), torch.float32, dev, "distances")
+    nbrs = out_tensor(neighbors, (nq, k), torch.int64, dev, "neighbors")
+    with torch.cuda.device(dev):
+        _native.check(_native.lib().mivs_ivf_flat_search(index.handle, stream_ptr(dev), ptr(q), nq, k, sp.n_probes,
+                                                         ptr(dist), ptr(nbrs), ptr(probes_out)))
+    if index.metric in _SQRT_METRICS:
+        dist = torch.sqrt(dist)
+    return emit(dist), emit(nbrs)
+
+
+def extend(index: Index, new_vectors, new_indices=None):
+    raise NotImplementedError("ivf_flat.extend is not implemented yet in mivs (rebuild the index instead)")
+
+
+def save(filename: str, index: Index, include_dataset: bool = True):
+    raise NotImplementedError("ivf_flat.save is not implemented yet in mivs")
+
+
+def load(filename: str, resources=None):
+    raise NotImplementedError("ivf_flat.load is not implemented yet in mivs")
+
+
+def default_n_lists(n_rows: int) -> int:
+    """The coordinator's default: max(1, min(256, N // 1000 + 1)) (index_building_coordinator.py:394)."""
+    return max(1, min(256, n_rows // 1000 + 1))
+
+
+__all__ = ["IndexParams", "SearchParams", "Index", "build", "build_from_centroids", "search", "extend", "save", "load",
+           "default_n_lists", "metric_code"]
+_ = math

@@ -1,0 +1,127 @@
+/*
+ * mivs — MI355X-native IVF-Flat / brute-force k-NN engine: the C-ABI.
+ *
+ * This is the drop-in boundary for the reference's hot path. The reference
+ * (tanujdargan/cuVS-rag) reaches its ANN arithmetic only through four Python
+ * call shapes into cuVS 25.6.0; each entry point below
+ * names the reference call it replaces. Host code (the Python package cuvs-rag_amd/mivs)
+ * binds these with ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *  - every function is re-entrant across devices and returns 0 (MIVS_OK) or
+ *    an MIVS_ERR_* code; mivs_last_error() returns a thread-local message;
+ *  - `stream` is a hipStream_t passed as void* (NULL = default stream); all
+ *    device work of a call is enqueued on it; pointers named d_* are device
+ *    pointers on `device` (borrowed, contiguous, row-major), h_* are host;
+ *  - results are ordered ascending by (distance, id) for L2 and descending by
+ *    inner product (ties: ascending id) for IP; missing results are
+ *    id = -1, distance = +inf (L2) / -inf (IP) (FAISS convention);
+ *  - arithmetic: DESIGN.md §"Arithmetic contract" (bit-exact with oracle/).
+ */
+#ifndef MIVS_H
+#define MIVS_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MIVS_OK 0
+#define MIVS_ERR_INVALID 1     /* bad argument (shape, k, n_probes, metric ...) */
+#define MIVS_ERR_OOM 2         /* hipErrorOutOfMemory (maps to torch.cuda.OutOfMemoryError) */
+#define MIVS_ERR_HIP 3         /* any other HIP runtime error */
+#define MIVS_ERR_UNSUPPORTED 4 /* valid request outside this build's limits */
+
+#define MIVS_METRIC_L2 0 /* cuVS "sqeuclidean" / FAISS METRIC_L2 */
+#define MIVS_METRIC_IP 1 /* cuVS "inner_product" / FAISS METRIC_INNER_PRODUCT */
+
+#define MIVS_MAX_K 64 /* largest k / n_probes served by the register top-k path */
+
+typedef struct mivs_index_s* mivs_index_t;
+
+/* cuvs.neighbors.ivf_flat.IndexParams (index_building_coordinator.py:395 sets only n_lists) */
+typedef struct {
+  int32_t n_lists;                  /* default in the coordinator: max(1, min(256, N // 1000 + 1)) */
+  int32_t metric;                   /* MIVS_METRIC_* */
+  int32_t kmeans_n_iters;           /* cuVS default 20 */
+  double kmeans_trainset_fraction;  /* cuVS default 0.5 */
+  int64_t kmeans_max_train_per_list;/* 0 = no cap; FAISS-style 256 caps the trainset at 256*n_lists */
+  int32_t add_data_on_build;        /* cuVS default true */
+  int32_t chunk_rows;               /* rows per scan work item (0 = 1024) */
+} mivs_ivf_flat_params;
+
+/* statistics of the last search on an index (bench roofline) */
+typedef struct {
+  int64_t n_queries;
+  int32_t n_probes;
+  int32_t k;
+  int64_t scanned_rows;     /* sum over (query, probed list) of list size: algorithmic rows */
+  int64_t streamed_groups;  /* sum over scan work items of groups read: 32-row groups streamed */
+  int64_t work_items;
+  float scan_ms;            /* device time of the fine-scan kernel (hipEvents on the call's stream) */
+  float coarse_ms;          /* device time of the coarse scan kernel */
+  float total_ms;           /* device time of the whole search call */
+} mivs_search_stats;
+
+const char* mivs_last_error(void);
+int32_t mivs_version(void);
+/* enable hipEvent timing inside search calls (mivs_search_stats.*_ms); 0 = off */
+void mivs_set_profiling(int32_t on);
+
+/* ---- IVF-Flat: replaces cuvs.neighbors.ivf_flat.build (index_building_coordinator.py:396,
+ *      improved_multi_gpu_rag.py:130, cuvs-2gpu-main.ipynb:1767) ---- */
+int32_t mivs_ivf_flat_build(int32_t device, void* stream, const float* d_data, int64_t n, int32_t dim,
+                            const mivs_ivf_flat_params* params, int64_t id_offset, mivs_index_t* out);
+/* build lists from given centroids (fixed-centroid parity; FAISS IndexIVFFlat with a trained quantizer) */
+int32_t mivs_ivf_flat_build_from_centroids(int32_t device, void* stream, const float* d_data, int64_t n,
+                                           int32_t dim, const float* d_centroids, int32_t n_lists,
+                                           int32_t metric, int64_t id_offset, int32_t chunk_rows,
+                                           mivs_index_t* out);
+/* ---- replaces cuvs.neighbors.ivf_flat.search(SearchParams(n_probes), index, q, k)
+ *      (improved_multi_gpu_rag.py:225-227, cuvs-2gpu-main.ipynb:1801) ----
+ *  d_probes (optional, may be NULL): [nq][n_probes] int32 probed list ids in probe order */
+int32_t mivs_ivf_flat_search(mivs_index_t index, void* stream, const float* d_queries, int64_t nq, int32_t k,
+                             int32_t n_probes, float* d_distances, int64_t* d_neighbors, int32_t* d_probes);
+int32_t mivs_ivf_flat_get_centroids(mivs_index_t index, void* stream, float* d_out /* [n_lists][dim] */);
+int32_t mivs_ivf_flat_get_list_sizes(mivs_index_t index, int64_t* h_out /* [n_lists] */);
+/* ids / rows of all lists concatenated in list order ([n_rows], [n_rows][dim]) */
+int32_t mivs_ivf_flat_get_list_ids(mivs_index_t index, void* stream, int64_t* d_out);
+int32_t mivs_ivf_flat_get_list_rows(mivs_index_t index, void* stream, float* d_out);
+
+/* ---- brute force: replaces FAISS IndexFlatL2.add/search (colab_a100_test.ipynb:433-456) and
+ *      cuvs.neighbors.brute_force build/search ---- */
+int32_t mivs_brute_force_build(int32_t device, void* stream, const float* d_data, int64_t n, int32_t dim,
+                               int32_t metric, int64_t id_offset, mivs_index_t* out);
+int32_t mivs_brute_force_search(mivs_index_t index, void* stream, const float* d_queries, int64_t nq, int32_t k,
+                                float* d_distances, int64_t* d_neighbors);
+
+int32_t mivs_index_info(mivs_index_t index, int64_t* n_rows, int32_t* dim, int32_t* n_lists, int32_t* metric,
+                        int32_t* device);
+int32_t mivs_index_last_search_stats(mivs_index_t index, mivs_search_stats* out);
+void mivs_index_free(mivs_index_t index);
+
+/* ---- k-means (the trainer inside ivf_flat::build; cuvs.cluster.kmeans) ----
+ * d_rows: optional [n_train] int64 row ids of the trainset (NULL: rows 0..n_train-1).
+ * d_centroids: in = initial centroids, out = centroids after n_iters Lloyd iterations. */
+int32_t mivs_kmeans_fit(int32_t device, void* stream, const float* d_data, int64_t n, int32_t dim,
+                        const int64_t* d_rows, int64_t n_train, int32_t n_clusters, int32_t n_iters,
+                        float* d_centroids);
+int32_t mivs_kmeans_predict(int32_t device, void* stream, const float* d_data, int64_t n, int32_t dim,
+                            const float* d_centroids, int32_t n_clusters, int32_t metric, int64_t* d_labels);
+
+/* ---- K7: merge m sorted candidate lists per query -> top-k (cross-shard merge after the
+ *      RCCL all-gather; replaces the host numpy merge at improved_multi_gpu_rag.py:266-275) ----
+ * inputs [nq][m][k_in], outputs [nq][k] */
+int32_t mivs_merge_topk(int32_t device, void* stream, const float* d_in_dist, const int64_t* d_in_ids, int64_t nq,
+                        int32_t m, int32_t k_in, int32_t k, int32_t metric, float* d_out_dist,
+                        int64_t* d_out_ids);
+
+/* ---- helpers exposed for parity tests and the bench ---- */
+int32_t mivs_row_norms(int32_t device, void* stream, const float* d_x, int64_t n, int32_t dim, float* d_out);
+int32_t mivs_synth_mixture(int32_t device, void* stream, float* d_out, int64_t row_begin, int64_t n, int32_t dim,
+                           uint64_t seed, int32_t n_centers, float sigma, int32_t normalize);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MIVS_H */

@@ -1,0 +1,312 @@
+/*
+ * mivs CPU oracle — TEST INFRASTRUCTURE ONLY (see mivs_oracle.h header).
+ *
+ * Bit-exact restatement of the arithmetic the HIP path performs
+ * (DESIGN.md §"Arithmetic contract"). Every function cites the reference
+ * call site whose behaviour it restates. Build: oracle/Makefile
+ * (-O2 -mfma -ffp-contract=off: every fused multiply-add below is an explicit
+ * fmaf, nothing else may be contracted or reassociated).
+ */
+#include "mivs_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* dims are zero-padded to a multiple of 32 (kDimAlign in mivs_common.hpp) */
+int orc_dim_pad(int d) { return (d + 31) & ~31; }
+
+/* The dot product in mivs k-order. The HIP kernels compute x·q with
+ * v_mfma_f32_32x32x2_f32, whose result is bit-for-bit the fmaf chain
+ * fma(a[k1],b[k1], fma(a[k0],b[k0], acc)) (verified on MI355X).
+ * Lane (row r, half h) feeds dims 8s+4h+j, j=0..3, so the chain visits
+ * k = 8s+j then 8s+4+j for j = 0..3, s = 0..dpad/8-1. Dims >= d are zero. */
+float orc_dot(const float* a, const float* b, int d) {
+  const int dp = orc_dim_pad(d);
+  float acc = 0.0f;
+  for (int s = 0; s < dp; s += 8) {
+    for (int j = 0; j < 4; ++j) {
+      const int k0 = s + j, k1 = s + 4 + j;
+      const float a0 = k0 < d ? a[k0] : 0.0f, b0 = k0 < d ? b[k0] : 0.0f;
+      const float a1 = k1 < d ? a[k1] : 0.0f, b1 = k1 < d ? b[k1] : 0.0f;
+      acc = fmaf(a0, b0, acc);
+      acc = fmaf(a1, b1, acc);
+    }
+  }
+  return acc;
+}
+
+void orc_norms(const float* x, int64_t n, int d, float* out) {
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; ++i) out[i] = orc_dot(x + i * d, x + i * d, d);
+}
+
+/* L2: the expanded squared distance ‖x‖² + ‖q‖² − 2 x·q, one fused rounding
+ * for the −2·dot term, clamped at 0 (FAISS/cuVS "L2Expanded" semantics,
+ * reached via ivf_flat.search at improved_multi_gpu_rag.py:227).
+ * IP: key = −x·q so that "smaller key is better" for both metrics. */
+float orc_key(float dot, float xn, float qn, int metric) {
+  if (metric == ORC_IP) return -dot;
+  const float t = xn + qn;
+  const float v = fmaf(-2.0f, dot, t);
+  return v > 0.0f ? v : 0.0f;
+}
+
+static float key_to_dist(float key, int metric) { return metric == ORC_IP ? -key : key; }
+
+/* ---- bounded max-heap on (key, id): keeps the k smallest pairs ---- */
+typedef struct { float key; int64_t id; } kv_t;
+
+static int kv_less(kv_t a, kv_t b) { return a.key < b.key || (a.key == b.key && a.id < b.id); }
+
+static void heap_push(kv_t* h, int* sz, int k, kv_t v) {
+  if (*sz < k) {
+    int i = (*sz)++;
+    h[i] = v;
+    while (i > 0) {
+      int p = (i - 1) / 2;
+      if (kv_less(h[p], h[i])) { kv_t t = h[p]; h[p] = h[i]; h[i] = t; i = p; } else break;
+    }
+  } else if (k > 0 && kv_less(v, h[0])) {
+    h[0] = v;
+    int i = 0;
+    for (;;) {
+      int l = 2 * i + 1, r = l + 1, m = i;
+      if (l < k && kv_less(h[m], h[l])) m = l;
+      if (r < k && kv_less(h[m], h[r])) m = r;
+      if (m == i) break;
+      kv_t t = h[m]; h[m] = h[i]; h[i] = t; i = m;
+    }
+  }
+}
+
+static int kv_cmp(const void* a, const void* b) {
+  kv_t x = *(const kv_t*)a, y = *(const kv_t*)b;
+  return kv_less(x, y) ? -1 : (kv_less(y, x) ? 1 : 0);
+}
+
+/* sorted ascending output; missing slots -> (+inf key, id -1) (FAISS convention) */
+static void heap_emit(kv_t* h, int sz, int k, int metric, float* od, int64_t* oi) {
+  qsort(h, (size_t)sz, sizeof(kv_t), kv_cmp);
+  for (int j = 0; j < k; ++j) {
+    if (j < sz) { od[j] = key_to_dist(h[j].key, metric); oi[j] = h[j].id; }
+    else { od[j] = key_to_dist(INFINITY, metric); oi[j] = -1; }
+  }
+}
+
+/* Exact kNN — FAISS IndexFlatL2.search (colab_a100_test.ipynb:454) / sklearn
+ * NearestNeighbors(brute) (VectorSearch_QuestionRetrieval.ipynb:878), with
+ * ties broken by id. */
+void orc_knn(const float* x, int64_t n, const float* q, int64_t nq, int d, int k, int metric,
+             int64_t id_offset, float* out_d, int64_t* out_i) {
+  float* xn = (float*)malloc(sizeof(float) * (size_t)(n > 0 ? n : 1));
+  orc_norms(x, n, d, xn);
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int64_t qi = 0; qi < nq; ++qi) {
+    kv_t* h = (kv_t*)malloc(sizeof(kv_t) * (size_t)(k > 0 ? k : 1));
+    int sz = 0;
+    const float* qq = q + qi * d;
+    const float qn = orc_dot(qq, qq, d);
+    for (int64_t i = 0; i < n; ++i) {
+      kv_t v = {orc_key(orc_dot(x + i * d, qq, d), xn[i], qn, metric), i + id_offset};
+      heap_push(h, &sz, k, v);
+    }
+    heap_emit(h, sz, k, metric, out_d + qi * k, out_i + qi * k);
+    free(h);
+  }
+  free(xn);
+}
+
+/* Global top-k merge of per-shard / per-probe candidate lists — the contract of
+ * SearchResultAggregator.merge_search_results (test_search_result_aggregator.py:308-358)
+ * and the notebook merge (cuvs-2gpu-main.ipynb:1820-1834), ties by id. */
+void orc_merge(const float* in_d, const int64_t* in_i, int64_t nq, int m, int kin, int k, int metric,
+               float* out_d, int64_t* out_i) {
+  kv_t* h = (kv_t*)malloc(sizeof(kv_t) * (size_t)(k > 0 ? k : 1));
+  for (int64_t qi = 0; qi < nq; ++qi) {
+    int sz = 0;
+    for (int64_t c = 0; c < (int64_t)m * kin; ++c) {
+      const int64_t id = in_i[qi * m * kin + c];
+      if (id < 0) continue;
+      const float dd = in_d[qi * m * kin + c];
+      kv_t v = {metric == ORC_IP ? -dd : dd, id};
+      heap_push(h, &sz, k, v);
+    }
+    heap_emit(h, sz, k, metric, out_d + qi * k, out_i + qi * k);
+  }
+  free(h);
+}
+
+/* k-means assign (cuVS kmeans predict inside ivf_flat::build, reached from
+ * index_building_coordinator.py:396): argmin over centroids of the ranking key,
+ * ties to the lower centroid id. */
+void orc_kmeans_assign(const float* x, const int64_t* rows, int64_t nr, const float* c, int nc, int d,
+                       int metric, int32_t* labels) {
+  float* cn = (float*)malloc(sizeof(float) * (size_t)nc);
+  orc_norms(c, nc, d, cn);
+#pragma omp parallel for schedule(static)
+  for (int64_t t = 0; t < nr; ++t) {
+    const float* xr = x + (rows ? rows[t] : t) * (int64_t)d;
+    const float xn = orc_dot(xr, xr, d);
+    float best = INFINITY;
+    int32_t bi = 0;
+    for (int j = 0; j < nc; ++j) {
+      const float kk = orc_key(orc_dot(c + (int64_t)j * d, xr, d), cn[j], xn, metric);
+      if (kk < best) { best = kk; bi = j; }
+    }
+    labels[t] = bi;
+  }
+  free(cn);
+}
+
+/* number of members summed per partial in the deterministic centroid update;
+ * MUST equal MIVS_KM_CHUNK in cuvs-rag_amd/csrc/mivs_common.hpp */
+#define ORC_KM_CHUNK 256
+
+/* stable counting sort of 0..nr-1 by label -> order[], offs[nc+1] */
+static void stable_by_label(const int32_t* labels, int64_t nr, int nc, int64_t* order, int64_t* offs) {
+  memset(offs, 0, sizeof(int64_t) * (size_t)(nc + 1));
+  for (int64_t t = 0; t < nr; ++t) offs[labels[t] + 1]++;
+  for (int j = 0; j < nc; ++j) offs[j + 1] += offs[j];
+  int64_t* fill = (int64_t*)malloc(sizeof(int64_t) * (size_t)nc);
+  memcpy(fill, offs, sizeof(int64_t) * (size_t)nc);
+  for (int64_t t = 0; t < nr; ++t) order[fill[labels[t]]++] = t;
+  free(fill);
+}
+
+/* Lloyd update: centroid = mean of its members, summed in fp64 over fixed
+ * chunks of ORC_KM_CHUNK members (member order = ascending train position),
+ * chunk partials added in chunk order; an empty cluster keeps its centroid. */
+void orc_kmeans_update(const float* x, const int64_t* rows, int64_t nr, const int32_t* labels, int nc, int d,
+                       float* c) {
+  int64_t* order = (int64_t*)malloc(sizeof(int64_t) * (size_t)(nr > 0 ? nr : 1));
+  int64_t* offs = (int64_t*)malloc(sizeof(int64_t) * (size_t)(nc + 1));
+  stable_by_label(labels, nr, nc, order, offs);
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int j = 0; j < nc; ++j) {
+    const int64_t b = offs[j], e = offs[j + 1], cnt = e - b;
+    if (cnt == 0) continue;
+    for (int kk = 0; kk < d; ++kk) {
+      double total = 0.0;
+      for (int64_t cb = b; cb < e; cb += ORC_KM_CHUNK) {
+        const int64_t ce = cb + ORC_KM_CHUNK < e ? cb + ORC_KM_CHUNK : e;
+        double s = 0.0;
+        for (int64_t m = cb; m < ce; ++m) {
+          const int64_t t = order[m];
+          s += (double)x[(rows ? rows[t] : t) * (int64_t)d + kk];
+        }
+        total += s;
+      }
+      c[(int64_t)j * d + kk] = (float)(total / (double)cnt);
+    }
+  }
+  free(order);
+  free(offs);
+}
+
+void orc_kmeans_fit(const float* x, const int64_t* rows, int64_t nr, int nc, int d, int iters, int metric,
+                    float* c) {
+  int32_t* labels = (int32_t*)malloc(sizeof(int32_t) * (size_t)(nr > 0 ? nr : 1));
+  for (int it = 0; it < iters; ++it) {
+    orc_kmeans_assign(x, rows, nr, c, nc, d, metric, labels);
+    orc_kmeans_update(x, rows, nr, labels, nc, d, c);
+  }
+  free(labels);
+}
+
+/* Trainset size: cuVS IndexParams.kmeans_trainset_fraction (default 0.5) with an
+ * optional FAISS-style cap of max_per_list rows per list (FAISS
+ * max_points_per_centroid = 256), never fewer rows than lists. */
+int64_t orc_train_count(int64_t n, int n_lists, double fraction, int64_t max_per_list) {
+  int64_t nt = (int64_t)((double)n * fraction);
+  if (max_per_list > 0 && nt > (int64_t)n_lists * max_per_list) nt = (int64_t)n_lists * max_per_list;
+  if (nt < n_lists) nt = n_lists;
+  if (nt > n) nt = n;
+  return nt;
+}
+
+/* strided trainset rows (cuVS subsamples the dataset with a fixed stride) */
+void orc_train_rows(int64_t n, int64_t n_train, int64_t* rows) {
+  for (int64_t i = 0; i < n_train; ++i) rows[i] = (i * n) / n_train;
+}
+
+/* initial centroid j = train row floor(j * n_train / n_lists) */
+void orc_init_rows(int64_t n_train, int n_lists, int64_t* which) {
+  for (int j = 0; j < n_lists; ++j) which[j] = ((int64_t)j * n_train) / n_lists;
+}
+
+/* cuVS ivf_flat::extend restated: label every row with the trained centroids,
+ * lists hold their rows in ascending id order (stable). */
+void orc_ivf_lists_from_centroids(const float* x, int64_t n, int d, const float* centroids, int n_lists,
+                                  int metric, int64_t id_offset, int64_t* list_sizes, int64_t* list_ids) {
+  int32_t* labels = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+  orc_kmeans_assign(x, NULL, n, centroids, n_lists, d, metric, labels);
+  int64_t* order = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+  int64_t* offs = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n_lists + 1));
+  stable_by_label(labels, n, n_lists, order, offs);
+  for (int j = 0; j < n_lists; ++j) list_sizes[j] = offs[j + 1] - offs[j];
+  for (int64_t i = 0; i < n; ++i) list_ids[i] = order[i] + id_offset;
+  free(labels);
+  free(order);
+  free(offs);
+}
+
+/* ivf_flat.build(IndexParams(n_lists=...), dataset) — index_building_coordinator.py:392-396 */
+void orc_ivf_build(const float* x, int64_t n, int d, int n_lists, int iters, double fraction,
+                   int64_t max_per_list, int metric, int64_t id_offset, float* centroids,
+                   int64_t* list_sizes, int64_t* list_ids) {
+  const int64_t nt = orc_train_count(n, n_lists, fraction, max_per_list);
+  int64_t* rows = (int64_t*)malloc(sizeof(int64_t) * (size_t)nt);
+  int64_t* which = (int64_t*)malloc(sizeof(int64_t) * (size_t)n_lists);
+  orc_train_rows(n, nt, rows);
+  orc_init_rows(nt, n_lists, which);
+  for (int j = 0; j < n_lists; ++j)
+    memcpy(centroids + (int64_t)j * d, x + rows[which[j]] * (int64_t)d, sizeof(float) * (size_t)d);
+  orc_kmeans_fit(x, rows, nt, n_lists, d, iters, ORC_L2, centroids);
+  orc_ivf_lists_from_centroids(x, n, d, centroids, n_lists, metric, id_offset, list_sizes, list_ids);
+  free(rows);
+  free(which);
+}
+
+/* ivf_flat.search(SearchParams(n_probes), index, q, k) — improved_multi_gpu_rag.py:225-227:
+ * coarse top-n_probes lists by (key, list id), exhaustive scan of those lists,
+ * top-k by (key, id). */
+void orc_ivf_search(const float* x, int64_t id_offset, int d, const float* centroids, int n_lists,
+                    const int64_t* list_sizes, const int64_t* list_ids, const float* q, int64_t nq,
+                    int n_probes, int k, int metric, float* out_d, int64_t* out_i, int32_t* out_probes) {
+  if (n_probes > n_lists) n_probes = n_lists;
+  int64_t* offs = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n_lists + 1));
+  offs[0] = 0;
+  for (int j = 0; j < n_lists; ++j) offs[j + 1] = offs[j] + list_sizes[j];
+  float* cn = (float*)malloc(sizeof(float) * (size_t)n_lists);
+  orc_norms(centroids, n_lists, d, cn);
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int64_t qi = 0; qi < nq; ++qi) {
+    const float* qq = q + qi * d;
+    const float qn = orc_dot(qq, qq, d);
+    kv_t* ph = (kv_t*)malloc(sizeof(kv_t) * (size_t)n_probes);
+    int psz = 0;
+    for (int j = 0; j < n_lists; ++j) {
+      kv_t v = {orc_key(orc_dot(centroids + (int64_t)j * d, qq, d), cn[j], qn, metric), j};
+      heap_push(ph, &psz, n_probes, v);
+    }
+    qsort(ph, (size_t)psz, sizeof(kv_t), kv_cmp);
+    kv_t* h = (kv_t*)malloc(sizeof(kv_t) * (size_t)(k > 0 ? k : 1));
+    int sz = 0;
+    for (int p = 0; p < psz; ++p) {
+      const int l = (int)ph[p].id;
+      if (out_probes) out_probes[qi * n_probes + p] = l;
+      for (int64_t m = offs[l]; m < offs[l + 1]; ++m) {
+        const int64_t id = list_ids[m];
+        const float* xr = x + (id - id_offset) * (int64_t)d;
+        kv_t v = {orc_key(orc_dot(xr, qq, d), orc_dot(xr, xr, d), qn, metric), id};
+        heap_push(h, &sz, k, v);
+      }
+    }
+    heap_emit(h, sz, k, metric, out_d + qi * k, out_i + qi * k);
+    free(h);
+    free(ph);
+  }
+  free(offs);
+  free(cn);
+}

@@ -1,0 +1,201 @@
+"""GPU parity: every kernel of the hot path vs the CPU oracle, BIT-EXACT.
+
+The oracle (oracle/mivs_oracle.c) restates the reference's cuVS/FAISS algorithm
+with the engine's pinned arithmetic order (DESIGN.md §"Arithmetic contract"),
+so distances are compared bitwise (np.float32 views as int32) and ids exactly.
+All calls go through libmivs.so (the C-ABI); nothing here has a CPU fallback.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.int32)
+
+
+def _data(n, d, seed, scale=1.0, normalize=False):
+    rng = np.random.default_rng(seed)
+    x = (rng.standard_normal((n, d)) * scale).astype(np.float32)
+    if normalize:
+        x /= np.linalg.norm(x, axis=1, keepdims=True).astype(np.float32)
+    return x
+
+
+def _gpu(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+@pytest.mark.parametrize("d", [1, 7, 32, 64, 100, 128, 384, 768, 1000])
+def test_row_norms_bitexact(mivs_lib, d):
+    from mivs import ops
+
+    x = _data(257, d, seed=d)
+    got = ops.row_norms(_gpu(x)).cpu().numpy()
+    np.testing.assert_array_equal(_bits(got), _bits(O.norms(x)))
+
+
+BF_CASES = [
+    # n, d, nq, k, metric
+    (1, 8, 3, 1, "sqeuclidean"),
+    (5, 16, 7, 10, "sqeuclidean"),        # n < k: padded with (-1, +inf)
+    (1000, 64, 33, 10, "sqeuclidean"),
+    (3001, 100, 65, 1, "sqeuclidean"),
+    (3001, 100, 65, 16, "sqeuclidean"),
+    (4096, 128, 100, 32, "sqeuclidean"),
+    (2500, 384, 40, 64, "sqeuclidean"),   # k=64: merge area in global scratch
+    (5000, 768, 64, 10, "sqeuclidean"),
+    (2000, 128, 50, 10, "inner_product"),
+    (777, 33, 31, 5, "inner_product"),
+]
+
+
+@pytest.mark.parametrize("n,d,nq,k,metric", BF_CASES)
+def test_brute_force_bitexact(mivs_lib, n, d, nq, k, metric):
+    from mivs.neighbors import brute_force
+
+    x = _data(n, d, seed=n + d)
+    q = _data(nq, d, seed=n + d + 1)
+    idx = brute_force.build(_gpu(x), metric=metric)
+    dist, ids = brute_force.search(idx, _gpu(q), k)
+    od, oi = O.knn(x, q, k, metric=metric)
+    np.testing.assert_array_equal(ids.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(dist.cpu().numpy()), _bits(od))
+
+
+def test_brute_force_id_offset_and_self_match(mivs_lib):
+    from mivs.neighbors import brute_force
+
+    x = _data(1500, 96, seed=3, normalize=True)
+    idx = brute_force.build(_gpu(x), ids_offset=1000)
+    dist, ids = brute_force.search(idx, _gpu(x[:200]), 3)
+    ids = ids.cpu().numpy()
+    dist = dist.cpu().numpy()
+    # a row queried against its own index is returned first at distance exactly 0
+    np.testing.assert_array_equal(ids[:, 0], np.arange(200) + 1000)
+    assert (dist[:, 0] == 0.0).all()
+    assert (np.diff(dist, axis=1) >= 0).all()
+
+
+@pytest.mark.parametrize("m,kin,k,metric", [(1, 3, 2, "sqeuclidean"), (8, 10, 10, "sqeuclidean"),
+                                            (40, 16, 10, "inner_product"), (3, 5, 12, "sqeuclidean"),
+                                            (7, 64, 64, "sqeuclidean")])
+def test_merge_topk_matches_oracle(mivs_lib, m, kin, k, metric):
+    from mivs import ops
+
+    rng = np.random.default_rng(m * 100 + k)
+    nq = 77
+    d = rng.random((nq, m, kin)).astype(np.float32)
+    d = np.round(d * 50) / 50  # force ties, broken by id
+    if metric == "inner_product":
+        d = -np.sort(-d, axis=2)
+    else:
+        d = np.sort(d, axis=2)
+    ids = rng.permutation(nq * m * kin).reshape(nq, m, kin).astype(np.int64)
+    ids[:, :, -1] = -1  # padding entries are skipped
+    od, oi = O.merge(d, ids, k, metric=metric)
+    gd, gi = ops.merge_topk(_gpu(d), _gpu(ids), k, metric=metric)
+    np.testing.assert_array_equal(gi.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(gd.cpu().numpy()), _bits(od))
+
+
+def test_reference_merge_fixture_on_gpu(mivs_lib):
+    """test_search_result_aggregator.py:330-358 — two shards merged at k=3."""
+    from mivs import ops
+
+    d = np.array([[[2, 4], [1, 3]], [[6, 8], [5, 7]]], np.float32)
+    i = np.array([[[20, 40], [10, 30]], [[60, 80], [50, 70]]], np.int64)
+    gd, gi = ops.merge_topk(_gpu(d), _gpu(i), 3)
+    np.testing.assert_array_equal(gd.cpu().numpy(), [[1, 2, 3], [5, 6, 7]])
+    np.testing.assert_array_equal(gi.cpu().numpy(), [[10, 20, 30], [50, 60, 70]])
+
+
+@pytest.mark.parametrize("n,d,nc,iters", [(3000, 32, 16, 5), (6000, 100, 40, 3), (20000, 64, 300, 2)])
+def test_kmeans_fit_bitexact(mivs_lib, n, d, nc, iters):
+    from mivs.cluster import kmeans
+
+    x = _data(n, d, seed=nc)
+    c0 = x[(np.arange(nc) * n) // nc]
+    got, _ = kmeans.fit(kmeans.KMeansParams(n_clusters=nc, max_iter=iters), _gpu(x), centroids=_gpu(c0))
+    exp = O.kmeans_fit(x, c0, iters)
+    np.testing.assert_array_equal(_bits(got.cpu().numpy()), _bits(exp))
+    lab = kmeans.predict(kmeans.KMeansParams(n_clusters=nc), got, _gpu(x)).cpu().numpy()
+    np.testing.assert_array_equal(lab, O.kmeans_assign(x, exp))
+
+
+IVF_BUILD_CASES = [
+    # n, d, n_lists, iters, fraction, chunk_rows
+    (5000, 100, 16, 5, 0.5, 0),
+    (8000, 128, 64, 4, 0.3, 64),     # several chunks per list
+    (12000, 768, 32, 2, 0.5, 0),
+    (9000, 64, 1100, 1, 1.0, 0),     # > 1024 lists: coarse step merges centroid chunks
+]
+
+
+@pytest.mark.parametrize("n,d,n_lists,iters,fraction,chunk_rows", IVF_BUILD_CASES)
+def test_ivf_flat_build_and_search_bitexact(mivs_lib, n, d, n_lists, iters, fraction, chunk_rows):
+    from mivs.neighbors import ivf_flat
+
+    x = _data(n, d, seed=n_lists, normalize=True)
+    q = _data(97, d, seed=n_lists + 7, normalize=True)
+    params = ivf_flat.IndexParams(n_lists=n_lists, kmeans_n_iters=iters, kmeans_trainset_fraction=fraction,
+                                  chunk_rows=chunk_rows)
+    idx = ivf_flat.build(params, _gpu(x), ids_offset=5)
+    oc, osz, oids = O.ivf_build(x, n_lists, iters=iters, fraction=fraction, id_offset=5)
+    np.testing.assert_array_equal(_bits(idx.centers.cpu().numpy()), _bits(oc))
+    np.testing.assert_array_equal(idx.list_sizes.numpy(), osz)
+    np.testing.assert_array_equal(idx.list_ids().cpu().numpy(), oids)
+    np.testing.assert_array_equal(idx.list_rows().cpu().numpy(), x[oids - 5])
+    for n_probes, k in [(1, 1), (4, 10), (min(20, n_lists), 32), (min(64, n_lists), 64)]:
+        probes = torch.empty((q.shape[0], n_probes), dtype=torch.int32, device="cuda")
+        dist, ids = ivf_flat.search(ivf_flat.SearchParams(n_probes=n_probes), idx, _gpu(q), k, probes_out=probes)
+        od, oi, op = O.ivf_search(x, oc, osz, oids, q, n_probes, k, id_offset=5)
+        np.testing.assert_array_equal(probes.cpu().numpy(), op)
+        np.testing.assert_array_equal(ids.cpu().numpy(), oi)
+        np.testing.assert_array_equal(_bits(dist.cpu().numpy()), _bits(od))
+
+
+def test_ivf_flat_inner_product_bitexact(mivs_lib):
+    from mivs.neighbors import ivf_flat
+
+    x = _data(6000, 96, seed=11, normalize=True)
+    q = _data(50, 96, seed=12, normalize=True)
+    c0 = x[(np.arange(24) * 6000) // 24]
+    idx = ivf_flat.build_from_centroids(_gpu(c0), _gpu(x), metric="inner_product")
+    osz, oids = O.ivf_lists(x, c0, metric="inner_product")
+    np.testing.assert_array_equal(idx.list_sizes.numpy(), osz)
+    np.testing.assert_array_equal(idx.list_ids().cpu().numpy(), oids)
+    dist, ids = ivf_flat.search(ivf_flat.SearchParams(n_probes=6), idx, _gpu(q), 10)
+    od, oi, _ = O.ivf_search(x, c0, osz, oids, q, 6, 10, metric="inner_product")
+    np.testing.assert_array_equal(ids.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(dist.cpu().numpy()), _bits(od))
+
+
+def test_ivf_full_probe_equals_brute_force(mivs_lib):
+    """n_probes = n_lists scans everything: IVF must return exactly the brute-force answer."""
+    from mivs.neighbors import brute_force, ivf_flat
+
+    x = _data(7000, 64, seed=21, normalize=True)
+    q = _data(120, 64, seed=22, normalize=True)
+    idx = ivf_flat.build(ivf_flat.IndexParams(n_lists=32, kmeans_n_iters=3), _gpu(x))
+    d1, i1 = ivf_flat.search(ivf_flat.SearchParams(n_probes=32), idx, _gpu(q), 10)
+    bf = brute_force.build(_gpu(x))
+    d2, i2 = brute_force.search(bf, _gpu(q), 10)
+    np.testing.assert_array_equal(i1.cpu().numpy(), i2.cpu().numpy())
+    np.testing.assert_array_equal(_bits(d1.cpu().numpy()), _bits(d2.cpu().numpy()))
+
+
+def test_distances_within_1e4_of_fp64(mivs_lib):
+    """north_star tolerance: L2 distances within 1e-4 of the exact (fp64) value."""
+    from mivs.neighbors import brute_force
+
+    x = _data(4000, 768, seed=31, normalize=True)
+    q = _data(64, 768, seed=32, normalize=True)
+    dist, ids = brute_force.search(brute_force.build(_gpu(x)), _gpu(q), 10)
+    ids = ids.cpu().numpy()
+    exact = ((x[ids].astype(np.float64) - q[:, None, :].astype(np.float64)) ** 2).sum(-1)
+    assert np.abs(dist.cpu().numpy() - exact).max() < 1e-4
