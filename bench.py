@@ -1,0 +1,305 @@
+#!/usr/bin/env python3
+"""bench.py — IVF-Flat 10M x 768 on MI355X: QPS @ recall@10 >= 0.95 + index-build vectors/s.
+
+Workload (BASELINE.json configs[2], the metric's config): per GPU a 10,000,000 x 768
+fp32 corpus shard (synthetic clustered data generated ON the device, L2-normalised),
+IVF-Flat n_lists=1024 (cuVS defaults: 20 k-means iterations on a 0.5 trainset
+fraction), batch of Q=10,000 held-out queries, n_probes=32, k=10.
+
+One step = one batched ivf_flat.search of the Q queries on every rank (+ for N>1 the
+RCCL all-gather of the per-shard top-k and the device merge). N GPUs = one process
+per GPU (torch.distributed.run), each rank owns shard `rank` of an N x 10M corpus
+(weak scaling, BASELINE configs[3] at N=8). `value` counts (query, 10M-row shard)
+searches per second = plain QPS at N=1; `qps_full_corpus` is Q / step time.
+
+Also reported: build vectors/s (wall clock, data resident in HBM), recall@10 against
+exact brute-force ground truth (same engine), the fine-scan kernel's roofline
+(hipEvents around the kernel over the timed steps; algorithmic flops and bytes from
+the engine's per-search counts) and the FAISS-algorithm CPU baseline timed on this
+host's cores on a bounded query sample (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cuvs-rag_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "QPS @ recall@10≥0.95 + index-build vectors/sec, 10M×768 IVF-Flat"
+PEAK_HBM_GBS = 8000.0       # MI355X HBM3E peak (MI355X_MICROARCH.md)
+PEAK_F32_MFMA_TFS = 157.3   # dense fp32 MFMA peak (v_mfma_f32_32x32x2_f32)
+QUERY_ROW_BASE = 1 << 40    # queries: same mixture, rows never in any corpus shard
+SEED = 0
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rows", type=int, default=10_000_000, help="corpus rows per GPU")
+    ap.add_argument("--dim", type=int, default=768)
+    ap.add_argument("--queries", type=int, default=10_000)
+    ap.add_argument("--n-lists", type=int, default=1024)
+    ap.add_argument("--n-probes", type=int, default=32)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--kmeans-iters", type=int, default=20)
+    ap.add_argument("--trainset-fraction", type=float, default=0.5)
+    ap.add_argument("--centers", type=int, default=4096, help="mixture centres of the synthetic corpus")
+    ap.add_argument("--sigma", type=float, default=0.35)
+    ap.add_argument("--gt-queries", type=int, default=2000, help="queries with exact ground truth for recall")
+    ap.add_argument("--sweep", default="", help="comma list of n_probes to sweep (QPS + recall each)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--json-out", default="")
+    return ap.parse_args()
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def sync_all(world):
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(v, world, dev):
+    if world == 1:
+        return float(v)
+    t = torch.tensor([float(v)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def recall_at_k(found: np.ndarray, truth: np.ndarray) -> float:
+    """RecallEvaluator.calculate_recall_at_k (improved_multi_gpu_rag.py:314-327) with relevant = exact top-k."""
+    k = truth.shape[1]
+    hits = sum(len(set(f[:k].tolist()) & set(t.tolist())) for f, t in zip(found, truth))
+    return hits / float(truth.size)
+
+
+def load_traffic(cfg_key: str):
+    """HBM bytes per fine-scan launch from the committed rocprofv3 --pmc summary, if one matches."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
+        try:
+            with open(path) as f:
+                j = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if j.get("config_key") == cfg_key and j.get("hbm_bytes_per_launch"):
+            return float(j["hbm_bytes_per_launch"]), os.path.relpath(path, ROOT)
+    return None, None
+
+
+def cpu_baseline(idx, q_host, gt, n_probes, k, target_s, rank_log):
+    """FAISS-algorithm IVF-Flat search (oracle/cpu_baseline.c, OpenMP over queries) on this host."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # bench.py's cpu_baseline leg is one of the oracle's allowed users
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    O.fast_set_threads(threads)
+    rank_log(f"[cpu] copying index to host ({idx.size} rows) ...")
+    rows = idx.list_rows().cpu().numpy()
+    ids = idx.list_ids().cpu().numpy()
+    sizes = idx.list_sizes.numpy()
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    cents = idx.centers.cpu().numpy()
+    O.fast_ivf_search(rows, ids, off, cents, q_host[:4], n_probes, k)  # warm caches / pages
+    t0 = time.perf_counter()
+    O.fast_ivf_search(rows, ids, off, cents, q_host[:16], n_probes, k)
+    per_q = (time.perf_counter() - t0) / 16
+    ns = int(max(16, min(q_host.shape[0], target_s / max(per_q, 1e-9))))
+    t0 = time.perf_counter()
+    _, ci = O.fast_ivf_search(rows, ids, off, cents, q_host[:ns], n_probes, k)
+    dt = time.perf_counter() - t0
+    nr = min(ns, gt.shape[0])
+    rec = recall_at_k(ci[:nr], gt[:nr]) if nr > 0 else None
+    del rows
+    return {"value": ns / dt, "unit": "QPS", "cores": threads, "kind": "port",
+            "sample": f"{ns} of the {q_host.shape[0]} benchmark queries, same index (copied to host), n_probes="
+                      f"{n_probes}, k={k}; FAISS IndexIVFFlat search algorithm restated in oracle/cpu_baseline.c "
+                      f"(faiss not installed); {dt:.1f} s",
+            "recall_at_10": rec}
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("for --gpus N>1 launch with: python -m torch.distributed.run --nproc-per-node N "
+                             "--master-addr 127.0.0.1 bench.py --gpus N")
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    import mivs
+    from mivs import _native, ops
+    from mivs.distributed import merge_across_ranks
+    from mivs.neighbors import brute_force, ivf_flat
+
+    mivs.load()
+    rl = lambda *m: log(rank, *m)  # noqa: E731
+    n, d, Q, k = a.rows, a.dim, a.queries, a.k
+    start = rank * n
+
+    # ---- data: generated on the device (no PCIe in any timed region) ----
+    x = ops.synth_mixture(n, d, SEED, n_centers=a.centers, sigma=a.sigma, row_begin=start, device=local)
+    q = ops.synth_mixture(Q, d, SEED, n_centers=a.centers, sigma=a.sigma, row_begin=QUERY_ROW_BASE, device=local)
+    sync_all(world)
+
+    # ---- build (wall clock, data resident) ----
+    params = ivf_flat.IndexParams(n_lists=a.n_lists, kmeans_n_iters=a.kmeans_iters,
+                                  kmeans_trainset_fraction=a.trainset_fraction)
+    sync_all(world)
+    t0 = time.perf_counter()
+    idx = ivf_flat.build(params, x, ids_offset=start)
+    torch.cuda.synchronize()
+    t_build = max_over_ranks(time.perf_counter() - t0, world, dev)
+    build_vps = n * world / t_build
+    sizes = idx.list_sizes.numpy()
+    rl(f"[build] {n * world} rows in {t_build:.2f} s -> {build_vps / 1e6:.2f} M vec/s; lists min/med/max "
+       f"{sizes.min()}/{int(np.median(sizes))}/{sizes.max()}")
+
+    sp = ivf_flat.SearchParams(n_probes=a.n_probes)
+
+    def step(qq, params=None):
+        dd, ii = ivf_flat.search(params or sp, idx, qq, k)
+        if world > 1:
+            dd, ii = merge_across_ranks(dd, ii, k)
+        return dd, ii
+
+    for _ in range(a.warmup):
+        step(q)
+    _native.set_profiling(True)
+    idx.profile_collect()  # drop warmup records
+    sync_all(world)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        res_d, res_i = step(q)
+    torch.cuda.synchronize()
+    t_local = time.perf_counter() - t0
+    sync_all(world)
+    t_steps = max_over_ranks(t_local, world, dev)
+    prof = idx.profile_collect()
+    _native.set_profiling(False)
+    stats = idx.last_search_stats()
+    ms_per_step = t_steps / a.steps * 1e3
+    qps_full = Q * a.steps / t_steps
+    value = qps_full * world  # (query, 10M-row shard) searches per second; = QPS at N=1
+    rl(f"[search] {a.steps} steps x {Q} queries: {ms_per_step:.3f} ms/step -> {qps_full:,.0f} QPS (full corpus)")
+
+    # ---- recall@10 vs exact ground truth (brute force on the same engine, merged over shards) ----
+    ng = min(a.gt_queries, Q)
+    bf = brute_force.build(x, ids_offset=start)
+    gd, gi = brute_force.search(bf, q[:ng], k)
+    bf.close()
+    del bf
+    torch.cuda.empty_cache()
+    if world > 1:
+        gd, gi = merge_across_ranks(gd, gi, k)
+    gt = gi.cpu().numpy()
+    found = res_i[:ng].cpu().numpy()
+    rec = recall_at_k(found, gt)
+    rl(f"[recall] recall@{k} = {rec:.4f} over {ng} queries (n_probes={a.n_probes})")
+
+    sweep = []
+    for s in [int(v) for v in a.sweep.split(",") if v.strip()]:
+        spp = ivf_flat.SearchParams(n_probes=s)
+        step(q, spp)
+        sync_all(world)
+        t0 = time.perf_counter()
+        for _ in range(max(3, a.steps // 4)):
+            sd, si = step(q, spp)
+        torch.cuda.synchronize()
+        ts = max_over_ranks(time.perf_counter() - t0, world, dev) / max(3, a.steps // 4)
+        sr = recall_at_k(si[:ng].cpu().numpy(), gt)
+        sweep.append({"n_probes": s, "qps_full_corpus": Q / ts, "recall_at_10": sr})
+        rl(f"[sweep] n_probes={s}: {Q / ts:,.0f} QPS recall@{k}={sr:.4f}")
+
+    # ---- roofline of the fine-scan kernel (algorithmic work per launch / avg launch time) ----
+    scan_ms = prof["scan_ms"] / max(prof["n_calls"], 1)
+    flops = 2.0 * d * stats["scanned_rows"]
+    bytes_alg = float(stats["streamed_groups"]) * 32 * d * 4
+    tflops = flops / (scan_ms * 1e-3) / 1e12
+    gbs = bytes_alg / (scan_ms * 1e-3) / 1e9
+    cfg_key = f"ivf_flat_n{n}_d{d}_q{Q}_l{a.n_lists}_p{a.n_probes}_k{k}"
+    traffic, traffic_src = load_traffic(cfg_key)
+    if tflops / PEAK_F32_MFMA_TFS >= gbs / PEAK_HBM_GBS:
+        roof = {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_F32_MFMA_TFS, "unit": "TFLOP/s",
+                "frac": round(tflops / PEAK_F32_MFMA_TFS, 4)}
+    else:
+        roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(gbs / PEAK_HBM_GBS, 4)}
+    roof["traffic"] = traffic
+    roof.update({"kernel": "mivs::k_scan<16,L2> (fine list scan)", "launch_ms": round(scan_ms, 4),
+                 "algorithmic_flops_per_launch": flops, "algorithmic_bytes_per_launch": bytes_alg,
+                 "achieved_gbs_algorithmic": round(gbs, 1), "achieved_tflops": round(tflops, 2),
+                 "traffic_source": traffic_src, "timing": "hipEvents around each fine-scan launch on the search stream, "
+                                                          f"{prof['n_calls']} timed steps"})
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(idx, q.cpu().numpy(), gt, a.n_probes, k, a.cpu_seconds, rl)
+            rl(f"[cpu] {cpu['value']:.2f} QPS on {cpu['cores']} threads (recall {cpu['recall_at_10']})")
+        except Exception as e:  # the GPU result stands without the CPU column
+            rl(f"[cpu] baseline failed: {e!r}")
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "QPS",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": f"synthetic: on-device Gaussian mixture ({a.centers} centres, sigma={a.sigma}, L2-normalised), "
+                f"seed {SEED}; queries = held-out rows of the same mixture",
+        "config": {"workload": f"IVF-Flat {n // 1_000_000}M x {d} fp32 per GPU, n_lists={a.n_lists}, "
+                               f"n_probes={a.n_probes}, k={k}, batch of {Q} queries",
+                   "rows_per_gpu": n, "rows_total": n * world, "dim": d, "queries": Q, "n_lists": a.n_lists,
+                   "n_probes": a.n_probes, "k": k, "kmeans_n_iters": a.kmeans_iters,
+                   "kmeans_trainset_fraction": a.trainset_fraction, "parallelism": f"corpus-shard{world}",
+                   "value_definition": "(query, 10M-row shard) searches per second; equals QPS at n_gpus=1"},
+        "qps_full_corpus": round(qps_full, 2),
+        "recall_at_10": round(rec, 4),
+        "build_vectors_per_s": round(build_vps, 1),
+        "build_s": round(t_build, 3),
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "search_stats": stats,
+        "n_probes_sweep": sweep,
+    }
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    idx.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

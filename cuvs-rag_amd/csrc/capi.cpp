@@ -160,17 +160,27 @@ struct Workspace {
       counts, fill, qp_slots, scan_tmp, gmerge;
 };
 
-struct Events {
-  hipEvent_t e[6] = {};
-  bool ok = false;
-  void create() {
-    if (ok) return;
-    for (auto& x : e) HIPCHK(hipEventCreate(&x));
-    ok = true;
+// hipEvent pairs recorded on the caller's stream around the pipeline stages of
+// every search call while profiling is on; summed by mivs_index_profile_collect
+// (no host sync inside the timed calls).
+struct ProfRec {
+  hipEvent_t e[4] = {};  // search begin, coarse end / fine-scan begin, fine-scan end, search end
+};
+
+struct Profiler {
+  std::vector<ProfRec> pending, pool;
+  ProfRec* begin(hipStream_t s) {
+    ProfRec r;
+    if (!pool.empty()) { r = pool.back(); pool.pop_back(); }
+    else for (auto& x : r.e) HIPCHK(hipEventCreate(&x));
+    pending.push_back(r);
+    HIPCHK(hipEventRecord(pending.back().e[0], s));
+    return &pending.back();
   }
-  ~Events() {
-    if (ok)
-      for (auto& x : e) (void)hipEventDestroy(x);
+  ~Profiler() {
+    for (auto* v : {&pending, &pool})
+      for (auto& r : *v)
+        for (auto& x : r.e) (void)hipEventDestroy(x);
   }
 };
 
@@ -185,8 +195,10 @@ struct mivs_index_s {
   Buf centroids_rm;
   std::mutex mu;
   Workspace ws;
-  Events ev;
-  mivs_search_stats stats{};
+  Profiler prof;
+  // what the last search did (for algorithmic roofline counts)
+  int64_t last_nq = 0;
+  int last_np = 0, last_k = 0;
 };
 
 namespace {
@@ -376,18 +388,14 @@ void check_common(int device, const void* data, int64_t n, int32_t dim) {
 void ivf_search_impl(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                      int64_t* out_i, int32_t* out_probes) {
   Workspace& ws = idx->ws;
-  const bool prof = g_profiling.load() != 0;
-  if (prof) idx->ev.create();
-  if (prof) HIPCHK(hipEventRecord(idx->ev.e[0], s));
+  ProfRec* pr = g_profiling.load() ? idx->prof.begin(s) : nullptr;
   ws.qn.reserve(sizeof(float) * nq);
   HIPCHK(launch_row_norms(q, nq, idx->d, ws.qn.as<float>(), s));
   // coarse: top-n_probes centroids per query
   ws.probes_d.reserve(sizeof(float) * nq * np);
   ws.probes_i.reserve(sizeof(int64_t) * nq * np);
-  if (prof) HIPCHK(hipEventRecord(idx->ev.e[1], s));
   single_list_topk(idx->cents, idx->G, q, ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, np, idx->metric,
                    ws.probes_d.as<float>(), ws.probes_i.as<int64_t>(), idx->device, ws, s);
-  if (prof) HIPCHK(hipEventRecord(idx->ev.e[2], s));
   if (out_probes) HIPCHK(launch_i64_to_i32(ws.probes_i.as<int64_t>(), nq * np, out_probes, s));
   // probe map
   const ListSet& L = idx->lists;
@@ -414,9 +422,9 @@ void ivf_search_impl(mivs_index_s* idx, hipStream_t s, const float* q, int64_t n
   ScanJob j{&L, idx->G, q, ws.qn.as<float>(), idx->d, idx->dp, k, idx->metric, ws.bucket_q.as<int64_t>(),
             ws.bucket_slot.as<int64_t>(), ws.bucket_off.as<int>(), ws.work_off.as<int>(), ws.part_d.as<float>(),
             ws.part_i.as<int64_t>()};
-  if (prof) HIPCHK(hipEventRecord(idx->ev.e[3], s));
+  if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
   run_scan(j, idx->device, ws, s);
-  if (prof) HIPCHK(hipEventRecord(idx->ev.e[4], s));
+  if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
   MergeArgs m{};
   m.in_d = ws.part_d.as<float>();
   m.in_i = ws.part_i.as<int64_t>();
@@ -428,27 +436,10 @@ void ivf_search_impl(mivs_index_s* idx, hipStream_t s, const float* q, int64_t n
   m.out_d = out_d;
   m.out_i = out_i;
   HIPCHK(launch_merge(m, s));
-  if (prof) {
-    HIPCHK(hipEventRecord(idx->ev.e[5], s));
-    HIPCHK(hipEventSynchronize(idx->ev.e[5]));
-    mivs_search_stats st{};
-    st.n_queries = nq;
-    st.n_probes = np;
-    st.k = k;
-    HIPCHK(hipEventElapsedTime(&st.coarse_ms, idx->ev.e[1], idx->ev.e[2]));
-    HIPCHK(hipEventElapsedTime(&st.scan_ms, idx->ev.e[3], idx->ev.e[4]));
-    HIPCHK(hipEventElapsedTime(&st.total_ms, idx->ev.e[0], idx->ev.e[5]));
-    std::vector<int> counts(L.n_lists), woff(L.n_lists + 1);
-    HIPCHK(hipMemcpy(counts.data(), ws.counts.p, sizeof(int) * L.n_lists, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(woff.data(), ws.work_off.p, sizeof(int) * (L.n_lists + 1), hipMemcpyDeviceToHost));
-    for (int l = 0; l < L.n_lists; ++l) {
-      const int64_t sz = L.h_off[l + 1] - L.h_off[l];
-      st.scanned_rows += (int64_t)counts[l] * sz;
-      st.streamed_groups += ceil_div(counts[l], kQTile) * (L.h_goff[l + 1] - L.h_goff[l]);
-    }
-    st.work_items = woff[L.n_lists];
-    idx->stats = st;
-  }
+  if (pr) HIPCHK(hipEventRecord(pr->e[3], s));
+  idx->last_nq = nq;
+  idx->last_np = np;
+  idx->last_k = k;
 }
 
 }  // namespace
@@ -630,28 +621,19 @@ int32_t mivs_brute_force_search(mivs_index_t idx, void* stream, const float* d_q
     std::lock_guard<std::mutex> g(idx->mu);
     DeviceGuard dg(idx->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const bool prof = g_profiling.load() != 0;
-    if (prof) {
-      idx->ev.create();
-      HIPCHK(hipEventRecord(idx->ev.e[0], s));
-    }
+    ProfRec* pr = g_profiling.load() ? idx->prof.begin(s) : nullptr;
     idx->ws.qn.reserve(sizeof(float) * nq);
     HIPCHK(launch_row_norms(d_q, nq, idx->d, idx->ws.qn.as<float>(), s));
+    if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
     single_list_topk(idx->lists, idx->G, d_q, idx->ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, k, idx->metric,
                      d_dist, d_ids, idx->device, idx->ws, s);
-    if (prof) {
-      HIPCHK(hipEventRecord(idx->ev.e[5], s));
-      HIPCHK(hipEventSynchronize(idx->ev.e[5]));
-      mivs_search_stats st{};
-      st.n_queries = nq;
-      st.k = k;
-      st.n_probes = 1;
-      st.scanned_rows = nq * idx->lists.n_rows;
-      st.streamed_groups = ceil_div(nq, kQTile) * idx->lists.n_groups;
-      HIPCHK(hipEventElapsedTime(&st.total_ms, idx->ev.e[0], idx->ev.e[5]));
-      st.scan_ms = st.total_ms;
-      idx->stats = st;
+    if (pr) {
+      HIPCHK(hipEventRecord(pr->e[2], s));
+      HIPCHK(hipEventRecord(pr->e[3], s));
     }
+    idx->last_nq = nq;
+    idx->last_np = 1;
+    idx->last_k = k;
   });
 }
 
@@ -670,7 +652,55 @@ int32_t mivs_index_info(mivs_index_t idx, int64_t* n_rows, int32_t* dim, int32_t
 int32_t mivs_index_last_search_stats(mivs_index_t idx, mivs_search_stats* out) {
   return guarded([&] {
     require(idx != nullptr && out != nullptr, "NULL argument");
-    *out = idx->stats;
+    DeviceGuard dg(idx->device);
+    std::lock_guard<std::mutex> g(idx->mu);
+    mivs_search_stats st{};
+    st.n_queries = idx->last_nq;
+    st.n_probes = idx->last_np;
+    st.k = idx->last_k;
+    const ListSet& L = idx->lists;
+    if (idx->last_nq > 0 && idx->kind == 0) {
+      HIPCHK(hipDeviceSynchronize());
+      std::vector<int> counts(L.n_lists), woff(L.n_lists + 1);
+      HIPCHK(hipMemcpy(counts.data(), idx->ws.counts.p, sizeof(int) * L.n_lists, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(woff.data(), idx->ws.work_off.p, sizeof(int) * (L.n_lists + 1), hipMemcpyDeviceToHost));
+      for (int l = 0; l < L.n_lists; ++l) {
+        st.scanned_rows += (int64_t)counts[l] * (L.h_off[l + 1] - L.h_off[l]);
+        st.streamed_groups += ceil_div(counts[l], kQTile) * (L.h_goff[l + 1] - L.h_goff[l]);
+      }
+      st.work_items = woff[L.n_lists];
+    } else if (idx->last_nq > 0) {
+      st.scanned_rows = idx->last_nq * L.n_rows;
+      st.streamed_groups = ceil_div(idx->last_nq, kQTile) * L.n_groups;
+      st.work_items = ceil_div(idx->last_nq, kQTile) * std::max<int64_t>(1, ceil_div(L.n_groups, idx->G));
+    }
+    *out = st;
+  });
+}
+
+int32_t mivs_index_profile_collect(mivs_index_t idx, mivs_profile* out) {
+  return guarded([&] {
+    require(idx != nullptr && out != nullptr, "NULL argument");
+    DeviceGuard dg(idx->device);
+    std::lock_guard<std::mutex> g(idx->mu);
+    mivs_profile p{};
+    p.scan_ms_min = 0.0f;
+    for (auto& r : idx->prof.pending) {
+      HIPCHK(hipEventSynchronize(r.e[3]));
+      float a = 0, b = 0, c = 0;
+      HIPCHK(hipEventElapsedTime(&a, r.e[0], r.e[1]));
+      HIPCHK(hipEventElapsedTime(&b, r.e[1], r.e[2]));
+      HIPCHK(hipEventElapsedTime(&c, r.e[0], r.e[3]));
+      p.coarse_ms += a;
+      p.scan_ms += b;
+      p.total_ms += c;
+      p.scan_ms_min = p.n_calls == 0 ? b : std::min(p.scan_ms_min, b);
+      p.scan_ms_max = std::max(p.scan_ms_max, b);
+      p.n_calls += 1;
+      idx->prof.pool.push_back(r);
+    }
+    idx->prof.pending.clear();
+    *out = p;
   });
 }
 

@@ -62,8 +62,19 @@ class SearchStats(ctypes.Structure):
         ("scanned_rows", c_int64),
         ("streamed_groups", c_int64),
         ("work_items", c_int64),
-        ("scan_ms", c_float),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+class Profile(ctypes.Structure):
+    _fields_ = [
+        ("n_calls", c_int32),
         ("coarse_ms", c_float),
+        ("scan_ms", c_float),
+        ("scan_ms_min", c_float),
+        ("scan_ms_max", c_float),
         ("total_ms", c_float),
     ]
 
@@ -91,6 +102,7 @@ _SIGS = {
     "mivs_index_info": (c_int32, [c_void_p, POINTER(c_int64), POINTER(c_int32), POINTER(c_int32), POINTER(c_int32),
                                   POINTER(c_int32)]),
     "mivs_index_last_search_stats": (c_int32, [c_void_p, POINTER(SearchStats)]),
+    "mivs_index_profile_collect": (c_int32, [c_void_p, POINTER(Profile)]),
     "mivs_index_free": (None, [c_void_p]),
     "mivs_kmeans_fit": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32, c_int32,
                                   c_void_p]),

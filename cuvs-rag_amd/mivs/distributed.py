@@ -1,0 +1,52 @@
+"""Cross-shard top-k exchange over torch.distributed (RCCL over xGMI on MI355X).
+
+One process per GPU; each rank holds one corpus shard (a contiguous row range,
+``GPUResourceManager.distribute_workload`` — gpu_resource_manager.py:190-202)
+with its own index whose ids are already global (``ids_offset = start_index``,
+fixing the reference's ``i * len(parts[i])`` remap, cuvs-2gpu-main.ipynb:1803).
+After each rank's local search, the per-shard ``[Q, k]`` (distance, id) tiles
+are exchanged with ONE all-gather (Q*k*12 bytes per rank) and merged on the
+device by the K7 wave merge — replacing the reference's host-side numpy
+argsort merge (improved_multi_gpu_rag.py:266-275, cuvs-2gpu-main.ipynb:1820-1834).
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+import torch.distributed as dist
+
+
+def all_gather_topk(distances: torch.Tensor, ids: torch.Tensor, group=None):
+    """-> (dist [Q, world, k], ids [Q, world, k]) gathered from every rank (rank order)."""
+    world = dist.get_world_size(group)
+    q, k = distances.shape
+    gd = torch.empty((world, q, k), dtype=distances.dtype, device=distances.device)
+    gi = torch.empty((world, q, k), dtype=ids.dtype, device=ids.device)
+    dist.all_gather_into_tensor(gd, distances.contiguous(), group=group)
+    dist.all_gather_into_tensor(gi, ids.contiguous(), group=group)
+    return gd.permute(1, 0, 2).contiguous(), gi.permute(1, 0, 2).contiguous()
+
+
+def merge_across_ranks(distances: torch.Tensor, ids: torch.Tensor, k: int, metric: str = "sqeuclidean",
+                       group=None, merge_fn: Optional[Callable] = None):
+    """Global top-k over all shards; every rank gets the same result.
+
+    ``merge_fn(dist[Q, m, k_in], ids[Q, m, k_in], k, metric)`` defaults to the K7 device merge
+    (``mivs.ops.merge_topk``); tests on the CPU gloo backend pass their own.
+    """
+    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return distances, ids
+    gd, gi = all_gather_topk(distances, ids, group)
+    if merge_fn is None:
+        from .ops import merge_topk as merge_fn
+    return merge_fn(gd, gi, k, metric)
+
+
+def allreduce_max(value: float, device: torch.device | None = None, group=None) -> float:
+    """Max of a host scalar over ranks (the bench's max-over-ranks timing)."""
+    if not dist.is_available() or not dist.is_initialized():
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device or "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())

@@ -43,6 +43,12 @@ class Index:
         _native.check(_native.lib().mivs_index_last_search_stats(self.handle, ctypes.byref(st)))
         return st.as_dict()
 
+    def profile_collect(self) -> dict:
+        """Device time of the searches since the last collect (needs mivs._native.set_profiling(True))."""
+        pr = _native.Profile()
+        _native.check(_native.lib().mivs_index_profile_collect(self.handle, ctypes.byref(pr)))
+        return pr.as_dict()
+
     def close(self):
         if self._h is not None and self._h.value and _native._lib is not None:
             _native._lib.mivs_index_free(self._h)

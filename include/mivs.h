@@ -50,22 +50,29 @@ typedef struct {
   int32_t chunk_rows;               /* rows per scan work item (0 = 1024) */
 } mivs_ivf_flat_params;
 
-/* statistics of the last search on an index (bench roofline) */
+/* what the last search on an index did (algorithmic counts for the bench roofline) */
 typedef struct {
   int64_t n_queries;
   int32_t n_probes;
   int32_t k;
   int64_t scanned_rows;     /* sum over (query, probed list) of list size: algorithmic rows */
-  int64_t streamed_groups;  /* sum over scan work items of groups read: 32-row groups streamed */
-  int64_t work_items;
-  float scan_ms;            /* device time of the fine-scan kernel (hipEvents on the call's stream) */
-  float coarse_ms;          /* device time of the coarse scan kernel */
-  float total_ms;           /* device time of the whole search call */
+  int64_t streamed_groups;  /* sum over fine-scan work items of 32-row groups streamed from HBM */
+  int64_t work_items;       /* fine-scan work items */
 } mivs_search_stats;
+
+/* device time of the searches issued since the last collect while profiling was on
+ * (hipEvents recorded on each call's stream; no host sync inside the calls) */
+typedef struct {
+  int32_t n_calls;
+  float coarse_ms;   /* sum: query norms + coarse probe selection */
+  float scan_ms;     /* sum: fine list-scan kernel (the roofline kernel) */
+  float scan_ms_min, scan_ms_max;
+  float total_ms;    /* sum: whole search call */
+} mivs_profile;
 
 const char* mivs_last_error(void);
 int32_t mivs_version(void);
-/* enable hipEvent timing inside search calls (mivs_search_stats.*_ms); 0 = off */
+/* enable hipEvent timing of search calls (mivs_index_profile_collect); 0 = off */
 void mivs_set_profiling(int32_t on);
 
 /* ---- IVF-Flat: replaces cuvs.neighbors.ivf_flat.build (index_building_coordinator.py:396,
@@ -98,6 +105,7 @@ int32_t mivs_brute_force_search(mivs_index_t index, void* stream, const float* d
 int32_t mivs_index_info(mivs_index_t index, int64_t* n_rows, int32_t* dim, int32_t* n_lists, int32_t* metric,
                         int32_t* device);
 int32_t mivs_index_last_search_stats(mivs_index_t index, mivs_search_stats* out);
+int32_t mivs_index_profile_collect(mivs_index_t index, mivs_profile* out);
 void mivs_index_free(mivs_index_t index);
 
 /* ---- k-means (the trainer inside ivf_flat::build; cuvs.cluster.kmeans) ----

@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Pick the synthetic corpus difficulty: recall@10 vs n_probes for several mixture sigmas.
+
+The reference benchmarks only isotropic torch.randn data (improved_multi_gpu_rag.py:431-434),
+on which IVF recall at n_probes=32/n_lists=1024 is far below 0.95 (SURVEY.md §7 'Hard parts');
+bench.py uses a clustered mixture whose sigma is chosen here so that recall@10 at the
+configured n_probes=32 sits near the 0.95 target instead of saturating at 1.0.
+"""
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "cuvs-rag_amd"))
+import numpy as np
+import torch
+
+from mivs import ops
+from mivs.neighbors import brute_force, ivf_flat
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--rows", type=int, default=10_000_000)
+ap.add_argument("--sigmas", default="0.35,1.0,2.0,4.0")
+ap.add_argument("--centers", type=int, default=4096)
+ap.add_argument("--probes", default="4,8,16,32,64")
+a = ap.parse_args()
+Q, k, d = 1000, 10, 768
+for sigma in [float(s) for s in a.sigmas.split(",")]:
+    x = ops.synth_mixture(a.rows, d, 0, n_centers=a.centers, sigma=sigma)
+    q = ops.synth_mixture(Q, d, 0, n_centers=a.centers, sigma=sigma, row_begin=1 << 40)
+    t0 = time.time()
+    idx = ivf_flat.build(ivf_flat.IndexParams(n_lists=1024), x)
+    torch.cuda.synchronize()
+    tb = time.time() - t0
+    bf = brute_force.build(x)
+    _, gt = brute_force.search(bf, q, k)
+    bf.close()
+    gt = gt.cpu().numpy()
+    sizes = idx.list_sizes.numpy()
+    out = []
+    for p in [int(v) for v in a.probes.split(",")]:
+        _, ii = ivf_flat.search(ivf_flat.SearchParams(n_probes=p), idx, q, k)
+        ii = ii.cpu().numpy()
+        rec = np.mean([len(set(a_) & set(b_)) / k for a_, b_ in zip(ii, gt)])
+        out.append(f"p{p}={rec:.3f}")
+    print(f"sigma={sigma} centers={a.centers} build={tb:.2f}s lists min/med/max={sizes.min()}/{int(np.median(sizes))}/"
+          f"{sizes.max()} recall: " + " ".join(out), flush=True)
+    idx.close()
+    del x, q
+    torch.cuda.empty_cache()
