@@ -21,10 +21,11 @@ def all_gather_topk(distances: torch.Tensor, ids: torch.Tensor, group=None):
     """-> (dist [Q, world, k], ids [Q, world, k]) gathered from every rank (rank order)."""
     world = dist.get_world_size(group)
     q, k = distances.shape
-    gd = torch.empty((world, q, k), dtype=distances.dtype, device=distances.device)
-    gi = torch.empty((world, q, k), dtype=ids.dtype, device=ids.device)
+    gd = torch.empty((world * q, k), dtype=distances.dtype, device=distances.device)
+    gi = torch.empty((world * q, k), dtype=ids.dtype, device=ids.device)
     dist.all_gather_into_tensor(gd, distances.contiguous(), group=group)
     dist.all_gather_into_tensor(gi, ids.contiguous(), group=group)
+    gd, gi = gd.view(world, q, k), gi.view(world, q, k)
     return gd.permute(1, 0, 2).contiguous(), gi.permute(1, 0, 2).contiguous()
 
 

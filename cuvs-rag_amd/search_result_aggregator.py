@@ -1,0 +1,294 @@
+"""Distributed search + global top-k merge across GPU shards.
+
+The reference ships this module as an EMPTY file (``Attempt_1/search_result_aggregator.py``,
+0 bytes); its API exists only as the contract in ``Attempt_1/test_search_result_aggregator.py``
+(:14-21 exports, :25-236 types, :239-499 behaviour) and ``Latest/cuVS-2-gpu/old/
+DesignDocument.md:119-137,174-189``. This is that contract, written for MI355X:
+
+  * per-GPU search runs on each shard's mivs index (``ivf_flat`` / ``brute_force``), one
+    thread per GPU (native calls release the GIL), queries copied to each device once;
+  * the global merge is the K7 wave top-k kernel on the device (``mivs.ops.merge_topk``),
+    replacing the reference's host numpy argsort (improved_multi_gpu_rag.py:266-275,
+    cuvs-2gpu-main.ipynb:1820-1834); rows merge independently, so the ``(P, k)`` concat +
+    axis-0 fancy-index bug (``index 2 is out of bounds``, RequirementsDocument.md:5) cannot occur;
+  * shards built by the coordinator carry GLOBAL ids (``ids_offset = start_index``), so no
+    ``i * len(parts[i])`` remap is needed (cuvs-2gpu-main.ipynb:1803).
+
+Without a usable engine (``CUVS_AVAILABLE`` False: no GPU) the aggregator runs the contract's
+simulation (``_simulate_search``) and merges on the host; it never falls back to CPU search.
+Multi-process (one rank per GPU) deployments merge with ``mivs.distributed.merge_across_ranks``.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+import time
+from concurrent.futures import ThreadPoolExecutor, as_completed
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from gpu_resource_manager import GPUResourceManager
+from mivs.backend import engine_available
+
+logger = logging.getLogger(__name__)
+
+CUVS_AVAILABLE = engine_available()
+
+
+@dataclass
+class SearchResult:
+    """One GPU's answer: distances f32 [nq, k'], global ids i64 [nq, k'] (contract :25-134)."""
+    distances: np.ndarray
+    indices: np.ndarray
+    gpu_id: int
+    query_time: float
+    k_requested: int
+    k_returned: int
+
+    def __post_init__(self):
+        if self.gpu_id < 0:
+            raise ValueError(f"gpu_id must be non-negative, got {self.gpu_id}")
+        if self.query_time < 0:
+            raise ValueError(f"query_time must be non-negative, got {self.query_time}")
+        if self.k_requested <= 0:
+            raise ValueError(f"k_requested must be positive, got {self.k_requested}")
+        if self.k_returned > self.k_requested:
+            raise ValueError(f"k_returned ({self.k_returned}) cannot exceed k_requested ({self.k_requested})")
+        if np.ndim(self.distances) != 2:
+            raise ValueError("distances must be 2D array")
+        if np.shape(self.distances) != np.shape(self.indices):
+            raise ValueError(f"distances shape {np.shape(self.distances)} != indices shape {np.shape(self.indices)}")
+
+    @property
+    def num_queries(self) -> int:
+        return int(np.shape(self.distances)[0])
+
+
+@dataclass
+class AggregatedSearchResult:
+    """Global top-k over all shards (contract :137-206)."""
+    final_distances: np.ndarray
+    final_indices: np.ndarray
+    total_query_time: float
+    gpu_results: List[SearchResult]
+    k_requested: int
+    k_returned: int
+    num_queries: int
+
+    def __post_init__(self):
+        if self.k_requested <= 0:
+            raise ValueError(f"k_requested must be positive, got {self.k_requested}")
+        if self.num_queries <= 0:
+            raise ValueError(f"num_queries must be positive, got {self.num_queries}")
+
+
+@dataclass
+class SearchConfig:
+    """Contract :212-236; ``search_params`` key 'nprobe'. ``id_offsets`` (mivs extension): per-GPU
+    offset added to local ids of indices built WITHOUT ``ids_offset``."""
+    k: int
+    search_params: Optional[Dict[str, Any]] = None
+    parallel_search: bool = True
+    timeout_seconds: Optional[float] = None
+    validate_results: bool = True
+    id_offsets: Optional[Dict[int, int]] = field(default=None)
+
+    def __post_init__(self):
+        if self.k <= 0:
+            raise ValueError(f"k must be positive, got {self.k}")
+        if self.timeout_seconds is not None and self.timeout_seconds <= 0:
+            raise ValueError(f"timeout_seconds must be positive, got {self.timeout_seconds}")
+
+
+def _host_merge(dist: np.ndarray, ids: np.ndarray, k: int) -> Tuple[np.ndarray, np.ndarray]:
+    """Row-wise (distance, id) ascending merge of [nq, m] candidates, first min(k, m) kept."""
+    kk = min(k, dist.shape[1])
+    out_d = np.empty((dist.shape[0], kk), np.float32)
+    out_i = np.empty((dist.shape[0], kk), np.int64)
+    for r in range(dist.shape[0]):
+        order = np.lexsort((ids[r], dist[r]))[:kk]
+        out_d[r], out_i[r] = dist[r, order], ids[r, order]
+    return out_d, out_i
+
+
+def _device_merge(dists: List[torch.Tensor], ids: List[torch.Tensor], k: int, metric: str,
+                  device: torch.device) -> Tuple[torch.Tensor, torch.Tensor]:
+    """K7 merge of per-shard [nq, k_i] tiles gathered on one device."""
+    from mivs import ops
+
+    kin = max(t.shape[1] for t in dists)
+    nq = dists[0].shape[0]
+    pad_d = torch.full((nq, len(dists), kin), float("inf"), dtype=torch.float32, device=device)
+    pad_i = torch.full((nq, len(dists), kin), -1, dtype=torch.int64, device=device)
+    for s, (d, i) in enumerate(zip(dists, ids)):
+        pad_d[:, s, : d.shape[1]] = d.to(device, non_blocking=True)
+        pad_i[:, s, : i.shape[1]] = i.to(device, non_blocking=True)
+    return ops.merge_topk(pad_d, pad_i, k, metric=metric)
+
+
+def combine_search_results(results: List[SearchResult], k: int) -> Tuple[np.ndarray, np.ndarray]:
+    """Functional form of :meth:`SearchResultAggregator.merge_search_results`."""
+    return SearchResultAggregator.__new__(SearchResultAggregator).merge_search_results(results, k)
+
+
+def filter_search_results_by_distance(result: SearchResult, max_distance: float) -> SearchResult:
+    """Mask entries farther than ``max_distance`` as (id -1, distance +inf), FAISS's missing-result form."""
+    d = np.array(result.distances, dtype=np.float32, copy=True)
+    i = np.array(result.indices, dtype=np.int64, copy=True)
+    drop = ~(d <= max_distance)
+    d[drop] = np.inf
+    i[drop] = -1
+    kept = int((~drop).sum(axis=1).max()) if d.size else 0
+    return SearchResult(d, i, result.gpu_id, result.query_time, result.k_requested, min(kept, result.k_requested))
+
+
+class SearchResultAggregator:
+    """Fans a query batch out to every shard's index and merges the answers into one global top-k."""
+
+    def __init__(self, gpu_manager: GPUResourceManager):
+        self.gpu_manager = gpu_manager
+        self.search_history: List[AggregatedSearchResult] = []
+        self._active_searches: Dict[int, bool] = {}
+        self._lock = threading.Lock()
+
+    # ---- validation / merge --------------------------------------------------------------------
+    def validate_search_results(self, gpu_results: List[SearchResult], expected_queries: int,
+                                expected_k: int) -> bool:
+        if not gpu_results:
+            raise ValueError("gpu_results cannot be empty")
+        for r in gpu_results:
+            if r.num_queries != expected_queries:
+                raise ValueError(f"GPU {r.gpu_id} has {r.num_queries} queries, expected {expected_queries}")
+            if np.isnan(np.asarray(r.distances, dtype=np.float32)).any():
+                raise ValueError(f"GPU {r.gpu_id} results contains NaN distances")
+        return True
+
+    def merge_search_results(self, gpu_results: List[SearchResult], k: int) -> Tuple[np.ndarray, np.ndarray]:
+        """Per query: all shards' candidates, ascending by (distance, id), first min(k, total) kept."""
+        if not gpu_results:
+            raise ValueError("Cannot merge empty results list")
+        nq = gpu_results[0].num_queries
+        for r in gpu_results:
+            if r.num_queries != nq:
+                raise ValueError(f"GPU {r.gpu_id} has {r.num_queries} queries, expected {nq}")
+        width = sum(np.shape(r.distances)[1] for r in gpu_results)
+        kk = min(k, width)
+        if CUVS_AVAILABLE and kk <= 64:
+            dev = torch.device(f"cuda:{torch.cuda.current_device()}")
+            d, i = _device_merge([torch.as_tensor(np.asarray(r.distances, np.float32)) for r in gpu_results],
+                                 [torch.as_tensor(np.asarray(r.indices, np.int64)) for r in gpu_results], kk,
+                                 "sqeuclidean", dev)
+            return d.cpu().numpy(), i.cpu().numpy()
+        dist = np.concatenate([np.asarray(r.distances, np.float32) for r in gpu_results], axis=1)
+        ids = np.concatenate([np.asarray(r.indices, np.int64) for r in gpu_results], axis=1)
+        return _host_merge(dist, ids, kk)
+
+    def _simulate_search(self, query: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Contract :389-403: shape (nq, k), non-negative, ascending per row. No device is touched."""
+        nq = query.shape[0]
+        dist, _ = torch.sort(torch.rand(nq, k) * 10.0, dim=1)
+        ids = torch.randint(0, 1_000_000, (nq, k), dtype=torch.int64)
+        return dist, ids
+
+    # ---- search ----------------------------------------------------------------------------------
+    def _search_one(self, gpu_id: int, index: Any, query: torch.Tensor, config: SearchConfig):
+        """-> (distances tensor [nq, k'], ids tensor [nq, k'], seconds) on that GPU (or simulated)."""
+        t0 = time.time()
+        if not CUVS_AVAILABLE:
+            d, i = self._simulate_search(query, config.k)
+            return d, i, time.time() - t0
+        from mivs.neighbors import brute_force, ivf_flat
+
+        device = self.gpu_manager.get_safe_device_string(gpu_id)
+        with torch.cuda.device(gpu_id):
+            q = query.to(device)
+            params = config.search_params or {}
+            if isinstance(index, ivf_flat.Index):
+                sp = ivf_flat.SearchParams(n_probes=int(params.get("nprobe", params.get("n_probes", 20))))
+                d, i = ivf_flat.search(sp, index, q, config.k)
+            elif isinstance(index, brute_force.Index):
+                d, i = brute_force.search(index, q, config.k)
+            else:
+                raise TypeError(f"GPU {gpu_id}: unsupported index object {type(index).__name__}")
+            d = d.tensor if hasattr(d, "tensor") else torch.as_tensor(d)
+            i = i.tensor if hasattr(i, "tensor") else torch.as_tensor(i)
+            if config.id_offsets and gpu_id in config.id_offsets:
+                i = torch.where(i >= 0, i + int(config.id_offsets[gpu_id]), i)
+            torch.cuda.current_stream().synchronize()
+        return d, i, time.time() - t0
+
+    def perform_distributed_search(self, query: torch.Tensor, indices: Dict[int, Any],
+                                   config: SearchConfig) -> AggregatedSearchResult:
+        if not isinstance(query, torch.Tensor):
+            raise ValueError("query must be a torch.Tensor")
+        if query.dim() != 2:
+            raise ValueError("query must be 2D tensor")
+        if query.size(0) == 0:
+            raise ValueError("query cannot be empty")
+        if not indices:
+            raise ValueError("indices dictionary cannot be empty")
+        for g in indices:
+            if not self.gpu_manager.validate_gpu_index(g):
+                raise ValueError(f"GPU {g} in indices is not available")
+
+        nq = query.size(0)
+        t0 = time.time()
+        with self._lock:
+            self._active_searches.update({g: True for g in indices})
+        raw: Dict[int, Tuple[torch.Tensor, torch.Tensor, float]] = {}
+        try:
+            if config.parallel_search and len(indices) > 1:
+                with ThreadPoolExecutor(max_workers=len(indices)) as pool:
+                    futs = {pool.submit(self._search_one, g, idx, query, config): g for g, idx in indices.items()}
+                    for fut in as_completed(futs, timeout=config.timeout_seconds):
+                        raw[futs[fut]] = fut.result()
+            else:
+                for g, idx in indices.items():
+                    raw[g] = self._search_one(g, idx, query, config)
+        finally:
+            with self._lock:
+                for g in indices:
+                    self._active_searches.pop(g, None)
+
+        order = sorted(raw)
+        gpu_results = [SearchResult(distances=raw[g][0].detach().cpu().numpy().astype(np.float32),
+                                    indices=raw[g][1].detach().cpu().numpy().astype(np.int64), gpu_id=g,
+                                    query_time=raw[g][2], k_requested=config.k,
+                                    k_returned=min(config.k, int(raw[g][0].shape[1]))) for g in order]
+        if config.validate_results:
+            self.validate_search_results(gpu_results, nq, config.k)
+        kk = min(config.k, sum(int(raw[g][0].shape[1]) for g in order))
+        if CUVS_AVAILABLE and kk <= 64:
+            metric = getattr(indices[order[0]], "metric", "sqeuclidean")
+            dev = torch.device(f"cuda:{order[0]}")
+            with torch.cuda.device(order[0]):
+                fd, fi = _device_merge([raw[g][0] for g in order], [raw[g][1] for g in order], kk, metric, dev)
+            final_d, final_i = fd.cpu().numpy(), fi.cpu().numpy()
+        else:
+            final_d, final_i = self.merge_search_results(gpu_results, config.k)
+        result = AggregatedSearchResult(final_distances=final_d, final_indices=final_i,
+                                        total_query_time=time.time() - t0, gpu_results=gpu_results,
+                                        k_requested=config.k, k_returned=int(final_d.shape[1]), num_queries=nq)
+        self.search_history.append(result)
+        return result
+
+    # ---- history ---------------------------------------------------------------------------------
+    def get_search_history(self) -> List[AggregatedSearchResult]:
+        return list(self.search_history)
+
+    def clear_search_history(self) -> None:
+        self.search_history.clear()
+
+    def get_active_searches(self) -> Dict[int, bool]:
+        with self._lock:
+            return dict(self._active_searches)
+
+    def __str__(self) -> str:
+        return f"SearchResultAggregator(history_size={len(self.search_history)})"
+
+    def __repr__(self) -> str:
+        return (f"SearchResultAggregator(gpu_manager={self.gpu_manager!r}, history_size={len(self.search_history)}, "
+                f"active_searches={len(self._active_searches)})")
