@@ -54,8 +54,10 @@ def parse():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--kmeans-iters", type=int, default=20)
     ap.add_argument("--trainset-fraction", type=float, default=0.5)
-    ap.add_argument("--centers", type=int, default=4096, help="mixture centres of the synthetic corpus")
-    ap.add_argument("--sigma", type=float, default=0.35)
+    # 65,536 centres, sigma 0.75 (tools/tune_dataset.py, profiles/r01_dataset_tuning.log): recall@10 0.96 at
+    # n_probes=32 and 0.94 at 16, i.e. 32 is the smallest swept n_probes reaching the 0.95 target
+    ap.add_argument("--centers", type=int, default=65536, help="mixture centres of the synthetic corpus")
+    ap.add_argument("--sigma", type=float, default=0.75)
     ap.add_argument("--gt-queries", type=int, default=2000, help="queries with exact ground truth for recall")
     ap.add_argument("--sweep", default="", help="comma list of n_probes to sweep (QPS + recall each)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")

@@ -234,11 +234,11 @@ void run_scan(const ScanJob& j, int device, Workspace& ws, hipStream_t s) {
   const int kcap = scan_kcap(j.k);
   require(kcap > 0, "k must be in [1, " + std::to_string(kMaxK) + "]", MIVS_ERR_UNSUPPORTED);
   require(j.dp <= 1024, "dim > 1024 is not supported by this build", MIVS_ERR_UNSUPPORTED);
-  const size_t lds = scan_lds_bytes(j.dp, kcap);
+  const size_t lds = scan_lds_bytes(j.dp, kcap, j.G);
   const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / lds)));
   const int grid = cu_count(device) * per_cu;
   float* gmerge = nullptr;
-  if (!scan_merge_in_lds(j.dp, kcap)) {
+  if (!scan_merge_in_lds(j.dp, kcap, j.G)) {
     ws.gmerge.reserve(scan_gmerge_bytes(grid, kcap));
     gmerge = ws.gmerge.as<float>();
   }
@@ -327,7 +327,8 @@ void assign_rows(const float* data, const float* data_norms, const int64_t* rows
 
 // n_iters Lloyd iterations on trainset rows; centroids_rm in/out [nc][d]
 void kmeans_fit_impl(const float* data, const float* data_norms, const int64_t* rows, int64_t n_train, int d, int dp,
-                     int nc, int iters, float* centroids_rm, int G, int device, Workspace& ws, hipStream_t s) {
+                     int nc, int iters, float* centroids_rm, int G, int device, Workspace& ws, hipStream_t s,
+                     bool balance = false) {
   if (iters <= 0) return;
   Buf labels, perm, off, partial, chunk_off, tmp, ctmp;
   labels.reserve(sizeof(int64_t) * n_train);
@@ -346,6 +347,9 @@ void kmeans_fit_impl(const float* data, const float* data_norms, const int64_t* 
                                 cb, s));
     HIPCHK(launch_km_update(data, d, rows, perm.as<int64_t>(), off.as<int64_t>(), nc, n_train,
                             partial.as<double>(), chunk_off.as<int64_t>(), tmp.p, centroids_rm, s));
+    if (balance && it < iters - kBalanceKeepLast)
+      HIPCHK(launch_km_rebalance(data, d, rows, labels.as<int64_t>(), off.as<int64_t>(), nc, n_train, it,
+                                 centroids_rm, s));
   }
   HIPCHK(hipStreamSynchronize(s));
 }
@@ -492,7 +496,7 @@ int32_t mivs_ivf_flat_build(int32_t device, void* stream, const float* d_data, i
     HIPCHK(launch_row_norms(d_data, n, dim, norms.as<float>(), s));
     HIPCHK(hipStreamSynchronize(s));
     kmeans_fit_impl(d_data, norms.as<float>(), rows.as<int64_t>(), nt, dim, idx->dp, nl, p->kmeans_n_iters,
-                    idx->centroids_rm.as<float>(), idx->G, device, idx->ws, s);
+                    idx->centroids_rm.as<float>(), idx->G, device, idx->ws, s, p->kmeans_balance != 0);
     make_single_list(idx->cents, idx->centroids_rm.as<float>(), nl, dim, idx->dp, 0, idx->G, s);
     if (p->add_data_on_build) {
       build_lists(idx.get(), d_data, norms.as<float>(), n, s);

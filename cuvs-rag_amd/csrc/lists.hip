@@ -90,15 +90,18 @@ __device__ __forceinline__ int find_list(const int64_t* __restrict__ off, int n_
 __global__ void k_unpack(const float* __restrict__ groups, int dp, int d, const int64_t* __restrict__ list_off,
                          const int64_t* __restrict__ list_goff, int n_lists, int64_t n_rows,
                          float* __restrict__ out) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_rows * (int64_t)d) return;
-  const int64_t row = t / d;
-  const int c = (int)(t - row * d);
-  const int l = find_list(list_off, n_lists, row);
-  const int64_t r = row - list_off[l];
-  const int64_t g = list_goff[l] + r / kGroupRows;
-  const int rr = (int)(r % kGroupRows);
-  out[t] = groups[g * (int64_t)(kGroupRows * dp) + (c >> 3) * 256 + rr * 8 + (c & 7)];
+  // grid-stride: n_rows * d can exceed the 2^32 work-item limit of one launch
+  const int64_t total = n_rows * (int64_t)d;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const int64_t row = t / d;
+    const int c = (int)(t - row * d);
+    const int l = find_list(list_off, n_lists, row);
+    const int64_t r = row - list_off[l];
+    const int64_t g = list_goff[l] + r / kGroupRows;
+    const int rr = (int)(r % kGroupRows);
+    out[t] = groups[g * (int64_t)(kGroupRows * dp) + (c >> 3) * 256 + rr * 8 + (c & 7)];
+  }
 }
 
 __global__ void k_compact_ids(const int64_t* __restrict__ row_ids, const int64_t* __restrict__ list_off,
@@ -112,11 +115,13 @@ __global__ void k_compact_ids(const int64_t* __restrict__ row_ids, const int64_t
 
 __global__ void k_gather_rows(const float* __restrict__ src, int d, const int64_t* __restrict__ rows, int64_t n,
                               float* __restrict__ dst) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n * (int64_t)d) return;
-  const int64_t i = t / d;
-  const int c = (int)(t - i * d);
-  dst[t] = src[rows[i] * (int64_t)d + c];
+  const int64_t total = n * (int64_t)d;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const int64_t i = t / d;
+    const int c = (int)(t - i * d);
+    dst[t] = src[rows[i] * (int64_t)d + c];
+  }
 }
 
 // ---- k-means update (K5): fixed member order, fp64 partials over kKmChunk members ----
@@ -167,13 +172,56 @@ __global__ __launch_bounds__(256) void k_km_final(const double* __restrict__ par
   }
 }
 
-// ---- synthetic clustered corpus (bench / large-scale tests) ----
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
   x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
   return x ^ (x >> 31);
 }
+
+// Balancing step (cuVS kmeans_balanced adjust_centers, restated in oracle orc_kmeans_rebalance):
+// a centroid j whose cluster holds fewer than kBalFrac x the average members is pulled next to the
+// centroid of an over-average cluster L found by probing train positions (r0 + p*kBalStep) mod n:
+// c_j = (wc * c_L + x_t) / (wc + 1), wc = min(size_j, 4). Big clusters are never written, so the
+// blocks are independent. One block per centroid.
+constexpr double kBalFrac = 0.25;
+constexpr float kBalWc = 4.0f;
+constexpr int kBalProbes = 64;
+constexpr uint64_t kBalStep = 2654435761ull;
+constexpr uint64_t kBalSeed = 0x5851F42D4C957F2Dull;
+
+__global__ __launch_bounds__(256) void k_km_rebalance(const float* __restrict__ x, int d,
+                                                      const int64_t* __restrict__ rows,
+                                                      const int64_t* __restrict__ labels,
+                                                      const int64_t* __restrict__ list_off, int nc,
+                                                      int64_t n_train, int it, float* __restrict__ cent) {
+  __shared__ int64_t donor;
+  const int c = blockIdx.x;
+  const double avg = (double)n_train / (double)nc;
+  const int64_t size = list_off[c + 1] - list_off[c];
+  if (!((double)size < kBalFrac * avg)) return;
+  if (threadIdx.x == 0) {
+    donor = -1;
+    const uint64_t r0 = splitmix64(kBalSeed ^ ((uint64_t)it << 32) ^ (uint64_t)c) % (uint64_t)n_train;
+    for (int p = 0; p < kBalProbes; ++p) {
+      const int64_t t = (int64_t)((r0 + (uint64_t)p * kBalStep) % (uint64_t)n_train);
+      const int64_t l = labels[t];
+      if ((double)(list_off[l + 1] - list_off[l]) > avg) { donor = t; break; }
+    }
+  }
+  __syncthreads();
+  if (donor < 0) return;
+  const int64_t row = rows ? rows[donor] : donor;
+  const int64_t L = labels[donor];
+  const float wc = (float)size < kBalWc ? (float)size : kBalWc;
+  for (int dim = threadIdx.x; dim < d; dim += blockDim.x) {
+    float v = wc * cent[L * d + dim];
+    v = v + x[row * d + dim];
+    cent[(int64_t)c * d + dim] = v / (wc + 1.0f);
+  }
+}
+
+// ---- synthetic clustered corpus (bench / large-scale tests) ----
 
 // Irwin-Hall(4) approximation of N(0,1) from one 64-bit hash (exact integer -> fp32 steps)
 __device__ __forceinline__ float gauss4(uint64_t h) {
@@ -211,6 +259,11 @@ __global__ __launch_bounds__(256) void k_synth(float* __restrict__ out, int64_t 
 }
 
 inline dim3 grid1(int64_t n, int b) { return dim3((unsigned)ceil_div(n > 0 ? n : 1, b)); }
+// for grid-stride kernels: cap so blocks * 256 stays far below the 2^32 work-item limit
+inline dim3 grid_capped(int64_t n, int b) {
+  const int64_t g = ceil_div(n > 0 ? n : 1, b);
+  return dim3((unsigned)(g < (1 << 20) ? g : (1 << 20)));
+}
 
 }  // namespace
 
@@ -233,7 +286,7 @@ hipError_t launch_row_norms(const float* x, int64_t n, int d, float* out, hipStr
 hipError_t launch_unpack_rows(const float* groups, int dp, int d, const int64_t* list_off, const int64_t* list_goff,
                               int n_lists, int64_t n_rows, float* out, hipStream_t s) {
   if (n_rows <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_unpack, grid1(n_rows * d, 256), dim3(256), 0, s, groups, dp, d, list_off, list_goff, n_lists,
+  hipLaunchKernelGGL(k_unpack, grid_capped(n_rows * d, 256), dim3(256), 0, s, groups, dp, d, list_off, list_goff, n_lists,
                      n_rows, out);
   return hipGetLastError();
 }
@@ -248,7 +301,7 @@ hipError_t launch_compact_ids(const int64_t* row_ids, const int64_t* list_off, c
 
 hipError_t launch_gather_rows(const float* src, int d, const int64_t* rows, int64_t n, float* dst, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_gather_rows, grid1(n * d, 256), dim3(256), 0, s, src, d, rows, n, dst);
+  hipLaunchKernelGGL(k_gather_rows, grid_capped(n * d, 256), dim3(256), 0, s, src, d, rows, n, dst);
   return hipGetLastError();
 }
 
@@ -271,10 +324,25 @@ hipError_t launch_km_update(const float* x, int d, const int64_t* rows, const in
   return hipGetLastError();
 }
 
+hipError_t launch_km_rebalance(const float* x, int d, const int64_t* rows, const int64_t* labels,
+                               const int64_t* list_off, int nc, int64_t n_train, int it, float* centroids,
+                               hipStream_t s) {
+  if (nc <= 0 || n_train <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_km_rebalance, dim3((unsigned)nc), dim3(256), 0, s, x, d, rows, labels, list_off, nc, n_train,
+                     it, centroids);
+  return hipGetLastError();
+}
+
 hipError_t launch_synth_mixture(float* out, int64_t row_begin, int64_t n, int d, uint64_t seed, int n_centers,
                                 float sigma, int normalize, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_synth, grid1(n, 4), dim3(256), 0, s, out, row_begin, n, d, seed, n_centers, sigma, normalize);
+  // one wave per row: launch in slices of 2^24 rows so a launch stays under 2^32 work-items
+  constexpr int64_t kSlice = int64_t(1) << 24;
+  for (int64_t b = 0; b < n; b += kSlice) {
+    const int64_t m = n - b < kSlice ? n - b : kSlice;
+    hipLaunchKernelGGL(k_synth, grid1(m, 4), dim3(256), 0, s, out + b * (int64_t)d, row_begin + b, m, d, seed,
+                       n_centers, sigma, normalize);
+  }
   return hipGetLastError();
 }
 

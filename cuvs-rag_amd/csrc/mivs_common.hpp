@@ -16,7 +16,7 @@ namespace mivs {
 
 constexpr int kGroupRows = 32;     // rows per interleaved group (= MFMA M)
 constexpr int kQTile = 32;         // queries per work item (= MFMA N)
-constexpr int kDimAlign = 32;      // dp = round_up(d, 32)
+constexpr int kDimAlign = 64;      // dp = round_up(d, 64): k-steps come in blocks of 8
 constexpr int kScanWaves = 8;      // waves per scan workgroup (2 per SIMD)
 constexpr int kScanThreads = kScanWaves * 64;
 constexpr int kKmChunk = 256;      // members per fp64 partial in the k-means update (== ORC_KM_CHUNK)
@@ -74,8 +74,8 @@ struct MergeArgs {
 // ---- host-side launchers (implemented in the .hip files) ----
 hipError_t launch_scan(const ScanArgs& a, int kcap, int grid, size_t lds_bytes, hipStream_t s);
 hipError_t launch_scan_ex(const ScanArgs& a, int kcap, int grid, size_t lds_bytes, float* gmerge, hipStream_t s);
-size_t scan_lds_bytes(int dp, int kcap);
-bool scan_merge_in_lds(int dp, int kcap);
+size_t scan_lds_bytes(int dp, int kcap, int chunk_groups);
+bool scan_merge_in_lds(int dp, int kcap, int chunk_groups);
 size_t scan_gmerge_bytes(int grid, int kcap);
 int scan_kcap(int k);
 hipError_t launch_train_rows(int64_t* rows, int64_t n, int64_t n_train, hipStream_t s);
@@ -113,6 +113,10 @@ hipError_t launch_km_update(const float* x, int d, const int64_t* rows, const in
                             const int64_t* list_off, int nc, int64_t n_members, double* partial,
                             int64_t* chunk_off, void* tmp, float* centroids, hipStream_t s);
 size_t km_partial_rows(int64_t n_members, int nc);
+constexpr int kBalanceKeepLast = 2;  // last k-means iterations without re-seeding (== ORC_BAL_KEEP_LAST)
+hipError_t launch_km_rebalance(const float* x, int d, const int64_t* rows, const int64_t* labels,
+                               const int64_t* list_off, int nc, int64_t n_train, int it, float* centroids,
+                               hipStream_t s);
 
 hipError_t launch_gather_rows(const float* src, int d, const int64_t* rows, int64_t n, float* dst, hipStream_t s);
 hipError_t launch_unpack_rows(const float* groups, int dp, int d, const int64_t* list_off, const int64_t* list_goff,

@@ -50,14 +50,62 @@ __device__ __forceinline__ void lane_insert(float (&lk)[KCAP], int (&lp)[KCAP], 
   }
 }
 
+// Block of BLK k-steps of one row group: BLK dwordx4 loads per lane (one contiguous 1 KiB wave load each)
+template <int BLK>
+__device__ __forceinline__ void load_block(float4 (&v)[BLK], const float* __restrict__ p) {
+#pragma unroll
+  for (int u = 0; u < BLK; ++u) v[u] = *reinterpret_cast<const float4*>(p + u * 256);
+}
+
+template <int BLK>
+__device__ __forceinline__ void mma_block(f32x16& acc, const float4 (&v)[BLK], const float* __restrict__ qrow) {
+#pragma unroll
+  for (int u = 0; u < BLK; ++u) {
+    const float4 b = *reinterpret_cast<const float4*>(qrow + u * 8);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v[u].x, b.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v[u].y, b.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v[u].z, b.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v[u].w, b.w, acc, 0, 0, 0);
+  }
+}
+
+// Dot tile of one finished group -> ranking keys -> this lane's register top-K.
+// Row norms come from LDS (staged per work item) so no VMEM wait can drain the prefetch stream.
+template <int KCAP, int METRIC>
+__device__ __forceinline__ void epilogue(const f32x16& acc, const float* __restrict__ gnorm, int64_t rbase, int h,
+                                         float qn, bool qvalid, float (&lk)[KCAP], int (&lp)[KCAP]) {
+  float xn[16];
+#pragma unroll
+  for (int q4 = 0; q4 < 4; ++q4) {
+    const float4 t = *reinterpret_cast<const float4*>(gnorm + 8 * q4 + 4 * h);
+    xn[4 * q4 + 0] = t.x; xn[4 * q4 + 1] = t.y; xn[4 * q4 + 2] = t.z; xn[4 * q4 + 3] = t.w;
+  }
+  if (!qvalid) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float key;
+    if (METRIC == kL2) {
+      const float v = fmaf(-2.0f, acc[r], xn[r] + qn);
+      key = v > 0.0f ? v : 0.0f;
+    } else {
+      key = xn[r] < INFINITY ? -acc[r] : INFINITY;
+    }
+    if (key < lk[KCAP - 1]) lane_insert<KCAP>(lk, lp, key, (int)(rbase + (r & 3) + 8 * (r >> 2) + 4 * h));
+  }
+}
+
 template <int KCAP, int METRIC>
 __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a, float* __restrict__ gmerge) {
+  // k-steps per register buffer: 8 (2 KiB of list rows in flight per lane-pair ring slot) unless the
+  // register top-K is large
+  constexpr int BLK = KCAP >= 32 ? 4 : 8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int64_t* s_q = reinterpret_cast<int64_t*>(smem);          // [32] query row ids (-1: empty lane)
   int64_t* s_slot = s_q + 32;                                // [32] output slot (already + chunk)
   float* s_qn = reinterpret_cast<float*>(s_slot + 32);       // [32]
   int* s_misc = reinterpret_cast<int*>(s_qn + 32);           // [4]
-  float* qtile = reinterpret_cast<float*>(smem + kSmallBytes);
+  float* s_norm = reinterpret_cast<float*>(smem + kSmallBytes);  // [G*32] row norms of the chunk
+  float* qtile = s_norm + a.chunk_groups * kGroupRows;
   const int dp = a.dp;
   const int qstride = dp + 4;  // +16 B per row: conflict-free ds_read_b128 of the B operand
 
@@ -71,7 +119,7 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a, float* __r
   const int j = lane & 31;  // query column of this lane in the MFMA tile
   const int h = lane >> 5;  // k-half / row-half of this lane
   const int total = a.work_off[a.n_lists];
-  const int S = dp >> 3;    // k-steps of 8 dims (multiple of 4)
+  const int bpg = (dp >> 3) / BLK;  // blocks per group (dp is a multiple of 64)
 
   for (;;) {
     if (tid == 0) s_misc[0] = atomicAdd(a.work_counter, 1);
@@ -109,6 +157,10 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a, float* __r
         s_qn[tid] = INFINITY;
       }
     }
+    {  // row norms of the chunk -> LDS
+      const int nn = (int)(g_end - g_begin) * kGroupRows;
+      for (int i = tid; i < nn; i += kScanThreads) s_norm[i] = a.row_norms[g_begin * kGroupRows + i];
+    }
     __syncthreads();
 
     // ---- stage the query tile in LDS (zero-padded dims, zero rows for empty lanes) ----
@@ -133,51 +185,48 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a, float* __r
     const bool qvalid = s_q[j] >= 0;
     const float* qrow = qtile + j * qstride + 4 * h;
 
-    for (int64_t g = g_begin + wave; g < g_end; g += kScanWaves) {
-      const float* gp = a.groups + g * (int64_t)(kGroupRows * dp) + j * 8 + 4 * h;
+    // ---- this wave's row groups g_begin+wave, +8, ... as ONE stream of BLK-step blocks, two
+    //      register buffers (A: even blocks, B: odd blocks): the load of block b+2 is issued right
+    //      after block b's MFMAs, so a full block of MFMAs covers every load, across group
+    //      boundaries too ----
+    const int64_t g0 = g_begin + wave;
+    const int ng = g_end > g0 ? (int)((g_end - g0 + kScanWaves - 1) / kScanWaves) : 0;
+    const int nb = ng * bpg;
+    if (nb > 0) {
+      const float* lane_base = a.groups + g0 * (int64_t)(kGroupRows * dp) + j * 8 + 4 * h;
+      const int64_t gstride = (int64_t)kScanWaves * kGroupRows * dp;
+      auto bptr = [&](int b) {
+        const int bb = b < nb ? b : nb - 1;  // past the end: re-read the last block (never consumed)
+        const int gi = bb / bpg;
+        return lane_base + gi * gstride + (bb - gi * bpg) * (BLK * 256);
+      };
+      float4 A[BLK], B[BLK];
+      load_block<BLK>(A, bptr(0));
+      load_block<BLK>(B, bptr(1));
       f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      float4 av[4], an[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) av[u] = *reinterpret_cast<const float4*>(gp + u * 256);
-      for (int s0 = 0; s0 < S; s0 += 4) {
-        if (s0 + 4 < S) {
-#pragma unroll
-          for (int u = 0; u < 4; ++u) an[u] = *reinterpret_cast<const float4*>(gp + (s0 + 4 + u) * 256);
+      const f32x16 zero = acc;
+      int gi = 0, sb = 0;  // group / block-in-group of the block being consumed
+      // Both halves run unconditionally (an odd stream gets one dummy block whose result is never
+      // used): every path through the body then issues the same loads in the same order, so the
+      // compiler's vmcnt at the loop head can keep the other buffer's loads in flight.
+      for (int b = 0; b < nb; b += 2) {
+        mma_block<BLK>(acc, A, qrow + sb * (BLK * 8));
+        load_block<BLK>(A, bptr(b + 2));
+        if (++sb == bpg) {
+          epilogue<KCAP, METRIC>(acc, s_norm + (wave + gi * kScanWaves) * kGroupRows,
+                                 (g0 + (int64_t)gi * kScanWaves) * kGroupRows, h, qn, qvalid, lk, lp);
+          acc = zero;
+          sb = 0;
+          ++gi;
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float4 b = *reinterpret_cast<const float4*>(qrow + (s0 + u) * 8);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u].x, b.x, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u].y, b.y, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u].z, b.z, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u].w, b.w, acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) av[u] = an[u];
-      }
-
-      // ---- epilogue: 16 rows of this lane's query ----
-      const int64_t rbase = g * kGroupRows;
-      float xn[16];
-#pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4) {
-        const float4 t = *reinterpret_cast<const float4*>(a.row_norms + rbase + 8 * q4 + 4 * h);
-        xn[4 * q4 + 0] = t.x; xn[4 * q4 + 1] = t.y; xn[4 * q4 + 2] = t.z; xn[4 * q4 + 3] = t.w;
-      }
-      if (qvalid) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float key;
-          if (METRIC == kL2) {
-            const float v = fmaf(-2.0f, acc[r], xn[r] + qn);
-            key = v > 0.0f ? v : 0.0f;
-          } else {
-            key = xn[r] < INFINITY ? -acc[r] : INFINITY;
-          }
-          if (key < lk[KCAP - 1]) {
-            const int pos = (int)(rbase + (r & 3) + 8 * (r >> 2) + 4 * h);
-            lane_insert<KCAP>(lk, lp, key, pos);
-          }
+        mma_block<BLK>(acc, B, qrow + sb * (BLK * 8));
+        load_block<BLK>(B, bptr(b + 3));
+        if (++sb == bpg && b + 1 < nb) {
+          epilogue<KCAP, METRIC>(acc, s_norm + (wave + gi * kScanWaves) * kGroupRows,
+                                 (g0 + (int64_t)gi * kScanWaves) * kGroupRows, h, qn, qvalid, lk, lp);
+          acc = zero;
+          sb = 0;
+          ++gi;
         }
       }
     }
@@ -255,16 +304,22 @@ int scan_kcap(int k) {
 
 static size_t merge_bytes(int kcap) { return (size_t)kQTile * 16 * kcap * 8; }
 static size_t qtile_bytes(int dp) { return (size_t)kQTile * (dp + 4) * 4; }
+static size_t norm_bytes(int chunk_groups) { return (size_t)chunk_groups * kGroupRows * 4; }
 static constexpr size_t kLdsMax = 160 * 1024;
 
-// LDS request; the merge area moves to global scratch when it does not fit
-size_t scan_lds_bytes(int dp, int kcap) {
+// LDS request: [small][chunk norms][query tile | merge area]; the merge area moves to global
+// scratch when it does not fit beside the norms
+size_t scan_lds_bytes(int dp, int kcap, int chunk_groups) {
+  const size_t base = kSmallBytes + norm_bytes(chunk_groups);
   const size_t q = qtile_bytes(dp), m = merge_bytes(kcap);
-  const size_t both = kSmallBytes + (q > m ? q : m);
-  return both <= kLdsMax ? both : kSmallBytes + q;
+  const size_t both = base + (q > m ? q : m);
+  return both <= kLdsMax ? both : base + q;
 }
 
-bool scan_merge_in_lds(int dp, int kcap) { return kSmallBytes + merge_bytes(kcap) <= kLdsMax && kSmallBytes + qtile_bytes(dp) <= kLdsMax; }
+bool scan_merge_in_lds(int dp, int kcap, int chunk_groups) {
+  const size_t base = kSmallBytes + norm_bytes(chunk_groups);
+  return base + merge_bytes(kcap) <= kLdsMax && base + qtile_bytes(dp) <= kLdsMax;
+}
 
 size_t scan_gmerge_bytes(int grid, int kcap) { return (size_t)grid * merge_bytes(kcap); }
 

@@ -33,7 +33,7 @@ logger = logging.getLogger(__name__)
 CUVS_AVAILABLE = engine_available()
 
 VALID_INDEX_TYPES = ["ivf_flat", "ivf_pq", "cagra", "brute_force"]
-_IVF_FLAT_KEYS = ("metric", "kmeans_n_iters", "kmeans_trainset_fraction", "kmeans_max_train_per_list",
+_IVF_FLAT_KEYS = ("metric", "kmeans_n_iters", "kmeans_trainset_fraction", "kmeans_max_train_per_list", "kmeans_balance",
                   "add_data_on_build", "chunk_rows")
 
 

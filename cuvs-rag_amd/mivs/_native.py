@@ -51,6 +51,7 @@ class IvfFlatParams(ctypes.Structure):
         ("kmeans_max_train_per_list", c_int64),
         ("add_data_on_build", c_int32),
         ("chunk_rows", c_int32),
+        ("kmeans_balance", c_int32),
     ]
 
 

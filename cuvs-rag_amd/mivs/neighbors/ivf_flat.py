@@ -46,7 +46,7 @@ class IndexParams:
     def __init__(self, n_lists: int = 1024, metric: str = "sqeuclidean", kmeans_n_iters: int = 20,
                  kmeans_trainset_fraction: float = 0.5, add_data_on_build: bool = True,
                  adaptive_centers: bool = False, conservative_memory_allocation: bool = False,
-                 kmeans_max_train_per_list: int = 0, chunk_rows: int = 0):
+                 kmeans_max_train_per_list: int = 0, chunk_rows: int = 0, kmeans_balance: bool = True):
         if int(n_lists) < 1:
             raise ValueError(f"n_lists must be >= 1, got {n_lists}")
         metric_code(metric)
@@ -61,11 +61,13 @@ class IndexParams:
         self.conservative_memory_allocation = bool(conservative_memory_allocation)
         self.kmeans_max_train_per_list = int(kmeans_max_train_per_list)
         self.chunk_rows = int(chunk_rows)
+        self.kmeans_balance = bool(kmeans_balance)
 
     def _c(self) -> _native.IvfFlatParams:
         return _native.IvfFlatParams(self.n_lists, metric_code(self.metric), self.kmeans_n_iters,
                                      self.kmeans_trainset_fraction, self.kmeans_max_train_per_list,
-                                     1 if self.add_data_on_build else 0, self.chunk_rows)
+                                     1 if self.add_data_on_build else 0, self.chunk_rows,
+                                     1 if self.kmeans_balance else 0)
 
     def __repr__(self):
         return (f"IndexParams(n_lists={self.n_lists}, metric={self.metric!r}, kmeans_n_iters={self.kmeans_n_iters}, "

@@ -48,6 +48,8 @@ typedef struct {
   int64_t kmeans_max_train_per_list;/* 0 = no cap; FAISS-style 256 caps the trainset at 256*n_lists */
   int32_t add_data_on_build;        /* cuVS default true */
   int32_t chunk_rows;               /* rows per scan work item (0 = 1024) */
+  int32_t kmeans_balance;           /* 1: re-seed under-filled clusters (balanced lists, the role of cuVS's
+                                       balanced k-means); 0: plain Lloyd */
 } mivs_ivf_flat_params;
 
 /* what the last search on an index did (algorithmic counts for the bench roofline) */

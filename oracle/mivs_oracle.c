@@ -13,8 +13,9 @@
 #include <stdlib.h>
 #include <string.h>
 
-/* dims are zero-padded to a multiple of 32 (kDimAlign in mivs_common.hpp) */
-int orc_dim_pad(int d) { return (d + 31) & ~31; }
+/* dims are zero-padded to a multiple of 64 (kDimAlign in mivs_common.hpp); zero dims add exact
+ * fmaf(0,0,acc) == acc steps (acc is never -0), so the padding is bitwise neutral */
+int orc_dim_pad(int d) { return (d + 63) & ~63; }
 
 /* The dot product in mivs k-order. The HIP kernels compute x·q with
  * v_mfma_f32_32x32x2_f32, whose result is bit-for-bit the fmaf chain
@@ -204,12 +205,66 @@ void orc_kmeans_update(const float* x, const int64_t* rows, int64_t nr, const in
   free(offs);
 }
 
+static uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+/* Balancing step — restates cuVS kmeans_balanced's adjust_centers (the balanced k-means inside
+ * ivf_flat::build): every centroid j whose cluster holds fewer than ORC_BAL_FRAC x the average
+ * members is pulled next to the centroid of an over-average cluster L:
+ *     c_j = (wc * c_L + x_t) / (wc + 1),  wc = min(size_j, ORC_BAL_WC)
+ * where x_t is the first member of an over-average cluster met by probing train positions
+ * (r0 + p*ORC_BAL_STEP) mod nr, p < ORC_BAL_PROBES, r0 = splitmix64(ORC_BAL_SEED ^ (it << 32) ^ j) mod nr
+ * (our deterministic probe sequence; cuVS uses its own). Placed that close to c_L, c_j splits L
+ * in the next assignment. MUST match k_km_rebalance in cuvs-rag_amd/csrc/lists.hip. */
+#define ORC_BAL_WC 4.0f
+#define ORC_BAL_FRAC 0.25
+#define ORC_BAL_PROBES 64
+#define ORC_BAL_STEP 2654435761ull
+#define ORC_BAL_SEED 0x5851F42D4C957F2Dull
+#define ORC_BAL_KEEP_LAST 2 /* the last iterations are plain Lloyd */
+
+void orc_kmeans_rebalance(const float* x, const int64_t* rows, int64_t nr, const int32_t* labels, int nc, int d,
+                          int it, float* c) {
+  int64_t* sizes = (int64_t*)calloc((size_t)nc, sizeof(int64_t));
+  for (int64_t t = 0; t < nr; ++t) sizes[labels[t]]++;
+  const double avg = (double)nr / (double)nc;
+  for (int j = 0; j < nc; ++j) {
+    if (!((double)sizes[j] < ORC_BAL_FRAC * avg)) continue;
+    const uint64_t r0 = splitmix64(ORC_BAL_SEED ^ ((uint64_t)it << 32) ^ (uint64_t)j) % (uint64_t)nr;
+    for (int p = 0; p < ORC_BAL_PROBES; ++p) {
+      const int64_t t = (int64_t)((r0 + (uint64_t)p * ORC_BAL_STEP) % (uint64_t)nr);
+      const int32_t L = labels[t];
+      if ((double)sizes[L] > avg) {
+        const float wc = (float)sizes[j] < ORC_BAL_WC ? (float)sizes[j] : ORC_BAL_WC;
+        const float* xr = x + (rows ? rows[t] : t) * (int64_t)d;
+        for (int kk = 0; kk < d; ++kk) {
+          float v = wc * c[(int64_t)L * d + kk];
+          v = v + xr[kk];
+          c[(int64_t)j * d + kk] = v / (wc + 1.0f);
+        }
+        break;
+      }
+    }
+  }
+  free(sizes);
+}
+
 void orc_kmeans_fit(const float* x, const int64_t* rows, int64_t nr, int nc, int d, int iters, int metric,
                     float* c) {
+  orc_kmeans_fit_ex(x, rows, nr, nc, d, iters, metric, 0, c);
+}
+
+void orc_kmeans_fit_ex(const float* x, const int64_t* rows, int64_t nr, int nc, int d, int iters, int metric,
+                       int balance, float* c) {
   int32_t* labels = (int32_t*)malloc(sizeof(int32_t) * (size_t)(nr > 0 ? nr : 1));
   for (int it = 0; it < iters; ++it) {
     orc_kmeans_assign(x, rows, nr, c, nc, d, metric, labels);
     orc_kmeans_update(x, rows, nr, labels, nc, d, c);
+    if (balance && it < iters - ORC_BAL_KEEP_LAST) orc_kmeans_rebalance(x, rows, nr, labels, nc, d, it, c);
   }
   free(labels);
 }
@@ -253,7 +308,7 @@ void orc_ivf_lists_from_centroids(const float* x, int64_t n, int d, const float*
 
 /* ivf_flat.build(IndexParams(n_lists=...), dataset) — index_building_coordinator.py:392-396 */
 void orc_ivf_build(const float* x, int64_t n, int d, int n_lists, int iters, double fraction,
-                   int64_t max_per_list, int metric, int64_t id_offset, float* centroids,
+                   int64_t max_per_list, int metric, int balance, int64_t id_offset, float* centroids,
                    int64_t* list_sizes, int64_t* list_ids) {
   const int64_t nt = orc_train_count(n, n_lists, fraction, max_per_list);
   int64_t* rows = (int64_t*)malloc(sizeof(int64_t) * (size_t)nt);
@@ -262,7 +317,7 @@ void orc_ivf_build(const float* x, int64_t n, int d, int n_lists, int iters, dou
   orc_init_rows(nt, n_lists, which);
   for (int j = 0; j < n_lists; ++j)
     memcpy(centroids + (int64_t)j * d, x + rows[which[j]] * (int64_t)d, sizeof(float) * (size_t)d);
-  orc_kmeans_fit(x, rows, nt, n_lists, d, iters, ORC_L2, centroids);
+  orc_kmeans_fit_ex(x, rows, nt, n_lists, d, iters, ORC_L2, balance, centroids);
   orc_ivf_lists_from_centroids(x, n, d, centroids, n_lists, metric, id_offset, list_sizes, list_ids);
   free(rows);
   free(which);

@@ -48,6 +48,11 @@ void orc_kmeans_update(const float* x, const int64_t* rows, int64_t nr, const in
                        float* c /* in: previous, out: updated */);
 void orc_kmeans_fit(const float* x, const int64_t* rows, int64_t nr, int nc, int d, int iters, int metric,
                     float* c /* in: init, out: final */);
+/* balance != 0: re-seed under-filled clusters after each update except the last two iterations */
+void orc_kmeans_fit_ex(const float* x, const int64_t* rows, int64_t nr, int nc, int d, int iters, int metric,
+                       int balance, float* c);
+void orc_kmeans_rebalance(const float* x, const int64_t* rows, int64_t nr, const int32_t* labels, int nc, int d,
+                          int it, float* c);
 
 /* trainset + init selection used by mivs_ivf_flat_build */
 int64_t orc_train_count(int64_t n, int n_lists, double fraction, int64_t max_per_list);
@@ -57,7 +62,7 @@ void orc_init_rows(int64_t n_train, int n_lists, int64_t* which /* indices into 
 /* IVF-Flat build: centroids out [n_lists][d]; list_sizes out [n_lists];
  * list_ids out [n] (lists concatenated in list order, each list by ascending id) */
 void orc_ivf_build(const float* x, int64_t n, int d, int n_lists, int iters, double fraction,
-                   int64_t max_per_list, int metric, int64_t id_offset, float* centroids,
+                   int64_t max_per_list, int metric, int balance, int64_t id_offset, float* centroids,
                    int64_t* list_sizes, int64_t* list_ids);
 void orc_ivf_lists_from_centroids(const float* x, int64_t n, int d, const float* centroids, int n_lists,
                                   int metric, int64_t id_offset, int64_t* list_sizes, int64_t* list_ids);

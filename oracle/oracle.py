@@ -41,10 +41,11 @@ def lib():
             "orc_kmeans_assign": (None, [P, P, i64, P, i32, i32, i32, P]),
             "orc_kmeans_update": (None, [P, P, i64, P, i32, i32, P]),
             "orc_kmeans_fit": (None, [P, P, i64, i32, i32, i32, i32, P]),
+            "orc_kmeans_fit_ex": (None, [P, P, i64, i32, i32, i32, i32, i32, P]),
             "orc_train_count": (i64, [i64, i32, f64, i64]),
             "orc_train_rows": (None, [i64, i64, P]),
             "orc_init_rows": (None, [i64, i32, P]),
-            "orc_ivf_build": (None, [P, i64, i32, i32, i32, f64, i64, i32, i64, P, P, P]),
+            "orc_ivf_build": (None, [P, i64, i32, i32, i32, f64, i64, i32, i32, i64, P, P, P]),
             "orc_ivf_lists_from_centroids": (None, [P, i64, i32, P, i32, i32, i64, P, P]),
             "orc_ivf_search": (None, [P, i64, i32, P, i32, P, P, P, i64, i32, i32, i32, P, P, P]),
             "orc_fast_threads": (i32, []),
@@ -121,12 +122,14 @@ def kmeans_assign(x, c, rows=None, metric="sqeuclidean"):
     return out
 
 
-def kmeans_fit(x, c0, iters, rows=None, metric="sqeuclidean"):
+def kmeans_fit(x, c0, iters, rows=None, metric="sqeuclidean", balance=False):
+    """Lloyd from c0; balance=True adds the under-filled-cluster re-seeding of the IVF build."""
     x = _f32(x)
     c = _f32(c0).copy()
     r = None if rows is None else _i64(rows)
     nr = x.shape[0] if r is None else r.shape[0]
-    lib().orc_kmeans_fit(_p(x), _p(r), nr, c.shape[0], x.shape[1], iters, metric_code(metric), _p(c))
+    lib().orc_kmeans_fit_ex(_p(x), _p(r), nr, c.shape[0], x.shape[1], iters, metric_code(metric), int(balance),
+                            _p(c))
     return c
 
 
@@ -140,15 +143,15 @@ def train_rows(n, n_train) -> np.ndarray:
     return out
 
 
-def ivf_build(x, n_lists, iters=20, fraction=0.5, max_per_list=0, metric="sqeuclidean", id_offset=0):
+def ivf_build(x, n_lists, iters=20, fraction=0.5, max_per_list=0, metric="sqeuclidean", id_offset=0, balance=True):
     """-> (centroids [n_lists, d], list_sizes [n_lists], list_ids [n])."""
     x = _f32(x)
     n, d = x.shape
     cents = np.empty((n_lists, d), np.float32)
     sizes = np.empty(n_lists, np.int64)
     ids = np.empty(n, np.int64)
-    lib().orc_ivf_build(_p(x), n, d, n_lists, iters, fraction, max_per_list, metric_code(metric), id_offset,
-                        _p(cents), _p(sizes), _p(ids))
+    lib().orc_ivf_build(_p(x), n, d, n_lists, iters, fraction, max_per_list, metric_code(metric), int(balance),
+                        id_offset, _p(cents), _p(sizes), _p(ids))
     return cents, sizes, ids
 
 

@@ -159,6 +159,32 @@ def test_ivf_flat_build_and_search_bitexact(mivs_lib, n, d, n_lists, iters, frac
         np.testing.assert_array_equal(_bits(dist.cpu().numpy()), _bits(od))
 
 
+def test_ivf_flat_unbalanced_lloyd_bitexact(mivs_lib):
+    from mivs.neighbors import ivf_flat
+
+    x = _data(9000, 64, seed=41, normalize=True)
+    idx = ivf_flat.build(ivf_flat.IndexParams(n_lists=48, kmeans_n_iters=6, kmeans_balance=False), _gpu(x))
+    oc, osz, oids = O.ivf_build(x, 48, iters=6, balance=False)
+    np.testing.assert_array_equal(_bits(idx.centers.cpu().numpy()), _bits(oc))
+    np.testing.assert_array_equal(idx.list_ids().cpu().numpy(), oids)
+
+
+def test_kmeans_rebalance_reseeds_starved_clusters(mivs_lib):
+    """Skewed init (most centroids on one cluster): balancing must leave no starved list; bit-exact."""
+    from mivs.neighbors import ivf_flat
+
+    rng = np.random.default_rng(51)
+    centers = rng.standard_normal((16, 32)).astype(np.float32) * 4
+    lab = np.sort(rng.integers(0, 16, 16000))  # rows sorted by cluster: strided init is skewed
+    x = (centers[lab] + rng.standard_normal((16000, 32))).astype(np.float32)
+    idx = ivf_flat.build(ivf_flat.IndexParams(n_lists=16, kmeans_n_iters=12, kmeans_trainset_fraction=1.0),
+                         _gpu(x))
+    oc, osz, oids = O.ivf_build(x, 16, iters=12, fraction=1.0)
+    np.testing.assert_array_equal(_bits(idx.centers.cpu().numpy()), _bits(oc))
+    np.testing.assert_array_equal(idx.list_sizes.numpy(), osz)
+    assert osz.min() > 0.25 * 1000
+
+
 def test_ivf_flat_inner_product_bitexact(mivs_lib):
     from mivs.neighbors import ivf_flat
 
@@ -199,3 +225,36 @@ def test_distances_within_1e4_of_fp64(mivs_lib):
     ids = ids.cpu().numpy()
     exact = ((x[ids].astype(np.float64) - q[:, None, :].astype(np.float64)) ** 2).sum(-1)
     assert np.abs(dist.cpu().numpy() - exact).max() < 1e-4
+
+
+def test_synth_slices_are_row_pure(mivs_lib):
+    """synth_mixture launches in 2^24-row slices; rows must be a pure function of the global row index."""
+    from mivs import ops
+
+    n = (1 << 24) + 1000
+    whole = ops.synth_mixture(n, 8, seed=5, n_centers=64)
+    tail = ops.synth_mixture(2000, 8, seed=5, n_centers=64, row_begin=(1 << 24) - 1000)
+    assert torch.equal(whole[(1 << 24) - 1000:], tail)
+
+
+def test_list_export_beyond_2p32_elements(mivs_lib):
+    """list_rows()/list_ids() on an index whose n*d exceeds 2^32 (one launch's work-item limit)."""
+    from mivs import ops
+    from mivs.neighbors import ivf_flat
+
+    n, d = 5_700_000, 768  # n*d = 4.38e9
+    x = ops.synth_mixture(n, d, seed=9, n_centers=1024, sigma=0.5)
+    cents = x[torch.arange(0, n, n // 256, device=x.device)[:256]].contiguous()
+    idx = ivf_flat.build_from_centroids(cents, x)
+    ids = idx.list_ids()
+    assert torch.equal(torch.sort(ids).values, torch.arange(n, device=ids.device))
+    rows = idx.list_rows()
+    g = torch.Generator(device="cpu").manual_seed(0)
+    sel = torch.cat([torch.randint(0, n, (20000,), generator=g), torch.arange(n - 4096, n)]).to(x.device)
+    assert torch.equal(rows[sel], x[ids[sel]])
+    del rows
+    # self-queries from the tail of the corpus find themselves at distance 0 with one probe per nearest list
+    q = x[n - 64:].contiguous()
+    dist, nid = ivf_flat.search(ivf_flat.SearchParams(n_probes=4), idx, q, 1)
+    assert torch.equal(nid[:, 0].cpu(), torch.arange(n - 64, n))
+    assert float(dist.abs().max()) < 1e-4
