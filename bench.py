@@ -205,6 +205,18 @@ def main():
     value = qps_full * world  # (query, 10M-row shard) searches per second; = QPS at N=1
     rl(f"[search] {a.steps} steps x {Q} queries: {ms_per_step:.3f} ms/step -> {qps_full:,.0f} QPS (full corpus)")
 
+    # ---- PCIe-inclusive rate (not `value`): queries start in pinned host memory, results return to host ----
+    q_host = q.cpu().pin_memory()
+    io_steps = max(2, a.steps // 4)
+    sync_all(world)
+    t0 = time.perf_counter()
+    for _ in range(io_steps):
+        hd, hi = step(q_host.to(dev, non_blocking=True))
+        hd, hi = hd.cpu(), hi.cpu()
+    t_io = max_over_ranks(time.perf_counter() - t0, world, dev) / io_steps
+    qps_host_io = Q / t_io
+    rl(f"[search] with host queries/results over PCIe: {qps_host_io:,.0f} QPS (full corpus)")
+
     # ---- recall@10 vs exact ground truth (brute force on the same engine, merged over shards) ----
     ng = min(a.gt_queries, Q)
     bf = brute_force.build(x, ids_offset=start)
@@ -283,6 +295,7 @@ def main():
                    "kmeans_trainset_fraction": a.trainset_fraction, "parallelism": f"corpus-shard{world}",
                    "value_definition": "(query, 10M-row shard) searches per second; equals QPS at n_gpus=1"},
         "qps_full_corpus": round(qps_full, 2),
+        "qps_host_io": round(qps_host_io, 2),
         "recall_at_10": round(rec, 4),
         "build_vectors_per_s": round(build_vps, 1),
         "build_s": round(t_build, 3),

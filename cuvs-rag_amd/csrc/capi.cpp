@@ -231,8 +231,9 @@ struct ScanJob {
 };
 
 void run_scan(const ScanJob& j, int device, Workspace& ws, hipStream_t s) {
-  const int kcap = scan_kcap(j.k);
-  require(kcap > 0, "k must be in [1, " + std::to_string(kMaxK) + "]", MIVS_ERR_UNSUPPORTED);
+  const int kcap = scan_kcap(j.k);  // 0 = DUMP mode (k > kMaxK): raw keys per slot for K8
+  require(j.k >= 1 && j.k <= kMaxSelectK, "k must be in [1, " + std::to_string(kMaxSelectK) + "]",
+          MIVS_ERR_UNSUPPORTED);
   require(j.dp <= 1024, "dim > 1024 is not supported by this build", MIVS_ERR_UNSUPPORTED);
   const size_t lds = scan_lds_bytes(j.dp, kcap, j.G);
   const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / lds)));
@@ -267,6 +268,20 @@ void run_scan(const ScanJob& j, int device, Workspace& ws, hipStream_t s) {
   HIPCHK(launch_scan_ex(a, kcap, grid, lds, gmerge, s));
 }
 
+// Bytes of K8 dump workspace one search call may hold (MIVS_SELECT_WORKSPACE_MB, default 4 GiB):
+// large-k searches run in query batches sized to it.
+size_t select_workspace_bytes() {
+  const char* e = getenv("MIVS_SELECT_WORKSPACE_MB");
+  const long long mb = e ? atoll(e) : 4096;
+  return (size_t)std::max<long long>(mb, 1) << 20;
+}
+
+// queries per batch when each query may need `per_query_bytes` of dump workspace
+int64_t select_batch(int64_t nq, size_t per_query_bytes) {
+  const int64_t b = (int64_t)(select_workspace_bytes() / std::max<size_t>(per_query_bytes, 1));
+  return std::max<int64_t>(1, std::min<int64_t>(nq, b));
+}
+
 // single-list job (brute force, coarse probe selection, k-means assign):
 // every query (or every row id of `rows`) against every row of `ls`.
 // Writes [nq][k] results into (out_d, out_i) (merging chunk partials if needed).
@@ -275,6 +290,42 @@ void single_list_topk(const ListSet& ls, int G, const float* queries, const floa
                       Workspace& ws, hipStream_t s) {
   const int64_t chunks = std::max<int64_t>(1, ceil_div(ls.n_groups, G));
   require(ceil_div(nq, kQTile) * chunks < (int64_t)INT32_MAX, "too many work items", MIVS_ERR_UNSUPPORTED);
+  if (k > kMaxK) {  // DUMP scan + K8 select, in query batches
+    const int64_t slot_rows = (int64_t)G * kGroupRows;
+    const int64_t qb = select_batch(nq, (size_t)(chunks * (slot_rows * 4 + 16)));
+    for (int64_t b0 = 0; b0 < nq; b0 += qb) {
+      const int64_t nb = std::min<int64_t>(qb, nq - b0);
+      ws.bucket_q.reserve(sizeof(int64_t) * nb);
+      ws.bucket_slot.reserve(sizeof(int64_t) * nb);
+      ws.bucket_off.reserve(sizeof(int) * 2);
+      ws.work_off.reserve(sizeof(int) * 2);
+      ws.part_d.reserve(sizeof(float) * (size_t)(nb * chunks * slot_rows));
+      ws.part_i.reserve(sizeof(int64_t) * (size_t)(nb * chunks * 2));
+      HIPCHK(launch_single_list_job(nb, chunks, ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(),
+                                    ws.bucket_off.as<int>(), ws.work_off.as<int>(), nullptr, s));
+      const float* qb_ptr = queries;
+      const float* qn_ptr = qnorms;
+      if (rows) HIPCHK(hipMemcpyAsync(ws.bucket_q.p, rows + b0, sizeof(int64_t) * nb, hipMemcpyDeviceToDevice, s));
+      else { qb_ptr = queries + b0 * (int64_t)d; qn_ptr = qnorms + b0; }
+      ScanJob j{&ls, G, qb_ptr, qn_ptr, d, dp, k, metric, ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(),
+                ws.bucket_off.as<int>(), ws.work_off.as<int>(), ws.part_d.as<float>(), ws.part_i.as<int64_t>()};
+      run_scan(j, device, ws, s);
+      SelectArgs sa{};
+      sa.keys = ws.part_d.as<float>();
+      sa.row_ids = ls.ids.as<int64_t>();
+      sa.slot_info = ws.part_i.as<int64_t>();
+      sa.slot_begin = nullptr;
+      sa.slots_per_q = chunks;
+      sa.slot_rows = (int)slot_rows;
+      sa.nq = nb;
+      sa.k = k;
+      sa.metric = metric;
+      sa.out_d = out_d + b0 * k;
+      sa.out_i = out_i + b0 * k;
+      HIPCHK(launch_select(sa, s));
+    }
+    return;
+  }
   ws.bucket_q.reserve(sizeof(int64_t) * nq);
   ws.bucket_slot.reserve(sizeof(int64_t) * nq);
   ws.bucket_off.reserve(sizeof(int) * 2);
@@ -389,8 +440,8 @@ void check_common(int device, const void* data, int64_t n, int32_t dim) {
 }
 
 
-void ivf_search_impl(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
-                     int64_t* out_i, int32_t* out_probes) {
+void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
+                      int64_t* out_i, int32_t* out_probes) {
   Workspace& ws = idx->ws;
   ProfRec* pr = g_profiling.load() ? idx->prof.begin(s) : nullptr;
   ws.qn.reserve(sizeof(float) * nq);
@@ -418,29 +469,62 @@ void ivf_search_impl(mivs_index_s* idx, hipStream_t s, const float* q, int64_t n
                           ws.counts.as<int>(), ws.fill.as<int>(), ws.bucket_off.as<int>(), ws.work_off.as<int>(),
                           ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(), ws.qp_slots.as<int64_t>(),
                           ws.slot_begin.as<int64_t>(), ws.scan_tmp.p, stb, s));
-  // fine scan into per-(query, probe, chunk) slots
+  // fine scan into per-(query, probe, chunk) slots: top-k partials (k <= 64) or raw keys (DUMP)
+  const bool dump = k > kMaxK;
+  const int64_t slot_rows = (int64_t)idx->G * kGroupRows;
   const int64_t max_slots = nq * L.top_chunks_prefix[std::min<int64_t>(np, L.n_lists)];
-  require(max_slots * k < ((int64_t)1 << 40), "search workspace too large", MIVS_ERR_UNSUPPORTED);
-  ws.part_d.reserve(sizeof(float) * (size_t)std::max<int64_t>(max_slots * k, 1));
-  ws.part_i.reserve(sizeof(int64_t) * (size_t)std::max<int64_t>(max_slots * k, 1));
+  const int64_t per_slot_d = dump ? slot_rows : k, per_slot_i = dump ? 2 : k;
+  require(max_slots * per_slot_d < ((int64_t)1 << 40), "search workspace too large", MIVS_ERR_UNSUPPORTED);
+  ws.part_d.reserve(sizeof(float) * (size_t)std::max<int64_t>(max_slots * per_slot_d, 1));
+  ws.part_i.reserve(sizeof(int64_t) * (size_t)std::max<int64_t>(max_slots * per_slot_i, 1));
   ScanJob j{&L, idx->G, q, ws.qn.as<float>(), idx->d, idx->dp, k, idx->metric, ws.bucket_q.as<int64_t>(),
             ws.bucket_slot.as<int64_t>(), ws.bucket_off.as<int>(), ws.work_off.as<int>(), ws.part_d.as<float>(),
             ws.part_i.as<int64_t>()};
   if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
   run_scan(j, idx->device, ws, s);
   if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
-  MergeArgs m{};
-  m.in_d = ws.part_d.as<float>();
-  m.in_i = ws.part_i.as<int64_t>();
-  m.slot_begin = ws.slot_begin.as<int64_t>();
-  m.nq = nq;
-  m.k_in = k;
-  m.k = k;
-  m.metric = idx->metric;
-  m.out_d = out_d;
-  m.out_i = out_i;
-  HIPCHK(launch_merge(m, s));
+  if (dump) {
+    SelectArgs sa{};
+    sa.keys = ws.part_d.as<float>();
+    sa.row_ids = L.ids.as<int64_t>();
+    sa.slot_info = ws.part_i.as<int64_t>();
+    sa.slot_begin = ws.slot_begin.as<int64_t>();
+    sa.slot_rows = (int)slot_rows;
+    sa.nq = nq;
+    sa.k = k;
+    sa.metric = idx->metric;
+    sa.out_d = out_d;
+    sa.out_i = out_i;
+    HIPCHK(launch_select(sa, s));
+  } else {
+    MergeArgs m{};
+    m.in_d = ws.part_d.as<float>();
+    m.in_i = ws.part_i.as<int64_t>();
+    m.slot_begin = ws.slot_begin.as<int64_t>();
+    m.nq = nq;
+    m.k_in = k;
+    m.k = k;
+    m.metric = idx->metric;
+    m.out_d = out_d;
+    m.out_i = out_i;
+    HIPCHK(launch_merge(m, s));
+  }
   if (pr) HIPCHK(hipEventRecord(pr->e[3], s));
+}
+
+void ivf_search_impl(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
+                     int64_t* out_i, int32_t* out_probes) {
+  int64_t qb = nq;
+  if (k > kMaxK) {  // DUMP workspace: bound it by batching queries
+    const ListSet& L = idx->lists;
+    const int64_t per_q_slots = std::max<int64_t>(1, L.top_chunks_prefix[std::min<int64_t>(np, L.n_lists)]);
+    qb = select_batch(nq, (size_t)per_q_slots * ((size_t)idx->G * kGroupRows * 4 + 16));
+  }
+  for (int64_t b0 = 0; b0 < nq; b0 += qb) {
+    const int64_t nb = std::min<int64_t>(qb, nq - b0);
+    ivf_search_batch(idx, s, q + b0 * (int64_t)idx->d, nb, k, np, out_d + b0 * k, out_i + b0 * k,
+                     out_probes ? out_probes + b0 * np : nullptr);
+  }
   idx->last_nq = nq;
   idx->last_np = np;
   idx->last_k = k;
@@ -545,14 +629,15 @@ int32_t mivs_ivf_flat_search(mivs_index_t idx, void* stream, const float* d_q, i
   return guarded([&] {
     require(idx != nullptr && idx->kind == 0, "not an ivf_flat index");
     require(nq >= 0, "nq must be >= 0");
-    require(k >= 1 && k <= kMaxK, "k must be in [1, " + std::to_string(kMaxK) + "]", MIVS_ERR_UNSUPPORTED);
+    require(k >= 1 && k <= kMaxSelectK, "k must be in [1, " + std::to_string(kMaxSelectK) + "]",
+            MIVS_ERR_UNSUPPORTED);
     require(n_probes >= 1, "n_probes must be >= 1");
-    require(n_probes <= kMaxK, "n_probes must be <= " + std::to_string(kMaxK), MIVS_ERR_UNSUPPORTED);
     require(nq == 0 || (d_q && d_dist && d_ids), "NULL query/output pointer");
     if (nq == 0) return;
     std::lock_guard<std::mutex> g(idx->mu);
     DeviceGuard dg(idx->device);
     const int np = std::min<int>(n_probes, idx->lists.n_lists);
+    require(np <= kMaxSelectK, "n_probes must be <= " + std::to_string(kMaxSelectK), MIVS_ERR_UNSUPPORTED);
     require(np == n_probes || d_probes == nullptr, "n_probes > n_lists with a probes output");
     ivf_search_impl(idx, static_cast<hipStream_t>(stream), d_q, nq, k, np, d_dist, d_ids, d_probes);
   });
@@ -619,7 +704,7 @@ int32_t mivs_brute_force_search(mivs_index_t idx, void* stream, const float* d_q
   return guarded([&] {
     require(idx != nullptr && idx->kind == 1, "not a brute-force index");
     require(nq >= 0, "nq must be >= 0");
-    require(k >= 1 && k <= kMaxK, "k must be in [1, " + std::to_string(kMaxK) + "]", MIVS_ERR_UNSUPPORTED);
+    require(k >= 1 && k <= kMaxSelectK, "k must be in [1, " + std::to_string(kMaxSelectK) + "]", MIVS_ERR_UNSUPPORTED);
     require(nq == 0 || (d_q && d_dist && d_ids), "NULL query/output pointer");
     if (nq == 0) return;
     std::lock_guard<std::mutex> g(idx->mu);
@@ -759,11 +844,24 @@ int32_t mivs_merge_topk(int32_t device, void* stream, const float* d_in_dist, co
                         int32_t m, int32_t k_in, int32_t k, int32_t metric, float* d_out_dist,
                         int64_t* d_out_ids) {
   return guarded([&] {
-    require(k >= 1 && k <= kMaxK, "k must be in [1, " + std::to_string(kMaxK) + "]", MIVS_ERR_UNSUPPORTED);
+    require(k >= 1 && k <= kMaxSelectK, "k must be in [1, " + std::to_string(kMaxSelectK) + "]", MIVS_ERR_UNSUPPORTED);
     require(m >= 0 && k_in >= 0 && nq >= 0, "bad shape");
     require(metric == MIVS_METRIC_L2 || metric == MIVS_METRIC_IP, "unknown metric");
     if (nq == 0) return;
     DeviceGuard dg(device);
+    if (k > kMaxK) {  // K8 select over the explicit [nq][m*k_in] candidates
+      SelectArgs sa{};
+      sa.keys = d_in_dist;
+      sa.ids = d_in_ids;
+      sa.n_in = (int64_t)m * k_in;
+      sa.nq = nq;
+      sa.k = k;
+      sa.metric = metric;
+      sa.out_d = d_out_dist;
+      sa.out_i = d_out_ids;
+      HIPCHK(launch_select(sa, static_cast<hipStream_t>(stream)));
+      return;
+    }
     MergeArgs a{};
     a.in_d = d_in_dist;
     a.in_i = d_in_ids;

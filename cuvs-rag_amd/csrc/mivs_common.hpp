@@ -22,6 +22,7 @@ constexpr int kScanThreads = kScanWaves * 64;
 constexpr int kKmChunk = 256;      // members per fp64 partial in the k-means update (== ORC_KM_CHUNK)
 constexpr int kDefaultChunkGroups = 32;  // groups (1024 rows) per scan work item
 constexpr int kMaxK = 64;          // register top-k capacity of scan + merge kernels
+constexpr int kMaxSelectK = 4096;  // largest k / n_probes (K8 select path above kMaxK)
 
 enum Metric : int { kL2 = 0, kIP = 1 };
 
@@ -52,9 +53,28 @@ struct ScanArgs {
   const int* bucket_off;      // [n_lists+1]
   const int* work_off;        // [n_lists+1]; total = work_off[n_lists]
   int* work_counter;          // zeroed before launch
-  float* out_d;               // [slots][k]
-  int64_t* out_i;             // [slots][k]
+  float* out_d;               // [slots][k]; DUMP mode (kcap 0): raw keys [slots][chunk_groups*32]
+  int64_t* out_i;             // [slots][k]; DUMP mode: [slots][2] = (first row position, rows)
   int d, dp, k, metric;
+};
+
+// Large-k select job (K8): per query, the k smallest (key, id) among its candidates.
+//   DUMP source (slot_info != nullptr): slots [slot_begin[q], slot_begin[q+1]) (or
+//     q*slots_per_q.. when slot_begin == nullptr) of keys[slot][slot_rows], ids from row_ids;
+//   EXPLICIT source (slot_info == nullptr): keys = distances [nq][n_in], ids [nq][n_in].
+struct SelectArgs {
+  const float* keys;
+  const int64_t* ids;
+  const int64_t* row_ids;
+  const int64_t* slot_info;
+  const int64_t* slot_begin;
+  int64_t slots_per_q;
+  int64_t n_in;
+  int slot_rows;
+  int64_t nq;
+  int k, metric;
+  float* out_d;
+  int64_t* out_i;
 };
 
 // Merge job: per query q, candidates = slots [slot_begin[q], slot_begin[q+1])
@@ -81,6 +101,7 @@ int scan_kcap(int k);
 hipError_t launch_train_rows(int64_t* rows, int64_t n, int64_t n_train, hipStream_t s);
 hipError_t launch_i64_to_i32(const int64_t* in, int64_t n, int32_t* out, hipStream_t s);
 hipError_t launch_merge(const MergeArgs& a, hipStream_t s);
+hipError_t launch_select(const SelectArgs& a, hipStream_t s);
 
 hipError_t launch_pack_groups(const float* src, int64_t src_rows_total, int d, int dp, const int64_t* src_index,
                               const int64_t* list_off, const int64_t* list_goff, const int* group_list,

@@ -94,11 +94,37 @@ __device__ __forceinline__ void epilogue(const f32x16& acc, const float* __restr
   }
 }
 
+// DUMP mode (KCAP == 0, k > 64): the group's keys go straight to the query's slot; rows
+// 8*r4 + 4h + {0..3} of this lane are contiguous, so each lane issues 4 dwordx4 stores.
+template <int METRIC>
+__device__ __forceinline__ void epilogue_dump(const f32x16& acc, const float* __restrict__ gnorm, int h, float qn,
+                                              float* __restrict__ dst /*slot keys + group row base*/) {
+  if (dst == nullptr) return;
+#pragma unroll
+  for (int r4 = 0; r4 < 4; ++r4) {
+    const float4 xn = *reinterpret_cast<const float4*>(gnorm + 8 * r4 + 4 * h);
+    float kv[4];
+    const float xs[4] = {xn.x, xn.y, xn.z, xn.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (METRIC == kL2) {
+        const float v = fmaf(-2.0f, acc[4 * r4 + i], xs[i] + qn);
+        kv[i] = v > 0.0f ? v : 0.0f;
+      } else {
+        kv[i] = xs[i] < INFINITY ? -acc[4 * r4 + i] : INFINITY;
+      }
+    }
+    *reinterpret_cast<float4*>(dst + 8 * r4 + 4 * h) = make_float4(kv[0], kv[1], kv[2], kv[3]);
+  }
+}
+
 template <int KCAP, int METRIC>
 __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a, float* __restrict__ gmerge) {
   // k-steps per register buffer: 8 (2 KiB of list rows in flight per lane-pair ring slot) unless the
   // register top-K is large
   constexpr int BLK = KCAP >= 32 ? 4 : 8;
+  constexpr bool DUMP = KCAP == 0;
+  constexpr int KR = DUMP ? 1 : KCAP;  // register list length
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int64_t* s_q = reinterpret_cast<int64_t*>(smem);          // [32] query row ids (-1: empty lane)
   int64_t* s_slot = s_q + 32;                                // [32] output slot (already + chunk)
@@ -110,8 +136,8 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a, float* __r
   const int qstride = dp + 4;  // +16 B per row: conflict-free ds_read_b128 of the B operand
 
   // merge area: LDS after the scan when it fits, else this block's global scratch
-  float* mkey = gmerge ? gmerge + (size_t)blockIdx.x * (kQTile * 16 * KCAP * 2) : qtile;
-  int* mpos = reinterpret_cast<int*>(mkey + kQTile * 16 * KCAP);
+  float* mkey = gmerge ? gmerge + (size_t)blockIdx.x * (kQTile * 16 * KR * 2) : qtile;
+  int* mpos = reinterpret_cast<int*>(mkey + kQTile * 16 * KR);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -160,6 +186,11 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a, float* __r
     {  // row norms of the chunk -> LDS
       const int nn = (int)(g_end - g_begin) * kGroupRows;
       for (int i = tid; i < nn; i += kScanThreads) s_norm[i] = a.row_norms[g_begin * kGroupRows + i];
+      if (DUMP && tid < nqt) {  // slot header: first row position + rows of this chunk
+        const int64_t slot = a.bucket_slot[e0 + tid] + chunk;
+        a.out_i[2 * slot] = g_begin * kGroupRows;
+        a.out_i[2 * slot + 1] = nn;
+      }
     }
     __syncthreads();
 
@@ -177,12 +208,14 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a, float* __r
     }
     __syncthreads();
 
-    float lk[KCAP];
-    int lp[KCAP];
+    float lk[KR];
+    int lp[KR];
 #pragma unroll
-    for (int t = 0; t < KCAP; ++t) { lk[t] = INFINITY; lp[t] = INT_MAX; }
+    for (int t = 0; t < KR; ++t) { lk[t] = INFINITY; lp[t] = INT_MAX; }
     const float qn = s_qn[j];
     const bool qvalid = s_q[j] >= 0;
+    const int slot_rows = a.chunk_groups * kGroupRows;
+    float* const dump_base = DUMP && qvalid ? a.out_d + s_slot[j] * (int64_t)slot_rows : nullptr;
     const float* qrow = qtile + j * qstride + 4 * h;
 
     // ---- this wave's row groups g_begin+wave, +8, ... as ONE stream of BLK-step blocks, two
@@ -213,8 +246,12 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a, float* __r
         mma_block<BLK>(acc, A, qrow + sb * (BLK * 8));
         load_block<BLK>(A, bptr(b + 2));
         if (++sb == bpg) {
-          epilogue<KCAP, METRIC>(acc, s_norm + (wave + gi * kScanWaves) * kGroupRows,
-                                 (g0 + (int64_t)gi * kScanWaves) * kGroupRows, h, qn, qvalid, lk, lp);
+          if constexpr (DUMP)
+            epilogue_dump<METRIC>(acc, s_norm + (wave + gi * kScanWaves) * kGroupRows, h, qn,
+                                  dump_base ? dump_base + (wave + gi * kScanWaves) * kGroupRows : nullptr);
+          else
+            epilogue<KCAP, METRIC>(acc, s_norm + (wave + gi * kScanWaves) * kGroupRows,
+                                   (g0 + (int64_t)gi * kScanWaves) * kGroupRows, h, qn, qvalid, lk, lp);
           acc = zero;
           sb = 0;
           ++gi;
@@ -222,8 +259,12 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a, float* __r
         mma_block<BLK>(acc, B, qrow + sb * (BLK * 8));
         load_block<BLK>(B, bptr(b + 3));
         if (++sb == bpg && b + 1 < nb) {
-          epilogue<KCAP, METRIC>(acc, s_norm + (wave + gi * kScanWaves) * kGroupRows,
-                                 (g0 + (int64_t)gi * kScanWaves) * kGroupRows, h, qn, qvalid, lk, lp);
+          if constexpr (DUMP)
+            epilogue_dump<METRIC>(acc, s_norm + (wave + gi * kScanWaves) * kGroupRows, h, qn,
+                                  dump_base ? dump_base + (wave + gi * kScanWaves) * kGroupRows : nullptr);
+          else
+            epilogue<KCAP, METRIC>(acc, s_norm + (wave + gi * kScanWaves) * kGroupRows,
+                                   (g0 + (int64_t)gi * kScanWaves) * kGroupRows, h, qn, qvalid, lk, lp);
           acc = zero;
           sb = 0;
           ++gi;
@@ -231,6 +272,10 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a, float* __r
       }
     }
 
+    if constexpr (DUMP) {
+      __syncthreads();  // LDS (s_*, qtile) reused by the next work item
+      continue;
+    }
     // ---- merge the 16 lane lists (8 waves x 2 halves) of every query ----
     __syncthreads();  // every wave is done with qtile (the merge area may alias it)
     {
@@ -293,6 +338,7 @@ hipError_t launch_k(const ScanArgs& a, int grid, size_t lds, float* gmerge, hipS
 }  // namespace
 
 int scan_kcap(int k) {
+  if (k > kMaxK) return 0;  // DUMP mode + K8 select
   if (k <= 1) return 1;
   if (k <= 4) return 4;
   if (k <= 8) return 8;
@@ -325,6 +371,7 @@ size_t scan_gmerge_bytes(int grid, int kcap) { return (size_t)grid * merge_bytes
 
 hipError_t launch_scan_ex(const ScanArgs& a, int kcap, int grid, size_t lds, float* gmerge, hipStream_t s) {
   switch (kcap) {
+    case 0: return launch_k<0>(a, grid, lds, gmerge, s);
     case 1: return launch_k<1>(a, grid, lds, gmerge, s);
     case 4: return launch_k<4>(a, grid, lds, gmerge, s);
     case 8: return launch_k<8>(a, grid, lds, gmerge, s);

@@ -1,0 +1,307 @@
+// K8 — large-k selection (k in (64, 4096]; also n_probes > 64) (DESIGN.md §"Kernels").
+//
+// The register top-k of the scan (K3) and of the wave merge (K7) stops at 64.
+// For larger k the scan runs in DUMP mode: every (query, chunk) slot receives
+// the raw ranking keys of the chunk's rows. This kernel then selects, per query
+// (one 1024-thread workgroup), the k smallest candidates under the total order
+// (key, id) — exactly the order the oracle and the k <= 64 path use:
+//
+//   pass 0      min / max of the orderable key bits + number of valid candidates
+//   pass 1..    2048-bin histogram of the current key range, LINEAR in the
+//               orderable bits (not radix digits: keys of one query crowd into a
+//               few exponents, linear bins spread them and keep LDS atomics
+//               uncontended); pick the bin holding the k-th candidate; stop as
+//               soon as everything below it plus the bin fits in CAP slots,
+//               else narrow the range to that bin (<= 3 passes for 32 bits)
+//   ties        a range of ONE key value that still overflows CAP (duplicate
+//               rows) is refined the same way over the ids of the tied rows
+//   collect     candidates <= the final bound -> LDS (<= CAP), bitonic sort by
+//               (key, id), write the first k; missing ranks get (id -1, +inf)
+//               (IP: -inf) like every other path.
+//
+// Candidate sources: DUMP slots (keys [slot][slot_rows], slot_info = (first row
+// position, rows) per slot, ids = row_ids[position]) or an EXPLICIT [nq][n_in]
+// (dist, id) array (cross-shard merge of large k; id < 0 = missing).
+// Replaces the large-k select_k inside cuVS ivf_flat::search / brute_force (reference
+// top_k = 2000, improved_multi_gpu_rag.py:65,247; 2*k per shard cuvs-2gpu-main.ipynb:1801).
+#include <climits>
+
+#include "mivs_common.hpp"
+
+namespace mivs {
+
+namespace {
+
+constexpr int kSelThreads = 1024;
+constexpr int kBins = 2048;
+
+__device__ __forceinline__ uint32_t ord_bits(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float from_ord(uint32_t o) {
+  return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
+}
+constexpr uint32_t kOrdInf = 0xFF800000u;  // ord_bits(+inf); every valid key is strictly below
+
+struct Cand {
+  uint32_t u;  // orderable key bits
+  bool valid;
+};
+
+// Candidate c of query q (flattened index over the query's candidate range).
+template <bool EXPLICIT, int METRIC>
+__device__ __forceinline__ Cand cand_key(const SelectArgs& a, int64_t base, int64_t t) {
+  Cand r;
+  if (EXPLICIT) {
+    const int64_t c = base + t;
+    const int64_t id = a.ids[c];
+    const float dd = a.keys[c];
+    const float key = METRIC == kIP ? -dd : dd;
+    r.u = ord_bits(key);
+    r.valid = id >= 0 && r.u < kOrdInf;
+  } else {
+    const int64_t s = base + t / a.slot_rows;
+    const int rr = (int)(t - (t / a.slot_rows) * a.slot_rows);
+    r.valid = false;
+    r.u = 0xFFFFFFFFu;
+    if (rr < (int)a.slot_info[2 * s + 1]) {
+      r.u = ord_bits(a.keys[s * a.slot_rows + rr]);
+      r.valid = r.u < kOrdInf;  // pad rows carry +inf
+    }
+  }
+  return r;
+}
+
+template <bool EXPLICIT>
+__device__ __forceinline__ int64_t cand_id(const SelectArgs& a, int64_t base, int64_t t) {
+  if (EXPLICIT) return a.ids[base + t];
+  const int64_t s = base + t / a.slot_rows;
+  const int rr = (int)(t - (t / a.slot_rows) * a.slot_rows);
+  return a.row_ids[a.slot_info[2 * s] + rr];
+}
+
+// Linear bins of width bw = ceil(w / 2048) over a range [lo, lo + w): bin = (v - lo) / bw.
+// Key ranges are < 2^32 wide, so the hot key passes use 32-bit division.
+__device__ __forceinline__ uint64_t bin_width(uint64_t w) { return (w + kBins - 1) / kBins; }
+__device__ __forceinline__ int bin_of_key(uint32_t u, uint32_t lo, uint32_t bw) { return (int)((u - lo) / bw); }
+__device__ __forceinline__ int bin_of_id(uint64_t v, uint64_t lo, uint64_t bw) { return (int)((v - lo) / bw); }
+
+template <typename T>
+__device__ __forceinline__ T block_reduce(T v, T* sbuf, int op /*0 sum, 1 min, 2 max*/) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const T x = __shfl_xor(v, o);
+    v = op == 0 ? v + x : (op == 1 ? (x < v ? x : v) : (x > v ? x : v));
+  }
+  __syncthreads();
+  if (lane == 0) sbuf[wave] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    T r = sbuf[0];
+    for (int i = 1; i < kSelThreads / 64; ++i) {
+      const T x = sbuf[i];
+      r = op == 0 ? r + x : (op == 1 ? (x < r ? x : r) : (x > r ? x : r));
+    }
+    sbuf[0] = r;
+  }
+  __syncthreads();
+  const T r = sbuf[0];
+  __syncthreads();
+  return r;
+}
+
+// Among bins, find b with below(b) < need <= below(b) + hist[b]; thread 0 writes (b, below).
+__device__ __forceinline__ void find_bin(const int* hist, int need, int* s_res) {
+  // each thread owns 2 consecutive bins; block-wide exclusive scan over 1024 pair sums
+  __shared__ int wsum[kSelThreads / 64];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int h0 = hist[2 * t], h1 = hist[2 * t + 1];
+  int inc = h0 + h1;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int x = __shfl_up(inc, o);
+    if (lane >= o) inc += x;
+  }
+  if (lane == 63) wsum[wave] = inc;
+  __syncthreads();
+  int woff = 0;
+  for (int i = 0; i < wave; ++i) woff += wsum[i];
+  const int excl = woff + inc - (h0 + h1);
+  if (excl < need && need <= excl + h0) { s_res[0] = 2 * t; s_res[1] = excl; }
+  else if (excl + h0 < need && need <= excl + h0 + h1) { s_res[0] = 2 * t + 1; s_res[1] = excl + h0; }
+  __syncthreads();
+}
+
+template <int CAP, bool EXPLICIT, int METRIC>
+__global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
+  __shared__ int hist[kBins];
+  __shared__ uint32_t sk[CAP];
+  __shared__ int64_t si[CAP];
+  __shared__ int s_res[4];
+  __shared__ uint64_t s_red[kSelThreads / 64];
+
+  const int64_t q = blockIdx.x;
+  const int tid = threadIdx.x;
+  int64_t base, ncand;
+  if (EXPLICIT) {
+    base = q * a.n_in;
+    ncand = a.n_in;
+  } else {
+    const int64_t sb = a.slot_begin ? a.slot_begin[q] : q * a.slots_per_q;
+    const int64_t se = a.slot_begin ? a.slot_begin[q + 1] : sb + a.slots_per_q;
+    base = sb;
+    ncand = (se - sb) * a.slot_rows;
+  }
+  const int k = a.k;
+
+  // ---- pass 0: valid count + key range ----
+  uint64_t cnt = 0, mn = 0xFFFFFFFFull, mx = 0;
+  for (int64_t t = tid; t < ncand; t += kSelThreads) {
+    const Cand c = cand_key<EXPLICIT, METRIC>(a, base, t);
+    if (c.valid) {
+      ++cnt;
+      mn = c.u < mn ? c.u : mn;
+      mx = c.u > mx ? c.u : mx;
+    }
+  }
+  const int64_t n_valid = (int64_t)block_reduce<uint64_t>(cnt, s_red, 0);
+  uint64_t klo = block_reduce<uint64_t>(mn, s_red, 1);
+  uint64_t khi = block_reduce<uint64_t>(mx, s_red, 2);
+
+  // selection bound: key u < klo always selected; u in [klo, khi] selected (key phase) or,
+  // in the id phase (klo == khi), with id in [ilo, ihi]
+  int64_t below = 0;  // candidates strictly below the current range
+  bool id_phase = false;
+  uint64_t ilo = 0, ihi = 0;
+  bool select_all = n_valid <= CAP;
+  const int need = (int)(n_valid < k ? n_valid : k);
+
+  while (!select_all) {
+    // range exhausted on the key: refine by id among the tied candidates
+    if (!id_phase && klo == khi) {
+      uint64_t imn = ~0ull, imx = 0;
+      for (int64_t t = tid; t < ncand; t += kSelThreads) {
+        const Cand c = cand_key<EXPLICIT, METRIC>(a, base, t);
+        if (c.valid && c.u == klo) {
+          const uint64_t id = (uint64_t)cand_id<EXPLICIT>(a, base, t);
+          imn = id < imn ? id : imn;
+          imx = id > imx ? id : imx;
+        }
+      }
+      ilo = block_reduce<uint64_t>(imn, s_red, 1);
+      ihi = block_reduce<uint64_t>(imx, s_red, 2);
+      id_phase = true;
+      if (ilo == ihi) break;  // identical (key, id) duplicates: nothing left to order
+    }
+    const uint64_t lo = id_phase ? ilo : klo;
+    const uint64_t w = (id_phase ? ihi : khi) - lo + 1;
+    const uint64_t bw = bin_width(w);
+    for (int i = tid; i < kBins; i += kSelThreads) hist[i] = 0;
+    __syncthreads();
+    for (int64_t t = tid; t < ncand; t += kSelThreads) {
+      const Cand c = cand_key<EXPLICIT, METRIC>(a, base, t);
+      if (!c.valid) continue;
+      if (!id_phase) {
+        if (c.u >= klo && c.u <= khi) atomicAdd(&hist[bin_of_key(c.u, (uint32_t)klo, (uint32_t)bw)], 1);
+      } else if (c.u == klo) {
+        const uint64_t id = (uint64_t)cand_id<EXPLICIT>(a, base, t);
+        if (id >= ilo && id <= ihi) atomicAdd(&hist[bin_of_id(id, ilo, bw)], 1);
+      }
+    }
+    __syncthreads();
+    find_bin(hist, need - (int)below, s_res);
+    const int b = s_res[0];
+    below += s_res[1];
+    const int hb = hist[b];
+    const uint64_t nlo = lo + (uint64_t)b * bw;
+    const uint64_t last = lo + w - 1;
+    const uint64_t nhi = nlo + bw - 1 < last ? nlo + bw - 1 : last;
+    __syncthreads();
+    if (id_phase) { ilo = nlo; ihi = nhi; }
+    else { klo = nlo; khi = nhi; }
+    if (below + hb <= CAP) break;
+    if (id_phase && ilo == ihi) break;
+  }
+
+  // ---- collect: everything at or below the bound ----
+  if (tid == 0) s_res[2] = 0;
+  __syncthreads();
+  for (int64_t t = tid; t < ncand; t += kSelThreads) {
+    const Cand c = cand_key<EXPLICIT, METRIC>(a, base, t);
+    if (!c.valid) continue;
+    bool take;
+    if (select_all) take = true;
+    else if (!id_phase) take = c.u <= khi;
+    else take = c.u < klo || (c.u == klo && (uint64_t)cand_id<EXPLICIT>(a, base, t) <= ihi);
+    if (take) {
+      const int pos = atomicAdd(&s_res[2], 1);
+      if (pos < CAP) {
+        sk[pos] = c.u;
+        si[pos] = cand_id<EXPLICIT>(a, base, t);
+      }
+    }
+  }
+  __syncthreads();
+  const int n_sel = s_res[2] < CAP ? s_res[2] : CAP;
+  int p2 = 1;
+  while (p2 < n_sel) p2 <<= 1;
+  for (int i = n_sel + tid; i < p2; i += kSelThreads) {
+    sk[i] = 0xFFFFFFFFu;
+    si[i] = LLONG_MAX;
+  }
+  __syncthreads();
+  // ---- bitonic sort of p2 (key, id) pairs ----
+  for (int size = 2; size <= p2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < (p2 >> 1); i += kSelThreads) {
+        const int lo_i = 2 * i - (i & (stride - 1));
+        const int hi_i = lo_i + stride;
+        const bool up = (lo_i & size) == 0;
+        const uint32_t ka = sk[lo_i], kb = sk[hi_i];
+        const int64_t ia = si[lo_i], ib = si[hi_i];
+        const bool gt = ka > kb || (ka == kb && ia > ib);
+        if (gt == up) {
+          sk[lo_i] = kb; sk[hi_i] = ka;
+          si[lo_i] = ib; si[hi_i] = ia;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int t = tid; t < k; t += kSelThreads) {
+    const bool valid = t < n_sel && t < need;
+    const float key = valid ? from_ord(sk[t]) : INFINITY;
+    a.out_d[q * k + t] = valid ? (METRIC == kIP ? -key : key) : (METRIC == kIP ? -INFINITY : INFINITY);
+    a.out_i[q * k + t] = valid ? si[t] : (int64_t)-1;
+  }
+}
+
+template <int CAP>
+hipError_t launch_cap(const SelectArgs& a, bool expl, hipStream_t s) {
+  const dim3 grid((unsigned)a.nq), block(kSelThreads);
+  if (expl) {
+    if (a.metric == kIP) hipLaunchKernelGGL((k_select<CAP, true, kIP>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_select<CAP, true, kL2>), grid, block, 0, s, a);
+  } else {  // dump keys are already ranking keys; METRIC only sets the sign of the output distance
+    if (a.metric == kIP) hipLaunchKernelGGL((k_select<CAP, false, kIP>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_select<CAP, false, kL2>), grid, block, 0, s, a);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_select(const SelectArgs& a, hipStream_t s) {
+  if (a.k < 1 || a.k > kMaxSelectK) return hipErrorInvalidValue;
+  if (a.nq <= 0) return hipSuccess;
+  if (a.nq > 0x7FFFFFFF) return hipErrorInvalidValue;
+  const bool expl = a.slot_info == nullptr;
+  if (a.k <= 512) return launch_cap<1024>(a, expl, s);
+  if (a.k <= 1024) return launch_cap<2048>(a, expl, s);
+  if (a.k <= 2048) return launch_cap<4096>(a, expl, s);
+  return launch_cap<8192>(a, expl, s);
+}
+
+}  // namespace mivs

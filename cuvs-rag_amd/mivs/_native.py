@@ -23,7 +23,7 @@ MIVS_ERR_UNSUPPORTED = 4
 
 METRIC_L2 = 0
 METRIC_IP = 1
-MAX_K = 64
+MAX_K = 4096  # include/mivs.h MIVS_MAX_K
 
 
 class MivsError(RuntimeError):

@@ -31,6 +31,7 @@ import numpy as np
 import torch
 
 from gpu_resource_manager import GPUResourceManager
+from mivs._native import MAX_K as _MAX_K
 from mivs.backend import engine_available
 
 logger = logging.getLogger(__name__)
@@ -176,7 +177,7 @@ class SearchResultAggregator:
                 raise ValueError(f"GPU {r.gpu_id} has {r.num_queries} queries, expected {nq}")
         width = sum(np.shape(r.distances)[1] for r in gpu_results)
         kk = min(k, width)
-        if CUVS_AVAILABLE and kk <= 64:
+        if CUVS_AVAILABLE and kk <= _MAX_K:
             dev = torch.device(f"cuda:{torch.cuda.current_device()}")
             d, i = _device_merge([torch.as_tensor(np.asarray(r.distances, np.float32)) for r in gpu_results],
                                  [torch.as_tensor(np.asarray(r.indices, np.int64)) for r in gpu_results], kk,
@@ -261,7 +262,7 @@ class SearchResultAggregator:
         if config.validate_results:
             self.validate_search_results(gpu_results, nq, config.k)
         kk = min(config.k, sum(int(raw[g][0].shape[1]) for g in order))
-        if CUVS_AVAILABLE and kk <= 64:
+        if CUVS_AVAILABLE and kk <= _MAX_K:
             metric = getattr(indices[order[0]], "metric", "sqeuclidean")
             dev = torch.device(f"cuda:{order[0]}")
             with torch.cuda.device(order[0]):

@@ -35,7 +35,8 @@ extern "C" {
 #define MIVS_METRIC_L2 0 /* cuVS "sqeuclidean" / FAISS METRIC_L2 */
 #define MIVS_METRIC_IP 1 /* cuVS "inner_product" / FAISS METRIC_INNER_PRODUCT */
 
-#define MIVS_MAX_K 64 /* largest k / n_probes served by the register top-k path */
+#define MIVS_MAX_K 4096         /* largest k / n_probes (k > 64 runs the DUMP scan + K8 select path) */
+#define MIVS_MAX_REGISTER_K 64 /* largest k served by the register top-k scan + K7 wave merge */
 
 typedef struct mivs_index_s* mivs_index_t;
 

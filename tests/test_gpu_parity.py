@@ -258,3 +258,95 @@ def test_list_export_beyond_2p32_elements(mivs_lib):
     dist, nid = ivf_flat.search(ivf_flat.SearchParams(n_probes=4), idx, q, 1)
     assert torch.equal(nid[:, 0].cpu(), torch.arange(n - 64, n))
     assert float(dist.abs().max()) < 1e-4
+
+
+# ---- large k (K8 select: DUMP scan + per-query range-refining select), reference top_k = 2000 ----
+BF_LARGE_K = [
+    # n, d, nq, k, metric
+    (3000, 64, 20, 2000, "sqeuclidean"),     # n <= CAP: select-all path
+    (1500, 64, 9, 2000, "sqeuclidean"),      # n < k: padded with (-1, +inf)
+    (20000, 96, 37, 100, "sqeuclidean"),     # refinement passes (CAP 1024)
+    (30000, 128, 16, 2000, "sqeuclidean"),
+    (50000, 32, 8, 4096, "sqeuclidean"),     # CAP 8192
+    (12000, 64, 25, 777, "inner_product"),
+]
+
+
+@pytest.mark.parametrize("n,d,nq,k,metric", BF_LARGE_K)
+def test_brute_force_large_k_bitexact(mivs_lib, n, d, nq, k, metric):
+    from mivs.neighbors import brute_force
+
+    x = _data(n, d, seed=n + k)
+    q = _data(nq, d, seed=n + k + 1)
+    dist, ids = brute_force.search(brute_force.build(_gpu(x), metric=metric), _gpu(q), k)
+    od, oi = O.knn(x, q, k, metric=metric)
+    np.testing.assert_array_equal(ids.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(dist.cpu().numpy()), _bits(od))
+
+
+def test_large_k_duplicate_rows_tie_break_by_id(mivs_lib):
+    """Duplicated corpus rows give equal keys: order by id, also when ties overflow the LDS capacity."""
+    from mivs.neighbors import brute_force
+
+    base = _data(3000, 48, seed=77)
+    x = np.concatenate([base] * 4)                      # every row 4 times
+    same = np.repeat(_data(1, 48, seed=78), 9000, 0)    # 9000 identical rows (id-phase refinement)
+    x = np.concatenate([x, same])
+    q = np.concatenate([base[:5], same[:2], _data(4, 48, seed=79)])
+    for k in (300, 1500, 4096):
+        dist, ids = brute_force.search(brute_force.build(_gpu(x)), _gpu(q), k)
+        od, oi = O.knn(x, q, k)
+        np.testing.assert_array_equal(ids.cpu().numpy(), oi)
+        np.testing.assert_array_equal(_bits(dist.cpu().numpy()), _bits(od))
+
+
+@pytest.mark.parametrize("n_probes,k,metric", [(8, 100, "sqeuclidean"), (128, 2000, "sqeuclidean"),
+                                                (100, 10, "sqeuclidean"), (40, 500, "inner_product")])
+def test_ivf_flat_large_k_and_probes_bitexact(mivs_lib, n_probes, k, metric):
+    from mivs.neighbors import ivf_flat
+
+    x = _data(40000, 64, seed=91, normalize=True)
+    q = _data(70, 64, seed=92, normalize=True)
+    idx = ivf_flat.build(ivf_flat.IndexParams(n_lists=256, kmeans_n_iters=3, metric=metric), _gpu(x))
+    oc, osz, oids = O.ivf_build(x, 256, iters=3, metric=metric)
+    np.testing.assert_array_equal(_bits(idx.centers.cpu().numpy()), _bits(oc))
+    probes = torch.empty((q.shape[0], n_probes), dtype=torch.int32, device="cuda")
+    dist, ids = ivf_flat.search(ivf_flat.SearchParams(n_probes=n_probes), idx, _gpu(q), k, probes_out=probes)
+    od, oi, op = O.ivf_search(x, oc, osz, oids, q, n_probes, k, metric=metric)
+    np.testing.assert_array_equal(probes.cpu().numpy(), op)
+    np.testing.assert_array_equal(ids.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(dist.cpu().numpy()), _bits(od))
+
+
+def test_large_k_query_batching(mivs_lib, monkeypatch):
+    """A tiny select workspace forces many query batches; results must not change."""
+    from mivs.neighbors import brute_force, ivf_flat
+
+    x = _data(20000, 64, seed=95, normalize=True)
+    q = _data(300, 64, seed=96, normalize=True)
+    idx = ivf_flat.build(ivf_flat.IndexParams(n_lists=64, kmeans_n_iters=2), _gpu(x))
+    bf = brute_force.build(_gpu(x))
+    ref = [ivf_flat.search(ivf_flat.SearchParams(n_probes=16), idx, _gpu(q), 200),
+           brute_force.search(bf, _gpu(q), 200)]
+    monkeypatch.setenv("MIVS_SELECT_WORKSPACE_MB", "1")
+    got = [ivf_flat.search(ivf_flat.SearchParams(n_probes=16), idx, _gpu(q), 200),
+           brute_force.search(bf, _gpu(q), 200)]
+    for (rd, ri), (gd, gi) in zip(ref, got):
+        assert torch.equal(ri, gi) and torch.equal(rd, gd)
+
+
+@pytest.mark.parametrize("m,kin,k,metric", [(4, 600, 1000, "sqeuclidean"), (8, 2000, 2000, "sqeuclidean"),
+                                            (3, 300, 4096, "inner_product")])
+def test_merge_topk_large_k_matches_oracle(mivs_lib, m, kin, k, metric):
+    from mivs import ops
+
+    rng = np.random.default_rng(m * 1000 + k)
+    nq = 13
+    d = (np.round(rng.random((nq, m, kin)) * 200) / 200).astype(np.float32)  # many ties, broken by id
+    d = -np.sort(-d, axis=2) if metric == "inner_product" else np.sort(d, axis=2)
+    ids = rng.permutation(nq * m * kin).reshape(nq, m, kin).astype(np.int64)
+    ids[:, :, -3:] = -1
+    od, oi = O.merge(d, ids, k, metric=metric)
+    gd, gi = ops.merge_topk(_gpu(d), _gpu(ids), k, metric=metric)
+    np.testing.assert_array_equal(gi.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(gd.cpu().numpy()), _bits(od))
