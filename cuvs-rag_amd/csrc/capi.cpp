@@ -198,7 +198,7 @@ struct mivs_index_s {
   Profiler prof;
   // what the last search did (for algorithmic roofline counts)
   int64_t last_nq = 0;
-  int last_np = 0, last_k = 0;
+  int last_np = 0, last_k = 0, last_qtile = kQTile;
 };
 
 namespace {
@@ -228,21 +228,23 @@ struct ScanJob {
   const int* work_off;
   float* out_d;
   int64_t* out_i;
+  int qtile;  // 32: K3, 64: K3w (must match the work decomposition of the probe map / single job)
 };
+
+// Query tile of the fine scan for k: K3w (64 queries, slab-staged) where it applies and
+// MIVS_SCAN_WIDE=1, else K3.
+int pick_qtile(int k, int d, int G) {
+  const char* e = getenv("MIVS_SCAN_WIDE");
+  if (!e || e[0] != '1') return kQTile;
+  const int kcap = scan_kcap(k);
+  return kcap > 0 && scan_wide_supported(kcap, d, dim_pad(d), G) ? 64 : kQTile;
+}
 
 void run_scan(const ScanJob& j, int device, Workspace& ws, hipStream_t s) {
   const int kcap = scan_kcap(j.k);  // 0 = DUMP mode (k > kMaxK): raw keys per slot for K8
   require(j.k >= 1 && j.k <= kMaxSelectK, "k must be in [1, " + std::to_string(kMaxSelectK) + "]",
           MIVS_ERR_UNSUPPORTED);
   require(j.dp <= 1024, "dim > 1024 is not supported by this build", MIVS_ERR_UNSUPPORTED);
-  const size_t lds = scan_lds_bytes(j.dp, kcap, j.G);
-  const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / lds)));
-  const int grid = cu_count(device) * per_cu;
-  float* gmerge = nullptr;
-  if (!scan_merge_in_lds(j.dp, kcap, j.G)) {
-    ws.gmerge.reserve(scan_gmerge_bytes(grid, kcap));
-    gmerge = ws.gmerge.as<float>();
-  }
   ws.counter.reserve(16);
   HIPCHK(hipMemsetAsync(ws.counter.p, 0, sizeof(int), s));
   ScanArgs a{};
@@ -265,6 +267,21 @@ void run_scan(const ScanJob& j, int device, Workspace& ws, hipStream_t s) {
   a.dp = j.dp;
   a.k = j.k;
   a.metric = j.metric;
+  a.qtile = j.qtile;
+  if (j.qtile == 64) {
+    require(kcap > 0 && scan_wide_supported(kcap, j.d, j.dp, j.G), "internal: wide scan not applicable");
+    const size_t lds = scan_wide_lds_bytes(kcap, j.G);
+    const int grid = cu_count(device) * std::min(2, scan_wide_occupancy(kcap, j.metric, lds));
+    HIPCHK(launch_scan_wide(a, kcap, grid, lds, s));
+    return;
+  }
+  const size_t lds = scan_lds_bytes(j.dp, kcap, j.G);
+  const int grid = cu_count(device) * std::max(1, std::min(2, scan_occupancy(kcap, j.metric, lds)));
+  float* gmerge = nullptr;
+  if (!scan_merge_in_lds(j.dp, kcap, j.G)) {
+    ws.gmerge.reserve(scan_gmerge_bytes(grid, kcap));
+    gmerge = ws.gmerge.as<float>();
+  }
   HIPCHK(launch_scan_ex(a, kcap, grid, lds, gmerge, s));
 }
 
@@ -301,14 +318,15 @@ void single_list_topk(const ListSet& ls, int G, const float* queries, const floa
       ws.work_off.reserve(sizeof(int) * 2);
       ws.part_d.reserve(sizeof(float) * (size_t)(nb * chunks * slot_rows));
       ws.part_i.reserve(sizeof(int64_t) * (size_t)(nb * chunks * 2));
-      HIPCHK(launch_single_list_job(nb, chunks, ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(),
+      HIPCHK(launch_single_list_job(nb, chunks, kQTile, ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(),
                                     ws.bucket_off.as<int>(), ws.work_off.as<int>(), nullptr, s));
       const float* qb_ptr = queries;
       const float* qn_ptr = qnorms;
       if (rows) HIPCHK(hipMemcpyAsync(ws.bucket_q.p, rows + b0, sizeof(int64_t) * nb, hipMemcpyDeviceToDevice, s));
       else { qb_ptr = queries + b0 * (int64_t)d; qn_ptr = qnorms + b0; }
       ScanJob j{&ls, G, qb_ptr, qn_ptr, d, dp, k, metric, ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(),
-                ws.bucket_off.as<int>(), ws.work_off.as<int>(), ws.part_d.as<float>(), ws.part_i.as<int64_t>()};
+                ws.bucket_off.as<int>(), ws.work_off.as<int>(), ws.part_d.as<float>(), ws.part_i.as<int64_t>(),
+                kQTile};
       run_scan(j, device, ws, s);
       SelectArgs sa{};
       sa.keys = ws.part_d.as<float>();
@@ -326,11 +344,12 @@ void single_list_topk(const ListSet& ls, int G, const float* queries, const floa
     }
     return;
   }
+  const int qtile = pick_qtile(k, d, G);
   ws.bucket_q.reserve(sizeof(int64_t) * nq);
   ws.bucket_slot.reserve(sizeof(int64_t) * nq);
   ws.bucket_off.reserve(sizeof(int) * 2);
   ws.work_off.reserve(sizeof(int) * 2);
-  HIPCHK(launch_single_list_job(nq, chunks, ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(),
+  HIPCHK(launch_single_list_job(nq, chunks, qtile, ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(),
                                 ws.bucket_off.as<int>(), ws.work_off.as<int>(), nullptr, s));
   if (rows) HIPCHK(hipMemcpyAsync(ws.bucket_q.p, rows, sizeof(int64_t) * nq, hipMemcpyDeviceToDevice, s));
   float* pd = out_d;
@@ -342,7 +361,7 @@ void single_list_topk(const ListSet& ls, int G, const float* queries, const floa
     pi = ws.part_i.as<int64_t>();
   }
   ScanJob j{&ls, G, queries, qnorms, d, dp, k, metric, ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(),
-            ws.bucket_off.as<int>(), ws.work_off.as<int>(), pd, pi};
+            ws.bucket_off.as<int>(), ws.work_off.as<int>(), pd, pi, qtile};
   run_scan(j, device, ws, s);
   if (chunks > 1) {
     MergeArgs m{};
@@ -465,12 +484,14 @@ void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t 
   ws.slot_begin.reserve(sizeof(int64_t) * (nq + 1));
   const size_t stb = scan_tmp_bytes(ne) + sizeof(int64_t) * (size_t)ne;
   ws.scan_tmp.reserve(stb);
-  HIPCHK(launch_probe_map(ws.probes_i.as<int64_t>(), nq, np, L.n_lists, L.goff.as<int64_t>(), idx->G,
+  const bool dump = k > kMaxK;
+  const int qtile = dump ? kQTile : pick_qtile(k, idx->d, idx->G);
+  idx->last_qtile = qtile;
+  HIPCHK(launch_probe_map(ws.probes_i.as<int64_t>(), nq, np, L.n_lists, L.goff.as<int64_t>(), idx->G, qtile,
                           ws.counts.as<int>(), ws.fill.as<int>(), ws.bucket_off.as<int>(), ws.work_off.as<int>(),
                           ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(), ws.qp_slots.as<int64_t>(),
                           ws.slot_begin.as<int64_t>(), ws.scan_tmp.p, stb, s));
   // fine scan into per-(query, probe, chunk) slots: top-k partials (k <= 64) or raw keys (DUMP)
-  const bool dump = k > kMaxK;
   const int64_t slot_rows = (int64_t)idx->G * kGroupRows;
   const int64_t max_slots = nq * L.top_chunks_prefix[std::min<int64_t>(np, L.n_lists)];
   const int64_t per_slot_d = dump ? slot_rows : k, per_slot_i = dump ? 2 : k;
@@ -479,7 +500,7 @@ void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t 
   ws.part_i.reserve(sizeof(int64_t) * (size_t)std::max<int64_t>(max_slots * per_slot_i, 1));
   ScanJob j{&L, idx->G, q, ws.qn.as<float>(), idx->d, idx->dp, k, idx->metric, ws.bucket_q.as<int64_t>(),
             ws.bucket_slot.as<int64_t>(), ws.bucket_off.as<int>(), ws.work_off.as<int>(), ws.part_d.as<float>(),
-            ws.part_i.as<int64_t>()};
+            ws.part_i.as<int64_t>(), qtile};
   if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
   run_scan(j, idx->device, ws, s);
   if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
@@ -723,6 +744,7 @@ int32_t mivs_brute_force_search(mivs_index_t idx, void* stream, const float* d_q
     idx->last_nq = nq;
     idx->last_np = 1;
     idx->last_k = k;
+    idx->last_qtile = k > kMaxK ? kQTile : pick_qtile(k, idx->d, idx->G);
   });
 }
 
@@ -747,6 +769,8 @@ int32_t mivs_index_last_search_stats(mivs_index_t idx, mivs_search_stats* out) {
     st.n_queries = idx->last_nq;
     st.n_probes = idx->last_np;
     st.k = idx->last_k;
+    st.query_tile = idx->last_qtile;
+    st.kcap = idx->last_k > 0 ? scan_kcap(idx->last_k) : 0;
     const ListSet& L = idx->lists;
     if (idx->last_nq > 0 && idx->kind == 0) {
       HIPCHK(hipDeviceSynchronize());
@@ -755,13 +779,13 @@ int32_t mivs_index_last_search_stats(mivs_index_t idx, mivs_search_stats* out) {
       HIPCHK(hipMemcpy(woff.data(), idx->ws.work_off.p, sizeof(int) * (L.n_lists + 1), hipMemcpyDeviceToHost));
       for (int l = 0; l < L.n_lists; ++l) {
         st.scanned_rows += (int64_t)counts[l] * (L.h_off[l + 1] - L.h_off[l]);
-        st.streamed_groups += ceil_div(counts[l], kQTile) * (L.h_goff[l + 1] - L.h_goff[l]);
+        st.streamed_groups += ceil_div(counts[l], idx->last_qtile) * (L.h_goff[l + 1] - L.h_goff[l]);
       }
       st.work_items = woff[L.n_lists];
     } else if (idx->last_nq > 0) {
       st.scanned_rows = idx->last_nq * L.n_rows;
-      st.streamed_groups = ceil_div(idx->last_nq, kQTile) * L.n_groups;
-      st.work_items = ceil_div(idx->last_nq, kQTile) * std::max<int64_t>(1, ceil_div(L.n_groups, idx->G));
+      st.streamed_groups = ceil_div(idx->last_nq, idx->last_qtile) * L.n_groups;
+      st.work_items = ceil_div(idx->last_nq, idx->last_qtile) * std::max<int64_t>(1, ceil_div(L.n_groups, idx->G));
     }
     *out = st;
   });

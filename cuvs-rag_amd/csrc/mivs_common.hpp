@@ -56,6 +56,7 @@ struct ScanArgs {
   float* out_d;               // [slots][k]; DUMP mode (kcap 0): raw keys [slots][chunk_groups*32]
   int64_t* out_i;             // [slots][k]; DUMP mode: [slots][2] = (first row position, rows)
   int d, dp, k, metric;
+  int qtile;                  // queries per work item: 32 (K3) or 64 (K3w)
 };
 
 // Large-k select job (K8): per query, the k smallest (key, id) among its candidates.
@@ -97,6 +98,13 @@ hipError_t launch_scan_ex(const ScanArgs& a, int kcap, int grid, size_t lds_byte
 size_t scan_lds_bytes(int dp, int kcap, int chunk_groups);
 bool scan_merge_in_lds(int dp, int kcap, int chunk_groups);
 size_t scan_gmerge_bytes(int grid, int kcap);
+// K3w: 64-query tiles with slab-staged queries (scan_wide.hip)
+size_t scan_wide_lds_bytes(int kcap, int chunk_groups);
+bool scan_wide_supported(int kcap, int d, int dp, int chunk_groups);
+hipError_t launch_scan_wide(const ScanArgs& a, int kcap, int grid, size_t lds_bytes, hipStream_t s);
+// workgroups of the scan kernel resident per CU at this LDS request (hipOccupancy: LDS + registers)
+int scan_occupancy(int kcap, int metric, size_t lds_bytes);
+int scan_wide_occupancy(int kcap, int metric, size_t lds_bytes);
 int scan_kcap(int k);
 hipError_t launch_train_rows(int64_t* rows, int64_t n, int64_t n_train, hipStream_t s);
 hipError_t launch_i64_to_i32(const int64_t* in, int64_t n, int32_t* out, hipStream_t s);
@@ -112,11 +120,11 @@ hipError_t launch_iota_i64(int64_t* out, int64_t n, int64_t start, int64_t step,
 hipError_t launch_fill_i32(int* out, int64_t n, int v, hipStream_t s);
 
 // single-list job prep: bucket = identity over nq queries, slot base = q * chunks
-hipError_t launch_single_list_job(int64_t nq, int64_t chunks, int64_t* bucket_q, int64_t* bucket_slot,
+hipError_t launch_single_list_job(int64_t nq, int64_t chunks, int qtile, int64_t* bucket_q, int64_t* bucket_slot,
                                   int* bucket_off, int* work_off, int64_t* slot_begin, hipStream_t s);
 // IVF probe map: probes [nq][np] (int64 list ids) -> buckets, work offsets, slot bases
 hipError_t launch_probe_map(const int64_t* probes, int64_t nq, int np, int n_lists, const int64_t* list_goff,
-                            int chunk_groups, int* counts, int* fill, int* bucket_off, int* work_off,
+                            int chunk_groups, int qtile, int* counts, int* fill, int* bucket_off, int* work_off,
                             int64_t* bucket_q, int64_t* bucket_slot, int64_t* qp_slots, int64_t* slot_begin,
                             void* scan_tmp, size_t scan_tmp_bytes, hipStream_t s);
 

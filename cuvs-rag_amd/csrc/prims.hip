@@ -140,7 +140,7 @@ __global__ void k_probe_count(const int64_t* __restrict__ probes, int64_t n, int
 }
 
 __global__ __launch_bounds__(1024) void k_probe_prefix(const int* __restrict__ counts, int n_lists,
-                                                       const int64_t* __restrict__ list_goff, int G,
+                                                       const int64_t* __restrict__ list_goff, int G, int qtile,
                                                        int* __restrict__ bucket_off, int* __restrict__ work_off,
                                                        int* __restrict__ fill) {
   __shared__ int64_t sh[16];
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(1024) void k_probe_prefix(const int* __restrict__ c
     if (l < n_lists) {
       c = counts[l];
       const int64_t chunks = ceil_div(list_goff[l + 1] - list_goff[l], G);
-      wk = ceil_div(c, kQTile) * chunks;
+      wk = ceil_div(c, qtile) * chunks;
       fill[l] = 0;
     }
     int64_t tb, tw;
@@ -189,7 +189,7 @@ __global__ void k_slot_begin(const int64_t* __restrict__ qp_base, const int64_t*
   if (q == nq) slot_begin[nq] = qp_base[nq * np - 1] + qp_slots[nq * np - 1];
 }
 
-__global__ void k_single_job(int64_t nq, int64_t chunks, int64_t* __restrict__ bucket_q,
+__global__ void k_single_job(int64_t nq, int64_t chunks, int qtile, int64_t* __restrict__ bucket_q,
                              int64_t* __restrict__ bucket_slot, int* __restrict__ bucket_off,
                              int* __restrict__ work_off, int64_t* __restrict__ slot_begin) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -202,7 +202,7 @@ __global__ void k_single_job(int64_t nq, int64_t chunks, int64_t* __restrict__ b
     bucket_off[0] = 0;
     bucket_off[1] = (int)nq;
     work_off[0] = 0;
-    work_off[1] = (int)(ceil_div(nq, kQTile) * chunks);
+    work_off[1] = (int)(ceil_div(nq, qtile) * chunks);
     if (slot_begin) slot_begin[nq] = nq * chunks;
   }
 }
@@ -304,7 +304,7 @@ hipError_t launch_counting_sort(const int64_t* labels, int64_t n, int nl, int64_
 }
 
 hipError_t launch_probe_map(const int64_t* probes, int64_t nq, int np, int n_lists, const int64_t* list_goff,
-                            int chunk_groups, int* counts, int* fill, int* bucket_off, int* work_off,
+                            int chunk_groups, int qtile, int* counts, int* fill, int* bucket_off, int* work_off,
                             int64_t* bucket_q, int64_t* bucket_slot, int64_t* qp_slots, int64_t* slot_begin,
                             void* scan_tmp, size_t scan_tmp_bytes_, hipStream_t s) {
   const int64_t n = nq * np;
@@ -314,8 +314,8 @@ hipError_t launch_probe_map(const int64_t* probes, int64_t nq, int np, int n_lis
   hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * n_lists, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_probe_count, grid1(n, 256), dim3(256), 0, s, probes, n, counts);
-  hipLaunchKernelGGL(k_probe_prefix, dim3(1), dim3(1024), 0, s, counts, n_lists, list_goff, chunk_groups, bucket_off,
-                     work_off, fill);
+  hipLaunchKernelGGL(k_probe_prefix, dim3(1), dim3(1024), 0, s, counts, n_lists, list_goff, chunk_groups, qtile,
+                     bucket_off, work_off, fill);
   hipLaunchKernelGGL(k_probe_fill, grid1(n, 256), dim3(256), 0, s, probes, n, np, bucket_off, fill, bucket_q,
                      bucket_slot, list_goff, chunk_groups, qp_slots);
   e = launch_exclusive_scan_i64(qp_slots, qp_base, n, stmp, s);
@@ -325,10 +325,10 @@ hipError_t launch_probe_map(const int64_t* probes, int64_t nq, int np, int n_lis
   return hipGetLastError();
 }
 
-hipError_t launch_single_list_job(int64_t nq, int64_t chunks, int64_t* bucket_q, int64_t* bucket_slot,
+hipError_t launch_single_list_job(int64_t nq, int64_t chunks, int qtile, int64_t* bucket_q, int64_t* bucket_slot,
                                   int* bucket_off, int* work_off, int64_t* slot_begin, hipStream_t s) {
-  hipLaunchKernelGGL(k_single_job, grid1(nq, 256), dim3(256), 0, s, nq, chunks, bucket_q, bucket_slot, bucket_off,
-                     work_off, slot_begin);
+  hipLaunchKernelGGL(k_single_job, grid1(nq, 256), dim3(256), 0, s, nq, chunks, qtile, bucket_q, bucket_slot,
+                     bucket_off, work_off, slot_begin);
   return hipGetLastError();
 }
 

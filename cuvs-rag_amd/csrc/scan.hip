@@ -382,6 +382,33 @@ hipError_t launch_scan_ex(const ScanArgs& a, int kcap, int grid, size_t lds, flo
   }
 }
 
+template <int KCAP, int METRIC>
+static int occ_km(size_t lds) {
+  int n = 0;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<KCAP, METRIC>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&k_scan<KCAP, METRIC>),
+                                                   kScanThreads, lds) != hipSuccess)
+    return 1;
+  return n > 0 ? n : 1;
+}
+
+template <int KCAP>
+static int occ_k(int metric, size_t lds) { return metric == kIP ? occ_km<KCAP, kIP>(lds) : occ_km<KCAP, kL2>(lds); }
+
+int scan_occupancy(int kcap, int metric, size_t lds) {
+  switch (kcap) {
+    case 0: return occ_k<0>(metric, lds);
+    case 1: return occ_k<1>(metric, lds);
+    case 4: return occ_k<4>(metric, lds);
+    case 8: return occ_k<8>(metric, lds);
+    case 16: return occ_k<16>(metric, lds);
+    case 32: return occ_k<32>(metric, lds);
+    case 64: return occ_k<64>(metric, lds);
+    default: return 1;
+  }
+}
+
 hipError_t launch_scan(const ScanArgs& a, int kcap, int grid, size_t lds_bytes, hipStream_t s) {
   return launch_scan_ex(a, kcap, grid, lds_bytes, nullptr, s);
 }

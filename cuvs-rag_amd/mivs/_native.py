@@ -63,6 +63,8 @@ class SearchStats(ctypes.Structure):
         ("scanned_rows", c_int64),
         ("streamed_groups", c_int64),
         ("work_items", c_int64),
+        ("query_tile", c_int32),
+        ("kcap", c_int32),
     ]
 
     def as_dict(self) -> dict:

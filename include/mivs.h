@@ -61,6 +61,8 @@ typedef struct {
   int64_t scanned_rows;     /* sum over (query, probed list) of list size: algorithmic rows */
   int64_t streamed_groups;  /* sum over fine-scan work items of 32-row groups streamed from HBM */
   int64_t work_items;       /* fine-scan work items */
+  int32_t query_tile;       /* queries per fine-scan work item: 32 (K3 k_scan) or 64 (K3w k_scan_wide) */
+  int32_t kcap;             /* register top-k capacity of the fine scan (0: DUMP mode + K8 select) */
 } mivs_search_stats;
 
 /* device time of the searches issued since the last collect while profiling was on

@@ -350,3 +350,39 @@ def test_merge_topk_large_k_matches_oracle(mivs_lib, m, kin, k, metric):
     gd, gi = ops.merge_topk(_gpu(d), _gpu(ids), k, metric=metric)
     np.testing.assert_array_equal(gi.cpu().numpy(), oi)
     np.testing.assert_array_equal(_bits(gd.cpu().numpy()), _bits(od))
+
+
+# ---- K3w (64-query tiles, slab-staged queries): same arithmetic, must be bit-identical ----
+WIDE_CASES = [
+    # n, d, nq, k, metric, n_lists (0 = brute force)
+    (5000, 768, 100, 10, "sqeuclidean", 0),
+    (3001, 128, 65, 1, "sqeuclidean", 0),
+    (4096, 256, 129, 16, "sqeuclidean", 0),
+    (2000, 128, 50, 8, "inner_product", 0),
+    (777, 124, 31, 4, "sqeuclidean", 0),      # d % 4 == 0, dp = 128, tail dims zero
+    (20000, 768, 300, 10, "sqeuclidean", 64),
+    (12000, 384, 97, 16, "sqeuclidean", 32),
+    (9000, 256, 70, 10, "inner_product", 40),
+]
+
+
+@pytest.mark.parametrize("n,d,nq,k,metric,n_lists", WIDE_CASES)
+def test_wide_scan_bitexact(mivs_lib, monkeypatch, n, d, nq, k, metric, n_lists):
+    from mivs.neighbors import brute_force, ivf_flat
+
+    monkeypatch.setenv("MIVS_SCAN_WIDE", "1")
+    x = _data(n, d, seed=n + d + 3, normalize=True)
+    q = _data(nq, d, seed=n + d + 4, normalize=True)
+    if n_lists == 0:
+        dist, ids = brute_force.search(brute_force.build(_gpu(x), metric=metric), _gpu(q), k)
+        od, oi = O.knn(x, q, k, metric=metric)
+    else:
+        idx = ivf_flat.build(ivf_flat.IndexParams(n_lists=n_lists, kmeans_n_iters=3, metric=metric), _gpu(x))
+        oc, osz, oids = O.ivf_build(x, n_lists, iters=3, metric=metric)
+        np.testing.assert_array_equal(_bits(idx.centers.cpu().numpy()), _bits(oc))
+        np.testing.assert_array_equal(idx.list_ids().cpu().numpy(), oids)
+        n_probes = min(8, n_lists)
+        dist, ids = ivf_flat.search(ivf_flat.SearchParams(n_probes=n_probes), idx, _gpu(q), k)
+        od, oi, _ = O.ivf_search(x, oc, osz, oids, q, n_probes, k, metric=metric)
+    np.testing.assert_array_equal(ids.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(dist.cpu().numpy()), _bits(od))

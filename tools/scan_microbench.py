@@ -47,5 +47,8 @@ def run(n, nq, d=768, reps=3):
 
 if __name__ == "__main__":
     total = 2 ** 33  # rows x queries per case
-    for n in [1024, 8192, 65536, 262144, 1 << 20, 4 << 20]:
-        run(n, max(32, total // n))
+    for wide in ("0", "1"):
+        os.environ["MIVS_SCAN_WIDE"] = wide
+        print(f"--- MIVS_SCAN_WIDE={wide} ({'K3w 64-query tiles' if wide == '1' else 'K3 32-query tiles'})", flush=True)
+        for n in [1024, 65536, 1 << 20, 4 << 20]:
+            run(n, max(32, total // n))
