@@ -231,11 +231,11 @@ struct ScanJob {
   int qtile;  // 32: K3, 64: K3w (must match the work decomposition of the probe map / single job)
 };
 
-// Query tile of the fine scan for k: K3w (64 queries, slab-staged) where it applies and
-// MIVS_SCAN_WIDE=1, else K3.
+// Query tile of the fine scan for k: K3w (64 queries, slab-staged) where it applies, else K3.
+// MIVS_SCAN_WIDE=0 forces K3 (A/B measurements).
 int pick_qtile(int k, int d, int G) {
   const char* e = getenv("MIVS_SCAN_WIDE");
-  if (!e || e[0] != '1') return kQTile;
+  if (e && e[0] == '0') return kQTile;
   const int kcap = scan_kcap(k);
   return kcap > 0 && scan_wide_supported(kcap, d, dim_pad(d), G) ? 64 : kQTile;
 }

@@ -106,6 +106,7 @@ hipError_t launch_scan_wide(const ScanArgs& a, int kcap, int grid, size_t lds_by
 int scan_occupancy(int kcap, int metric, size_t lds_bytes);
 int scan_wide_occupancy(int kcap, int metric, size_t lds_bytes);
 int scan_kcap(int k);
+int scan_waves(int kcap);  // waves per K3 workgroup for this register list length
 hipError_t launch_train_rows(int64_t* rows, int64_t n, int64_t n_train, hipStream_t s);
 hipError_t launch_i64_to_i32(const int64_t* in, int64_t n, int32_t* out, hipStream_t s);
 hipError_t launch_merge(const MergeArgs& a, hipStream_t s);

@@ -118,12 +118,15 @@ __device__ __forceinline__ void epilogue_dump(const f32x16& acc, const float* __
   }
 }
 
-template <int KCAP, int METRIC>
-__global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a, float* __restrict__ gmerge) {
+// W waves per workgroup: 16 (4 per SIMD; needs <= 128 VGPRs, KCAP <= 16) or 8
+template <int KCAP, int METRIC, int W>
+__global__ __launch_bounds__(W * 64, 1) void k_scan(ScanArgs a, float* __restrict__ gmerge) {
   // k-steps per register buffer: 8 (2 KiB of list rows in flight per lane-pair ring slot) unless the
   // register top-K is large
   constexpr int BLK = KCAP >= 32 ? 4 : 8;
   constexpr bool DUMP = KCAP == 0;
+  constexpr int NT = W * 64;
+  constexpr int NS = 2 * W;  // lane lists per query (W waves x 2 halves)
   constexpr int KR = DUMP ? 1 : KCAP;  // register list length
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int64_t* s_q = reinterpret_cast<int64_t*>(smem);          // [32] query row ids (-1: empty lane)
@@ -136,8 +139,8 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a, float* __r
   const int qstride = dp + 4;  // +16 B per row: conflict-free ds_read_b128 of the B operand
 
   // merge area: LDS after the scan when it fits, else this block's global scratch
-  float* mkey = gmerge ? gmerge + (size_t)blockIdx.x * (kQTile * 16 * KR * 2) : qtile;
-  int* mpos = reinterpret_cast<int*>(mkey + kQTile * 16 * KR);
+  float* mkey = gmerge ? gmerge + (size_t)blockIdx.x * (kQTile * NS * KR * 2) : qtile;
+  int* mpos = reinterpret_cast<int*>(mkey + kQTile * NS * KR);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -185,7 +188,7 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a, float* __r
     }
     {  // row norms of the chunk -> LDS
       const int nn = (int)(g_end - g_begin) * kGroupRows;
-      for (int i = tid; i < nn; i += kScanThreads) s_norm[i] = a.row_norms[g_begin * kGroupRows + i];
+      for (int i = tid; i < nn; i += NT) s_norm[i] = a.row_norms[g_begin * kGroupRows + i];
       if (DUMP && tid < nqt) {  // slot header: first row position + rows of this chunk
         const int64_t slot = a.bucket_slot[e0 + tid] + chunk;
         a.out_i[2 * slot] = g_begin * kGroupRows;
@@ -197,7 +200,7 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a, float* __r
     // ---- stage the query tile in LDS (zero-padded dims, zero rows for empty lanes) ----
     {
       const int c4 = dp >> 2;
-      for (int i = tid; i < kQTile * c4; i += kScanThreads) {
+      for (int i = tid; i < kQTile * c4; i += NT) {
         const int r = i / c4;
         const int c = (i - r * c4) << 2;
         const int64_t q = s_q[r];
@@ -223,11 +226,11 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a, float* __r
     //      after block b's MFMAs, so a full block of MFMAs covers every load, across group
     //      boundaries too ----
     const int64_t g0 = g_begin + wave;
-    const int ng = g_end > g0 ? (int)((g_end - g0 + kScanWaves - 1) / kScanWaves) : 0;
+    const int ng = g_end > g0 ? (int)((g_end - g0 + W - 1) / W) : 0;
     const int nb = ng * bpg;
     if (nb > 0) {
       const float* lane_base = a.groups + g0 * (int64_t)(kGroupRows * dp) + j * 8 + 4 * h;
-      const int64_t gstride = (int64_t)kScanWaves * kGroupRows * dp;
+      const int64_t gstride = (int64_t)W * kGroupRows * dp;
       auto bptr = [&](int b) {
         const int bb = b < nb ? b : nb - 1;  // past the end: re-read the last block (never consumed)
         const int gi = bb / bpg;
@@ -247,11 +250,11 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a, float* __r
         load_block<BLK>(A, bptr(b + 2));
         if (++sb == bpg) {
           if constexpr (DUMP)
-            epilogue_dump<METRIC>(acc, s_norm + (wave + gi * kScanWaves) * kGroupRows, h, qn,
-                                  dump_base ? dump_base + (wave + gi * kScanWaves) * kGroupRows : nullptr);
+            epilogue_dump<METRIC>(acc, s_norm + (wave + gi * W) * kGroupRows, h, qn,
+                                  dump_base ? dump_base + (wave + gi * W) * kGroupRows : nullptr);
           else
-            epilogue<KCAP, METRIC>(acc, s_norm + (wave + gi * kScanWaves) * kGroupRows,
-                                   (g0 + (int64_t)gi * kScanWaves) * kGroupRows, h, qn, qvalid, lk, lp);
+            epilogue<KCAP, METRIC>(acc, s_norm + (wave + gi * W) * kGroupRows,
+                                   (g0 + (int64_t)gi * W) * kGroupRows, h, qn, qvalid, lk, lp);
           acc = zero;
           sb = 0;
           ++gi;
@@ -260,11 +263,11 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a, float* __r
         load_block<BLK>(B, bptr(b + 3));
         if (++sb == bpg && b + 1 < nb) {
           if constexpr (DUMP)
-            epilogue_dump<METRIC>(acc, s_norm + (wave + gi * kScanWaves) * kGroupRows, h, qn,
-                                  dump_base ? dump_base + (wave + gi * kScanWaves) * kGroupRows : nullptr);
+            epilogue_dump<METRIC>(acc, s_norm + (wave + gi * W) * kGroupRows, h, qn,
+                                  dump_base ? dump_base + (wave + gi * W) * kGroupRows : nullptr);
           else
-            epilogue<KCAP, METRIC>(acc, s_norm + (wave + gi * kScanWaves) * kGroupRows,
-                                   (g0 + (int64_t)gi * kScanWaves) * kGroupRows, h, qn, qvalid, lk, lp);
+            epilogue<KCAP, METRIC>(acc, s_norm + (wave + gi * W) * kGroupRows,
+                                   (g0 + (int64_t)gi * W) * kGroupRows, h, qn, qvalid, lk, lp);
           acc = zero;
           sb = 0;
           ++gi;
@@ -276,22 +279,22 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a, float* __r
       __syncthreads();  // LDS (s_*, qtile) reused by the next work item
       continue;
     }
-    // ---- merge the 16 lane lists (8 waves x 2 halves) of every query ----
+    // ---- merge the NS lane lists (W waves x 2 halves) of every query ----
     __syncthreads();  // every wave is done with qtile (the merge area may alias it)
     {
       const int src = wave * 2 + h;
 #pragma unroll
       for (int t = 0; t < KCAP; ++t) {
-        mkey[(j * 16 + src) * KCAP + t] = lk[t];
-        mpos[(j * 16 + src) * KCAP + t] = lp[t];
+        mkey[(j * NS + src) * KCAP + t] = lk[t];
+        mpos[(j * NS + src) * KCAP + t] = lp[t];
       }
     }
     __syncthreads();
     {
-      const int jj = tid >> 4;  // query of this 16-thread segment
-      const int ss = tid & 15;  // source list of this thread
-      const float* myk = mkey + (jj * 16 + ss) * KCAP;
-      const int* myp = mpos + (jj * 16 + ss) * KCAP;
+      const int jj = tid / NS;  // query of this NS-thread segment
+      const int ss = tid % NS;  // source list of this thread
+      const float* myk = mkey + (jj * NS + ss) * KCAP;
+      const int* myp = mpos + (jj * NS + ss) * KCAP;
       const int64_t slot = s_slot[jj];
       int head = 0;
       float hk = myk[0];
@@ -300,9 +303,9 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a, float* __r
         float bk = hk;
         int bp = hp;
 #pragma unroll
-        for (int off = 8; off >= 1; off >>= 1) {
-          const float ok = __shfl_xor(bk, off, 16);
-          const int op = __shfl_xor(bp, off, 16);
+        for (int off = NS / 2; off >= 1; off >>= 1) {
+          const float ok = __shfl_xor(bk, off, NS);
+          const int op = __shfl_xor(bp, off, NS);
           if (ok < bk || (ok == bk && op < bp)) { bk = ok; bp = op; }
         }
         if (ss == 0 && slot >= 0) {
@@ -321,18 +324,24 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a, float* __r
   }
 }
 
-template <int KCAP, int METRIC>
-hipError_t launch_km(const ScanArgs& a, int grid, size_t lds, float* gmerge, hipStream_t s) {
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<KCAP, METRIC>),
+template <int KCAP, int METRIC, int W>
+hipError_t launch_kmw(const ScanArgs& a, int grid, size_t lds, float* gmerge, hipStream_t s) {
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<KCAP, METRIC, W>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL((k_scan<KCAP, METRIC>), dim3(grid), dim3(kScanThreads), lds, s, a, gmerge);
+  hipLaunchKernelGGL((k_scan<KCAP, METRIC, W>), dim3(grid), dim3(W * 64), lds, s, a, gmerge);
   return hipGetLastError();
 }
 
 template <int KCAP>
 hipError_t launch_k(const ScanArgs& a, int grid, size_t lds, float* gmerge, hipStream_t s) {
-  return a.metric == kIP ? launch_km<KCAP, kIP>(a, grid, lds, gmerge, s) : launch_km<KCAP, kL2>(a, grid, lds, gmerge, s);
+  if constexpr (KCAP <= 16) {
+    if (scan_waves(KCAP) == 16)
+      return a.metric == kIP ? launch_kmw<KCAP, kIP, 16>(a, grid, lds, gmerge, s)
+                             : launch_kmw<KCAP, kL2, 16>(a, grid, lds, gmerge, s);
+  }
+  return a.metric == kIP ? launch_kmw<KCAP, kIP, 8>(a, grid, lds, gmerge, s)
+                         : launch_kmw<KCAP, kL2, 8>(a, grid, lds, gmerge, s);
 }
 
 }  // namespace
@@ -342,13 +351,23 @@ int scan_kcap(int k) {
   if (k <= 1) return 1;
   if (k <= 4) return 4;
   if (k <= 8) return 8;
+  if (k <= 12) return 12;  // k = 10 (the benchmark's k): 8 fewer list registers than 16
   if (k <= 16) return 16;
   if (k <= 32) return 32;
   if (k <= 64) return 64;
   return -1;
 }
 
-static size_t merge_bytes(int kcap) { return (size_t)kQTile * 16 * kcap * 8; }
+// waves per K3 workgroup: 16 (4 waves per SIMD, register budget <= 128) for the DUMP scan, else 8.
+// MIVS_SCAN_WAVES=8 forces 8 (A/B measurements).
+int scan_waves(int kcap) {
+  // 16 waves need <= 128 VGPRs: only the DUMP instantiation fits without spilling
+  const char* e = getenv("MIVS_SCAN_WAVES");
+  if (e && atoi(e) == 8) return 8;
+  return kcap == 0 ? 16 : 8;
+}
+
+static size_t merge_bytes(int kcap) { return (size_t)kQTile * 2 * scan_waves(kcap) * kcap * 8; }
 static size_t qtile_bytes(int dp) { return (size_t)kQTile * (dp + 4) * 4; }
 static size_t norm_bytes(int chunk_groups) { return (size_t)chunk_groups * kGroupRows * 4; }
 static constexpr size_t kLdsMax = 160 * 1024;
@@ -375,6 +394,7 @@ hipError_t launch_scan_ex(const ScanArgs& a, int kcap, int grid, size_t lds, flo
     case 1: return launch_k<1>(a, grid, lds, gmerge, s);
     case 4: return launch_k<4>(a, grid, lds, gmerge, s);
     case 8: return launch_k<8>(a, grid, lds, gmerge, s);
+    case 12: return launch_k<12>(a, grid, lds, gmerge, s);
     case 16: return launch_k<16>(a, grid, lds, gmerge, s);
     case 32: return launch_k<32>(a, grid, lds, gmerge, s);
     case 64: return launch_k<64>(a, grid, lds, gmerge, s);
@@ -382,19 +402,24 @@ hipError_t launch_scan_ex(const ScanArgs& a, int kcap, int grid, size_t lds, flo
   }
 }
 
-template <int KCAP, int METRIC>
-static int occ_km(size_t lds) {
+template <int KCAP, int METRIC, int W>
+static int occ_kmw(size_t lds) {
   int n = 0;
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<KCAP, METRIC>),
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan<KCAP, METRIC, W>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&k_scan<KCAP, METRIC>),
-                                                   kScanThreads, lds) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&k_scan<KCAP, METRIC, W>),
+                                                   W * 64, lds) != hipSuccess)
     return 1;
   return n > 0 ? n : 1;
 }
 
 template <int KCAP>
-static int occ_k(int metric, size_t lds) { return metric == kIP ? occ_km<KCAP, kIP>(lds) : occ_km<KCAP, kL2>(lds); }
+static int occ_k(int metric, size_t lds) {
+  if constexpr (KCAP <= 16) {
+    if (scan_waves(KCAP) == 16) return metric == kIP ? occ_kmw<KCAP, kIP, 16>(lds) : occ_kmw<KCAP, kL2, 16>(lds);
+  }
+  return metric == kIP ? occ_kmw<KCAP, kIP, 8>(lds) : occ_kmw<KCAP, kL2, 8>(lds);
+}
 
 int scan_occupancy(int kcap, int metric, size_t lds) {
   switch (kcap) {
@@ -402,6 +427,7 @@ int scan_occupancy(int kcap, int metric, size_t lds) {
     case 1: return occ_k<1>(metric, lds);
     case 4: return occ_k<4>(metric, lds);
     case 8: return occ_k<8>(metric, lds);
+    case 12: return occ_k<12>(metric, lds);
     case 16: return occ_k<16>(metric, lds);
     case 32: return occ_k<32>(metric, lds);
     case 64: return occ_k<64>(metric, lds);

@@ -27,7 +27,6 @@ namespace {
 constexpr int kWQ = 64;             // queries per tile
 constexpr int kSlab = 128;          // dims per staged query slab = one step (16 k-steps: blocks A and B)
 constexpr int kSld = kSlab + 4;     // LDS row stride of a slab (floats); = 4 mod 64 banks
-constexpr int kPassG = kScanWaves;  // 8 groups per pass (one per wave)
 constexpr int kWSmall = 64 * 8 + 64 * 8 + 64 * 4 + 16;  // s_q, s_slot, s_qn, s_misc
 
 template <int KCAP>
@@ -66,11 +65,15 @@ __device__ __forceinline__ void wepilogue(const f32x16& acc, const float* __rest
   }
 }
 
-// 8 k-steps (half a slab) of one row group against both query tiles of the slab in LDS
-__device__ __forceinline__ void mma8(f32x16& c0, f32x16& c1, const float4 (&v)[8], const float* __restrict__ q0,
-                                     const float* __restrict__ q1) {
+// 8 k-steps of one row group against both query tiles, each k-step's A register refilled from
+// `next` right after its 8 MFMAs. The sched_group_barriers pin the per-k-step issue pattern
+// (8 MFMA, 1 VMEM, 2 DS): one wide load per 8 MFMAs keeps the stream in flight without ever
+// stalling the two accumulator chains (tools/mfma_probe.hip P7: 96 % of the fp32 MFMA peak).
+template <int U0, int U1>
+__device__ __forceinline__ void mma8_refill(f32x16& c0, f32x16& c1, float4 (&v)[8], const float* __restrict__ q0,
+                                            const float* __restrict__ q1, const float* __restrict__ next) {
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
+  for (int u = U0; u < U1; ++u) {
     const float4 b0 = *reinterpret_cast<const float4*>(q0 + u * 8);
     const float4 b1 = *reinterpret_cast<const float4*>(q1 + u * 8);
     c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v[u].x, b0.x, c0, 0, 0, 0);
@@ -81,6 +84,10 @@ __device__ __forceinline__ void mma8(f32x16& c0, f32x16& c1, const float4 (&v)[8
     c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v[u].z, b1.z, c1, 0, 0, 0);
     c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v[u].w, b0.w, c0, 0, 0, 0);
     c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v[u].w, b1.w, c1, 0, 0, 0);
+    v[u] = *reinterpret_cast<const float4*>(next + u * 256);
+    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);  // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
   }
 }
 
@@ -89,8 +96,14 @@ __device__ __forceinline__ void load8(float4 (&v)[8], const float* __restrict__ 
   for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(p + u * 256);
 }
 
-template <int KCAP, int METRIC>
-__global__ __launch_bounds__(kScanThreads, 1) void k_scan_wide(ScanArgs a) {
+// W waves per workgroup (4: two workgroups per CU interleave their barriers / merges on every
+// SIMD; 8: one workgroup per CU). A pass covers W row groups, one per wave.
+template <int KCAP, int METRIC, int W>
+__global__ __launch_bounds__(W * 64, 1) void k_scan_wide(ScanArgs a) {
+  constexpr int NT = W * 64;
+  constexpr int NS = 2 * W;          // lane lists per query (W waves x 2 halves)
+  constexpr int SPT = 2048 / NT;     // staged float4s per thread per slab (64 queries x 128 dims)
+  constexpr int RS = NT / 32;        // query rows covered per staging sub-pass
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int64_t* s_q = reinterpret_cast<int64_t*>(smem);       // [64] query row ids (-1: empty)
   int64_t* s_slot = s_q + kWQ;                            // [64] output slot (already + chunk)
@@ -99,7 +112,7 @@ __global__ __launch_bounds__(kScanThreads, 1) void k_scan_wide(ScanArgs a) {
   float* s_norm = reinterpret_cast<float*>(smem + kWSmall);  // [G*32]
   float* qs = s_norm + a.chunk_groups * kGroupRows;       // [2][64][kSld]; merge area after the scan
   float* mkey = qs;
-  int* mpos = reinterpret_cast<int*>(mkey + 32 * 16 * KCAP);
+  int* mpos = reinterpret_cast<int*>(mkey + 32 * NS * KCAP);
 
   const int dp = a.dp;
   const int tid = threadIdx.x;
@@ -109,6 +122,9 @@ __global__ __launch_bounds__(kScanThreads, 1) void k_scan_wide(ScanArgs a) {
   const int h = lane >> 5;
   const int total = a.work_off[a.n_lists];
   const int64_t gstride = (int64_t)kGroupRows * dp;  // floats per group
+  const int ns = dp / kSlab;
+  const int sr = tid >> 5;          // staging: query row (+ RS i) and dim offset within the slab
+  const int sc = (tid & 31) << 2;
 
   for (;;) {
     if (tid == 0) s_misc[0] = atomicAdd(a.work_counter, 1);
@@ -147,7 +163,7 @@ __global__ __launch_bounds__(kScanThreads, 1) void k_scan_wide(ScanArgs a) {
     }
     {
       const int nn = (int)(g_end - g_begin) * kGroupRows;
-      for (int i = tid; i < nn; i += kScanThreads) s_norm[i] = a.row_norms[g_begin * kGroupRows + i];
+      for (int i = tid; i < nn; i += NT) s_norm[i] = a.row_norms[g_begin * kGroupRows + i];
     }
     __syncthreads();
 
@@ -158,58 +174,48 @@ __global__ __launch_bounds__(kScanThreads, 1) void k_scan_wide(ScanArgs a) {
     const float qn0 = s_qn[j], qn1 = s_qn[32 + j];
     const bool qv0 = s_q[j] >= 0, qv1 = s_q[32 + j] >= 0;
 
-    // slab staging: the 64 x 128 slab is 2048 float4s, thread tid owns float4s tid + 512 i (i < 4):
-    // query row (tid >> 5) + 16 i, dims ((tid & 31) << 2) .. + 3
-    const int sr = tid >> 5;
-    const int sc = (tid & 31) << 2;
-    const int64_t sq0 = s_q[sr], sq1 = s_q[sr + 16], sq2 = s_q[sr + 32], sq3 = s_q[sr + 48];
-    // per staged float4: source offset (floats) into a.queries and a validity mask; an invalid
-    // query lane reads query row 0 (always mapped) and is zeroed by the mask: the staging loads are
-    // branch- and select-free, so no VMEM wait is forced inside the step loop (d % 4 == 0 required)
-    const int64_t so0 = sq0 >= 0 ? sq0 * (int64_t)a.d : 0, so1 = sq1 >= 0 ? sq1 * (int64_t)a.d : 0;
-    const int64_t so2 = sq2 >= 0 ? sq2 * (int64_t)a.d : 0, so3 = sq3 >= 0 ? sq3 * (int64_t)a.d : 0;
-    auto stage_one = [&](int64_t off, bool qok, int c) {
-      const bool ok = qok && c < a.d;
-      const uint32_t m = ok ? 0xFFFFFFFFu : 0u;
-      const float4 t = *reinterpret_cast<const float4*>(a.queries + (ok ? off + c : 0));
-      return make_float4(__uint_as_float(__float_as_uint(t.x) & m), __uint_as_float(__float_as_uint(t.y) & m),
-                         __uint_as_float(__float_as_uint(t.z) & m), __uint_as_float(__float_as_uint(t.w) & m));
+    // query-slab staging: staged float4 i of this thread = query row sr + RS i (int32 row id kept,
+    // -1: empty lane), dims slab * 128 + sc .. + 3. An invalid float4 reads query row 0 (always
+    // mapped) and is zeroed by a mask: the loads are branch- and select-free (d % 4 == 0 required).
+    // Slabs are staged in two halves of SPT / 2 float4s to keep the in-flight registers low.
+    int sq[SPT];
+#pragma unroll
+    for (int i = 0; i < SPT; ++i) sq[i] = (int)s_q[sr + RS * i];
+    auto stage_load = [&](int slab, int half, float4 (&v)[SPT / 2]) {
+      const int c = slab * kSlab + sc;
+#pragma unroll
+      for (int i = 0; i < SPT / 2; ++i) {
+        const int qi = sq[half * (SPT / 2) + i];
+        const uint32_t m2 = (qi >= 0 && c < a.d) ? 0xFFFFFFFFu : 0u;
+        const float4 t = *reinterpret_cast<const float4*>(a.queries + (m2 ? (int64_t)qi * a.d + c : 0));
+        v[i] = make_float4(__uint_as_float(__float_as_uint(t.x) & m2), __uint_as_float(__float_as_uint(t.y) & m2),
+                           __uint_as_float(__float_as_uint(t.z) & m2), __uint_as_float(__float_as_uint(t.w) & m2));
+      }
     };
-#define MIVS_STAGE_LOAD(S, V0, V1, V2, V3)            \
-  do {                                                \
-    const int c_ = (S) * kSlab + sc;                  \
-    V0 = stage_one(so0, sq0 >= 0, c_);                \
-    V1 = stage_one(so1, sq1 >= 0, c_);                \
-    V2 = stage_one(so2, sq2 >= 0, c_);                \
-    V3 = stage_one(so3, sq3 >= 0, c_);                \
-  } while (0)
-#define MIVS_STAGE_STORE(BUF, V0, V1, V2, V3)                                   \
-  do {                                                                        \
-    float* b_ = qs + (BUF) * (kWQ * kSld) + sr * kSld + sc;                   \
-    *reinterpret_cast<float4*>(b_) = V0;                                      \
-    *reinterpret_cast<float4*>(b_ + 16 * kSld) = V1;                          \
-    *reinterpret_cast<float4*>(b_ + 32 * kSld) = V2;                          \
-    *reinterpret_cast<float4*>(b_ + 48 * kSld) = V3;                          \
-  } while (0)
+    auto stage_store = [&](int buf, int half, const float4 (&v)[SPT / 2]) {
+      float* b = qs + buf * (kWQ * kSld) + (sr + RS * half * (SPT / 2)) * kSld + sc;
+#pragma unroll
+      for (int i = 0; i < SPT / 2; ++i) *reinterpret_cast<float4*>(b + RS * i * kSld) = v[i];
+    };
 
     // ONE stream of (pass, slab) steps: pass = one group per wave, slab = 16 k-steps = register
     // blocks A (k-steps 0-7) and B (8-15). The loads of step t+1 (both blocks + the next query slab)
     // are issued during step t, across pass boundaries too; past the end the current blocks are
     // re-read (L2 hits, never consumed).
-    const int ns = dp / kSlab;
-    const int npass = (int)((g_end - g_begin + kPassG - 1) / kPassG);
+    const int npass = (int)((g_end - g_begin + W - 1) / W);
     const int nsteps = npass * ns;
     auto grp_ptr = [&](int pass) {
-      const int64_t g = g_begin + pass * kPassG + wave;
+      const int64_t g = g_begin + pass * W + wave;
       return a.groups + (g < g_end ? g : g_begin) * gstride + j * 8 + 4 * h;
     };
     float4 A[8], B[8];
     {
-      float4 v0, v1, v2, v3;
-      MIVS_STAGE_LOAD(0, v0, v1, v2, v3);
-      MIVS_STAGE_STORE(0, v0, v1, v2, v3);
-      // same issue order as the loop body (all of A, then all of B): the wait counts the loop head
-      // inherits from this path then match the steady state
+      float4 v[SPT / 2];
+      stage_load(0, 0, v);
+      stage_store(0, 0, v);
+      stage_load(0, 1, v);
+      stage_store(0, 1, v);
+      // same issue order as the loop body (all of A, then all of B)
       __builtin_amdgcn_sched_barrier(0);
       load8(A, grp_ptr(0));
       __builtin_amdgcn_sched_barrier(0);
@@ -224,26 +230,32 @@ __global__ __launch_bounds__(kScanThreads, 1) void k_scan_wide(ScanArgs a) {
     for (int t = 0; t < nsteps; ++t) {
       const int tn = t + 1 < nsteps ? t + 1 : t;
       const int pn = tn / ns, sn = tn - pn * ns;
-      float4 n0, n1, n2, n3;
-      MIVS_STAGE_LOAD(sn, n0, n1, n2, n3);
       const float* qb = qs + (t & 1) * (kWQ * kSld) + 4 * h;
       const float* q0 = qb + j * kSld;
       const float* q1 = qb + (32 + j) * kSld;
       const float* pnext = grp_ptr(pn) + sn * (16 * 256);
-      // sched_barrier: keep each refill right behind the MFMAs that free its registers, so a full
-      // block of MFMAs (64) covers it; left alone the scheduler sinks both refills to the step end
-      mma8(c0, c1, A, q0, q1);
+      // issue order per step: A block (8 x [8 MFMA, 1 refill]), slab half 0 loads, B k-steps 0-3,
+      // slab half 0 stores + half 1 loads, B k-steps 4-7, slab half 1 stores. sched_barriers keep
+      // the slab loads out of the refill slots.
+      const bool stage = t + 1 < nsteps;
+      const int nb = (t + 1) & 1;
+      float4 nv[SPT / 2];
       __builtin_amdgcn_sched_barrier(0);
-      load8(A, pnext);
+      mma8_refill<0, 8>(c0, c1, A, q0, q1, pnext);
       __builtin_amdgcn_sched_barrier(0);
-      mma8(c0, c1, B, q0 + 64, q1 + 64);
+      stage_load(sn, 0, nv);
       __builtin_amdgcn_sched_barrier(0);
-      load8(B, pnext + 8 * 256);
+      mma8_refill<0, 4>(c0, c1, B, q0 + 64, q1 + 64, pnext + 8 * 256);
       __builtin_amdgcn_sched_barrier(0);
-      if (t + 1 < nsteps) MIVS_STAGE_STORE((t + 1) & 1, n0, n1, n2, n3);
+      if (stage) stage_store(nb, 0, nv);
+      stage_load(sn, 1, nv);
+      __builtin_amdgcn_sched_barrier(0);
+      mma8_refill<4, 8>(c0, c1, B, q0 + 64, q1 + 64, pnext + 8 * 256);
+      __builtin_amdgcn_sched_barrier(0);
+      if (stage) stage_store(nb, 1, nv);
       __syncthreads();
       if (s == ns - 1) {  // pass p complete: keys -> lane lists
-        const int64_t g = g_begin + p * kPassG + wave;
+        const int64_t g = g_begin + p * W + wave;
         if (g < g_end) {
           const float* gn = s_norm + (g - g_begin) * kGroupRows;
           wepilogue<KCAP, METRIC>(c0, gn, g * kGroupRows, h, qn0, qv0, lk0, lp0);
@@ -258,9 +270,7 @@ __global__ __launch_bounds__(kScanThreads, 1) void k_scan_wide(ScanArgs a) {
       }
     }
 
-#undef MIVS_STAGE_LOAD
-#undef MIVS_STAGE_STORE
-    // ---- merge: two rounds of 32 queries, 16 lane lists (8 waves x 2 halves) per query ----
+    // ---- merge: two rounds of 32 queries, NS lane lists (W waves x 2 halves) per query ----
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       __syncthreads();  // slab buffers / previous round done
@@ -268,15 +278,15 @@ __global__ __launch_bounds__(kScanThreads, 1) void k_scan_wide(ScanArgs a) {
         const int src = wave * 2 + h;
 #pragma unroll
         for (int i = 0; i < KCAP; ++i) {
-          mkey[(j * 16 + src) * KCAP + i] = t == 0 ? lk0[i] : lk1[i];
-          mpos[(j * 16 + src) * KCAP + i] = t == 0 ? lp0[i] : lp1[i];
+          mkey[(j * NS + src) * KCAP + i] = t == 0 ? lk0[i] : lk1[i];
+          mpos[(j * NS + src) * KCAP + i] = t == 0 ? lp0[i] : lp1[i];
         }
       }
       __syncthreads();
-      const int jj = tid >> 4;
-      const int ss = tid & 15;
-      const float* myk = mkey + (jj * 16 + ss) * KCAP;
-      const int* myp = mpos + (jj * 16 + ss) * KCAP;
+      const int jj = tid / NS;
+      const int ss = tid % NS;
+      const float* myk = mkey + (jj * NS + ss) * KCAP;
+      const int* myp = mpos + (jj * NS + ss) * KCAP;
       const int64_t slot = s_slot[t * 32 + jj];
       int head = 0;
       float hk = myk[0];
@@ -285,9 +295,9 @@ __global__ __launch_bounds__(kScanThreads, 1) void k_scan_wide(ScanArgs a) {
         float bk = hk;
         int bp = hp;
 #pragma unroll
-        for (int off = 8; off >= 1; off >>= 1) {
-          const float ok = __shfl_xor(bk, off, 16);
-          const int op = __shfl_xor(bp, off, 16);
+        for (int off = NS / 2; off >= 1; off >>= 1) {
+          const float ok = __shfl_xor(bk, off, NS);
+          const int op = __shfl_xor(bp, off, NS);
           if (ok < bk || (ok == bk && op < bp)) { bk = ok; bp = op; }
         }
         if (ss == 0 && slot >= 0) {
@@ -306,52 +316,64 @@ __global__ __launch_bounds__(kScanThreads, 1) void k_scan_wide(ScanArgs a) {
   }
 }
 
-template <int KCAP, int METRIC>
-hipError_t launch_wm(const ScanArgs& a, int grid, size_t lds, hipStream_t s) {
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_wide<KCAP, METRIC>),
+// waves per K3w workgroup: MIVS_SCAN_WIDE_WAVES (4 or 8), default 4
+int wide_waves() {
+  const char* e = getenv("MIVS_SCAN_WIDE_WAVES");
+  return e && atoi(e) == 8 ? 8 : 4;
+}
+
+template <int KCAP, int METRIC, int W>
+hipError_t launch_wmw(const ScanArgs& a, int grid, size_t lds, hipStream_t s) {
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_wide<KCAP, METRIC, W>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL((k_scan_wide<KCAP, METRIC>), dim3(grid), dim3(kScanThreads), lds, s, a);
+  hipLaunchKernelGGL((k_scan_wide<KCAP, METRIC, W>), dim3(grid), dim3(W * 64), lds, s, a);
   return hipGetLastError();
 }
 
 template <int KCAP>
 hipError_t launch_w(const ScanArgs& a, int grid, size_t lds, hipStream_t s) {
-  return a.metric == kIP ? launch_wm<KCAP, kIP>(a, grid, lds, s) : launch_wm<KCAP, kL2>(a, grid, lds, s);
+  if (wide_waves() == 8)
+    return a.metric == kIP ? launch_wmw<KCAP, kIP, 8>(a, grid, lds, s) : launch_wmw<KCAP, kL2, 8>(a, grid, lds, s);
+  return a.metric == kIP ? launch_wmw<KCAP, kIP, 4>(a, grid, lds, s) : launch_wmw<KCAP, kL2, 4>(a, grid, lds, s);
 }
 
 }  // namespace
 
 size_t scan_wide_lds_bytes(int kcap, int chunk_groups) {
   const size_t slabs = (size_t)2 * kWQ * kSld * 4;
-  const size_t merge = (size_t)32 * 16 * kcap * 8;
+  const size_t merge = (size_t)32 * 2 * wide_waves() * kcap * 8;
   return kWSmall + (size_t)chunk_groups * kGroupRows * 4 + (slabs > merge ? slabs : merge);
 }
 
 bool scan_wide_supported(int kcap, int d, int dp, int chunk_groups) {
-  return (kcap == 1 || kcap == 4 || kcap == 8 || kcap == 16) && d % 4 == 0 && dp % kSlab == 0 &&
+  return (kcap == 1 || kcap == 4 || kcap == 8 || kcap == 12 || kcap == 16) && d % 4 == 0 && dp % kSlab == 0 &&
          scan_wide_lds_bytes(kcap, chunk_groups) <= 160 * 1024;
 }
 
-template <int KCAP, int METRIC>
-static int wocc_km(size_t lds) {
+template <int KCAP, int METRIC, int W>
+static int wocc_kmw(size_t lds) {
   int n = 0;
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_wide<KCAP, METRIC>),
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_wide<KCAP, METRIC, W>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&k_scan_wide<KCAP, METRIC>),
-                                                   kScanThreads, lds) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&k_scan_wide<KCAP, METRIC, W>),
+                                                   W * 64, lds) != hipSuccess)
     return 1;
   return n > 0 ? n : 1;
 }
 
 template <int KCAP>
-static int wocc_k(int metric, size_t lds) { return metric == kIP ? wocc_km<KCAP, kIP>(lds) : wocc_km<KCAP, kL2>(lds); }
+static int wocc_k(int metric, size_t lds) {
+  if (wide_waves() == 8) return metric == kIP ? wocc_kmw<KCAP, kIP, 8>(lds) : wocc_kmw<KCAP, kL2, 8>(lds);
+  return metric == kIP ? wocc_kmw<KCAP, kIP, 4>(lds) : wocc_kmw<KCAP, kL2, 4>(lds);
+}
 
 int scan_wide_occupancy(int kcap, int metric, size_t lds) {
   switch (kcap) {
     case 1: return wocc_k<1>(metric, lds);
     case 4: return wocc_k<4>(metric, lds);
     case 8: return wocc_k<8>(metric, lds);
+    case 12: return wocc_k<12>(metric, lds);
     case 16: return wocc_k<16>(metric, lds);
     default: return 1;
   }
@@ -362,6 +384,7 @@ hipError_t launch_scan_wide(const ScanArgs& a, int kcap, int grid, size_t lds, h
     case 1: return launch_w<1>(a, grid, lds, s);
     case 4: return launch_w<4>(a, grid, lds, s);
     case 8: return launch_w<8>(a, grid, lds, s);
+    case 12: return launch_w<12>(a, grid, lds, s);
     case 16: return launch_w<16>(a, grid, lds, s);
     default: return hipErrorInvalidValue;
   }

@@ -366,11 +366,13 @@ WIDE_CASES = [
 ]
 
 
+@pytest.mark.parametrize("waves", ["4", "8"])
 @pytest.mark.parametrize("n,d,nq,k,metric,n_lists", WIDE_CASES)
-def test_wide_scan_bitexact(mivs_lib, monkeypatch, n, d, nq, k, metric, n_lists):
+def test_wide_scan_bitexact(mivs_lib, monkeypatch, n, d, nq, k, metric, n_lists, waves):
     from mivs.neighbors import brute_force, ivf_flat
 
     monkeypatch.setenv("MIVS_SCAN_WIDE", "1")
+    monkeypatch.setenv("MIVS_SCAN_WIDE_WAVES", waves)
     x = _data(n, d, seed=n + d + 3, normalize=True)
     q = _data(nq, d, seed=n + d + 4, normalize=True)
     if n_lists == 0:

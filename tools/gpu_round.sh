@@ -7,8 +7,8 @@ TAG=${1:-r01}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-export MIVS_SCAN_WIDE=${WIDE:-0}
-if [ "$MIVS_SCAN_WIDE" = "1" ]; then KSUB="k_scan_wide<16, 0>"; KRE='k_scan_wide<16'; T=64; else KSUB="k_scan<16, 0>"; KRE='k_scan<16'; T=32; fi
+export MIVS_SCAN_WIDE=${WIDE:-1}
+if [ "$MIVS_SCAN_WIDE" = "1" ]; then KSUB="k_scan_wide<12, 0, 4>"; KRE='k_scan_wide<12'; T=64; else KSUB="k_scan<12, 0, 8>"; KRE='k_scan<12'; T=32; fi
 if [ "${TESTS:-1}" = "1" ]; then
   timeout -k 10 700 python -m pytest tests -m gpu -x -q > $OUT/tests.log 2>&1
   rc=$?

@@ -47,8 +47,10 @@ def run(n, nq, d=768, reps=3):
 
 if __name__ == "__main__":
     total = 2 ** 33  # rows x queries per case
-    for wide in ("0", "1"):
+    for wide, waves in (("0", "8"), ("1", "8"), ("1", "4")):
         os.environ["MIVS_SCAN_WIDE"] = wide
-        print(f"--- MIVS_SCAN_WIDE={wide} ({'K3w 64-query tiles' if wide == '1' else 'K3 32-query tiles'})", flush=True)
-        for n in [1024, 65536, 1 << 20, 4 << 20]:
+        os.environ["MIVS_SCAN_WIDE_WAVES"] = waves
+        kind = f"K3w 64-query tiles, {waves}-wave workgroups" if wide == "1" else "K3 32-query tiles"
+        print(f"--- MIVS_SCAN_WIDE={wide} MIVS_SCAN_WIDE_WAVES={waves} ({kind})", flush=True)
+        for n in [1024, 1 << 20, 4 << 20]:
             run(n, max(32, total // n))
