@@ -187,12 +187,15 @@ struct Profiler {
 }  // namespace
 
 struct mivs_index_s {
-  int kind = 0;  // 0 = ivf_flat, 1 = brute force
+  int kind = 0;  // 0 = ivf_flat, 1 = brute force, 2 = ivf_pq
   int device = 0, d = 0, dp = 0, metric = 0, G = kDefaultChunkGroups;
   int64_t id_offset = 0;
   ListSet lists;  // data
   ListSet cents;  // IVF: the centroid "list"
   Buf centroids_rm;
+  // IVF-PQ: codes in the interleaved group layout + codebooks (lists.off/goff/ids/h_* describe the lists)
+  int pq_dim = 0, pq_bits = 0, pq_len = 0, pq_dim_pad = 0, rot_dim_pad = 0;
+  Buf pq_codes, pq_books;
   std::mutex mu;
   Workspace ws;
   Profiler prof;
@@ -666,7 +669,7 @@ int32_t mivs_ivf_flat_search(mivs_index_t idx, void* stream, const float* d_q, i
 
 int32_t mivs_ivf_flat_get_centroids(mivs_index_t idx, void* stream, float* d_out) {
   return guarded([&] {
-    require(idx != nullptr && idx->kind == 0, "not an ivf_flat index");
+    require(idx != nullptr && (idx->kind == 0 || idx->kind == 2), "not an IVF index");
     DeviceGuard dg(idx->device);
     HIPCHK(hipMemcpyAsync(d_out, idx->centroids_rm.p, sizeof(float) * (size_t)idx->lists.n_lists * idx->d,
                           hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
@@ -697,6 +700,226 @@ int32_t mivs_ivf_flat_get_list_rows(mivs_index_t idx, void* stream, float* d_out
     const ListSet& L = idx->lists;
     HIPCHK(launch_unpack_rows(L.groups.as<float>(), idx->dp, idx->d, L.off.as<int64_t>(), L.goff.as<int64_t>(),
                               L.n_lists, L.n_rows, d_out, static_cast<hipStream_t>(stream)));
+  });
+}
+
+int32_t mivs_ivf_pq_build(int32_t device, void* stream, const float* d_data, int64_t n, int32_t dim,
+                          const mivs_ivf_pq_params* p, int64_t id_offset, mivs_index_t* out) {
+  return guarded([&] {
+    require(p != nullptr && out != nullptr, "params/out is NULL");
+    check_common(device, d_data, n, dim);
+    require(p->metric == MIVS_METRIC_L2, "ivf_pq: only the L2 metric is supported by this build", MIVS_ERR_UNSUPPORTED);
+    require(p->pq_bits == 8, "ivf_pq: pq_bits must be 8 in this build", MIVS_ERR_UNSUPPORTED);
+    require(p->pq_dim >= 1 && p->pq_dim <= dim, "pq_dim must be in [1, dim]");
+    require(p->n_lists >= 1 && p->n_lists <= 32768, "n_lists must be in [1, 32768]");
+    require(n >= p->n_lists, "n_rows must be >= n_lists");
+    require(p->kmeans_n_iters >= 0, "kmeans_n_iters must be >= 0");
+    require(p->kmeans_trainset_fraction > 0.0 && p->kmeans_trainset_fraction <= 1.0,
+            "kmeans_trainset_fraction must be in (0, 1]");
+    require(p->max_train_points_per_pq_code >= 1, "max_train_points_per_pq_code must be >= 1");
+    const int pl = (dim + p->pq_dim - 1) / p->pq_dim;
+    require(pl <= 64, "pq_len = ceil(dim / pq_dim) must be <= 64", MIVS_ERR_UNSUPPORTED);
+    const int64_t n_pq = std::min<int64_t>(n, p->max_train_points_per_pq_code << p->pq_bits);
+    require(n_pq >= (1 << p->pq_bits), "ivf_pq: need at least 2^pq_bits rows to train the codebooks");
+    DeviceGuard dg(device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    auto idx = std::make_unique<mivs_index_s>();
+    idx->kind = 2;
+    idx->device = device;
+    idx->d = dim;
+    idx->dp = dim_pad(dim);
+    idx->metric = MIVS_METRIC_L2;
+    idx->id_offset = id_offset;
+    idx->pq_dim = p->pq_dim;
+    idx->pq_bits = p->pq_bits;
+    idx->pq_len = pl;
+    idx->pq_dim_pad = (p->pq_dim + 15) / 16 * 16;
+    idx->rot_dim_pad = (p->pq_dim * pl + 3) / 4 * 4;
+    const int nl = p->n_lists;
+    const int nc = 1 << p->pq_bits;
+    // ---- coarse k-means (as ivf_flat: trainset, strided init) ----
+    int64_t nt = (int64_t)((double)n * p->kmeans_trainset_fraction);
+    nt = std::min<int64_t>(std::max<int64_t>(nt, nl), n);
+    Buf rows, init_rows, norms, labels, perm, off, ctmp;
+    rows.reserve(sizeof(int64_t) * nt);
+    HIPCHK(launch_train_rows(rows.as<int64_t>(), n, nt, s));
+    std::vector<int64_t> h_init(nl);
+    for (int j = 0; j < nl; ++j) h_init[j] = ((((int64_t)j * nt) / nl) * n) / nt;
+    init_rows.reserve(sizeof(int64_t) * std::max(nl, nc));
+    HIPCHK(hipMemcpyAsync(init_rows.p, h_init.data(), sizeof(int64_t) * nl, hipMemcpyHostToDevice, s));
+    idx->centroids_rm.reserve(sizeof(float) * (size_t)nl * dim);
+    HIPCHK(launch_gather_rows(d_data, dim, init_rows.as<int64_t>(), nl, idx->centroids_rm.as<float>(), s));
+    norms.reserve(sizeof(float) * n);
+    HIPCHK(launch_row_norms(d_data, n, dim, norms.as<float>(), s));
+    HIPCHK(hipStreamSynchronize(s));
+    kmeans_fit_impl(d_data, norms.as<float>(), rows.as<int64_t>(), nt, dim, idx->dp, nl, p->kmeans_n_iters,
+                    idx->centroids_rm.as<float>(), idx->G, device, idx->ws, s, p->kmeans_balance != 0);
+    make_single_list(idx->cents, idx->centroids_rm.as<float>(), nl, dim, idx->dp, 0, idx->G, s);
+    // ---- lists: L2 assignment of every row, stable order by label ----
+    labels.reserve(sizeof(int64_t) * n);
+    perm.reserve(sizeof(int64_t) * n);
+    off.reserve(sizeof(int64_t) * (nl + 1));
+    assign_rows(d_data, norms.as<float>(), nullptr, n, dim, idx->dp, idx->cents, idx->G, kL2, labels.as<int64_t>(),
+                device, idx->ws, s);
+    const size_t cb = csort_tmp_bytes(n, nl);
+    ctmp.reserve(cb);
+    HIPCHK(launch_counting_sort(labels.as<int64_t>(), n, nl, perm.as<int64_t>(), off.as<int64_t>(), ctmp.p, cb, s));
+    ListSet& L = idx->lists;
+    L.n_lists = nl;
+    L.n_rows = n;
+    L.h_off.assign(nl + 1, 0);
+    HIPCHK(hipMemcpyAsync(L.h_off.data(), off.p, sizeof(int64_t) * (nl + 1), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    L.h_goff.assign(nl + 1, 0);
+    for (int l = 0; l < nl; ++l) L.h_goff[l + 1] = L.h_goff[l] + ceil_div(L.h_off[l + 1] - L.h_off[l], kGroupRows);
+    L.n_groups = L.h_goff.back();
+    L.off.reserve(sizeof(int64_t) * (nl + 1));
+    L.goff.reserve(sizeof(int64_t) * (nl + 1));
+    HIPCHK(hipMemcpyAsync(L.off.p, L.h_off.data(), sizeof(int64_t) * (nl + 1), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(L.goff.p, L.h_goff.data(), sizeof(int64_t) * (nl + 1), hipMemcpyHostToDevice, s));
+    L.finalize_host(idx->G);
+    // ---- codebooks: per subspace k-means on residual sub-vectors of a strided trainset ----
+    Buf prow, resid, rnorm;
+    prow.reserve(sizeof(int64_t) * n_pq);
+    HIPCHK(launch_train_rows(prow.as<int64_t>(), n, n_pq, s));
+    resid.reserve(sizeof(float) * (size_t)p->pq_dim * n_pq * pl);
+    HIPCHK(launch_pq_residuals(d_data, dim, prow.as<int64_t>(), n_pq, labels.as<int64_t>(),
+                               idx->centroids_rm.as<float>(), p->pq_dim, pl, resid.as<float>(), s));
+    std::vector<int64_t> h_cinit(nc);
+    for (int c = 0; c < nc; ++c) h_cinit[c] = ((int64_t)c * n_pq) / nc;
+    HIPCHK(hipMemcpyAsync(init_rows.p, h_cinit.data(), sizeof(int64_t) * nc, hipMemcpyHostToDevice, s));
+    idx->pq_books.reserve(sizeof(float) * (size_t)p->pq_dim * nc * pl);
+    rnorm.reserve(sizeof(float) * n_pq);
+    for (int j = 0; j < p->pq_dim; ++j) {
+      const float* rj = resid.as<float>() + (size_t)j * n_pq * pl;
+      float* bj = idx->pq_books.as<float>() + (size_t)j * nc * pl;
+      HIPCHK(launch_gather_rows(rj, pl, init_rows.as<int64_t>(), nc, bj, s));
+      HIPCHK(launch_row_norms(rj, n_pq, pl, rnorm.as<float>(), s));
+      kmeans_fit_impl(rj, rnorm.as<float>(), nullptr, n_pq, pl, dim_pad(pl), nc, p->kmeans_n_iters, bj, idx->G,
+                      device, idx->ws, s, p->kmeans_balance != 0);
+    }
+    // ---- encode + ids into the interleaved layout ----
+    const int64_t slots = std::max<int64_t>(L.n_groups, 1) * kGroupRows;
+    idx->pq_codes.reserve((size_t)slots * idx->pq_dim_pad);
+    HIPCHK(hipMemsetAsync(idx->pq_codes.p, 0, (size_t)slots * idx->pq_dim_pad, s));
+    L.ids.reserve(sizeof(int64_t) * slots);
+    HIPCHK(hipMemsetAsync(L.ids.p, 0xFF, sizeof(int64_t) * slots, s));
+    if (p->add_data_on_build) {
+      HIPCHK(launch_pq_encode(d_data, dim, perm.as<int64_t>(), n, L.off.as<int64_t>(), L.goff.as<int64_t>(), nl,
+                              idx->centroids_rm.as<float>(), idx->pq_books.as<float>(), p->pq_dim, pl,
+                              idx->pq_dim_pad, static_cast<uint8_t*>(idx->pq_codes.p), s));
+      HIPCHK(launch_pq_ids(perm.as<int64_t>(), n, L.off.as<int64_t>(), L.goff.as<int64_t>(), nl, id_offset,
+                           L.ids.as<int64_t>(), s));
+    } else {
+      L.n_rows = 0;
+      std::fill(L.h_off.begin(), L.h_off.end(), 0);
+      std::fill(L.h_goff.begin(), L.h_goff.end(), 0);
+      L.n_groups = 0;
+      HIPCHK(hipMemcpyAsync(L.off.p, L.h_off.data(), sizeof(int64_t) * (nl + 1), hipMemcpyHostToDevice, s));
+      HIPCHK(hipMemcpyAsync(L.goff.p, L.h_goff.data(), sizeof(int64_t) * (nl + 1), hipMemcpyHostToDevice, s));
+      L.finalize_host(idx->G);
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    *out = idx.release();
+  });
+}
+
+int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int64_t nq, int32_t k,
+                           int32_t n_probes, float* d_dist, int64_t* d_ids, int32_t* d_probes) {
+  return guarded([&] {
+    require(idx != nullptr && idx->kind == 2, "not an ivf_pq index");
+    require(nq >= 0, "nq must be >= 0");
+    require(k >= 1 && k <= 32, "ivf_pq: k must be in [1, 32] in this build", MIVS_ERR_UNSUPPORTED);
+    require(n_probes >= 1, "n_probes must be >= 1");
+    require(nq == 0 || (d_q && d_dist && d_ids), "NULL query/output pointer");
+    if (nq == 0) return;
+    std::lock_guard<std::mutex> g(idx->mu);
+    DeviceGuard dg(idx->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int np = std::min<int>(n_probes, idx->lists.n_lists);
+    require(np <= kMaxSelectK, "n_probes must be <= " + std::to_string(kMaxSelectK), MIVS_ERR_UNSUPPORTED);
+    require(np == n_probes || d_probes == nullptr, "n_probes > n_lists with a probes output");
+    const int kcap = scan_kcap(k);
+    require(pq_scan_lds_bytes(idx->rot_dim_pad, idx->pq_dim, kcap) <= 160 * 1024,
+            "ivf_pq: pq_dim x 256 LUT + merge area exceed the 160 KB LDS", MIVS_ERR_UNSUPPORTED);
+    Workspace& ws = idx->ws;
+    ProfRec* pr = g_profiling.load() ? idx->prof.begin(s) : nullptr;
+    ws.qn.reserve(sizeof(float) * nq);
+    HIPCHK(launch_row_norms(d_q, nq, idx->d, ws.qn.as<float>(), s));
+    ws.probes_d.reserve(sizeof(float) * nq * np);
+    ws.probes_i.reserve(sizeof(int64_t) * nq * np);
+    single_list_topk(idx->cents, idx->G, d_q, ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, np, kL2,
+                     ws.probes_d.as<float>(), ws.probes_i.as<int64_t>(), idx->device, ws, s);
+    if (d_probes) HIPCHK(launch_i64_to_i32(ws.probes_i.as<int64_t>(), nq * np, d_probes, s));
+    ws.part_d.reserve(sizeof(float) * (size_t)(nq * np * k));
+    ws.part_i.reserve(sizeof(int64_t) * (size_t)(nq * np * k));
+    PqScanArgs a{};
+    a.queries = d_q;
+    a.cents = idx->centroids_rm.as<float>();
+    a.books = idx->pq_books.as<float>();
+    a.codes = static_cast<const uint8_t*>(idx->pq_codes.p);
+    a.row_ids = idx->lists.ids.as<int64_t>();
+    a.list_off = idx->lists.off.as<int64_t>();
+    a.list_goff = idx->lists.goff.as<int64_t>();
+    a.probes = ws.probes_i.as<int64_t>();
+    a.n_slots = nq * np;
+    a.n_probes = np;
+    a.d = idx->d;
+    a.rot_dim_pad = idx->rot_dim_pad;
+    a.pq_dim = idx->pq_dim;
+    a.pq_dim_pad = idx->pq_dim_pad;
+    a.pq_len = idx->pq_len;
+    a.k = k;
+    a.out_d = ws.part_d.as<float>();
+    a.out_i = ws.part_i.as<int64_t>();
+    if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
+    HIPCHK(launch_pq_scan(a, kcap, s));
+    if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
+    MergeArgs m{};
+    m.in_d = ws.part_d.as<float>();
+    m.in_i = ws.part_i.as<int64_t>();
+    m.slot_begin = nullptr;
+    m.slots_per_q = np;
+    m.nq = nq;
+    m.k_in = k;
+    m.k = k;
+    m.metric = kL2;
+    m.out_d = d_dist;
+    m.out_i = d_ids;
+    HIPCHK(launch_merge(m, s));
+    if (pr) HIPCHK(hipEventRecord(pr->e[3], s));
+    idx->last_nq = nq;
+    idx->last_np = np;
+    idx->last_k = k;
+  });
+}
+
+int32_t mivs_ivf_pq_info(mivs_index_t idx, int32_t* pq_dim, int32_t* pq_bits, int32_t* pq_len) {
+  return guarded([&] {
+    require(idx != nullptr && idx->kind == 2, "not an ivf_pq index");
+    if (pq_dim) *pq_dim = idx->pq_dim;
+    if (pq_bits) *pq_bits = idx->pq_bits;
+    if (pq_len) *pq_len = idx->pq_len;
+  });
+}
+
+int32_t mivs_ivf_pq_get_codebooks(mivs_index_t idx, void* stream, float* d_out) {
+  return guarded([&] {
+    require(idx != nullptr && idx->kind == 2, "not an ivf_pq index");
+    DeviceGuard dg(idx->device);
+    HIPCHK(hipMemcpyAsync(d_out, idx->pq_books.p, sizeof(float) * (size_t)idx->pq_dim * (1 << idx->pq_bits) * idx->pq_len,
+                          hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
+  });
+}
+
+int32_t mivs_ivf_pq_get_codes(mivs_index_t idx, void* stream, uint8_t* d_out) {
+  return guarded([&] {
+    require(idx != nullptr && idx->kind == 2, "not an ivf_pq index");
+    DeviceGuard dg(idx->device);
+    const ListSet& L = idx->lists;
+    HIPCHK(launch_pq_unpack(static_cast<const uint8_t*>(idx->pq_codes.p), L.n_rows, L.off.as<int64_t>(),
+                            L.goff.as<int64_t>(), L.n_lists, idx->pq_dim, idx->pq_dim_pad, d_out,
+                            static_cast<hipStream_t>(stream)));
   });
 }
 

@@ -92,6 +92,22 @@ struct MergeArgs {
   int64_t* out_i;
 };
 
+// IVF-PQ scan job (K9, pq.hip): one workgroup per (query, probe) slot = q * n_probes + p.
+struct PqScanArgs {
+  const float* queries;        // [nq][d]
+  const float* cents;          // [n_lists][d] row-major
+  const float* books;          // [pq_dim][256][pq_len]
+  const uint8_t* codes;        // interleaved groups [g][pq_dim_pad/16][32][16]
+  const int64_t* row_ids;      // [groups*32]
+  const int64_t* list_off;     // [n_lists+1] rows
+  const int64_t* list_goff;    // [n_lists+1] groups
+  const int64_t* probes;       // [nq][n_probes] list ids
+  int64_t n_slots;             // nq * n_probes
+  int n_probes, d, rot_dim_pad, pq_dim, pq_dim_pad, pq_len, k;
+  float* out_d;                // [n_slots][k]
+  int64_t* out_i;
+};
+
 // ---- host-side launchers (implemented in the .hip files) ----
 hipError_t launch_scan(const ScanArgs& a, int kcap, int grid, size_t lds_bytes, hipStream_t s);
 hipError_t launch_scan_ex(const ScanArgs& a, int kcap, int grid, size_t lds_bytes, float* gmerge, hipStream_t s);
@@ -147,6 +163,19 @@ constexpr int kBalanceKeepLast = 2;  // last k-means iterations without re-seedi
 hipError_t launch_km_rebalance(const float* x, int d, const int64_t* rows, const int64_t* labels,
                                const int64_t* list_off, int nc, int64_t n_train, int it, float* centroids,
                                hipStream_t s);
+
+// IVF-PQ (pq.hip)
+size_t pq_scan_lds_bytes(int rot_dim_pad, int pq_dim, int kcap);
+hipError_t launch_pq_residuals(const float* x, int d, const int64_t* rows, int64_t nt, const int64_t* labels,
+                               const float* cents, int pq_dim, int pl, float* out, hipStream_t s);
+hipError_t launch_pq_encode(const float* x, int d, const int64_t* perm, int64_t n, const int64_t* list_off,
+                            const int64_t* list_goff, int n_lists, const float* cents, const float* books, int pq_dim,
+                            int pl, int pq_dim_pad, uint8_t* codes, hipStream_t s);
+hipError_t launch_pq_ids(const int64_t* perm, int64_t n, const int64_t* list_off, const int64_t* list_goff,
+                         int n_lists, int64_t id_offset, int64_t* ids, hipStream_t s);
+hipError_t launch_pq_unpack(const uint8_t* codes, int64_t n, const int64_t* list_off, const int64_t* list_goff,
+                            int n_lists, int pq_dim, int pq_dim_pad, uint8_t* out, hipStream_t s);
+hipError_t launch_pq_scan(const PqScanArgs& a, int kcap, hipStream_t s);
 
 hipError_t launch_gather_rows(const float* src, int d, const int64_t* rows, int64_t n, float* dst, hipStream_t s);
 hipError_t launch_unpack_rows(const float* groups, int dp, int d, const int64_t* list_off, const int64_t* list_goff,

@@ -122,7 +122,7 @@ class ParallelIndexBuilder:
 
     def build_index_on_gpu(self, gpu_config: GPUConfig, embeddings: torch.Tensor, index_type: IndexType,
                            params: Dict, ids_offset: int = 0) -> Tuple[Any, float]:
-        from mivs.neighbors import brute_force, ivf_flat
+        from mivs.neighbors import brute_force, ivf_flat, ivf_pq
 
         t0 = time.time()
         with CUDAMemoryManager.managed_allocation(gpu_config, f"building {index_type.value} index"):
@@ -138,7 +138,15 @@ class ParallelIndexBuilder:
             elif index_type in (IndexType.BRUTE_FORCE, IndexType.FAISS_FLAT):
                 index = brute_force.build(embeddings, metric=params.get("metric", "sqeuclidean"),
                                           ids_offset=ids_offset)
-            elif index_type in (IndexType.IVF_PQ, IndexType.CAGRA, IndexType.FAISS_IVF):
+            elif index_type == IndexType.IVF_PQ:
+                # reference :131-137: n_lists min(512, N // 500 + 1), pq_dim 96, pq_bits 8
+                n_lists = params.get("n_lists", min(512, embeddings.shape[0] // 500 + 1))
+                extra = {k: params[k] for k in ("kmeans_n_iters", "kmeans_trainset_fraction",
+                                                "max_train_points_per_pq_code") if k in params}
+                index = ivf_pq.build(ivf_pq.IndexParams(n_lists=n_lists, pq_dim=params.get("pq_dim", 96),
+                                                        pq_bits=params.get("pq_bits", 8), **extra),
+                                     embeddings, ids_offset=ids_offset)
+            elif index_type in (IndexType.CAGRA, IndexType.FAISS_IVF):
                 raise NotImplementedError(f"{index_type.value} is not implemented in mivs yet")
             else:
                 raise ValueError(f"Unsupported index type: {index_type}")
@@ -183,7 +191,7 @@ class ParallelSearchEngine:
 
     def search_on_gpu(self, gpu_id: int, index: Any, query: torch.Tensor, k: int):
         """-> (distances, neighbors) device tensors [Q, k] for this shard (global ids)."""
-        from mivs.neighbors import brute_force, ivf_flat
+        from mivs.neighbors import brute_force, ivf_flat, ivf_pq
 
         torch.cuda.set_device(gpu_id)
         if not query.is_cuda or query.device.index != gpu_id:
@@ -194,6 +202,8 @@ class ParallelSearchEngine:
         try:
             if isinstance(index, ivf_flat.Index):
                 d, i = ivf_flat.search(ivf_flat.SearchParams(n_probes=self.search_config.n_probes), index, query, k)
+            elif isinstance(index, ivf_pq.Index):
+                d, i = ivf_pq.search(ivf_pq.SearchParams(n_probes=self.search_config.n_probes), index, query, k)
             elif isinstance(index, brute_force.Index):
                 d, i = brute_force.search(index, query, k)
             else:

@@ -35,6 +35,8 @@ CUVS_AVAILABLE = engine_available()
 VALID_INDEX_TYPES = ["ivf_flat", "ivf_pq", "cagra", "brute_force"]
 _IVF_FLAT_KEYS = ("metric", "kmeans_n_iters", "kmeans_trainset_fraction", "kmeans_max_train_per_list", "kmeans_balance",
                   "add_data_on_build", "chunk_rows")
+_IVF_PQ_KEYS = ("metric", "kmeans_n_iters", "kmeans_trainset_fraction", "max_train_points_per_pq_code",
+                "kmeans_balance", "add_data_on_build")
 
 
 @dataclass
@@ -210,7 +212,7 @@ class IndexBuildingCoordinator:
             logger.warning("mivs engine not available, simulating index build")
             time.sleep(0.1)
             return {"type": config.index_type, "size": embeddings.shape[0], "dim": embeddings.shape[1]}
-        from mivs.neighbors import brute_force, ivf_flat
+        from mivs.neighbors import brute_force, ivf_flat, ivf_pq
 
         p = config.index_params
         try:
@@ -221,9 +223,17 @@ class IndexBuildingCoordinator:
                                       ids_offset=id_offset)
             if config.index_type == "brute_force":
                 return brute_force.build(embeddings, metric=p.get("metric", "sqeuclidean"), ids_offset=id_offset)
-            if config.index_type in ("ivf_pq", "cagra"):
-                raise NotImplementedError(f"{config.index_type} is not implemented in mivs yet "
-                                          "(ivf_flat and brute_force are; SURVEY.md §8(f))")
+            if config.index_type == "ivf_pq":
+                # reference :398-404: n_lists default as ivf_flat, pq_bits 8, pq_dim min(64, d // 4)
+                n_lists = p.get("n_lists", ivf_flat.default_n_lists(embeddings.shape[0]))
+                pq_bits = p.get("pq_bits", 8)
+                pq_dim = p.get("pq_dim", ivf_pq.default_pq_dim(embeddings.shape[1]))
+                extra = {k: p[k] for k in _IVF_PQ_KEYS if k in p}
+                return ivf_pq.build(ivf_pq.IndexParams(n_lists=n_lists, pq_bits=pq_bits, pq_dim=pq_dim, **extra),
+                                    embeddings, ids_offset=id_offset)
+            if config.index_type == "cagra":
+                raise NotImplementedError("cagra is not implemented in mivs (ivf_flat, ivf_pq and brute_force are; "
+                                          "SURVEY.md §8(f))")
             raise ValueError(f"Unsupported index type: {config.index_type}")
         except Exception as e:
             raise RuntimeError(f"Failed to create {config.index_type} index: {e}") from e
@@ -249,7 +259,7 @@ class IndexBuildingCoordinator:
     @staticmethod
     def _self_query_ok(index: Any, embeddings: torch.Tensor) -> bool:
         """A stored row queried against its own index must come back at distance 0 (L2 indices)."""
-        from mivs.neighbors import brute_force, ivf_flat
+        from mivs.neighbors import brute_force, ivf_flat, ivf_pq
 
         if getattr(index, "metric", "sqeuclidean") not in ("sqeuclidean", "l2", "L2Expanded"):
             return len(index) == embeddings.shape[0]
@@ -257,6 +267,11 @@ class IndexBuildingCoordinator:
         if n == 0 or len(index) != n:
             return len(index) == n
         probe = embeddings[[0, n // 2, n - 1]]
+        if isinstance(index, ivf_pq.Index):
+            # PQ distances are approximate: the probe rows must come back with valid neighbours
+            _, i = ivf_pq.search(ivf_pq.SearchParams(n_probes=min(4, index.n_lists)), index, probe, 1)
+            i = i.tensor if hasattr(i, "tensor") else i
+            return bool((torch.as_tensor(i).reshape(-1).cpu() >= 0).all())
         if isinstance(index, ivf_flat.Index):
             d, _ = ivf_flat.search(ivf_flat.SearchParams(n_probes=1), index, probe, 1)
         else:

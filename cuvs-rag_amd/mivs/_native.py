@@ -55,6 +55,21 @@ class IvfFlatParams(ctypes.Structure):
     ]
 
 
+class IvfPqParams(ctypes.Structure):
+    """include/mivs.h mivs_ivf_pq_params."""
+    _fields_ = [
+        ("n_lists", c_int32),
+        ("metric", c_int32),
+        ("kmeans_n_iters", c_int32),
+        ("kmeans_trainset_fraction", c_double),
+        ("pq_dim", c_int32),
+        ("pq_bits", c_int32),
+        ("max_train_points_per_pq_code", c_int64),
+        ("kmeans_balance", c_int32),
+        ("add_data_on_build", c_int32),
+    ]
+
+
 class SearchStats(ctypes.Structure):
     _fields_ = [
         ("n_queries", c_int64),
@@ -99,6 +114,13 @@ _SIGS = {
     "mivs_ivf_flat_get_list_sizes": (c_int32, [c_void_p, c_void_p]),
     "mivs_ivf_flat_get_list_ids": (c_int32, [c_void_p, c_void_p, c_void_p]),
     "mivs_ivf_flat_get_list_rows": (c_int32, [c_void_p, c_void_p, c_void_p]),
+    "mivs_ivf_pq_build": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int32, POINTER(IvfPqParams), c_int64,
+                                    POINTER(c_void_p)]),
+    "mivs_ivf_pq_search": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p,
+                                     c_void_p]),
+    "mivs_ivf_pq_info": (c_int32, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
+    "mivs_ivf_pq_get_codebooks": (c_int32, [c_void_p, c_void_p, c_void_p]),
+    "mivs_ivf_pq_get_codes": (c_int32, [c_void_p, c_void_p, c_void_p]),
     "mivs_brute_force_build": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int64,
                                          POINTER(c_void_p)]),
     "mivs_brute_force_search": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),

@@ -1,8 +1,8 @@
-"""mivs.neighbors — the ``cuvs.neighbors`` modules the reference imports (ivf_flat, brute_force).
+"""mivs.neighbors — the ``cuvs.neighbors`` modules the reference imports (ivf_flat, ivf_pq, brute_force).
 
-``ivf_pq`` and ``cagra`` are named by the reference (index_building_coordinator.py:398-414) but are
-outside this round's hot path; importing them raises a clear error.
+``cagra`` is named by the reference (index_building_coordinator.py:405-412) but is outside the
+hot path.
 """
-from . import brute_force, ivf_flat  # noqa: F401
+from . import brute_force, ivf_flat, ivf_pq  # noqa: F401
 
-__all__ = ["ivf_flat", "brute_force"]
+__all__ = ["ivf_flat", "ivf_pq", "brute_force"]

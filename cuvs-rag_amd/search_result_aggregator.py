@@ -201,7 +201,7 @@ class SearchResultAggregator:
         if not CUVS_AVAILABLE:
             d, i = self._simulate_search(query, config.k)
             return d, i, time.time() - t0
-        from mivs.neighbors import brute_force, ivf_flat
+        from mivs.neighbors import brute_force, ivf_flat, ivf_pq
 
         device = self.gpu_manager.get_safe_device_string(gpu_id)
         with torch.cuda.device(gpu_id):
@@ -210,6 +210,9 @@ class SearchResultAggregator:
             if isinstance(index, ivf_flat.Index):
                 sp = ivf_flat.SearchParams(n_probes=int(params.get("nprobe", params.get("n_probes", 20))))
                 d, i = ivf_flat.search(sp, index, q, config.k)
+            elif isinstance(index, ivf_pq.Index):
+                sp = ivf_pq.SearchParams(n_probes=int(params.get("nprobe", params.get("n_probes", 20))))
+                d, i = ivf_pq.search(sp, index, q, config.k)
             elif isinstance(index, brute_force.Index):
                 d, i = brute_force.search(index, q, config.k)
             else:

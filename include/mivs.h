@@ -53,6 +53,20 @@ typedef struct {
                                        balanced k-means); 0: plain Lloyd */
 } mivs_ivf_flat_params;
 
+/* cuvs.neighbors.ivf_pq.IndexParams (index_building_coordinator.py:398-404: n_lists, pq_bits=8,
+ * pq_dim=min(64, d // 4); improved_multi_gpu_rag.py:131-137: pq_dim=96, pq_bits=8) */
+typedef struct {
+  int32_t n_lists;
+  int32_t metric;                   /* MIVS_METRIC_L2 (this build) */
+  int32_t kmeans_n_iters;           /* coarse and codebook k-means iterations (cuVS default 20) */
+  double kmeans_trainset_fraction;  /* coarse trainset fraction (cuVS default 0.5) */
+  int32_t pq_dim;                   /* sub-quantizers; pq_len = ceil(dim / pq_dim) dims each */
+  int32_t pq_bits;                  /* 8 (256-entry codebooks) in this build */
+  int64_t max_train_points_per_pq_code; /* codebook trainset = min(n, this * 2^pq_bits) rows (cuVS 256) */
+  int32_t kmeans_balance;
+  int32_t add_data_on_build;        /* 1: encode the dataset during build */
+} mivs_ivf_pq_params;
+
 /* what the last search on an index did (algorithmic counts for the bench roofline) */
 typedef struct {
   int64_t n_queries;
@@ -112,6 +126,20 @@ int32_t mivs_index_info(mivs_index_t index, int64_t* n_rows, int32_t* dim, int32
 int32_t mivs_index_last_search_stats(mivs_index_t index, mivs_search_stats* out);
 int32_t mivs_index_profile_collect(mivs_index_t index, mivs_profile* out);
 void mivs_index_free(mivs_index_t index);
+
+/* ---- IVF-PQ: replaces ivf_pq.build (index_building_coordinator.py:404, improved_multi_gpu_rag.py:137)
+ * and ivf_pq.search (improved_multi_gpu_rag.py:228-230). L2, pq_bits 8, k <= 32. Codes live on the
+ * device (pq_dim bytes per row); the dataset is only read during build. */
+int32_t mivs_ivf_pq_build(int32_t device, void* stream, const float* d_data, int64_t n, int32_t dim,
+                          const mivs_ivf_pq_params* params, int64_t id_offset, mivs_index_t* out);
+int32_t mivs_ivf_pq_search(mivs_index_t index, void* stream, const float* d_queries, int64_t n_queries, int32_t k,
+                           int32_t n_probes, float* d_distances, int64_t* d_neighbors, int32_t* d_probes);
+/* pq_dim, pq_bits, pq_len of an IVF-PQ index */
+int32_t mivs_ivf_pq_info(mivs_index_t index, int32_t* pq_dim, int32_t* pq_bits, int32_t* pq_len);
+/* d_out: [pq_dim][2^pq_bits][pq_len] fp32 codebooks */
+int32_t mivs_ivf_pq_get_codebooks(mivs_index_t index, void* stream, float* d_out);
+/* d_out: [n_rows][pq_dim] uint8 codes in list order (row t belongs to mivs_ivf_flat_get_list_ids()[t]) */
+int32_t mivs_ivf_pq_get_codes(mivs_index_t index, void* stream, uint8_t* d_out);
 
 /* ---- k-means (the trainer inside ivf_flat::build; cuvs.cluster.kmeans) ----
  * d_rows: optional [n_train] int64 row ids of the trainset (NULL: rows 0..n_train-1).

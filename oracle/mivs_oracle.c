@@ -365,3 +365,172 @@ void orc_ivf_search(const float* x, int64_t id_offset, int d, const float* centr
   free(offs);
   free(cn);
 }
+
+/* ======================================================================================
+ * IVF-PQ — cuVS ivf_pq (cuvs 25.6.0) as the reference reaches it:
+ *   index_building_coordinator.py:398-404  ivf_pq.IndexParams(n_lists, pq_bits=8,
+ *                                           pq_dim=min(64, d // 4)); ivf_pq.build
+ *   improved_multi_gpu_rag.py:131-137,228-230  pq_dim=96, pq_bits=8; ivf_pq.search
+ * Published algorithm restated (no reference fixture pins PQ numerics: parity unpinned beyond
+ * the pinned Lloyd k-means it is built from):
+ *   coarse k-means on the trainset (as IVF-Flat) -> lists by L2 assignment;
+ *   rot_dim = pq_dim * pq_len, pq_len = ceil(d / pq_dim); identity rotation, dims >= d read 0;
+ *   per subspace j a 2^pq_bits-entry codebook = k-means on the residual sub-vectors
+ *   (x - c_label)[j*pq_len, (j+1)*pq_len) of min(n, max_per_code * 2^pq_bits) strided rows;
+ *   code_j(x) = argmin_c ||r_j - B_j[c]||^2 (ties: lowest c);
+ *   search: per probed list l, LUT_j[c] = ||(q - c_l)_j - B_j[c]||^2 and
+ *   dist(x) = sum_j LUT_j[code_j(x)] (j ascending, fp32); top-k by (dist, id) over all probes.
+ * Pinned order: ||a - b||^2 over pq_len dims = acc = fmaf(a_i - b_i, a_i - b_i, acc), i ascending.
+ * ====================================================================================== */
+int orc_pq_len(int d, int pq_dim) { return (d + pq_dim - 1) / pq_dim; }
+
+int64_t orc_pq_train_count(int64_t n, int pq_bits, int64_t max_per_code) {
+  const int64_t cap = max_per_code << pq_bits;
+  return n < cap ? n : cap;
+}
+
+float orc_pq_l2(const float* a, const float* b, int pl) {
+  float acc = 0.0f;
+  for (int i = 0; i < pl; ++i) {
+    const float t = a[i] - b[i];
+    acc = fmaf(t, t, acc);
+  }
+  return acc;
+}
+
+/* residual sub-vector j (pq_len dims) of row x w.r.t. centre c; dims >= d are 0 */
+static void pq_residual(const float* x, const float* c, int d, int j, int pl, float* out) {
+  for (int i = 0; i < pl; ++i) {
+    const int k = j * pl + i;
+    out[i] = k < d ? x[k] - c[k] : 0.0f;
+  }
+}
+
+void orc_ivfpq_train_codebooks(const float* x, int64_t n, int d, const float* centroids, const int32_t* labels,
+                               int pq_dim, int pq_bits, int iters, int balance, int64_t max_per_code,
+                               float* codebooks /* [pq_dim][2^pq_bits][pq_len] */) {
+  const int pl = orc_pq_len(d, pq_dim);
+  const int nc = 1 << pq_bits;
+  const int64_t nt = orc_pq_train_count(n, pq_bits, max_per_code);
+  int64_t* rows = (int64_t*)malloc(sizeof(int64_t) * (size_t)nt);
+  orc_train_rows(n, nt, rows);
+  int64_t* which = (int64_t*)malloc(sizeof(int64_t) * (size_t)nc);
+  orc_init_rows(nt, nc, which);
+  float* r = (float*)malloc(sizeof(float) * (size_t)nt * pl);
+  for (int j = 0; j < pq_dim; ++j) {
+    for (int64_t t = 0; t < nt; ++t)
+      pq_residual(x + rows[t] * (int64_t)d, centroids + (int64_t)labels[rows[t]] * d, d, j, pl, r + t * pl);
+    float* cb = codebooks + (int64_t)j * nc * pl;
+    for (int c = 0; c < nc; ++c) memcpy(cb + (int64_t)c * pl, r + which[c] * pl, sizeof(float) * (size_t)pl);
+    orc_kmeans_fit_ex(r, NULL, nt, nc, pl, iters, ORC_L2, balance, cb);
+  }
+  free(r);
+  free(which);
+  free(rows);
+}
+
+void orc_ivfpq_encode(const float* x, const int64_t* rows, int64_t nr, int d, const float* centroids,
+                      const int32_t* labels /* per row of x */, const float* codebooks, int pq_dim, int pq_bits,
+                      uint8_t* codes /* [nr][pq_dim] */) {
+  const int pl = orc_pq_len(d, pq_dim);
+  const int nc = 1 << pq_bits;
+#pragma omp parallel
+  {
+    float* r = (float*)malloc(sizeof(float) * (size_t)pl);
+#pragma omp for
+    for (int64_t t = 0; t < nr; ++t) {
+      const int64_t row = rows ? rows[t] : t;
+      for (int j = 0; j < pq_dim; ++j) {
+        pq_residual(x + row * (int64_t)d, centroids + (int64_t)labels[row] * d, d, j, pl, r);
+        const float* cb = codebooks + (int64_t)j * nc * pl;
+        int best = 0;
+        float bd = orc_pq_l2(r, cb, pl);
+        for (int c = 1; c < nc; ++c) {
+          const float v = orc_pq_l2(r, cb + (int64_t)c * pl, pl);
+          if (v < bd) { bd = v; best = c; }
+        }
+        codes[t * pq_dim + j] = (uint8_t)best;
+      }
+    }
+    free(r);
+  }
+}
+
+void orc_ivfpq_build(const float* x, int64_t n, int d, int n_lists, int iters, double fraction, int pq_dim,
+                     int pq_bits, int64_t max_per_code, int balance, int64_t id_offset, float* centroids,
+                     float* codebooks, int64_t* list_sizes, int64_t* list_ids, uint8_t* codes) {
+  const int64_t nt = orc_train_count(n, n_lists, fraction, 0);
+  int64_t* rows = (int64_t*)malloc(sizeof(int64_t) * (size_t)nt);
+  int64_t* which = (int64_t*)malloc(sizeof(int64_t) * (size_t)n_lists);
+  orc_train_rows(n, nt, rows);
+  orc_init_rows(nt, n_lists, which);
+  for (int j = 0; j < n_lists; ++j)
+    memcpy(centroids + (int64_t)j * d, x + rows[which[j]] * (int64_t)d, sizeof(float) * (size_t)d);
+  orc_kmeans_fit_ex(x, rows, nt, n_lists, d, iters, ORC_L2, balance, centroids);
+  int32_t* labels = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+  orc_kmeans_assign(x, NULL, n, centroids, n_lists, d, ORC_L2, labels);
+  orc_ivfpq_train_codebooks(x, n, d, centroids, labels, pq_dim, pq_bits, iters, balance, max_per_code, codebooks);
+  int64_t* order = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+  int64_t* offs = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n_lists + 1));
+  stable_by_label(labels, n, n_lists, order, offs);
+  for (int j = 0; j < n_lists; ++j) list_sizes[j] = offs[j + 1] - offs[j];
+  for (int64_t t = 0; t < n; ++t) list_ids[t] = order[t] + id_offset;
+  orc_ivfpq_encode(x, order, n, d, centroids, labels, codebooks, pq_dim, pq_bits, codes);
+  free(offs);
+  free(order);
+  free(labels);
+  free(rows);
+  free(which);
+}
+
+void orc_ivfpq_search(const float* centroids, int n_lists, int d, const float* codebooks, int pq_dim, int pq_bits,
+                      const int64_t* list_sizes, const int64_t* list_ids, const uint8_t* codes, const float* q,
+                      int64_t nq, int n_probes, int k, float* out_d, int64_t* out_i, int32_t* out_probes) {
+  if (n_probes > n_lists) n_probes = n_lists;
+  const int pl = orc_pq_len(d, pq_dim);
+  const int nc = 1 << pq_bits;
+  int64_t* offs = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n_lists + 1));
+  offs[0] = 0;
+  for (int j = 0; j < n_lists; ++j) offs[j + 1] = offs[j] + list_sizes[j];
+  float* cn = (float*)malloc(sizeof(float) * (size_t)n_lists);
+  orc_norms(centroids, n_lists, d, cn);
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int64_t qi = 0; qi < nq; ++qi) {
+    const float* qq = q + qi * d;
+    const float qn = orc_dot(qq, qq, d);
+    kv_t* ph = (kv_t*)malloc(sizeof(kv_t) * (size_t)n_probes);
+    int psz = 0;
+    for (int j = 0; j < n_lists; ++j) {
+      kv_t v = {orc_key(orc_dot(centroids + (int64_t)j * d, qq, d), cn[j], qn, ORC_L2), j};
+      heap_push(ph, &psz, n_probes, v);
+    }
+    qsort(ph, (size_t)psz, sizeof(kv_t), kv_cmp);
+    float* lut = (float*)malloc(sizeof(float) * (size_t)pq_dim * nc);
+    float* r = (float*)malloc(sizeof(float) * (size_t)pl);
+    kv_t* h = (kv_t*)malloc(sizeof(kv_t) * (size_t)(k > 0 ? k : 1));
+    int sz = 0;
+    for (int p = 0; p < psz; ++p) {
+      const int l = (int)ph[p].id;
+      if (out_probes) out_probes[qi * n_probes + p] = l;
+      for (int j = 0; j < pq_dim; ++j) {
+        pq_residual(qq, centroids + (int64_t)l * d, d, j, pl, r);
+        for (int c = 0; c < nc; ++c)
+          lut[j * nc + c] = orc_pq_l2(r, codebooks + ((int64_t)j * nc + c) * pl, pl);
+      }
+      for (int64_t m = offs[l]; m < offs[l + 1]; ++m) {
+        const uint8_t* cd = codes + m * pq_dim;
+        float dist = 0.0f;
+        for (int j = 0; j < pq_dim; ++j) dist = dist + lut[j * nc + cd[j]];
+        kv_t v = {dist, list_ids[m]};
+        heap_push(h, &sz, k, v);
+      }
+    }
+    heap_emit(h, sz, k, ORC_L2, out_d + qi * k, out_i + qi * k);
+    free(h);
+    free(r);
+    free(lut);
+    free(ph);
+  }
+  free(offs);
+  free(cn);
+}

@@ -48,6 +48,10 @@ def lib():
             "orc_ivf_build": (None, [P, i64, i32, i32, i32, f64, i64, i32, i32, i64, P, P, P]),
             "orc_ivf_lists_from_centroids": (None, [P, i64, i32, P, i32, i32, i64, P, P]),
             "orc_ivf_search": (None, [P, i64, i32, P, i32, P, P, P, i64, i32, i32, i32, P, P, P]),
+            "orc_pq_len": (i32, [i32, i32]),
+            "orc_pq_train_count": (i64, [i64, i32, i64]),
+            "orc_ivfpq_build": (None, [P, i64, i32, i32, i32, f64, i32, i32, i64, i32, i64, P, P, P, P, P]),
+            "orc_ivfpq_search": (None, [P, i32, i32, P, i32, i32, P, P, P, P, i64, i32, i32, P, P, P]),
             "orc_fast_threads": (i32, []),
             "orc_fast_set_threads": (None, [i32]),
             "orc_fast_knn": (None, [P, i64, P, i64, i32, i32, P, P]),
@@ -175,6 +179,44 @@ def ivf_search(x, centroids, sizes, ids, q, n_probes, k, metric="sqeuclidean", i
     op = np.empty((nq, np_), np.int32)
     lib().orc_ivf_search(_p(x), id_offset, x.shape[1], _p(c), c.shape[0], _p(sizes), _p(ids), _p(q), nq, np_, k,
                          metric_code(metric), _p(od), _p(oi), _p(op))
+    return od, oi, op
+
+
+# ---- IVF-PQ (cuVS ivf_pq restated; parity unpinned beyond the Lloyd k-means it builds on) ----
+def pq_len(d, pq_dim) -> int:
+    return int(lib().orc_pq_len(d, pq_dim))
+
+
+def ivfpq_build(x, n_lists, pq_dim, pq_bits=8, iters=20, fraction=0.5, max_per_code=256, balance=True,
+                id_offset=0):
+    """-> (centroids [n_lists, d], codebooks [pq_dim, 2^pq_bits, pq_len], list_sizes [n_lists],
+    list_ids [n], codes [n, pq_dim] uint8 in list order)."""
+    x = _f32(x)
+    n, d = x.shape
+    pl = pq_len(d, pq_dim)
+    cents = np.empty((n_lists, d), np.float32)
+    cbs = np.empty((pq_dim, 1 << pq_bits, pl), np.float32)
+    sizes = np.empty(n_lists, np.int64)
+    ids = np.empty(n, np.int64)
+    codes = np.empty((n, pq_dim), np.uint8)
+    lib().orc_ivfpq_build(_p(x), n, d, n_lists, iters, fraction, pq_dim, pq_bits, max_per_code, int(balance),
+                          id_offset, _p(cents), _p(cbs), _p(sizes), _p(ids), _p(codes))
+    return cents, cbs, sizes, ids, codes
+
+
+def ivfpq_search(centroids, codebooks, sizes, ids, codes, q, n_probes, k):
+    """-> (dist [nq,k], ids [nq,k], probes [nq, n_probes]); L2 only."""
+    c, cb, q = _f32(centroids), _f32(codebooks), _f32(q)
+    sizes, ids = _i64(sizes), _i64(ids)
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    nq = q.shape[0]
+    pq_dim, ncodes, _ = cb.shape
+    np_ = min(n_probes, c.shape[0])
+    od = np.empty((nq, k), np.float32)
+    oi = np.empty((nq, k), np.int64)
+    op = np.empty((nq, np_), np.int32)
+    lib().orc_ivfpq_search(_p(c), c.shape[0], c.shape[1], _p(cb), pq_dim, int(ncodes).bit_length() - 1, _p(sizes),
+                           _p(ids), _p(codes), _p(q), nq, np_, k, _p(od), _p(oi), _p(op))
     return od, oi, op
 
 

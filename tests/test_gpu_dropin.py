@@ -69,3 +69,35 @@ def test_improved_driver_main_small(mivs_lib):
 
     out = imr.main(num_vectors_per_gpu=20000, dim=128, n_queries=16, top_k=20)
     assert out["build"]["success"] and out["recall"] > 0.5
+
+
+def test_coordinator_ivf_pq_seam(mivs_lib):
+    """index_type 'ivf_pq' through the coordinator (reference :398-404 defaults) and the aggregator,
+    bit-exact against the oracle's IVF-PQ restatement."""
+    import index_building_coordinator as ibc
+    import search_result_aggregator as sra
+    from embedding_distribution_manager import EmbeddingDistributionManager
+    from gpu_resource_manager import GPUResourceManager
+
+    rng = np.random.default_rng(12)
+    x = rng.standard_normal((8000, 64)).astype(np.float32)
+    q = rng.standard_normal((21, 64)).astype(np.float32)
+    gm = GPUResourceManager()
+    dm = EmbeddingDistributionManager(gm)
+    dist = dm.distribute_embeddings(torch.from_numpy(x), target_gpus=[0])
+    co = ibc.IndexBuildingCoordinator(gm)
+    cfg = ibc.IndexBuildConfig("ivf_pq", {"n_lists": 16, "kmeans_n_iters": 3, "max_train_points_per_pq_code": 16},
+                               parallel_build=False, max_retries=0)
+    res = co.build_indices_parallel(dist, cfg)
+    assert res.success, res.build_results[0].error_message
+    idx = co.get_built_indices()[0]
+    assert idx.pq_dim == 16 and idx.pq_bits == 8  # min(64, d // 4)
+    agg = sra.SearchResultAggregator(gm)
+    out = agg.perform_distributed_search(torch.from_numpy(q), co.get_built_indices(),
+                                         sra.SearchConfig(k=10, search_params={"nprobe": 5}))
+    oc, ocb, osz, oids, ocodes = O.ivfpq_build(x, 16, 16, iters=3, max_per_code=16)
+    od, oi, _ = O.ivfpq_search(oc, ocb, osz, oids, ocodes, q, 5, 10)
+    np.testing.assert_array_equal(out.final_indices, oi)
+    np.testing.assert_array_equal(out.final_distances.view(np.int32), od.view(np.int32))
+    co.cleanup_all_indices()
+    dm.cleanup_distribution()

@@ -388,3 +388,58 @@ def test_wide_scan_bitexact(mivs_lib, monkeypatch, n, d, nq, k, metric, n_lists,
         od, oi, _ = O.ivf_search(x, oc, osz, oids, q, n_probes, k, metric=metric)
     np.testing.assert_array_equal(ids.cpu().numpy(), oi)
     np.testing.assert_array_equal(_bits(dist.cpu().numpy()), _bits(od))
+
+
+# ---- IVF-PQ (K9 LUT scan): codebooks, codes and search bit-exact vs oracle orc_ivfpq_* ----
+PQ_CASES = [
+    # n, d, n_lists, pq_dim, iters, nq, n_probes, k
+    (6000, 64, 16, 16, 4, 40, 4, 10),
+    (9000, 128, 24, 32, 3, 33, 8, 16),
+    (4000, 100, 8, 20, 3, 17, 8, 5),      # pq_len 5, rot_dim 100: no padding dims
+    (5000, 96, 12, 40, 2, 29, 5, 32),     # pq_len 3, rot_dim 120 > d: zero-padded dims
+    (12000, 768, 32, 96, 2, 20, 6, 10),   # the reference's pq_dim = 96 at d = 768
+]
+
+
+@pytest.mark.parametrize("n,d,n_lists,pq_dim,iters,nq,n_probes,k", PQ_CASES)
+def test_ivf_pq_build_and_search_bitexact(mivs_lib, n, d, n_lists, pq_dim, iters, nq, n_probes, k):
+    from mivs.neighbors import ivf_pq
+
+    x = _data(n, d, seed=n + pq_dim, normalize=True)
+    q = _data(nq, d, seed=n + pq_dim + 1, normalize=True)
+    params = ivf_pq.IndexParams(n_lists=n_lists, pq_dim=pq_dim, kmeans_n_iters=iters, max_train_points_per_pq_code=32)
+    idx = ivf_pq.build(params, _gpu(x), ids_offset=3)
+    oc, ocb, osz, oids, ocodes = O.ivfpq_build(x, n_lists, pq_dim, iters=iters, max_per_code=32, id_offset=3)
+    np.testing.assert_array_equal(_bits(idx.centers.cpu().numpy()), _bits(oc))
+    np.testing.assert_array_equal(_bits(idx.pq_centers.cpu().numpy()), _bits(ocb))
+    np.testing.assert_array_equal(idx.list_sizes.numpy(), osz)
+    np.testing.assert_array_equal(idx.list_ids().cpu().numpy(), oids)
+    np.testing.assert_array_equal(idx.codes().cpu().numpy(), ocodes)
+    probes = torch.empty((nq, n_probes), dtype=torch.int32, device="cuda")
+    dist, ids = ivf_pq.search(ivf_pq.SearchParams(n_probes=n_probes), idx, _gpu(q), k, probes_out=probes)
+    od, oi, op = O.ivfpq_search(oc, ocb, osz, oids, ocodes, q, n_probes, k)
+    np.testing.assert_array_equal(probes.cpu().numpy(), op)
+    np.testing.assert_array_equal(ids.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(dist.cpu().numpy()), _bits(od))
+
+
+def test_ivf_pq_fp16_dataset_and_recall(mivs_lib):
+    """fp16 input (BASELINE config 5) is widened on the device: the index equals the one built from the
+    widened fp32 copy, and PQ recall against exact neighbours is in the expected range for pq_len 4."""
+    from mivs import ops
+    from mivs.neighbors import brute_force, ivf_pq
+
+    x = ops.synth_mixture(50000, 128, 4, n_centers=256, sigma=0.35)
+    q = ops.synth_mixture(200, 128, 4, n_centers=256, sigma=0.35, row_begin=1 << 40)
+    params = ivf_pq.IndexParams(n_lists=64, pq_dim=32, kmeans_n_iters=5)
+    idx = ivf_pq.build(params, x.half())
+    ref = ivf_pq.build(params, x.half().float())
+    assert idx.size == 50000 and idx.pq_len == 4
+    assert torch.equal(idx.codes(), ref.codes()) and torch.equal(idx.pq_centers, ref.pq_centers)
+    d1, i1 = ivf_pq.search(ivf_pq.SearchParams(n_probes=16), idx, q, 10)
+    d2, i2 = ivf_pq.search(ivf_pq.SearchParams(n_probes=16), ref, q, 10)
+    assert torch.equal(i1, i2) and torch.equal(d1, d2)
+    _, gt = brute_force.search(brute_force.build(x.half().float()), q, 10)
+    ids, gt = i1.cpu().numpy(), gt.cpu().numpy()
+    rec = np.mean([len(set(a) & set(b)) / 10 for a, b in zip(ids, gt)])
+    assert rec > 0.3, rec
