@@ -840,8 +840,9 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
     require(np <= kMaxSelectK, "n_probes must be <= " + std::to_string(kMaxSelectK), MIVS_ERR_UNSUPPORTED);
     require(np == n_probes || d_probes == nullptr, "n_probes > n_lists with a probes output");
     const int kcap = scan_kcap(k);
-    require(pq_scan_lds_bytes(idx->rot_dim_pad, idx->pq_dim, kcap) <= 160 * 1024,
-            "ivf_pq: pq_dim x 256 LUT + merge area exceed the 160 KB LDS", MIVS_ERR_UNSUPPORTED);
+    require(pq_tile_lds_bytes(idx->rot_dim_pad, idx->pq_len) <= 160 * 1024 ||
+                pq_scan_lds_bytes(idx->rot_dim_pad, idx->pq_dim, kcap) <= 160 * 1024,
+            "ivf_pq: the LUT scan does not fit the 160 KB LDS for this pq_dim / pq_len", MIVS_ERR_UNSUPPORTED);
     Workspace& ws = idx->ws;
     ProfRec* pr = g_profiling.load() ? idx->prof.begin(s) : nullptr;
     ws.qn.reserve(sizeof(float) * nq);
@@ -851,42 +852,118 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
     single_list_topk(idx->cents, idx->G, d_q, ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, np, kL2,
                      ws.probes_d.as<float>(), ws.probes_i.as<int64_t>(), idx->device, ws, s);
     if (d_probes) HIPCHK(launch_i64_to_i32(ws.probes_i.as<int64_t>(), nq * np, d_probes, s));
-    ws.part_d.reserve(sizeof(float) * (size_t)(nq * np * k));
-    ws.part_i.reserve(sizeof(int64_t) * (size_t)(nq * np * k));
-    PqScanArgs a{};
-    a.queries = d_q;
-    a.cents = idx->centroids_rm.as<float>();
-    a.books = idx->pq_books.as<float>();
-    a.codes = static_cast<const uint8_t*>(idx->pq_codes.p);
-    a.row_ids = idx->lists.ids.as<int64_t>();
-    a.list_off = idx->lists.off.as<int64_t>();
-    a.list_goff = idx->lists.goff.as<int64_t>();
-    a.probes = ws.probes_i.as<int64_t>();
-    a.n_slots = nq * np;
-    a.n_probes = np;
-    a.d = idx->d;
-    a.rot_dim_pad = idx->rot_dim_pad;
-    a.pq_dim = idx->pq_dim;
-    a.pq_dim_pad = idx->pq_dim_pad;
-    a.pq_len = idx->pq_len;
-    a.k = k;
-    a.out_d = ws.part_d.as<float>();
-    a.out_i = ws.part_i.as<int64_t>();
-    if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
-    HIPCHK(launch_pq_scan(a, kcap, s));
-    if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
-    MergeArgs m{};
-    m.in_d = ws.part_d.as<float>();
-    m.in_i = ws.part_i.as<int64_t>();
-    m.slot_begin = nullptr;
-    m.slots_per_q = np;
-    m.nq = nq;
-    m.k_in = k;
-    m.k = k;
-    m.metric = kL2;
-    m.out_d = d_dist;
-    m.out_i = d_ids;
-    HIPCHK(launch_merge(m, s));
+    const ListSet& L = idx->lists;
+    const char* tiled_env = getenv("MIVS_PQ_TILED");
+    const bool tiled = (tiled_env && tiled_env[0] == '1') ||
+                       pq_scan_lds_bytes(idx->rot_dim_pad, idx->pq_dim, kcap) > 160 * 1024;
+    if (tiled && pq_tile_lds_bytes(idx->rot_dim_pad, idx->pq_len) <= 160 * 1024) {
+      // K9b (used when K9's whole-LUT LDS does not fit, or MIVS_PQ_TILED=1): probe map
+      // (list -> 16-query tiles x 512-row chunks), tiled scan, K7 merge of the slots
+      const int64_t ne = nq * np;
+      ws.counts.reserve(sizeof(int) * L.n_lists);
+      ws.fill.reserve(sizeof(int) * L.n_lists);
+      ws.bucket_off.reserve(sizeof(int) * (L.n_lists + 1));
+      ws.work_off.reserve(sizeof(int) * (L.n_lists + 1));
+      ws.bucket_q.reserve(sizeof(int64_t) * ne);
+      ws.bucket_slot.reserve(sizeof(int64_t) * ne);
+      ws.qp_slots.reserve(sizeof(int64_t) * ne);
+      ws.slot_begin.reserve(sizeof(int64_t) * (nq + 1));
+      const size_t stb = scan_tmp_bytes(ne) + sizeof(int64_t) * (size_t)ne;
+      ws.scan_tmp.reserve(stb);
+      HIPCHK(launch_probe_map(ws.probes_i.as<int64_t>(), nq, np, L.n_lists, L.goff.as<int64_t>(), kPqChunkGroups,
+                              kPqTileQueries, ws.counts.as<int>(), ws.fill.as<int>(), ws.bucket_off.as<int>(),
+                              ws.work_off.as<int>(), ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(),
+                              ws.qp_slots.as<int64_t>(), ws.slot_begin.as<int64_t>(), ws.scan_tmp.p, stb, s));
+      // slots: per (query, probe) one per 512-row chunk of the probed list
+      int64_t max_chunks = 0;
+      {
+        std::vector<int64_t> c(L.n_lists);
+        for (int l = 0; l < L.n_lists; ++l) c[l] = ceil_div(L.h_goff[l + 1] - L.h_goff[l], kPqChunkGroups);
+        std::sort(c.begin(), c.end(), std::greater<int64_t>());
+        for (int l = 0; l < std::min<int>(np, L.n_lists); ++l) max_chunks += c[l];
+      }
+      const int64_t max_slots = std::max<int64_t>(nq * max_chunks, 1);
+      ws.part_d.reserve(sizeof(float) * (size_t)(max_slots * k));
+      ws.part_i.reserve(sizeof(int64_t) * (size_t)(max_slots * k));
+      ws.counter.reserve(16);
+      HIPCHK(hipMemsetAsync(ws.counter.p, 0, sizeof(int), s));
+      PqTileArgs a{};
+      a.queries = d_q;
+      a.cents = idx->centroids_rm.as<float>();
+      a.books = idx->pq_books.as<float>();
+      a.codes = static_cast<const uint8_t*>(idx->pq_codes.p);
+      a.row_ids = L.ids.as<int64_t>();
+      a.list_off = L.off.as<int64_t>();
+      a.list_goff = L.goff.as<int64_t>();
+      a.n_lists = L.n_lists;
+      a.bucket_q = ws.bucket_q.as<int64_t>();
+      a.bucket_slot = ws.bucket_slot.as<int64_t>();
+      a.bucket_off = ws.bucket_off.as<int>();
+      a.work_off = ws.work_off.as<int>();
+      a.work_counter = ws.counter.as<int>();
+      a.d = idx->d;
+      a.rot_dim_pad = idx->rot_dim_pad;
+      a.pq_dim = idx->pq_dim;
+      a.pq_dim_pad = idx->pq_dim_pad;
+      a.pq_len = idx->pq_len;
+      a.k = k;
+      a.out_d = ws.part_d.as<float>();
+      a.out_i = ws.part_i.as<int64_t>();
+      const size_t lds = pq_tile_lds_bytes(idx->rot_dim_pad, idx->pq_len);
+      const int per_cu = std::max<int>(1, std::min<int>(3, (int)((160 * 1024) / lds)));
+      if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
+      HIPCHK(launch_pq_scan_tiled(a, kcap, cu_count(idx->device) * per_cu, s));
+      if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
+      MergeArgs m{};
+      m.in_d = ws.part_d.as<float>();
+      m.in_i = ws.part_i.as<int64_t>();
+      m.slot_begin = ws.slot_begin.as<int64_t>();
+      m.nq = nq;
+      m.k_in = k;
+      m.k = k;
+      m.metric = kL2;
+      m.out_d = d_dist;
+      m.out_i = d_ids;
+      HIPCHK(launch_merge(m, s));
+    } else {
+      // K9: one workgroup per (query, probe) with the whole pq_dim x 256 LUT in LDS
+      ws.part_d.reserve(sizeof(float) * (size_t)(nq * np * k));
+      ws.part_i.reserve(sizeof(int64_t) * (size_t)(nq * np * k));
+      PqScanArgs a{};
+      a.queries = d_q;
+      a.cents = idx->centroids_rm.as<float>();
+      a.books = idx->pq_books.as<float>();
+      a.codes = static_cast<const uint8_t*>(idx->pq_codes.p);
+      a.row_ids = L.ids.as<int64_t>();
+      a.list_off = L.off.as<int64_t>();
+      a.list_goff = L.goff.as<int64_t>();
+      a.probes = ws.probes_i.as<int64_t>();
+      a.n_slots = nq * np;
+      a.n_probes = np;
+      a.d = idx->d;
+      a.rot_dim_pad = idx->rot_dim_pad;
+      a.pq_dim = idx->pq_dim;
+      a.pq_dim_pad = idx->pq_dim_pad;
+      a.pq_len = idx->pq_len;
+      a.k = k;
+      a.out_d = ws.part_d.as<float>();
+      a.out_i = ws.part_i.as<int64_t>();
+      if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
+      HIPCHK(launch_pq_scan(a, kcap, s));
+      if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
+      MergeArgs m{};
+      m.in_d = ws.part_d.as<float>();
+      m.in_i = ws.part_i.as<int64_t>();
+      m.slot_begin = nullptr;
+      m.slots_per_q = np;
+      m.nq = nq;
+      m.k_in = k;
+      m.k = k;
+      m.metric = kL2;
+      m.out_d = d_dist;
+      m.out_i = d_ids;
+      HIPCHK(launch_merge(m, s));
+    }
     if (pr) HIPCHK(hipEventRecord(pr->e[3], s));
     idx->last_nq = nq;
     idx->last_np = np;

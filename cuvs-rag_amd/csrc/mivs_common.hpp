@@ -108,6 +108,28 @@ struct PqScanArgs {
   int64_t* out_i;
 };
 
+// IVF-PQ tiled scan (K9b, pq.hip): work item = (list, <= 16 queries, 512-row chunk) from the probe map.
+constexpr int kPqTileQueries = 16;
+constexpr int kPqChunkGroups = 16;  // 512 rows
+struct PqTileArgs {
+  const float* queries;
+  const float* cents;
+  const float* books;
+  const uint8_t* codes;
+  const int64_t* row_ids;
+  const int64_t* list_off;
+  const int64_t* list_goff;
+  int n_lists;
+  const int64_t* bucket_q;
+  const int64_t* bucket_slot;
+  const int* bucket_off;
+  const int* work_off;
+  int* work_counter;
+  int d, rot_dim_pad, pq_dim, pq_dim_pad, pq_len, k;
+  float* out_d;     // [slots][k]
+  int64_t* out_i;
+};
+
 // ---- host-side launchers (implemented in the .hip files) ----
 hipError_t launch_scan(const ScanArgs& a, int kcap, int grid, size_t lds_bytes, hipStream_t s);
 hipError_t launch_scan_ex(const ScanArgs& a, int kcap, int grid, size_t lds_bytes, float* gmerge, hipStream_t s);
@@ -176,6 +198,8 @@ hipError_t launch_pq_ids(const int64_t* perm, int64_t n, const int64_t* list_off
 hipError_t launch_pq_unpack(const uint8_t* codes, int64_t n, const int64_t* list_off, const int64_t* list_goff,
                             int n_lists, int pq_dim, int pq_dim_pad, uint8_t* out, hipStream_t s);
 hipError_t launch_pq_scan(const PqScanArgs& a, int kcap, hipStream_t s);
+size_t pq_tile_lds_bytes(int rot_dim_pad, int pq_len);
+hipError_t launch_pq_scan_tiled(const PqTileArgs& a, int kcap, int grid, hipStream_t s);
 
 hipError_t launch_gather_rows(const float* src, int d, const int64_t* rows, int64_t n, float* dst, hipStream_t s);
 hipError_t launch_unpack_rows(const float* groups, int dp, int d, const int64_t* list_off, const int64_t* list_goff,

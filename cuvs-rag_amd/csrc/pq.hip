@@ -20,6 +20,8 @@ namespace mivs {
 namespace {
 
 constexpr int kPqCodes = 256;  // pq_bits = 8
+constexpr int kPqTileQ = 16;         // queries per K9b work item
+constexpr int kPqChunkRows = 512;    // rows per K9b work item (one per thread)
 
 __device__ __forceinline__ int pq_find_list(const int64_t* __restrict__ off, int n_lists, int64_t p) {
   int lo = 0, hi = n_lists - 1;
@@ -163,16 +165,53 @@ __global__ __launch_bounds__(512) void k_pq_scan(PqScanArgs a) {
     s_res[i] = i < a.d ? a.queries[q * a.d + i] - a.cents[(int64_t)l * a.d + i] : 0.0f;
   __syncthreads();
   const int nlut = a.pq_dim * kPqCodes;
-  for (int e = tid; e < nlut; e += NT) {
-    const int j = e >> 8;
-    const float* b = a.books + (int64_t)e * pl;
-    const float* r = s_res + j * pl;
-    float acc = 0.0f;
-    for (int i = 0; i < pl; ++i) {
-      const float t = r[i] - b[i];
-      acc = fmaf(t, t, acc);
+  if ((pl & 3) == 0 && pl <= 16) {
+    // 4 entries per thread in flight: their codebook rows (pl/4 float4 each) are all requested
+    // before the first FMA, so the L2 latency is paid once per 4 entries, not once per entry
+    const int nv = pl >> 2;
+    for (int base = tid; base < nlut; base += 4 * NT) {
+      float4 bv[4][4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int e = base + v * NT;
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4)
+          if (c4 < nv && e < nlut) bv[v][c4] = *reinterpret_cast<const float4*>(a.books + (int64_t)e * pl + 4 * c4);
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int e = base + v * NT;
+        if (e >= nlut) break;
+        const float* r = s_res + (e >> 8) * pl;
+        float acc = 0.0f;
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) {
+          if (c4 < nv) {
+            const float t0 = r[4 * c4 + 0] - bv[v][c4].x;
+            acc = fmaf(t0, t0, acc);
+            const float t1 = r[4 * c4 + 1] - bv[v][c4].y;
+            acc = fmaf(t1, t1, acc);
+            const float t2 = r[4 * c4 + 2] - bv[v][c4].z;
+            acc = fmaf(t2, t2, acc);
+            const float t3 = r[4 * c4 + 3] - bv[v][c4].w;
+            acc = fmaf(t3, t3, acc);
+          }
+        }
+        lut[e] = acc;
+      }
     }
-    lut[e] = acc;
+  } else {
+    for (int e = tid; e < nlut; e += NT) {
+      const int j = e >> 8;
+      const float* b = a.books + (int64_t)e * pl;
+      const float* r = s_res + j * pl;
+      float acc = 0.0f;
+      for (int i = 0; i < pl; ++i) {
+        const float t = r[i] - b[i];
+        acc = fmaf(t, t, acc);
+      }
+      lut[e] = acc;
+    }
   }
   __syncthreads();
 
@@ -262,12 +301,192 @@ __global__ __launch_bounds__(512) void k_pq_scan(PqScanArgs a) {
   }
 }
 
+// K9b: work item = (list l, tile of <= 16 queries probing l, chunk of 16 groups = 512 rows), dequeued
+// like K3 from the IVF probe map. Subspace-outer loop: per subspace j the codebook B_j (256 x pl)
+// and the tile's 16 LUT rows LUT_j[q][c] = ||(q - c_l)_j - B_j[c]||^2 are built in LDS once and
+// every thread (one row of the chunk) adds LUT_j[q][code_j(row)] for the 16 queries: each
+// codebook byte crosses L2 once per work item instead of once per (query, probe), and the sums
+// run in the oracle's order (j ascending). Then per query a wave picks the chunk's top-k.
+template <int KCAP>
+__global__ __launch_bounds__(512) void k_pq_scan_tiled(PqTileArgs a) {
+  constexpr int NT = 512, TQ = kPqTileQ, ROWS = kPqChunkRows;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int64_t* s_q = reinterpret_cast<int64_t*>(smem);          // [TQ]
+  int64_t* s_slot = s_q + TQ;                               // [TQ]
+  int* s_misc = reinterpret_cast<int*>(s_slot + TQ);        // [4]
+  float* s_cb = reinterpret_cast<float*>(smem + 256 + 16);  // [2][256 * pl]   codebook, double-buffered
+  float* s_lut = s_cb + 2 * 256 * a.pq_len;                 // [2][TQ][256]
+  float* s_rj = s_lut + 2 * TQ * 256;                       // [2][TQ][pl]    query residuals of subspace j
+  float* s_dist = s_cb;                                     // [TQ][ROWS], after the subspace loop
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int pl = a.pq_len;
+  const int total = a.work_off[a.n_lists];
+  for (;;) {
+    if (tid == 0) s_misc[0] = atomicAdd(a.work_counter, 1);
+    __syncthreads();
+    const int w = s_misc[0];
+    if (w >= total) break;
+    int lo = 0, hi = a.n_lists - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (a.work_off[mid] <= w) lo = mid; else hi = mid - 1;
+    }
+    const int l = lo;
+    const int m = a.bucket_off[l + 1] - a.bucket_off[l];
+    const int tiles = (m + TQ - 1) / TQ;
+    const int local = w - a.work_off[l];
+    const int chunk = local / tiles;
+    const int tile = local - chunk * tiles;
+    const int e0 = a.bucket_off[l] + tile * TQ;
+    const int nqt = m - tile * TQ < TQ ? m - tile * TQ : TQ;
+    const int64_t nrows = a.list_off[l + 1] - a.list_off[l];
+    const int64_t r0 = (int64_t)chunk * ROWS;                      // first row of the chunk in the list
+    const int nr = (int)(nrows - r0 < ROWS ? nrows - r0 : ROWS);   // valid rows of the chunk
+    const int64_t g0 = a.list_goff[l];
+    if (tid < TQ) {
+      if (tid < nqt) {
+        s_q[tid] = a.bucket_q[e0 + tid];
+        s_slot[tid] = a.bucket_slot[e0 + tid] + chunk;
+      } else {
+        s_q[tid] = -1;
+        s_slot[tid] = -1;
+      }
+    }
+    __syncthreads();
+    // this thread's row and its code address
+    const int row = tid;
+    const bool rvalid = row < nr;
+    const int64_t rpos = r0 + (rvalid ? row : 0);
+    const uint8_t* cg = a.codes + (g0 + rpos / kGroupRows) * (int64_t)kGroupRows * a.pq_dim_pad +
+                        (rpos % kGroupRows) * 16;
+    float acc[TQ];
+#pragma unroll
+    for (int t = 0; t < TQ; ++t) acc[t] = 0.0f;
+    // stage subspace j: codebook B_j and the tile's residual sub-vectors (q - c_l)_j (dims >= d: 0)
+    auto load_stage = [&](int j, int buf) {
+      const float* src = a.books + (int64_t)j * 256 * pl;
+      float* dst = s_cb + buf * 256 * pl;
+      for (int i = tid; i < 256 * pl; i += NT) dst[i] = src[i];
+      for (int i = tid; i < TQ * pl; i += NT) {
+        const int t = i / pl, k = j * pl + (i - t * pl);
+        const int64_t q = s_q[t];
+        s_rj[buf * TQ * pl + i] = (q >= 0 && k < a.d) ? a.queries[q * a.d + k] - a.cents[(int64_t)l * a.d + k] : 0.0f;
+      }
+    };
+    load_stage(0, 0);
+    __syncthreads();
+    uint4 cw = make_uint4(0, 0, 0, 0);
+    for (int j = 0; j < a.pq_dim; ++j) {
+      const int buf = j & 1;
+      // LUT_j for the tile: entry e = (t, c), t < TQ, c < 256 -> 4096 entries, 8 per thread
+      const float* cb = s_cb + buf * 256 * pl;
+      float* lut = s_lut + buf * TQ * 256;
+      for (int e = tid; e < TQ * 256; e += NT) {
+        const int t = e >> 8, c = e & 255;
+        const float* r = s_rj + buf * TQ * pl + t * pl;
+        const float* b = cb + c * pl;
+        float v = 0.0f;
+        for (int i = 0; i < pl; ++i) {
+          const float dd = r[i] - b[i];
+          v = fmaf(dd, dd, v);
+        }
+        lut[e] = v;
+      }
+      if (j + 1 < a.pq_dim) load_stage(j + 1, buf ^ 1);
+      if ((j & 15) == 0) cw = *reinterpret_cast<const uint4*>(cg + (int64_t)(j >> 4) * (kGroupRows * 16));
+      __syncthreads();
+      const int jb = j & 15;
+      const uint32_t word = jb < 4 ? cw.x : (jb < 8 ? cw.y : (jb < 12 ? cw.z : cw.w));
+      const int code = (word >> (8 * (jb & 3))) & 0xFF;
+#pragma unroll
+      for (int t = 0; t < TQ; ++t) acc[t] = acc[t] + lut[t * 256 + code];
+    }
+    // distances of the chunk -> LDS [TQ][ROWS] (+inf on pad rows; overlays the dead codebook / LUT
+    // buffers), then per query a wave's top-k
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < TQ; ++t) s_dist[t * ROWS + row] = rvalid ? acc[t] : INFINITY;
+    __syncthreads();
+    for (int t = wave; t < TQ; t += NT / 64) {
+      const int64_t slot = s_slot[t];
+      if (slot < 0) continue;
+      float lk[KCAP];
+      int lp[KCAP];
+#pragma unroll
+      for (int i = 0; i < KCAP; ++i) { lk[i] = INFINITY; lp[i] = INT_MAX; }
+      for (int r = lane; r < ROWS; r += 64) {
+        const float v = s_dist[t * ROWS + r];
+        if (v < lk[KCAP - 1]) pq_insert<KCAP>(lk, lp, v, r);
+      }
+      // 64-lane merge: per rank the (dist, row) minimum; the winner lane advances its head
+      float hk = lk[0];
+      int hp = lp[0];
+      for (int rk = 0; rk < a.k; ++rk) {
+        float bk = hk;
+        int bp = hp;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+          const float ok = __shfl_xor(bk, off);
+          const int op = __shfl_xor(bp, off);
+          if (ok < bk || (ok == bk && op < bp)) { bk = ok; bp = op; }
+        }
+        if (lane == 0) {
+          const bool valid = bp != INT_MAX;
+          a.out_d[slot * a.k + rk] = valid ? bk : INFINITY;
+          a.out_i[slot * a.k + rk] = valid ? a.row_ids[g0 * kGroupRows + r0 + bp] : (int64_t)-1;
+        }
+        if (hk == bk && hp == bp) {
+          // registers cannot be indexed dynamically: shift the list down by one instead
+#pragma unroll
+          for (int i = 0; i + 1 < KCAP; ++i) { lk[i] = lk[i + 1]; lp[i] = lp[i + 1]; }
+          lk[KCAP - 1] = INFINITY;
+          lp[KCAP - 1] = INT_MAX;
+          hk = lk[0];
+          hp = lp[0];
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 inline dim3 gridc(int64_t n, int b) {
   const int64_t g = ceil_div(n > 0 ? n : 1, b);
   return dim3((unsigned)(g < (1 << 20) ? g : (1 << 20)));
 }
 
 }  // namespace
+
+size_t pq_tile_lds_bytes(int rot_dim_pad, int pq_len) {
+  (void)rot_dim_pad;
+  const size_t loop = (size_t)2 * 256 * pq_len * 4 + (size_t)2 * kPqTileQ * 256 * 4 + (size_t)2 * kPqTileQ * pq_len * 4;
+  const size_t dist = (size_t)kPqTileQ * kPqChunkRows * 4;
+  return 256 + 16 + (loop > dist ? loop : dist);
+}
+
+template <int KCAP>
+static hipError_t launch_pq_tiled_k(const PqTileArgs& a, int grid, size_t lds, hipStream_t s) {
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pq_scan_tiled<KCAP>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL(k_pq_scan_tiled<KCAP>, dim3((unsigned)grid), dim3(512), lds, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_pq_scan_tiled(const PqTileArgs& a, int kcap, int grid, hipStream_t s) {
+  const size_t lds = pq_tile_lds_bytes(a.rot_dim_pad, a.pq_len);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  switch (kcap) {
+    case 1: return launch_pq_tiled_k<1>(a, grid, lds, s);
+    case 4: return launch_pq_tiled_k<4>(a, grid, lds, s);
+    case 8: return launch_pq_tiled_k<8>(a, grid, lds, s);
+    case 12: return launch_pq_tiled_k<12>(a, grid, lds, s);
+    case 16: return launch_pq_tiled_k<16>(a, grid, lds, s);
+    case 32: return launch_pq_tiled_k<32>(a, grid, lds, s);
+    default: return hipErrorInvalidValue;
+  }
+}
 
 size_t pq_scan_lds_bytes(int rot_dim_pad, int pq_dim, int kcap) {
   const size_t lut = (size_t)pq_dim * kPqCodes * 4;
