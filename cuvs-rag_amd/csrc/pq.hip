@@ -22,6 +22,7 @@ namespace {
 constexpr int kPqCodes = 256;  // pq_bits = 8
 constexpr int kPqTileQ = 16;         // queries per K9b work item
 constexpr int kPqChunkRows = 512;    // rows per K9b work item (one per thread)
+constexpr int kPqMaxChunks = 8;      // K9 register path: pq_dim <= 128 (8 x 16 codes per row)
 
 __device__ __forceinline__ int pq_find_list(const int64_t* __restrict__ off, int n_lists, int64_t p) {
   int lo = 0, hi = n_lists - 1;
@@ -137,9 +138,8 @@ __device__ __forceinline__ void pq_insert(float (&lk)[KCAP], int (&lp)[KCAP], fl
 //      register top-KCAP by (dist, row position);
 //   4. the NT lane lists -> LDS; wave w merges its 64 lists (64-lane min-reduction per rank),
 //      then wave 0 merges the NT/64 wave lists; the slot's top-k (dist, id) -> out.
-template <int KCAP>
-__global__ __launch_bounds__(512) void k_pq_scan(PqScanArgs a) {
-  constexpr int NT = 512;
+template <int KCAP, int NT>
+__global__ __launch_bounds__(NT) void k_pq_scan(PqScanArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* s_res = reinterpret_cast<float*>(smem);                 // [rot_dim]
   float* lut = s_res + a.rot_dim_pad;                            // [pq_dim][256]
@@ -222,20 +222,53 @@ __global__ __launch_bounds__(512) void k_pq_scan(PqScanArgs a) {
   const int64_t r0 = a.list_off[l], nrows = a.list_off[l + 1] - r0;
   const int64_t g0 = a.list_goff[l];
   const int nchunk = a.pq_dim_pad >> 4;
-  for (int64_t r = tid; r < nrows; r += NT) {
-    const uint8_t* cg = a.codes + (g0 + r / kGroupRows) * (int64_t)kGroupRows * a.pq_dim_pad + (r % kGroupRows) * 16;
-    float dist = 0.0f;
-    int j = 0;
-    for (int ch = 0; ch < nchunk; ++ch) {
-      const uint4 w = *reinterpret_cast<const uint4*>(cg + (int64_t)ch * (kGroupRows * 16));
-      const uint32_t wv[4] = {w.x, w.y, w.z, w.w};
+  auto row_codes = [&](int64_t r) {
+    return a.codes + (g0 + r / kGroupRows) * (int64_t)kGroupRows * a.pq_dim_pad + (r % kGroupRows) * 16;
+  };
+  if (nchunk <= kPqMaxChunks) {
+    // all code chunks of the NEXT row are requested before the current row's LUT lookups
+    uint4 cur[kPqMaxChunks], nxt[kPqMaxChunks];
+    auto load_row = [&](int64_t r, uint4 (&w)[kPqMaxChunks]) {
+      const uint8_t* cg = row_codes(r < nrows ? r : 0);
 #pragma unroll
-      for (int b = 0; b < 16; ++b) {
-        if (j + b < a.pq_dim) dist = dist + lut[((j + b) << 8) + ((wv[b >> 2] >> (8 * (b & 3))) & 0xFF)];
+      for (int ch = 0; ch < kPqMaxChunks; ++ch)
+        if (ch < nchunk) w[ch] = *reinterpret_cast<const uint4*>(cg + (int64_t)ch * (kGroupRows * 16));
+    };
+    if (tid < nrows) load_row(tid, cur);
+    for (int64_t r = tid; r < nrows; r += NT) {
+      if (r + NT < nrows) load_row(r + NT, nxt);
+      float dist = 0.0f;
+#pragma unroll
+      for (int ch = 0; ch < kPqMaxChunks; ++ch) {
+        if (ch < nchunk) {
+          const uint32_t wv[4] = {cur[ch].x, cur[ch].y, cur[ch].z, cur[ch].w};
+#pragma unroll
+          for (int b = 0; b < 16; ++b) {
+            const int j = ch * 16 + b;
+            if (j < a.pq_dim) dist = dist + lut[(j << 8) + ((wv[b >> 2] >> (8 * (b & 3))) & 0xFF)];
+          }
+        }
       }
-      j += 16;
+      if (dist < lk[KCAP - 1]) pq_insert<KCAP>(lk, lp, dist, (int)r);
+#pragma unroll
+      for (int ch = 0; ch < kPqMaxChunks; ++ch) cur[ch] = nxt[ch];
     }
-    if (dist < lk[KCAP - 1]) pq_insert<KCAP>(lk, lp, dist, (int)r);
+  } else {
+    for (int64_t r = tid; r < nrows; r += NT) {
+      const uint8_t* cg = row_codes(r);
+      float dist = 0.0f;
+      int j = 0;
+      for (int ch = 0; ch < nchunk; ++ch) {
+        const uint4 w = *reinterpret_cast<const uint4*>(cg + (int64_t)ch * (kGroupRows * 16));
+        const uint32_t wv[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int b = 0; b < 16; ++b) {
+          if (j + b < a.pq_dim) dist = dist + lut[((j + b) << 8) + ((wv[b >> 2] >> (8 * (b & 3))) & 0xFF)];
+        }
+        j += 16;
+      }
+      if (dist < lk[KCAP - 1]) pq_insert<KCAP>(lk, lp, dist, (int)r);
+    }
   }
   __syncthreads();  // LUT dead: the merge area aliases it
 #pragma unroll
@@ -488,9 +521,18 @@ hipError_t launch_pq_scan_tiled(const PqTileArgs& a, int kcap, int grid, hipStre
   }
 }
 
-size_t pq_scan_lds_bytes(int rot_dim_pad, int pq_dim, int kcap) {
+// K9 workgroup size: 1024 threads (4 waves per SIMD) when the merge area of 1024 lane lists
+// still fits beside the LUT, else 512
+static int pq_scan_threads(int rot_dim_pad, int pq_dim, int kcap) {
   const size_t lut = (size_t)pq_dim * kPqCodes * 4;
-  const size_t merge = (size_t)512 * kcap * 8 + (size_t)8 * kcap * 8;
+  const size_t merge = (size_t)1024 * kcap * 8 + (size_t)16 * kcap * 8;
+  return (size_t)rot_dim_pad * 4 + (lut > merge ? lut : merge) <= 160 * 1024 ? 1024 : 512;
+}
+
+size_t pq_scan_lds_bytes(int rot_dim_pad, int pq_dim, int kcap) {
+  const int nt = pq_scan_threads(rot_dim_pad, pq_dim, kcap);
+  const size_t lut = (size_t)pq_dim * kPqCodes * 4;
+  const size_t merge = (size_t)nt * kcap * 8 + (size_t)(nt / 64) * kcap * 8;
   return (size_t)rot_dim_pad * 4 + (lut > merge ? lut : merge);
 }
 
@@ -532,13 +574,19 @@ hipError_t launch_pq_unpack(const uint8_t* codes, int64_t n, const int64_t* list
   return hipGetLastError();
 }
 
-template <int KCAP>
-static hipError_t launch_pq_scan_k(const PqScanArgs& a, size_t lds, hipStream_t s) {
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pq_scan<KCAP>),
+template <int KCAP, int NT>
+static hipError_t launch_pq_scan_kn(const PqScanArgs& a, size_t lds, hipStream_t s) {
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pq_scan<KCAP, NT>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL(k_pq_scan<KCAP>, dim3((unsigned)a.n_slots), dim3(512), lds, s, a);
+  hipLaunchKernelGGL((k_pq_scan<KCAP, NT>), dim3((unsigned)a.n_slots), dim3(NT), lds, s, a);
   return hipGetLastError();
+}
+
+template <int KCAP>
+static hipError_t launch_pq_scan_k(const PqScanArgs& a, size_t lds, hipStream_t s) {
+  if (pq_scan_threads(a.rot_dim_pad, a.pq_dim, KCAP) == 1024) return launch_pq_scan_kn<KCAP, 1024>(a, lds, s);
+  return launch_pq_scan_kn<KCAP, 512>(a, lds, s);
 }
 
 hipError_t launch_pq_scan(const PqScanArgs& a, int kcap, hipStream_t s) {
