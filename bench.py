@@ -37,6 +37,7 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "QPS @ recall@10≥0.95 + index-build vectors/sec, 10M×768 IVF-Flat"
 PEAK_HBM_GBS = 8000.0       # MI355X HBM3E peak (MI355X_MICROARCH.md)
 PEAK_F32_MFMA_TFS = 157.3   # dense fp32 MFMA peak (v_mfma_f32_32x32x2_f32)
+PEAK_F16_MFMA_TFS = 2500.0  # dense fp16 MFMA peak (v_mfma_f32_32x32x16_f16; no sparsity)
 QUERY_ROW_BASE = 1 << 40    # queries: same mixture, rows never in any corpus shard
 SEED = 0
 
@@ -252,23 +253,32 @@ def main():
 
     # ---- roofline of the fine-scan kernel (algorithmic work per launch / avg launch time) ----
     scan_ms = prof["scan_ms"] / max(prof["n_calls"], 1)
+    pf = bool(stats.get("prefilter"))
+    dp = (d + 63) // 64 * 64
     flops = 2.0 * d * stats["scanned_rows"]
-    bytes_alg = float(stats["streamed_groups"]) * 32 * d * 4
+    # SURVEY §8(d) de-duplicated bytes: every query tile streams the rows of its list once
+    # (fp16 copy: 2 B per padded dim for the pre-filter scan K10, else fp32)
+    bytes_alg = float(stats["streamed_groups"]) * 32 * (dp * 2 if pf else d * 4)
     tflops = flops / (scan_ms * 1e-3) / 1e12
     gbs = bytes_alg / (scan_ms * 1e-3) / 1e9
     metric_tag = "L2"
-    kname = (f"mivs::k_scan_wide<{stats['kcap']},{metric_tag}>" if stats["query_tile"] == 64
-             else f"mivs::k_scan<{stats['kcap']},{metric_tag}>")
-    cfg_key = f"ivf_flat_n{n}_d{d}_q{Q}_l{a.n_lists}_p{a.n_probes}_k{k}_t{stats['query_tile']}"
+    if pf:
+        kname = f"mivs::k_pf_scan<{metric_tag}>"
+    else:
+        kname = (f"mivs::k_scan_wide<{stats['kcap']},{metric_tag}>" if stats["query_tile"] == 64
+                 else f"mivs::k_scan<{stats['kcap']},{metric_tag}>")
+    peak_mfma = PEAK_F16_MFMA_TFS if pf else PEAK_F32_MFMA_TFS
+    cfg_key = f"ivf_flat_n{n}_d{d}_q{Q}_l{a.n_lists}_p{a.n_probes}_k{k}_t{stats['query_tile']}" + ("_pf" if pf else "")
     traffic, traffic_src = load_traffic(cfg_key)
-    # bound: whichever peak the launch's work needs longer for -- the fp32 MFMA pipe for the
-    # algorithmic flops, or HBM for the bytes that actually crossed it (rocprof FETCH+WRITE when a
-    # committed PMC summary matches this config, else SURVEY §8(d)'s per-tile streamed bytes)
-    t_mfma = flops / (PEAK_F32_MFMA_TFS * 1e12)
+    # bound: whichever peak the launch's work needs longer for -- the MFMA pipe (fp16 for K10, fp32
+    # for the exact scans) for the algorithmic flops, or HBM for the bytes that actually crossed it
+    # (rocprof FETCH+WRITE when a committed PMC summary matches this config, else SURVEY §8(d)'s
+    # per-tile streamed bytes)
+    t_mfma = flops / (peak_mfma * 1e12)
     t_hbm = (traffic if traffic else bytes_alg) / (PEAK_HBM_GBS * 1e9)
     if t_mfma >= t_hbm:
-        roof = {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_F32_MFMA_TFS, "unit": "TFLOP/s",
-                "frac": round(tflops / PEAK_F32_MFMA_TFS, 4)}
+        roof = {"bound": "mfma", "achieved": round(tflops, 2), "peak": peak_mfma, "unit": "TFLOP/s",
+                "frac": round(tflops / peak_mfma, 4)}
     else:
         roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(gbs / PEAK_HBM_GBS, 4)}
@@ -300,7 +310,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32",  # results are the exact fp32 answer (the fp16 pre-filter only selects candidates)
         "data": f"synthetic: on-device Gaussian mixture ({a.centers} centres, sigma={a.sigma}, L2-normalised), "
                 f"seed {SEED}; queries = held-out rows of the same mixture",
         "config": {"workload": f"IVF-Flat {n // 1_000_000}M x {d} fp32 per GPU, n_lists={a.n_lists}, "

@@ -158,6 +158,8 @@ void pack_lists(ListSet& ls, const float* src, int d, int dp, const int64_t* per
 struct Workspace {
   Buf qn, bucket_q, bucket_slot, bucket_off, work_off, counter, part_d, part_i, slot_begin, probes_d, probes_i,
       counts, fill, qp_slots, scan_tmp, gmerge;
+  // fp16 pre-filter path (K10 / K11) and its exact-scan fallback
+  Buf qh, qscale, qres, pf_key, pf_pos, pf_bound, pf_stats, ovf_q, ovf_rows, ovf_d, ovf_i;
 };
 
 // hipEvent pairs recorded on the caller's stream around the pipeline stages of
@@ -196,12 +198,19 @@ struct mivs_index_s {
   // IVF-PQ: codes in the interleaved group layout + codebooks (lists.off/goff/ids/h_* describe the lists)
   int pq_dim = 0, pq_bits = 0, pq_len = 0, pq_dim_pad = 0, rot_dim_pad = 0;
   Buf pq_codes, pq_books;
+  // fp16 copy of the lists for the K10 pre-filter; empty = exact scan only
+  Buf groups_h;
+  int hx_exp = 0;
+  float x_norm_max = 0.0f, x_res_max = 0.0f;
+  std::vector<int64_t> pf_top_chunks_prefix;  // as ListSet::top_chunks_prefix, for kPfChunkGroups
   std::mutex mu;
   Workspace ws;
   Profiler prof;
   // what the last search did (for algorithmic roofline counts)
   int64_t last_nq = 0;
   int last_np = 0, last_k = 0, last_qtile = kQTile;
+  int last_pf = 0;
+  int64_t last_ovf = 0, last_window = 0;
 };
 
 namespace {
@@ -462,10 +471,143 @@ void check_common(int device, const void* data, int64_t n, int32_t dim) {
 }
 
 
+// ---- fp16 pre-filter (K10 / K11) ----
+bool pf_default_on() {
+  const char* e = getenv("MIVS_PREFILTER");
+  return !(e && e[0] == '0');
+}
+
+// build the fp16 copy of idx->lists (+ the per-index maxima the refine window needs)
+void pf_enable(mivs_index_s* idx, hipStream_t s) {
+  const ListSet& L = idx->lists;
+  idx->groups_h.release();
+  if (L.n_groups == 0 || idx->dp % 64 != 0) return;
+  const int64_t nslot = L.n_groups * (int64_t)kGroupRows;
+  Buf st;
+  st.reserve(4 * sizeof(unsigned));
+  HIPCHK(hipMemsetAsync(st.p, 0, 4 * sizeof(unsigned), s));
+  HIPCHK(launch_abs_max(L.groups.as<float>(), nslot * idx->dp, st.as<unsigned>(), s));
+  HIPCHK(launch_norm_max(L.norms.as<float>(), nslot, st.as<unsigned>() + 1, s));
+  unsigned h[4] = {0, 0, 0, 0};
+  HIPCHK(hipMemcpyAsync(h, st.p, 2 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  float absmax, normmax;
+  std::memcpy(&absmax, &h[0], 4);
+  std::memcpy(&normmax, &h[1], 4);
+  idx->hx_exp = pf_hx_exp(absmax);
+  idx->groups_h.reserve(sizeof(uint16_t) * (size_t)nslot * idx->dp);
+  HIPCHK(launch_groups_to_half(L.groups.as<float>(), L.n_groups, idx->dp, idx->hx_exp, idx->groups_h.as<uint16_t>(),
+                               st.as<unsigned>() + 2, s));
+  HIPCHK(hipMemcpyAsync(&h[2], st.as<unsigned>() + 2, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  float resmax;
+  std::memcpy(&resmax, &h[2], 4);
+  idx->x_norm_max = sqrtf(normmax) * (1.0f + 0x1p-12f);
+  idx->x_res_max = resmax;
+  std::vector<int64_t> c(L.n_lists);
+  for (int l = 0; l < L.n_lists; ++l) c[l] = L.chunks_of(l, kPfChunkGroups);
+  std::sort(c.begin(), c.end(), std::greater<int64_t>());
+  idx->pf_top_chunks_prefix.assign(L.n_lists + 1, 0);
+  for (int l = 0; l < L.n_lists; ++l) idx->pf_top_chunks_prefix[l + 1] = idx->pf_top_chunks_prefix[l] + c[l];
+}
+
 void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
-                      int64_t* out_i, int32_t* out_probes) {
+                      int64_t* out_i, int32_t* out_probes, bool allow_pf = true, bool prof = true);
+
+// K10 scan + K11 refine for a probe map built with (kPfChunkGroups, kPfQTile); queries the refine
+// could not prove are re-run through the exact scan and scattered back.
+void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
+                    int64_t* out_i, ProfRec* pr) {
   Workspace& ws = idx->ws;
-  ProfRec* pr = g_profiling.load() ? idx->prof.begin(s) : nullptr;
+  const ListSet& L = idx->lists;
+  const int dp = idx->dp;
+  ws.qh.reserve(sizeof(uint16_t) * (size_t)nq * dp);
+  ws.qscale.reserve(sizeof(float) * nq);
+  ws.qres.reserve(sizeof(float) * nq);
+  HIPCHK(launch_queries_to_half(q, nq, idx->d, dp, idx->hx_exp, ws.qh.as<uint16_t>(), ws.qscale.as<float>(),
+                                ws.qres.as<float>(), s));
+  const int64_t max_slots = std::max<int64_t>(1, nq * idx->pf_top_chunks_prefix[std::min<int64_t>(np, L.n_lists)]);
+  // per-slot candidates: room above k so that a neighbourhood packed into one chunk does not overflow
+  const int slot_k = k <= 10 ? 16 : kPfSlotKMax;
+  ws.pf_key.reserve(sizeof(float) * (size_t)max_slots * slot_k);
+  ws.pf_pos.reserve(sizeof(int) * (size_t)max_slots * slot_k);
+  ws.pf_bound.reserve(sizeof(float) * (size_t)max_slots);
+  ws.counter.reserve(16);
+  HIPCHK(hipMemsetAsync(ws.counter.p, 0, sizeof(int), s));
+  PfScanArgs a{};
+  a.groups_h = idx->groups_h.as<uint16_t>();
+  a.row_norms = L.norms.as<float>();
+  a.list_goff = L.goff.as<int64_t>();
+  a.n_lists = L.n_lists;
+  a.chunk_groups = kPfChunkGroups;
+  a.qh = ws.qh.as<uint16_t>();
+  a.qscale = ws.qscale.as<float>();
+  a.qnorms = ws.qn.as<float>();
+  a.bucket_q = ws.bucket_q.as<int64_t>();
+  a.bucket_slot = ws.bucket_slot.as<int64_t>();
+  a.bucket_off = ws.bucket_off.as<int>();
+  a.work_off = ws.work_off.as<int>();
+  a.work_counter = ws.counter.as<int>();
+  a.slot_key = ws.pf_key.as<float>();
+  a.slot_pos = ws.pf_pos.as<int>();
+  a.slot_bound = ws.pf_bound.as<float>();
+  a.slot_k = slot_k;
+  a.dp = dp;
+  a.metric = idx->metric;
+  if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
+  HIPCHK(launch_pf_scan(a, cu_count(idx->device), pf_scan_lds_bytes(dp), s));
+  if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
+  ws.pf_stats.reserve(32);
+  HIPCHK(hipMemsetAsync(ws.pf_stats.p, 0, 32, s));
+  ws.ovf_q.reserve(sizeof(int64_t) * nq);
+  PfRefineArgs r{};
+  r.slot_key = ws.pf_key.as<float>();
+  r.slot_pos = ws.pf_pos.as<int>();
+  r.slot_bound = ws.pf_bound.as<float>();
+  r.slot_begin = ws.slot_begin.as<int64_t>();
+  r.slot_k = slot_k;
+  r.nq = nq;
+  r.k = k;
+  r.d = idx->d;
+  r.dp = dp;
+  r.metric = idx->metric;
+  r.groups = L.groups.as<float>();
+  r.row_norms = L.norms.as<float>();
+  r.row_ids = L.ids.as<int64_t>();
+  r.queries = q;
+  r.qnorms = ws.qn.as<float>();
+  r.qres = ws.qres.as<float>();
+  r.x_norm_max = idx->x_norm_max;
+  r.x_res_max = idx->x_res_max;
+  r.out_d = out_d;
+  r.out_i = out_i;
+  r.ovf_count = ws.pf_stats.as<int>();
+  r.ovf_q = ws.ovf_q.as<int64_t>();
+  r.n_window = reinterpret_cast<int64_t*>(ws.pf_stats.as<char>() + 8);
+  HIPCHK(launch_pf_refine(r, s));
+  int64_t h[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(h, ws.pf_stats.p, 16, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));  // the only host sync of the search: the fallback size
+  const int64_t novf = (int64_t)(int32_t)(h[0] & 0xFFFFFFFF);
+  idx->last_ovf += novf;
+  idx->last_window += h[1];
+  if (novf > 0) {
+    ws.ovf_rows.reserve(sizeof(float) * (size_t)novf * idx->d);
+    ws.ovf_d.reserve(sizeof(float) * (size_t)novf * k);
+    ws.ovf_i.reserve(sizeof(int64_t) * (size_t)novf * k);
+    HIPCHK(launch_gather_rows(q, idx->d, ws.ovf_q.as<int64_t>(), novf, ws.ovf_rows.as<float>(), s));
+    ivf_search_batch(idx, s, ws.ovf_rows.as<float>(), novf, k, np, ws.ovf_d.as<float>(), ws.ovf_i.as<int64_t>(),
+                     nullptr, false, false);
+    HIPCHK(launch_scatter_results(ws.ovf_d.as<float>(), ws.ovf_i.as<int64_t>(), ws.ovf_q.as<int64_t>(), novf, k,
+                                  out_d, out_i, s));
+  }
+}
+
+void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
+                      int64_t* out_i, int32_t* out_probes, bool allow_pf, bool prof) {
+  Workspace& ws = idx->ws;
+  ProfRec* pr = prof && g_profiling.load() ? idx->prof.begin(s) : nullptr;
+  const bool pf = allow_pf && idx->groups_h.p != nullptr && k <= kPfMaxK;
   ws.qn.reserve(sizeof(float) * nq);
   HIPCHK(launch_row_norms(q, nq, idx->d, ws.qn.as<float>(), s));
   // coarse: top-n_probes centroids per query
@@ -488,12 +630,21 @@ void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t 
   const size_t stb = scan_tmp_bytes(ne) + sizeof(int64_t) * (size_t)ne;
   ws.scan_tmp.reserve(stb);
   const bool dump = k > kMaxK;
-  const int qtile = dump ? kQTile : pick_qtile(k, idx->d, idx->G);
-  idx->last_qtile = qtile;
-  HIPCHK(launch_probe_map(ws.probes_i.as<int64_t>(), nq, np, L.n_lists, L.goff.as<int64_t>(), idx->G, qtile,
-                          ws.counts.as<int>(), ws.fill.as<int>(), ws.bucket_off.as<int>(), ws.work_off.as<int>(),
-                          ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(), ws.qp_slots.as<int64_t>(),
-                          ws.slot_begin.as<int64_t>(), ws.scan_tmp.p, stb, s));
+  const int qtile = pf ? kPfQTile : (dump ? kQTile : pick_qtile(k, idx->d, idx->G));
+  if (prof) {
+    idx->last_qtile = qtile;
+    idx->last_pf = pf ? 1 : 0;
+  }
+  HIPCHK(launch_probe_map(ws.probes_i.as<int64_t>(), nq, np, L.n_lists, L.goff.as<int64_t>(),
+                          pf ? kPfChunkGroups : idx->G, qtile, ws.counts.as<int>(), ws.fill.as<int>(),
+                          ws.bucket_off.as<int>(), ws.work_off.as<int>(), ws.bucket_q.as<int64_t>(),
+                          ws.bucket_slot.as<int64_t>(), ws.qp_slots.as<int64_t>(), ws.slot_begin.as<int64_t>(),
+                          ws.scan_tmp.p, stb, s));
+  if (pf) {
+    pf_scan_refine(idx, s, q, nq, k, np, out_d, out_i, pr);
+    if (pr) HIPCHK(hipEventRecord(pr->e[3], s));
+    return;
+  }
   // fine scan into per-(query, probe, chunk) slots: top-k partials (k <= 64) or raw keys (DUMP)
   const int64_t slot_rows = (int64_t)idx->G * kGroupRows;
   const int64_t max_slots = nq * L.top_chunks_prefix[std::min<int64_t>(np, L.n_lists)];
@@ -544,6 +695,8 @@ void ivf_search_impl(mivs_index_s* idx, hipStream_t s, const float* q, int64_t n
     const int64_t per_q_slots = std::max<int64_t>(1, L.top_chunks_prefix[std::min<int64_t>(np, L.n_lists)]);
     qb = select_batch(nq, (size_t)per_q_slots * ((size_t)idx->G * kGroupRows * 4 + 16));
   }
+  idx->last_ovf = 0;
+  idx->last_window = 0;
   for (int64_t b0 = 0; b0 < nq; b0 += qb) {
     const int64_t nb = std::min<int64_t>(qb, nq - b0);
     ivf_search_batch(idx, s, q + b0 * (int64_t)idx->d, nb, k, np, out_d + b0 * k, out_i + b0 * k,
@@ -611,6 +764,7 @@ int32_t mivs_ivf_flat_build(int32_t device, void* stream, const float* d_data, i
     } else {
       build_lists(idx.get(), d_data, norms.as<float>(), 0, s);
     }
+    if (p->prefilter && pf_default_on()) pf_enable(idx.get(), s);
     HIPCHK(hipStreamSynchronize(s));
     *out = idx.release();
   });
@@ -643,6 +797,7 @@ int32_t mivs_ivf_flat_build_from_centroids(int32_t device, void* stream, const f
     norms.reserve(sizeof(float) * std::max<int64_t>(n, 1));
     HIPCHK(launch_row_norms(d_data, n, dim, norms.as<float>(), s));
     build_lists(idx.get(), d_data, norms.as<float>(), n, s);
+    if (pf_default_on()) pf_enable(idx.get(), s);
     HIPCHK(hipStreamSynchronize(s));
     *out = idx.release();
   });
@@ -1071,6 +1226,9 @@ int32_t mivs_index_last_search_stats(mivs_index_t idx, mivs_search_stats* out) {
     st.k = idx->last_k;
     st.query_tile = idx->last_qtile;
     st.kcap = idx->last_k > 0 ? scan_kcap(idx->last_k) : 0;
+    st.prefilter = idx->last_pf;
+    st.overflow_queries = idx->last_ovf;
+    st.window_candidates = idx->last_window;
     const ListSet& L = idx->lists;
     if (idx->last_nq > 0 && idx->kind == 0) {
       HIPCHK(hipDeviceSynchronize());
@@ -1114,6 +1272,30 @@ int32_t mivs_index_profile_collect(mivs_index_t idx, mivs_profile* out) {
     }
     idx->prof.pending.clear();
     *out = p;
+  });
+}
+
+int32_t mivs_index_set_prefilter(mivs_index_t idx, void* stream, int32_t enable) {
+  return guarded([&] {
+    require(idx != nullptr, "index is NULL");
+    require(idx->kind == 0 || idx->kind == 1, "the fp16 pre-filter applies to ivf_flat / brute_force indexes",
+            MIVS_ERR_UNSUPPORTED);
+    std::lock_guard<std::mutex> g(idx->mu);
+    DeviceGuard dg(idx->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    HIPCHK(hipStreamSynchronize(s));
+    if (enable) {
+      if (!idx->groups_h.p) pf_enable(idx, s);
+    } else {
+      idx->groups_h.release();
+    }
+  });
+}
+
+int32_t mivs_index_get_prefilter(mivs_index_t idx, int32_t* enabled) {
+  return guarded([&] {
+    require(idx != nullptr && enabled != nullptr, "NULL argument");
+    *enabled = idx->groups_h.p != nullptr ? 1 : 0;
   });
 }
 

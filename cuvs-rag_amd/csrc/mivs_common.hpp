@@ -130,6 +130,84 @@ struct PqTileArgs {
   int64_t* out_i;
 };
 
+// ---------------------------------------------------------------------------
+// fp16 pre-filter + exact refine (prefilter.hip).
+//   K10 scans an fp16 copy of the lists (same group layout, scaled by 2^hx_exp)
+//   against fp16 queries (per-query scale) with v_mfma_f32_32x32x16_f16 and keeps,
+//   per (query, probe, chunk) slot, the slot_k smallest APPROXIMATE keys + a
+//   lower bound of every key it dropped. K11 then takes, per query, every
+//   candidate whose approximate key is within 2*delta of the k-th (delta = a
+//   rigorous bound on |approx key - pinned fp32 key|), recomputes those in the
+//   pinned fp32 order and emits the exact top-k. Queries whose dropped-key bound
+//   reaches the window are listed for the exact scan (never silently wrong).
+// ---------------------------------------------------------------------------
+constexpr int kPfQTile = 64;     // queries per K10 work item
+constexpr int kPfLaneK = 8;      // per-lane approximate list length in K10
+constexpr int kPfSlotKMax = 32;  // approximate candidates kept per slot: 16 for k <= 10, else 32
+constexpr int kPfMaxK = 16;      // largest k served by the pre-filter path
+constexpr int kPfCap = 64;       // refine capacity (window candidates per query)
+constexpr int kPfChunkGroups = 64;  // groups (2048 rows) per K10 work item
+
+struct PfScanArgs {
+  const uint16_t* groups_h;   // fp16 lists, group layout [g][dp/8][32][8]
+  const float* row_norms;     // pinned fp32 norms (+inf on pad rows)
+  const int64_t* list_goff;
+  int n_lists;
+  int chunk_groups;
+  const uint16_t* qh;         // fp16 queries [nq][dp], query q scaled by 2^qexp[q]
+  const float* qscale;        // 2^-(hx_exp + qexp[q]): fp16 dot -> approximate fp32 dot (exact scaling)
+  const float* qnorms;        // pinned fp32 query norms
+  const int64_t* bucket_q;
+  const int64_t* bucket_slot;
+  const int* bucket_off;
+  const int* work_off;
+  int* work_counter;
+  float* slot_key;            // [slots][slot_k] ascending approximate keys (+inf: empty)
+  int* slot_pos;              // [slots][slot_k] row positions
+  float* slot_bound;          // [slots] every dropped candidate's approximate key is >= this
+  int slot_k;
+  int dp, metric;
+};
+
+struct PfRefineArgs {
+  const float* slot_key;
+  const int* slot_pos;
+  const float* slot_bound;
+  const int64_t* slot_begin;  // [nq+1]
+  int slot_k;
+  int64_t nq;
+  int k, d, dp, metric;
+  const float* groups;        // fp32 lists (group layout) for the exact recompute
+  const float* row_norms;
+  const int64_t* row_ids;
+  const float* queries;       // fp32 [nq][d]
+  const float* qnorms;
+  const float* qres;          // [nq] ||q - q_h|| (fp16 rounding residual, unscaled)
+  float x_norm_max, x_res_max;  // max ||x||, max ||x - x_h|| over the index rows
+  float* out_d;
+  int64_t* out_i;
+  int* ovf_count;             // queries that need the exact scan
+  int64_t* ovf_q;
+  int64_t* n_window;          // optional: total window candidates (stats)
+};
+
+hipError_t launch_pf_scan(const PfScanArgs& a, int grid, size_t lds, hipStream_t s);
+size_t pf_scan_lds_bytes(int dp);
+hipError_t launch_pf_refine(const PfRefineArgs& a, hipStream_t s);
+// fp32 groups -> fp16 groups scaled by 2^hx_exp (FTZ below the fp16 normal range), per-index maxima of
+// ||x - x_h|| and max |x| (as float bits, atomicMax) into stats[0..1] (zeroed by the caller)
+hipError_t launch_groups_to_half(const float* groups, int64_t n_groups, int dp, int hx_exp, uint16_t* out,
+                                 unsigned* stats, hipStream_t s);
+hipError_t launch_abs_max(const float* x, int64_t n, unsigned* out, hipStream_t s);
+hipError_t launch_norm_max(const float* norms, int64_t n, unsigned* out, hipStream_t s);
+// queries fp32 [nq][d] -> fp16 [nq][dp] with a per-query power-of-two scale, qscale = 2^-(hx_exp+e_q),
+// qres = ||q - q_h|| (unscaled)
+hipError_t launch_queries_to_half(const float* q, int64_t nq, int d, int dp, int hx_exp, uint16_t* qh, float* qscale,
+                                  float* qres, hipStream_t s);
+int pf_hx_exp(float abs_max);  // row-side fp16 scale exponent from max |x|
+hipError_t launch_scatter_results(const float* in_d, const int64_t* in_i, const int64_t* rows, int64_t n, int k,
+                                  float* out_d, int64_t* out_i, hipStream_t s);
+
 // ---- host-side launchers (implemented in the .hip files) ----
 hipError_t launch_scan(const ScanArgs& a, int kcap, int grid, size_t lds_bytes, hipStream_t s);
 hipError_t launch_scan_ex(const ScanArgs& a, int kcap, int grid, size_t lds_bytes, float* gmerge, hipStream_t s);

@@ -1,0 +1,570 @@
+// K10 / K11 — fp16 pre-filter list scan + exact fp32 refine.
+//
+// Why: at the benchmark shape every list is probed by ~300 queries, so the exact
+// fp32 scan (K3w) is bound by the fp32 MFMA rate (157 TF). The fp16 MFMA runs 16x
+// faster per FLOP and an fp16 copy of the lists streams half the bytes. The price
+// is an approximate dot; the refine step makes the RESULT exact again:
+//
+//   K10: per (list, 2048-row chunk, 64-query tile): approximate keys from
+//        v_mfma_f32_32x32x16_f16 (fp16 rows x fp16 queries, fp32 accumulate, exact
+//        power-of-two unscaling); per query the slot_k smallest approximate keys
+//        of the chunk + a LOWER BOUND of every approximate key it dropped.
+//   K11: per query, Ak = k-th smallest approximate key, delta = a rigorous bound of
+//        |approx key - pinned fp32 key| (Cauchy-Schwarz on the fp16 rounding
+//        residuals + worst-case fp32 summation error of both dot products),
+//        window T = Ak + 2 delta. Every candidate with approx key <= T is recomputed
+//        in the pinned fp32 order (= oracle orc_dot / the fp32 MFMA chain); the true
+//        top-k is inside the window, so the output equals the exact scan bit for bit.
+//        If a dropped key could be inside the window (bound <= T) or the window holds
+//        more than kPfCap candidates, the query is listed for the exact scan.
+#include <climits>
+
+#include "mivs_common.hpp"
+
+namespace mivs {
+
+namespace {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+
+constexpr int kPfWaves = 8;
+constexpr int kPfThreads = kPfWaves * 64;
+constexpr int kPfDepth = 8;  // A-operand k-steps (1 KiB wave loads) in flight per wave
+constexpr int kPfSmall = kPfQTile * 8 * 2 + kPfQTile * 4 * 2 + 16;  // s_q, s_slot, s_qn, s_qs, s_misc
+constexpr int kPfMergeBytes = kPfQTile * 16 * kPfLaneK * 8;          // [64 queries][16 lane lists][KL] (key, pos)
+
+__device__ __forceinline__ h8 ld_h8(const uint16_t* p) { return *reinterpret_cast<const h8*>(p); }
+
+template <int KL>
+__device__ __forceinline__ void pf_insert(float (&lk)[KL], int (&lp)[KL], float key, int pos) {
+#pragma unroll
+  for (int t = KL - 1; t >= 0; --t) {
+    const float prev = t > 0 ? lk[t > 0 ? t - 1 : 0] : -INFINITY;
+    const int prevp = t > 0 ? lp[t > 0 ? t - 1 : 0] : 0;
+    const bool shift = key < prev;
+    const bool place = !shift && key < lk[t];
+    lk[t] = shift ? prev : (place ? key : lk[t]);
+    lp[t] = shift ? prevp : (place ? pos : lp[t]);
+  }
+}
+
+// approximate key of one accumulator element: the dot is acc * 2^-(row exp + query exp), exact
+template <int METRIC>
+__device__ __forceinline__ float pf_key(float acc, float qs, float xn, float qn) {
+  const float v = acc * qs;
+  if (METRIC == kL2) {
+    const float t = fmaf(-2.0f, v, xn + qn);
+    return t > 0.0f ? t : 0.0f;
+  }
+  return xn < INFINITY ? -v : INFINITY;
+}
+
+template <int METRIC>
+__device__ __forceinline__ void pf_epilogue(const f32x16& c0, const f32x16& c1, const float* __restrict__ norms,
+                                            int64_t g, int h, float qn0, float qs0, bool qv0, float qn1, float qs1,
+                                            bool qv1, float (&lk0)[kPfLaneK], int (&lp0)[kPfLaneK],
+                                            float (&lk1)[kPfLaneK], int (&lp1)[kPfLaneK]) {
+  const int64_t rb = g * kGroupRows;
+  float xn[16];
+#pragma unroll
+  for (int q4 = 0; q4 < 4; ++q4) {
+    const float4 t = *reinterpret_cast<const float4*>(norms + rb + 8 * q4 + 4 * h);
+    xn[4 * q4 + 0] = t.x; xn[4 * q4 + 1] = t.y; xn[4 * q4 + 2] = t.z; xn[4 * q4 + 3] = t.w;
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int pos = (int)(rb + (r & 3) + 8 * (r >> 2) + 4 * h);
+    if (qv0) {
+      const float key = pf_key<METRIC>(c0[r], qs0, xn[r], qn0);
+      if (key < lk0[kPfLaneK - 1]) pf_insert<kPfLaneK>(lk0, lp0, key, pos);
+    }
+    if (qv1) {
+      const float key = pf_key<METRIC>(c1[r], qs1, xn[r], qn1);
+      if (key < lk1[kPfLaneK - 1]) pf_insert<kPfLaneK>(lk1, lp1, key, pos);
+    }
+  }
+}
+
+// K10. One workgroup (8 waves) per CU, persistent over (list, chunk, 64-query tile) work items.
+// The query tile stays in LDS for the whole chunk as the B operand ([2][dp/8][32] x 16 B, the
+// 32-query slot XOR-swizzled by the block index: conflict-free staging writes and B reads).
+// Each wave streams its own 32-row groups (pass p: group g_begin + 8p + wave) as the A operand
+// straight from HBM: one 1 KiB contiguous wave load per k-step, kPfDepth k-steps in flight across
+// pass boundaries; 2 MFMAs (the two 32-query column tiles) per load.
+template <int METRIC>
+__global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int64_t* s_q = reinterpret_cast<int64_t*>(smem);          // [64] query ids (-1: empty)
+  int64_t* s_slot = s_q + kPfQTile;                          // [64] output slot (already + chunk)
+  float* s_qn = reinterpret_cast<float*>(s_slot + kPfQTile);  // [64]
+  float* s_qs = s_qn + kPfQTile;                              // [64]
+  int* s_misc = reinterpret_cast<int*>(s_qs + kPfQTile);
+  char* s_b = smem + kPfSmall;
+  float* mkey = reinterpret_cast<float*>(s_b);
+  int* mpos = reinterpret_cast<int*>(mkey + kPfQTile * 16 * kPfLaneK);
+
+  const int dp = a.dp;
+  const int nb = dp >> 3;  // 8-dim blocks
+  const int nk = dp >> 4;  // 16-dim k-steps
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int j = lane & 31;
+  const int h = lane >> 5;
+  const int total = a.work_off[a.n_lists];
+  const int64_t pstride = (int64_t)kPfWaves * nb * 256;  // halves between a wave's consecutive groups
+
+  for (;;) {
+    if (tid == 0) s_misc[0] = atomicAdd(a.work_counter, 1);
+    __syncthreads();
+    const int w = s_misc[0];
+    if (w >= total) break;
+
+    int lo = 0, hi = a.n_lists - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (a.work_off[mid] <= w) lo = mid; else hi = mid - 1;
+    }
+    const int l = lo;
+    const int m = a.bucket_off[l + 1] - a.bucket_off[l];
+    const int tiles = (m + kPfQTile - 1) / kPfQTile;
+    const int local = w - a.work_off[l];
+    const int chunk = local / tiles;
+    const int tile = local - chunk * tiles;
+    const int64_t g_begin = a.list_goff[l] + (int64_t)chunk * a.chunk_groups;
+    const int64_t g_lim = a.list_goff[l + 1];
+    const int64_t g_end = g_begin + a.chunk_groups < g_lim ? g_begin + a.chunk_groups : g_lim;
+    const int e0 = a.bucket_off[l] + tile * kPfQTile;
+    const int nqt = m - tile * kPfQTile < kPfQTile ? m - tile * kPfQTile : kPfQTile;
+
+    if (tid < kPfQTile) {
+      if (tid < nqt) {
+        const int64_t q = a.bucket_q[e0 + tid];
+        s_q[tid] = q;
+        s_slot[tid] = a.bucket_slot[e0 + tid] + chunk;
+        s_qn[tid] = a.qnorms[q];
+        s_qs[tid] = a.qscale[q];
+      } else {
+        s_q[tid] = -1;
+        s_slot[tid] = -1;
+        s_qn[tid] = INFINITY;
+        s_qs[tid] = 0.0f;
+      }
+    }
+    __syncthreads();
+    // stage the fp16 query tile: nb/8 16-B pieces per thread (dp % 64 == 0), loads batched by 4
+    {
+      const int per = nb >> 3;
+      for (int i0 = 0; i0 < per; i0 += 4) {
+        uint4 v[4];
+        int dst[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int i = tid + (i0 + u) * kPfThreads;
+          const int qi = i / nb, b = i - qi * nb;
+          const int64_t q = (i0 + u < per) ? s_q[qi] : -1;
+          v[u] = make_uint4(0u, 0u, 0u, 0u);
+          if (q >= 0) v[u] = *reinterpret_cast<const uint4*>(a.qh + q * dp + 8 * b);
+          dst[u] = (i0 + u < per) ? (((qi >> 5) * nb + b) << 5) + ((qi & 31) ^ (b & 31)) : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (dst[u] >= 0) *reinterpret_cast<uint4*>(s_b + (size_t)dst[u] * 16) = v[u];
+      }
+    }
+    __syncthreads();
+
+    float lk0[kPfLaneK], lk1[kPfLaneK];
+    int lp0[kPfLaneK], lp1[kPfLaneK];
+#pragma unroll
+    for (int t = 0; t < kPfLaneK; ++t) { lk0[t] = INFINITY; lp0[t] = INT_MAX; lk1[t] = INFINITY; lp1[t] = INT_MAX; }
+    const float qn0 = s_qn[j], qn1 = s_qn[32 + j], qs0 = s_qs[j], qs1 = s_qs[32 + j];
+    const bool qv0 = s_q[j] >= 0, qv1 = s_q[32 + j] >= 0;
+
+    const int ng = (int)(g_end - g_begin);
+    const int npw = wave < ng ? (ng - wave + kPfWaves - 1) / kPfWaves : 0;  // passes of this wave
+    const int nt = npw * nk;                                                // its k-steps
+    if (nt > 0) {
+      const uint16_t* abase = a.groups_h + ((g_begin + wave) * nb + h) * 256 + j * 8;
+      h8 ring[kPfDepth];
+      int fp = 0, fs = 0;  // (pass, k-step) of the next load
+#pragma unroll
+      for (int u = 0; u < kPfDepth; ++u) {
+        ring[u] = ld_h8(abase + (u < nt ? fp * pstride + fs * 512 : 0));  // past the end: step 0 (never used)
+        if (++fs == nk) { fs = 0; ++fp; }
+      }
+      const f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      f32x16 c0 = zero, c1 = zero;
+      int pass = 0, step = 0;
+      for (int t0 = 0; t0 < nt; t0 += kPfDepth) {
+#pragma unroll
+        for (int u = 0; u < kPfDepth; ++u) {
+          if (t0 + u < nt) {
+            const int bb = 2 * step + h;
+            const int sl = (j ^ (bb & 31)) << 4;
+            const h8 b0 = *reinterpret_cast<const h8*>(s_b + (bb << 9) + sl);
+            const h8 b1 = *reinterpret_cast<const h8*>(s_b + ((nb + bb) << 9) + sl);
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ring[u], b0, c0, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ring[u], b1, c1, 0, 0, 0);
+            ring[u] = ld_h8(abase + (t0 + u + kPfDepth < nt ? fp * pstride + fs * 512 : 0));
+            if (++fs == nk) { fs = 0; ++fp; }
+            if (++step == nk) {
+              pf_epilogue<METRIC>(c0, c1, a.row_norms, g_begin + pass * kPfWaves + wave, h, qn0, qs0, qv0, qn1, qs1,
+                                  qv1, lk0, lp0, lk1, lp1);
+              c0 = zero;
+              c1 = zero;
+              step = 0;
+              ++pass;
+            }
+          }
+        }
+      }
+    }
+
+    // ---- per query: 16 lane lists (8 waves x 2 halves) -> slot top-slot_k + dropped-key bound ----
+    __syncthreads();  // the B image is dead
+    {
+      const int src = wave * 2 + h;
+#pragma unroll
+      for (int i = 0; i < kPfLaneK; ++i) {
+        mkey[(j * 16 + src) * kPfLaneK + i] = lk0[i];
+        mpos[(j * 16 + src) * kPfLaneK + i] = lp0[i];
+        mkey[((32 + j) * 16 + src) * kPfLaneK + i] = lk1[i];
+        mpos[((32 + j) * 16 + src) * kPfLaneK + i] = lp1[i];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int rnd = 0; rnd < 2; ++rnd) {
+      const int qi = rnd * 32 + (tid >> 4);
+      const int src = tid & 15;
+      const float* myk = mkey + (qi * 16 + src) * kPfLaneK;
+      const int* myp = mpos + (qi * 16 + src) * kPfLaneK;
+      const int64_t slot = s_slot[qi];
+      // a full lane list dropped keys >= its last entry
+      float bnd = myk[kPfLaneK - 1];
+#pragma unroll
+      for (int off = 8; off >= 1; off >>= 1) bnd = fminf(bnd, __shfl_xor(bnd, off, 16));
+      int head = 0;
+      float hk = myk[0];
+      int hp = myp[0];
+      for (int r = 0; r <= a.slot_k; ++r) {  // slot_k outputs, then the smallest key left behind
+        float bk = hk;
+        int bp = hp;
+#pragma unroll
+        for (int off = 8; off >= 1; off >>= 1) {
+          const float ok = __shfl_xor(bk, off, 16);
+          const int op = __shfl_xor(bp, off, 16);
+          if (ok < bk || (ok == bk && op < bp)) { bk = ok; bp = op; }
+        }
+        if (r < a.slot_k) {
+          if (src == 0 && slot >= 0) {
+            a.slot_key[slot * a.slot_k + r] = bk;
+            a.slot_pos[slot * a.slot_k + r] = bp;
+          }
+        } else {
+          bnd = fminf(bnd, bk);
+        }
+        if (hk == bk && hp == bp && head < kPfLaneK) {
+          ++head;
+          hk = head < kPfLaneK ? myk[head] : INFINITY;
+          hp = head < kPfLaneK ? myp[head] : INT_MAX;
+        }
+      }
+      if (src == 0 && slot >= 0) a.slot_bound[slot] = bnd;
+    }
+    __syncthreads();
+  }
+}
+
+// K11. One wave per query (4 per workgroup; every wave reaches every barrier).
+template <int METRIC>
+__global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
+  __shared__ float s_ck[4][kPfCap];
+  __shared__ int s_cp[4][kPfCap];
+  __shared__ __attribute__((aligned(16))) float s_qv[4][1024];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int64_t q = (int64_t)blockIdx.x * 4 + wv;
+  const bool live = q < a.nq;
+  const int k = a.k;
+  int64_t sb = 0, se = 0;
+  if (live) { sb = a.slot_begin[q]; se = a.slot_begin[q + 1]; }
+  const int64_t c1 = se * a.slot_k;
+
+  // phase 1: Ak = k-th smallest approximate key (running top-k over the lanes, K7's ballot insertion)
+  float mk = INFINITY, tk = INFINITY;
+  for (int64_t c = sb * a.slot_k; c < c1; c += 64) {
+    const int64_t cc = c + lane;
+    const float ck = cc < c1 ? a.slot_key[cc] : INFINITY;
+    uint64_t mask = __ballot(ck < tk);
+    while (mask) {
+      const int b = __ffsll((unsigned long long)mask) - 1;
+      const float nk = __shfl(ck, b);
+      const int pos = __popcll(__ballot(lane < k && mk <= nk));
+      const float pk = __shfl_up(mk, 1);
+      if (lane == pos) mk = nk;
+      else if (lane > pos) mk = pk;
+      tk = __shfl(mk, k - 1);
+      mask &= ~(1ull << b);
+      mask &= __ballot(ck < tk);
+    }
+  }
+  float bmin = INFINITY;
+  for (int64_t sl = sb + lane; sl < se; sl += 64) bmin = fminf(bmin, a.slot_bound[sl]);
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) bmin = fminf(bmin, __shfl_xor(bmin, off));
+
+  // the window: delta >= |approx key - pinned key| for every candidate of this query
+  const float qn = live ? a.qnorms[q] : 0.0f;
+  const float nq = sqrtf(qn) * (1.0f + 0x1p-12f);
+  const float sq = live ? a.qres[q] : 0.0f;
+  const float nx = a.x_norm_max, rx = a.x_res_max;
+  const float nxh = nx + rx, nqh = nq + sq;
+  const float ga = 2.0f * (float)a.dp * 0x1p-24f;   // fp16-product sums inside the MFMA (any order, any rounding)
+  const float gp = 1.01f * (float)a.dp * 0x1p-24f;  // the pinned fp32 fma chain
+  const float dd = nxh * sq + rx * nq + ga * nxh * nqh + gp * nx * nq;
+  float delta = METRIC == kL2 ? 2.0f * dd + 4.0f * 0x1p-24f * (nx * nx + qn) : dd;
+  delta = delta * (1.0f + 0x1p-10f) + 1e-30f;
+  const float T = tk + 2.0f * delta + fabsf(tk) * 0x1p-20f;  // +inf when fewer than k candidates
+  bool ovf = bmin < INFINITY && bmin <= T;
+
+  // phase 2: collect the window (ballot prefix, no atomics)
+  int cnt = 0;
+  for (int64_t c = sb * a.slot_k; c < c1; c += 64) {
+    const int64_t cc = c + lane;
+    const float ck = cc < c1 ? a.slot_key[cc] : INFINITY;
+    const bool take = ck <= T;
+    const uint64_t msk = __ballot(take);
+    if (take) {
+      const int at = cnt + __popcll(msk & ((1ull << lane) - 1));
+      if (at < kPfCap) { s_ck[wv][at] = ck; s_cp[wv][at] = a.slot_pos[cc]; }
+    }
+    cnt += __popcll(msk);
+  }
+  ovf = ovf || cnt > kPfCap;
+  if (live && ovf && lane == 0) {
+    const int at = atomicAdd(a.ovf_count, 1);
+    a.ovf_q[at] = q;
+  }
+  if (live && !ovf && lane == 0 && a.n_window) atomicAdd(reinterpret_cast<unsigned long long*>(a.n_window),
+                                                          (unsigned long long)cnt);
+  // the query row in LDS (zero past d), for the exact recompute
+  for (int i = lane; i < a.dp; i += 64) s_qv[wv][i] = (live && i < a.d) ? a.queries[q * a.d + i] : 0.0f;
+  __syncthreads();
+
+  // phase 3: exact keys in the pinned order (oracle orc_dot), then a bitonic sort by (key, id)
+  float P = INFINITY;
+  int64_t id = LLONG_MAX;
+  if (live && !ovf && lane < cnt) {
+    const int pos = s_cp[wv][lane];
+    const int nb = a.dp >> 3;
+    const float* rowp = a.groups + ((int64_t)(pos >> 5) * nb * kGroupRows + (pos & 31)) * 8;
+    const float* qv = s_qv[wv];
+    float acc = 0.0f;
+#pragma unroll 4
+    for (int b = 0; b < nb; ++b) {
+      const float4 x0 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * 256);
+      const float4 x1 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * 256 + 4);
+      const float4 y0 = *reinterpret_cast<const float4*>(qv + 8 * b);
+      const float4 y1 = *reinterpret_cast<const float4*>(qv + 8 * b + 4);
+      acc = fmaf(x0.x, y0.x, acc); acc = fmaf(x1.x, y1.x, acc);
+      acc = fmaf(x0.y, y0.y, acc); acc = fmaf(x1.y, y1.y, acc);
+      acc = fmaf(x0.z, y0.z, acc); acc = fmaf(x1.z, y1.z, acc);
+      acc = fmaf(x0.w, y0.w, acc); acc = fmaf(x1.w, y1.w, acc);
+    }
+    if (METRIC == kL2) {
+      const float v = fmaf(-2.0f, acc, a.row_norms[pos] + qn);
+      P = v > 0.0f ? v : 0.0f;
+    } else {
+      P = -acc;
+    }
+    id = a.row_ids[pos];
+  }
+#pragma unroll
+  for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const float oP = __shfl_xor(P, stride);
+      const int64_t oid = __shfl_xor(id, stride);
+      const bool want_min = ((lane & stride) == 0) == ((lane & size) == 0);  // ascending blocks keep min low
+      const bool o_lt = oP < P || (oP == P && oid < id);
+      const bool o_gt = oP > P || (oP == P && oid > id);
+      if (want_min ? o_lt : o_gt) { P = oP; id = oid; }
+    }
+  }
+  if (live && !ovf && lane < k) {
+    const bool valid = id != LLONG_MAX;
+    a.out_d[q * k + lane] = valid ? (METRIC == kIP ? -P : P) : (METRIC == kIP ? -INFINITY : INFINITY);
+    a.out_i[q * k + lane] = valid ? id : (int64_t)-1;
+  }
+}
+
+__device__ __forceinline__ int pf_exp_for(float m) {
+  if (!(m > 0.0f) || !(m < INFINITY)) return 0;
+  int e = 14 - ilogbf(m);  // m * 2^e in [2^14, 2^15)
+  return e < -60 ? -60 : (e > 60 ? 60 : e);
+}
+
+__device__ __forceinline__ uint16_t pf_to_half(float v, float sc, float isc, float& res) {
+  _Float16 hv = (_Float16)(v * sc);
+  if (fabsf((float)hv) < 0x1p-14f) hv = (_Float16)0.0f;  // no fp16 subnormals reach the MFMA
+  const float e = v - (float)hv * isc;                      // exact (Sterbenz, or hv == 0)
+  res = fmaf(e, e, res);
+  return __builtin_bit_cast(uint16_t, hv);
+}
+
+__global__ void k_groups_to_half(const float* __restrict__ groups, int64_t n_groups, int dp, int hx_exp,
+                                 uint16_t* __restrict__ out, unsigned* __restrict__ stats) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t g = t >> 5;
+  const int r = (int)(t & 31);
+  float res = 0.0f;
+  if (g < n_groups) {
+    const int nb = dp >> 3;
+    const float sc = ldexpf(1.0f, hx_exp), isc = ldexpf(1.0f, -hx_exp);
+    for (int b = 0; b < nb; ++b) {
+      const int64_t o = ((g * nb + b) * kGroupRows + r) * 8;
+      const float4 x0 = *reinterpret_cast<const float4*>(groups + o);
+      const float4 x1 = *reinterpret_cast<const float4*>(groups + o + 4);
+      uint4 pk;
+      pk.x = pf_to_half(x0.x, sc, isc, res) | ((unsigned)pf_to_half(x0.y, sc, isc, res) << 16);
+      pk.y = pf_to_half(x0.z, sc, isc, res) | ((unsigned)pf_to_half(x0.w, sc, isc, res) << 16);
+      pk.z = pf_to_half(x1.x, sc, isc, res) | ((unsigned)pf_to_half(x1.y, sc, isc, res) << 16);
+      pk.w = pf_to_half(x1.z, sc, isc, res) | ((unsigned)pf_to_half(x1.w, sc, isc, res) << 16);
+      *reinterpret_cast<uint4*>(out + o) = pk;
+    }
+  }
+  float rn = sqrtf(res) * (1.0f + 0x1p-12f);
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) rn = fmaxf(rn, __shfl_xor(rn, off));
+  if ((threadIdx.x & 63) == 0) atomicMax(stats, __float_as_uint(rn));
+}
+
+__global__ void k_abs_max(const float* __restrict__ x, int64_t n, unsigned* __restrict__ out) {
+  float m = 0.0f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    m = fmaxf(m, fabsf(x[i]));
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+}
+
+__global__ void k_norm_max(const float* __restrict__ x, int64_t n, unsigned* __restrict__ out) {
+  float m = 0.0f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = x[i];
+    if (v < INFINITY) m = fmaxf(m, v);
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+}
+
+// one wave per query
+__global__ __launch_bounds__(256) void k_queries_to_half(const float* __restrict__ q, int64_t nq, int d, int dp,
+                                                         int hx_exp, uint16_t* __restrict__ qh,
+                                                         float* __restrict__ qscale, float* __restrict__ qres) {
+  const int lane = threadIdx.x & 63;
+  const int64_t qi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (qi >= nq) return;
+  const float* row = q + qi * d;
+  float m = 0.0f;
+  for (int i = lane; i < d; i += 64) m = fmaxf(m, fabsf(row[i]));
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+  const int e = pf_exp_for(m);
+  const float sc = ldexpf(1.0f, e), isc = ldexpf(1.0f, -e);
+  float res = 0.0f;
+  for (int i = lane; i < dp; i += 64) qh[qi * dp + i] = pf_to_half(i < d ? row[i] : 0.0f, sc, isc, res);
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) res += __shfl_xor(res, off);
+  if (lane == 0) {
+    qscale[qi] = ldexpf(1.0f, -(hx_exp + e));
+    qres[qi] = sqrtf(res) * (1.0f + 0x1p-12f);
+  }
+}
+
+__global__ void k_scatter_results(const float* __restrict__ in_d, const int64_t* __restrict__ in_i,
+                                  const int64_t* __restrict__ rows, int64_t n, int k, float* __restrict__ out_d,
+                                  int64_t* __restrict__ out_i) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * k) return;
+  const int64_t i = t / k, c = t - i * k;
+  out_d[rows[i] * k + c] = in_d[t];
+  out_i[rows[i] * k + c] = in_i[t];
+}
+
+inline dim3 pf_grid(int64_t n, int b) { return dim3((unsigned)ceil_div(n > 0 ? n : 1, b)); }
+
+}  // namespace
+
+int pf_hx_exp(float abs_max) {
+  if (!(abs_max > 0.0f) || !(abs_max < INFINITY)) return 0;
+  const int e = 14 - ilogbf(abs_max);
+  return e < -60 ? -60 : (e > 60 ? 60 : e);
+}
+
+size_t pf_scan_lds_bytes(int dp) {
+  const size_t b = (size_t)dp * kPfQTile * 2;
+  return kPfSmall + (b > (size_t)kPfMergeBytes ? b : (size_t)kPfMergeBytes);
+}
+
+hipError_t launch_pf_scan(const PfScanArgs& a, int grid, size_t lds, hipStream_t s) {
+  if (a.dp % 64 != 0 || a.dp > 1024) return hipErrorInvalidValue;
+  static const hipError_t a0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pf_scan<kL2>),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  static const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pf_scan<kIP>),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (a0 != hipSuccess) return a0;
+  if (a1 != hipSuccess) return a1;
+  if (a.metric == kIP) hipLaunchKernelGGL(k_pf_scan<kIP>, dim3(grid), dim3(kPfThreads), lds, s, a);
+  else hipLaunchKernelGGL(k_pf_scan<kL2>, dim3(grid), dim3(kPfThreads), lds, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_pf_refine(const PfRefineArgs& a, hipStream_t s) {
+  if (a.k < 1 || a.k > kPfMaxK || a.dp > 1024) return hipErrorInvalidValue;
+  if (a.nq <= 0) return hipSuccess;
+  if (a.metric == kIP) hipLaunchKernelGGL(k_pf_refine<kIP>, pf_grid(a.nq, 4), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(k_pf_refine<kL2>, pf_grid(a.nq, 4), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_groups_to_half(const float* groups, int64_t n_groups, int dp, int hx_exp, uint16_t* out,
+                                 unsigned* stats, hipStream_t s) {
+  if (n_groups <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_groups_to_half, pf_grid(n_groups * kGroupRows, 256), dim3(256), 0, s, groups, n_groups, dp,
+                     hx_exp, out, stats);
+  return hipGetLastError();
+}
+
+hipError_t launch_abs_max(const float* x, int64_t n, unsigned* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int64_t blocks = ceil_div(n, 256) < 4096 ? ceil_div(n, 256) : 4096;
+  hipLaunchKernelGGL(k_abs_max, dim3((unsigned)blocks), dim3(256), 0, s, x, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_norm_max(const float* x, int64_t n, unsigned* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int64_t blocks = ceil_div(n, 256) < 4096 ? ceil_div(n, 256) : 4096;
+  hipLaunchKernelGGL(k_norm_max, dim3((unsigned)blocks), dim3(256), 0, s, x, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_queries_to_half(const float* q, int64_t nq, int d, int dp, int hx_exp, uint16_t* qh, float* qscale,
+                                  float* qres, hipStream_t s) {
+  if (nq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_queries_to_half, pf_grid(nq, 4), dim3(256), 0, s, q, nq, d, dp, hx_exp, qh, qscale, qres);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter_results(const float* in_d, const int64_t* in_i, const int64_t* rows, int64_t n, int k,
+                                  float* out_d, int64_t* out_i, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_scatter_results, pf_grid(n * k, 256), dim3(256), 0, s, in_d, in_i, rows, n, k, out_d, out_i);
+  return hipGetLastError();
+}
+
+}  // namespace mivs

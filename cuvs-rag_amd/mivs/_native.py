@@ -52,6 +52,7 @@ class IvfFlatParams(ctypes.Structure):
         ("add_data_on_build", c_int32),
         ("chunk_rows", c_int32),
         ("kmeans_balance", c_int32),
+        ("prefilter", c_int32),
     ]
 
 
@@ -80,6 +81,9 @@ class SearchStats(ctypes.Structure):
         ("work_items", c_int64),
         ("query_tile", c_int32),
         ("kcap", c_int32),
+        ("prefilter", c_int32),
+        ("overflow_queries", c_int64),
+        ("window_candidates", c_int64),
     ]
 
     def as_dict(self) -> dict:
@@ -128,6 +132,8 @@ _SIGS = {
                                   POINTER(c_int32)]),
     "mivs_index_last_search_stats": (c_int32, [c_void_p, POINTER(SearchStats)]),
     "mivs_index_profile_collect": (c_int32, [c_void_p, POINTER(Profile)]),
+    "mivs_index_set_prefilter": (c_int32, [c_void_p, c_void_p, c_int32]),
+    "mivs_index_get_prefilter": (c_int32, [c_void_p, POINTER(c_int32)]),
     "mivs_index_free": (None, [c_void_p]),
     "mivs_kmeans_fit": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32, c_int32,
                                   c_void_p]),

@@ -46,7 +46,8 @@ class IndexParams:
     def __init__(self, n_lists: int = 1024, metric: str = "sqeuclidean", kmeans_n_iters: int = 20,
                  kmeans_trainset_fraction: float = 0.5, add_data_on_build: bool = True,
                  adaptive_centers: bool = False, conservative_memory_allocation: bool = False,
-                 kmeans_max_train_per_list: int = 0, chunk_rows: int = 0, kmeans_balance: bool = True):
+                 kmeans_max_train_per_list: int = 0, chunk_rows: int = 0, kmeans_balance: bool = True,
+                 prefilter: bool = True):
         if int(n_lists) < 1:
             raise ValueError(f"n_lists must be >= 1, got {n_lists}")
         metric_code(metric)
@@ -62,12 +63,14 @@ class IndexParams:
         self.kmeans_max_train_per_list = int(kmeans_max_train_per_list)
         self.chunk_rows = int(chunk_rows)
         self.kmeans_balance = bool(kmeans_balance)
+        # fp16 copy of the lists for the exact-result fp16 pre-filter search
+        self.prefilter = bool(prefilter)
 
     def _c(self) -> _native.IvfFlatParams:
         return _native.IvfFlatParams(self.n_lists, metric_code(self.metric), self.kmeans_n_iters,
                                      self.kmeans_trainset_fraction, self.kmeans_max_train_per_list,
                                      1 if self.add_data_on_build else 0, self.chunk_rows,
-                                     1 if self.kmeans_balance else 0)
+                                     1 if self.kmeans_balance else 0, 1 if self.prefilter else 0)
 
     def __repr__(self):
         return (f"IndexParams(n_lists={self.n_lists}, metric={self.metric!r}, kmeans_n_iters={self.kmeans_n_iters}, "
@@ -133,6 +136,18 @@ class Index:
         _native.check(_native.lib().mivs_ivf_flat_get_list_rows(self.handle, stream_ptr(self.device), ptr(out)))
         return out
 
+    @property
+    def prefilter(self) -> bool:
+        """True when the fp16 copy of the lists is kept for the exact-result pre-filter search."""
+        v = ctypes.c_int32()
+        _native.check(_native.lib().mivs_index_get_prefilter(self.handle, ctypes.byref(v)))
+        return bool(v.value)
+
+    def set_prefilter(self, enable: bool) -> None:
+        """Build (True) or free (False) the fp16 copy; search results are identical either way."""
+        _native.check(_native.lib().mivs_index_set_prefilter(self.handle, stream_ptr(self.device),
+                                                             1 if enable else 0))
+
     def last_search_stats(self) -> dict:
         st = _native.SearchStats()
         _native.check(_native.lib().mivs_index_last_search_stats(self.handle, ctypes.byref(st)))
@@ -180,7 +195,7 @@ def build(index_params: IndexParams, dataset, resources=None, ids_offset: int = 
 
 
 def build_from_centroids(centroids, dataset, metric: str = "sqeuclidean", ids_offset: int = 0,
-                         chunk_rows: int = 0) -> Index:
+                         chunk_rows: int = 0, prefilter: bool = True) -> Index:
     """IVF-Flat lists from given centroids (FAISS IndexIVFFlat with a pre-trained quantizer)."""
     x = as_device_f32(dataset, name="dataset")
     dev = x.device.index
@@ -192,7 +207,10 @@ def build_from_centroids(centroids, dataset, metric: str = "sqeuclidean", ids_of
         _native.check(_native.lib().mivs_ivf_flat_build_from_centroids(
             dev, stream_ptr(dev), ptr(x), x.shape[0], x.shape[1], ptr(c), c.shape[0], metric_code(metric),
             int(ids_offset), int(chunk_rows), ctypes.byref(h)))
-    return Index(h.value, metric)
+    idx = Index(h.value, metric)
+    if not prefilter:
+        idx.set_prefilter(False)
+    return idx
 
 
 def search(search_params: SearchParams, index: Index, queries, k: int, neighbors=None, distances=None,

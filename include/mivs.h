@@ -51,6 +51,8 @@ typedef struct {
   int32_t chunk_rows;               /* rows per scan work item (0 = 1024) */
   int32_t kmeans_balance;           /* 1: re-seed under-filled clusters (balanced lists, the role of cuVS's
                                        balanced k-means); 0: plain Lloyd */
+  int32_t prefilter;                /* 1: also keep an fp16 copy of the lists for the exact-result fp16
+                                       pre-filter search (k <= 16); 0: fp32 scan only */
 } mivs_ivf_flat_params;
 
 /* cuvs.neighbors.ivf_pq.IndexParams (index_building_coordinator.py:398-404: n_lists, pq_bits=8,
@@ -77,6 +79,9 @@ typedef struct {
   int64_t work_items;       /* fine-scan work items */
   int32_t query_tile;       /* queries per fine-scan work item: 32 (K3 k_scan) or 64 (K3w k_scan_wide) */
   int32_t kcap;             /* register top-k capacity of the fine scan (0: DUMP mode + K8 select) */
+  int32_t prefilter;        /* 1: the fp16 pre-filter scan (K10) + exact refine (K11) served the search */
+  int64_t overflow_queries; /* queries the refine could not prove, re-run through the exact fp32 scan */
+  int64_t window_candidates;/* candidates recomputed in fp32 by the refine (sum over queries) */
 } mivs_search_stats;
 
 /* device time of the searches issued since the last collect while profiling was on
@@ -125,6 +130,11 @@ int32_t mivs_index_info(mivs_index_t index, int64_t* n_rows, int32_t* dim, int32
                         int32_t* device);
 int32_t mivs_index_last_search_stats(mivs_index_t index, mivs_search_stats* out);
 int32_t mivs_index_profile_collect(mivs_index_t index, mivs_profile* out);
+/* keep (1) or drop (0) the fp16 copy of the lists that the pre-filter search uses (ivf_flat, brute force).
+ * Results are identical either way (the refine recomputes every candidate that can reach the top-k in
+ * the pinned fp32 order); the copy costs 2 bytes per padded dimension per row of HBM. */
+int32_t mivs_index_set_prefilter(mivs_index_t index, void* stream, int32_t enable);
+int32_t mivs_index_get_prefilter(mivs_index_t index, int32_t* enabled);
 void mivs_index_free(mivs_index_t index);
 
 /* ---- IVF-PQ: replaces ivf_pq.build (index_building_coordinator.py:404, improved_multi_gpu_rag.py:137)

@@ -1,14 +1,16 @@
 #!/bin/bash
 # One GPU-box session: parity tests, then the default bench under rocprofv3 kernel-trace,
 # then two separate PMC passes (FETCH_SIZE, WRITE_SIZE) over the fine-scan kernel and their summary.
-# Usage: [WIDE=0|1] [PMC=0|1] [MICRO=0|1] bash tools/gpu_round.sh TAG
+# Usage: [PF=0|1] [WIDE=0|1] [PMC=0|1] [MICRO=0|1] [TESTS=0|1] bash tools/gpu_round.sh TAG
 set -u
 TAG=${1:-r01}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 export MIVS_SCAN_WIDE=${WIDE:-1}
-if [ "$MIVS_SCAN_WIDE" = "1" ]; then KSUB="k_scan_wide<12, 0, 4>"; KRE='k_scan_wide<12'; T=64; else KSUB="k_scan<12, 0, 8>"; KRE='k_scan<12'; T=32; fi
+export MIVS_PREFILTER=${PF:-1}
+if [ "$MIVS_PREFILTER" = "1" ]; then KSUB="k_pf_scan<0>"; KRE='k_pf_scan'; T=64_pf;
+elif [ "$MIVS_SCAN_WIDE" = "1" ]; then KSUB="k_scan_wide<12, 0, 4>"; KRE='k_scan_wide<12'; T=64; else KSUB="k_scan<12, 0, 8>"; KRE='k_scan<12'; T=32; fi
 if [ "${TESTS:-1}" = "1" ]; then
   timeout -k 10 700 python -m pytest tests -m gpu -x -q > $OUT/tests.log 2>&1
   rc=$?
