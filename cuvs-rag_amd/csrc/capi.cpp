@@ -532,8 +532,8 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   ws.pf_key.reserve(sizeof(float) * (size_t)max_slots * slot_k);
   ws.pf_pos.reserve(sizeof(int) * (size_t)max_slots * slot_k);
   ws.pf_bound.reserve(sizeof(float) * (size_t)max_slots);
-  ws.counter.reserve(16);
-  HIPCHK(hipMemsetAsync(ws.counter.p, 0, sizeof(int), s));
+  ws.counter.reserve(8 * 16 * sizeof(int));
+  HIPCHK(hipMemsetAsync(ws.counter.p, 0, 8 * 16 * sizeof(int), s));
   PfScanArgs a{};
   a.groups_h = idx->groups_h.as<uint16_t>();
   a.row_norms = L.norms.as<float>();
@@ -555,7 +555,7 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   a.dp = dp;
   a.metric = idx->metric;
   if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
-  HIPCHK(launch_pf_scan(a, cu_count(idx->device), pf_scan_lds_bytes(dp), s));
+  HIPCHK(launch_pf_scan(a, std::max(8, cu_count(idx->device) / 8 * 8), pf_scan_lds_bytes(dp, kPfChunkGroups), s));
   if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
   ws.pf_stats.reserve(32);
   HIPCHK(hipMemsetAsync(ws.pf_stats.p, 0, 32, s));

@@ -161,7 +161,7 @@ struct PfScanArgs {
   const int64_t* bucket_slot;
   const int* bucket_off;
   const int* work_off;
-  int* work_counter;
+  int* work_counter;          // [8 queues x 16] (one cache line each), zeroed before launch
   float* slot_key;            // [slots][slot_k] ascending approximate keys (+inf: empty)
   int* slot_pos;              // [slots][slot_k] row positions
   float* slot_bound;          // [slots] every dropped candidate's approximate key is >= this
@@ -192,7 +192,7 @@ struct PfRefineArgs {
 };
 
 hipError_t launch_pf_scan(const PfScanArgs& a, int grid, size_t lds, hipStream_t s);
-size_t pf_scan_lds_bytes(int dp);
+size_t pf_scan_lds_bytes(int dp, int chunk_groups);
 hipError_t launch_pf_refine(const PfRefineArgs& a, hipStream_t s);
 // fp32 groups -> fp16 groups scaled by 2^hx_exp (FTZ below the fp16 normal range), per-index maxima of
 // ||x - x_h|| and max |x| (as float bits, atomicMax) into stats[0..1] (zeroed by the caller)

@@ -29,7 +29,6 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
 constexpr int kPfWaves = 8;
 constexpr int kPfThreads = kPfWaves * 64;
-constexpr int kPfDepth = 8;  // A-operand k-steps (1 KiB wave loads) in flight per wave
 constexpr int kPfSmall = kPfQTile * 8 * 2 + kPfQTile * 4 * 2 + 16;  // s_q, s_slot, s_qn, s_qs, s_misc
 constexpr int kPfMergeBytes = kPfQTile * 16 * kPfLaneK * 8;          // [64 queries][16 lane lists][KL] (key, pos)
 
@@ -60,15 +59,14 @@ __device__ __forceinline__ float pf_key(float acc, float qs, float xn, float qn)
 }
 
 template <int METRIC>
-__device__ __forceinline__ void pf_epilogue(const f32x16& c0, const f32x16& c1, const float* __restrict__ norms,
-                                            int64_t g, int h, float qn0, float qs0, bool qv0, float qn1, float qs1,
+__device__ __forceinline__ void pf_epilogue(const f32x16& c0, const f32x16& c1, const float* __restrict__ s_gnorm,
+                                            int64_t rb, int h, float qn0, float qs0, bool qv0, float qn1, float qs1,
                                             bool qv1, float (&lk0)[kPfLaneK], int (&lp0)[kPfLaneK],
                                             float (&lk1)[kPfLaneK], int (&lp1)[kPfLaneK]) {
-  const int64_t rb = g * kGroupRows;
   float xn[16];
 #pragma unroll
   for (int q4 = 0; q4 < 4; ++q4) {
-    const float4 t = *reinterpret_cast<const float4*>(norms + rb + 8 * q4 + 4 * h);
+    const float4 t = *reinterpret_cast<const float4*>(s_gnorm + 8 * q4 + 4 * h);
     xn[4 * q4 + 0] = t.x; xn[4 * q4 + 1] = t.y; xn[4 * q4 + 2] = t.z; xn[4 * q4 + 3] = t.w;
   }
 #pragma unroll
@@ -87,11 +85,16 @@ __device__ __forceinline__ void pf_epilogue(const f32x16& c0, const f32x16& c1, 
 
 // K10. One workgroup (8 waves) per CU, persistent over (list, chunk, 64-query tile) work items.
 // The query tile stays in LDS for the whole chunk as the B operand ([2][dp/8][32] x 16 B, the
-// 32-query slot XOR-swizzled by the block index: conflict-free staging writes and B reads).
-// Each wave streams its own 32-row groups (pass p: group g_begin + 8p + wave) as the A operand
-// straight from HBM: one 1 KiB contiguous wave load per k-step, kPfDepth k-steps in flight across
-// pass boundaries; 2 MFMAs (the two 32-query column tiles) per load.
-template <int METRIC>
+// 32-query slot XOR-swizzled by the block index: conflict-free staging writes and B reads), next to
+// the chunk's row norms. Each wave streams its own 32-row groups (pass p: group g_begin + 8p + wave)
+// as the A operand straight from HBM: one 1 KiB contiguous wave load per k-step, D k-steps in
+// flight across pass boundaries (a ring of D registers refilled right after their MFMAs); 2 MFMAs
+// (the two 32-query column tiles) per load.
+// Work items are dealt from 8 queues, one per XCD group (blockIdx % 8): queue g holds the g-th
+// eighth of the (list, chunk, tile)-ordered items, so the query tiles of one chunk run at the same
+// time on CUs sharing an L2 and all but the first read the chunk's rows as L2 hits. A workgroup
+// whose queue is empty takes items from the next queues.
+template <int METRIC, int D>
 __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int64_t* s_q = reinterpret_cast<int64_t*>(smem);          // [64] query ids (-1: empty)
@@ -99,23 +102,37 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
   float* s_qn = reinterpret_cast<float*>(s_slot + kPfQTile);  // [64]
   float* s_qs = s_qn + kPfQTile;                              // [64]
   int* s_misc = reinterpret_cast<int*>(s_qs + kPfQTile);
-  char* s_b = smem + kPfSmall;
+  float* s_norm = reinterpret_cast<float*>(smem + kPfSmall);  // [chunk_groups * 32]
+  char* s_b = smem + kPfSmall + a.chunk_groups * kGroupRows * 4;
   float* mkey = reinterpret_cast<float*>(s_b);
   int* mpos = reinterpret_cast<int*>(mkey + kPfQTile * 16 * kPfLaneK);
 
   const int dp = a.dp;
   const int nb = dp >> 3;  // 8-dim blocks
-  const int nk = dp >> 4;  // 16-dim k-steps
+  const int nk = dp >> 4;  // 16-dim k-steps (a multiple of D)
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: the k-loop is a scalar loop
   const int j = lane & 31;
   const int h = lane >> 5;
   const int total = a.work_off[a.n_lists];
+  const int grp = blockIdx.x & 7;
   const int64_t pstride = (int64_t)kPfWaves * nb * 256;  // halves between a wave's consecutive groups
+  if (tid == 0) s_misc[1] = 0;                            // queues exhausted so far
 
   for (;;) {
-    if (tid == 0) s_misc[0] = atomicAdd(a.work_counter, 1);
+    if (tid == 0) {
+      int qs = s_misc[1], w = total;
+      while (qs < 8) {
+        const int g = (grp + qs) & 7;
+        const int lo_g = (int)((int64_t)total * g / 8), hi_g = (int)((int64_t)total * (g + 1) / 8);
+        const int i = atomicAdd(a.work_counter + 16 * g, 1);
+        if (lo_g + i < hi_g) { w = lo_g + i; break; }
+        ++qs;
+      }
+      s_misc[1] = qs;
+      s_misc[0] = w;
+    }
     __syncthreads();
     const int w = s_misc[0];
     if (w >= total) break;
@@ -136,6 +153,7 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
     const int64_t g_end = g_begin + a.chunk_groups < g_lim ? g_begin + a.chunk_groups : g_lim;
     const int e0 = a.bucket_off[l] + tile * kPfQTile;
     const int nqt = m - tile * kPfQTile < kPfQTile ? m - tile * kPfQTile : kPfQTile;
+    const int ng = (int)(g_end - g_begin);
 
     if (tid < kPfQTile) {
       if (tid < nqt) {
@@ -151,6 +169,7 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
         s_qs[tid] = 0.0f;
       }
     }
+    for (int i = tid; i < ng * kGroupRows; i += kPfThreads) s_norm[i] = a.row_norms[g_begin * kGroupRows + i];
     __syncthreads();
     // stage the fp16 query tile: nb/8 16-B pieces per thread (dp % 64 == 0), loads batched by 4
     {
@@ -181,42 +200,52 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
     const float qn0 = s_qn[j], qn1 = s_qn[32 + j], qs0 = s_qs[j], qs1 = s_qs[32 + j];
     const bool qv0 = s_q[j] >= 0, qv1 = s_q[32 + j] >= 0;
 
-    const int ng = (int)(g_end - g_begin);
     const int npw = wave < ng ? (ng - wave + kPfWaves - 1) / kPfWaves : 0;  // passes of this wave
-    const int nt = npw * nk;                                                // its k-steps
-    if (nt > 0) {
+    if (npw > 0) {
       const uint16_t* abase = a.groups_h + ((g_begin + wave) * nb + h) * 256 + j * 8;
-      h8 ring[kPfDepth];
-      int fp = 0, fs = 0;  // (pass, k-step) of the next load
+      const uint16_t* nptr = abase;  // pass base of the next load
+      int ls = 0, lpass = 0;         // k-step / pass of the next load (past the end: re-read the last pass)
+      h8 ring[D];
+      // the ring holds one block of D k-steps; (nptr, ls) = the next block to load (nk % D == 0)
 #pragma unroll
-      for (int u = 0; u < kPfDepth; ++u) {
-        ring[u] = ld_h8(abase + (u < nt ? fp * pstride + fs * 512 : 0));  // past the end: step 0 (never used)
-        if (++fs == nk) { fs = 0; ++fp; }
+      for (int u = 0; u < D; ++u) {
+        ring[u] = ld_h8(nptr + (ls + u) * 512);
+        __builtin_amdgcn_sched_barrier(0);  // issue in ring order: the loop header then waits vmcnt(D-1)
       }
+      ls += D;
+      if (ls == nk) { ls = 0; if (++lpass < npw) nptr += pstride; }
       const f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       f32x16 c0 = zero, c1 = zero;
-      int pass = 0, step = 0;
-      for (int t0 = 0; t0 < nt; t0 += kPfDepth) {
+      int p = 0, s = 0;
+      // ONE flat loop over (pass, k-step) in blocks of D (nk % D == 0, so a pass ends on a block end):
+      // the compiler then keeps the ring's loads counted (vmcnt(D-1)) across pass boundaries
+      for (int t0 = 0; t0 < npw * nk; t0 += D) {
 #pragma unroll
-        for (int u = 0; u < kPfDepth; ++u) {
-          if (t0 + u < nt) {
-            const int bb = 2 * step + h;
-            const int sl = (j ^ (bb & 31)) << 4;
-            const h8 b0 = *reinterpret_cast<const h8*>(s_b + (bb << 9) + sl);
-            const h8 b1 = *reinterpret_cast<const h8*>(s_b + ((nb + bb) << 9) + sl);
-            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ring[u], b0, c0, 0, 0, 0);
-            c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ring[u], b1, c1, 0, 0, 0);
-            ring[u] = ld_h8(abase + (t0 + u + kPfDepth < nt ? fp * pstride + fs * 512 : 0));
-            if (++fs == nk) { fs = 0; ++fp; }
-            if (++step == nk) {
-              pf_epilogue<METRIC>(c0, c1, a.row_norms, g_begin + pass * kPfWaves + wave, h, qn0, qs0, qv0, qn1, qs1,
-                                  qv1, lk0, lp0, lk1, lp1);
-              c0 = zero;
-              c1 = zero;
-              step = 0;
-              ++pass;
-            }
-          }
+        for (int u = 0; u < D; ++u) {
+          const int bb = 2 * (s + u) + h;
+          const int sl = (j ^ (bb & 31)) << 4;
+          const h8 b0 = *reinterpret_cast<const h8*>(s_b + (bb << 9) + sl);
+          const h8 b1 = *reinterpret_cast<const h8*>(s_b + ((nb + bb) << 9) + sl);
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ring[u], b0, c0, 0, 0, 0);
+          c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ring[u], b1, c1, 0, 0, 0);
+          ring[u] = ld_h8(nptr + (ls + u) * 512);
+          // pin the per-k-step issue order (2 DS reads, 2 MFMAs, then the refill) so the refill of
+          // ring[u] is issued right after its last use and D loads stay in flight
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+        }
+        ls += D;
+        if (ls == nk) { ls = 0; if (++lpass < npw) nptr += pstride; }
+        s += D;
+        if (s == nk) {
+          const int lg = p * kPfWaves + wave;  // group within the chunk
+          pf_epilogue<METRIC>(c0, c1, s_norm + lg * kGroupRows, (g_begin + lg) * kGroupRows, h, qn0, qs0, qv0,
+                              qn1, qs1, qv1, lk0, lp0, lk1, lp1);
+          c0 = zero;
+          c1 = zero;
+          s = 0;
+          ++p;
         }
       }
     }
@@ -505,22 +534,26 @@ int pf_hx_exp(float abs_max) {
   return e < -60 ? -60 : (e > 60 ? 60 : e);
 }
 
-size_t pf_scan_lds_bytes(int dp) {
+size_t pf_scan_lds_bytes(int dp, int chunk_groups) {
   const size_t b = (size_t)dp * kPfQTile * 2;
-  return kPfSmall + (b > (size_t)kPfMergeBytes ? b : (size_t)kPfMergeBytes);
+  return kPfSmall + (size_t)chunk_groups * kGroupRows * 4 + (b > (size_t)kPfMergeBytes ? b : (size_t)kPfMergeBytes);
 }
 
-hipError_t launch_pf_scan(const PfScanArgs& a, int grid, size_t lds, hipStream_t s) {
-  if (a.dp % 64 != 0 || a.dp > 1024) return hipErrorInvalidValue;
-  static const hipError_t a0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pf_scan<kL2>),
-                                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  static const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pf_scan<kIP>),
-                                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  if (a0 != hipSuccess) return a0;
-  if (a1 != hipSuccess) return a1;
-  if (a.metric == kIP) hipLaunchKernelGGL(k_pf_scan<kIP>, dim3(grid), dim3(kPfThreads), lds, s, a);
-  else hipLaunchKernelGGL(k_pf_scan<kL2>, dim3(grid), dim3(kPfThreads), lds, s, a);
+template <int METRIC, int D>
+static hipError_t launch_pf_scan_md(const PfScanArgs& a, int grid, size_t lds, hipStream_t s) {
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pf_scan<METRIC, D>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL((k_pf_scan<METRIC, D>), dim3(grid), dim3(kPfThreads), lds, s, a);
   return hipGetLastError();
+}
+
+// grid: a multiple of 8 (one queue per XCD group); the work counters (8 x 16 ints) are zeroed by the caller
+hipError_t launch_pf_scan(const PfScanArgs& a, int grid, size_t lds, hipStream_t s) {
+  if (a.dp % 64 != 0 || a.dp > 1024 || lds > 160 * 1024) return hipErrorInvalidValue;
+  const bool d8 = (a.dp / 16) % 8 == 0;  // k-steps in flight per wave: 8 when the k-loop allows, else 4
+  if (a.metric == kIP) return d8 ? launch_pf_scan_md<kIP, 8>(a, grid, lds, s) : launch_pf_scan_md<kIP, 4>(a, grid, lds, s);
+  return d8 ? launch_pf_scan_md<kL2, 8>(a, grid, lds, s) : launch_pf_scan_md<kL2, 4>(a, grid, lds, s);
 }
 
 hipError_t launch_pf_refine(const PfRefineArgs& a, hipStream_t s) {
