@@ -159,7 +159,7 @@ struct Workspace {
   Buf qn, bucket_q, bucket_slot, bucket_off, work_off, counter, part_d, part_i, slot_begin, probes_d, probes_i,
       counts, fill, qp_slots, scan_tmp, gmerge;
   // fp16 pre-filter path (K10 / K11) and its exact-scan fallback
-  Buf qh, qscale, qres, pf_key, pf_pos, pf_bound, pf_stats, ovf_q, ovf_rows, ovf_d, ovf_i;
+  Buf qh, qscale, qres, qtheta, pf_key, pf_pos, pf_bound, pf_stats, ovf_q, ovf_rows, ovf_d, ovf_i;
 };
 
 // hipEvent pairs recorded on the caller's stream around the pipeline stages of
@@ -554,6 +554,13 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   a.slot_k = slot_k;
   a.dp = dp;
   a.metric = idx->metric;
+  a.qres = ws.qres.as<float>();
+  a.x_norm_max = idx->x_norm_max;
+  a.x_res_max = idx->x_res_max;
+  ws.qtheta.reserve(sizeof(unsigned) * nq);
+  HIPCHK(launch_fill_i32(ws.qtheta.as<int>(), nq, (int)kPfOrdInf, s));
+  a.qtheta = ws.qtheta.as<unsigned>();
+  a.k = k;
   if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
   HIPCHK(launch_pf_scan(a, std::max(8, cu_count(idx->device) / 8 * 8), pf_scan_lds_bytes(dp, kPfChunkGroups), s));
   if (pr) HIPCHK(hipEventRecord(pr->e[2], s));

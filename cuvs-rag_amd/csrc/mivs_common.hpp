@@ -167,6 +167,11 @@ struct PfScanArgs {
   float* slot_bound;          // [slots] every dropped candidate's approximate key is >= this
   int slot_k;
   int dp, metric;
+  const float* qres;          // [nq] ||q - q_h|| (the window bound theta of the scan)
+  float x_norm_max, x_res_max;
+  unsigned* qtheta;           // [nq] order-mapped window bound per query, shared by all work items
+                              // (set to the mapping of +inf before the launch)
+  int k;
 };
 
 struct PfRefineArgs {
@@ -194,6 +199,7 @@ struct PfRefineArgs {
 hipError_t launch_pf_scan(const PfScanArgs& a, int grid, size_t lds, hipStream_t s);
 size_t pf_scan_lds_bytes(int dp, int chunk_groups);
 hipError_t launch_pf_refine(const PfRefineArgs& a, hipStream_t s);
+constexpr unsigned kPfOrdInf = 0xFF800000u;  // order mapping of +inf (qtheta's initial value)
 // fp32 groups -> fp16 groups scaled by 2^hx_exp (FTZ below the fp16 normal range), per-index maxima of
 // ||x - x_h|| and max |x| (as float bits, atomicMax) into stats[0..1] (zeroed by the caller)
 hipError_t launch_groups_to_half(const float* groups, int64_t n_groups, int dp, int hx_exp, uint16_t* out,

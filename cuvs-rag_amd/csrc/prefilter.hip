@@ -18,6 +18,7 @@
 //        If a dropped key could be inside the window (bound <= T) or the window holds
 //        more than kPfCap candidates, the query is listed for the exact scan.
 #include <climits>
+#include <cstdlib>
 
 #include "mivs_common.hpp"
 
@@ -58,10 +59,42 @@ __device__ __forceinline__ float pf_key(float acc, float qs, float xn, float qn)
   return xn < INFINITY ? -v : INFINITY;
 }
 
+// delta >= |approximate key - pinned fp32 key| for every (row, query q) of the index:
+//   |x.q - x_h.q_h| <= |x_h||q - q_h| + |x - x_h||q|   (Cauchy-Schwarz on the fp16 rounding residuals)
+//   + 2 dp u |x_h||q_h|  (the fp16-product sum inside the MFMA, any order and rounding)
+//   + 1.01 dp u |x||q|   (the pinned fp32 fma chain);  L2 keys: x2, plus the roundings of the key itself.
+// Index-wide maxima of |x| and |x - x_h| stand in for the row's own values.
+template <int METRIC>
+__device__ __forceinline__ float pf_delta(float qn, float qres, float x_norm_max, float x_res_max, int dp) {
+  const float nq = sqrtf(qn) * (1.0f + 0x1p-12f);
+  const float nx = x_norm_max, rx = x_res_max;
+  const float nxh = nx + rx, nqh = nq + qres;
+  const float ga = 2.0f * (float)dp * 0x1p-24f;
+  const float gp = 1.01f * (float)dp * 0x1p-24f;
+  const float dd = nxh * qres + rx * nq + ga * nxh * nqh + gp * nx * nq;
+  const float delta = METRIC == kL2 ? 2.0f * dd + 4.0f * 0x1p-24f * (nx * nx + qn) : dd;
+  return delta * (1.0f + 0x1p-10f) + 1e-30f;
+}
+
+// order-preserving float <-> uint32 (atomicMin over signed keys)
+__device__ __forceinline__ unsigned pf_ord(float x) {
+  const unsigned b = __float_as_uint(x);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float pf_unord(unsigned u) {
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
+}
+
+// the refine window above a k-th approximate key kth: every candidate whose pinned key can reach the
+// top-k has approximate key <= pf_window(Ak). Monotone in kth, so any kth' >= Ak gives a window >= it.
+__device__ __forceinline__ float pf_window(float kth, float delta) {
+  return kth + 2.0f * delta + fabsf(kth) * 0x1p-20f;
+}
+
 template <int METRIC>
 __device__ __forceinline__ void pf_epilogue(const f32x16& c0, const f32x16& c1, const float* __restrict__ s_gnorm,
-                                            int64_t rb, int h, float qn0, float qs0, bool qv0, float qn1, float qs1,
-                                            bool qv1, float (&lk0)[kPfLaneK], int (&lp0)[kPfLaneK],
+                                            int64_t rb, int h, float qn0, float qs0, float th0, float qn1,
+                                            float qs1, float th1, float (&lk0)[kPfLaneK], int (&lp0)[kPfLaneK],
                                             float (&lk1)[kPfLaneK], int (&lp1)[kPfLaneK]) {
   float xn[16];
 #pragma unroll
@@ -69,24 +102,39 @@ __device__ __forceinline__ void pf_epilogue(const f32x16& c0, const f32x16& c1, 
     const float4 t = *reinterpret_cast<const float4*>(s_gnorm + 8 * q4 + 4 * h);
     xn[4 * q4 + 0] = t.x; xn[4 * q4 + 1] = t.y; xn[4 * q4 + 2] = t.z; xn[4 * q4 + 3] = t.w;
   }
+  // a key is kept if it beats the lane list AND lies within the query's window bound theta
+  // (th = -inf for empty query slots: nothing is kept)
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int pos = (int)(rb + (r & 3) + 8 * (r >> 2) + 4 * h);
-    if (qv0) {
-      const float key = pf_key<METRIC>(c0[r], qs0, xn[r], qn0);
-      if (key < lk0[kPfLaneK - 1]) pf_insert<kPfLaneK>(lk0, lp0, key, pos);
-    }
-    if (qv1) {
-      const float key = pf_key<METRIC>(c1[r], qs1, xn[r], qn1);
-      if (key < lk1[kPfLaneK - 1]) pf_insert<kPfLaneK>(lk1, lp1, key, pos);
-    }
+    const float k0 = pf_key<METRIC>(c0[r], qs0, xn[r], qn0);
+    if (k0 < lk0[kPfLaneK - 1] && k0 <= th0) pf_insert<kPfLaneK>(lk0, lp0, k0, pos);
+    const float k1 = pf_key<METRIC>(c1[r], qs1, xn[r], qn1);
+    if (k1 < lk1[kPfLaneK - 1] && k1 <= th1) pf_insert<kPfLaneK>(lk1, lp1, k1, pos);
   }
 }
 
+// theta of a query from its 16 lane lists' last entries (s_l8[16]): with two full lists whose last
+// entries are v1 <= v2, at least 16 >= k kept keys are <= v2, so the query's k-th approximate key over
+// the whole search is <= v2 and the refine window is <= pf_window(v2).
+__device__ __forceinline__ float pf_theta(const float* __restrict__ l8, float delta) {
+  float m1 = INFINITY, m2 = INFINITY;
+#pragma unroll
+  for (int i = 0; i < 16; i += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(l8 + i);
+    const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      m2 = fminf(m2, fmaxf(m1, e[t]));
+      m1 = fminf(m1, e[t]);
+    }
+  }
+  return m2 < INFINITY ? pf_window(m2, delta) : INFINITY;
+}
+
 // K10. One workgroup (8 waves) per CU, persistent over (list, chunk, 64-query tile) work items.
-// The query tile stays in LDS for the whole chunk as the B operand ([2][dp/8][32] x 16 B, the
-// 32-query slot XOR-swizzled by the block index: conflict-free staging writes and B reads), next to
-// the chunk's row norms. Each wave streams its own 32-row groups (pass p: group g_begin + 8p + wave)
+// The query tile stays in LDS for the whole chunk as the B operand ([2][dp/8][32] x 16 B: each
+// k-step's operand is one contiguous 1 KiB wave read), next to the chunk's row norms. Each wave streams its own 32-row groups (pass p: group g_begin + 8p + wave)
 // as the A operand straight from HBM: one 1 KiB contiguous wave load per k-step, D k-steps in
 // flight across pass boundaries (a ring of D registers refilled right after their MFMAs); 2 MFMAs
 // (the two 32-query column tiles) per load.
@@ -102,8 +150,11 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
   float* s_qn = reinterpret_cast<float*>(s_slot + kPfQTile);  // [64]
   float* s_qs = s_qn + kPfQTile;                              // [64]
   int* s_misc = reinterpret_cast<int*>(s_qs + kPfQTile);
-  float* s_norm = reinterpret_cast<float*>(smem + kPfSmall);  // [chunk_groups * 32]
-  char* s_b = smem + kPfSmall + a.chunk_groups * kGroupRows * 4;
+  float* s_dl = reinterpret_cast<float*>(smem + kPfSmall);    // [64] per-query window delta
+  float* s_th = s_dl + kPfQTile;                                // [64] theta at item start
+  float* s_l8 = s_th + kPfQTile;                                // [64][16] lane lists' last entries
+  float* s_norm = s_l8 + kPfQTile * 16;                         // [chunk_groups * 32]
+  char* s_b = reinterpret_cast<char*>(s_norm + a.chunk_groups * kGroupRows);
   float* mkey = reinterpret_cast<float*>(s_b);
   int* mpos = reinterpret_cast<int*>(mkey + kPfQTile * 16 * kPfLaneK);
 
@@ -160,35 +211,44 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
         const int64_t q = a.bucket_q[e0 + tid];
         s_q[tid] = q;
         s_slot[tid] = a.bucket_slot[e0 + tid] + chunk;
-        s_qn[tid] = a.qnorms[q];
+        const float qn = a.qnorms[q];
+        s_qn[tid] = qn;
         s_qs[tid] = a.qscale[q];
+        s_dl[tid] = pf_delta<METRIC>(qn, a.qres[q], a.x_norm_max, a.x_res_max, dp);
+        s_th[tid] = pf_unord(__hip_atomic_load(a.qtheta + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
       } else {
         s_q[tid] = -1;
         s_slot[tid] = -1;
         s_qn[tid] = INFINITY;
         s_qs[tid] = 0.0f;
+        s_dl[tid] = 0.0f;
+        s_th[tid] = -INFINITY;
       }
     }
+    for (int i = tid; i < kPfQTile * 16; i += kPfThreads) s_l8[i] = INFINITY;
     for (int i = tid; i < ng * kGroupRows; i += kPfThreads) s_norm[i] = a.row_norms[g_begin * kGroupRows + i];
     __syncthreads();
-    // stage the fp16 query tile: nb/8 16-B pieces per thread (dp % 64 == 0), loads batched by 4
+    // stage the fp16 query tile. B image: [2 query groups][nb blocks][32 queries] x 16 B, so that the
+    // operand of (group t, k-step s) for lane (j, h) sits at t*nb*512 + s*1024 + lane*16: one contiguous
+    // 1 KiB wave read (conflict-free) at an immediate offset per k-step. Piece i of the image is
+    // written by thread i mod 512 (linear, conflict-free); its source is a 16-B piece of query row
+    // (i/32/nb)*32 + i%32. nb/8 pieces per thread (dp % 64 == 0), loads batched by 4.
     {
       const int per = nb >> 3;
       for (int i0 = 0; i0 < per; i0 += 4) {
         uint4 v[4];
-        int dst[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int i = tid + (i0 + u) * kPfThreads;
-          const int qi = i / nb, b = i - qi * nb;
-          const int64_t q = (i0 + u < per) ? s_q[qi] : -1;
+          const int gb = i >> 5;
+          const int qg = gb / nb, b = gb - qg * nb;
+          const int64_t q = (i0 + u < per) ? s_q[qg * 32 + (i & 31)] : -1;
           v[u] = make_uint4(0u, 0u, 0u, 0u);
           if (q >= 0) v[u] = *reinterpret_cast<const uint4*>(a.qh + q * dp + 8 * b);
-          dst[u] = (i0 + u < per) ? (((qi >> 5) * nb + b) << 5) + ((qi & 31) ^ (b & 31)) : -1;
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-          if (dst[u] >= 0) *reinterpret_cast<uint4*>(s_b + (size_t)dst[u] * 16) = v[u];
+          if (i0 + u < per) *reinterpret_cast<uint4*>(s_b + (size_t)(tid + (i0 + u) * kPfThreads) * 16) = v[u];
       }
     }
     __syncthreads();
@@ -198,8 +258,13 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
 #pragma unroll
     for (int t = 0; t < kPfLaneK; ++t) { lk0[t] = INFINITY; lp0[t] = INT_MAX; lk1[t] = INFINITY; lp1[t] = INT_MAX; }
     const float qn0 = s_qn[j], qn1 = s_qn[32 + j], qs0 = s_qs[j], qs1 = s_qs[32 + j];
-    const bool qv0 = s_q[j] >= 0, qv1 = s_q[32 + j] >= 0;
+    const float dl0 = s_dl[j], dl1 = s_dl[32 + j];
+    // per-query window bound theta (refreshed after every pass from all lane lists); -inf: empty slot
+    // starts from the query's window bound over the items finished so far (qtheta, all workgroups)
+    float th0 = s_th[j], th1 = s_th[32 + j];
+    const int src = wave * 2 + h;  // this lane's list index among the query's 16
 
+    const char* s_bl = s_b + lane * 16;  // this lane's B operand at k-step s: + s * 1024 (+ nb * 512: group 1)
     const int npw = wave < ng ? (ng - wave + kPfWaves - 1) / kPfWaves : 0;  // passes of this wave
     if (npw > 0) {
       const uint16_t* abase = a.groups_h + ((g_begin + wave) * nb + h) * 256 + j * 8;
@@ -222,10 +287,8 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
       for (int t0 = 0; t0 < npw * nk; t0 += D) {
 #pragma unroll
         for (int u = 0; u < D; ++u) {
-          const int bb = 2 * (s + u) + h;
-          const int sl = (j ^ (bb & 31)) << 4;
-          const h8 b0 = *reinterpret_cast<const h8*>(s_b + (bb << 9) + sl);
-          const h8 b1 = *reinterpret_cast<const h8*>(s_b + ((nb + bb) << 9) + sl);
+          const h8 b0 = *reinterpret_cast<const h8*>(s_bl + (s + u) * 1024);
+          const h8 b1 = *reinterpret_cast<const h8*>(s_bl + nb * 512 + (s + u) * 1024);
           c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ring[u], b0, c0, 0, 0, 0);
           c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ring[u], b1, c1, 0, 0, 0);
           ring[u] = ld_h8(nptr + (ls + u) * 512);
@@ -240,8 +303,14 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
         s += D;
         if (s == nk) {
           const int lg = p * kPfWaves + wave;  // group within the chunk
-          pf_epilogue<METRIC>(c0, c1, s_norm + lg * kGroupRows, (g_begin + lg) * kGroupRows, h, qn0, qs0, qv0,
-                              qn1, qs1, qv1, lk0, lp0, lk1, lp1);
+          pf_epilogue<METRIC>(c0, c1, s_norm + lg * kGroupRows, (g_begin + lg) * kGroupRows, h, qn0, qs0, th0,
+                              qn1, qs1, th1, lk0, lp0, lk1, lp1);
+          // publish this lane's list ends, refresh theta from all 16 (no barrier: every value ever
+          // stored is the end of a real list, so a stale read only gives a looser, still valid theta)
+          s_l8[j * 16 + src] = lk0[kPfLaneK - 1];
+          s_l8[(32 + j) * 16 + src] = lk1[kPfLaneK - 1];
+          th0 = fminf(th0, pf_theta(s_l8 + j * 16, dl0));
+          th1 = fminf(th1, pf_theta(s_l8 + (32 + j) * 16, dl1));
           c0 = zero;
           c1 = zero;
           s = 0;
@@ -253,7 +322,6 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
     // ---- per query: 16 lane lists (8 waves x 2 halves) -> slot top-slot_k + dropped-key bound ----
     __syncthreads();  // the B image is dead
     {
-      const int src = wave * 2 + h;
 #pragma unroll
       for (int i = 0; i < kPfLaneK; ++i) {
         mkey[(j * 16 + src) * kPfLaneK + i] = lk0[i];
@@ -270,8 +338,12 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
       const float* myk = mkey + (qi * 16 + src) * kPfLaneK;
       const int* myp = mpos + (qi * 16 + src) * kPfLaneK;
       const int64_t slot = s_slot[qi];
-      // a full lane list dropped keys >= its last entry
+      // a full lane list dropped keys >= its last entry; keys above theta were dropped, and every
+      // lane's theta is >= the one from the final list ends
       float bnd = myk[kPfLaneK - 1];
+      // (theta drops are keys > theta: the bound is the next float up, so a theta equal to the
+      // refine's window -- the common case when one slot holds the whole top-k -- is no overflow)
+      if (src == 0) bnd = fminf(bnd, nextafterf(fminf(s_th[qi], pf_theta(s_l8 + qi * 16, s_dl[qi])), INFINITY));
 #pragma unroll
       for (int off = 8; off >= 1; off >>= 1) bnd = fminf(bnd, __shfl_xor(bnd, off, 16));
       int head = 0;
@@ -290,6 +362,9 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
           if (src == 0 && slot >= 0) {
             a.slot_key[slot * a.slot_k + r] = bk;
             a.slot_pos[slot * a.slot_k + r] = bp;
+            // the query's k-th key over the whole search is <= this slot's k-th: tighten its theta
+            if (r == a.k - 1 && bk < INFINITY)
+              atomicMin(a.qtheta + s_q[qi], pf_ord(pf_window(bk, s_dl[qi])));
           }
         } else {
           bnd = fminf(bnd, bk);
@@ -346,16 +421,8 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
 
   // the window: delta >= |approx key - pinned key| for every candidate of this query
   const float qn = live ? a.qnorms[q] : 0.0f;
-  const float nq = sqrtf(qn) * (1.0f + 0x1p-12f);
-  const float sq = live ? a.qres[q] : 0.0f;
-  const float nx = a.x_norm_max, rx = a.x_res_max;
-  const float nxh = nx + rx, nqh = nq + sq;
-  const float ga = 2.0f * (float)a.dp * 0x1p-24f;   // fp16-product sums inside the MFMA (any order, any rounding)
-  const float gp = 1.01f * (float)a.dp * 0x1p-24f;  // the pinned fp32 fma chain
-  const float dd = nxh * sq + rx * nq + ga * nxh * nqh + gp * nx * nq;
-  float delta = METRIC == kL2 ? 2.0f * dd + 4.0f * 0x1p-24f * (nx * nx + qn) : dd;
-  delta = delta * (1.0f + 0x1p-10f) + 1e-30f;
-  const float T = tk + 2.0f * delta + fabsf(tk) * 0x1p-20f;  // +inf when fewer than k candidates
+  const float delta = pf_delta<METRIC>(qn, live ? a.qres[q] : 0.0f, a.x_norm_max, a.x_res_max, a.dp);
+  const float T = pf_window(tk, delta);  // +inf when fewer than k candidates
   bool ovf = bmin < INFINITY && bmin <= T;
 
   // phase 2: collect the window (ballot prefix, no atomics)
@@ -536,7 +603,8 @@ int pf_hx_exp(float abs_max) {
 
 size_t pf_scan_lds_bytes(int dp, int chunk_groups) {
   const size_t b = (size_t)dp * kPfQTile * 2;
-  return kPfSmall + (size_t)chunk_groups * kGroupRows * 4 + (b > (size_t)kPfMergeBytes ? b : (size_t)kPfMergeBytes);
+  return kPfSmall + (size_t)kPfQTile * 18 * 4 + (size_t)chunk_groups * kGroupRows * 4 +
+         (b > (size_t)kPfMergeBytes ? b : (size_t)kPfMergeBytes);
 }
 
 template <int METRIC, int D>
@@ -551,9 +619,16 @@ static hipError_t launch_pf_scan_md(const PfScanArgs& a, int grid, size_t lds, h
 // grid: a multiple of 8 (one queue per XCD group); the work counters (8 x 16 ints) are zeroed by the caller
 hipError_t launch_pf_scan(const PfScanArgs& a, int grid, size_t lds, hipStream_t s) {
   if (a.dp % 64 != 0 || a.dp > 1024 || lds > 160 * 1024) return hipErrorInvalidValue;
-  const bool d8 = (a.dp / 16) % 8 == 0;  // k-steps in flight per wave: 8 when the k-loop allows, else 4
-  if (a.metric == kIP) return d8 ? launch_pf_scan_md<kIP, 8>(a, grid, lds, s) : launch_pf_scan_md<kIP, 4>(a, grid, lds, s);
-  return d8 ? launch_pf_scan_md<kL2, 8>(a, grid, lds, s) : launch_pf_scan_md<kL2, 4>(a, grid, lds, s);
+  // k-steps in flight per wave: 16 when the k-loop allows (the A stream is latency-bound), else 8 or 4
+  const int nk = a.dp / 16;
+  const int dsel = getenv("MIVS_PF_DEPTH") ? atoi(getenv("MIVS_PF_DEPTH")) : 16;
+  const int D = (dsel >= 16 && nk % 16 == 0) ? 16 : ((dsel >= 8 && nk % 8 == 0) ? 8 : 4);
+  if (a.metric == kIP) {
+    if (D == 16) return launch_pf_scan_md<kIP, 16>(a, grid, lds, s);
+    return D == 8 ? launch_pf_scan_md<kIP, 8>(a, grid, lds, s) : launch_pf_scan_md<kIP, 4>(a, grid, lds, s);
+  }
+  if (D == 16) return launch_pf_scan_md<kL2, 16>(a, grid, lds, s);
+  return D == 8 ? launch_pf_scan_md<kL2, 8>(a, grid, lds, s) : launch_pf_scan_md<kL2, 4>(a, grid, lds, s);
 }
 
 hipError_t launch_pf_refine(const PfRefineArgs& a, hipStream_t s) {
