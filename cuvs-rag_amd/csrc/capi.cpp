@@ -202,7 +202,8 @@ struct mivs_index_s {
   Buf groups_h;
   int hx_exp = 0;
   float x_norm_max = 0.0f, x_res_max = 0.0f;
-  std::vector<int64_t> pf_top_chunks_prefix;  // as ListSet::top_chunks_prefix, for kPfChunkGroups
+  int pf_G = kPfChunkGroups;                  // groups per K10 work item
+  std::vector<int64_t> pf_top_chunks_prefix;  // as ListSet::top_chunks_prefix, for pf_G
   std::mutex mu;
   Workspace ws;
   Profiler prof;
@@ -505,7 +506,9 @@ void pf_enable(mivs_index_s* idx, hipStream_t s) {
   idx->x_norm_max = sqrtf(normmax) * (1.0f + 0x1p-12f);
   idx->x_res_max = resmax;
   std::vector<int64_t> c(L.n_lists);
-  for (int l = 0; l < L.n_lists; ++l) c[l] = L.chunks_of(l, kPfChunkGroups);
+  const char* ce = getenv("MIVS_PF_CHUNK_ROWS");
+  idx->pf_G = ce ? std::max(1, std::min(256, atoi(ce) / kGroupRows)) : kPfChunkGroups;
+  for (int l = 0; l < L.n_lists; ++l) c[l] = L.chunks_of(l, idx->pf_G);
   std::sort(c.begin(), c.end(), std::greater<int64_t>());
   idx->pf_top_chunks_prefix.assign(L.n_lists + 1, 0);
   for (int l = 0; l < L.n_lists; ++l) idx->pf_top_chunks_prefix[l + 1] = idx->pf_top_chunks_prefix[l] + c[l];
@@ -539,7 +542,7 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   a.row_norms = L.norms.as<float>();
   a.list_goff = L.goff.as<int64_t>();
   a.n_lists = L.n_lists;
-  a.chunk_groups = kPfChunkGroups;
+  a.chunk_groups = idx->pf_G;
   a.qh = ws.qh.as<uint16_t>();
   a.qscale = ws.qscale.as<float>();
   a.qnorms = ws.qn.as<float>();
@@ -561,8 +564,9 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   HIPCHK(launch_fill_i32(ws.qtheta.as<int>(), nq, (int)kPfOrdInf, s));
   a.qtheta = ws.qtheta.as<unsigned>();
   a.k = k;
+  a.flags = getenv("MIVS_PF_FLAGS") ? atoi(getenv("MIVS_PF_FLAGS")) : 0;
   if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
-  HIPCHK(launch_pf_scan(a, std::max(8, cu_count(idx->device) / 8 * 8), pf_scan_lds_bytes(dp, kPfChunkGroups), s));
+  HIPCHK(launch_pf_scan(a, std::max(8, cu_count(idx->device) / 8 * 8), pf_scan_lds_bytes(dp, idx->pf_G), s));
   if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
   ws.pf_stats.reserve(32);
   HIPCHK(hipMemsetAsync(ws.pf_stats.p, 0, 32, s));
@@ -643,7 +647,7 @@ void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t 
     idx->last_pf = pf ? 1 : 0;
   }
   HIPCHK(launch_probe_map(ws.probes_i.as<int64_t>(), nq, np, L.n_lists, L.goff.as<int64_t>(),
-                          pf ? kPfChunkGroups : idx->G, qtile, ws.counts.as<int>(), ws.fill.as<int>(),
+                          pf ? idx->pf_G : idx->G, qtile, ws.counts.as<int>(), ws.fill.as<int>(),
                           ws.bucket_off.as<int>(), ws.work_off.as<int>(), ws.bucket_q.as<int64_t>(),
                           ws.bucket_slot.as<int64_t>(), ws.qp_slots.as<int64_t>(), ws.slot_begin.as<int64_t>(),
                           ws.scan_tmp.p, stb, s));

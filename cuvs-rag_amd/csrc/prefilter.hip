@@ -233,7 +233,7 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
     // 1 KiB wave read (conflict-free) at an immediate offset per k-step. Piece i of the image is
     // written by thread i mod 512 (linear, conflict-free); its source is a 16-B piece of query row
     // (i/32/nb)*32 + i%32. nb/8 pieces per thread (dp % 64 == 0), loads batched by 4.
-    {
+    if (!(a.flags & 8)) {
       const int per = nb >> 3;
       for (int i0 = 0; i0 < per; i0 += 4) {
         uint4 v[4];
@@ -264,6 +264,8 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
     float th0 = s_th[j], th1 = s_th[32 + j];
     const int src = wave * 2 + h;  // this lane's list index among the query's 16
 
+    const int nolds = (a.flags & 4) ? 0 : 1;  // experiment: re-read one B address
+    const int nost = (a.flags & 2) ? 0 : 1;  // experiment: re-read one k-step (L1/L2 hits) instead of streaming
     const char* s_bl = s_b + lane * 16;  // this lane's B operand at k-step s: + s * 1024 (+ nb * 512: group 1)
     const int npw = wave < ng ? (ng - wave + kPfWaves - 1) / kPfWaves : 0;  // passes of this wave
     if (npw > 0) {
@@ -282,16 +284,21 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
       const f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       f32x16 c0 = zero, c1 = zero;
       int p = 0, s = 0;
+      // B operands one k-step ahead (slot u & 1): the LDS latency hides behind a k-step of MFMAs
+      h8 bq0[2], bq1[2];
+      bq0[0] = *reinterpret_cast<const h8*>(s_bl);
+      bq1[0] = *reinterpret_cast<const h8*>(s_bl + nb * 512);
       // ONE flat loop over (pass, k-step) in blocks of D (nk % D == 0, so a pass ends on a block end):
       // the compiler then keeps the ring's loads counted (vmcnt(D-1)) across pass boundaries
       for (int t0 = 0; t0 < npw * nk; t0 += D) {
 #pragma unroll
         for (int u = 0; u < D; ++u) {
-          const h8 b0 = *reinterpret_cast<const h8*>(s_bl + (s + u) * 1024);
-          const h8 b1 = *reinterpret_cast<const h8*>(s_bl + nb * 512 + (s + u) * 1024);
-          c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ring[u], b0, c0, 0, 0, 0);
-          c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ring[u], b1, c1, 0, 0, 0);
-          ring[u] = ld_h8(nptr + (ls + u) * 512);
+          const int sn = (u == D - 1 && s + D == nk) ? 0 : s + u + 1;  // the next k-step (B is per k-step)
+          bq0[(u + 1) & 1] = *reinterpret_cast<const h8*>(s_bl + sn * 1024 * nolds);
+          bq1[(u + 1) & 1] = *reinterpret_cast<const h8*>(s_bl + nb * 512 + sn * 1024 * nolds);
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ring[u], bq0[u & 1], c0, 0, 0, 0);
+          c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ring[u], bq1[u & 1], c1, 0, 0, 0);
+          ring[u] = ld_h8(nptr + (ls + u) * 512 * nost);
           // pin the per-k-step issue order (2 DS reads, 2 MFMAs, then the refill) so the refill of
           // ring[u] is issued right after its last use and D loads stay in flight
           __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
@@ -301,7 +308,7 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
         ls += D;
         if (ls == nk) { ls = 0; if (++lpass < npw) nptr += pstride; }
         s += D;
-        if (s == nk) {
+        if (s == nk && !(a.flags & 1)) {
           const int lg = p * kPfWaves + wave;  // group within the chunk
           pf_epilogue<METRIC>(c0, c1, s_norm + lg * kGroupRows, (g_begin + lg) * kGroupRows, h, qn0, qs0, th0,
                               qn1, qs1, th1, lk0, lp0, lk1, lp1);
@@ -311,6 +318,8 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
           s_l8[(32 + j) * 16 + src] = lk1[kPfLaneK - 1];
           th0 = fminf(th0, pf_theta(s_l8 + j * 16, dl0));
           th1 = fminf(th1, pf_theta(s_l8 + (32 + j) * 16, dl1));
+        }
+        if (s == nk) {
           c0 = zero;
           c1 = zero;
           s = 0;
@@ -333,6 +342,7 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
     __syncthreads();
 #pragma unroll
     for (int rnd = 0; rnd < 2; ++rnd) {
+      if (a.flags & 16) break;
       const int qi = rnd * 32 + (tid >> 4);
       const int src = tid & 15;
       const float* myk = mkey + (qi * 16 + src) * kPfLaneK;
@@ -346,6 +356,30 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
       if (src == 0) bnd = fminf(bnd, nextafterf(fminf(s_th[qi], pf_theta(s_l8 + qi * 16, s_dl[qi])), INFINITY));
 #pragma unroll
       for (int off = 8; off >= 1; off >>= 1) bnd = fminf(bnd, __shfl_xor(bnd, off, 16));
+      // fast path (the common case once theta is tight): fewer than k kept keys in all 16 lists
+      // -> compact them unsorted into the slot (the refine needs no order), pad with +inf
+      int cnt = 0;
+#pragma unroll
+      for (int i = 0; i < kPfLaneK; ++i) cnt += myk[i] < INFINITY ? 1 : 0;
+      int pre = cnt;  // inclusive prefix over the query's 16 lists
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) {
+        const int o = __shfl_up(pre, off, 16);
+        if (src >= off) pre += o;
+      }
+      const int total = __shfl(pre, 15, 16);
+      if (total < a.k) {  // uniform within the 16-lane group
+        if (slot >= 0) {
+          const int64_t sb = slot * a.slot_k;
+          const int base = pre - cnt;
+#pragma unroll
+          for (int i = 0; i < kPfLaneK; ++i)
+            if (i < cnt) { a.slot_key[sb + base + i] = myk[i]; a.slot_pos[sb + base + i] = myp[i]; }
+          for (int t = total + src; t < a.slot_k; t += 16) { a.slot_key[sb + t] = INFINITY; a.slot_pos[sb + t] = INT_MAX; }
+          if (src == 0) a.slot_bound[slot] = bnd;
+        }
+        continue;
+      }
       int head = 0;
       float hk = myk[0];
       int hp = myp[0];
