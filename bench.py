@@ -256,9 +256,14 @@ def main():
     pf = bool(stats.get("prefilter"))
     dp = (d + 63) // 64 * 64
     flops = 2.0 * d * stats["scanned_rows"]
-    # SURVEY §8(d) de-duplicated bytes: every query tile streams the rows of its list once
-    # (fp16 copy: 2 B per padded dim for the pre-filter scan K10, else fp32)
-    bytes_alg = float(stats["streamed_groups"]) * 32 * (dp * 2 if pf else d * 4)
+    # SURVEY §8(d) de-duplicated per-tile bytes: every query tile streams the rows of its list once
+    # (the pre-filter scan K10 reads the fp16 copy: 2 B per padded dim; the exact scans fp32)
+    row_bytes = dp * 2 if pf else d * 4
+    bytes_tile = float(stats["streamed_groups"]) * 32 * row_bytes
+    # compulsory bytes: every probed list once (what a kernel that shares each row among all of its
+    # queries must read from HBM); the K10 tiles of one list run together on one XCD, so the per-tile
+    # re-reads are L2 hits (rocprof FETCH_SIZE, profiles/r01_pf_pmc*.json)
+    bytes_alg = float(stats.get("unique_groups") or stats["streamed_groups"]) * 32 * row_bytes if pf else bytes_tile
     tflops = flops / (scan_ms * 1e-3) / 1e12
     gbs = bytes_alg / (scan_ms * 1e-3) / 1e9
     metric_tag = "L2"
@@ -271,11 +276,9 @@ def main():
     cfg_key = f"ivf_flat_n{n}_d{d}_q{Q}_l{a.n_lists}_p{a.n_probes}_k{k}_t{stats['query_tile']}" + ("_pf" if pf else "")
     traffic, traffic_src = load_traffic(cfg_key)
     # bound: whichever peak the launch's work needs longer for -- the MFMA pipe (fp16 for K10, fp32
-    # for the exact scans) for the algorithmic flops, or HBM for the bytes that actually crossed it
-    # (rocprof FETCH+WRITE when a committed PMC summary matches this config, else SURVEY §8(d)'s
-    # per-tile streamed bytes)
+    # for the exact scans) for the algorithmic flops, or HBM for the algorithmic bytes
     t_mfma = flops / (peak_mfma * 1e12)
-    t_hbm = (traffic if traffic else bytes_alg) / (PEAK_HBM_GBS * 1e9)
+    t_hbm = bytes_alg / (PEAK_HBM_GBS * 1e9)
     if t_mfma >= t_hbm:
         roof = {"bound": "mfma", "achieved": round(tflops, 2), "peak": peak_mfma, "unit": "TFLOP/s",
                 "frac": round(tflops / peak_mfma, 4)}
@@ -286,7 +289,10 @@ def main():
     roof.update({"kernel": f"{kname} (fine list scan, {stats['query_tile']}-query tiles)",
                  "launch_ms": round(scan_ms, 4),
                  "algorithmic_flops_per_launch": flops, "algorithmic_bytes_per_launch": bytes_alg,
+                 "per_tile_bytes_per_launch": bytes_tile,
                  "achieved_gbs_algorithmic": round(gbs, 1), "achieved_tflops": round(tflops, 2),
+                 "mfma_frac": round(tflops / peak_mfma, 4), "hbm_frac_algorithmic": round(gbs / PEAK_HBM_GBS, 4),
+                 "per_tile_gbs": round(bytes_tile / (scan_ms * 1e-3) / 1e9, 1),
                  "traffic_gbs": round(traffic / (scan_ms * 1e-3) / 1e9, 1) if traffic else None,
                  "traffic_source": traffic_src, "timing": "hipEvents around each fine-scan launch on the search stream, "
                                                           f"{prof['n_calls']} timed steps"})

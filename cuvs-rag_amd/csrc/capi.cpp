@@ -1249,11 +1249,13 @@ int32_t mivs_index_last_search_stats(mivs_index_t idx, mivs_search_stats* out) {
       for (int l = 0; l < L.n_lists; ++l) {
         st.scanned_rows += (int64_t)counts[l] * (L.h_off[l + 1] - L.h_off[l]);
         st.streamed_groups += ceil_div(counts[l], idx->last_qtile) * (L.h_goff[l + 1] - L.h_goff[l]);
+        if (counts[l] > 0) st.unique_groups += L.h_goff[l + 1] - L.h_goff[l];
       }
       st.work_items = woff[L.n_lists];
     } else if (idx->last_nq > 0) {
       st.scanned_rows = idx->last_nq * L.n_rows;
       st.streamed_groups = ceil_div(idx->last_nq, idx->last_qtile) * L.n_groups;
+      st.unique_groups = L.n_groups;
       st.work_items = ceil_div(idx->last_nq, idx->last_qtile) * std::max<int64_t>(1, ceil_div(L.n_groups, idx->G));
     }
     *out = st;

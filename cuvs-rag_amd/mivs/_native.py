@@ -84,6 +84,7 @@ class SearchStats(ctypes.Structure):
         ("prefilter", c_int32),
         ("overflow_queries", c_int64),
         ("window_candidates", c_int64),
+        ("unique_groups", c_int64),
     ]
 
     def as_dict(self) -> dict:

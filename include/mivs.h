@@ -82,6 +82,7 @@ typedef struct {
   int32_t prefilter;        /* 1: the fp16 pre-filter scan (K10) + exact refine (K11) served the search */
   int64_t overflow_queries; /* queries the refine could not prove, re-run through the exact fp32 scan */
   int64_t window_candidates;/* candidates recomputed in fp32 by the refine (sum over queries) */
+  int64_t unique_groups;    /* 32-row groups of the lists probed by at least one query (compulsory bytes) */
 } mivs_search_stats;
 
 /* device time of the searches issued since the last collect while profiling was on
