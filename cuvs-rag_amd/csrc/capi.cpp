@@ -507,7 +507,11 @@ void pf_enable(mivs_index_s* idx, hipStream_t s) {
   idx->x_res_max = resmax;
   std::vector<int64_t> c(L.n_lists);
   const char* ce = getenv("MIVS_PF_CHUNK_ROWS");
-  idx->pf_G = ce ? std::max(1, std::min(256, atoi(ce) / kGroupRows)) : kPfChunkGroups;
+  // rows per work item: as many as the LDS holds the norms of beside the query tile (the tile's
+  // staging is paid once per item), unless MIVS_PF_CHUNK_ROWS asks for fewer
+  int gmax = kPfChunkGroups;
+  while (pf_scan_lds_bytes(idx->dp, gmax + 1) <= 160 * 1024) ++gmax;
+  idx->pf_G = std::max(1, std::min(gmax, ce ? atoi(ce) / kGroupRows : kPfChunkGroups));
   for (int l = 0; l < L.n_lists; ++l) c[l] = L.chunks_of(l, idx->pf_G);
   std::sort(c.begin(), c.end(), std::greater<int64_t>());
   idx->pf_top_chunks_prefix.assign(L.n_lists + 1, 0);
@@ -565,9 +569,24 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   a.qtheta = ws.qtheta.as<unsigned>();
   a.k = k;
   a.flags = getenv("MIVS_PF_FLAGS") ? atoi(getenv("MIVS_PF_FLAGS")) : 0;
+  Buf pbuf;
+  if (a.flags & 32) {  // diagnostic: K10 phase clocks to stderr
+    pbuf.reserve(16 * sizeof(unsigned long long));
+    HIPCHK(hipMemsetAsync(pbuf.p, 0, 16 * sizeof(unsigned long long), s));
+    a.prof = pbuf.as<unsigned long long>();
+  }
   if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
   HIPCHK(launch_pf_scan(a, std::max(8, cu_count(idx->device) / 8 * 8), pf_scan_lds_bytes(dp, idx->pf_G), s));
   if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
+  if (a.flags & 32) {
+    unsigned long long hp[16];
+    HIPCHK(hipMemcpyAsync(hp, pbuf.p, sizeof(hp), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const double w = (double)hp[7];
+    fprintf(stderr, "[k10 phases] waves-cycles %.4g clock %.3f GHz | fetch %.3f staging %.3f loop %.3f "
+            "barrier %.3f merge %.3f | epilogues %llu slow %.4f\n", w, hp[8] ? (double)hp[7] / hp[8] * 0.1 : 0.0,
+            hp[0] / w, hp[1] / w, hp[2] / w, hp[3] / w, hp[4] / w, hp[5], hp[5] ? (double)hp[6] / hp[5] : 0.0);
+  }
   ws.pf_stats.reserve(32);
   HIPCHK(hipMemsetAsync(ws.pf_stats.p, 0, 32, s));
   ws.ovf_q.reserve(sizeof(int64_t) * nq);

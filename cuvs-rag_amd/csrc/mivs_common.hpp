@@ -172,7 +172,9 @@ struct PfScanArgs {
   unsigned* qtheta;           // [nq] order-mapped window bound per query, shared by all work items
                               // (set to the mapping of +inf before the launch)
   int k;
-  int flags;                  // timing experiments only (MIVS_PF_FLAGS): 1 skip epilogue, 2 no A stream
+  int flags;                  // timing experiments only (MIVS_PF_FLAGS): 1 skip epilogue, 8 skip staging,
+                              // 16 skip merge, 32 phase clocks into prof
+  unsigned long long* prof;   // [16] diagnostic phase clocks, or nullptr
 };
 
 struct PfRefineArgs {

@@ -91,17 +91,43 @@ __device__ __forceinline__ float pf_window(float kth, float delta) {
   return kth + 2.0f * delta + fabsf(kth) * 0x1p-20f;
 }
 
+// the epilogue's fast filter. The exact test keeps key < lk_last && key <= th, i.e. key < U with
+// U = min(lk_last, next float above th). The filter value of an accumulator element is ONE fma,
+//   L2: f = fl(xn - 2 acc qs)  (key = max(fl(fl(xn + qn) - 2 acc qs), 0))     IP: f = acc * -qs = key,
+// and f < pf_uf(U) for every key < U: for L2 the margin (xn_max^2 + qn + |U|) 2^-20 is 4x the sum of the
+// roundings of f, of the key and of U - qn (|2 acc qs| <= 1.01 (xn + qn)). The filter only has false
+// positives, which the exact test then rejects. -inf: the query slot is empty.
 template <int METRIC>
-__device__ __forceinline__ void pf_epilogue(const f32x16& c0, const f32x16& c1, const float* __restrict__ s_gnorm,
-                                            int64_t rb, int h, float qn0, float qs0, float th0, float qn1,
-                                            float qs1, float th1, float (&lk0)[kPfLaneK], int (&lp0)[kPfLaneK],
-                                            float (&lk1)[kPfLaneK], int (&lp1)[kPfLaneK]) {
+__device__ __forceinline__ float pf_uf(float lk_last, float th, float qn, float xnmax2) {
+  const float U = fminf(lk_last, nextafterf(th, INFINITY));
+  if (!(U > -INFINITY) || !(qn < INFINITY)) return -INFINITY;
+  if (!(U < INFINITY)) return INFINITY;
+  if (METRIC == kL2) return (U - qn) + (xnmax2 + qn + fabsf(U)) * 0x1p-20f;
+  return U;
+}
+
+template <int METRIC>
+__device__ __forceinline__ bool pf_epilogue(const f32x16& c0, const f32x16& c1, const float* __restrict__ s_gnorm,
+                                            int64_t rb, int h, float qn0, float qs0, float th0, float uf0, float qn1,
+                                            float qs1, float th1, float uf1, float (&lk0)[kPfLaneK],
+                                            int (&lp0)[kPfLaneK], float (&lk1)[kPfLaneK], int (&lp1)[kPfLaneK]) {
   float xn[16];
 #pragma unroll
   for (int q4 = 0; q4 < 4; ++q4) {
     const float4 t = *reinterpret_cast<const float4*>(s_gnorm + 8 * q4 + 4 * h);
     xn[4 * q4 + 0] = t.x; xn[4 * q4 + 1] = t.y; xn[4 * q4 + 2] = t.z; xn[4 * q4 + 3] = t.w;
   }
+  // fast path: one fma + one compare per element; once theta is tight almost every group ends here
+  const float m0 = METRIC == kL2 ? -2.0f * qs0 : -qs0;
+  const float m1 = METRIC == kL2 ? -2.0f * qs1 : -qs1;
+  float mn0 = INFINITY, mn1 = INFINITY;  // (no NaN reaches here: accumulators are finite, pad norms +inf)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float b = METRIC == kL2 ? xn[r] : 0.0f;
+    mn0 = fminf(mn0, fmaf(c0[r], m0, b));
+    mn1 = fminf(mn1, fmaf(c1[r], m1, b));
+  }
+  if (__ballot(mn0 < uf0 || mn1 < uf1) == 0) return false;
   // a key is kept if it beats the lane list AND lies within the query's window bound theta
   // (th = -inf for empty query slots: nothing is kept)
 #pragma unroll
@@ -112,6 +138,7 @@ __device__ __forceinline__ void pf_epilogue(const f32x16& c0, const f32x16& c1, 
     const float k1 = pf_key<METRIC>(c1[r], qs1, xn[r], qn1);
     if (k1 < lk1[kPfLaneK - 1] && k1 <= th1) pf_insert<kPfLaneK>(lk1, lp1, k1, pos);
   }
+  return true;
 }
 
 // theta of a query from its 16 lane lists' last entries (s_l8[16]): with two full lists whose last
@@ -169,9 +196,15 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
   const int total = a.work_off[a.n_lists];
   const int grp = blockIdx.x & 7;
   const int64_t pstride = (int64_t)kPfWaves * nb * 256;  // halves between a wave's consecutive groups
+  const float xnmax2 = a.x_norm_max * a.x_norm_max;       // >= every row's pinned norm
   if (tid == 0) s_misc[1] = 0;                            // queues exhausted so far
+  // diagnostic phase clocks (a.prof != nullptr only under MIVS_PF_FLAGS & 32)
+  unsigned long long pr_top = 0, pr_item = 0, pr_stage = 0, pr_loop = 0, pr_bar = 0, pr_slow = 0, pr_epi = 0;
+  const unsigned long long pr_t0 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
+  const unsigned long long pr_r0 = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
 
   for (;;) {
+    const unsigned long long pr_a = a.prof ? __builtin_amdgcn_s_memtime() : 0;
     if (tid == 0) {
       int qs = s_misc[1], w = total;
       while (qs < 8) {
@@ -187,6 +220,7 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
     __syncthreads();
     const int w = s_misc[0];
     if (w >= total) break;
+    const unsigned long long pr_b = a.prof ? __builtin_amdgcn_s_memtime() : 0;
 
     int lo = 0, hi = a.n_lists - 1;
     while (lo < hi) {
@@ -252,6 +286,7 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
       }
     }
     __syncthreads();
+    const unsigned long long pr_c = a.prof ? __builtin_amdgcn_s_memtime() : 0;
 
     float lk0[kPfLaneK], lk1[kPfLaneK];
     int lp0[kPfLaneK], lp1[kPfLaneK];
@@ -262,10 +297,9 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
     // per-query window bound theta (refreshed after every pass from all lane lists); -inf: empty slot
     // starts from the query's window bound over the items finished so far (qtheta, all workgroups)
     float th0 = s_th[j], th1 = s_th[32 + j];
+    float uf0 = pf_uf<METRIC>(INFINITY, th0, qn0, xnmax2), uf1 = pf_uf<METRIC>(INFINITY, th1, qn1, xnmax2);
     const int src = wave * 2 + h;  // this lane's list index among the query's 16
 
-    const int nolds = (a.flags & 4) ? 0 : 1;  // experiment: re-read one B address
-    const int nost = (a.flags & 2) ? 0 : 1;  // experiment: re-read one k-step (L1/L2 hits) instead of streaming
     const char* s_bl = s_b + lane * 16;  // this lane's B operand at k-step s: + s * 1024 (+ nb * 512: group 1)
     const int npw = wave < ng ? (ng - wave + kPfWaves - 1) / kPfWaves : 0;  // passes of this wave
     if (npw > 0) {
@@ -294,11 +328,11 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
 #pragma unroll
         for (int u = 0; u < D; ++u) {
           const int sn = (u == D - 1 && s + D == nk) ? 0 : s + u + 1;  // the next k-step (B is per k-step)
-          bq0[(u + 1) & 1] = *reinterpret_cast<const h8*>(s_bl + sn * 1024 * nolds);
-          bq1[(u + 1) & 1] = *reinterpret_cast<const h8*>(s_bl + nb * 512 + sn * 1024 * nolds);
+          bq0[(u + 1) & 1] = *reinterpret_cast<const h8*>(s_bl + sn * 1024);
+          bq1[(u + 1) & 1] = *reinterpret_cast<const h8*>(s_bl + nb * 512 + sn * 1024);
           c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ring[u], bq0[u & 1], c0, 0, 0, 0);
           c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ring[u], bq1[u & 1], c1, 0, 0, 0);
-          ring[u] = ld_h8(nptr + (ls + u) * 512 * nost);
+          ring[u] = ld_h8(nptr + (ls + u) * 512);
           // pin the per-k-step issue order (2 DS reads, 2 MFMAs, then the refill) so the refill of
           // ring[u] is issued right after its last use and D loads stay in flight
           __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
@@ -310,14 +344,18 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
         s += D;
         if (s == nk && !(a.flags & 1)) {
           const int lg = p * kPfWaves + wave;  // group within the chunk
-          pf_epilogue<METRIC>(c0, c1, s_norm + lg * kGroupRows, (g_begin + lg) * kGroupRows, h, qn0, qs0, th0,
-                              qn1, qs1, th1, lk0, lp0, lk1, lp1);
+          if (a.prof) ++pr_epi;
+          const bool slow = pf_epilogue<METRIC>(c0, c1, s_norm + lg * kGroupRows, (g_begin + lg) * kGroupRows, h, qn0, qs0, th0,
+                              uf0, qn1, qs1, th1, uf1, lk0, lp0, lk1, lp1);
+          if (a.prof && slow) ++pr_slow;
           // publish this lane's list ends, refresh theta from all 16 (no barrier: every value ever
           // stored is the end of a real list, so a stale read only gives a looser, still valid theta)
           s_l8[j * 16 + src] = lk0[kPfLaneK - 1];
           s_l8[(32 + j) * 16 + src] = lk1[kPfLaneK - 1];
           th0 = fminf(th0, pf_theta(s_l8 + j * 16, dl0));
           th1 = fminf(th1, pf_theta(s_l8 + (32 + j) * 16, dl1));
+          uf0 = pf_uf<METRIC>(lk0[kPfLaneK - 1], th0, qn0, xnmax2);
+          uf1 = pf_uf<METRIC>(lk1[kPfLaneK - 1], th1, qn1, xnmax2);
         }
         if (s == nk) {
           c0 = zero;
@@ -329,7 +367,9 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
     }
 
     // ---- per query: 16 lane lists (8 waves x 2 halves) -> slot top-slot_k + dropped-key bound ----
+    const unsigned long long pr_d = a.prof ? __builtin_amdgcn_s_memtime() : 0;
     __syncthreads();  // the B image is dead
+    const unsigned long long pr_e = a.prof ? __builtin_amdgcn_s_memtime() : 0;
     {
 #pragma unroll
       for (int i = 0; i < kPfLaneK; ++i) {
@@ -412,6 +452,20 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
       if (src == 0 && slot >= 0) a.slot_bound[slot] = bnd;
     }
     __syncthreads();
+    if (a.prof) {
+      const unsigned long long pr_f = __builtin_amdgcn_s_memtime();
+      pr_top += pr_b - pr_a; pr_item += pr_c - pr_b; pr_stage += pr_d - pr_c; pr_loop += pr_e - pr_d;
+      pr_bar += pr_f - pr_e;
+    }
+  }
+  if (a.prof && lane == 0) {
+    // [0] fetch, [1] staging, [2] main loop, [3] post-loop barrier wait, [4] merge (cycles, summed over
+    // waves), [5] epilogues, [6] slow-path epilogues, [7] wave-cycles, [8] 100 MHz ticks
+    atomicAdd(a.prof + 0, pr_top); atomicAdd(a.prof + 1, pr_item); atomicAdd(a.prof + 2, pr_stage);
+    atomicAdd(a.prof + 3, pr_loop); atomicAdd(a.prof + 4, pr_bar); atomicAdd(a.prof + 5, pr_epi);
+    atomicAdd(a.prof + 6, pr_slow);
+    atomicAdd(a.prof + 7, __builtin_amdgcn_s_memtime() - pr_t0);
+    atomicAdd(a.prof + 8, __builtin_amdgcn_s_memrealtime() - pr_r0);
   }
 }
 
