@@ -204,6 +204,8 @@ struct mivs_index_s {
   float x_norm_max = 0.0f, x_res_max = 0.0f;
   int pf_G = kPfChunkGroups;                  // groups per K10 work item
   std::vector<int64_t> pf_top_chunks_prefix;  // as ListSet::top_chunks_prefix, for pf_G
+  int pr_G = kPrChunkGroups;                  // groups per K12 work item
+  std::vector<int64_t> pr_top_chunks_prefix;  // as ListSet::top_chunks_prefix, for pr_G
   std::mutex mu;
   Workspace ws;
   Profiler prof;
@@ -512,10 +514,24 @@ void pf_enable(mivs_index_s* idx, hipStream_t s) {
   int gmax = kPfChunkGroups;
   while (pf_scan_lds_bytes(idx->dp, gmax + 1) <= 160 * 1024) ++gmax;
   idx->pf_G = std::max(1, std::min(gmax, ce ? atoi(ce) / kGroupRows : kPfChunkGroups));
-  for (int l = 0; l < L.n_lists; ++l) c[l] = L.chunks_of(l, idx->pf_G);
-  std::sort(c.begin(), c.end(), std::greater<int64_t>());
-  idx->pf_top_chunks_prefix.assign(L.n_lists + 1, 0);
-  for (int l = 0; l < L.n_lists; ++l) idx->pf_top_chunks_prefix[l + 1] = idx->pf_top_chunks_prefix[l] + c[l];
+  auto top_prefix = [&](int G, std::vector<int64_t>& out) {
+    for (int l = 0; l < L.n_lists; ++l) c[l] = L.chunks_of(l, G);
+    std::sort(c.begin(), c.end(), std::greater<int64_t>());
+    out.assign(L.n_lists + 1, 0);
+    for (int l = 0; l < L.n_lists; ++l) out[l + 1] = out[l] + c[l];
+  };
+  top_prefix(idx->pf_G, idx->pf_top_chunks_prefix);
+  // K12 items: the LDS holds a ring of groups, not the chunk's norms, so any chunk length fits
+  const char* re = getenv("MIVS_PR_CHUNK_ROWS");
+  idx->pr_G = std::max(1, re ? atoi(re) / kGroupRows : kPrChunkGroups);
+  top_prefix(idx->pr_G, idx->pr_top_chunks_prefix);
+}
+
+// K12 (register-resident 128-query tiles) serves the pre-filter scan only on request
+// (MIVS_PF_REG=1): at d = 768 its 4-entry lane lists send too many queries to the exact fallback
+bool pr_use(const mivs_index_s* idx) {
+  const char* e = getenv("MIVS_PF_REG");
+  return e && e[0] == '1' && pr_scan_supported(idx->dp);
 }
 
 void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
@@ -524,7 +540,7 @@ void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t 
 // K10 scan + K11 refine for a probe map built with (kPfChunkGroups, kPfQTile); queries the refine
 // could not prove are re-run through the exact scan and scattered back.
 void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
-                    int64_t* out_i, ProfRec* pr) {
+                    int64_t* out_i, ProfRec* pr, bool use_r) {
   Workspace& ws = idx->ws;
   const ListSet& L = idx->lists;
   const int dp = idx->dp;
@@ -533,9 +549,12 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   ws.qres.reserve(sizeof(float) * nq);
   HIPCHK(launch_queries_to_half(q, nq, idx->d, dp, idx->hx_exp, ws.qh.as<uint16_t>(), ws.qscale.as<float>(),
                                 ws.qres.as<float>(), s));
-  const int64_t max_slots = std::max<int64_t>(1, nq * idx->pf_top_chunks_prefix[std::min<int64_t>(np, L.n_lists)]);
+  const std::vector<int64_t>& tcp = use_r ? idx->pr_top_chunks_prefix : idx->pf_top_chunks_prefix;
+  const int64_t max_slots = std::max<int64_t>(1, nq * tcp[std::min<int64_t>(np, L.n_lists)]);
   // per-slot candidates: room above k so that a neighbourhood packed into one chunk does not overflow
-  const int slot_k = k <= 10 ? 16 : kPfSlotKMax;
+  // (K12: the query's four lane lists of 4)
+  const char* ske = getenv("MIVS_PF_SLOT_K");  // K10 slot size override (16 or 32)
+  const int slot_k = use_r ? kPrSlotK : (ske ? (atoi(ske) > 16 ? kPfSlotKMax : 16) : (k <= 10 ? 16 : kPfSlotKMax));
   ws.pf_key.reserve(sizeof(float) * (size_t)max_slots * slot_k);
   ws.pf_pos.reserve(sizeof(int) * (size_t)max_slots * slot_k);
   ws.pf_bound.reserve(sizeof(float) * (size_t)max_slots);
@@ -546,7 +565,7 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   a.row_norms = L.norms.as<float>();
   a.list_goff = L.goff.as<int64_t>();
   a.n_lists = L.n_lists;
-  a.chunk_groups = idx->pf_G;
+  a.chunk_groups = use_r ? idx->pr_G : idx->pf_G;
   a.qh = ws.qh.as<uint16_t>();
   a.qscale = ws.qscale.as<float>();
   a.qnorms = ws.qn.as<float>();
@@ -576,16 +595,24 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
     a.prof = pbuf.as<unsigned long long>();
   }
   if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
-  HIPCHK(launch_pf_scan(a, std::max(8, cu_count(idx->device) / 8 * 8), pf_scan_lds_bytes(dp, idx->pf_G), s));
+  const int grid = std::max(8, cu_count(idx->device) / 8 * 8);
+  if (use_r) HIPCHK(launch_pr_scan(a, grid, s));
+  else HIPCHK(launch_pf_scan(a, grid, pf_scan_lds_bytes(dp, idx->pf_G), s));
   if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
   if (a.flags & 32) {
     unsigned long long hp[16];
     HIPCHK(hipMemcpyAsync(hp, pbuf.p, sizeof(hp), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     const double w = (double)hp[7];
-    fprintf(stderr, "[k10 phases] waves-cycles %.4g clock %.3f GHz | fetch %.3f staging %.3f loop %.3f "
-            "barrier %.3f merge %.3f | epilogues %llu slow %.4f\n", w, hp[8] ? (double)hp[7] / hp[8] * 0.1 : 0.0,
-            hp[0] / w, hp[1] / w, hp[2] / w, hp[3] / w, hp[4] / w, hp[5], hp[5] ? (double)hp[6] / hp[5] : 0.0);
+    if (use_r)
+      fprintf(stderr, "[k12 phases] waves-cycles %.4g clock %.3f GHz | fetch %.3f setup %.3f loop %.3f tail %.3f | "
+              "groups/wave %.1f cycles/group %.0f slow %.4f\n", w, hp[8] ? (double)hp[7] / hp[8] * 0.1 : 0.0,
+              hp[0] / w, hp[1] / w, hp[2] / w, hp[3] / w, hp[5] / 4.0 / (w / (double)(hp[7] ? hp[7] : 1)),
+              hp[5] ? (double)hp[2] / hp[5] : 0.0, hp[5] ? (double)hp[6] / hp[5] : 0.0);
+    else
+      fprintf(stderr, "[k10 phases] waves-cycles %.4g clock %.3f GHz | fetch %.3f staging %.3f loop %.3f "
+              "barrier %.3f merge %.3f | epilogues %llu slow %.4f\n", w, hp[8] ? (double)hp[7] / hp[8] * 0.1 : 0.0,
+              hp[0] / w, hp[1] / w, hp[2] / w, hp[3] / w, hp[4] / w, hp[5], hp[5] ? (double)hp[6] / hp[5] : 0.0);
   }
   ws.pf_stats.reserve(32);
   HIPCHK(hipMemsetAsync(ws.pf_stats.p, 0, 32, s));
@@ -660,18 +687,19 @@ void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t 
   const size_t stb = scan_tmp_bytes(ne) + sizeof(int64_t) * (size_t)ne;
   ws.scan_tmp.reserve(stb);
   const bool dump = k > kMaxK;
-  const int qtile = pf ? kPfQTile : (dump ? kQTile : pick_qtile(k, idx->d, idx->G));
+  const bool use_r = pf && pr_use(idx);
+  const int qtile = pf ? (use_r ? kPrQTile : kPfQTile) : (dump ? kQTile : pick_qtile(k, idx->d, idx->G));
   if (prof) {
     idx->last_qtile = qtile;
     idx->last_pf = pf ? 1 : 0;
   }
   HIPCHK(launch_probe_map(ws.probes_i.as<int64_t>(), nq, np, L.n_lists, L.goff.as<int64_t>(),
-                          pf ? idx->pf_G : idx->G, qtile, ws.counts.as<int>(), ws.fill.as<int>(),
+                          pf ? (use_r ? idx->pr_G : idx->pf_G) : idx->G, qtile, ws.counts.as<int>(), ws.fill.as<int>(),
                           ws.bucket_off.as<int>(), ws.work_off.as<int>(), ws.bucket_q.as<int64_t>(),
                           ws.bucket_slot.as<int64_t>(), ws.qp_slots.as<int64_t>(), ws.slot_begin.as<int64_t>(),
                           ws.scan_tmp.p, stb, s));
   if (pf) {
-    pf_scan_refine(idx, s, q, nq, k, np, out_d, out_i, pr);
+    pf_scan_refine(idx, s, q, nq, k, np, out_d, out_i, pr, use_r);
     if (pr) HIPCHK(hipEventRecord(pr->e[3], s));
     return;
   }

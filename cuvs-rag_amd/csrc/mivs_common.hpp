@@ -201,6 +201,12 @@ struct PfRefineArgs {
 
 hipError_t launch_pf_scan(const PfScanArgs& a, int grid, size_t lds, hipStream_t s);
 size_t pf_scan_lds_bytes(int dp, int chunk_groups);
+// K12: register-resident 128-query tiles, LDS-DMA row ring (dp/16 in {4,8,12,16,24,32,48})
+constexpr int kPrQTile = 128;
+constexpr int kPrSlotK = 16;  // K12 slot: the query's 4 lane lists of 4 approximate candidates
+constexpr int kPrChunkGroups = 256;  // default groups (8192 rows) per K12 work item (MIVS_PR_CHUNK_ROWS)
+bool pr_scan_supported(int dp);
+hipError_t launch_pr_scan(const PfScanArgs& a, int grid, hipStream_t s);
 hipError_t launch_pf_refine(const PfRefineArgs& a, hipStream_t s);
 constexpr unsigned kPfOrdInf = 0xFF800000u;  // order mapping of +inf (qtheta's initial value)
 // fp32 groups -> fp16 groups scaled by 2^hx_exp (FTZ below the fp16 normal range), per-index maxima of

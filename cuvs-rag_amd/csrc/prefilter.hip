@@ -18,6 +18,7 @@
 //        If a dropped key could be inside the window (bound <= T) or the window holds
 //        more than kPfCap candidates, the query is listed for the exact scan.
 #include <climits>
+#include <utility>
 #include <cstdlib>
 
 #include "mivs_common.hpp"
@@ -679,6 +680,382 @@ __global__ void k_scatter_results(const float* __restrict__ in_d, const int64_t*
   out_i[rows[i] * k + c] = in_i[t];
 }
 
+// ---------------------------------------------------------------------------------------------
+// K12 `k_pf_scan_r` — the pre-filter scan with REGISTER-resident query tiles.
+//
+// K10 keeps a 64-query tile in LDS and streams rows into VGPRs, so every row read from HBM/L2 feeds
+// 64 queries and the scan needs 64 B/clk/CU at the MFMA rate. K12 swaps the roles: one workgroup of
+// 8 waves per CU, persistent over (list, chunk, 128-query tile) items; wave w holds queries
+// 32(w&3)..+31 of the tile as the MFMA B operand in registers for ONE HALF of the dims (k-steps
+// [(w>>2)NK/2, ...), 96 VGPRs at d = 768), so a wave pair (w, w^4) covers 32 queries x all dims at
+// two waves per SIMD. The chunk's fp16 32-row groups are staged HBM -> VGPR ring (two groups ahead)
+// -> LDS double buffer; each wave reads its half of each k-step's A operand once from LDS (inline-asm
+// ds_read, counted lgkmcnt). A row read from HBM/L2 thus feeds 128 queries (32 B/clk/CU at the MFMA
+// rate). Per group the pair exchanges half of its 32x32 partial dots through LDS (2 KiB per wave), so
+// each wave finishes 8 of the 16 keys per lane; the filter + exact insertion of group g run during
+// group g+1 (two accumulators). Per query the 4 lane lists (row quarter h, dh) of kPrLaneK keys go to
+// one slot of 32 candidates + a lower bound of every key dropped; K11 then refines as for K10.
+// The two partial sums add in a different order than one MFMA chain: the approximate keys stay
+// within pf_delta (its MFMA term bounds any summation order).
+// ---------------------------------------------------------------------------------------------
+constexpr int kPrWaves = 8;
+constexpr int kPrThreads = kPrWaves * 64;
+constexpr int kPrLaneK = 4;
+constexpr int kPrLists = 4;  // lane lists per query: row half h x dim half dh
+static_assert(kPrLists * kPrLaneK == kPrSlotK, "K12 slot size");
+
+__host__ __device__ constexpr int pr_waitcnt(int vm, int lgkm) {
+  return (vm & 0xF) | (((vm >> 4) & 3) << 14) | (0x7 << 4) | ((lgkm & 0xF) << 8);
+}
+
+// lk[k-1] as a select chain (the empty asm keeps hipcc from turning it into an indexed load, which
+// would put the list in scratch memory)
+template <int KL>
+__device__ __forceinline__ float pr_kth(const float (&lk)[KL], int k) {
+  float v = lk[0];
+#pragma unroll
+  for (int t = 1; t < KL; ++t) {
+    v = (t == k - 1) ? lk[t] : v;
+    asm volatile("" : "+v"(v));
+  }
+  return v;
+}
+
+// two 16-B LDS reads in one inline-asm statement with its own lgkmcnt(0) (a plain ds_read here makes
+// hipcc wait for the counted A reads in flight; offsets in bytes)
+__device__ __forceinline__ void pr_ld8(unsigned addr0, unsigned addr1, float (&v)[8]) {
+  float4 t0, t1;
+  asm volatile(
+      "ds_read_b128 %0, %2\n\t"
+      "ds_read_b128 %1, %3\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(t0), "=&v"(t1)
+      : "v"(addr0), "v"(addr1)
+      : "memory");
+  v[0] = t0.x; v[1] = t0.y; v[2] = t0.z; v[3] = t0.w;
+  v[4] = t1.x; v[5] = t1.y; v[6] = t1.z; v[7] = t1.w;
+}
+
+__device__ __forceinline__ unsigned lds_off(const void* p) { return (unsigned)(uintptr_t)p; }
+
+// compile-time loop: f(std::integral_constant<int, I>) for I = 0..N-1 (immediate LDS offsets in asm)
+template <typename F, int... I>
+__device__ __forceinline__ void pr_sfor_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void pr_sfor(F&& f) {
+  pr_sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+template <int OFF>
+__device__ __forceinline__ void pr_ds_read(h8& d, unsigned addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF));
+}
+template <int N>
+__device__ __forceinline__ void pr_lgkm(h8& d) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(d) : "i"(N));
+}
+
+// shader-clock stamp with its own lgkmcnt(0) (s_memtime returns out of order with LDS reads)
+__device__ __forceinline__ unsigned long long pr_stamp() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  return t;
+}
+
+template <int METRIC, int NK>
+__global__ __launch_bounds__(kPrThreads, 1) void k_pf_scan_r(PfScanArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int GB = NK * 1024;       // bytes of one fp16 group
+  constexpr int NH = NK / 2;          // k-steps of one dim half
+  constexpr int NPW = NK / kPrWaves;  // k-step pieces each wave stages per group
+  constexpr int NLOAD = NPW + 1;      // + the group's norms
+  constexpr int DP = NK * 16;
+  static_assert(NK % kPrWaves == 0 && NLOAD <= NH, "piece schedule");
+  char* s_grp = smem;                                           // [2][GB] group double buffer
+  float* s_x = reinterpret_cast<float*>(smem + 2 * GB);         // [2][8 waves][64 lanes][8] partial dots
+  float* s_nrm = s_x + 2 * kPrWaves * 64 * 8;                   // [4][64] norms ring
+  int* s_misc = reinterpret_cast<int*>(s_nrm + 4 * 64);
+  // item-end scratch (aliases the group buffers): keys/pos [128 q][4 lists][8], bounds [128][4]
+  float* s_ok = reinterpret_cast<float*>(smem);
+  int* s_op = reinterpret_cast<int*>(s_ok + kPrQTile * kPrLists * kPrLaneK);
+  float* s_ob = reinterpret_cast<float*>(s_op + kPrQTile * kPrLists * kPrLaneK);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int qb = wave & 3, dh = wave >> 2;
+  const int j = lane & 31;
+  const int h = lane >> 5;
+  const int total = a.work_off[a.n_lists];
+  const int grp = blockIdx.x & 7;
+  const float xnmax2 = a.x_norm_max * a.x_norm_max;
+  if (tid == 0) s_misc[1] = 0;
+  // diagnostic phase clocks (a.prof only under MIVS_PF_FLAGS & 32): [0] fetch, [1] setup, [2] group loop,
+  // [3] tail + output, [5] groups, [6] slow passes, [7] wave-cycles, [8] 100 MHz ticks
+  unsigned long long pr_acc[4] = {0, 0, 0, 0}, pr_groups = 0, pr_slow = 0;
+  const unsigned long long pr_t0 = a.prof ? pr_stamp() : 0;
+  const unsigned long long pr_r0 = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
+
+  for (;;) {
+    const unsigned long long pa = a.prof ? pr_stamp() : 0;
+    if (tid == 0) {
+      int qs = s_misc[1], w = total;
+      while (qs < 8) {
+        const int g = (grp + qs) & 7;
+        const int lo_g = (int)((int64_t)total * g / 8), hi_g = (int)((int64_t)total * (g + 1) / 8);
+        const int i = atomicAdd(a.work_counter + 16 * g, 1);
+        if (lo_g + i < hi_g) { w = lo_g + i; break; }
+        ++qs;
+      }
+      s_misc[1] = qs;
+      s_misc[0] = w;
+    }
+    __syncthreads();
+    const int w = s_misc[0];
+    if (w >= total) break;
+    const unsigned long long pb = a.prof ? pr_stamp() : 0;
+    int lo = 0, hi = a.n_lists - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (a.work_off[mid] <= w) lo = mid; else hi = mid - 1;
+    }
+    const int l = lo;
+    const int m = a.bucket_off[l + 1] - a.bucket_off[l];
+    const int tiles = (m + kPrQTile - 1) / kPrQTile;
+    const int local = w - a.work_off[l];
+    const int chunk = local / tiles;
+    const int tile = local - chunk * tiles;
+    const int64_t g_begin = a.list_goff[l] + (int64_t)chunk * a.chunk_groups;
+    const int64_t g_lim = a.list_goff[l + 1];
+    const int ng = (int)((g_begin + a.chunk_groups < g_lim ? g_begin + a.chunk_groups : g_lim) - g_begin);
+    const int e0 = a.bucket_off[l] + tile * kPrQTile;
+    const int nqt = m - tile * kPrQTile < kPrQTile ? m - tile * kPrQTile : kPrQTile;
+
+    // this lane's query (an empty slot computes on query row 0 with th = -inf: nothing is kept)
+    const int qi = qb * 32 + j;
+    int64_t q = -1;
+    float qn = INFINITY, qs = 0.0f, dl = 0.0f, th = -INFINITY;
+    if (qi < nqt) {
+      q = a.bucket_q[e0 + qi];
+      qn = a.qnorms[q];
+      qs = a.qscale[q];
+      dl = pf_delta<METRIC>(qn, a.qres[q], a.x_norm_max, a.x_res_max, DP);
+      th = pf_unord(__hip_atomic_load(a.qtheta + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    h8 qr[NH];
+    {
+      const uint16_t* qp = a.qh + (q >= 0 ? q : 0) * (int64_t)DP + 16 * (dh * NH) + 8 * h;
+#pragma unroll
+      for (int t = 0; t < NH; ++t) qr[t] = ld_h8(qp + 16 * t);
+    }
+    const float mq = METRIC == kL2 ? -2.0f * qs : -qs;
+    float lk[kPrLaneK];
+    int lp[kPrLaneK];
+#pragma unroll
+    for (int t = 0; t < kPrLaneK; ++t) { lk[t] = INFINITY; lp[t] = INT_MAX; }
+    float uf = pf_uf<METRIC>(INFINITY, th, qn, xnmax2);
+
+    // register-staged row ring: piece i of a group (k-step wave*NPW + i) is loaded two groups ahead and
+    // written to the LDS buffer of the next group while this group's MFMAs run (loads past the chunk end
+    // are clamped to its last group, so the steady-state vmcnt is one constant)
+    const uint16_t* gsrc = a.groups_h + g_begin * (int64_t)(NK * 512) + (wave * NPW) * 512 + lane * 8;
+    const float* nsrc = a.row_norms + g_begin * kGroupRows + j;
+    h8 rs0[NPW], rs1[NPW];
+    float rn0, rn1;
+    auto load_piece = [&](h8 (&rs)[NPW], int gg, int i) {
+      const int gc = gg < ng ? gg : ng - 1;
+      rs[i] = ld_h8(gsrc + (int64_t)gc * (NK * 512) + i * 512);
+    };
+    auto load_norm = [&](float& rn, int gg) {
+      const int gc = gg < ng ? gg : ng - 1;
+      rn = nsrc[(int64_t)gc * kGroupRows];
+    };
+    auto write_piece = [&](const h8 (&rs)[NPW], int gg, int i) {
+      *reinterpret_cast<h8*>(s_grp + (gg & 1) * GB + (wave * NPW + i) * 1024 + lane * 16) = rs[i];
+    };
+    auto write_norm = [&](float rn, int gg) { s_nrm[(gg & 3) * 64 + lane] = rn; };
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) load_piece(rs0, 0, i);
+    load_norm(rn0, 0);
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) write_piece(rs0, 0, i);
+    write_norm(rn0, 0);
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) load_piece(rs1, 1, i);
+    load_norm(rn1, 1);
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) load_piece(rs0, 2, i);
+    load_norm(rn0, 2);
+
+    const f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    f32x16 acc = zero;
+    float keep[8];  // this wave's half of the previous group's dots (the partner's half arrives via LDS)
+    // rows of dot i of this lane: r = 8 dh + i -> (r & 3) + 8 (r >> 2) + 4 h
+    const unsigned nrm_off = (unsigned)(16 * dh + 4 * h) * 4;
+    // group gg's 8 approximate dots of this lane: this wave's half of `prev` + the partner's exchanged half
+    auto dots = [&](int gg, float (&v)[8]) {
+      float px[8];
+      const unsigned xo = lds_off(s_x + (((gg & 1) * kPrWaves + (wave ^ 4)) * 64 + lane) * 8);
+      pr_ld8(xo, xo + 16, px);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = keep[i] + px[i];
+    };
+    // the one-fma filter: may any key of this wave pass the exact test?
+    auto finish = [&](int gg) -> bool {
+      float v[8], xn[8];
+      dots(gg, v);
+      const unsigned no = lds_off(s_nrm + (gg & 3) * 64) + nrm_off;
+      pr_ld8(no, no + 32, xn);
+      float mn = INFINITY;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) mn = fminf(mn, fmaf(v[i], mq, METRIC == kL2 ? xn[i] : 0.0f));
+      return __ballot(mn < uf) != 0;
+    };
+    auto slow = [&](int gg) {
+      float v[8], xn[8];
+      dots(gg, v);
+      const unsigned no = lds_off(s_nrm + (gg & 3) * 64) + nrm_off;
+      pr_ld8(no, no + 32, xn);
+      const int64_t rb = (g_begin + gg) * kGroupRows + 16 * dh + 4 * h;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float key = pf_key<METRIC>(v[i], qs, xn[i], qn);
+        if (key < lk[kPrLaneK - 1] && key <= th) pf_insert<kPrLaneK>(lk, lp, key, (int)(rb + (i & 3) + 8 * (i >> 2)));
+      }
+      if (a.k <= kPrLaneK) {
+        const float kth = pr_kth<kPrLaneK>(lk, a.k);
+        if (kth < INFINITY) th = fminf(th, pf_window(kth, dl));
+      }
+      uf = pf_uf<METRIC>(lk[kPrLaneK - 1], th, qn, xnmax2);
+    };
+    // the half of `acc` the partner finishes, to LDS (group gg's exchange buffer); this wave's half to keep
+    auto exchange = [&](int gg) {
+      float* xp = s_x + (((gg & 1) * kPrWaves + wave) * 64 + lane) * 8;
+      float e[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float lo_ = acc[i], hi_ = acc[8 + i];
+        asm volatile("" : "+v"(lo_), "+v"(hi_));  // keeps hipcc from indexing the vector by dh (s_set_gpr_idx)
+        e[i] = dh ? lo_ : hi_;
+        keep[i] = dh ? hi_ : lo_;
+      }
+      *reinterpret_cast<float4*>(xp) = make_float4(e[0], e[1], e[2], e[3]);
+      *reinterpret_cast<float4*>(xp + 4) = make_float4(e[4], e[5], e[6], e[7]);
+    };
+
+    // one group: barrier (its LDS rows and group g-1's exchange are in), this wave's NH MFMAs with the
+    // next group's staging and group g-1's filter interleaved, group g-1's exact pass if a lane hit,
+    // then this group's exchange
+    auto body = [&](h8 (&rs)[NPW], float& rn, int g) {
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_waitcnt(pr_waitcnt(63, 0));
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const unsigned abase = lds_off(s_grp + (g & 1) * GB) + (dh * NH) * 1024 + lane * 16;
+      constexpr int PD = 2;  // A reads in flight ahead of the MFMA (two waves per SIMD hide the rest)
+      h8 ab[PD + 1];
+      pr_sfor<PD>([&](auto T) { pr_ds_read<decltype(T)::value * 1024>(ab[decltype(T)::value], abase); });
+      acc = zero;
+      bool hit = false;
+      pr_sfor<NH>([&](auto T) {
+        constexpr int t = decltype(T)::value;
+        if constexpr (t + PD < NH) pr_ds_read<(t + PD) * 1024>(ab[(t + PD) % (PD + 1)], abase);
+        pr_lgkm<(NH - 1 - t < PD ? NH - 1 - t : PD)>(ab[t % (PD + 1)]);  // A reads issued after this one
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab[t % (PD + 1)], qr[t], acc, 0, 0, 0);
+        // the NLOAD staging ops: group g+1 from registers to LDS, the registers reloaded with group g+3
+        pr_sfor<NLOAD>([&](auto P) {
+          constexpr int p = decltype(P)::value;
+          if constexpr (t == 1 + p * (NH - 1) / NLOAD) {
+            if constexpr (p < NPW) {
+              write_piece(rs, g + 1, p);
+              load_piece(rs, g + 3, p);
+            } else {
+              write_norm(rn, g + 1);
+              load_norm(rn, g + 3);
+            }
+          }
+        });
+        if constexpr (t == (NH > 4 ? 4 : NH - 1)) {
+          if (g > 0) hit = finish(g - 1);
+        }
+      });
+      if (hit) {
+        slow(g - 1);
+        if (a.prof) ++pr_slow;
+      }
+      exchange(g);
+    };
+
+    const unsigned long long pc = a.prof ? pr_stamp() : 0;
+    int g = 0;
+    for (; g + 1 < ng; g += 2) {
+      body(rs1, rn1, g);
+      body(rs0, rn0, g + 1);
+    }
+    if (g < ng) body(rs1, rn1, g);
+    // the last group's keys: its exchange is in after one more barrier
+    __builtin_amdgcn_s_waitcnt(pr_waitcnt(0, 0));  // the tail's loads (clamped re-loads) and LDS writes
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (finish(ng - 1)) slow(ng - 1);
+    const unsigned long long pd = a.prof ? pr_stamp() : 0;
+
+    // per query: the 4 lane lists -> the slot (4 x kPrLaneK candidates, unsorted), the dropped-key bound,
+    // and the window above the k-th kept key into qtheta
+    __syncthreads();  // every wave is done with the group buffers (the scratch aliases them)
+    {
+      const int li = dh * 2 + h;
+      float* ok = s_ok + (qi * kPrLists + li) * kPrLaneK;
+      int* op = s_op + (qi * kPrLists + li) * kPrLaneK;
+#pragma unroll
+      for (int t = 0; t < kPrLaneK; ++t) { ok[t] = lk[t]; op[t] = lp[t]; }
+      s_ob[qi * kPrLists + li] = fminf(lk[kPrLaneK - 1], nextafterf(th, INFINITY));
+    }
+    __syncthreads();
+    if (tid < nqt) {
+      const int64_t qq = a.bucket_q[e0 + tid];
+      const int64_t slot = a.bucket_slot[e0 + tid] + chunk;
+      const float* ok = s_ok + tid * kPrLists * kPrLaneK;
+      const int* op = s_op + tid * kPrLists * kPrLaneK;
+      float* dk = a.slot_key + slot * (kPrLists * kPrLaneK);
+      int* dp_ = a.slot_pos + slot * (kPrLists * kPrLaneK);
+      for (int t = 0; t < kPrLists * kPrLaneK; t += 4) {
+        *reinterpret_cast<float4*>(dk + t) = *reinterpret_cast<const float4*>(ok + t);
+        *reinterpret_cast<int4*>(dp_ + t) = *reinterpret_cast<const int4*>(op + t);
+      }
+      const float4 b4 = *reinterpret_cast<const float4*>(s_ob + tid * kPrLists);
+      a.slot_bound[slot] = fminf(fminf(b4.x, b4.y), fminf(b4.z, b4.w));
+      // k-th smallest kept key (rank count over the 32; ties broken by position in the scratch)
+      float kth = INFINITY;
+      for (int c = 0; c < kPrLists * kPrLaneK; ++c) {
+        const float v = ok[c];
+        if (!(v < kth)) continue;
+        int rank = 0;
+        for (int e = 0; e < kPrLists * kPrLaneK; ++e) rank += (ok[e] < v || (ok[e] == v && e < c)) ? 1 : 0;
+        if (rank == a.k - 1) kth = v;
+      }
+      if (kth < INFINITY) {
+        const float qn2 = a.qnorms[qq];
+        atomicMin(a.qtheta + qq, pf_ord(pf_window(kth, pf_delta<METRIC>(qn2, a.qres[qq], a.x_norm_max,
+                                                                        a.x_res_max, DP))));
+      }
+    }
+    __syncthreads();
+    if (a.prof) {
+      const unsigned long long pe = pr_stamp();
+      pr_acc[0] += pb - pa; pr_acc[1] += pc - pb; pr_acc[2] += pd - pc; pr_acc[3] += pe - pd;
+      pr_groups += ng;
+    }
+  }
+  if (a.prof && lane == 0) {
+    atomicAdd(a.prof + 0, pr_acc[0]); atomicAdd(a.prof + 1, pr_acc[1]); atomicAdd(a.prof + 2, pr_acc[2]);
+    atomicAdd(a.prof + 3, pr_acc[3]); atomicAdd(a.prof + 5, pr_groups); atomicAdd(a.prof + 6, pr_slow);
+    atomicAdd(a.prof + 7, pr_stamp() - pr_t0);
+    atomicAdd(a.prof + 8, __builtin_amdgcn_s_memrealtime() - pr_r0);
+  }
+}
+
 inline dim3 pf_grid(int64_t n, int b) { return dim3((unsigned)ceil_div(n > 0 ? n : 1, b)); }
 
 }  // namespace
@@ -717,6 +1094,44 @@ hipError_t launch_pf_scan(const PfScanArgs& a, int grid, size_t lds, hipStream_t
   }
   if (D == 16) return launch_pf_scan_md<kL2, 16>(a, grid, lds, s);
   return D == 8 ? launch_pf_scan_md<kL2, 8>(a, grid, lds, s) : launch_pf_scan_md<kL2, 4>(a, grid, lds, s);
+}
+
+size_t pr_scan_lds_bytes(int dp) { return (size_t)2 * dp * 64 + 2 * kPrWaves * 64 * 8 * 4 + 4 * 64 * 4 + 16; }
+
+bool pr_scan_supported(int dp) {
+  const int nk = dp / 16;
+  return dp % 64 == 0 && (nk == 8 || nk == 16 || nk == 24 || nk == 32 || nk == 40 || nk == 48) &&
+         pr_scan_lds_bytes(dp) <= 160 * 1024;
+}
+
+template <int METRIC, int NK>
+static hipError_t launch_pr_scan_mk(const PfScanArgs& a, int grid, hipStream_t s) {
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pf_scan_r<METRIC, NK>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL((k_pf_scan_r<METRIC, NK>), dim3(grid), dim3(kPrThreads), pr_scan_lds_bytes(NK * 16), s, a);
+  return hipGetLastError();
+}
+
+template <int METRIC>
+static hipError_t launch_pr_scan_m(const PfScanArgs& a, int grid, hipStream_t s) {
+  switch (a.dp / 16) {
+    case 8: return launch_pr_scan_mk<METRIC, 8>(a, grid, s);
+    case 16: return launch_pr_scan_mk<METRIC, 16>(a, grid, s);
+    case 24: return launch_pr_scan_mk<METRIC, 24>(a, grid, s);
+    case 32: return launch_pr_scan_mk<METRIC, 32>(a, grid, s);
+    case 40: return launch_pr_scan_mk<METRIC, 40>(a, grid, s);
+    case 48: return launch_pr_scan_mk<METRIC, 48>(a, grid, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// grid: a multiple of 8 (one queue per XCD group), one workgroup per CU; work counters zeroed by the caller;
+// the probe map was built with kPrQTile-query tiles, slots hold kPrSlotK candidates
+hipError_t launch_pr_scan(const PfScanArgs& a, int grid, hipStream_t s) {
+  if (!pr_scan_supported(a.dp) || a.slot_k != kPrSlotK || a.k < 1 || a.k > kPfMaxK)
+    return hipErrorInvalidValue;
+  return a.metric == kIP ? launch_pr_scan_m<kIP>(a, grid, s) : launch_pr_scan_m<kL2>(a, grid, s);
 }
 
 hipError_t launch_pf_refine(const PfRefineArgs& a, hipStream_t s) {
