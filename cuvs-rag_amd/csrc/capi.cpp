@@ -400,10 +400,179 @@ void make_single_list(ListSet& ls, const float* src, int64_t n, int d, int dp, i
   pack_lists(ls, src, d, dp, nullptr, off, id_offset, nullptr, G, s);
 }
 
-// K4 assign of rows (rows == nullptr: all n rows) to centroids -> labels
+// ---- fp16 pre-filter assign: k-means assign and list fill as a one-list K10 scan
+// (queries = data rows, rows = centroids, k = 1) + the K11 exact refine; labels equal the fp32 K4's ----
+struct PfAssign {
+  Buf qh, qscale, qres;  // fp16 copy of every data row: 2^hx x a per-row power of two (k_queries_to_half)
+  int hx = 0;
+  bool ok = false;
+};
+
+bool pf_assign_on() {
+  const char* e = getenv("MIVS_PF_ASSIGN");
+  return !(e && e[0] == '0');
+}
+
+// once per build: the data's fp16 copy, scaled by hx from the data's |x| max (every centroid is a mean of
+// data rows, so the same hx keeps the centroids' fp16 copies in range; their own residuals enter delta)
+void pf_assign_prepare(PfAssign& P, const float* data, int64_t n, int d, int dp, hipStream_t s) {
+  P.ok = false;
+  if (n <= 0 || dp % 64 != 0 || dp > 1024 || !pf_assign_on()) return;
+  Buf st;
+  st.reserve(16);
+  HIPCHK(hipMemsetAsync(st.p, 0, 16, s));
+  HIPCHK(launch_abs_max(data, n * d, st.as<unsigned>(), s));
+  unsigned h = 0;
+  HIPCHK(hipMemcpyAsync(&h, st.p, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  float absmax;
+  std::memcpy(&absmax, &h, 4);
+  P.hx = pf_hx_exp(absmax);
+  P.qh.reserve(sizeof(uint16_t) * (size_t)n * dp);
+  P.qscale.reserve(sizeof(float) * n);
+  P.qres.reserve(sizeof(float) * n);
+  HIPCHK(launch_queries_to_half(data, n, d, dp, P.hx, P.qh.as<uint16_t>(), P.qscale.as<float>(),
+                                P.qres.as<float>(), s));
+  P.ok = true;
+}
+
+void pf_assign_rows(const PfAssign& P, const float* data, const float* data_norms, const int64_t* rows, int64_t nr,
+                    int d, int dp, const ListSet& cents, int G, int64_t* labels, int device, Workspace& ws,
+                    hipStream_t s) {
+  // the centroids' fp16 copy (scale 2^hx) and the maxima the refine window needs
+  const int64_t nslot = cents.n_groups * (int64_t)kGroupRows;
+  Buf ch, st;
+  ch.reserve(sizeof(uint16_t) * (size_t)nslot * dp);
+  st.reserve(16);
+  HIPCHK(hipMemsetAsync(st.p, 0, 16, s));
+  HIPCHK(launch_norm_max(cents.norms.as<float>(), nslot, st.as<unsigned>(), s));
+  HIPCHK(launch_groups_to_half(cents.groups.as<float>(), cents.n_groups, dp, P.hx, ch.as<uint16_t>(),
+                               st.as<unsigned>() + 1, s));
+  unsigned h[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(h, st.p, 8, hipMemcpyDeviceToHost, s));
+  // probe map: one list (the centroids), every query in its bucket. K12 (128 register-resident queries per
+  // CU, the centroids streamed from L2) unless MIVS_PF_ASSIGN_REG=0 or dp is outside its instantiations
+  const char* are = getenv("MIVS_PF_ASSIGN_REG");
+  const bool use_r = !(are && are[0] == '0') && pr_scan_supported(dp);
+  const int cg = use_r ? std::max<int>(1, (int)std::min<int64_t>(cents.n_groups, 1 << 20))
+                       : std::max(1, std::min<int>(kPfChunkGroups, (int)cents.n_groups));
+  const int64_t chunks = std::max<int64_t>(1, ceil_div(cents.n_groups, cg));
+  const int64_t nslots = nr * chunks;
+  ws.bucket_q.reserve(sizeof(int64_t) * nr);
+  ws.bucket_slot.reserve(sizeof(int64_t) * nr);
+  ws.bucket_off.reserve(sizeof(int) * 2);
+  ws.work_off.reserve(sizeof(int) * 2);
+  ws.slot_begin.reserve(sizeof(int64_t) * (nr + 1));
+  HIPCHK(launch_single_list_job(nr, chunks, use_r ? kPrQTile : kPfQTile, ws.bucket_q.as<int64_t>(),
+                                ws.bucket_slot.as<int64_t>(), ws.bucket_off.as<int>(), ws.work_off.as<int>(),
+                                ws.slot_begin.as<int64_t>(), s));
+  if (rows) HIPCHK(hipMemcpyAsync(ws.bucket_q.p, rows, sizeof(int64_t) * nr, hipMemcpyDeviceToDevice, s));
+  const int slot_k = use_r ? kPrSlotK : 16;
+  ws.pf_key.reserve(sizeof(float) * (size_t)nslots * slot_k);
+  ws.pf_pos.reserve(sizeof(int) * (size_t)nslots * slot_k);
+  ws.pf_bound.reserve(sizeof(float) * (size_t)nslots);
+  ws.counter.reserve(8 * 16 * sizeof(int));
+  HIPCHK(hipMemsetAsync(ws.counter.p, 0, 8 * 16 * sizeof(int), s));
+  int64_t n_ids = nr;  // qtheta is indexed by data row: as many entries as the largest row id + 1
+  if (rows) {
+    int64_t last = 0;
+    HIPCHK(hipMemcpyAsync(&last, rows + nr - 1, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    n_ids = last + 1;  // the trainset rows are increasing (launch_train_rows)
+  }
+  ws.qtheta.reserve(sizeof(unsigned) * n_ids);
+  HIPCHK(launch_fill_i32(ws.qtheta.as<int>(), n_ids, (int)kPfOrdInf, s));
+  HIPCHK(hipStreamSynchronize(s));
+  float normmax, resmax;
+  std::memcpy(&normmax, &h[0], 4);
+  std::memcpy(&resmax, &h[1], 4);
+  PfScanArgs a{};
+  a.groups_h = ch.as<uint16_t>();
+  a.row_norms = cents.norms.as<float>();
+  a.list_goff = cents.goff.as<int64_t>();
+  a.n_lists = 1;
+  a.chunk_groups = cg;
+  a.qh = P.qh.as<uint16_t>();
+  a.qscale = P.qscale.as<float>();
+  a.qnorms = data_norms;
+  a.bucket_q = ws.bucket_q.as<int64_t>();
+  a.bucket_slot = ws.bucket_slot.as<int64_t>();
+  a.bucket_off = ws.bucket_off.as<int>();
+  a.work_off = ws.work_off.as<int>();
+  a.work_counter = ws.counter.as<int>();
+  a.slot_key = ws.pf_key.as<float>();
+  a.slot_pos = ws.pf_pos.as<int>();
+  a.slot_bound = ws.pf_bound.as<float>();
+  a.slot_k = slot_k;
+  a.dp = dp;
+  a.metric = kL2;
+  a.qres = P.qres.as<float>();
+  a.x_norm_max = sqrtf(normmax) * (1.0f + 0x1p-12f);
+  a.x_res_max = resmax;
+  a.qtheta = ws.qtheta.as<unsigned>();
+  a.k = 1;
+  const int grid = std::max(8, cu_count(device) / 8 * 8);
+  if (use_r) HIPCHK(launch_pr_scan(a, grid, s));
+  else HIPCHK(launch_pf_scan(a, grid, pf_scan_lds_bytes(dp, cg), s));
+  Buf tmp_d, stats;
+  tmp_d.reserve(sizeof(float) * (size_t)std::max<int64_t>(nr, 1));
+  stats.reserve(32);
+  HIPCHK(hipMemsetAsync(stats.p, 0, 32, s));
+  ws.ovf_q.reserve(sizeof(int64_t) * nr);
+  PfRefineArgs r{};
+  r.slot_key = ws.pf_key.as<float>();
+  r.slot_pos = ws.pf_pos.as<int>();
+  r.slot_bound = ws.pf_bound.as<float>();
+  r.slot_begin = ws.slot_begin.as<int64_t>();
+  r.slot_k = slot_k;
+  r.nq = nr;
+  r.k = 1;
+  r.d = d;
+  r.dp = dp;
+  r.metric = kL2;
+  r.groups = cents.groups.as<float>();
+  r.row_norms = cents.norms.as<float>();
+  r.row_ids = cents.ids.as<int64_t>();
+  r.queries = data;
+  r.qnorms = data_norms;
+  r.qres = P.qres.as<float>();
+  r.qrows = rows;
+  r.labels_only = 1;
+  r.x_norm_max = a.x_norm_max;
+  r.x_res_max = a.x_res_max;
+  r.out_d = tmp_d.as<float>();
+  r.out_i = labels;
+  r.ovf_count = stats.as<int>();
+  r.ovf_q = ws.ovf_q.as<int64_t>();
+  HIPCHK(launch_pf_refine(r, s));
+  int hn = 0;
+  HIPCHK(hipMemcpyAsync(&hn, stats.p, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (hn > 0) {  // rows the refine could not prove: the exact K4 scan, scattered back
+    const int64_t no = hn;
+    Buf orow, od, oi;
+    orow.reserve(sizeof(int64_t) * no);
+    od.reserve(sizeof(float) * no);
+    oi.reserve(sizeof(int64_t) * no);
+    if (rows) HIPCHK(launch_gather_ids(rows, ws.ovf_q.as<int64_t>(), no, orow.as<int64_t>(), s));
+    else HIPCHK(hipMemcpyAsync(orow.p, ws.ovf_q.p, sizeof(int64_t) * no, hipMemcpyDeviceToDevice, s));
+    single_list_topk(cents, G, data, data_norms, orow.as<int64_t>(), no, d, dp, 1, kL2, od.as<float>(),
+                     oi.as<int64_t>(), device, ws, s);
+    HIPCHK(launch_scatter_results(od.as<float>(), oi.as<int64_t>(), ws.ovf_q.as<int64_t>(), no, 1,
+                                  tmp_d.as<float>(), labels, s));
+    HIPCHK(hipStreamSynchronize(s));
+  }
+}
+
+// K4 assign of rows (rows == nullptr: all n rows) to centroids -> labels; through the fp16 pre-filter
+// when `pfa` holds the data's fp16 copy (L2 only)
 void assign_rows(const float* data, const float* data_norms, const int64_t* rows, int64_t nr, int d, int dp,
                  const ListSet& cents, int G, int metric, int64_t* labels, int device, Workspace& ws,
-                 hipStream_t s) {
+                 hipStream_t s, const PfAssign* pfa = nullptr) {
+  if (pfa && pfa->ok && metric == kL2 && nr > 0) {
+    pf_assign_rows(*pfa, data, data_norms, rows, nr, d, dp, cents, G, labels, device, ws, s);
+    return;
+  }
   Buf dist;
   dist.reserve(sizeof(float) * (size_t)std::max<int64_t>(nr, 1));
   single_list_topk(cents, G, data, data_norms, rows, nr, d, dp, 1, metric, dist.as<float>(), labels, device, ws, s);
@@ -413,7 +582,7 @@ void assign_rows(const float* data, const float* data_norms, const int64_t* rows
 // n_iters Lloyd iterations on trainset rows; centroids_rm in/out [nc][d]
 void kmeans_fit_impl(const float* data, const float* data_norms, const int64_t* rows, int64_t n_train, int d, int dp,
                      int nc, int iters, float* centroids_rm, int G, int device, Workspace& ws, hipStream_t s,
-                     bool balance = false) {
+                     bool balance = false, const PfAssign* pfa = nullptr) {
   if (iters <= 0) return;
   Buf labels, perm, off, partial, chunk_off, tmp, ctmp;
   labels.reserve(sizeof(int64_t) * n_train);
@@ -427,7 +596,7 @@ void kmeans_fit_impl(const float* data, const float* data_norms, const int64_t* 
   for (int it = 0; it < iters; ++it) {
     ListSet cents;
     make_single_list(cents, centroids_rm, nc, d, dp, 0, G, s);
-    assign_rows(data, data_norms, rows, n_train, d, dp, cents, G, kL2, labels.as<int64_t>(), device, ws, s);
+    assign_rows(data, data_norms, rows, n_train, d, dp, cents, G, kL2, labels.as<int64_t>(), device, ws, s, pfa);
     HIPCHK(launch_counting_sort(labels.as<int64_t>(), n_train, nc, perm.as<int64_t>(), off.as<int64_t>(), ctmp.p,
                                 cb, s));
     HIPCHK(launch_km_update(data, d, rows, perm.as<int64_t>(), off.as<int64_t>(), nc, n_train,
@@ -440,7 +609,8 @@ void kmeans_fit_impl(const float* data, const float* data_norms, const int64_t* 
 }
 
 // lists of `idx` from final centroids: assign every row, stable sort, pack
-void build_lists(mivs_index_s* idx, const float* data, const float* data_norms, int64_t n, hipStream_t s) {
+void build_lists(mivs_index_s* idx, const float* data, const float* data_norms, int64_t n, hipStream_t s,
+                 const PfAssign* pfa = nullptr) {
   const int nl = idx->cents.n_lists == 1 ? (int)idx->cents.n_rows : idx->cents.n_lists;
   Buf labels, perm, off, ctmp;
   labels.reserve(sizeof(int64_t) * std::max<int64_t>(n, 1));
@@ -448,7 +618,7 @@ void build_lists(mivs_index_s* idx, const float* data, const float* data_norms, 
   off.reserve(sizeof(int64_t) * (nl + 1));
   if (n > 0)
     assign_rows(data, data_norms, nullptr, n, idx->d, idx->dp, idx->cents, idx->G, idx->metric,
-                labels.as<int64_t>(), idx->device, idx->ws, s);
+                labels.as<int64_t>(), idx->device, idx->ws, s, pfa);
   const size_t cb = csort_tmp_bytes(n, nl);
   ctmp.reserve(cb);
   HIPCHK(launch_counting_sort(labels.as<int64_t>(), n, nl, perm.as<int64_t>(), off.as<int64_t>(), ctmp.p, cb, s));
@@ -814,11 +984,13 @@ int32_t mivs_ivf_flat_build(int32_t device, void* stream, const float* d_data, i
     norms.reserve(sizeof(float) * n);
     HIPCHK(launch_row_norms(d_data, n, dim, norms.as<float>(), s));
     HIPCHK(hipStreamSynchronize(s));
+    PfAssign pfa;  // the data's fp16 copy: k-means assign + list fill through the pre-filter
+    pf_assign_prepare(pfa, d_data, n, dim, idx->dp, s);
     kmeans_fit_impl(d_data, norms.as<float>(), rows.as<int64_t>(), nt, dim, idx->dp, nl, p->kmeans_n_iters,
-                    idx->centroids_rm.as<float>(), idx->G, device, idx->ws, s, p->kmeans_balance != 0);
+                    idx->centroids_rm.as<float>(), idx->G, device, idx->ws, s, p->kmeans_balance != 0, &pfa);
     make_single_list(idx->cents, idx->centroids_rm.as<float>(), nl, dim, idx->dp, 0, idx->G, s);
     if (p->add_data_on_build) {
-      build_lists(idx.get(), d_data, norms.as<float>(), n, s);
+      build_lists(idx.get(), d_data, norms.as<float>(), n, s, &pfa);
     } else {
       build_lists(idx.get(), d_data, norms.as<float>(), 0, s);
     }

@@ -197,6 +197,9 @@ struct PfRefineArgs {
   int* ovf_count;             // queries that need the exact scan
   int64_t* ovf_q;
   int64_t* n_window;          // optional: total window candidates (stats)
+  const int64_t* qrows;       // optional: query q is row qrows[q] of queries / qnorms / qres (k-means trainset)
+  int labels_only;            // k = 1: a window of ONE candidate is the answer without its exact key
+                              // (out_d then holds its approximate key)
 };
 
 hipError_t launch_pf_scan(const PfScanArgs& a, int grid, size_t lds, hipStream_t s);
@@ -208,6 +211,7 @@ constexpr int kPrChunkGroups = 256;  // default groups (8192 rows) per K12 work 
 bool pr_scan_supported(int dp);
 hipError_t launch_pr_scan(const PfScanArgs& a, int grid, hipStream_t s);
 hipError_t launch_pf_refine(const PfRefineArgs& a, hipStream_t s);
+hipError_t launch_gather_ids(const int64_t* src, const int64_t* idx, int64_t n, int64_t* out, hipStream_t s);
 constexpr unsigned kPfOrdInf = 0xFF800000u;  // order mapping of +inf (qtheta's initial value)
 // fp32 groups -> fp16 groups scaled by 2^hx_exp (FTZ below the fp16 normal range), per-index maxima of
 // ||x - x_h|| and max |x| (as float bits, atomicMax) into stats[0..1] (zeroed by the caller)

@@ -509,8 +509,9 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
   for (int off = 32; off >= 1; off >>= 1) bmin = fminf(bmin, __shfl_xor(bmin, off));
 
   // the window: delta >= |approx key - pinned key| for every candidate of this query
-  const float qn = live ? a.qnorms[q] : 0.0f;
-  const float delta = pf_delta<METRIC>(qn, live ? a.qres[q] : 0.0f, a.x_norm_max, a.x_res_max, a.dp);
+  const int64_t qrow = live && a.qrows ? a.qrows[q] : q;  // the query's row in queries / qnorms / qres
+  const float qn = live ? a.qnorms[qrow] : 0.0f;
+  const float delta = pf_delta<METRIC>(qn, live ? a.qres[qrow] : 0.0f, a.x_norm_max, a.x_res_max, a.dp);
   const float T = pf_window(tk, delta);  // +inf when fewer than k candidates
   bool ovf = bmin < INFINITY && bmin <= T;
 
@@ -535,7 +536,7 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
   if (live && !ovf && lane == 0 && a.n_window) atomicAdd(reinterpret_cast<unsigned long long*>(a.n_window),
                                                           (unsigned long long)cnt);
   // the query row in LDS (zero past d), for the exact recompute
-  for (int i = lane; i < a.dp; i += 64) s_qv[wv][i] = (live && i < a.d) ? a.queries[q * a.d + i] : 0.0f;
+  for (int i = lane; i < a.dp; i += 64) s_qv[wv][i] = (live && i < a.d) ? a.queries[qrow * a.d + i] : 0.0f;
   __syncthreads();
 
   // phase 3: exact keys in the pinned order (oracle orc_dot), then a bitonic sort by (key, id)
@@ -1056,6 +1057,114 @@ __global__ __launch_bounds__(kPrThreads, 1) void k_pf_scan_r(PfScanArgs a) {
   }
 }
 
+// K11 for k = 1 (the pre-filter assign): one LANE per query. The window is
+// min approx key + 2 delta; its candidates (1-3 at k-means shapes) get the pinned fp32 key (the same
+// chain as K11 / orc_dot, the query read from global), the smallest (key, id) is the label.
+template <int METRIC>
+__global__ __launch_bounds__(256) void k_pf_refine1(PfRefineArgs a) {
+  const int64_t q0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = q0 < a.nq;  // (every lane reaches the wave reduction below)
+  const int64_t q = live ? q0 : a.nq - 1;
+  const int64_t qrow = a.qrows ? a.qrows[q] : q;
+  const int64_t sb = live ? a.slot_begin[q] : 0, se = live ? a.slot_begin[q + 1] : 0;
+  float ak = INFINITY, bmin = INFINITY;
+  for (int64_t sl = sb; sl < se; ++sl) {
+    bmin = fminf(bmin, a.slot_bound[sl]);
+    const float* kp = a.slot_key + sl * a.slot_k;
+    for (int t = 0; t < a.slot_k; t += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(kp + t);
+      ak = fminf(fminf(ak, v.x), fminf(fminf(v.y, v.z), v.w));
+    }
+  }
+  const float qn = a.qnorms[qrow];
+  const float T = pf_window(ak, pf_delta<METRIC>(qn, a.qres[qrow], a.x_norm_max, a.x_res_max, a.dp));
+  bool ovf = live && (!(ak < INFINITY) || (bmin < INFINITY && bmin <= T));
+  float bestP = INFINITY;
+  int64_t bestId = LLONG_MAX;
+  int cnt = 0;
+  const int nb = a.dp >> 3;
+  const float* qv = a.queries + qrow * a.d;
+  const bool vec = (a.d & 7) == 0 && (reinterpret_cast<uintptr_t>(qv) & 15) == 0;
+  bool done = false;
+  if (a.labels_only && !ovf) {
+    // the true top-1 is inside the window: a window of one candidate needs no exact key
+    int64_t only = -1;
+    float only_k = INFINITY;
+    for (int64_t sl = sb; sl < se && cnt < 2; ++sl)
+      for (int t = 0; t < a.slot_k; ++t) {
+        const float key = a.slot_key[sl * a.slot_k + t];
+        if (key <= T) {
+          ++cnt;
+          only = sl * a.slot_k + t;
+          only_k = key;
+        }
+      }
+    if (cnt == 1) {
+      bestP = only_k;
+      bestId = a.row_ids[a.slot_pos[only]];
+      done = true;
+    }
+    if (cnt != 1) cnt = 0;  // 0 or >= 2 candidates: the exact pass below decides
+  }
+  for (int64_t sl = sb; sl < se && !ovf && !done; ++sl) {
+    for (int t = 0; t < a.slot_k; ++t) {
+      const float key = a.slot_key[sl * a.slot_k + t];
+      if (!(key <= T)) continue;
+      if (++cnt > kPfCap) { ovf = true; break; }
+      const int pos = a.slot_pos[sl * a.slot_k + t];
+      const float* rowp = a.groups + ((int64_t)(pos >> 5) * nb * kGroupRows + (pos & 31)) * 8;
+      float acc = 0.0f;
+      for (int b = 0; b < nb; ++b) {
+        const float4 x0 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * 256);
+        const float4 x1 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * 256 + 4);
+        float y[8];
+        if (vec) {
+          const float4 y0 = *reinterpret_cast<const float4*>(qv + 8 * b);
+          const float4 y1 = *reinterpret_cast<const float4*>(qv + 8 * b + 4);
+          y[0] = y0.x; y[1] = y0.y; y[2] = y0.z; y[3] = y0.w; y[4] = y1.x; y[5] = y1.y; y[6] = y1.z; y[7] = y1.w;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) y[i] = 8 * b + i < a.d ? qv[8 * b + i] : 0.0f;
+        }
+        acc = fmaf(x0.x, y[0], acc); acc = fmaf(x1.x, y[4], acc);
+        acc = fmaf(x0.y, y[1], acc); acc = fmaf(x1.y, y[5], acc);
+        acc = fmaf(x0.z, y[2], acc); acc = fmaf(x1.z, y[6], acc);
+        acc = fmaf(x0.w, y[3], acc); acc = fmaf(x1.w, y[7], acc);
+      }
+      float P;
+      if (METRIC == kL2) {
+        const float v = fmaf(-2.0f, acc, a.row_norms[pos] + qn);
+        P = v > 0.0f ? v : 0.0f;
+      } else {
+        P = -acc;
+      }
+      const int64_t id = a.row_ids[pos];
+      if (P < bestP || (P == bestP && id < bestId)) { bestP = P; bestId = id; }
+    }
+  }
+  if (a.n_window) {  // window candidates of the proven queries (stats), one atomic per wave
+    unsigned long long c = ovf ? 0ull : (unsigned long long)cnt;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off);
+    if ((threadIdx.x & 63) == 0) atomicAdd(reinterpret_cast<unsigned long long*>(a.n_window), c);
+  }
+  if (!live) return;
+  if (ovf) {
+    const int at = atomicAdd(a.ovf_count, 1);
+    a.ovf_q[at] = q;
+    return;
+  }
+  const bool valid = bestId != LLONG_MAX;
+  a.out_d[q] = valid ? (METRIC == kIP ? -bestP : bestP) : (METRIC == kIP ? -INFINITY : INFINITY);
+  a.out_i[q] = valid ? bestId : (int64_t)-1;
+}
+
+__global__ void k_gather_ids(const int64_t* __restrict__ src, const int64_t* __restrict__ idx, int64_t n,
+                             int64_t* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) out[t] = src[idx[t]];
+}
+
 inline dim3 pf_grid(int64_t n, int b) { return dim3((unsigned)ceil_div(n > 0 ? n : 1, b)); }
 
 }  // namespace
@@ -1137,6 +1246,11 @@ hipError_t launch_pr_scan(const PfScanArgs& a, int grid, hipStream_t s) {
 hipError_t launch_pf_refine(const PfRefineArgs& a, hipStream_t s) {
   if (a.k < 1 || a.k > kPfMaxK || a.dp > 1024) return hipErrorInvalidValue;
   if (a.nq <= 0) return hipSuccess;
+  if (a.k == 1 && a.slot_k % 4 == 0) {  // lane per query
+    if (a.metric == kIP) hipLaunchKernelGGL(k_pf_refine1<kIP>, pf_grid(a.nq, 256), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_pf_refine1<kL2>, pf_grid(a.nq, 256), dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
   if (a.metric == kIP) hipLaunchKernelGGL(k_pf_refine<kIP>, pf_grid(a.nq, 4), dim3(256), 0, s, a);
   else hipLaunchKernelGGL(k_pf_refine<kL2>, pf_grid(a.nq, 4), dim3(256), 0, s, a);
   return hipGetLastError();
@@ -1168,6 +1282,12 @@ hipError_t launch_queries_to_half(const float* q, int64_t nq, int d, int dp, int
                                   float* qres, hipStream_t s) {
   if (nq <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_queries_to_half, pf_grid(nq, 4), dim3(256), 0, s, q, nq, d, dp, hx_exp, qh, qscale, qres);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_ids(const int64_t* src, const int64_t* idx, int64_t n, int64_t* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_ids, pf_grid(n, 256), dim3(256), 0, s, src, idx, n, out);
   return hipGetLastError();
 }
 
