@@ -319,20 +319,25 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
       const f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       f32x16 c0 = zero, c1 = zero;
       int p = 0, s = 0;
-      // B operands one k-step ahead (slot u & 1): the LDS latency hides behind a k-step of MFMAs
-      h8 bq0[2], bq1[2];
-      bq0[0] = *reinterpret_cast<const h8*>(s_bl);
-      bq1[0] = *reinterpret_cast<const h8*>(s_bl + nb * 512);
+      // B operands PB k-steps ahead (slot u % (PB + 1)): the LDS latency hides behind PB k-steps of MFMAs
+      constexpr int PB = D % 3 == 0 ? 2 : 1;
+      h8 bq0[PB + 1], bq1[PB + 1];
+#pragma unroll
+      for (int t = 0; t < PB; ++t) {
+        bq0[t] = *reinterpret_cast<const h8*>(s_bl + (t % nk) * 1024);
+        bq1[t] = *reinterpret_cast<const h8*>(s_bl + nb * 512 + (t % nk) * 1024);
+      }
       // ONE flat loop over (pass, k-step) in blocks of D (nk % D == 0, so a pass ends on a block end):
       // the compiler then keeps the ring's loads counted (vmcnt(D-1)) across pass boundaries
       for (int t0 = 0; t0 < npw * nk; t0 += D) {
 #pragma unroll
         for (int u = 0; u < D; ++u) {
-          const int sn = (u == D - 1 && s + D == nk) ? 0 : s + u + 1;  // the next k-step (B is per k-step)
-          bq0[(u + 1) & 1] = *reinterpret_cast<const h8*>(s_bl + sn * 1024);
-          bq1[(u + 1) & 1] = *reinterpret_cast<const h8*>(s_bl + nb * 512 + sn * 1024);
-          c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ring[u], bq0[u & 1], c0, 0, 0, 0);
-          c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ring[u], bq1[u & 1], c1, 0, 0, 0);
+          int sn = s + u + PB;  // the k-step PB ahead (B is per k-step; wraps into the next pass)
+          if (sn >= nk) sn -= nk;
+          bq0[(u + PB) % (PB + 1)] = *reinterpret_cast<const h8*>(s_bl + sn * 1024);
+          bq1[(u + PB) % (PB + 1)] = *reinterpret_cast<const h8*>(s_bl + nb * 512 + sn * 1024);
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ring[u], bq0[u % (PB + 1)], c0, 0, 0, 0);
+          c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ring[u], bq1[u % (PB + 1)], c1, 0, 0, 0);
           ring[u] = ld_h8(nptr + (ls + u) * 512);
           // pin the per-k-step issue order (2 DS reads, 2 MFMAs, then the refill) so the refill of
           // ring[u] is issued right after its last use and D loads stay in flight
@@ -1196,12 +1201,17 @@ hipError_t launch_pf_scan(const PfScanArgs& a, int grid, size_t lds, hipStream_t
   // k-steps in flight per wave: 16 when the k-loop allows (the A stream is latency-bound), else 8 or 4
   const int nk = a.dp / 16;
   const int dsel = getenv("MIVS_PF_DEPTH") ? atoi(getenv("MIVS_PF_DEPTH")) : 16;
-  const int D = (dsel >= 16 && nk % 16 == 0) ? 16 : ((dsel >= 8 && nk % 8 == 0) ? 8 : 4);
+  const int D = (dsel >= 24 && nk % 24 == 0) ? 24 : (dsel >= 16 && nk % 16 == 0) ? 16
+               : (dsel >= 12 && nk % 12 == 0) ? 12 : ((dsel >= 8 && nk % 8 == 0) ? 8 : 4);
   if (a.metric == kIP) {
+    if (D == 24) return launch_pf_scan_md<kIP, 24>(a, grid, lds, s);
+    if (D == 12) return launch_pf_scan_md<kIP, 12>(a, grid, lds, s);
     if (D == 16) return launch_pf_scan_md<kIP, 16>(a, grid, lds, s);
     return D == 8 ? launch_pf_scan_md<kIP, 8>(a, grid, lds, s) : launch_pf_scan_md<kIP, 4>(a, grid, lds, s);
   }
+  if (D == 24) return launch_pf_scan_md<kL2, 24>(a, grid, lds, s);
   if (D == 16) return launch_pf_scan_md<kL2, 16>(a, grid, lds, s);
+  if (D == 12) return launch_pf_scan_md<kL2, 12>(a, grid, lds, s);
   return D == 8 ? launch_pf_scan_md<kL2, 8>(a, grid, lds, s) : launch_pf_scan_md<kL2, 4>(a, grid, lds, s);
 }
 
