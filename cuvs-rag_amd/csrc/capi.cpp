@@ -1033,6 +1033,98 @@ int32_t mivs_ivf_flat_build_from_centroids(int32_t device, void* stream, const f
   });
 }
 
+int32_t mivs_ivf_flat_build_from_lists(int32_t device, void* stream, const float* d_rows, const int64_t* d_ids,
+                                       const int64_t* h_list_sizes, int64_t n, int32_t dim, const float* d_centroids,
+                                       int32_t n_lists, int32_t metric, int32_t chunk_rows, int32_t prefilter,
+                                       mivs_index_t* out) {
+  return guarded([&] {
+    require(out != nullptr && d_centroids != nullptr && h_list_sizes != nullptr, "centroids/sizes/out is NULL");
+    check_common(device, d_rows, n, dim);
+    require(n == 0 || d_ids != nullptr, "ids is NULL");
+    require(metric == MIVS_METRIC_L2 || metric == MIVS_METRIC_IP, "unknown metric");
+    require(n_lists >= 1 && n_lists <= 32768, "n_lists must be in [1, 32768]");
+    std::vector<int64_t> h_off(n_lists + 1, 0);
+    for (int l = 0; l < n_lists; ++l) {
+      require(h_list_sizes[l] >= 0, "negative list size");
+      h_off[l + 1] = h_off[l] + h_list_sizes[l];
+    }
+    require(h_off[n_lists] == n, "list sizes do not add up to n");
+    DeviceGuard dg(device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    auto idx = std::make_unique<mivs_index_s>();
+    idx->kind = 0;
+    idx->device = device;
+    idx->d = dim;
+    idx->dp = dim_pad(dim);
+    idx->metric = metric;
+    idx->G = chunk_groups_from_rows(chunk_rows);
+    idx->centroids_rm.reserve(sizeof(float) * (size_t)n_lists * dim);
+    HIPCHK(hipMemcpyAsync(idx->centroids_rm.p, d_centroids, sizeof(float) * (size_t)n_lists * dim,
+                          hipMemcpyDeviceToDevice, s));
+    make_single_list(idx->cents, idx->centroids_rm.as<float>(), n_lists, dim, idx->dp, 0, idx->G, s);
+    pack_lists(idx->lists, d_rows, dim, idx->dp, nullptr, h_off, 0, d_ids, idx->G, s);
+    if (prefilter && pf_default_on()) pf_enable(idx.get(), s);
+    HIPCHK(hipStreamSynchronize(s));
+    *out = idx.release();
+  });
+}
+
+int32_t mivs_ivf_flat_extend(mivs_index_t idx, void* stream, const float* d_new, const int64_t* d_new_ids,
+                             int64_t n_new) {
+  return guarded([&] {
+    require(idx != nullptr && idx->kind == 0, "not an ivf_flat index");
+    require(n_new >= 0, "n_new must be >= 0");
+    require(n_new == 0 || d_new != nullptr, "new vectors are NULL");
+    if (n_new == 0) return;
+    std::lock_guard<std::mutex> g(idx->mu);
+    DeviceGuard dg(idx->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    ListSet& L = idx->lists;
+    const int d = idx->d;
+    const int nl = idx->cents.n_lists == 1 ? (int)idx->cents.n_rows : idx->cents.n_lists;
+    const int64_t n_old = L.n_rows, n_all = n_old + n_new;
+    // every row in list order (old rows first, so each list keeps its current order), ids beside them
+    Buf rows, ids, labels, norms, perm, off, ctmp;
+    rows.reserve(sizeof(float) * (size_t)n_all * d);
+    ids.reserve(sizeof(int64_t) * (size_t)n_all);
+    labels.reserve(sizeof(int64_t) * (size_t)n_all);
+    if (n_old > 0) {
+      HIPCHK(launch_unpack_rows(L.groups.as<float>(), idx->dp, d, L.off.as<int64_t>(), L.goff.as<int64_t>(), L.n_lists,
+                                n_old, rows.as<float>(), s));
+      HIPCHK(launch_compact_ids(L.ids.as<int64_t>(), L.off.as<int64_t>(), L.goff.as<int64_t>(), L.n_lists, n_old,
+                                ids.as<int64_t>(), s));
+      std::vector<int64_t> h_lab(n_old);
+      for (int l = 0; l < L.n_lists; ++l)
+        for (int64_t r = L.h_off[l]; r < L.h_off[l + 1]; ++r) h_lab[r] = l;
+      HIPCHK(hipMemcpyAsync(labels.p, h_lab.data(), sizeof(int64_t) * n_old, hipMemcpyHostToDevice, s));
+      HIPCHK(hipStreamSynchronize(s));
+    }
+    float* new_rows = rows.as<float>() + n_old * d;
+    HIPCHK(hipMemcpyAsync(new_rows, d_new, sizeof(float) * (size_t)n_new * d, hipMemcpyDeviceToDevice, s));
+    if (d_new_ids) HIPCHK(hipMemcpyAsync(ids.as<int64_t>() + n_old, d_new_ids, sizeof(int64_t) * n_new,
+                                         hipMemcpyDeviceToDevice, s));
+    else HIPCHK(launch_iota_i64(ids.as<int64_t>() + n_old, n_new, n_old, 1, s));
+    norms.reserve(sizeof(float) * (size_t)n_new);
+    HIPCHK(launch_row_norms(new_rows, n_new, d, norms.as<float>(), s));
+    assign_rows(new_rows, norms.as<float>(), nullptr, n_new, d, idx->dp, idx->cents, idx->G, idx->metric,
+                labels.as<int64_t>() + n_old, idx->device, idx->ws, s);
+    // stable counting sort by list, then re-pack every list
+    perm.reserve(sizeof(int64_t) * (size_t)n_all);
+    off.reserve(sizeof(int64_t) * (nl + 1));
+    const size_t cb = csort_tmp_bytes(n_all, nl);
+    ctmp.reserve(cb);
+    HIPCHK(launch_counting_sort(labels.as<int64_t>(), n_all, nl, perm.as<int64_t>(), off.as<int64_t>(), ctmp.p, cb, s));
+    std::vector<int64_t> h_off(nl + 1);
+    HIPCHK(hipMemcpyAsync(h_off.data(), off.p, sizeof(int64_t) * (nl + 1), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const bool had_pf = idx->groups_h.p != nullptr;
+    idx->groups_h.release();
+    pack_lists(L, rows.as<float>(), d, idx->dp, perm.as<int64_t>(), h_off, 0, ids.as<int64_t>(), idx->G, s);
+    if (had_pf) pf_enable(idx, s);
+    HIPCHK(hipStreamSynchronize(s));
+  });
+}
+
 int32_t mivs_ivf_flat_search(mivs_index_t idx, void* stream, const float* d_q, int64_t nq, int32_t k,
                              int32_t n_probes, float* d_dist, int64_t* d_ids, int32_t* d_probes) {
   return guarded([&] {

@@ -113,6 +113,9 @@ _SIGS = {
                                       POINTER(c_void_p)]),
     "mivs_ivf_flat_build_from_centroids": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_int32,
                                                      c_int32, c_int64, c_int32, POINTER(c_void_p)]),
+    "mivs_ivf_flat_build_from_lists": (c_int32, [c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,
+                                                 c_void_p, c_int32, c_int32, c_int32, c_int32, POINTER(c_void_p)]),
+    "mivs_ivf_flat_extend": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64]),
     "mivs_ivf_flat_search": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p,
                                        c_void_p]),
     "mivs_ivf_flat_get_centroids": (c_int32, [c_void_p, c_void_p, c_void_p]),

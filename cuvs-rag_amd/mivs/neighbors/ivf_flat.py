@@ -237,16 +237,73 @@ def search(search_params: SearchParams, index: Index, queries, k: int, neighbors
     return emit(dist), emit(nbrs)
 
 
-def extend(index: Index, new_vectors, new_indices=None):
-    raise NotImplementedError("ivf_flat.extend is not implemented yet in mivs (rebuild the index instead)")
+def extend(index: Index, new_vectors, new_indices=None) -> Index:
+    """cuvs.neighbors.ivf_flat.extend: append rows to their nearest lists (the build's assign; each list
+    keeps its current rows first). ``new_indices`` None: ids ``len(index) .. len(index) + n - 1``.
+    Returns ``index`` (extended in place)."""
+    if not isinstance(index, Index):
+        raise TypeError("index must be an ivf_flat.Index")
+    dev = index.device
+    x = as_device_f32(new_vectors, device=dev, name="new_vectors")
+    if x.shape[1] != index.dim:
+        raise ValueError(f"new_vectors have dim {x.shape[1]}, index has {index.dim}")
+    ids = None
+    if new_indices is not None:
+        ids = torch.as_tensor(new_indices).to(device=f"cuda:{dev}", dtype=torch.int64).contiguous().reshape(-1)
+        if ids.numel() != x.shape[0]:
+            raise ValueError(f"new_indices has {ids.numel()} entries, new_vectors {x.shape[0]} rows")
+    with torch.cuda.device(dev):
+        _native.check(_native.lib().mivs_ivf_flat_extend(index.handle, stream_ptr(dev), ptr(x), ptr(ids), x.shape[0]))
+    index.size += int(x.shape[0])
+    return index
+
+
+_SAVE_MAGIC = "mivs-ivf-flat-v1"
 
 
 def save(filename: str, index: Index, include_dataset: bool = True):
-    raise NotImplementedError("ivf_flat.save is not implemented yet in mivs")
+    """cuvs.neighbors.ivf_flat.save: centroids, list sizes and (with include_dataset) every list's rows and
+    ids, in list order, as a numpy .npz (plain arrays, no pickled objects)."""
+    import numpy as np
+
+    if not isinstance(index, Index):
+        raise TypeError("index must be an ivf_flat.Index")
+    torch.cuda.synchronize(index.device)
+    sizes = index.list_sizes.numpy()
+    if include_dataset:
+        rows = index.list_rows().cpu().numpy()
+        ids = index.list_ids().cpu().numpy()
+    else:
+        rows = np.zeros((0, index.dim), np.float32)
+        ids = np.zeros((0,), np.int64)
+        sizes = np.zeros_like(sizes)
+    np.savez(filename, magic=np.array(_SAVE_MAGIC), metric=np.array(index.metric),
+             centers=index.centers.cpu().numpy(), list_sizes=sizes.astype(np.int64), ids=ids.astype(np.int64),
+             rows=rows.astype(np.float32))
 
 
-def load(filename: str, resources=None):
-    raise NotImplementedError("ivf_flat.load is not implemented yet in mivs")
+def load(filename: str, resources=None, device: int | None = None, prefilter: bool = True) -> Index:
+    """cuvs.neighbors.ivf_flat.load: an index written by `save`, on `device` (default: the current one).
+    The lists keep their saved order and ids, so searches return what the saved index returned."""
+    import numpy as np
+
+    with np.load(filename, allow_pickle=False) as z:
+        if str(z["magic"]) != _SAVE_MAGIC:
+            raise ValueError(f"{filename!r} is not an mivs ivf_flat file")
+        metric = str(z["metric"])
+        centers, sizes, ids, rows = z["centers"], z["list_sizes"], z["ids"], z["rows"]
+    dev = torch.cuda.current_device() if device is None else int(device)
+    n_lists, dim = centers.shape
+    c = torch.from_numpy(np.ascontiguousarray(centers, dtype=np.float32)).to(f"cuda:{dev}")
+    r = torch.from_numpy(np.ascontiguousarray(rows, dtype=np.float32).reshape(-1, dim)).to(f"cuda:{dev}")
+    i = torch.from_numpy(np.ascontiguousarray(ids, dtype=np.int64)).to(f"cuda:{dev}")
+    hs = np.ascontiguousarray(sizes, dtype=np.int64)
+    h = ctypes.c_void_p()
+    with torch.cuda.device(dev):
+        _native.check(_native.lib().mivs_ivf_flat_build_from_lists(
+            dev, stream_ptr(dev), ptr(r), ptr(i), hs.ctypes.data_as(ctypes.c_void_p), r.shape[0], dim, ptr(c),
+            n_lists, metric_code(metric), 0, 1 if prefilter else 0, ctypes.byref(h)))
+    return Index(h.value, metric)
 
 
 def default_n_lists(n_rows: int) -> int:

@@ -109,6 +109,22 @@ int32_t mivs_ivf_flat_build_from_centroids(int32_t device, void* stream, const f
                                            int32_t dim, const float* d_centroids, int32_t n_lists,
                                            int32_t metric, int64_t id_offset, int32_t chunk_rows,
                                            mivs_index_t* out);
+
+/* Rebuild an IVF-Flat index from its exported parts: rows [n][dim] and ids [n] in list order (device),
+ * per-list sizes [n_lists] (HOST), centroids [n_lists][dim] (device). The lists keep the given order.
+ * Replaces the deserialize half of cuvs.neighbors.ivf_flat.save/load (cuvs 25.06, third-party; the
+ * reference's FAISS-side equivalent is faiss.read_index, Latest/faiss.ipynb:682-693). */
+int32_t mivs_ivf_flat_build_from_lists(int32_t device, void* stream, const float* d_rows, const int64_t* d_ids,
+                                       const int64_t* h_list_sizes, int64_t n, int32_t dim, const float* d_centroids,
+                                       int32_t n_lists, int32_t metric, int32_t chunk_rows, int32_t prefilter,
+                                       mivs_index_t* out);
+
+/* Append n_new rows [n_new][dim] (device) to an IVF-Flat index: each goes to its nearest list (the
+ * build's assign) after the list's current rows. d_new_ids == NULL: ids n_old .. n_old + n_new - 1.
+ * Replaces cuvs.neighbors.ivf_flat.extend (cuvs 25.06; FAISS IndexIVFFlat.add,
+ * colab_a100_test.ipynb:479). */
+int32_t mivs_ivf_flat_extend(mivs_index_t index, void* stream, const float* d_new, const int64_t* d_new_ids,
+                             int64_t n_new);
 /* ---- replaces cuvs.neighbors.ivf_flat.search(SearchParams(n_probes), index, q, k)
  *      (improved_multi_gpu_rag.py:225-227, cuvs-2gpu-main.ipynb:1801) ----
  *  d_probes (optional, may be NULL): [nq][n_probes] int32 probed list ids in probe order */
