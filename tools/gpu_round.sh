@@ -9,7 +9,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 export MIVS_SCAN_WIDE=${WIDE:-1}
 export MIVS_PREFILTER=${PF:-1}
-if [ "$MIVS_PREFILTER" = "1" ]; then KSUB="k_pf_scan<0"; KRE="k_pf_scan"; T=64_pf;
+if [ "$MIVS_PREFILTER" = "1" ]; then KSUB="k_pf_scan<0"; KRE="k_pf_scan<"; T=64_pf;
 elif [ "$MIVS_SCAN_WIDE" = "1" ]; then KSUB="k_scan_wide<12, 0, 4>"; KRE='k_scan_wide<12'; T=64; else KSUB="k_scan<12, 0, 8>"; KRE='k_scan<12'; T=32; fi
 if [ "${TESTS:-1}" = "1" ]; then
   timeout -k 10 700 python -m pytest tests -m gpu -x -q > $OUT/tests.log 2>&1
