@@ -190,6 +190,7 @@ def main():
         step(q)
     _native.set_profiling(True)
     idx.profile_collect()  # drop warmup records
+    torch.cuda.synchronize()
     sync_all(world)
     t0 = time.perf_counter()
     for _ in range(a.steps):
