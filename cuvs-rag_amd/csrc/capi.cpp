@@ -511,6 +511,7 @@ void pf_assign_rows(const PfAssign& P, const float* data, const float* data_norm
   a.x_res_max = resmax;
   a.qtheta = ws.qtheta.as<unsigned>();
   a.k = 1;
+  a.no_theta = chunks == 1 ? 1 : 0;  // every row's one work item: no bound to share
   const int grid = std::max(8, cu_count(device) / 8 * 8);
   if (use_r) HIPCHK(launch_pr_scan(a, grid, s));
   else HIPCHK(launch_pf_scan(a, grid, pf_scan_lds_bytes(dp, cg), s));

@@ -147,13 +147,26 @@ __global__ __launch_bounds__(256) void k_km_partial(const float* __restrict__ x,
   const int c = lo;
   const int64_t m0 = list_off[c] + (b - chunk_off[c]) * kKmChunk;
   const int64_t m1 = m0 + kKmChunk < list_off[c + 1] ? m0 + kKmChunk : list_off[c + 1];
+  const int cnt = (int)(m1 - m0);
+  // the chunk's member rows once into LDS (the perm -> rows -> x chain is then one load deep), then 8
+  // member loads in flight per dim; the fp64 sum keeps the member order (orc_kmeans_update)
+  __shared__ int64_t s_row[kKmChunk];
+  for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
+    const int64_t t = perm[m0 + i];
+    s_row[i] = rows ? rows[t] : t;
+  }
+  __syncthreads();
   for (int dim = threadIdx.x; dim < d; dim += blockDim.x) {
     double s = 0.0;
-    for (int64_t m = m0; m < m1; ++m) {
-      const int64_t t = perm[m];
-      const int64_t row = rows ? rows[t] : t;
-      s += (double)x[row * d + dim];
+    int m = 0;
+    for (; m + 8 <= cnt; m += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = x[s_row[m + u] * d + dim];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += (double)v[u];
     }
+    for (; m < cnt; ++m) s += (double)x[s_row[m] * d + dim];
     partial[b * d + dim] = s;
   }
 }

@@ -175,6 +175,7 @@ struct PfScanArgs {
   int flags;                  // timing experiments only (MIVS_PF_FLAGS): 1 skip epilogue, 8 skip staging,
                               // 16 skip merge, 32 phase clocks into prof
   unsigned long long* prof;   // [16] diagnostic phase clocks, or nullptr
+  int no_theta;               // 1: no query has another work item (one list, one chunk): skip qtheta updates
 };
 
 struct PfRefineArgs {

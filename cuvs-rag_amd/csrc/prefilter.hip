@@ -1032,9 +1032,9 @@ __global__ __launch_bounds__(kPrThreads, 1) void k_pf_scan_r(PfScanArgs a) {
       }
       const float4 b4 = *reinterpret_cast<const float4*>(s_ob + tid * kPrLists);
       a.slot_bound[slot] = fminf(fminf(b4.x, b4.y), fminf(b4.z, b4.w));
-      // k-th smallest kept key (rank count over the 32; ties broken by position in the scratch)
+      // k-th smallest kept key (rank count over the slot; ties broken by position in the scratch)
       float kth = INFINITY;
-      for (int c = 0; c < kPrLists * kPrLaneK; ++c) {
+      for (int c = 0; c < kPrLists * kPrLaneK && !a.no_theta; ++c) {
         const float v = ok[c];
         if (!(v < kth)) continue;
         int rank = 0;
