@@ -513,8 +513,25 @@ void pf_assign_rows(const PfAssign& P, const float* data, const float* data_norm
   a.k = 1;
   a.no_theta = chunks == 1 ? 1 : 0;  // every row's one work item: no bound to share
   const int grid = std::max(8, cu_count(device) / 8 * 8);
+  Buf pbuf;
+  const bool pprof = getenv("MIVS_PF_FLAGS") && (atoi(getenv("MIVS_PF_FLAGS")) & 32) && use_r;
+  if (pprof) {  // diagnostic: K12 phase clocks of the assign to stderr
+    pbuf.reserve(16 * sizeof(unsigned long long));
+    HIPCHK(hipMemsetAsync(pbuf.p, 0, 16 * sizeof(unsigned long long), s));
+    a.prof = pbuf.as<unsigned long long>();
+  }
   if (use_r) HIPCHK(launch_pr_scan(a, grid, s));
   else HIPCHK(launch_pf_scan(a, grid, pf_scan_lds_bytes(dp, cg), s));
+  if (pprof) {
+    unsigned long long hp[16];
+    HIPCHK(hipMemcpyAsync(hp, pbuf.p, sizeof(hp), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const double w = (double)hp[7];
+    fprintf(stderr, "[k12 assign phases] nr %lld clock %.3f GHz | fetch %.3f setup %.3f loop %.3f tail %.3f | "
+            "cycles/group %.0f slow %.4f\n", (long long)nr, hp[8] ? (double)hp[7] / hp[8] * 0.1 : 0.0, hp[0] / w,
+            hp[1] / w, hp[2] / w, hp[3] / w, hp[5] ? (double)hp[2] / hp[5] : 0.0,
+            hp[5] ? (double)hp[6] / hp[5] : 0.0);
+  }
   Buf tmp_d, stats;
   tmp_d.reserve(sizeof(float) * (size_t)std::max<int64_t>(nr, 1));
   stats.reserve(32);
