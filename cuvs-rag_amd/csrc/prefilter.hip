@@ -36,6 +36,37 @@ constexpr int kPfMergeBytes = kPfQTile * 16 * kPfLaneK * 8;          // [64 quer
 
 __device__ __forceinline__ h8 ld_h8(const uint16_t* p) { return *reinterpret_cast<const h8*>(p); }
 
+// ---- 16-lane (DPP row) reductions: a butterfly over quad_perm [1,0,3,2], quad_perm [2,3,0,1],
+// row_half_mirror, row_mirror -- every lane of the row ends with the row's result, without the LDS
+// round trips of ds_bpermute (__shfl_xor) ----
+template <int CTRL>
+__device__ __forceinline__ int pf_dpp(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ float pf_dpp(float v) {
+  return __builtin_bit_cast(float, pf_dpp<CTRL>(__builtin_bit_cast(int, v)));
+}
+template <int CTRL>
+__device__ __forceinline__ void pf_row_min_step(float& k, int& p) {
+  const float ok = pf_dpp<CTRL>(k);
+  const int op = pf_dpp<CTRL>(p);
+  if (ok < k || (ok == k && op < p)) { k = ok; p = op; }
+}
+// lexicographic (key, pos) minimum over the 16 lanes of a DPP row
+__device__ __forceinline__ void pf_row_min(float& k, int& p) {
+  pf_row_min_step<0xB1>(k, p);
+  pf_row_min_step<0x4E>(k, p);
+  pf_row_min_step<0x141>(k, p);
+  pf_row_min_step<0x140>(k, p);
+}
+__device__ __forceinline__ float pf_row_fmin(float v) {
+  v = fminf(v, pf_dpp<0xB1>(v));
+  v = fminf(v, pf_dpp<0x4E>(v));
+  v = fminf(v, pf_dpp<0x141>(v));
+  return fminf(v, pf_dpp<0x140>(v));
+}
+
 template <int KL>
 __device__ __forceinline__ void pf_insert(float (&lk)[KL], int (&lp)[KL], float key, int pos) {
 #pragma unroll
@@ -400,20 +431,23 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
       // (theta drops are keys > theta: the bound is the next float up, so a theta equal to the
       // refine's window -- the common case when one slot holds the whole top-k -- is no overflow)
       if (src == 0) bnd = fminf(bnd, nextafterf(fminf(s_th[qi], pf_theta(s_l8 + qi * 16, s_dl[qi])), INFINITY));
-#pragma unroll
-      for (int off = 8; off >= 1; off >>= 1) bnd = fminf(bnd, __shfl_xor(bnd, off, 16));
+      bnd = pf_row_fmin(bnd);
       // fast path (the common case once theta is tight): fewer than k kept keys in all 16 lists
       // -> compact them unsorted into the slot (the refine needs no order), pad with +inf
       int cnt = 0;
 #pragma unroll
       for (int i = 0; i < kPfLaneK; ++i) cnt += myk[i] < INFINITY ? 1 : 0;
-      int pre = cnt;  // inclusive prefix over the query's 16 lists
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1) {
-        const int o = __shfl_up(pre, off, 16);
-        if (src >= off) pre += o;
-      }
-      const int total = __shfl(pre, 15, 16);
+      // inclusive prefix over the query's 16 lists (DPP row_shr 1, 2, 4, 8 with zero fill) and the total
+      int pre = cnt;
+      pre += __builtin_amdgcn_update_dpp(0, pre, 0x111, 0xF, 0xF, true);
+      pre += __builtin_amdgcn_update_dpp(0, pre, 0x112, 0xF, 0xF, true);
+      pre += __builtin_amdgcn_update_dpp(0, pre, 0x114, 0xF, 0xF, true);
+      pre += __builtin_amdgcn_update_dpp(0, pre, 0x118, 0xF, 0xF, true);
+      int total = cnt;
+      total += pf_dpp<0xB1>(total);
+      total += pf_dpp<0x4E>(total);
+      total += pf_dpp<0x141>(total);
+      total += pf_dpp<0x140>(total);
       if (total < a.k) {  // uniform within the 16-lane group
         if (slot >= 0) {
           const int64_t sb = slot * a.slot_k;
@@ -432,11 +466,11 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
       for (int r = 0; r <= a.slot_k; ++r) {  // slot_k outputs, then the smallest key left behind
         float bk = hk;
         int bp = hp;
-#pragma unroll
-        for (int off = 8; off >= 1; off >>= 1) {
-          const float ok = __shfl_xor(bk, off, 16);
-          const int op = __shfl_xor(bp, off, 16);
-          if (ok < bk || (ok == bk && op < bp)) { bk = ok; bp = op; }
+        pf_row_min(bk, bp);
+        if (!(bk < INFINITY)) {  // every list is exhausted: the rest of the slot is empty, nothing left behind
+          if (src == 0 && slot >= 0)
+            for (int t = r; t < a.slot_k; ++t) { a.slot_key[slot * a.slot_k + t] = INFINITY; a.slot_pos[slot * a.slot_k + t] = INT_MAX; }
+          break;
         }
         if (r < a.slot_k) {
           if (src == 0 && slot >= 0) {
