@@ -1247,15 +1247,19 @@ int32_t mivs_ivf_pq_build(int32_t device, void* stream, const float* d_data, int
     norms.reserve(sizeof(float) * n);
     HIPCHK(launch_row_norms(d_data, n, dim, norms.as<float>(), s));
     HIPCHK(hipStreamSynchronize(s));
-    kmeans_fit_impl(d_data, norms.as<float>(), rows.as<int64_t>(), nt, dim, idx->dp, nl, p->kmeans_n_iters,
-                    idx->centroids_rm.as<float>(), idx->G, device, idx->ws, s, p->kmeans_balance != 0);
-    make_single_list(idx->cents, idx->centroids_rm.as<float>(), nl, dim, idx->dp, 0, idx->G, s);
-    // ---- lists: L2 assignment of every row, stable order by label ----
-    labels.reserve(sizeof(int64_t) * n);
-    perm.reserve(sizeof(int64_t) * n);
-    off.reserve(sizeof(int64_t) * (nl + 1));
-    assign_rows(d_data, norms.as<float>(), nullptr, n, dim, idx->dp, idx->cents, idx->G, kL2, labels.as<int64_t>(),
-                device, idx->ws, s);
+    {
+      PfAssign pfa;  // coarse k-means + list assign through the fp16 pre-filter
+      pf_assign_prepare(pfa, d_data, n, dim, idx->dp, s);
+      kmeans_fit_impl(d_data, norms.as<float>(), rows.as<int64_t>(), nt, dim, idx->dp, nl, p->kmeans_n_iters,
+                      idx->centroids_rm.as<float>(), idx->G, device, idx->ws, s, p->kmeans_balance != 0, &pfa);
+      make_single_list(idx->cents, idx->centroids_rm.as<float>(), nl, dim, idx->dp, 0, idx->G, s);
+      // ---- lists: L2 assignment of every row, stable order by label ----
+      labels.reserve(sizeof(int64_t) * n);
+      perm.reserve(sizeof(int64_t) * n);
+      off.reserve(sizeof(int64_t) * (nl + 1));
+      assign_rows(d_data, norms.as<float>(), nullptr, n, dim, idx->dp, idx->cents, idx->G, kL2,
+                  labels.as<int64_t>(), device, idx->ws, s, &pfa);
+    }
     const size_t cb = csort_tmp_bytes(n, nl);
     ctmp.reserve(cb);
     HIPCHK(launch_counting_sort(labels.as<int64_t>(), n, nl, perm.as<int64_t>(), off.as<int64_t>(), ctmp.p, cb, s));
