@@ -408,6 +408,13 @@ struct PfAssign {
   bool ok = false;
 };
 
+// the most groups a K10 work item may span: its chunk's norms sit in LDS beside the query tile
+int pf_max_chunk_groups(int dp) {
+  int g = 1;
+  while (pf_scan_lds_bytes(dp, g + 1) <= 160 * 1024) ++g;
+  return g;
+}
+
 bool pf_assign_on() {
   const char* e = getenv("MIVS_PF_ASSIGN");
   return !(e && e[0] == '0');
@@ -455,7 +462,8 @@ void pf_assign_rows(const PfAssign& P, const float* data, const float* data_norm
   const char* are = getenv("MIVS_PF_ASSIGN_REG");
   const bool use_r = !(are && are[0] == '0') && pr_scan_supported(dp);
   const int cg = use_r ? std::max<int>(1, (int)std::min<int64_t>(cents.n_groups, 1 << 20))
-                       : std::max(1, std::min<int>(kPfChunkGroups, (int)cents.n_groups));
+                       : std::max(1, std::min<int>(std::min(kPfChunkGroups, pf_max_chunk_groups(dp)),
+                                                   (int)cents.n_groups));
   const int64_t chunks = std::max<int64_t>(1, ceil_div(cents.n_groups, cg));
   const int64_t nslots = nr * chunks;
   ws.bucket_q.reserve(sizeof(int64_t) * nr);
@@ -699,8 +707,7 @@ void pf_enable(mivs_index_s* idx, hipStream_t s) {
   const char* ce = getenv("MIVS_PF_CHUNK_ROWS");
   // rows per work item: as many as the LDS holds the norms of beside the query tile (the tile's
   // staging is paid once per item), unless MIVS_PF_CHUNK_ROWS asks for fewer
-  int gmax = kPfChunkGroups;
-  while (pf_scan_lds_bytes(idx->dp, gmax + 1) <= 160 * 1024) ++gmax;
+  const int gmax = pf_max_chunk_groups(idx->dp);
   idx->pf_G = std::max(1, std::min(gmax, ce ? atoi(ce) / kGroupRows : kPfChunkGroups));
   auto top_prefix = [&](int G, std::vector<int64_t>& out) {
     for (int l = 0; l < L.n_lists; ++l) c[l] = L.chunks_of(l, G);
@@ -742,7 +749,7 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   // per-slot candidates: room above k so that a neighbourhood packed into one chunk does not overflow
   // (K12: the query's four lane lists of 4)
   const char* ske = getenv("MIVS_PF_SLOT_K");  // K10 slot size override (16 or 32)
-  const int slot_k = use_r ? kPrSlotK : (ske ? (atoi(ske) > 16 ? kPfSlotKMax : 16) : (k <= 10 ? 16 : kPfSlotKMax));
+  const int slot_k = use_r ? kPrSlotK : (ske ? (atoi(ske) > 16 ? kPfSlotKMax : 16) : kPfSlotKMax);
   ws.pf_key.reserve(sizeof(float) * (size_t)max_slots * slot_k);
   ws.pf_pos.reserve(sizeof(int) * (size_t)max_slots * slot_k);
   ws.pf_bound.reserve(sizeof(float) * (size_t)max_slots);

@@ -146,7 +146,7 @@ constexpr int kPfLaneK = 8;      // per-lane approximate list length in K10
 constexpr int kPfSlotKMax = 32;  // approximate candidates kept per slot: 16 for k <= 10, else 32
 constexpr int kPfMaxK = 16;      // largest k served by the pre-filter path
 constexpr int kPfCap = 64;       // refine capacity (window candidates per query)
-constexpr int kPfChunkGroups = 128;  // default groups (4096 rows) per K10 work item (MIVS_PF_CHUNK_ROWS)
+constexpr int kPfChunkGroups = 256;  // default groups (8192 rows) per K10 work item (MIVS_PF_CHUNK_ROWS)
 
 struct PfScanArgs {
   const uint16_t* groups_h;   // fp16 lists, group layout [g][dp/8][32][8]

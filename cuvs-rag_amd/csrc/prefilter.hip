@@ -201,7 +201,7 @@ __device__ __forceinline__ float pf_theta(const float* __restrict__ l8, float de
 // eighth of the (list, chunk, tile)-ordered items, so the query tiles of one chunk run at the same
 // time on CUs sharing an L2 and all but the first read the chunk's rows as L2 hits. A workgroup
 // whose queue is empty takes items from the next queues.
-template <int METRIC, int D>
+template <int METRIC, int D, int R>
 __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int64_t* s_q = reinterpret_cast<int64_t*>(smem);          // [64] query ids (-1: empty)
@@ -333,7 +333,82 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
     const int src = wave * 2 + h;  // this lane's list index among the query's 16
 
     const char* s_bl = s_b + lane * 16;  // this lane's B operand at k-step s: + s * 1024 (+ nb * 512: group 1)
-    const int npw = wave < ng ? (ng - wave + kPfWaves - 1) / kPfWaves : 0;  // passes of this wave
+    const int npw = wave < ng ? (ng - wave + kPfWaves - 1) / kPfWaves : 0;  // groups (passes) of this wave
+    // the epilogue of one finished group (its 32 x 64 dots) + the theta refresh
+    auto epilogue = [&](const f32x16& c0, const f32x16& c1, int lg) {
+      if (a.flags & 1) return;
+      if (a.prof) ++pr_epi;
+      const bool slow = pf_epilogue<METRIC>(c0, c1, s_norm + lg * kGroupRows, (g_begin + lg) * kGroupRows, h, qn0,
+                                            qs0, th0, uf0, qn1, qs1, th1, uf1, lk0, lp0, lk1, lp1);
+      if (a.prof && slow) ++pr_slow;
+      // publish this lane's list ends, refresh theta from all 16 (no barrier: every value ever
+      // stored is the end of a real list, so a stale read only gives a looser, still valid theta)
+      s_l8[j * 16 + src] = lk0[kPfLaneK - 1];
+      s_l8[(32 + j) * 16 + src] = lk1[kPfLaneK - 1];
+      th0 = fminf(th0, pf_theta(s_l8 + j * 16, dl0));
+      th1 = fminf(th1, pf_theta(s_l8 + (32 + j) * 16, dl1));
+      uf0 = pf_uf<METRIC>(lk0[kPfLaneK - 1], th0, qn0, xnmax2);
+      uf1 = pf_uf<METRIC>(lk1[kPfLaneK - 1], th1, qn1, xnmax2);
+    };
+    if constexpr (R == 2) {
+      // two groups per pass (g = wave + 8i, pairs i = 2p, 2p + 1): every B operand read from LDS feeds
+      // 4 MFMAs instead of 2, halving the LDS traffic per flop; an odd last pair re-reads its first group
+      const int npair = (npw + 1) >> 1;
+      if (npw > 0) {
+        const uint16_t* abase = a.groups_h + ((g_begin + wave) * nb + h) * 256 + j * 8;
+        int lp_ = 0, ls = 0;  // pair / k-step of the next load (past the end: re-read the last pair)
+        auto pair_ptr = [&](int pr, int which) {
+          int gi = 2 * pr + which;
+          gi = gi < npw ? gi : npw - 1;
+          return abase + (int64_t)gi * pstride;
+        };
+        const uint16_t* na = pair_ptr(0, 0);
+        const uint16_t* nbp = pair_ptr(0, 1);
+        h8 ra[D], rb[D];
+#pragma unroll
+        for (int u = 0; u < D; ++u) {
+          ra[u] = ld_h8(na + (ls + u) * 512);
+          rb[u] = ld_h8(nbp + (ls + u) * 512);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        ls += D;
+        if (ls == nk) { ls = 0; if (++lp_ < npair) { na = pair_ptr(lp_, 0); nbp = pair_ptr(lp_, 1); } }
+        const f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        f32x16 a0 = zero, a1 = zero, b0 = zero, b1 = zero;
+        int p = 0, s = 0;
+        h8 bq0[2], bq1[2];
+        bq0[0] = *reinterpret_cast<const h8*>(s_bl);
+        bq1[0] = *reinterpret_cast<const h8*>(s_bl + nb * 512);
+        for (int t0 = 0; t0 < npair * nk; t0 += D) {
+#pragma unroll
+          for (int u = 0; u < D; ++u) {
+            int sn = s + u + 1;
+            if (sn >= nk) sn -= nk;
+            bq0[(u + 1) & 1] = *reinterpret_cast<const h8*>(s_bl + sn * 1024);
+            bq1[(u + 1) & 1] = *reinterpret_cast<const h8*>(s_bl + nb * 512 + sn * 1024);
+            a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[u], bq0[u & 1], a0, 0, 0, 0);
+            a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[u], bq1[u & 1], a1, 0, 0, 0);
+            b0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(rb[u], bq0[u & 1], b0, 0, 0, 0);
+            b1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(rb[u], bq1[u & 1], b1, 0, 0, 0);
+            ra[u] = ld_h8(na + (ls + u) * 512);
+            rb[u] = ld_h8(nbp + (ls + u) * 512);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);  // VMEM read
+          }
+          ls += D;
+          if (ls == nk) { ls = 0; if (++lp_ < npair) { na = pair_ptr(lp_, 0); nbp = pair_ptr(lp_, 1); } }
+          s += D;
+          if (s == nk) {
+            epilogue(a0, a1, 2 * p * kPfWaves + wave);
+            if (2 * p + 1 < npw) epilogue(b0, b1, (2 * p + 1) * kPfWaves + wave);
+            a0 = zero; a1 = zero; b0 = zero; b1 = zero;
+            s = 0;
+            ++p;
+          }
+        }
+      }
+    } else {
     if (npw > 0) {
       const uint16_t* abase = a.groups_h + ((g_begin + wave) * nb + h) * 256 + j * 8;
       const uint16_t* nptr = abase;  // pass base of the next load
@@ -379,21 +454,7 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
         ls += D;
         if (ls == nk) { ls = 0; if (++lpass < npw) nptr += pstride; }
         s += D;
-        if (s == nk && !(a.flags & 1)) {
-          const int lg = p * kPfWaves + wave;  // group within the chunk
-          if (a.prof) ++pr_epi;
-          const bool slow = pf_epilogue<METRIC>(c0, c1, s_norm + lg * kGroupRows, (g_begin + lg) * kGroupRows, h, qn0, qs0, th0,
-                              uf0, qn1, qs1, th1, uf1, lk0, lp0, lk1, lp1);
-          if (a.prof && slow) ++pr_slow;
-          // publish this lane's list ends, refresh theta from all 16 (no barrier: every value ever
-          // stored is the end of a real list, so a stale read only gives a looser, still valid theta)
-          s_l8[j * 16 + src] = lk0[kPfLaneK - 1];
-          s_l8[(32 + j) * 16 + src] = lk1[kPfLaneK - 1];
-          th0 = fminf(th0, pf_theta(s_l8 + j * 16, dl0));
-          th1 = fminf(th1, pf_theta(s_l8 + (32 + j) * 16, dl1));
-          uf0 = pf_uf<METRIC>(lk0[kPfLaneK - 1], th0, qn0, xnmax2);
-          uf1 = pf_uf<METRIC>(lk1[kPfLaneK - 1], th1, qn1, xnmax2);
-        }
+        if (s == nk) epilogue(c0, c1, p * kPfWaves + wave);
         if (s == nk) {
           c0 = zero;
           c1 = zero;
@@ -401,6 +462,8 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
           ++p;
         }
       }
+    }
+
     }
 
     // ---- per query: 16 lane lists (8 waves x 2 halves) -> slot top-slot_k + dropped-key bound ----
@@ -1220,33 +1283,34 @@ size_t pf_scan_lds_bytes(int dp, int chunk_groups) {
          (b > (size_t)kPfMergeBytes ? b : (size_t)kPfMergeBytes);
 }
 
-template <int METRIC, int D>
+template <int METRIC, int D, int R>
 static hipError_t launch_pf_scan_md(const PfScanArgs& a, int grid, size_t lds, hipStream_t s) {
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pf_scan<METRIC, D>),
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pf_scan<METRIC, D, R>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL((k_pf_scan<METRIC, D>), dim3(grid), dim3(kPfThreads), lds, s, a);
+  hipLaunchKernelGGL((k_pf_scan<METRIC, D, R>), dim3(grid), dim3(kPfThreads), lds, s, a);
   return hipGetLastError();
+}
+
+template <int METRIC>
+static hipError_t launch_pf_scan_m(const PfScanArgs& a, int grid, size_t lds, hipStream_t s) {
+  // default: two groups per pass with 6-deep rings (half the LDS operand traffic per flop: the kernel is
+  // power-bound); MIVS_PF_PAIR=0: one group per pass with MIVS_PF_DEPTH (16) k-steps in flight
+  const int nk = a.dp / 16;
+  const char* pe = getenv("MIVS_PF_PAIR");
+  const bool pair = !(pe && pe[0] == '0');
+  if (pair) return nk % 6 == 0 ? launch_pf_scan_md<METRIC, 6, 2>(a, grid, lds, s)
+                               : launch_pf_scan_md<METRIC, 4, 2>(a, grid, lds, s);
+  const int dsel = getenv("MIVS_PF_DEPTH") ? atoi(getenv("MIVS_PF_DEPTH")) : 16;
+  if (dsel >= 16 && nk % 16 == 0) return launch_pf_scan_md<METRIC, 16, 1>(a, grid, lds, s);
+  if (dsel >= 8 && nk % 8 == 0) return launch_pf_scan_md<METRIC, 8, 1>(a, grid, lds, s);
+  return launch_pf_scan_md<METRIC, 4, 1>(a, grid, lds, s);
 }
 
 // grid: a multiple of 8 (one queue per XCD group); the work counters (8 x 16 ints) are zeroed by the caller
 hipError_t launch_pf_scan(const PfScanArgs& a, int grid, size_t lds, hipStream_t s) {
   if (a.dp % 64 != 0 || a.dp > 1024 || lds > 160 * 1024) return hipErrorInvalidValue;
-  // k-steps in flight per wave: 16 when the k-loop allows (the A stream is latency-bound), else 8 or 4
-  const int nk = a.dp / 16;
-  const int dsel = getenv("MIVS_PF_DEPTH") ? atoi(getenv("MIVS_PF_DEPTH")) : 16;
-  const int D = (dsel >= 24 && nk % 24 == 0) ? 24 : (dsel >= 16 && nk % 16 == 0) ? 16
-               : (dsel >= 12 && nk % 12 == 0) ? 12 : ((dsel >= 8 && nk % 8 == 0) ? 8 : 4);
-  if (a.metric == kIP) {
-    if (D == 24) return launch_pf_scan_md<kIP, 24>(a, grid, lds, s);
-    if (D == 12) return launch_pf_scan_md<kIP, 12>(a, grid, lds, s);
-    if (D == 16) return launch_pf_scan_md<kIP, 16>(a, grid, lds, s);
-    return D == 8 ? launch_pf_scan_md<kIP, 8>(a, grid, lds, s) : launch_pf_scan_md<kIP, 4>(a, grid, lds, s);
-  }
-  if (D == 24) return launch_pf_scan_md<kL2, 24>(a, grid, lds, s);
-  if (D == 16) return launch_pf_scan_md<kL2, 16>(a, grid, lds, s);
-  if (D == 12) return launch_pf_scan_md<kL2, 12>(a, grid, lds, s);
-  return D == 8 ? launch_pf_scan_md<kL2, 8>(a, grid, lds, s) : launch_pf_scan_md<kL2, 4>(a, grid, lds, s);
+  return a.metric == kIP ? launch_pf_scan_m<kIP>(a, grid, lds, s) : launch_pf_scan_m<kL2>(a, grid, lds, s);
 }
 
 size_t pr_scan_lds_bytes(int dp) { return (size_t)2 * dp * 64 + 2 * kPrWaves * 64 * 8 * 4 + 4 * 64 * 4 + 16; }
