@@ -53,6 +53,7 @@ PF_CASES = [
     (9000, 384, 33, 20, 8, 16, "sqeuclidean"),     # k = kPfMaxK
     (7000, 128, 90, 24, 6, 10, "inner_product"),
     (5000, 33, 40, 8, 3, 7, "inner_product"),
+    (4000, 1000, 40, 8, 3, 10, "sqeuclidean"),     # dp = 1024: the LDS-capped work-item size
 ]
 
 
