@@ -162,13 +162,19 @@ __device__ __forceinline__ bool pf_epilogue(const f32x16& c0, const f32x16& c1, 
   if (__ballot(mn0 < uf0 || mn1 < uf1) == 0) return false;
   // a key is kept if it beats the lane list AND lies within the query's window bound theta
   // (th = -inf for empty query slots: nothing is kept)
+  // the exact key only where the one-fma filter passes (it never rejects a key the exact test keeps)
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int pos = (int)(rb + (r & 3) + 8 * (r >> 2) + 4 * h);
-    const float k0 = pf_key<METRIC>(c0[r], qs0, xn[r], qn0);
-    if (k0 < lk0[kPfLaneK - 1] && k0 <= th0) pf_insert<kPfLaneK>(lk0, lp0, k0, pos);
-    const float k1 = pf_key<METRIC>(c1[r], qs1, xn[r], qn1);
-    if (k1 < lk1[kPfLaneK - 1] && k1 <= th1) pf_insert<kPfLaneK>(lk1, lp1, k1, pos);
+    const float b = METRIC == kL2 ? xn[r] : 0.0f;
+    if (fmaf(c0[r], m0, b) < uf0) {
+      const float k0 = pf_key<METRIC>(c0[r], qs0, xn[r], qn0);
+      if (k0 < lk0[kPfLaneK - 1] && k0 <= th0) pf_insert<kPfLaneK>(lk0, lp0, k0, pos);
+    }
+    if (fmaf(c1[r], m1, b) < uf1) {
+      const float k1 = pf_key<METRIC>(c1[r], qs1, xn[r], qn1);
+      if (k1 < lk1[kPfLaneK - 1] && k1 <= th1) pf_insert<kPfLaneK>(lk1, lp1, k1, pos);
+    }
   }
   return true;
 }
