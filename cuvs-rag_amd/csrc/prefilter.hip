@@ -347,6 +347,9 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
       const bool slow = pf_epilogue<METRIC>(c0, c1, s_norm + lg * kGroupRows, (g_begin + lg) * kGroupRows, h, qn0,
                                             qs0, th0, uf0, qn1, qs1, th1, uf1, lk0, lp0, lk1, lp1);
       if (a.prof && slow) ++pr_slow;
+      // no insertion anywhere in this wave: its lists, and so its published ends, did not change (the
+      // other waves' ends may have, but a stale theta is only looser, still valid)
+      if (!slow) return;
       // publish this lane's list ends, refresh theta from all 16 (no barrier: every value ever
       // stored is the end of a real list, so a stale read only gives a looser, still valid theta)
       s_l8[j * 16 + src] = lk0[kPfLaneK - 1];
