@@ -753,9 +753,17 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   ws.pf_key.reserve(sizeof(float) * (size_t)max_slots * slot_k);
   ws.pf_pos.reserve(sizeof(int) * (size_t)max_slots * slot_k);
   ws.pf_bound.reserve(sizeof(float) * (size_t)max_slots);
-  ws.counter.reserve(8 * 16 * sizeof(int));
-  HIPCHK(hipMemsetAsync(ws.counter.p, 0, 8 * 16 * sizeof(int), s));
+  // the 8 queue counters, then (K10) one convoy position per (list, chunk)
+  const char* cve = getenv("MIVS_PF_CONVOY");
+  const bool convoy = !use_r && !(cve && cve[0] == '0');
+  const int64_t n_cpos = convoy ? (int64_t)L.n_lists * tcp[1] : 0;
+  ws.counter.reserve(sizeof(int) * (8 * 16 + n_cpos));
+  HIPCHK(hipMemsetAsync(ws.counter.p, 0, sizeof(int) * (8 * 16 + n_cpos), s));
   PfScanArgs a{};
+  if (convoy) {
+    a.chunk_pos = ws.counter.as<int>() + 8 * 16;
+    a.chunk_stride = (int)tcp[1];
+  }
   a.groups_h = idx->groups_h.as<uint16_t>();
   a.row_norms = L.norms.as<float>();
   a.list_goff = L.goff.as<int64_t>();

@@ -176,6 +176,9 @@ struct PfScanArgs {
                               // 16 skip merge, 32 phase clocks into prof
   unsigned long long* prof;   // [16] diagnostic phase clocks, or nullptr
   int no_theta;               // 1: no query has another work item (one list, one chunk): skip qtheta updates
+  int* chunk_pos;             // [n_lists * chunk_stride] K10 convoy: the pair a chunk's tiles are scanning
+                              // (zeroed before launch), or nullptr (every tile scans from pair 0)
+  int chunk_stride;           // max chunks per list
 };
 
 struct PfRefineArgs {

@@ -299,6 +299,8 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
     }
     for (int i = tid; i < kPfQTile * 16; i += kPfThreads) s_l8[i] = INFINITY;
     for (int i = tid; i < ng * kGroupRows; i += kPfThreads) s_norm[i] = a.row_norms[g_begin * kGroupRows + i];
+    int* const cpos = a.chunk_pos ? a.chunk_pos + (int64_t)l * a.chunk_stride + chunk : nullptr;
+    if (tid == 0) s_misc[2] = cpos ? __hip_atomic_load(cpos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
     __syncthreads();
     // stage the fp16 query tile. B image: [2 query groups][nb blocks][32 queries] x 16 B, so that the
     // operand of (group t, k-step s) for lane (j, h) sits at t*nb*512 + s*1024 + lane*16: one contiguous
@@ -362,12 +364,18 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
     if constexpr (R == 2) {
       // two groups per pass (g = wave + 8i, pairs i = 2p, 2p + 1): every B operand read from LDS feeds
       // 4 MFMAs instead of 2, halving the LDS traffic per flop; an odd last pair re-reads its first group
+      // Convoy: the tiles of one chunk start at different times on CUs of one XCD; a late tile joins
+      // the pair the earlier ones are scanning (cpos, published after every pair) and wraps round to the
+      // pairs it skipped, so the tiles read the chunk together as L2 hits instead of a second time from
+      // HBM once their lag exceeds the L2's reach. The visiting order changes no result.
       const int npair = (npw + 1) >> 1;
       if (npw > 0) {
+        const int rot = s_misc[2] % npair;
+        auto phys = [&](int pr) { return pr + rot < npair ? pr + rot : pr + rot - npair; };
         const uint16_t* abase = a.groups_h + ((g_begin + wave) * nb + h) * 256 + j * 8;
         int lp_ = 0, ls = 0;  // pair / k-step of the next load (past the end: re-read the last pair)
         auto pair_ptr = [&](int pr, int which) {
-          int gi = 2 * pr + which;
+          int gi = 2 * phys(pr) + which;
           gi = gi < npw ? gi : npw - 1;
           return abase + (int64_t)gi * pstride;
         };
@@ -409,8 +417,11 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
           if (ls == nk) { ls = 0; if (++lp_ < npair) { na = pair_ptr(lp_, 0); nbp = pair_ptr(lp_, 1); } }
           s += D;
           if (s == nk) {
-            epilogue(a0, a1, 2 * p * kPfWaves + wave);
-            if (2 * p + 1 < npw) epilogue(b0, b1, (2 * p + 1) * kPfWaves + wave);
+            const int pp = phys(p);
+            if (cpos && wave == 0 && lane == 0)
+              __hip_atomic_store(cpos, pp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            epilogue(a0, a1, 2 * pp * kPfWaves + wave);
+            if (2 * pp + 1 < npw) epilogue(b0, b1, (2 * pp + 1) * kPfWaves + wave);
             a0 = zero; a1 = zero; b0 = zero; b1 = zero;
             s = 0;
             ++p;
