@@ -74,7 +74,8 @@ def build(dataset, metric: str = "sqeuclidean", metric_arg: float = 2.0, resourc
     return Index(h.value, metric)
 
 
-def search(index: Index, queries, k: int, neighbors=None, distances=None, resources=None):
+def _search(index, queries, k: int, neighbors=None, distances=None):
+    """search() without the output hook: torch tensors on the index's device (mivs.neighbors.streaming)."""
     if not isinstance(index, Index):
         raise TypeError("index must be a brute_force.Index")
     k = int(k)
@@ -91,8 +92,16 @@ def search(index: Index, queries, k: int, neighbors=None, distances=None, resour
         _native.check(_native.lib().mivs_brute_force_search(index.handle, stream_ptr(dev), ptr(q), nq, k, ptr(dist),
                                                             ptr(nbrs)))
     if index.metric in _SQRT_METRICS:
-        dist = torch.sqrt(dist)
-    return emit(dist), emit(nbrs)
+        dist.sqrt_()  # in place: a caller-provided `distances` holds the final values
+    return dist, nbrs
+
+
+def _emit2(r):
+    return emit(r[0]), emit(r[1])
+
+
+def search(index: Index, queries, k: int, neighbors=None, distances=None, resources=None):
+    return _emit2(_search(index, queries, k, neighbors, distances))
 
 
 def knn(dataset, queries, k: int, metric: str = "sqeuclidean"):

@@ -213,9 +213,8 @@ def build_from_centroids(centroids, dataset, metric: str = "sqeuclidean", ids_of
     return idx
 
 
-def search(search_params: SearchParams, index: Index, queries, k: int, neighbors=None, distances=None,
-           resources=None, probes_out: torch.Tensor | None = None):
-    """k-NN over the n_probes closest lists. Returns ``(distances, neighbors)`` ([nq, k] f32, [nq, k] i64)."""
+def _search(search_params, index, queries, k: int, neighbors=None, distances=None, probes_out=None):
+    """search() without the output hook: torch tensors on the index's device (mivs.neighbors.streaming)."""
     if not isinstance(index, Index):
         raise TypeError("index must be an ivf_flat.Index")
     sp = search_params if search_params is not None else SearchParams()
@@ -233,8 +232,18 @@ def search(search_params: SearchParams, index: Index, queries, k: int, neighbors
         _native.check(_native.lib().mivs_ivf_flat_search(index.handle, stream_ptr(dev), ptr(q), nq, k, sp.n_probes,
                                                          ptr(dist), ptr(nbrs), ptr(probes_out)))
     if index.metric in _SQRT_METRICS:
-        dist = torch.sqrt(dist)
-    return emit(dist), emit(nbrs)
+        dist.sqrt_()  # in place: a caller-provided `distances` holds the final values
+    return dist, nbrs
+
+
+def _emit2(r):
+    return emit(r[0]), emit(r[1])
+
+
+def search(search_params: SearchParams, index: Index, queries, k: int, neighbors=None, distances=None,
+           resources=None, probes_out: torch.Tensor | None = None):
+    """k-NN over the n_probes closest lists. Returns ``(distances, neighbors)`` ([nq, k] f32, [nq, k] i64)."""
+    return _emit2(_search(search_params, index, queries, k, neighbors, distances, probes_out))
 
 
 def extend(index: Index, new_vectors, new_indices=None) -> Index:

@@ -191,9 +191,8 @@ def build(index_params: IndexParams, dataset, resources=None, ids_offset: int = 
     return Index(h.value, index_params.metric)
 
 
-def search(search_params: SearchParams, index: Index, queries, k: int, neighbors=None, distances=None,
-           resources=None, probes_out: torch.Tensor | None = None):
-    """Approximate k-NN from the PQ codes of the n_probes closest lists -> ``(distances, neighbors)``."""
+def _search(search_params, index, queries, k: int, neighbors=None, distances=None, probes_out=None):
+    """search() without the output hook: torch tensors on the index's device (mivs.neighbors.streaming)."""
     if not isinstance(index, Index):
         raise TypeError("index must be an ivf_pq.Index")
     sp = search_params if search_params is not None else SearchParams()
@@ -210,7 +209,17 @@ def search(search_params: SearchParams, index: Index, queries, k: int, neighbors
     with torch.cuda.device(dev):
         _native.check(_native.lib().mivs_ivf_pq_search(index.handle, stream_ptr(dev), ptr(q), nq, k, sp.n_probes,
                                                        ptr(dist), ptr(nbrs), ptr(probes_out)))
-    return emit(dist), emit(nbrs)
+    return dist, nbrs
+
+
+def _emit2(r):
+    return emit(r[0]), emit(r[1])
+
+
+def search(search_params: SearchParams, index: Index, queries, k: int, neighbors=None, distances=None,
+           resources=None, probes_out: torch.Tensor | None = None):
+    """Approximate k-NN from the PQ codes of the n_probes closest lists -> ``(distances, neighbors)``."""
+    return _emit2(_search(search_params, index, queries, k, neighbors, distances, probes_out))
 
 
 def default_pq_dim(dim: int) -> int:

@@ -434,3 +434,11 @@ class TestSearchResultAggregator:
         mock_mgr.validate_gpu_index.side_effect = lambda g: False
         with pytest.raises(ValueError, match="GPU 99 in indices is not available"):
             a.perform_distributed_search(torch.randn(2, 8), {99: Mock()}, cfg)
+
+
+def test_streaming_rejects_unknown_index():
+    """streaming.search_host checks the index kind before touching the GPU."""
+    from mivs.neighbors import streaming
+
+    with pytest.raises(TypeError, match="ivf_flat, ivf_pq or brute_force"):
+        streaming.search_host(object(), np.zeros((2, 4), np.float32), 1)
