@@ -1752,6 +1752,19 @@ int32_t mivs_row_norms(int32_t device, void* stream, const float* d_x, int64_t n
   });
 }
 
+int32_t mivs_normalize_rows(int32_t device, void* stream, const float* d_x, int64_t n, int32_t dim, float* d_out) {
+  return guarded([&] {
+    require(dim >= 1 && n >= 0, "bad shape");
+    require(n == 0 || (d_x && d_out), "null pointer");
+    DeviceGuard dg(device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    Buf n2;
+    n2.reserve(sizeof(float) * (size_t)std::max<int64_t>(n, 1));
+    HIPCHK(launch_normalize_rows(d_x, n, dim, n2.as<float>(), d_out, s));
+    HIPCHK(hipStreamSynchronize(s));  // n2 is freed on return
+  });
+}
+
 int32_t mivs_synth_mixture(int32_t device, void* stream, float* d_out, int64_t row_begin, int64_t n, int32_t dim,
                            uint64_t seed, int32_t n_centers, float sigma, int32_t normalize) {
   return guarded([&] {

@@ -77,6 +77,27 @@ __global__ void k_row_norms(const float* __restrict__ x, int64_t n, int d, float
   out[i] = acc;
 }
 
+// cosine metric: x / sqrt(‖x‖²) per row (‖x‖² from k_row_norms: the pinned order), a zero row stays
+// zero (sklearn normalize / cosine_similarity; VectorSearch_QuestionRetrieval.ipynb:839,878). One
+// thread per 4 consecutive floats of the row-major matrix (d % 4 == 0) or per float.
+template <int V>
+__global__ void k_scale_rows(const float* __restrict__ x, const float* __restrict__ n2, int64_t n, int d,
+                             float* __restrict__ out) {
+  const int64_t nv = n * (int64_t)d / V;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nv; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = t * V;
+    const float nrm = sqrtf(n2[e / d]);
+    if constexpr (V == 4) {
+      float4 v = *reinterpret_cast<const float4*>(x + e);
+      if (nrm > 0.0f) { v.x /= nrm; v.y /= nrm; v.z /= nrm; v.w /= nrm; }
+      else v = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(out + e) = v;
+    } else {
+      out[e] = nrm > 0.0f ? x[e] / nrm : 0.0f;
+    }
+  }
+}
+
 __device__ __forceinline__ int find_list(const int64_t* __restrict__ off, int n_lists, int64_t r) {
   int lo = 0, hi = n_lists - 1;
   while (lo < hi) {
@@ -287,6 +308,18 @@ hipError_t launch_pack_groups(const float* src, int64_t /*src_rows_total*/, int 
   if (n_groups <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_pack, grid1(n_groups, 4), dim3(256), 0, s, src, d, dp, src_index, list_off, list_goff,
                      group_list, n_groups, groups, norms, ids_out, id_map, id_offset);
+  return hipGetLastError();
+}
+
+hipError_t launch_normalize_rows(const float* x, int64_t n, int d, float* n2, float* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipError_t e = launch_row_norms(x, n, d, n2, s);
+  if (e != hipSuccess) return e;
+  const bool v4 = d % 4 == 0 && (reinterpret_cast<uintptr_t>(x) % 16) == 0 && (reinterpret_cast<uintptr_t>(out) % 16) == 0;
+  const int64_t nv = n * (int64_t)d / (v4 ? 4 : 1);
+  const int grid = (int)std::min<int64_t>((nv + 255) / 256, 65536);
+  if (v4) hipLaunchKernelGGL(k_scale_rows<4>, dim3(grid), dim3(256), 0, s, x, n2, n, d, out);
+  else hipLaunchKernelGGL(k_scale_rows<1>, dim3(grid), dim3(256), 0, s, x, n2, n, d, out);
   return hipGetLastError();
 }
 

@@ -256,6 +256,8 @@ hipError_t launch_pack_groups(const float* src, int64_t src_rows_total, int d, i
                               int64_t n_groups, float* groups, float* norms, int64_t* ids_out,
                               const int64_t* id_map, int64_t id_offset, hipStream_t s);
 hipError_t launch_row_norms(const float* x, int64_t n, int d, float* out, hipStream_t s);
+// cosine: out = x / sqrt(pinned ‖x‖²) per row (zero rows stay zero); n2: [n] scratch (the squared norms)
+hipError_t launch_normalize_rows(const float* x, int64_t n, int d, float* n2, float* out, hipStream_t s);
 hipError_t launch_iota_i64(int64_t* out, int64_t n, int64_t start, int64_t step, hipStream_t s);
 hipError_t launch_fill_i32(int* out, int64_t n, int v, hipStream_t s);
 

@@ -11,7 +11,7 @@ __version__ = "0.1.0"
 
 
 def __getattr__(name):  # lazy: importing mivs must not require a GPU
-    if name in ("neighbors", "cluster", "ops", "distributed"):
+    if name in ("neighbors", "cluster", "ops", "distributed", "faiss_io"):
         import importlib
 
         return importlib.import_module(f"{__name__}.{name}")

@@ -146,6 +146,7 @@ _SIGS = {
     "mivs_merge_topk": (c_int32, [c_int32, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_int32,
                                   c_void_p, c_void_p]),
     "mivs_row_norms": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int32, c_void_p]),
+    "mivs_normalize_rows": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int32, c_void_p]),
     "mivs_synth_mixture": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int64, c_int32, c_uint64, c_int32,
                                      c_float, c_int32]),
 }

@@ -13,7 +13,7 @@ import ctypes
 
 import torch
 
-from .. import _native
+from .. import _cosine, _native
 from .._tensors import as_device_f32, emit, out_tensor, ptr, stream_ptr
 from .ivf_flat import _SQRT_METRICS, metric_code
 
@@ -66,6 +66,8 @@ class Index:
 
 def build(dataset, metric: str = "sqeuclidean", metric_arg: float = 2.0, resources=None, ids_offset: int = 0) -> Index:
     x = as_device_f32(dataset, name="dataset")
+    if _cosine.is_cosine(metric):
+        x = _cosine.normalize_rows(x)
     dev = x.device.index
     h = ctypes.c_void_p()
     with torch.cuda.device(dev):
@@ -85,6 +87,9 @@ def _search(index, queries, k: int, neighbors=None, distances=None):
     q = as_device_f32(queries, device=dev, name="queries")
     if q.shape[1] != index.dim:
         raise ValueError(f"queries have dim {q.shape[1]}, index has {index.dim}")
+    cos = _cosine.is_cosine(index.metric)
+    if cos:
+        q = _cosine.normalize_rows(q)
     nq = q.shape[0]
     dist = out_tensor(distances, (nq, k), torch.float32, dev, "distances")
     nbrs = out_tensor(neighbors, (nq, k), torch.int64, dev, "neighbors")
@@ -93,6 +98,8 @@ def _search(index, queries, k: int, neighbors=None, distances=None):
                                                             ptr(nbrs)))
     if index.metric in _SQRT_METRICS:
         dist.sqrt_()  # in place: a caller-provided `distances` holds the final values
+    if cos:
+        _cosine.to_distance_(dist)
     return dist, nbrs
 
 

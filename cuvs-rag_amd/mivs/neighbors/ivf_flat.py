@@ -19,6 +19,7 @@ import math
 import torch
 
 from .. import _native
+from .. import _cosine
 from .._tensors import as_device_f32, emit, out_tensor, ptr, stream_ptr
 
 _METRICS = {
@@ -29,6 +30,8 @@ _METRICS = {
     "L2SqrtExpanded": _native.METRIC_L2,
     "inner_product": _native.METRIC_IP,
     "InnerProduct": _native.METRIC_IP,
+    "cosine": _native.METRIC_IP,  # over normalised rows, distance 1 - ip (mivs._cosine)
+    "CosineExpanded": _native.METRIC_IP,
 }
 _SQRT_METRICS = ("euclidean", "L2SqrtExpanded")
 
@@ -182,6 +185,8 @@ def build(index_params: IndexParams, dataset, resources=None, ids_offset: int = 
     if not isinstance(index_params, IndexParams):
         raise TypeError("index_params must be an ivf_flat.IndexParams")
     x = as_device_f32(dataset, name="dataset")
+    if _cosine.is_cosine(index_params.metric):
+        x = _cosine.normalize_rows(x)
     dev = x.device.index
     n, d = x.shape
     if n < index_params.n_lists:
@@ -198,6 +203,8 @@ def build_from_centroids(centroids, dataset, metric: str = "sqeuclidean", ids_of
                          chunk_rows: int = 0, prefilter: bool = True) -> Index:
     """IVF-Flat lists from given centroids (FAISS IndexIVFFlat with a pre-trained quantizer)."""
     x = as_device_f32(dataset, name="dataset")
+    if _cosine.is_cosine(metric):
+        x = _cosine.normalize_rows(x)
     dev = x.device.index
     c = as_device_f32(centroids, device=dev, name="centroids")
     if c.shape[1] != x.shape[1]:
@@ -225,6 +232,9 @@ def _search(search_params, index, queries, k: int, neighbors=None, distances=Non
     q = as_device_f32(queries, device=dev, name="queries")
     if q.shape[1] != index.dim:
         raise ValueError(f"queries have dim {q.shape[1]}, index has {index.dim}")
+    cos = _cosine.is_cosine(index.metric)
+    if cos:
+        q = _cosine.normalize_rows(q)
     nq = q.shape[0]
     dist = out_tensor(distances, (nq, k), torch.float32, dev, "distances")
     nbrs = out_tensor(neighbors, (nq, k), torch.int64, dev, "neighbors")
@@ -233,6 +243,8 @@ def _search(search_params, index, queries, k: int, neighbors=None, distances=Non
                                                          ptr(dist), ptr(nbrs), ptr(probes_out)))
     if index.metric in _SQRT_METRICS:
         dist.sqrt_()  # in place: a caller-provided `distances` holds the final values
+    if cos:
+        _cosine.to_distance_(dist)
     return dist, nbrs
 
 
@@ -256,6 +268,8 @@ def extend(index: Index, new_vectors, new_indices=None) -> Index:
     x = as_device_f32(new_vectors, device=dev, name="new_vectors")
     if x.shape[1] != index.dim:
         raise ValueError(f"new_vectors have dim {x.shape[1]}, index has {index.dim}")
+    if _cosine.is_cosine(index.metric):
+        x = _cosine.normalize_rows(x)
     ids = None
     if new_indices is not None:
         ids = torch.as_tensor(new_indices).to(device=f"cuda:{dev}", dtype=torch.int64).contiguous().reshape(-1)

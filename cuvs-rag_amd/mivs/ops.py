@@ -23,8 +23,15 @@ def merge_topk(dist: torch.Tensor, ids: torch.Tensor, k: int, metric: str = "sqe
     oi = torch.empty((nq, k), dtype=torch.int64, device=dist.device)
     with torch.cuda.device(dev):
         _native.check(_native.lib().mivs_merge_topk(dev, stream_ptr(dev), ptr(d), ptr(i), nq, m, k_in, k,
-                                                    metric_code(metric), ptr(od), ptr(oi)))
+                                                    _merge_order(metric), ptr(od), ptr(oi)))
     return od, oi
+
+
+def _merge_order(metric: str) -> int:
+    """Cosine results are distances 1 - ip (smaller is better): merged in the L2 order."""
+    from ._cosine import is_cosine
+
+    return _native.METRIC_L2 if is_cosine(metric) else metric_code(metric)
 
 
 def row_norms(x) -> torch.Tensor:

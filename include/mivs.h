@@ -186,6 +186,11 @@ int32_t mivs_merge_topk(int32_t device, void* stream, const float* d_in_dist, co
 
 /* ---- helpers exposed for parity tests and the bench ---- */
 int32_t mivs_row_norms(int32_t device, void* stream, const float* d_x, int64_t n, int32_t dim, float* d_out);
+/* cosine metric support: d_out[i] = d_x[i] / sqrt(pinned ||x_i||^2), zero rows stay zero (may alias
+ * d_x). Replaces the normalisation inside sklearn cosine_similarity / NearestNeighbors(metric='cosine')
+ * (Attempt_1/VectorSearch_QuestionRetrieval.ipynb:839,878); ivf_flat / brute_force "cosine" build an
+ * inner-product index over normalised rows and report 1 - ip. */
+int32_t mivs_normalize_rows(int32_t device, void* stream, const float* d_x, int64_t n, int32_t dim, float* d_out);
 int32_t mivs_synth_mixture(int32_t device, void* stream, float* d_out, int64_t row_begin, int64_t n, int32_t dim,
                            uint64_t seed, int32_t n_centers, float sigma, int32_t normalize);
 

@@ -42,6 +42,16 @@ void orc_norms(const float* x, int64_t n, int d, float* out) {
   for (int64_t i = 0; i < n; ++i) out[i] = orc_dot(x + i * d, x + i * d, d);
 }
 
+/* cosine: x / sqrt(||x||^2) per row with the pinned norm, zero rows stay zero (sklearn normalize,
+ * as in cosine_similarity / NearestNeighbors(metric='cosine') at
+ * Attempt_1/VectorSearch_QuestionRetrieval.ipynb:839,878). */
+void orc_normalize_rows(const float* x, int64_t n, int d, float* out) {
+  for (int64_t i = 0; i < n; ++i) {
+    const float nrm = sqrtf(orc_dot(x + i * d, x + i * d, d));
+    for (int j = 0; j < d; ++j) out[i * d + j] = nrm > 0.0f ? x[i * d + j] / nrm : 0.0f;
+  }
+}
+
 /* L2: the expanded squared distance ‖x‖² + ‖q‖² − 2 x·q, one fused rounding
  * for the −2·dot term, clamped at 0 (FAISS/cuVS "L2Expanded" semantics,
  * reached via ivf_flat.search at improved_multi_gpu_rag.py:227).

@@ -30,6 +30,7 @@ int orc_dim_pad(int d);
 /* dot in the mivs k-order (MFMA 32x32x2 f32 chain, DESIGN.md §Arithmetic contract) */
 float orc_dot(const float* a, const float* b, int d);
 void orc_norms(const float* x, int64_t n, int d, float* out);
+void orc_normalize_rows(const float* x, int64_t n, int d, float* out);
 /* key used for ranking: L2 -> clamped expanded squared distance, IP -> -dot */
 float orc_key(float dot, float xn, float qn, int metric);
 

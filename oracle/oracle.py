@@ -36,6 +36,7 @@ def lib():
             "orc_dim_pad": (i32, [i32]),
             "orc_dot": (ctypes.c_float, [P, P, i32]),
             "orc_norms": (None, [P, i64, i32, P]),
+            "orc_normalize_rows": (None, [P, i64, i32, P]),
             "orc_knn": (None, [P, i64, P, i64, i32, i32, i32, i64, P, P]),
             "orc_merge": (None, [P, P, i64, i32, i32, i32, i32, P, P]),
             "orc_kmeans_assign": (None, [P, P, i64, P, i32, i32, i32, P]),
@@ -79,6 +80,8 @@ def _p(a):
 def metric_code(metric) -> int:
     if isinstance(metric, int):
         return metric
+    if metric in ("cosine", "CosineExpanded"):
+        raise ValueError("cosine: normalize_rows() both sides, search with inner_product, report 1 - ip")
     return IP if metric in ("inner_product", "ip", "IP") else L2
 
 
@@ -92,6 +95,22 @@ def norms(x) -> np.ndarray:
     out = np.empty(x.shape[0], np.float32)
     lib().orc_norms(_p(x), x.shape[0], x.shape[1], _p(out))
     return out
+
+
+def normalize_rows(x) -> np.ndarray:
+    """x / sqrt(pinned ||x||^2) per row; zero rows stay zero (mivs_oracle.c orc_normalize_rows)."""
+    x = _f32(x)
+    out = np.empty_like(x)
+    lib().orc_normalize_rows(_p(x), x.shape[0], x.shape[1], _p(out))
+    return out
+
+
+def cosine_knn(x, q, k, id_offset=0):
+    """Exact k-NN by cosine distance 1 - cos(q, x) (sklearn NearestNeighbors(metric='cosine',
+    algorithm='brute'), VectorSearch_QuestionRetrieval.ipynb:878): inner-product top-k of the
+    normalised rows, distance 1 - ip in fp32."""
+    d, i = knn(normalize_rows(x), normalize_rows(q), k, "inner_product", id_offset)
+    return (np.float32(1.0) - d).astype(np.float32), i
 
 
 def knn(x, q, k, metric="sqeuclidean", id_offset=0):
