@@ -1462,13 +1462,39 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
       a.k = k;
       a.out_d = ws.part_d.as<float>();
       a.out_i = ws.part_i.as<int64_t>();
+      a.flags = getenv("MIVS_PQ_FLAGS") ? atoi(getenv("MIVS_PQ_FLAGS")) : 0;
+      // list-sorted, XCD-aware slot order (MIVS_PQ_ORDER=0: slot order q * n_probes + p): the probe map
+      // with one chunk per list gives, per list, the queries probing it and their output slots
+      const char* oe = getenv("MIVS_PQ_ORDER");
+      const bool order = !(oe && oe[0] == '0');
+      if (order) {
+        const int64_t ne = nq * np;
+        ws.counts.reserve(sizeof(int) * L.n_lists);
+        ws.fill.reserve(sizeof(int) * L.n_lists);
+        ws.bucket_off.reserve(sizeof(int) * (L.n_lists + 1));
+        ws.work_off.reserve(sizeof(int) * (L.n_lists + 1));
+        ws.bucket_q.reserve(sizeof(int64_t) * ne);
+        ws.bucket_slot.reserve(sizeof(int64_t) * ne);
+        ws.qp_slots.reserve(sizeof(int64_t) * ne);
+        ws.slot_begin.reserve(sizeof(int64_t) * (nq + 1));
+        const size_t stb = scan_tmp_bytes(ne) + sizeof(int64_t) * (size_t)ne;
+        ws.scan_tmp.reserve(stb);
+        HIPCHK(launch_probe_map(ws.probes_i.as<int64_t>(), nq, np, L.n_lists, L.goff.as<int64_t>(), 1 << 28, 1,
+                                ws.counts.as<int>(), ws.fill.as<int>(), ws.bucket_off.as<int>(), ws.work_off.as<int>(),
+                                ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(), ws.qp_slots.as<int64_t>(),
+                                ws.slot_begin.as<int64_t>(), ws.scan_tmp.p, stb, s));
+        a.ent_q = ws.bucket_q.as<int64_t>();
+        a.ent_slot = ws.bucket_slot.as<int64_t>();
+        a.ent_off = ws.bucket_off.as<int>();
+        a.n_lists = L.n_lists;
+      }
       if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
       HIPCHK(launch_pq_scan(a, kcap, s));
       if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
       MergeArgs m{};
       m.in_d = ws.part_d.as<float>();
       m.in_i = ws.part_i.as<int64_t>();
-      m.slot_begin = nullptr;
+      m.slot_begin = order ? ws.slot_begin.as<int64_t>() : nullptr;
       m.slots_per_q = np;
       m.nq = nq;
       m.k_in = k;

@@ -106,6 +106,14 @@ struct PqScanArgs {
   int n_probes, d, rot_dim_pad, pq_dim, pq_dim_pad, pq_len, k;
   float* out_d;                // [n_slots][k]
   int64_t* out_i;
+  int flags;                   // timing experiments only (MIVS_PQ_FLAGS): 1 skip LUT, 2 skip scan, 4 skip merge
+  // optional list-sorted order (the probe map with one chunk per list): workgroup b serves entry e
+  // (XCD-aware: XCD b % 8 walks its contiguous eighth of the entries), query ent_q[e], output slot
+  // ent_slot[e], list = the bucket of e in ent_off. nullptr: workgroup b serves slot b = q*n_probes+p.
+  const int64_t* ent_q;
+  const int64_t* ent_slot;
+  const int* ent_off;          // [n_lists+1]
+  int n_lists;
 };
 
 // IVF-PQ tiled scan (K9b, pq.hip): work item = (list, <= 16 queries, 512-row chunk) from the probe map.

@@ -148,9 +148,29 @@ __global__ __launch_bounds__(NT) void k_pq_scan(PqScanArgs a) {
   float* wkey = mkey + 2 * NT * KCAP;                            // [NT/64][k] wave results
   int* wpos = reinterpret_cast<int*>(wkey + (NT / 64) * KCAP);
 
-  const int64_t slot = blockIdx.x;  // = q * n_probes + probe
-  const int64_t q = slot / a.n_probes;
-  const int l = (int)a.probes[slot];
+  int64_t slot, q;
+  int l;
+  if (a.ent_q) {
+    // list-sorted entries, XCD-aware: the workgroups of XCD x = b % 8 take the x-th contiguous range in
+    // order, so the ~m_l queries probing list l run together on one XCD and share its codes in L2
+    const int64_t nb = gridDim.x, b = blockIdx.x, x = b & 7;
+    int64_t e = b >> 3;
+    for (int y = 0; y < x; ++y) e += (nb - y + 7) >> 3;
+    if (e >= a.ent_off[a.n_lists]) return;
+    int lo = 0, hi = a.n_lists - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (a.ent_off[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    l = lo;
+    if (a.list_goff[l + 1] == a.list_goff[l]) return;  // an empty list owns no output slot
+    q = a.ent_q[e];
+    slot = a.ent_slot[e];
+  } else {
+    slot = blockIdx.x;  // = q * n_probes + probe
+    q = slot / a.n_probes;
+    l = (int)a.probes[slot];
+  }
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   if (l < 0) {  // no probe (degenerate query): empty slot
@@ -164,7 +184,7 @@ __global__ __launch_bounds__(NT) void k_pq_scan(PqScanArgs a) {
   for (int i = tid; i < a.rot_dim_pad; i += NT)
     s_res[i] = i < a.d ? a.queries[q * a.d + i] - a.cents[(int64_t)l * a.d + i] : 0.0f;
   __syncthreads();
-  const int nlut = a.pq_dim * kPqCodes;
+  const int nlut = a.flags & 1 ? 0 : a.pq_dim * kPqCodes;
   if ((pl & 3) == 0 && pl <= 16) {
     // 4 entries per thread in flight: their codebook rows (pl/4 float4 each) are all requested
     // before the first FMA, so the L2 latency is paid once per 4 entries, not once per entry
@@ -219,7 +239,7 @@ __global__ __launch_bounds__(NT) void k_pq_scan(PqScanArgs a) {
   int lp[KCAP];
 #pragma unroll
   for (int t = 0; t < KCAP; ++t) { lk[t] = INFINITY; lp[t] = INT_MAX; }
-  const int64_t r0 = a.list_off[l], nrows = a.list_off[l + 1] - r0;
+  const int64_t r0 = a.list_off[l], nrows = a.flags & 2 ? 0 : a.list_off[l + 1] - r0;
   const int64_t g0 = a.list_goff[l];
   const int nchunk = a.pq_dim_pad >> 4;
   auto row_codes = [&](int64_t r) {
@@ -270,17 +290,22 @@ __global__ __launch_bounds__(NT) void k_pq_scan(PqScanArgs a) {
       if (dist < lk[KCAP - 1]) pq_insert<KCAP>(lk, lp, dist, (int)r);
     }
   }
+  if (a.flags & 4) {  // timing experiment: no merge, one store keeps the scan alive
+    if (lk[0] < -1.0f) a.out_d[slot * a.k] = lk[0] + (float)lp[0];
+    return;
+  }
   __syncthreads();  // LUT dead: the merge area aliases it
+  // lane lists transposed ([rank][thread]): the stores and every head read are conflict-free
 #pragma unroll
   for (int t = 0; t < KCAP; ++t) {
-    mkey[tid * KCAP + t] = lk[t];
-    mpos[tid * KCAP + t] = lp[t];
+    mkey[t * NT + tid] = lk[t];
+    mpos[t * NT + tid] = lp[t];
   }
   __syncthreads();
   // stage 1: wave w merges lane lists w*64 .. w*64+63
   {
-    const float* myk = mkey + tid * KCAP;
-    const int* myp = mpos + tid * KCAP;
+    const float* myk = mkey + tid;
+    const int* myp = mpos + tid;
     int head = 0;
     float hk = myk[0];
     int hp = myp[0];
@@ -296,8 +321,8 @@ __global__ __launch_bounds__(NT) void k_pq_scan(PqScanArgs a) {
       if (lane == 0) { wkey[wave * KCAP + t] = bk; wpos[wave * KCAP + t] = bp; }
       if (hk == bk && hp == bp && head < KCAP) {
         ++head;
-        hk = head < KCAP ? myk[head] : INFINITY;
-        hp = head < KCAP ? myp[head] : INT_MAX;
+        hk = head < KCAP ? myk[head * NT] : INFINITY;
+        hp = head < KCAP ? myp[head * NT] : INT_MAX;
       }
     }
   }
