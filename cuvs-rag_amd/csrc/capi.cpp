@@ -1488,8 +1488,13 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
         a.ent_off = ws.bucket_off.as<int>();
         a.n_lists = L.n_lists;
       }
+      a.pq_half = (int)ceil_div(ceil_div(idx->pq_dim, 2), 16) * 16;
+      const char* spe = getenv("MIVS_PQ_SPLIT");
+      const bool split = !(spe && spe[0] == '0') && !(a.flags & 7);
       if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
-      HIPCHK(launch_pq_scan(a, kcap, s));
+      hipError_t se = split ? launch_pq_scan_split(a, kcap, s) : hipErrorNotSupported;
+      if (se == hipErrorNotSupported) se = launch_pq_scan(a, kcap, s);
+      HIPCHK(se);
       if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
       MergeArgs m{};
       m.in_d = ws.part_d.as<float>();

@@ -114,6 +114,7 @@ struct PqScanArgs {
   const int64_t* ent_slot;
   const int* ent_off;          // [n_lists+1]
   int n_lists;
+  int pq_half;                 // K9s: subspaces per LUT half (a multiple of 16, 2 * pq_half >= pq_dim)
 };
 
 // IVF-PQ tiled scan (K9b, pq.hip): work item = (list, <= 16 queries, 512-row chunk) from the probe map.
@@ -309,6 +310,8 @@ hipError_t launch_pq_ids(const int64_t* perm, int64_t n, const int64_t* list_off
 hipError_t launch_pq_unpack(const uint8_t* codes, int64_t n, const int64_t* list_off, const int64_t* list_goff,
                             int n_lists, int pq_dim, int pq_dim_pad, uint8_t* out, hipStream_t s);
 hipError_t launch_pq_scan(const PqScanArgs& a, int kcap, hipStream_t s);
+// K9s (split LUT, three workgroups per CU); hipErrorNotSupported when its shape limits are not met
+hipError_t launch_pq_scan_split(const PqScanArgs& a, int kcap, hipStream_t s);
 size_t pq_tile_lds_bytes(int rot_dim_pad, int pq_len);
 hipError_t launch_pq_scan_tiled(const PqTileArgs& a, int kcap, int grid, hipStream_t s);
 

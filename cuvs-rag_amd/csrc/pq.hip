@@ -359,6 +359,221 @@ __global__ __launch_bounds__(NT) void k_pq_scan(PqScanArgs a) {
   }
 }
 
+// LUT entries e < nlut (subspace e >> 8, code e & 255) of a pq_len = 4 * PL4 codebook slice: each
+// thread keeps V = 8 / PL4 entries' codebook rows (32 floats) in flight before the first FMA; the
+// fmaf chain of K9 / the oracle
+template <int PL4, int NT>
+__device__ __forceinline__ void pq_lut_build(const float* __restrict__ books, const float* res, int nlut, int tid,
+                                             float* lut) {
+  constexpr int pl = 4 * PL4, V = PL4 >= 4 ? 2 : 8 / PL4;
+  for (int base = tid; base < nlut; base += V * NT) {
+    float4 bv[V][PL4];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const int e = base + v * NT < nlut ? base + v * NT : base;
+#pragma unroll
+      for (int c4 = 0; c4 < PL4; ++c4) bv[v][c4] = *reinterpret_cast<const float4*>(books + (int64_t)e * pl + 4 * c4);
+    }
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const int e = base + v * NT;
+      if (e >= nlut) break;
+      const float* r = res + (e >> 8) * pl;
+      float acc = 0.0f;
+#pragma unroll
+      for (int c4 = 0; c4 < PL4; ++c4) {
+        const float t0 = r[4 * c4 + 0] - bv[v][c4].x;
+        acc = fmaf(t0, t0, acc);
+        const float t1 = r[4 * c4 + 1] - bv[v][c4].y;
+        acc = fmaf(t1, t1, acc);
+        const float t2 = r[4 * c4 + 2] - bv[v][c4].z;
+        acc = fmaf(t2, t2, acc);
+        const float t3 = r[4 * c4 + 3] - bv[v][c4].w;
+        acc = fmaf(t3, t3, acc);
+      }
+      lut[e] = acc;
+    }
+  }
+}
+
+// K9s: K9 with the LUT built and consumed in two halves of the subspaces (j < ph, then j >= ph), so a
+// workgroup (4 waves) needs ph x 256 x 4 B of LDS (48 KiB at pq_dim 96) instead of the whole LUT and
+// three workgroups share a CU: one's LUT build, barrier waits and merge overlap the others' scans. Each
+// thread keeps the partial sums of its rows (<= 16 per 4096-row block) in registers across the two
+// halves, so every row's sum still runs j = 0, 1, ..., pq_dim-1 from 0 (the oracle's order); a list
+// longer than 4096 rows is scanned block by block (the LUT halves rebuilt per block). The lane lists
+// merge in registers (per wave, k rounds of a 64-lane min), then wave 0 merges the 4 wave lists.
+template <int KCAP>
+__global__ __launch_bounds__(256) void k_pq_scan_split(PqScanArgs a) {
+  constexpr int NT = 256, NW = NT / 64, RM = 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int ph = a.pq_half;
+  float* s_res = reinterpret_cast<float*>(smem);  // [rot_dim_pad]
+  float* lut = s_res + a.rot_dim_pad;             // [ph][256]
+  float* wkey = lut + ph * kPqCodes;              // [NW][KCAP]
+  int* wpos = reinterpret_cast<int*>(wkey + NW * KCAP);
+
+  int64_t slot, q;
+  int l;
+  if (a.ent_q) {
+    const int64_t nb = gridDim.x, b = blockIdx.x, x = b & 7;
+    int64_t e = b >> 3;
+    for (int y = 0; y < x; ++y) e += (nb - y + 7) >> 3;
+    if (e >= a.ent_off[a.n_lists]) return;
+    int lo = 0, hi = a.n_lists - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (a.ent_off[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    l = lo;
+    if (a.list_goff[l + 1] == a.list_goff[l]) return;  // an empty list owns no output slot
+    q = a.ent_q[e];
+    slot = a.ent_slot[e];
+  } else {
+    slot = blockIdx.x;
+    q = slot / a.n_probes;
+    l = (int)a.probes[slot];
+  }
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  if (l < 0) {
+    for (int t = tid; t < a.k; t += NT) {
+      a.out_d[slot * a.k + t] = INFINITY;
+      a.out_i[slot * a.k + t] = -1;
+    }
+    return;
+  }
+  const int pl = a.pq_len;
+  for (int i = tid; i < a.rot_dim_pad; i += NT)
+    s_res[i] = i < a.d ? a.queries[q * a.d + i] - a.cents[(int64_t)l * a.d + i] : 0.0f;
+
+  float lk[KCAP];
+  int lp[KCAP];
+#pragma unroll
+  for (int t = 0; t < KCAP; ++t) { lk[t] = INFINITY; lp[t] = INT_MAX; }
+  const int64_t nrows = a.list_off[l + 1] - a.list_off[l];
+  const int64_t g0 = a.list_goff[l];
+  auto row_codes = [&](int64_t r) {
+    return a.codes + (g0 + r / kGroupRows) * (int64_t)kGroupRows * a.pq_dim_pad + (r % kGroupRows) * 16;
+  };
+  for (int64_t rb = 0; rb < nrows; rb += (int64_t)NT * RM) {
+    float ps[RM];
+#pragma unroll
+    for (int i = 0; i < RM; ++i) ps[i] = 0.0f;
+    for (int h = 0; h < 2; ++h) {
+      const int j0 = h * ph, j1 = j0 + ph < a.pq_dim ? j0 + ph : a.pq_dim;
+      if (j0 >= j1) break;
+      __syncthreads();  // s_res is written / the previous half's scan is done with the LUT
+      // LUT[j - j0][c] = ||res_j - B_j[c]||^2 for j in [j0, j1): the K9 fmaf chain, entries 4 at a time
+      const int nlut = (j1 - j0) * kPqCodes;
+      const float* books = a.books + (int64_t)j0 * kPqCodes * pl;
+      const float* res = s_res + j0 * pl;
+      switch (pl >> 2) {
+        case 1: pq_lut_build<1, NT>(books, res, nlut, tid, lut); break;
+        case 2: pq_lut_build<2, NT>(books, res, nlut, tid, lut); break;
+        case 3: pq_lut_build<3, NT>(books, res, nlut, tid, lut); break;
+        default: pq_lut_build<4, NT>(books, res, nlut, tid, lut); break;
+      }
+      __syncthreads();
+      // this half's code chunks of each of my rows (<= 4 x 16 codes), the next row's requested first
+      const int c0 = j0 >> 4, nch = ((j1 + 15) >> 4) - c0;
+      uint4 cur[4], nxt[4];
+      auto load_row = [&](int64_t r, uint4 (&w)[4]) {
+        const uint8_t* cg = row_codes(r < nrows ? r : 0);
+#pragma unroll
+        for (int ch = 0; ch < 4; ++ch)
+          if (ch < nch) w[ch] = *reinterpret_cast<const uint4*>(cg + (int64_t)(c0 + ch) * (kGroupRows * 16));
+      };
+      load_row(rb + tid, cur);
+      // one row per iteration (not unrolled: the register budget is three workgroups per CU); the
+      // partial sums rotate through ps so that ps[0] is always the current row's
+#pragma unroll 1
+      for (int i = 0; i < RM; ++i) {
+        const int64_t r = rb + tid + (int64_t)i * NT;
+        const bool more = i + 1 < RM && r + NT < nrows;
+        if (more) load_row(r + NT, nxt);
+        float dist = ps[0];
+        if (r < nrows) {
+#pragma unroll
+          for (int ch = 0; ch < 4; ++ch) {
+            if (ch < nch) {
+              const uint32_t wv[4] = {cur[ch].x, cur[ch].y, cur[ch].z, cur[ch].w};
+              const float* lj = lut + (ch << 12);  // subspace (c0 + ch) * 16 - j0 = ch * 16
+              const int jn = j1 - j0 - ch * 16;    // valid subspaces of this chunk (16 unless the last)
+#pragma unroll
+              for (int b = 0; b < 16; ++b)
+                if (b < jn) dist = dist + lj[(b << 8) + ((wv[b >> 2] >> (8 * (b & 3))) & 0xFF)];
+              __builtin_amdgcn_sched_barrier(0);  // one chunk's 16 lookups in flight: bounds the VGPRs
+            }
+          }
+        }
+#pragma unroll
+        for (int t = 0; t + 1 < RM; ++t) ps[t] = ps[t + 1];
+        ps[RM - 1] = dist;
+        if (more) {
+#pragma unroll
+          for (int ch = 0; ch < 4; ++ch) cur[ch] = nxt[ch];
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      const int64_t r = rb + tid + (int64_t)i * NT;
+      if (r < nrows && ps[i] < lk[KCAP - 1]) pq_insert<KCAP>(lk, lp, ps[i], (int)r);
+    }
+  }
+  // stage 1 (registers): per wave, k rounds of the 64-lane (dist, row) minimum; the winner lane drops
+  // its head by shifting its sorted list down (rows are unique, so one lane wins; exhausted lanes
+  // hold (+inf, INT_MAX) and shifting those changes nothing)
+  for (int t = 0; t < a.k; ++t) {
+    float bk = lk[0];
+    int bp = lp[0];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const float ok = __shfl_xor(bk, off);
+      const int op = __shfl_xor(bp, off);
+      if (ok < bk || (ok == bk && op < bp)) { bk = ok; bp = op; }
+    }
+    if (lane == 0) { wkey[wave * KCAP + t] = bk; wpos[wave * KCAP + t] = bp; }
+    if (lk[0] == bk && lp[0] == bp) {
+#pragma unroll
+      for (int i = 0; i + 1 < KCAP; ++i) { lk[i] = lk[i + 1]; lp[i] = lp[i + 1]; }
+      lk[KCAP - 1] = INFINITY;
+      lp[KCAP - 1] = INT_MAX;
+    }
+  }
+  __syncthreads();
+  // stage 2: wave 0, lanes 0..NW-1 hold the wave lists
+  if (wave == 0) {
+    const bool src = lane < NW;
+    const float* myk = wkey + (src ? lane : 0) * KCAP;
+    const int* myp = wpos + (src ? lane : 0) * KCAP;
+    int head = 0;
+    float hk = src ? myk[0] : INFINITY;
+    int hp = src ? myp[0] : INT_MAX;
+    for (int t = 0; t < a.k; ++t) {
+      float bk = hk;
+      int bp = hp;
+#pragma unroll
+      for (int off = NW / 2; off >= 1; off >>= 1) {
+        const float ok = __shfl_xor(bk, off, NW);
+        const int op = __shfl_xor(bp, off, NW);
+        if (ok < bk || (ok == bk && op < bp)) { bk = ok; bp = op; }
+      }
+      if (lane == 0) {
+        const bool valid = bp != INT_MAX;
+        a.out_d[slot * a.k + t] = valid ? bk : INFINITY;
+        a.out_i[slot * a.k + t] = valid ? a.row_ids[g0 * kGroupRows + bp] : (int64_t)-1;
+      }
+      if (src && hk == bk && hp == bp && head < a.k) {
+        ++head;
+        hk = head < a.k ? myk[head] : INFINITY;
+        hp = head < a.k ? myp[head] : INT_MAX;
+      }
+    }
+  }
+}
+
 // K9b: work item = (list l, tile of <= 16 queries probing l, chunk of 16 groups = 512 rows), dequeued
 // like K3 from the IVF probe map. Subspace-outer loop: per subspace j the codebook B_j (256 x pl)
 // and the tile's 16 LUT rows LUT_j[q][c] = ||(q - c_l)_j - B_j[c]||^2 are built in LDS once and
@@ -612,6 +827,41 @@ template <int KCAP>
 static hipError_t launch_pq_scan_k(const PqScanArgs& a, size_t lds, hipStream_t s) {
   if (pq_scan_threads(a.rot_dim_pad, a.pq_dim, KCAP) == 1024) return launch_pq_scan_kn<KCAP, 1024>(a, lds, s);
   return launch_pq_scan_kn<KCAP, 512>(a, lds, s);
+}
+
+size_t pq_split_lds_bytes(int rot_dim_pad, int pq_half, int kcap) {
+  return (size_t)rot_dim_pad * 4 + (size_t)pq_half * kPqCodes * 4 + (size_t)4 * kcap * 8;
+}
+
+template <int KCAP>
+static hipError_t launch_pq_split_k(const PqScanArgs& a, size_t lds, hipStream_t s) {
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pq_scan_split<KCAP>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL((k_pq_scan_split<KCAP>), dim3((unsigned)a.n_slots), dim3(256), lds, s, a);
+  return hipGetLastError();
+}
+
+// K9s when it applies (pq_len <= 16 and a multiple of 4, each half <= 64 subspaces): returns
+// hipErrorNotSupported otherwise, for the caller to use K9
+hipError_t launch_pq_scan_split(const PqScanArgs& a, int kcap, hipStream_t s) {
+  if (a.n_slots <= 0) return hipSuccess;
+  if (a.n_slots > 0x7FFFFFFF) return hipErrorInvalidValue;
+  if ((a.pq_len & 3) != 0 || a.pq_len > 16 || a.pq_half <= 0 || a.pq_half > 64 || (a.pq_half & 15) != 0 ||
+      2 * a.pq_half < a.pq_dim)
+    return hipErrorNotSupported;
+  const size_t lds = pq_split_lds_bytes(a.rot_dim_pad, a.pq_half, kcap);
+  if (lds > 160 * 1024) return hipErrorNotSupported;
+  switch (kcap) {
+    case 1: return launch_pq_split_k<1>(a, lds, s);
+    case 4: return launch_pq_split_k<4>(a, lds, s);
+    case 8: return launch_pq_split_k<8>(a, lds, s);
+    case 12: return launch_pq_split_k<12>(a, lds, s);
+    case 16: return launch_pq_split_k<16>(a, lds, s);
+    case 32: return launch_pq_split_k<32>(a, lds, s);
+    case 64: return launch_pq_split_k<64>(a, lds, s);
+    default: return hipErrorNotSupported;
+  }
 }
 
 hipError_t launch_pq_scan(const PqScanArgs& a, int kcap, hipStream_t s) {

@@ -398,6 +398,7 @@ PQ_CASES = [
     (4000, 100, 8, 20, 3, 17, 8, 5),      # pq_len 5, rot_dim 100: no padding dims
     (5000, 96, 12, 40, 2, 29, 5, 32),     # pq_len 3, rot_dim 120 > d: zero-padded dims
     (12000, 768, 32, 96, 2, 20, 6, 10),   # the reference's pq_dim = 96 at d = 768
+    (9000, 32, 2, 8, 3, 15, 2, 10),       # lists > 4096 rows (K9s row blocks), one LUT half only
 ]
 
 
