@@ -155,7 +155,7 @@ constexpr int kPfLaneK = 8;      // per-lane approximate list length in K10
 constexpr int kPfSlotKMax = 32;  // approximate candidates kept per slot: 16 for k <= 10, else 32
 constexpr int kPfMaxK = 16;      // largest k served by the pre-filter path
 constexpr int kPfCap = 64;       // refine capacity (window candidates per query)
-constexpr int kPfChunkGroups = 256;  // default groups (8192 rows) per K10 work item (MIVS_PF_CHUNK_ROWS)
+constexpr int kPfChunkGroups = 512;  // default groups (16384 rows) per K10 work item (MIVS_PF_CHUNK_ROWS)
 
 struct PfScanArgs {
   const uint16_t* groups_h;   // fp16 lists, group layout [g][dp/8][32][8]
@@ -217,6 +217,9 @@ struct PfRefineArgs {
 
 hipError_t launch_pf_scan(const PfScanArgs& a, int grid, size_t lds, hipStream_t s);
 size_t pf_scan_lds_bytes(int dp, int chunk_groups);
+bool pf_pair_mode();  // K10 two groups per pass (default; MIVS_PF_PAIR=0: one), which also frees the chunk
+                      // size from LDS (the row norms are loaded per pass)
+constexpr int kPfMaxPairGroups = 1 << 15;  // K10 chunk cap in pair mode (1M rows; positions stay int)
 // K12: register-resident 128-query tiles, LDS-DMA row ring (dp/16 in {4,8,12,16,24,32,48})
 constexpr int kPrQTile = 128;
 constexpr int kPrSlotK = 16;  // K12 slot: the query's 4 lane lists of 4 approximate candidates

@@ -218,8 +218,10 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
   float* s_dl = reinterpret_cast<float*>(smem + kPfSmall);    // [64] per-query window delta
   float* s_th = s_dl + kPfQTile;                                // [64] theta at item start
   float* s_l8 = s_th + kPfQTile;                                // [64][16] lane lists' last entries
-  float* s_norm = s_l8 + kPfQTile * 16;                         // [chunk_groups * 32]
-  char* s_b = reinterpret_cast<char*>(s_norm + a.chunk_groups * kGroupRows);
+  // R = 1: the chunk's row norms [chunk_groups * 32]; R = 2: per wave the norms of its current pass's two
+  // groups [8 waves][2][32] (loaded one pass ahead), so the chunk size is not bound by LDS
+  float* s_norm = s_l8 + kPfQTile * 16;
+  char* s_b = reinterpret_cast<char*>(s_norm + (R == 2 ? kPfWaves * 64 : a.chunk_groups * kGroupRows));
   float* mkey = reinterpret_cast<float*>(s_b);
   int* mpos = reinterpret_cast<int*>(mkey + kPfQTile * 16 * kPfLaneK);
 
@@ -298,7 +300,8 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
       }
     }
     for (int i = tid; i < kPfQTile * 16; i += kPfThreads) s_l8[i] = INFINITY;
-    for (int i = tid; i < ng * kGroupRows; i += kPfThreads) s_norm[i] = a.row_norms[g_begin * kGroupRows + i];
+    if constexpr (R == 1)
+      for (int i = tid; i < ng * kGroupRows; i += kPfThreads) s_norm[i] = a.row_norms[g_begin * kGroupRows + i];
     int* const cpos = a.chunk_pos ? a.chunk_pos + (int64_t)l * a.chunk_stride + chunk : nullptr;
     if (tid == 0) s_misc[2] = cpos ? __hip_atomic_load(cpos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
     __syncthreads();
@@ -343,10 +346,10 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
     const char* s_bl = s_b + lane * 16;  // this lane's B operand at k-step s: + s * 1024 (+ nb * 512: group 1)
     const int npw = wave < ng ? (ng - wave + kPfWaves - 1) / kPfWaves : 0;  // groups (passes) of this wave
     // the epilogue of one finished group (its 32 x 64 dots) + the theta refresh
-    auto epilogue = [&](const f32x16& c0, const f32x16& c1, int lg) {
+    auto epilogue = [&](const f32x16& c0, const f32x16& c1, int lg, const float* gnorm) {
       if (a.flags & 1) return;
       if (a.prof) ++pr_epi;
-      const bool slow = pf_epilogue<METRIC>(c0, c1, s_norm + lg * kGroupRows, (g_begin + lg) * kGroupRows, h, qn0,
+      const bool slow = pf_epilogue<METRIC>(c0, c1, gnorm, (g_begin + lg) * kGroupRows, h, qn0,
                                             qs0, th0, uf0, qn1, qs1, th1, uf1, lk0, lp0, lk1, lp1);
       if (a.prof && slow) ++pr_slow;
       // no insertion anywhere in this wave: its lists, and so its published ends, did not change (the
@@ -381,6 +384,15 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
         };
         const uint16_t* na = pair_ptr(0, 0);
         const uint16_t* nbp = pair_ptr(0, 1);
+        // row norms of a pair: lane L holds row L & 31 of its group 2 * pair + (L >> 5) (an odd last pair
+        // repeats its first group, as the rows do); written to this wave's LDS slot at the pair's end
+        float* const wn = s_norm + wave * 64;
+        auto pair_norm = [&](int pr) {
+          int gi = 2 * phys(pr) + (lane >> 5);
+          gi = gi < npw ? gi : npw - 1;
+          return a.row_norms[(g_begin + wave + (int64_t)gi * kPfWaves) * kGroupRows + (lane & 31)];
+        };
+        float nrm = pair_norm(0);
         h8 ra[D], rb[D];
 #pragma unroll
         for (int u = 0; u < D; ++u) {
@@ -420,8 +432,10 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
             const int pp = phys(p);
             if (cpos && wave == 0 && lane == 0)
               __hip_atomic_store(cpos, pp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            epilogue(a0, a1, 2 * pp * kPfWaves + wave);
-            if (2 * pp + 1 < npw) epilogue(b0, b1, (2 * pp + 1) * kPfWaves + wave);
+            wn[lane] = nrm;  // this pair's norms (read back by this wave only: LDS keeps its order)
+            if (p + 1 < npair) nrm = pair_norm(p + 1);
+            epilogue(a0, a1, 2 * pp * kPfWaves + wave, wn);
+            if (2 * pp + 1 < npw) epilogue(b0, b1, (2 * pp + 1) * kPfWaves + wave, wn + kGroupRows);
             a0 = zero; a1 = zero; b0 = zero; b1 = zero;
             s = 0;
             ++p;
@@ -474,7 +488,7 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
         ls += D;
         if (ls == nk) { ls = 0; if (++lpass < npw) nptr += pstride; }
         s += D;
-        if (s == nk) epilogue(c0, c1, p * kPfWaves + wave);
+        if (s == nk) epilogue(c0, c1, p * kPfWaves + wave, s_norm + (p * kPfWaves + wave) * kGroupRows);
         if (s == nk) {
           c0 = zero;
           c1 = zero;
@@ -1297,10 +1311,15 @@ int pf_hx_exp(float abs_max) {
   return e < -60 ? -60 : (e > 60 ? 60 : e);
 }
 
+bool pf_pair_mode() {
+  const char* pe = getenv("MIVS_PF_PAIR");
+  return !(pe && pe[0] == '0');
+}
+
 size_t pf_scan_lds_bytes(int dp, int chunk_groups) {
   const size_t b = (size_t)dp * kPfQTile * 2;
-  return kPfSmall + (size_t)kPfQTile * 18 * 4 + (size_t)chunk_groups * kGroupRows * 4 +
-         (b > (size_t)kPfMergeBytes ? b : (size_t)kPfMergeBytes);
+  const size_t norms = pf_pair_mode() ? (size_t)kPfWaves * 64 * 4 : (size_t)chunk_groups * kGroupRows * 4;
+  return kPfSmall + (size_t)kPfQTile * 18 * 4 + norms + (b > (size_t)kPfMergeBytes ? b : (size_t)kPfMergeBytes);
 }
 
 template <int METRIC, int D, int R>
@@ -1317,9 +1336,7 @@ static hipError_t launch_pf_scan_m(const PfScanArgs& a, int grid, size_t lds, hi
   // default: two groups per pass with 6-deep rings (half the LDS operand traffic per flop: the kernel is
   // power-bound); MIVS_PF_PAIR=0: one group per pass with MIVS_PF_DEPTH (16) k-steps in flight
   const int nk = a.dp / 16;
-  const char* pe = getenv("MIVS_PF_PAIR");
-  const bool pair = !(pe && pe[0] == '0');
-  if (pair) return nk % 6 == 0 ? launch_pf_scan_md<METRIC, 6, 2>(a, grid, lds, s)
+  if (pf_pair_mode()) return nk % 6 == 0 ? launch_pf_scan_md<METRIC, 6, 2>(a, grid, lds, s)
                                : launch_pf_scan_md<METRIC, 4, 2>(a, grid, lds, s);
   const int dsel = getenv("MIVS_PF_DEPTH") ? atoi(getenv("MIVS_PF_DEPTH")) : 16;
   if (dsel >= 16 && nk % 16 == 0) return launch_pf_scan_md<METRIC, 16, 1>(a, grid, lds, s);
