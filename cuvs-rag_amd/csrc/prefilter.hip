@@ -807,6 +807,47 @@ __global__ __launch_bounds__(256) void k_queries_to_half(const float* __restrict
   }
 }
 
+// k_queries_to_half for d % 4 == 0: the wave's row loaded once as NV float4 per lane (dp <= 256 NV),
+// all loads in flight together, max and conversion from registers, 8-byte stores
+template <int NV>
+__global__ __launch_bounds__(256) void k_queries_to_half_v(const float* __restrict__ q, int64_t nq, int d, int dp,
+                                                           int hx_exp, uint16_t* __restrict__ qh,
+                                                           float* __restrict__ qscale, float* __restrict__ qres) {
+  const int lane = threadIdx.x & 63;
+  const int64_t qi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (qi >= nq) return;
+  const float4* row = reinterpret_cast<const float4*>(q + qi * d);
+  float4 v[NV];
+  float m = 0.0f;
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    const int c4 = lane + 64 * u;
+    v[u] = 4 * c4 < d ? row[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+  const int e = pf_exp_for(m);
+  const float sc = ldexpf(1.0f, e), isc = ldexpf(1.0f, -e);
+  float res = 0.0f;
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    const int c4 = lane + 64 * u;
+    if (4 * c4 < dp) {
+      uint2 pk;
+      pk.x = pf_to_half(v[u].x, sc, isc, res) | ((unsigned)pf_to_half(v[u].y, sc, isc, res) << 16);
+      pk.y = pf_to_half(v[u].z, sc, isc, res) | ((unsigned)pf_to_half(v[u].w, sc, isc, res) << 16);
+      *reinterpret_cast<uint2*>(qh + qi * dp + 4 * c4) = pk;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) res += __shfl_xor(res, off);
+  if (lane == 0) {
+    qscale[qi] = ldexpf(1.0f, -(hx_exp + e));
+    qres[qi] = sqrtf(res) * (1.0f + 0x1p-12f);
+  }
+}
+
 __global__ void k_scatter_results(const float* __restrict__ in_d, const int64_t* __restrict__ in_i,
                                   const int64_t* __restrict__ rows, int64_t n, int k, float* __restrict__ out_d,
                                   int64_t* __restrict__ out_i) {
@@ -1426,7 +1467,13 @@ hipError_t launch_norm_max(const float* x, int64_t n, unsigned* out, hipStream_t
 hipError_t launch_queries_to_half(const float* q, int64_t nq, int d, int dp, int hx_exp, uint16_t* qh, float* qscale,
                                   float* qres, hipStream_t s) {
   if (nq <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_queries_to_half, pf_grid(nq, 4), dim3(256), 0, s, q, nq, d, dp, hx_exp, qh, qscale, qres);
+  const bool vec = (d & 3) == 0 && (reinterpret_cast<uintptr_t>(q) & 15) == 0 && dp <= 1024;
+  const int nv = (dp + 255) / 256;
+  if (vec && nv == 1) hipLaunchKernelGGL(k_queries_to_half_v<1>, pf_grid(nq, 4), dim3(256), 0, s, q, nq, d, dp, hx_exp, qh, qscale, qres);
+  else if (vec && nv == 2) hipLaunchKernelGGL(k_queries_to_half_v<2>, pf_grid(nq, 4), dim3(256), 0, s, q, nq, d, dp, hx_exp, qh, qscale, qres);
+  else if (vec && nv == 3) hipLaunchKernelGGL(k_queries_to_half_v<3>, pf_grid(nq, 4), dim3(256), 0, s, q, nq, d, dp, hx_exp, qh, qscale, qres);
+  else if (vec && nv == 4) hipLaunchKernelGGL(k_queries_to_half_v<4>, pf_grid(nq, 4), dim3(256), 0, s, q, nq, d, dp, hx_exp, qh, qscale, qres);
+  else hipLaunchKernelGGL(k_queries_to_half, pf_grid(nq, 4), dim3(256), 0, s, q, nq, d, dp, hx_exp, qh, qscale, qres);
   return hipGetLastError();
 }
 
