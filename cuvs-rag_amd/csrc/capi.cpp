@@ -732,6 +732,8 @@ bool pr_use(const mivs_index_s* idx) {
 
 void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                       int64_t* out_i, int32_t* out_probes, bool allow_pf = true, bool prof = true);
+void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
+                       int64_t* out_i, bool pf, ProfRec* pr, bool prof);
 
 // K10 scan + K11 refine for a probe map built with (kPfChunkGroups, kPfQTile); queries the refine
 // could not prove are re-run through the exact scan and scattered back.
@@ -857,8 +859,15 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
     ws.ovf_d.reserve(sizeof(float) * (size_t)novf * k);
     ws.ovf_i.reserve(sizeof(int64_t) * (size_t)novf * k);
     HIPCHK(launch_gather_rows(q, idx->d, ws.ovf_q.as<int64_t>(), novf, ws.ovf_rows.as<float>(), s));
-    ivf_search_batch(idx, s, ws.ovf_rows.as<float>(), novf, k, np, ws.ovf_d.as<float>(), ws.ovf_i.as<int64_t>(),
-                     nullptr, false, false);
+    if (idx->kind == 1) {  // brute force: the exact scan of the one list
+      ws.qn.reserve(sizeof(float) * novf);
+      HIPCHK(launch_row_norms(ws.ovf_rows.as<float>(), novf, idx->d, ws.qn.as<float>(), s));
+      single_list_topk(idx->lists, idx->G, ws.ovf_rows.as<float>(), ws.qn.as<float>(), nullptr, novf, idx->d, idx->dp,
+                       k, idx->metric, ws.ovf_d.as<float>(), ws.ovf_i.as<int64_t>(), idx->device, ws, s);
+    } else {
+      ivf_search_batch(idx, s, ws.ovf_rows.as<float>(), novf, k, np, ws.ovf_d.as<float>(), ws.ovf_i.as<int64_t>(),
+                       nullptr, false, false);
+    }
     HIPCHK(launch_scatter_results(ws.ovf_d.as<float>(), ws.ovf_i.as<int64_t>(), ws.ovf_q.as<int64_t>(), novf, k,
                                   out_d, out_i, s));
   }
@@ -877,6 +886,14 @@ void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t 
   single_list_topk(idx->cents, idx->G, q, ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, np, idx->metric,
                    ws.probes_d.as<float>(), ws.probes_i.as<int64_t>(), idx->device, ws, s);
   if (out_probes) HIPCHK(launch_i64_to_i32(ws.probes_i.as<int64_t>(), nq * np, out_probes, s));
+  ivf_search_probed(idx, s, q, nq, k, np, out_d, out_i, pf, pr, prof);
+}
+
+// the fine part of a search whose probes are in ws.probes_i ([nq][np]) and query norms in ws.qn:
+// probe map, then the pre-filter scan + refine (pf) or the exact scan + merge / select
+void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
+                       int64_t* out_i, bool pf, ProfRec* pr, bool prof) {
+  Workspace& ws = idx->ws;
   // probe map
   const ListSet& L = idx->lists;
   const int64_t ne = nq * np;
@@ -1562,6 +1579,7 @@ int32_t mivs_brute_force_build(int32_t device, void* stream, const float* d_data
     idx->metric = metric;
     idx->id_offset = id_offset;
     make_single_list(idx->lists, d_data, n, dim, idx->dp, id_offset, idx->G, s);
+    if (pf_default_on()) pf_enable(idx.get(), s);  // k <= 16 searches go through the fp16 pre-filter
     *out = idx.release();
   });
 }
@@ -1580,6 +1598,18 @@ int32_t mivs_brute_force_search(mivs_index_t idx, void* stream, const float* d_q
     ProfRec* pr = g_profiling.load() ? idx->prof.begin(s) : nullptr;
     idx->ws.qn.reserve(sizeof(float) * nq);
     HIPCHK(launch_row_norms(d_q, nq, idx->d, idx->ws.qn.as<float>(), s));
+    if (idx->groups_h.p != nullptr && k <= kPfMaxK) {
+      // the fp16 pre-filter + exact refine, as an IVF search in which every query probes the one list
+      idx->ws.probes_i.reserve(sizeof(int64_t) * nq);
+      HIPCHK(hipMemsetAsync(idx->ws.probes_i.p, 0, sizeof(int64_t) * nq, s));
+      idx->last_ovf = 0;
+      idx->last_window = 0;
+      ivf_search_probed(idx, s, d_q, nq, k, 1, d_dist, d_ids, true, pr, true);
+      idx->last_nq = nq;
+      idx->last_np = 1;
+      idx->last_k = k;
+      return;
+    }
     if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
     single_list_topk(idx->lists, idx->G, d_q, idx->ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, k, idx->metric,
                      d_dist, d_ids, idx->device, idx->ws, s);

@@ -656,7 +656,7 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
   for (int64_t c = sb * a.slot_k; c < c1; c += 64) {
     const int64_t cc = c + lane;
     const float ck = cc < c1 ? a.slot_key[cc] : INFINITY;
-    const bool take = ck <= T;
+    const bool take = ck <= T && ck < INFINITY;  // +inf: an empty slot entry (fewer than k candidates: T = +inf)
     const uint64_t msk = __ballot(take);
     if (take) {
       const int at = cnt + __popcll(msk & ((1ull << lane) - 1));

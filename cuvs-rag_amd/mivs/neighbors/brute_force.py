@@ -38,6 +38,19 @@ class Index:
     def __len__(self):
         return self.size
 
+    @property
+    def prefilter(self) -> bool:
+        """True when the fp16 copy of the rows is kept: k <= 16 searches then run the fp16 pre-filter
+        scan + exact fp32 refine instead of the fp32 scan; results are identical."""
+        v = ctypes.c_int32()
+        _native.check(_native.lib().mivs_index_get_prefilter(self.handle, ctypes.byref(v)))
+        return bool(v.value)
+
+    def set_prefilter(self, enable: bool) -> None:
+        """Build (True) or free (False) the fp16 copy of the rows."""
+        _native.check(_native.lib().mivs_index_set_prefilter(self.handle, stream_ptr(self.device),
+                                                             1 if enable else 0))
+
     def last_search_stats(self) -> dict:
         st = _native.SearchStats()
         _native.check(_native.lib().mivs_index_last_search_stats(self.handle, ctypes.byref(st)))

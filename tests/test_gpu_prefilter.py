@@ -49,6 +49,8 @@ PF_CASES = [
     # n, d, nq, n_lists, n_probes, k, metric
     (8000, 64, 70, 32, 4, 10, "sqeuclidean"),
     (6000, 100, 65, 16, 5, 1, "sqeuclidean"),      # d % 64 != 0: zero-padded dims
+    (40, 64, 9, 8, 2, 16, "sqeuclidean"),          # fewer probed rows than k: padded (-1, +inf)
+    (40, 64, 9, 8, 2, 16, "inner_product"),
     (12000, 768, 130, 24, 6, 10, "sqeuclidean"),   # the benchmark's d
     (9000, 384, 33, 20, 8, 16, "sqeuclidean"),     # k = kPfMaxK
     (7000, 128, 90, 24, 6, 10, "inner_product"),
@@ -62,7 +64,8 @@ def test_prefilter_bitexact_vs_oracle(mivs_lib, n, d, nq, n_lists, n_probes, k, 
     x = _data(n, d, seed=n + d, normalize=True)
     q = _data(nq, d, seed=n + d + 1, normalize=True)
     _, st = _check_vs_oracle(x, q, n_lists, n_probes, k, metric)
-    assert st["window_candidates"] >= k * nq - st["overflow_queries"] * k
+    if n >= 1000:  # (the tiny cases probe fewer than k rows: their windows hold all of them)
+        assert st["window_candidates"] >= k * nq - st["overflow_queries"] * k
 
 
 @pytest.mark.parametrize("scale", [1e4, 3e-7, 1.0])
@@ -131,3 +134,30 @@ def test_prefilter_matches_fp32_scan_at_scale(mivs_lib):
         idx.set_prefilter(False)
         d2, i2 = ivf_flat.search(sp, idx, q, k)
         assert torch.equal(i1, i2) and torch.equal(d1, d2)
+
+
+@pytest.mark.parametrize("metric", ["sqeuclidean", "inner_product"])
+@pytest.mark.parametrize("k", [1, 10, 16])
+def test_brute_force_prefilter_bitexact(mivs_lib, metric, k):
+    """brute_force.search with k <= 16 runs the fp16 pre-filter over the one list (three 16384-row
+    work items here) + the exact refine: identical to the fp32 scan and to the oracle."""
+    from mivs.neighbors import brute_force
+
+    rng = np.random.default_rng(77 + k)
+    x = rng.standard_normal((40000, 128)).astype(np.float32)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    q = rng.standard_normal((300, 128)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    idx = brute_force.build(torch.from_numpy(x).cuda(), metric=metric, ids_offset=11)
+    assert idx.prefilter
+    d1, i1 = brute_force.search(idx, torch.from_numpy(q).cuda(), k)
+    st = idx.last_search_stats()
+    idx.set_prefilter(False)
+    assert not idx.prefilter
+    d0, i0 = brute_force.search(idx, torch.from_numpy(q).cuda(), k)
+    np.testing.assert_array_equal(i1.cpu().numpy(), i0.cpu().numpy())
+    np.testing.assert_array_equal(d1.cpu().numpy().view(np.int32), d0.cpu().numpy().view(np.int32))
+    od, oi = O.knn(x, q, k, metric=metric, id_offset=11)
+    np.testing.assert_array_equal(i1.cpu().numpy(), oi)
+    np.testing.assert_array_equal(d1.cpu().numpy().view(np.int32), od.view(np.int32))
+    assert st["overflow_queries"] <= 300
