@@ -410,7 +410,7 @@ struct PfAssign {
 
 // the most groups a K10 work item may span: its chunk's norms sit in LDS beside the query tile
 int pf_max_chunk_groups(int dp) {
-  if (pf_pair_mode() && pf_scan_lds_bytes(dp, 1) <= 160 * 1024) return kPfMaxPairGroups;
+  if (pf_scan_lds_bytes(dp, 1) <= 160 * 1024) return kPfMaxPairGroups;
   int g = 1;
   while (pf_scan_lds_bytes(dp, g + 1) <= 160 * 1024) ++g;
   return g;

@@ -218,10 +218,10 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
   float* s_dl = reinterpret_cast<float*>(smem + kPfSmall);    // [64] per-query window delta
   float* s_th = s_dl + kPfQTile;                                // [64] theta at item start
   float* s_l8 = s_th + kPfQTile;                                // [64][16] lane lists' last entries
-  // R = 1: the chunk's row norms [chunk_groups * 32]; R = 2: per wave the norms of its current pass's two
-  // groups [8 waves][2][32] (loaded one pass ahead), so the chunk size is not bound by LDS
+  // per wave the row norms of its current pass's groups [8 waves][64] (loaded one pass ahead), so the
+  // chunk size is not bound by LDS
   float* s_norm = s_l8 + kPfQTile * 16;
-  char* s_b = reinterpret_cast<char*>(s_norm + (R == 2 ? kPfWaves * 64 : a.chunk_groups * kGroupRows));
+  char* s_b = reinterpret_cast<char*>(s_norm + kPfWaves * 64);
   float* mkey = reinterpret_cast<float*>(s_b);
   int* mpos = reinterpret_cast<int*>(mkey + kPfQTile * 16 * kPfLaneK);
 
@@ -300,8 +300,6 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
       }
     }
     for (int i = tid; i < kPfQTile * 16; i += kPfThreads) s_l8[i] = INFINITY;
-    if constexpr (R == 1)
-      for (int i = tid; i < ng * kGroupRows; i += kPfThreads) s_norm[i] = a.row_norms[g_begin * kGroupRows + i];
     int* const cpos = a.chunk_pos ? a.chunk_pos + (int64_t)l * a.chunk_stride + chunk : nullptr;
     if (tid == 0) s_misc[2] = cpos ? __hip_atomic_load(cpos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
     __syncthreads();
@@ -444,9 +442,17 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
       }
     } else {
     if (npw > 0) {
+      // convoy start as in the pair path, in passes of one group per wave
+      const int rot = s_misc[2] % npw;
+      auto phys1 = [&](int pr) { return pr + rot < npw ? pr + rot : pr + rot - npw; };
       const uint16_t* abase = a.groups_h + ((g_begin + wave) * nb + h) * 256 + j * 8;
-      const uint16_t* nptr = abase;  // pass base of the next load
+      const uint16_t* nptr = abase + (int64_t)phys1(0) * pstride;  // pass base of the next load
       int ls = 0, lpass = 0;         // k-step / pass of the next load (past the end: re-read the last pass)
+      float* const wn = s_norm + wave * 64;
+      auto pass_norm = [&](int pr) {
+        return a.row_norms[(g_begin + wave + (int64_t)phys1(pr) * kPfWaves) * kGroupRows + (lane & 31)];
+      };
+      float nrm = pass_norm(0);
       h8 ring[D];
       // the ring holds one block of D k-steps; (nptr, ls) = the next block to load (nk % D == 0)
 #pragma unroll
@@ -455,7 +461,7 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
         __builtin_amdgcn_sched_barrier(0);  // issue in ring order: the loop header then waits vmcnt(D-1)
       }
       ls += D;
-      if (ls == nk) { ls = 0; if (++lpass < npw) nptr += pstride; }
+      if (ls == nk) { ls = 0; if (++lpass < npw) nptr = abase + (int64_t)phys1(lpass) * pstride; }
       const f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       f32x16 c0 = zero, c1 = zero;
       int p = 0, s = 0;
@@ -486,9 +492,16 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
           __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
         }
         ls += D;
-        if (ls == nk) { ls = 0; if (++lpass < npw) nptr += pstride; }
+        if (ls == nk) { ls = 0; if (++lpass < npw) nptr = abase + (int64_t)phys1(lpass) * pstride; }
         s += D;
-        if (s == nk) epilogue(c0, c1, p * kPfWaves + wave, s_norm + (p * kPfWaves + wave) * kGroupRows);
+        if (s == nk) {
+          const int pp = phys1(p);
+          if (cpos && wave == 0 && lane == 0)
+            __hip_atomic_store(cpos, pp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          wn[lane] = nrm;
+          if (p + 1 < npw) nrm = pass_norm(p + 1);
+          epilogue(c0, c1, pp * kPfWaves + wave, wn);
+        }
         if (s == nk) {
           c0 = zero;
           c1 = zero;
@@ -1359,7 +1372,8 @@ bool pf_pair_mode() {
 
 size_t pf_scan_lds_bytes(int dp, int chunk_groups) {
   const size_t b = (size_t)dp * kPfQTile * 2;
-  const size_t norms = pf_pair_mode() ? (size_t)kPfWaves * 64 * 4 : (size_t)chunk_groups * kGroupRows * 4;
+  (void)chunk_groups;  // the row norms go through a per-wave slot: any chunk length fits
+  const size_t norms = (size_t)kPfWaves * 64 * 4;
   return kPfSmall + (size_t)kPfQTile * 18 * 4 + norms + (b > (size_t)kPfMergeBytes ? b : (size_t)kPfMergeBytes);
 }
 
