@@ -55,6 +55,7 @@ def main():
     del bf, xf
     torch.cuda.empty_cache()
     sweep = []
+    sizes = idx.list_sizes.cpu()
     for npb in [int(s) for s in a.sweep.split(",") if s.strip()]:
         sp = ivf_pq.SearchParams(n_probes=npb)
         ivf_pq.search(sp, idx, q, k)
@@ -71,9 +72,19 @@ def main():
         _native.set_profiling(False)
         found = ids[:ng].cpu().numpy()
         rec = float(np.mean([len(set(r) & set(g)) / k for r, g in zip(found, gt)]))
+        # LUT-gather roofline of the scan: one LDS lookup per (probed row, subspace); ds_read_b32 peaks at
+        # 32 lookups / clk / CU (two 32-lane groups, conflict-free) -> 256 CUs x 2.4 GHz x 32
+        probes = torch.empty((Q, npb), dtype=torch.int32, device="cuda")
+        ivf_pq.search(sp, idx, q, k, probes_out=probes)
+        rows = int(sizes[probes.long().cpu()].sum())
+        scan_ms = pr["scan_ms"] / max(pr["n_calls"], 1)
+        lookups = rows * a.pq_dim
+        peak = 256 * 2.4e9 * 32
         sweep.append({"n_probes": npb, "qps": Q / ts, "ms_per_batch": ts * 1e3, "recall_at_10": rec,
-                      "scan_ms": pr["scan_ms"] / max(pr["n_calls"], 1),
-                      "coarse_ms": pr["coarse_ms"] / max(pr["n_calls"], 1)})
+                      "scan_ms": scan_ms, "coarse_ms": pr["coarse_ms"] / max(pr["n_calls"], 1),
+                      "roofline": {"bound": "lds", "achieved": lookups / (scan_ms * 1e-3) / 1e9, "peak": peak / 1e9,
+                                   "unit": "Glookups/s", "frac": lookups / (scan_ms * 1e-3) / peak,
+                                   "lookups_per_batch": lookups, "rows_scanned": rows}})
         print(f"[search] n_probes={npb}: {Q / ts:,.0f} QPS recall@{k}={rec:.4f} scan {sweep[-1]['scan_ms']:.2f} ms",
               file=sys.stderr, flush=True)
     print(json.dumps({"metric": "IVF-PQ QPS @ recall@10 + build vectors/s (per-GPU share of 100M x 768 fp16)",
