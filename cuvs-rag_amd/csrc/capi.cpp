@@ -23,87 +23,13 @@
 #include <vector>
 
 #include "../../include/mivs.h"
+#include "capi_util.hpp"
 #include "mivs_common.hpp"
 
 using namespace mivs;
+using namespace mivs_capi;
 
 namespace {
-
-thread_local std::string g_err;
-std::atomic<int> g_profiling{0};
-
-struct MivsError : std::runtime_error {
-  int code;
-  MivsError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
-};
-
-void hipchk(hipError_t e, const char* what) {
-  if (e == hipSuccess) return;
-  (void)hipGetLastError();
-  const int code = e == hipErrorOutOfMemory ? MIVS_ERR_OOM : MIVS_ERR_HIP;
-  int dev = -1;
-  (void)hipGetDevice(&dev);
-  throw MivsError(code, std::string(what) + ": " + hipGetErrorString(e) + " (device " + std::to_string(dev) + ")");
-}
-#define HIPCHK(x) hipchk((x), #x)
-
-void require(bool ok, const std::string& msg, int code = MIVS_ERR_INVALID) {
-  if (!ok) throw MivsError(code, msg);
-}
-
-template <class F>
-int32_t guarded(F&& f) {
-  try {
-    f();
-    return MIVS_OK;
-  } catch (const MivsError& e) {
-    g_err = e.what();
-    return e.code;
-  } catch (const std::bad_alloc&) {
-    g_err = "host allocation failed";
-    return MIVS_ERR_OOM;
-  } catch (const std::exception& e) {
-    g_err = e.what();
-    return MIVS_ERR_HIP;
-  }
-}
-
-// owning device buffer (grow-only when reused as workspace)
-struct Buf {
-  void* p = nullptr;
-  size_t n = 0;
-  Buf() = default;
-  Buf(const Buf&) = delete;
-  Buf& operator=(const Buf&) = delete;
-  ~Buf() { release(); }
-  void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    n = 0;
-  }
-  void reserve(size_t bytes) {
-    if (bytes <= n && p) return;
-    if (p) HIPCHK(hipDeviceSynchronize());  // in-flight work may still use the old workspace
-    release();
-    HIPCHK(hipMalloc(&p, bytes > 0 ? bytes : 16));
-    n = bytes;
-  }
-  template <class T>
-  T* as() const { return static_cast<T*>(p); }
-};
-
-int cu_count(int device) {
-  static std::mutex mu;
-  static std::vector<int> cache;
-  std::lock_guard<std::mutex> g(mu);
-  if ((int)cache.size() <= device) cache.resize(device + 1, 0);
-  if (cache[device] == 0) {
-    hipDeviceProp_t prop;
-    HIPCHK(hipGetDeviceProperties(&prop, device));
-    cache[device] = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-  }
-  return cache[device];
-}
 
 // A set of inverted lists in the interleaved group layout.
 struct ListSet {
@@ -217,18 +143,6 @@ struct mivs_index_s {
 };
 
 namespace {
-
-struct DeviceGuard {
-  int prev = -1;
-  explicit DeviceGuard(int dev) {
-    HIPCHK(hipGetDevice(&prev));
-    if (prev != dev) HIPCHK(hipSetDevice(dev));
-  }
-  ~DeviceGuard() {
-    int cur = -1;
-    if (hipGetDevice(&cur) == hipSuccess && cur != prev && prev >= 0) (void)hipSetDevice(prev);
-  }
-};
 
 // ---- one scan job: lists x buckets -> partial slots ----
 struct ScanJob {
@@ -1154,7 +1068,9 @@ int32_t mivs_ivf_flat_extend(mivs_index_t idx, void* stream, const float* d_new,
     HIPCHK(hipMemcpyAsync(new_rows, d_new, sizeof(float) * (size_t)n_new * d, hipMemcpyDeviceToDevice, s));
     if (d_new_ids) HIPCHK(hipMemcpyAsync(ids.as<int64_t>() + n_old, d_new_ids, sizeof(int64_t) * n_new,
                                          hipMemcpyDeviceToDevice, s));
-    else HIPCHK(launch_iota_i64(ids.as<int64_t>() + n_old, n_new, n_old, 1, s));
+    // default ids continue the index's own global range: a shard built with ids_offset = start_index
+    // keeps its new rows inside that range instead of colliding with shard 0's ids
+    else HIPCHK(launch_iota_i64(ids.as<int64_t>() + n_old, n_new, idx->id_offset + n_old, 1, s));
     norms.reserve(sizeof(float) * (size_t)n_new);
     HIPCHK(launch_row_norms(new_rows, n_new, d, norms.as<float>(), s));
     assign_rows(new_rows, norms.as<float>(), nullptr, n_new, d, idx->dp, idx->cents, idx->G, idx->metric,
@@ -1610,6 +1526,10 @@ int32_t mivs_brute_force_search(mivs_index_t idx, void* stream, const float* d_q
       idx->last_k = k;
       return;
     }
+    // the exact fp32 scan: no pre-filter ran, nothing overflowed (stats must not keep a previous search's)
+    idx->last_pf = 0;
+    idx->last_ovf = 0;
+    idx->last_window = 0;
     if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
     single_list_topk(idx->lists, idx->G, d_q, idx->ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, k, idx->metric,
                      d_dist, d_ids, idx->device, idx->ws, s);
@@ -1663,10 +1583,12 @@ int32_t mivs_index_last_search_stats(mivs_index_t idx, mivs_search_stats* out) {
       }
       st.work_items = woff[L.n_lists];
     } else if (idx->last_nq > 0) {
+      // brute force: the pre-filter scan (K10) works in pf_G-group chunks, the exact scans in G
+      const int G = idx->last_pf ? idx->pf_G : idx->G;
       st.scanned_rows = idx->last_nq * L.n_rows;
       st.streamed_groups = ceil_div(idx->last_nq, idx->last_qtile) * L.n_groups;
       st.unique_groups = L.n_groups;
-      st.work_items = ceil_div(idx->last_nq, idx->last_qtile) * std::max<int64_t>(1, ceil_div(L.n_groups, idx->G));
+      st.work_items = ceil_div(idx->last_nq, idx->last_qtile) * std::max<int64_t>(1, ceil_div(L.n_groups, G));
     }
     *out = st;
   });

@@ -1,0 +1,104 @@
+// Shared plumbing of the C-ABI translation units (capi.cpp, comm.cpp): the thread-local error
+// channel behind mivs_last_error(), HIP status -> MIVS_ERR_* mapping, owning device buffers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/mivs.h"
+
+namespace mivs_capi {
+
+inline thread_local std::string g_err;
+inline std::atomic<int> g_profiling{0};
+
+struct MivsError : std::runtime_error {
+  int code;
+  MivsError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+inline void hipchk(hipError_t e, const char* what) {
+  if (e == hipSuccess) return;
+  (void)hipGetLastError();
+  const int code = e == hipErrorOutOfMemory ? MIVS_ERR_OOM : MIVS_ERR_HIP;
+  int dev = -1;
+  (void)hipGetDevice(&dev);
+  throw MivsError(code, std::string(what) + ": " + hipGetErrorString(e) + " (device " + std::to_string(dev) + ")");
+}
+#define HIPCHK(x) hipchk((x), #x)
+
+inline void require(bool ok, const std::string& msg, int code = MIVS_ERR_INVALID) {
+  if (!ok) throw MivsError(code, msg);
+}
+
+template <class F>
+int32_t guarded(F&& f) {
+  try {
+    f();
+    return MIVS_OK;
+  } catch (const MivsError& e) {
+    g_err = e.what();
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    g_err = "host allocation failed";
+    return MIVS_ERR_OOM;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return MIVS_ERR_HIP;
+  }
+}
+
+// owning device buffer (grow-only when reused as workspace)
+struct Buf {
+  void* p = nullptr;
+  size_t n = 0;
+  Buf() = default;
+  Buf(const Buf&) = delete;
+  Buf& operator=(const Buf&) = delete;
+  ~Buf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  void reserve(size_t bytes) {
+    if (bytes <= n && p) return;
+    if (p) HIPCHK(hipDeviceSynchronize());  // in-flight work may still use the old workspace
+    release();
+    HIPCHK(hipMalloc(&p, bytes > 0 ? bytes : 16));
+    n = bytes;
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+inline int cu_count(int device) {
+  static std::mutex mu;
+  static std::vector<int> cache;
+  std::lock_guard<std::mutex> g(mu);
+  if ((int)cache.size() <= device) cache.resize(device + 1, 0);
+  if (cache[device] == 0) {
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    cache[device] = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  }
+  return cache[device];
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    HIPCHK(hipGetDevice(&prev));
+    if (prev != dev) HIPCHK(hipSetDevice(dev));
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur != prev && prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+}  // namespace mivs_capi

@@ -28,9 +28,16 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
   if (q >= a.nq) return;
   int64_t sb, se;
   if (a.slot_begin) { sb = a.slot_begin[q]; se = a.slot_begin[q + 1]; }
+  else if (a.part_stride > 0) { sb = 0; se = a.slots_per_q; }
   else { sb = q * a.slots_per_q; se = sb + a.slots_per_q; }
   const int64_t c1 = se * a.k_in;
   const int k = a.k;
+  // candidate c -> element: contiguous, or (part c / k_in, rank c % k_in) of the rank-major gather
+  auto at = [&](int64_t c) {
+    if (a.part_stride <= 0) return c;
+    const int64_t p = c / a.k_in;
+    return p * a.part_stride + q * a.k_in + (c - p * a.k_in);
+  };
 
   float mk = INFINITY;      // rank `lane` of the running top-k
   int64_t mi = LLONG_MAX;
@@ -41,9 +48,10 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
     float ck = INFINITY;
     int64_t ci = LLONG_MAX;
     if (cc < c1) {
-      const int64_t id = a.in_i[cc];
+      const int64_t e = at(cc);
+      const int64_t id = a.in_i[e];
       if (id >= 0) {
-        const float dd = a.in_d[cc];
+        const float dd = a.in_d[e];
         ck = METRIC == kIP ? -dd : dd;
         ci = id;
       }

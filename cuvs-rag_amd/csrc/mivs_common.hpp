@@ -90,6 +90,9 @@ struct MergeArgs {
   int k_in, k, metric;
   float* out_d;
   int64_t* out_i;
+  // > 0: gathered layout [slots_per_q parts][nq][k_in] with parts part_stride elements apart (the
+  // all-gather receive buffer, rank-major); 0: [nq][slots][k_in] / slot_begin as above
+  int64_t part_stride;
 };
 
 // IVF-PQ scan job (K9, pq.hip): one workgroup per (query, probe) slot = q * n_probes + p.

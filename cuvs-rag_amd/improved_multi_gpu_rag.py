@@ -10,8 +10,12 @@ cuVS calls replaced by ``mivs.neighbors`` (hand-written HIP kernels on MI355X).
 
 Behavioural fixes:
   * ``parallel_search`` merges PER QUERY ([Q, k] in, [Q, k] out) on the device instead of
-    flattening every query's candidates together (:259-273, only correct for Q = 1); a 1-D or
-    single-row query still returns 1-D arrays as before;
+    flattening every query's candidates together (:259-273, only correct for Q = 1); a 1-D query
+    still returns 1-D arrays as before, a 2-D batch always returns [Q, k] (also for Q = 1);
+  * the per-GPU tiles meet over RCCL (``mivs.comm``: one grouped all-gather on xGMI, K7 on the
+    device) and merge in the indices' metric order (inner product descending);
+  * worker searches always get device tensors (a thread-local ``output_as("torch")``) whatever
+    hook the driver set with ``set_output_as`` (:114), so ``.to(dev)`` never meets a numpy array;
   * shard ``i``'s ids are made global with its row offset (the reference applied none);
   * ``build_indices_parallel`` reports wall-clock ``total_time`` next to the summed per-GPU time.
 """
@@ -101,6 +105,10 @@ class CUDAMemoryManager:
         finally:
             after = gpu_config.get_available_memory()
             logger.info("[GPU %d] Completed %s, used %.2f GB", gpu_config.device_id, operation, before - after)
+
+
+def _metric_of(index: Any) -> str:
+    return str(getattr(index, "metric", "sqeuclidean"))
 
 
 def _to_numpy(x) -> np.ndarray:
@@ -198,8 +206,9 @@ class ParallelSearchEngine:
             query = query.to(f"cuda:{gpu_id}")
         if query.dim() == 1:
             query = query.unsqueeze(0)
-        prev = mivs_config.get_output_as()
-        try:
+        # the driver's hook (e.g. copy_to_host, reference :114) applies to what parallel_search returns,
+        # not to the per-shard tiles, which must stay on the device for the merge
+        with mivs_config.output_as("torch"):
             if isinstance(index, ivf_flat.Index):
                 d, i = ivf_flat.search(ivf_flat.SearchParams(n_probes=self.search_config.n_probes), index, query, k)
             elif isinstance(index, ivf_pq.Index):
@@ -208,8 +217,6 @@ class ParallelSearchEngine:
                 d, i = brute_force.search(index, query, k)
             else:
                 raise ValueError(f"Unsupported index type: {self.index_type}")
-        finally:
-            mivs_config.set_output_as(prev)
         d = d.tensor if hasattr(d, "tensor") else d
         i = i.tensor if hasattr(i, "tensor") else i
         return d, i
@@ -232,14 +239,19 @@ class ParallelSearchEngine:
         if not res:
             return np.array([]), np.array([])
         order = sorted(res)
-        dev = torch.device(f"cuda:{order[0]}")
-        d = torch.stack([res[g][0].to(dev) for g in order], dim=1)
-        i = torch.stack([res[g][1].to(dev) for g in order], dim=1)
-        kk = min(k, d.shape[1] * d.shape[2])
-        with torch.cuda.device(dev):
-            fd, fi = ops.merge_topk(d, i, kk)
+        metric = _metric_of(self.gpu_indexes[order[0]])
+        kk = min(k, sum(int(res[g][0].shape[1]) for g in order))
+        if len(order) > 1:
+            from mivs.comm import local_comm
+
+            out = local_comm(order).merge_topk_allgather({g: res[g][0] for g in order}, {g: res[g][1] for g in order},
+                                                         kk, metric, out_devices=[order[0]])
+            fd, fi = out[order[0]]
+        else:
+            with torch.cuda.device(order[0]):
+                fd, fi = ops.merge_topk(res[order[0]][0], res[order[0]][1], kk, metric=metric)
         fd, fi = _to_numpy(fd), _to_numpy(fi)
-        return (fd[0], fi[0]) if single or q.shape[0] == 1 else (fd, fi)
+        return (fd[0], fi[0]) if single else (fd, fi)
 
     def batch_search(self, queries: List[torch.Tensor]) -> List[Tuple[np.ndarray, np.ndarray]]:
         """Searches `search_batch_size` queries per device call (the reference ran one call per query)."""
@@ -284,16 +296,23 @@ class RecallEvaluator:
                 for i in range(num_queries)}
 
     @staticmethod
-    def exact_ground_truth(index_parts: Dict[int, Any], queries: torch.Tensor, k: int) -> np.ndarray:
+    def exact_ground_truth(index_parts: Dict[int, Any], queries: torch.Tensor, k: int,
+                           metric: str = "sqeuclidean") -> np.ndarray:
         """Exact top-k ids over all shards (brute force on each shard's own rows is the caller's job);
-        here: merge of per-shard exact results already computed as {gpu: (dist, ids)}."""
+        here: merge of per-shard exact results already computed as {gpu: (dist, ids)}, in the order of
+        ``metric`` (inner product: descending)."""
         from mivs import ops
 
         order = sorted(index_parts)
         dev = torch.device(f"cuda:{order[0]}")
-        d = torch.stack([index_parts[g][0].to(dev) for g in order], dim=1)
-        i = torch.stack([index_parts[g][1].to(dev) for g in order], dim=1)
-        return _to_numpy(ops.merge_topk(d, i, k)[1])
+
+        def t(x):
+            return (x.tensor if hasattr(x, "tensor") else torch.as_tensor(x)).to(dev)
+
+        d = torch.stack([t(index_parts[g][0]) for g in order], dim=1)
+        i = torch.stack([t(index_parts[g][1]) for g in order], dim=1)
+        with torch.cuda.device(dev):
+            return _to_numpy(ops.merge_topk(d, i, k, metric=metric)[1])
 
 
 def get_memory_stats() -> Dict:

@@ -145,6 +145,13 @@ _SIGS = {
                                       c_void_p]),
     "mivs_merge_topk": (c_int32, [c_int32, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_int32,
                                   c_void_p, c_void_p]),
+    "mivs_merge_topk_gathered": (c_int32, [c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_int64, c_int32, c_int32,
+                                           c_int32, c_void_p, c_void_p]),
+    "mivs_comm_init_all": (c_int32, [c_int32, POINTER(c_int32), POINTER(c_void_p)]),
+    "mivs_comm_size": (c_int32, [c_void_p, POINTER(c_int32)]),
+    "mivs_merge_topk_allgather": (c_int32, [c_void_p, POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), c_int64,
+                                            c_int32, c_int32, c_int32, POINTER(c_void_p), POINTER(c_void_p)]),
+    "mivs_comm_destroy": (None, [c_void_p]),
     "mivs_row_norms": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int32, c_void_p]),
     "mivs_normalize_rows": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int32, c_void_p]),
     "mivs_synth_mixture": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int64, c_int32, c_uint64, c_int32,

@@ -9,6 +9,7 @@ here: results are handed to the hook as a :class:`DeviceArray` (which has
 from __future__ import annotations
 
 import threading
+from contextlib import contextmanager
 from typing import Any, Callable, Union
 
 import torch
@@ -39,24 +40,49 @@ class DeviceArray:
         return f"DeviceArray(shape={self.shape}, dtype={self.dtype}, device={self.tensor.device})"
 
 
+# The process-wide hook (what pylibraft.config.set_output_as sets), and a per-thread override used by
+# the engine's own worker threads: a driver thread that set the hook to copy_to_host must not change
+# what a search running on another thread returns, and a worker that needs device tensors must not
+# flip the hook under the driver's feet.
 _state = threading.local()
 _global: Union[str, Callable[[DeviceArray], Any]] = "torch"
+_KINDS = ("torch", "raft", "mivs", "numpy", "cupy")
+
+
+def _check(output) -> None:
+    if isinstance(output, str) and output not in _KINDS:
+        raise ValueError(f"unknown output type {output!r}")
+    if not isinstance(output, str) and not callable(output):
+        raise ValueError(f"output must be one of {_KINDS} or a callable, got {output!r}")
 
 
 def set_output_as(output: Union[str, Callable[[DeviceArray], Any]]) -> None:
-    """'torch' (default), 'raft'/'mivs' (DeviceArray), 'numpy', or a callable taking a DeviceArray."""
+    """'torch' (default), 'raft'/'mivs' (DeviceArray), 'numpy', or a callable taking a DeviceArray.
+    Process-wide, like pylibraft's; threads inside an ``output_as`` block keep their own setting."""
     global _global
-    if isinstance(output, str) and output not in ("torch", "raft", "mivs", "numpy", "cupy"):
-        raise ValueError(f"unknown output type {output!r}")
+    _check(output)
     _global = output
 
 
 def get_output_as():
-    return _global
+    """The setting in force on this thread (its ``output_as`` override, else the process-wide hook)."""
+    return getattr(_state, "override", None) or _global
+
+
+@contextmanager
+def output_as(output: Union[str, Callable[[DeviceArray], Any]]):
+    """Thread-local override of the output hook for the duration of the block (nests)."""
+    _check(output)
+    prev = getattr(_state, "override", None)
+    _state.override = output
+    try:
+        yield
+    finally:
+        _state.override = prev
 
 
 def convert_output(t: torch.Tensor):
-    out = _global
+    out = get_output_as()
     if callable(out):
         return out(DeviceArray(t))
     if out == "torch":

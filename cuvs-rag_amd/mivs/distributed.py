@@ -17,15 +17,20 @@ import torch
 import torch.distributed as dist
 
 
-def all_gather_topk(distances: torch.Tensor, ids: torch.Tensor, group=None):
-    """-> (dist [Q, world, k], ids [Q, world, k]) gathered from every rank (rank order)."""
+def all_gather_raw(distances: torch.Tensor, ids: torch.Tensor, group=None):
+    """-> (dist [world, Q, k], ids [world, Q, k]): the rank-major all-gather receive buffers."""
     world = dist.get_world_size(group)
     q, k = distances.shape
     gd = torch.empty((world * q, k), dtype=distances.dtype, device=distances.device)
     gi = torch.empty((world * q, k), dtype=ids.dtype, device=ids.device)
     dist.all_gather_into_tensor(gd, distances.contiguous(), group=group)
     dist.all_gather_into_tensor(gi, ids.contiguous(), group=group)
-    gd, gi = gd.view(world, q, k), gi.view(world, q, k)
+    return gd.view(world, q, k), gi.view(world, q, k)
+
+
+def all_gather_topk(distances: torch.Tensor, ids: torch.Tensor, group=None):
+    """-> (dist [Q, world, k], ids [Q, world, k]) gathered from every rank (rank order)."""
+    gd, gi = all_gather_raw(distances, ids, group)
     return gd.permute(1, 0, 2).contiguous(), gi.permute(1, 0, 2).contiguous()
 
 
@@ -33,14 +38,18 @@ def merge_across_ranks(distances: torch.Tensor, ids: torch.Tensor, k: int, metri
                        group=None, merge_fn: Optional[Callable] = None):
     """Global top-k over all shards; every rank gets the same result.
 
-    ``merge_fn(dist[Q, m, k_in], ids[Q, m, k_in], k, metric)`` defaults to the K7 device merge
-    (``mivs.ops.merge_topk``); tests on the CPU gloo backend pass their own.
+    The default merge is K7 reading the rank-major receive buffer in place
+    (``mivs.ops.merge_topk_gathered``: no transpose). ``merge_fn(dist[Q, m, k_in], ids[Q, m, k_in],
+    k, metric)`` replaces it (tests on the CPU gloo backend pass their own).
     """
     if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
         return distances, ids
-    gd, gi = all_gather_topk(distances, ids, group)
     if merge_fn is None:
-        from .ops import merge_topk as merge_fn
+        from .ops import merge_topk_gathered
+
+        gd, gi = all_gather_raw(distances, ids, group)
+        return merge_topk_gathered(gd, gi, k, metric)
+    gd, gi = all_gather_topk(distances, ids, group)
     return merge_fn(gd, gi, k, metric)
 
 

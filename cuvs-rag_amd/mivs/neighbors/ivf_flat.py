@@ -260,7 +260,9 @@ def search(search_params: SearchParams, index: Index, queries, k: int, neighbors
 
 def extend(index: Index, new_vectors, new_indices=None) -> Index:
     """cuvs.neighbors.ivf_flat.extend: append rows to their nearest lists (the build's assign; each list
-    keeps its current rows first). ``new_indices`` None: ids ``len(index) .. len(index) + n - 1``.
+    keeps its current rows first). ``new_indices`` None: ids ``ids_offset + len(index) ..
+    ids_offset + len(index) + n - 1`` (``ids_offset`` as given to ``build``; 0 for a loaded index), so a
+    shard of a sharded corpus keeps its new rows inside its own global id range.
     Returns ``index`` (extended in place)."""
     if not isinstance(index, Index):
         raise TypeError("index must be an ivf_flat.Index")

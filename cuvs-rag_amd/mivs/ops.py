@@ -27,6 +27,22 @@ def merge_topk(dist: torch.Tensor, ids: torch.Tensor, k: int, metric: str = "sqe
     return od, oi
 
 
+def merge_topk_gathered(dist: torch.Tensor, ids: torch.Tensor, k: int, metric: str = "sqeuclidean"):
+    """K7 over an all-gather receive buffer: dist/ids [parts, nq, k_in] (rank-major) -> [nq, k]."""
+    if dist.shape != ids.shape or dist.dim() != 3:
+        raise ValueError("dist/ids must have equal shape [parts, nq, k_in]")
+    parts, nq, k_in = dist.shape
+    dev = dist.device.index
+    d = dist.contiguous().float()
+    i = ids.contiguous().to(torch.int64)
+    od = torch.empty((nq, k), dtype=torch.float32, device=dist.device)
+    oi = torch.empty((nq, k), dtype=torch.int64, device=dist.device)
+    with torch.cuda.device(dev):
+        _native.check(_native.lib().mivs_merge_topk_gathered(dev, stream_ptr(dev), ptr(d), ptr(i), parts, nq, k_in, k,
+                                                             _merge_order(metric), ptr(od), ptr(oi)))
+    return od, oi
+
+
 def _merge_order(metric: str) -> int:
     """Cosine results are distances 1 - ip (smaller is better): merged in the L2 order."""
     from ._cosine import is_cosine

@@ -5,18 +5,26 @@ The reference ships this module as an EMPTY file (``Attempt_1/search_result_aggr
 (:14-21 exports, :25-236 types, :239-499 behaviour) and ``Latest/cuVS-2-gpu/old/
 DesignDocument.md:119-137,174-189``. This is that contract, written for MI355X:
 
-  * per-GPU search runs on each shard's mivs index (``ivf_flat`` / ``brute_force``), one
-    thread per GPU (native calls release the GIL), queries copied to each device once;
-  * the global merge is the K7 wave top-k kernel on the device (``mivs.ops.merge_topk``),
-    replacing the reference's host numpy argsort (improved_multi_gpu_rag.py:266-275,
-    cuvs-2gpu-main.ipynb:1820-1834); rows merge independently, so the ``(P, k)`` concat +
-    axis-0 fancy-index bug (``index 2 is out of bounds``, RequirementsDocument.md:5) cannot occur;
+  * per-GPU search runs on each shard's mivs index (``ivf_flat`` / ``ivf_pq`` / ``brute_force``),
+    one thread per GPU (native calls release the GIL), queries copied to each device once;
+  * the per-shard [Q, k] tiles stay on their devices and are merged over RCCL: one grouped
+    all-gather on xGMI (``mivs.comm.LocalComm`` -> ``mivs_merge_topk_allgather``) and the K7 wave
+    merge on the device, replacing the reference's host numpy argsort
+    (improved_multi_gpu_rag.py:266-275, cuvs-2gpu-main.ipynb:1820-1834). Under torch.distributed
+    (one process per GPU) the local result is then merged across ranks with
+    ``mivs.distributed.merge_across_ranks`` (RCCL all-gather, same K7 merge). Rows merge
+    independently, so the ``(P, k)`` concat + axis-0 fancy-index bug (``index 2 is out of bounds``,
+    RequirementsDocument.md:5) cannot occur;
+  * the merge order follows the indices' metric (ascending L2 / cosine distance, descending inner
+    product), ties by id;
   * shards built by the coordinator carry GLOBAL ids (``ids_offset = start_index``), so no
     ``i * len(parts[i])`` remap is needed (cuvs-2gpu-main.ipynb:1803).
 
+The per-GPU ``SearchResult`` objects of the contract hold host numpy arrays; they are copied out
+once, after the device merge has been enqueued, never fed back to a device.
+
 Without a usable engine (``CUVS_AVAILABLE`` False: no GPU) the aggregator runs the contract's
 simulation (``_simulate_search``) and merges on the host; it never falls back to CPU search.
-Multi-process (one rank per GPU) deployments merge with ``mivs.distributed.merge_across_ranks``.
 """
 from __future__ import annotations
 
@@ -96,38 +104,94 @@ class SearchConfig:
     timeout_seconds: Optional[float] = None
     validate_results: bool = True
     id_offsets: Optional[Dict[int, int]] = field(default=None)
+    # mivs extension: how per-shard tiles meet for the merge. "auto": RCCL all-gather across the GPUs
+    # of this process when there are several, the K7 merge alone for one; "rccl": always the RCCL
+    # exchange (also for one GPU); "peer": peer copies to the first GPU, then K7
+    exchange: str = "auto"
 
     def __post_init__(self):
         if self.k <= 0:
             raise ValueError(f"k must be positive, got {self.k}")
         if self.timeout_seconds is not None and self.timeout_seconds <= 0:
             raise ValueError(f"timeout_seconds must be positive, got {self.timeout_seconds}")
+        if self.exchange not in ("auto", "rccl", "peer"):
+            raise ValueError(f"exchange must be 'auto', 'rccl' or 'peer', got {self.exchange!r}")
 
 
-def _host_merge(dist: np.ndarray, ids: np.ndarray, k: int) -> Tuple[np.ndarray, np.ndarray]:
-    """Row-wise (distance, id) ascending merge of [nq, m] candidates, first min(k, m) kept."""
+def _descending(metric: str) -> bool:
+    """Inner product ranks larger first; L2, euclidean and cosine (1 - ip) distances smaller first."""
+    return str(metric).lower() in ("inner_product", "innerproduct", "ip", "dot")
+
+
+def _host_merge(dist: np.ndarray, ids: np.ndarray, k: int, metric: str = "sqeuclidean"
+                ) -> Tuple[np.ndarray, np.ndarray]:
+    """Row-wise merge of [nq, m] candidates by (distance, id) -- distance descending for inner
+    product -- first min(k, m) kept; id -1 entries (missing results) sort last."""
     kk = min(k, dist.shape[1])
     out_d = np.empty((dist.shape[0], kk), np.float32)
     out_i = np.empty((dist.shape[0], kk), np.int64)
+    desc = _descending(metric)
     for r in range(dist.shape[0]):
-        order = np.lexsort((ids[r], dist[r]))[:kk]
+        key = -dist[r].astype(np.float64) if desc else dist[r].astype(np.float64)
+        order = np.lexsort((ids[r], key, ids[r] < 0))[:kk]
         out_d[r], out_i[r] = dist[r, order], ids[r, order]
     return out_d, out_i
 
 
 def _device_merge(dists: List[torch.Tensor], ids: List[torch.Tensor], k: int, metric: str,
                   device: torch.device) -> Tuple[torch.Tensor, torch.Tensor]:
-    """K7 merge of per-shard [nq, k_i] tiles gathered on one device."""
+    """K7 merge of per-shard [nq, k_i] tiles after peer copies to one device."""
     from mivs import ops
 
     kin = max(t.shape[1] for t in dists)
     nq = dists[0].shape[0]
-    pad_d = torch.full((nq, len(dists), kin), float("inf"), dtype=torch.float32, device=device)
+    fill = float("-inf") if _descending(metric) else float("inf")
+    pad_d = torch.full((nq, len(dists), kin), fill, dtype=torch.float32, device=device)
     pad_i = torch.full((nq, len(dists), kin), -1, dtype=torch.int64, device=device)
     for s, (d, i) in enumerate(zip(dists, ids)):
         pad_d[:, s, : d.shape[1]] = d.to(device, non_blocking=True)
         pad_i[:, s, : i.shape[1]] = i.to(device, non_blocking=True)
     return ops.merge_topk(pad_d, pad_i, k, metric=metric)
+
+
+def _pad_tile(d: torch.Tensor, i: torch.Tensor, kin: int, metric: str) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Widen a [nq, k'] tile to [nq, kin] with missing-result padding (id -1)."""
+    if d.shape[1] == kin:
+        return d.contiguous().float(), i.contiguous().to(torch.int64)
+    fill = float("-inf") if _descending(metric) else float("inf")
+    pd = torch.full((d.shape[0], kin), fill, dtype=torch.float32, device=d.device)
+    pi = torch.full((d.shape[0], kin), -1, dtype=torch.int64, device=d.device)
+    pd[:, : d.shape[1]] = d
+    pi[:, : i.shape[1]] = i
+    return pd, pi
+
+
+def _rccl_merge(tiles: Dict[int, Tuple[torch.Tensor, torch.Tensor]], k: int, metric: str
+                ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """All-gather every GPU's tile over RCCL (one process, ncclCommInitAll) + K7 on the first GPU."""
+    from mivs.comm import local_comm
+
+    devs = sorted(tiles)
+    kin = max(int(tiles[g][0].shape[1]) for g in devs)
+    dd, ii = {}, {}
+    for g in devs:
+        with torch.cuda.device(g):
+            dd[g], ii[g] = _pad_tile(tiles[g][0], tiles[g][1], kin, metric)
+    out = local_comm(devs).merge_topk_allgather(dd, ii, k, metric, out_devices=[devs[0]])
+    return out[devs[0]]
+
+
+def _rank_merge(d: torch.Tensor, i: torch.Tensor, k: int, metric: str):
+    """Under torch.distributed (one process per GPU): merge this rank's result with every other rank's
+    over the RCCL all-gather (``mivs.distributed.merge_across_ranks``); identity otherwise."""
+    import torch.distributed as tdist
+
+    if not (tdist.is_available() and tdist.is_initialized() and tdist.get_world_size() > 1):
+        return d, i
+    from mivs.distributed import merge_across_ranks
+
+    with torch.cuda.device(d.device.index):
+        return merge_across_ranks(d.contiguous(), i.contiguous(), k, metric)
 
 
 def combine_search_results(results: List[SearchResult], k: int) -> Tuple[np.ndarray, np.ndarray]:
@@ -167,8 +231,10 @@ class SearchResultAggregator:
                 raise ValueError(f"GPU {r.gpu_id} results contains NaN distances")
         return True
 
-    def merge_search_results(self, gpu_results: List[SearchResult], k: int) -> Tuple[np.ndarray, np.ndarray]:
-        """Per query: all shards' candidates, ascending by (distance, id), first min(k, total) kept."""
+    def merge_search_results(self, gpu_results: List[SearchResult], k: int,
+                             metric: str = "sqeuclidean") -> Tuple[np.ndarray, np.ndarray]:
+        """Per query: all shards' candidates by (distance, id) -- ascending, or descending distance for
+        ``metric="inner_product"`` -- first min(k, total) kept."""
         if not gpu_results:
             raise ValueError("Cannot merge empty results list")
         nq = gpu_results[0].num_queries
@@ -181,11 +247,11 @@ class SearchResultAggregator:
             dev = torch.device(f"cuda:{torch.cuda.current_device()}")
             d, i = _device_merge([torch.as_tensor(np.asarray(r.distances, np.float32)) for r in gpu_results],
                                  [torch.as_tensor(np.asarray(r.indices, np.int64)) for r in gpu_results], kk,
-                                 "sqeuclidean", dev)
+                                 metric, dev)
             return d.cpu().numpy(), i.cpu().numpy()
         dist = np.concatenate([np.asarray(r.distances, np.float32) for r in gpu_results], axis=1)
         ids = np.concatenate([np.asarray(r.indices, np.int64) for r in gpu_results], axis=1)
-        return _host_merge(dist, ids, kk)
+        return _host_merge(dist, ids, kk, metric)
 
     def _simulate_search(self, query: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
         """Contract :389-403: shape (nq, k), non-negative, ascending per row. No device is touched."""
@@ -258,21 +324,33 @@ class SearchResultAggregator:
                     self._active_searches.pop(g, None)
 
         order = sorted(raw)
-        gpu_results = [SearchResult(distances=raw[g][0].detach().cpu().numpy().astype(np.float32),
-                                    indices=raw[g][1].detach().cpu().numpy().astype(np.int64), gpu_id=g,
-                                    query_time=raw[g][2], k_requested=config.k,
+        metric = str(getattr(indices[order[0]], "metric", "sqeuclidean"))
+        kk = min(config.k, sum(int(raw[g][0].shape[1]) for g in order))
+        final_dev = None
+        if CUVS_AVAILABLE and kk <= _MAX_K:
+            # device merge first: the tiles never round-trip through the host on the way to it
+            if config.validate_results:
+                for g in order:
+                    if bool(torch.isnan(raw[g][0]).any()):
+                        raise ValueError(f"GPU {g} results contains NaN distances")
+            use_rccl = config.exchange == "rccl" or (config.exchange == "auto" and len(order) > 1)
+            if use_rccl:
+                fd, fi = _rccl_merge({g: (raw[g][0], raw[g][1]) for g in order}, kk, metric)
+            else:
+                with torch.cuda.device(order[0]):
+                    fd, fi = _device_merge([raw[g][0] for g in order], [raw[g][1] for g in order], kk, metric,
+                                           torch.device(f"cuda:{order[0]}"))
+            final_dev = _rank_merge(fd, fi, kk, metric)
+        gpu_results = [SearchResult(distances=raw[g][0].detach().cpu().numpy().astype(np.float32, copy=False),
+                                    indices=raw[g][1].detach().cpu().numpy().astype(np.int64, copy=False),
+                                    gpu_id=g, query_time=raw[g][2], k_requested=config.k,
                                     k_returned=min(config.k, int(raw[g][0].shape[1]))) for g in order]
         if config.validate_results:
             self.validate_search_results(gpu_results, nq, config.k)
-        kk = min(config.k, sum(int(raw[g][0].shape[1]) for g in order))
-        if CUVS_AVAILABLE and kk <= _MAX_K:
-            metric = getattr(indices[order[0]], "metric", "sqeuclidean")
-            dev = torch.device(f"cuda:{order[0]}")
-            with torch.cuda.device(order[0]):
-                fd, fi = _device_merge([raw[g][0] for g in order], [raw[g][1] for g in order], kk, metric, dev)
-            final_d, final_i = fd.cpu().numpy(), fi.cpu().numpy()
+        if final_dev is not None:
+            final_d, final_i = final_dev[0].cpu().numpy(), final_dev[1].cpu().numpy()
         else:
-            final_d, final_i = self.merge_search_results(gpu_results, config.k)
+            final_d, final_i = self.merge_search_results(gpu_results, config.k, metric)
         result = AggregatedSearchResult(final_distances=final_d, final_indices=final_i,
                                         total_query_time=time.time() - t0, gpu_results=gpu_results,
                                         k_requested=config.k, k_returned=int(final_d.shape[1]), num_queries=nq)

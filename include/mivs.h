@@ -120,7 +120,8 @@ int32_t mivs_ivf_flat_build_from_lists(int32_t device, void* stream, const float
                                        mivs_index_t* out);
 
 /* Append n_new rows [n_new][dim] (device) to an IVF-Flat index: each goes to its nearest list (the
- * build's assign) after the list's current rows. d_new_ids == NULL: ids n_old .. n_old + n_new - 1.
+ * build's assign) after the list's current rows. d_new_ids == NULL: ids id_offset + n_old ..
+ * id_offset + n_old + n_new - 1 (id_offset as given at build).
  * Replaces cuvs.neighbors.ivf_flat.extend (cuvs 25.06; FAISS IndexIVFFlat.add,
  * colab_a100_test.ipynb:479). */
 int32_t mivs_ivf_flat_extend(mivs_index_t index, void* stream, const float* d_new, const int64_t* d_new_ids,
@@ -183,6 +184,31 @@ int32_t mivs_kmeans_predict(int32_t device, void* stream, const float* d_data, i
 int32_t mivs_merge_topk(int32_t device, void* stream, const float* d_in_dist, const int64_t* d_in_ids, int64_t nq,
                         int32_t m, int32_t k_in, int32_t k, int32_t metric, float* d_out_dist,
                         int64_t* d_out_ids);
+
+/* K7 over an all-gather receive buffer: d_in_* = [parts][nq][k_in] (rank-major, what
+ * ncclAllGather / torch all_gather_into_tensor leave), outputs [nq][k]. Same order and padding as
+ * mivs_merge_topk. */
+int32_t mivs_merge_topk_gathered(int32_t device, void* stream, const float* d_in_dist, const int64_t* d_in_ids,
+                                 int32_t parts, int64_t nq, int32_t k_in, int32_t k, int32_t metric,
+                                 float* d_out_dist, int64_t* d_out_ids);
+
+/* ---- cross-shard exchange over RCCL (xGMI), single process, one communicator per local device.
+ * Replaces the reference's host gather + numpy argsort of the per-GPU results
+ * (Latest/cuVS-2-gpu/improved_multi_gpu_rag.py:239-277, cuvs-2gpu-main.ipynb:1820-1834), the merge
+ * behind SearchResultAggregator.perform_distributed_search (Attempt_1/test_search_result_aggregator.py:
+ * 405-457). RCCL is loaded at mivs_comm_init_all (the copy already in the process, e.g. PyTorch's, when
+ * there is one); without it these return MIVS_ERR_UNSUPPORTED. ---- */
+typedef struct mivs_comm_s* mivs_comm_t;
+/* ncclCommInitAll over devs[0..ndev-1]; rank r = devs[r] */
+int32_t mivs_comm_init_all(int32_t ndev, const int32_t* devs, mivs_comm_t* out);
+int32_t mivs_comm_size(mivs_comm_t comm, int32_t* ndev);
+/* Every rank r contributes its shard's top-k_in (d_dist[r], d_ids[r]: [nq][k_in] on devs[r], ids already
+ * global); one grouped ncclAllGather per array, then the K7 merge on every rank whose d_out_dist[r] is
+ * non-NULL -> [nq][k] global top-k. streams[r] (NULL = default) orders it after the producer. */
+int32_t mivs_merge_topk_allgather(mivs_comm_t comm, void* const* streams, const float* const* d_dist,
+                                  const int64_t* const* d_ids, int64_t nq, int32_t k_in, int32_t k,
+                                  int32_t metric, float* const* d_out_dist, int64_t* const* d_out_ids);
+void mivs_comm_destroy(mivs_comm_t comm);
 
 /* ---- helpers exposed for parity tests and the bench ---- */
 int32_t mivs_row_norms(int32_t device, void* stream, const float* d_x, int64_t n, int32_t dim, float* d_out);

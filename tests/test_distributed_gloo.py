@@ -42,7 +42,7 @@ def _rank(rank, world, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from gpu_resource_manager import GPUResourceManager
-    from mivs.distributed import allreduce_max, merge_across_ranks
+    from mivs.distributed import all_gather_raw, allreduce_max, merge_across_ranks
 
     rng = np.random.default_rng(0)
     x = rng.standard_normal((1003, 16)).astype(np.float32)
@@ -57,7 +57,10 @@ def _rank(rank, world, port, out):
     li = torch.from_numpy((loc + start).astype(np.int64))  # global ids = start_index + local id
     gd, gi = merge_across_ranks(ld, li, 5, merge_fn=_host_merge)
     t = allreduce_max(float(rank + 1))
-    out[rank] = (gi.numpy().tolist(), t)
+    # the rank-major receive buffer the device merge (mivs_merge_topk_gathered) reads in place
+    rd, ri = all_gather_raw(ld, li)
+    assert tuple(ri.shape) == (world, 7, 5) and torch.equal(ri[rank], li) and torch.equal(rd[rank], ld)
+    out[rank] = (gi.numpy().tolist(), t, ri.numpy().tolist())
     dist.destroy_process_group()
 
 
@@ -74,9 +77,10 @@ def test_two_rank_shard_merge_equals_single_shard():
     d = ((q[:, None, :] - x[None]) ** 2).sum(-1)
     exact = np.argsort(d, axis=1, kind="stable")[:, :5]
     for r in range(world):
-        ids, t = res[r]
+        ids, t, raw = res[r]
         np.testing.assert_array_equal(np.asarray(ids), exact)
         assert t == 2.0  # max over ranks
+        assert raw == res[0][2]  # every rank holds the same gathered buffer
 
 
 def test_single_process_merge_is_identity():

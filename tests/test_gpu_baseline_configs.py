@@ -1,0 +1,202 @@
+"""Correctness at the FULL sizes of BASELINE.json's single-GPU configs (VERDICT r1 "next" #1).
+
+The bench measures these shapes; these tests make its numbers evidence:
+
+* configs[0] -- 10k x 768 brute force, k = 10: the GPU returns sklearn's ids on the committed
+  golden fixture (tests/golden/knn_synthetic_10k.npz, made by sklearn NearestNeighbors(brute), the
+  reference's CPU baseline, VectorSearch_QuestionRetrieval.ipynb:878).
+* configs[1] -- 1M x 768 brute force, k = 10, 10k queries: the default fp16 pre-filter path (K10 + K11)
+  equals the exact fp32 scan for every query, and the oracle for a query sample.
+* configs[2] -- 10M x 768 IVF-Flat, n_lists 1024, n_probes 32, k = 10, 10k queries (the bench's
+  workload, same generator and seeds as bench.py): (i) K10/K11 == the exact fp32 scan for all 10k
+  queries, (ii) the oracle over the exported centroids and lists == the GPU for 200 sampled queries
+  (ids, distance bits and probes), (iii) the build's labels are the same with the fp16 pre-filter assign
+  (default) and the fp32 assign (MIVS_PF_ASSIGN=0), and the oracle's assign of a 100k-row sample at the
+  GPU's final centroids gives the GPU's lists.
+* configs[4], the per-GPU share -- 12.5M x 768 fp16 IVF-PQ, n_lists 4096, pq_dim 96: the oracle's PQ
+  search over the exported centroids, codebooks and codes == the GPU for a query sample.
+
+Shapes follow the reference's own runs where it has them (submit_narval_job.sh:91-217: 1M x 768;
+cuvs-2gpu-main.ipynb:1756-1834: per-shard IVF-Flat build + search). Sizes are the BASELINE ones; the
+oracle sees samples (it runs on the host's cores).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+SEED = 0
+QUERY_ROW_BASE = 1 << 40  # bench.py: queries are rows of the mixture that no corpus holds
+CENTERS, SIGMA = 65536, 0.75  # bench.py defaults (tools/tune_dataset.py)
+
+
+def _mixture(n, d, row_begin=0):
+    from mivs import ops
+
+    return ops.synth_mixture(n, d, SEED, n_centers=CENTERS, sigma=SIGMA, row_begin=row_begin, device=0)
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.int32)
+
+
+def _sample(n, m, seed):
+    return np.sort(np.random.default_rng(seed).choice(n, size=m, replace=False))
+
+
+def test_config0_bruteforce_10k_matches_sklearn_golden(mivs_lib):
+    from mivs.neighbors import brute_force
+
+    g = np.load(os.path.join(GOLD, "knn_synthetic_10k.npz"))
+    rng = np.random.default_rng(int(g["seed"]))
+    x = rng.standard_normal((int(g["n"]), int(g["d"]))).astype(np.float32)
+    q = rng.standard_normal((int(g["nq"]), int(g["d"]))).astype(np.float32)
+    bf = brute_force.build(torch.from_numpy(x).to("cuda:0"))
+    d, i = brute_force.search(bf, torch.from_numpy(q).to("cuda:0"), int(g["k"]))
+    np.testing.assert_array_equal(i.cpu().numpy(), g["ids"])
+    np.testing.assert_allclose(d.cpu().numpy(), g["sqdist"], rtol=1e-4)  # north_star: L2 within 1e-4
+    ed, ei = O.knn(x, q, int(g["k"]))
+    np.testing.assert_array_equal(_bits(d.cpu().numpy()), _bits(ed))
+    bf.close()
+
+
+def test_config1_bruteforce_1m_prefilter_equals_exact_and_oracle(mivs_lib):
+    from mivs.neighbors import brute_force
+
+    n, dim, nq, k = 1_000_000, 768, 10_000, 10
+    x = _mixture(n, dim)
+    q = _mixture(nq, dim, QUERY_ROW_BASE)
+    bf = brute_force.build(x)
+    d_pf, i_pf = brute_force.search(bf, q, k)
+    assert bf.last_search_stats()["prefilter"] == 1
+    bf.set_prefilter(False)
+    d_ex, i_ex = brute_force.search(bf, q, k)
+    np.testing.assert_array_equal(i_pf.cpu().numpy(), i_ex.cpu().numpy())
+    np.testing.assert_array_equal(_bits(d_pf.cpu().numpy()), _bits(d_ex.cpu().numpy()))
+    s = _sample(nq, 100, 1)
+    xh = x.cpu().numpy()
+    ed, ei = O.knn(xh, q.cpu().numpy()[s], k)
+    np.testing.assert_array_equal(i_pf.cpu().numpy()[s], ei)
+    np.testing.assert_array_equal(_bits(d_pf.cpu().numpy()[s]), _bits(ed))
+    bf.close()
+
+
+@pytest.fixture(scope="module")
+def ivf_10m():
+    """configs[2]: the bench's corpus, queries and index (cuVS defaults: 20 iterations, fraction 0.5)."""
+    import mivs
+    from mivs.neighbors import ivf_flat
+
+    mivs.load()
+    n, dim, nq = 10_000_000, 768, 10_000
+    x = _mixture(n, dim)
+    q = _mixture(nq, dim, QUERY_ROW_BASE)
+    idx = ivf_flat.build(ivf_flat.IndexParams(n_lists=1024), x)
+    yield x, q, idx
+    idx.close()
+    del x, q
+    torch.cuda.empty_cache()
+
+
+def test_config2_ivf_10m_prefilter_equals_exact_all_queries(ivf_10m):
+    from mivs.neighbors import ivf_flat
+
+    x, q, idx = ivf_10m
+    sp = ivf_flat.SearchParams(n_probes=32)
+    probes = torch.empty((q.shape[0], 32), dtype=torch.int32, device="cuda:0")
+    d_pf, i_pf = ivf_flat.search(sp, idx, q, 10, probes_out=probes)
+    st = idx.last_search_stats()
+    assert st["prefilter"] == 1 and st["n_queries"] == 10_000
+    idx.set_prefilter(False)
+    try:
+        d_ex, i_ex = ivf_flat.search(sp, idx, q, 10)
+        assert idx.last_search_stats()["prefilter"] == 0
+    finally:
+        idx.set_prefilter(True)
+    np.testing.assert_array_equal(i_pf.cpu().numpy(), i_ex.cpu().numpy())
+    np.testing.assert_array_equal(_bits(d_pf.cpu().numpy()), _bits(d_ex.cpu().numpy()))
+    # every query found 10 neighbours, ordered by (distance, id)
+    dd, ii = d_pf.cpu().numpy(), i_pf.cpu().numpy()
+    assert (ii >= 0).all() and (ii < x.shape[0]).all()
+    assert (np.diff(dd, axis=1) >= 0).all()
+
+
+def test_config2_ivf_10m_oracle_on_query_sample(ivf_10m):
+    from mivs.neighbors import ivf_flat
+
+    x, q, idx = ivf_10m
+    s = _sample(q.shape[0], 200, 2)
+    qs = q[torch.from_numpy(s).to("cuda:0")]
+    probes = torch.empty((len(s), 32), dtype=torch.int32, device="cuda:0")
+    d, i = ivf_flat.search(ivf_flat.SearchParams(n_probes=32), idx, qs, 10, probes_out=probes)
+    xh = x.cpu().numpy()
+    od, oi, op = O.ivf_search(xh, idx.centers.cpu().numpy(), idx.list_sizes.numpy(), idx.list_ids().cpu().numpy(),
+                              qs.cpu().numpy(), 32, 10)
+    np.testing.assert_array_equal(probes.cpu().numpy(), op)
+    np.testing.assert_array_equal(i.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(d.cpu().numpy()), _bits(od))
+
+
+def _labels_of(idx, n):
+    """row -> list from the index's list order (ids are row numbers: ids_offset 0)."""
+    sizes = idx.list_sizes.numpy()
+    ids = idx.list_ids().cpu().numpy()
+    lab = np.empty(n, np.int32)
+    lab[ids] = np.repeat(np.arange(len(sizes), dtype=np.int32), sizes)
+    return lab, sizes
+
+
+def test_config2_ivf_10m_build_labels_fp16_assign_equal_fp32_and_oracle(ivf_10m):
+    from mivs.neighbors import ivf_flat
+
+    x, q, idx = ivf_10m
+    n = x.shape[0]
+    lab_pf, sizes_pf = _labels_of(idx, n)
+    cents = idx.centers.cpu().numpy()
+    old = os.environ.get("MIVS_PF_ASSIGN")
+    os.environ["MIVS_PF_ASSIGN"] = "0"
+    try:
+        idx32 = ivf_flat.build(ivf_flat.IndexParams(n_lists=1024, prefilter=False), x)
+    finally:
+        if old is None:
+            os.environ.pop("MIVS_PF_ASSIGN")
+        else:
+            os.environ["MIVS_PF_ASSIGN"] = old
+    lab_32, sizes_32 = _labels_of(idx32, n)
+    np.testing.assert_array_equal(_bits(idx32.centers.cpu().numpy()), _bits(cents))
+    np.testing.assert_array_equal(sizes_32, sizes_pf)
+    np.testing.assert_array_equal(lab_32, lab_pf)
+    idx32.close()
+    torch.cuda.empty_cache()
+    rows = _sample(n, 100_000, 3)
+    xs = x[torch.from_numpy(rows).to("cuda:0")].cpu().numpy()
+    np.testing.assert_array_equal(O.kmeans_assign(xs, cents), lab_pf[rows])
+
+
+def test_config4_share_ivf_pq_12m5_fp16_oracle_on_query_sample(mivs_lib):
+    """Per-GPU share of configs[4]: 100M x 768 fp16 over 8 GPUs = 12.5M rows, n_lists 4096,
+    pq_dim 96 / pq_bits 8 (improved_multi_gpu_rag.py:131-137)."""
+    from mivs.neighbors import ivf_pq
+
+    n, dim = 12_500_000, 768
+    xh16 = _mixture(n, dim).half()
+    torch.cuda.empty_cache()
+    q = _mixture(64, dim, QUERY_ROW_BASE)
+    idx = ivf_pq.build(ivf_pq.IndexParams(n_lists=4096, pq_dim=96, pq_bits=8), xh16)
+    d, i = ivf_pq.search(ivf_pq.SearchParams(n_probes=32), idx, q, 10)
+    cents = idx.centers.cpu().numpy()
+    books = idx.pq_centers.cpu().numpy()
+    codes = idx.codes().cpu().numpy()
+    sizes = idx.list_sizes.numpy()
+    ids = idx.list_ids().cpu().numpy()
+    assert sizes.sum() == n and (np.sort(ids) == np.arange(n)).all()
+    od, oi, _ = O.ivfpq_search(cents, books, sizes, ids, codes, q.cpu().numpy(), 32, 10)
+    np.testing.assert_array_equal(i.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(d.cpu().numpy()), _bits(od))
+    idx.close()
