@@ -60,9 +60,12 @@ def parse():
     ap.add_argument("--centers", type=int, default=65536, help="mixture centres of the synthetic corpus")
     ap.add_argument("--sigma", type=float, default=0.75)
     ap.add_argument("--gt-queries", type=int, default=2000, help="queries with exact ground truth for recall")
-    ap.add_argument("--sweep", default="", help="comma list of n_probes to sweep (QPS + recall each)")
+    ap.add_argument("--sweep", default="8,16,32,64", help="comma list of n_probes to sweep (QPS + recall each); "
+                                                           "'' to skip")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--flat-rows", type=int, default=1_000_000,
+                    help="BASELINE configs[1] side line: brute force over this many rows (0: skip)")
     ap.add_argument("--json-out", default="")
     return ap.parse_args()
 
@@ -106,12 +109,54 @@ def load_traffic(cfg_key: str):
     return None, None
 
 
+def host_cpu_info() -> dict:
+    """What the CPU baseline ran on: model, logical / physical cores and NUMA nodes of the node (lscpu),
+    the cores this process may run on (sched_getaffinity) and the share the job is given (OMP_NUM_THREADS,
+    set per GPU by the harness)."""
+    info = {"logical_cpus": os.cpu_count()}
+    try:
+        aff = sorted(os.sched_getaffinity(0))
+        info["affinity_cpus"] = len(aff)
+    except AttributeError:
+        aff = []
+    try:
+        import subprocess
+
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        kv = {}
+        for ln in out.splitlines():
+            if ":" in ln:
+                a_, b_ = ln.split(":", 1)
+                kv[a_.strip()] = b_.strip()
+        info["model"] = kv.get("Model name")
+        sockets = int(kv.get("Socket(s)", "0") or 0)
+        cores = int(kv.get("Core(s) per socket", "0") or 0)
+        info["physical_cores"] = sockets * cores if sockets and cores else None
+        info["threads_per_core"] = int(kv.get("Thread(s) per core", "0") or 0) or None
+        info["numa_nodes"] = int(kv.get("NUMA node(s)", "0") or 0) or None
+    except Exception as e:  # lscpu missing: the counts above still stand
+        info["lscpu_error"] = repr(e)
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    info["omp_num_threads"] = omp or None
+    return info
+
+
+def cpu_threads() -> int:
+    """Every core this process may use, within the job's share (OMP_NUM_THREADS when the harness sets it)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n, omp) if omp else n)
+
+
 def cpu_baseline(idx, q_host, gt, n_probes, k, target_s, rank_log):
     """FAISS-algorithm IVF-Flat search (oracle/cpu_baseline.c, OpenMP over queries) on this host."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # bench.py's cpu_baseline leg is one of the oracle's allowed users
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads = cpu_threads()
     O.fast_set_threads(threads)
     rank_log(f"[cpu] copying index to host ({idx.size} rows) ...")
     rows = idx.list_rows().cpu().numpy()
@@ -130,11 +175,62 @@ def cpu_baseline(idx, q_host, gt, n_probes, k, target_s, rank_log):
     nr = min(ns, gt.shape[0])
     rec = recall_at_k(ci[:nr], gt[:nr]) if nr > 0 else None
     del rows
-    return {"value": ns / dt, "unit": "QPS", "cores": threads, "kind": "port",
+    return {"value": ns / dt, "unit": "QPS", "cores": threads, "kind": "port", "host": host_cpu_info(),
             "sample": f"{ns} of the {q_host.shape[0]} benchmark queries, same index (copied to host), n_probes="
                       f"{n_probes}, k={k}; FAISS IndexIVFFlat search algorithm restated in oracle/cpu_baseline.c "
                       f"(faiss not installed); {dt:.1f} s",
             "recall_at_10": rec}
+
+
+def flat_side_line(a, q, k, rl):
+    """BASELINE configs[1]: exact k-NN over a 1M x 768 fp32 corpus of the same mixture on the GPU (the
+    fp16 pre-filter + exact refine path, k <= 16), next to the FAISS IndexFlatL2 algorithm on this host's
+    cores (oracle/cpu_baseline.c orc_fast_knn) on a bounded query sample."""
+    from mivs import ops
+    from mivs.neighbors import brute_force
+
+    n = a.flat_rows
+    xf = ops.synth_mixture(n, a.dim, SEED + 7, n_centers=a.centers, sigma=a.sigma, device=torch.cuda.current_device())
+    bf = brute_force.build(xf)
+    brute_force.search(bf, q, k)
+    torch.cuda.synchronize()
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fd, fi = brute_force.search(bf, q, k)
+    torch.cuda.synchronize()
+    t_gpu = (time.perf_counter() - t0) / reps
+    gpu_qps = q.shape[0] / t_gpu
+    rl(f"[flat] {n} x {a.dim} brute force, k={k}: {gpu_qps:,.0f} QPS on the GPU")
+    line = {"rows": n, "dim": a.dim, "k": k, "queries": q.shape[0], "gpu_qps": round(gpu_qps, 1),
+            "gpu_ms_per_batch": round(t_gpu * 1e3, 3), "gpu_path": "fp16 pre-filter (K10) + exact fp32 refine (K11)"}
+    if not a.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O  # the cpu_baseline leg (an allowed oracle user)
+
+        threads = cpu_threads()
+        O.fast_set_threads(threads)
+        xh = xf.cpu().numpy()
+        qh = q[:512].cpu().numpy()
+        O.fast_knn(xh, qh[:4], k)
+        t0 = time.perf_counter()
+        O.fast_knn(xh, qh[:16], k)
+        per_q = (time.perf_counter() - t0) / 16
+        ns = int(max(16, min(qh.shape[0], 6.0 / max(per_q, 1e-9))))
+        t0 = time.perf_counter()
+        _, ci = O.fast_knn(xh, qh[:ns], k)
+        dt = time.perf_counter() - t0
+        agree = float(np.mean(ci == fi[:ns].cpu().numpy()))
+        line["cpu_baseline"] = {"value": round(ns / dt, 2), "unit": "QPS", "cores": threads, "kind": "port",
+                                "sample": f"{ns} queries, FAISS IndexFlatL2 algorithm (oracle/cpu_baseline.c); {dt:.1f} s",
+                                "ids_equal_to_gpu_frac": round(agree, 4)}
+        line["gpu_over_cpu"] = round(gpu_qps / (ns / dt), 1)
+        rl(f"[flat] CPU {ns / dt:.1f} QPS on {threads} threads")
+        del xh
+    bf.close()
+    del xf
+    torch.cuda.empty_cache()
+    return line
 
 
 def main():
@@ -283,11 +379,11 @@ def main():
     tflops = flops / (scan_ms * 1e-3) / 1e12
     gbs = bytes_alg / (scan_ms * 1e-3) / 1e9
     metric_tag = "L2"
-    if pf:
-        kname = f"mivs::k_pf_scan<{metric_tag}>"
-    else:
-        kname = (f"mivs::k_scan_wide<{stats['kcap']},{metric_tag}>" if stats["query_tile"] == 64
-                 else f"mivs::k_scan<{stats['kcap']},{metric_tag}>")
+    kname = {13: f"mivs::k_rs_scan<{metric_tag}> (K13 row-stationary fp16 pre-filter)",
+             10: f"mivs::k_pf_scan<{metric_tag}> (K10 fp16 pre-filter)",
+             12: f"mivs::k_pf_scan_r<{metric_tag}> (K12)",
+             31: f"mivs::k_scan_wide<{stats['kcap']},{metric_tag}> (K3w exact fp32)",
+             3: f"mivs::k_scan<{stats['kcap']},{metric_tag}> (K3 exact fp32)"}.get(stats.get("scan_kernel"), "?")
     peak_mfma = PEAK_F16_MFMA_TFS if pf else PEAK_F32_MFMA_TFS
     cfg_key = f"ivf_flat_n{n}_d{d}_q{Q}_l{a.n_lists}_p{a.n_probes}_k{k}_t{stats['query_tile']}" + ("_pf" if pf else "")
     traffic, traffic_src = load_traffic(cfg_key)
@@ -321,6 +417,13 @@ def main():
         except Exception as e:  # the GPU result stands without the CPU column
             rl(f"[cpu] baseline failed: {e!r}")
 
+    flat = None
+    if rank == 0 and world == 1 and a.flat_rows > 0:
+        try:
+            flat = flat_side_line(a, q, k, rl)
+        except Exception as e:  # the IVF line stands without it
+            rl(f"[flat] side line failed: {e!r}")
+
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -351,6 +454,7 @@ def main():
         "cpu_baseline": cpu,
         "search_stats": stats,
         "n_probes_sweep": sweep,
+        "flat_bruteforce_1m": flat,
     }
     if rank == 0:
         line = json.dumps(out)

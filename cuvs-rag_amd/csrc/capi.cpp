@@ -86,6 +86,10 @@ struct Workspace {
       counts, fill, qp_slots, scan_tmp, gmerge;
   // fp16 pre-filter path (K10 / K11) and its exact-scan fallback
   Buf qh, qscale, qres, qtheta, pf_key, pf_pos, pf_bound, pf_stats, ovf_q, ovf_rows, ovf_d, ovf_i;
+  // K13 row-stationary scan: the full probe list, the pre-pass result, per-query headers and candidates
+  Buf probes_full, pre_d, pre_i, qhdr, cand_cnt, cand_key, cand_pos, slot_iota, rs_tiles;
+  // per-list query counts of the last search's own probe map (an exact fallback re-maps its queries)
+  Buf stat_counts, rs_ovf_q, rs_ovf_rows, rs_ovf_d, rs_ovf_i, rs_items;
 };
 
 // hipEvent pairs recorded on the caller's stream around the pipeline stages of
@@ -139,6 +143,7 @@ struct mivs_index_s {
   int64_t last_nq = 0;
   int last_np = 0, last_k = 0, last_qtile = kQTile;
   int last_pf = 0;
+  int last_scan = 0;  // fine-scan kernel of the last search: 3 K3, 31 K3w, 10 K10, 12 K12, 13 K13
   int64_t last_ovf = 0, last_window = 0;
 };
 
@@ -645,9 +650,15 @@ bool pr_use(const mivs_index_s* idx) {
 }
 
 void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
-                      int64_t* out_i, int32_t* out_probes, bool allow_pf = true, bool prof = true);
+                      int64_t* out_i, int32_t* out_probes, bool allow_pf = true, bool prof = true,
+                      bool allow_rs = true);
 void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
-                       int64_t* out_i, bool pf, ProfRec* pr, bool prof);
+                       int64_t* out_i, bool pf, ProfRec* pr, bool prof, const int64_t* probes = nullptr,
+                       bool allow_rs = true);
+
+void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
+                        int64_t* out_i, const float* slot_key, const int* slot_pos, const float* slot_bound,
+                        const int* slot_cnt, const int64_t* slot_begin, int slot_k, bool fallback_pf = false);
 
 // K10 scan + K11 refine for a probe map built with (kPfChunkGroups, kPfQTile); queries the refine
 // could not prove are re-run through the exact scan and scattered back.
@@ -734,14 +745,27 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
               "barrier %.3f merge %.3f | epilogues %llu slow %.4f\n", w, hp[8] ? (double)hp[7] / hp[8] * 0.1 : 0.0,
               hp[0] / w, hp[1] / w, hp[2] / w, hp[3] / w, hp[4] / w, hp[5], hp[5] ? (double)hp[6] / hp[5] : 0.0);
   }
+  pf_refine_fallback(idx, s, q, nq, k, np, out_d, out_i, ws.pf_key.as<float>(), ws.pf_pos.as<int>(),
+                     ws.pf_bound.as<float>(), nullptr, ws.slot_begin.as<int64_t>(), slot_k);
+}
+
+// K11 over the scan's candidate slots, then the exact scan for the queries the refine could not prove
+// (scattered back into out_d / out_i). slot_cnt: K13's per-query candidate counts (slot_bound unused).
+void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
+                        int64_t* out_i, const float* slot_key, const int* slot_pos, const float* slot_bound,
+                        const int* slot_cnt, const int64_t* slot_begin, int slot_k, bool fallback_pf) {
+  Workspace& ws = idx->ws;
+  const ListSet& L = idx->lists;
+  const int dp = idx->dp;
   ws.pf_stats.reserve(32);
   HIPCHK(hipMemsetAsync(ws.pf_stats.p, 0, 32, s));
   ws.ovf_q.reserve(sizeof(int64_t) * nq);
   PfRefineArgs r{};
-  r.slot_key = ws.pf_key.as<float>();
-  r.slot_pos = ws.pf_pos.as<int>();
-  r.slot_bound = ws.pf_bound.as<float>();
-  r.slot_begin = ws.slot_begin.as<int64_t>();
+  r.slot_key = slot_key;
+  r.slot_pos = slot_pos;
+  r.slot_bound = slot_bound;
+  r.slot_cnt = slot_cnt;
+  r.slot_begin = slot_begin;
   r.slot_k = slot_k;
   r.nq = nq;
   r.k = k;
@@ -768,6 +792,21 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   const int64_t novf = (int64_t)(int32_t)(h[0] & 0xFFFFFFFF);
   idx->last_ovf += novf;
   idx->last_window += h[1];
+  if (novf > 0 && fallback_pf) {
+    // K13's unproven queries go through K10 (whose own unproven ones go to the exact scan): own buffers,
+    // since the nested search uses the ovf_* ones
+    ws.rs_ovf_q.reserve(sizeof(int64_t) * (size_t)novf);
+    ws.rs_ovf_rows.reserve(sizeof(float) * (size_t)novf * idx->d);
+    ws.rs_ovf_d.reserve(sizeof(float) * (size_t)novf * k);
+    ws.rs_ovf_i.reserve(sizeof(int64_t) * (size_t)novf * k);
+    HIPCHK(hipMemcpyAsync(ws.rs_ovf_q.p, ws.ovf_q.p, sizeof(int64_t) * novf, hipMemcpyDeviceToDevice, s));
+    HIPCHK(launch_gather_rows(q, idx->d, ws.rs_ovf_q.as<int64_t>(), novf, ws.rs_ovf_rows.as<float>(), s));
+    ivf_search_batch(idx, s, ws.rs_ovf_rows.as<float>(), novf, k, np, ws.rs_ovf_d.as<float>(),
+                     ws.rs_ovf_i.as<int64_t>(), nullptr, true, false, false);
+    HIPCHK(launch_scatter_results(ws.rs_ovf_d.as<float>(), ws.rs_ovf_i.as<int64_t>(), ws.rs_ovf_q.as<int64_t>(), novf,
+                                  k, out_d, out_i, s));
+    return;
+  }
   if (novf > 0) {
     ws.ovf_rows.reserve(sizeof(float) * (size_t)novf * idx->d);
     ws.ovf_d.reserve(sizeof(float) * (size_t)novf * k);
@@ -788,7 +827,7 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
 }
 
 void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
-                      int64_t* out_i, int32_t* out_probes, bool allow_pf, bool prof) {
+                      int64_t* out_i, int32_t* out_probes, bool allow_pf, bool prof, bool allow_rs) {
   Workspace& ws = idx->ws;
   ProfRec* pr = prof && g_profiling.load() ? idx->prof.begin(s) : nullptr;
   const bool pf = allow_pf && idx->groups_h.p != nullptr && k <= kPfMaxK;
@@ -800,14 +839,109 @@ void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t 
   single_list_topk(idx->cents, idx->G, q, ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, np, idx->metric,
                    ws.probes_d.as<float>(), ws.probes_i.as<int64_t>(), idx->device, ws, s);
   if (out_probes) HIPCHK(launch_i64_to_i32(ws.probes_i.as<int64_t>(), nq * np, out_probes, s));
-  ivf_search_probed(idx, s, q, nq, k, np, out_d, out_i, pf, pr, prof);
+  ivf_search_probed(idx, s, q, nq, k, np, out_d, out_i, pf, pr, prof, nullptr, allow_rs);
 }
 
 // the fine part of a search whose probes are in ws.probes_i ([nq][np]) and query norms in ws.qn:
 // probe map, then the pre-filter scan + refine (pf) or the exact scan + merge / select
-void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
-                       int64_t* out_i, bool pf, ProfRec* pr, bool prof) {
+// K13 serves the fp16 pre-filter search of an IVF index probed by >= 2 lists per query (its bound T_q
+// comes from a pre-pass over each query's nearest list); MIVS_PF_ROWSTAT=0 keeps K10 (A/B runs)
+bool rs_use(const mivs_index_s* idx, int np) {
+  const char* e = getenv("MIVS_PF_ROWSTAT");
+  return idx->kind == 0 && np >= 2 && rs_scan_supported(idx->dp) && !(e && e[0] == '0');
+}
+
+// The K13 search of queries whose probes are in ws.probes_i and norms in ws.qn:
+//   1. pre-pass: each query's nearest list through K10 + K11 -> the exact k-th key there;
+//   2. per-query header {qs, uf, qn, T_q}, T_q >= the final refine window;
+//   3. probe map in (list, 8-group block) items, one query tile column per list;
+//   4. K13 appends every (approximate key <= T_q, row) to the query's candidate buffer;
+//   5. K11 over the buffers + the exact fallback.
+void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
+               int64_t* out_i, ProfRec* pr) {
   Workspace& ws = idx->ws;
+  const ListSet& L = idx->lists;
+  const int dp = idx->dp;
+  const int64_t ne = nq * np;
+  ws.probes_full.reserve(sizeof(int64_t) * ne);
+  HIPCHK(hipMemcpyAsync(ws.probes_full.p, ws.probes_i.p, sizeof(int64_t) * ne, hipMemcpyDeviceToDevice, s));
+  // 1. the nearest list of every query (probe 0): an n_probes = 1 search through K10 / K11
+  ws.pre_d.reserve(sizeof(float) * nq * k);
+  ws.pre_i.reserve(sizeof(int64_t) * nq * k);
+  HIPCHK(hipMemcpy2DAsync(ws.probes_i.p, sizeof(int64_t), ws.probes_full.p, sizeof(int64_t) * np, sizeof(int64_t), nq,
+                          hipMemcpyDeviceToDevice, s));
+  const int64_t keep_ovf = idx->last_ovf, keep_window = idx->last_window;  // stats count the main pass only
+  ivf_search_probed(idx, s, q, nq, k, 1, ws.pre_d.as<float>(), ws.pre_i.as<int64_t>(), true, nullptr, false,
+                    ws.probes_i.as<int64_t>(), false);
+  idx->last_ovf = keep_ovf;
+  idx->last_window = keep_window;
+  // the pre-pass's own exact fallback may have reused the norm / fp16 query buffers for its rows
+  HIPCHK(launch_row_norms(q, nq, idx->d, ws.qn.as<float>(), s));
+  HIPCHK(launch_queries_to_half(q, nq, idx->d, dp, idx->hx_exp, ws.qh.as<uint16_t>(), ws.qscale.as<float>(),
+                                ws.qres.as<float>(), s));
+  // 2. headers
+  ws.qhdr.reserve(sizeof(float4) * (nq + 1));
+  HIPCHK(launch_rs_headers(ws.pre_d.as<float>(), ws.pre_i.as<int64_t>(), nq, k, ws.qscale.as<float>(),
+                           ws.qn.as<float>(), ws.qres.as<float>(), idx->x_norm_max, idx->x_res_max, dp, idx->metric,
+                           ws.qhdr.as<float4>(), s));
+  // 3. probe map: items = (list, block of kRsBlockGroups groups); every query of a list in one tile column
+  const size_t stb = scan_tmp_bytes(ne) + sizeof(int64_t) * (size_t)ne;
+  ws.scan_tmp.reserve(stb);
+  HIPCHK(launch_probe_map(ws.probes_full.as<int64_t>(), nq, np, L.n_lists, L.goff.as<int64_t>(), kRsBlockGroups,
+                          1 << 30, ws.counts.as<int>(), ws.fill.as<int>(), ws.bucket_off.as<int>(),
+                          ws.work_off.as<int>(), ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(),
+                          ws.qp_slots.as<int64_t>(), ws.slot_begin.as<int64_t>(), ws.scan_tmp.p, stb, s));
+  {  // (cheap: n_lists ints)
+    ws.stat_counts.reserve(sizeof(int) * L.n_lists);
+    HIPCHK(hipMemcpyAsync(ws.stat_counts.p, ws.counts.p, sizeof(int) * L.n_lists, hipMemcpyDeviceToDevice, s));
+  }
+  // the query tiles in the LDS image layout (one contiguous 1 KiB per DMA wave-instruction)
+  ws.rs_tiles.reserve((size_t)rs_tiles_bytes(ne, L.n_lists, dp));
+  HIPCHK(launch_rs_tiles(ws.bucket_q.as<int64_t>(), ws.bucket_off.as<int>(), L.n_lists, ws.qh.as<uint16_t>(),
+                         ws.qhdr.as<float4>(), (int)nq, dp, ws.rs_tiles.as<char>(), s));
+  // 4. K13
+  ws.cand_cnt.reserve(sizeof(int) * nq);
+  ws.cand_key.reserve(sizeof(float) * (size_t)nq * kRsCap);
+  ws.cand_pos.reserve(sizeof(int) * (size_t)nq * kRsCap);
+  HIPCHK(hipMemsetAsync(ws.cand_cnt.p, 0, sizeof(int) * nq, s));
+  int64_t max_items = 0;  // every list probed: the item table's bound (the probe map decides the count)
+  for (int l = 0; l < L.n_lists; ++l) max_items += ceil_div(L.h_goff[l + 1] - L.h_goff[l], kRsBlockGroups);
+  ws.rs_items.reserve(sizeof(int4) * (size_t)std::max<int64_t>(max_items, 1));
+  HIPCHK(launch_rs_items(ws.work_off.as<int>(), ws.bucket_off.as<int>(), L.goff.as<int64_t>(), L.n_lists,
+                         (int)max_items, ws.rs_items.as<int4>(), s));
+  RsScanArgs a{};
+  a.groups_h = idx->groups_h.as<uint16_t>();
+  a.row_norms = L.norms.as<float>();
+  a.list_goff = L.goff.as<int64_t>();
+  a.n_lists = L.n_lists;
+  a.bucket_q = ws.bucket_q.as<int64_t>();
+  a.bucket_off = ws.bucket_off.as<int>();
+  a.work_off = ws.work_off.as<int>();
+  a.items = ws.rs_items.as<int4>();
+  a.tiles = ws.rs_tiles.as<char>();
+  a.qnorms = ws.qn.as<float>();
+  a.nq = (int)nq;
+  a.metric = idx->metric;
+  a.cap = kRsCap;
+  a.cand_cnt = ws.cand_cnt.as<int>();
+  a.cand_key = ws.cand_key.as<float>();
+  a.cand_pos = ws.cand_pos.as<int>();
+  a.flags = getenv("MIVS_RS_FLAGS") ? atoi(getenv("MIVS_RS_FLAGS")) : 0;
+  if (a.flags & 2) a.flags |= 1;  // stale LDS tiles: never run an epilogue on them
+  if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
+  HIPCHK(launch_rs_scan(a, dp, std::max(8, cu_count(idx->device) / 8 * 8), s));
+  if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
+  // 5. exact ranking of the candidates (one slot per query)
+  ws.slot_iota.reserve(sizeof(int64_t) * (nq + 1));
+  HIPCHK(launch_iota_i64(ws.slot_iota.as<int64_t>(), nq + 1, 0, 1, s));
+  pf_refine_fallback(idx, s, q, nq, k, np, out_d, out_i, ws.cand_key.as<float>(), ws.cand_pos.as<int>(), nullptr,
+                     ws.cand_cnt.as<int>(), ws.slot_iota.as<int64_t>(), kRsCap, true);
+}
+
+void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
+                       int64_t* out_i, bool pf, ProfRec* pr, bool prof, const int64_t* probes, bool allow_rs) {
+  Workspace& ws = idx->ws;
+  if (!probes) probes = ws.probes_i.as<int64_t>();
   // probe map
   const ListSet& L = idx->lists;
   const int64_t ne = nq * np;
@@ -828,7 +962,17 @@ void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t
     idx->last_qtile = qtile;
     idx->last_pf = pf ? 1 : 0;
   }
-  HIPCHK(launch_probe_map(ws.probes_i.as<int64_t>(), nq, np, L.n_lists, L.goff.as<int64_t>(),
+  if (pf && allow_rs && rs_use(idx, np)) {
+    if (prof) {
+      idx->last_qtile = kRsQTile;
+      idx->last_scan = 13;
+    }
+    rs_search(idx, s, q, nq, k, np, out_d, out_i, pr);
+    if (pr) HIPCHK(hipEventRecord(pr->e[3], s));
+    return;
+  }
+  if (prof) idx->last_scan = pf ? (use_r ? 12 : 10) : (qtile == 64 ? 31 : 3);
+  HIPCHK(launch_probe_map(probes, nq, np, L.n_lists, L.goff.as<int64_t>(),
                           pf ? (use_r ? idx->pr_G : idx->pf_G) : idx->G, qtile, ws.counts.as<int>(), ws.fill.as<int>(),
                           ws.bucket_off.as<int>(), ws.work_off.as<int>(), ws.bucket_q.as<int64_t>(),
                           ws.bucket_slot.as<int64_t>(), ws.qp_slots.as<int64_t>(), ws.slot_begin.as<int64_t>(),
@@ -1277,7 +1421,8 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
   return guarded([&] {
     require(idx != nullptr && idx->kind == 2, "not an ivf_pq index");
     require(nq >= 0, "nq must be >= 0");
-    require(k >= 1 && k <= 32, "ivf_pq: k must be in [1, 32] in this build", MIVS_ERR_UNSUPPORTED);
+    require(k >= 1 && k <= kMaxK, "ivf_pq: k must be in [1, " + std::to_string(kMaxK) + "] in this build",
+            MIVS_ERR_UNSUPPORTED);
     require(n_probes >= 1, "n_probes must be >= 1");
     require(nq == 0 || (d_q && d_dist && d_ids), "NULL query/output pointer");
     if (nq == 0) return;
@@ -1289,7 +1434,9 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
     require(np == n_probes || d_probes == nullptr, "n_probes > n_lists with a probes output");
     const int kcap = scan_kcap(k);
     require(pq_tile_lds_bytes(idx->rot_dim_pad, idx->pq_len) <= 160 * 1024 ||
-                pq_scan_lds_bytes(idx->rot_dim_pad, idx->pq_dim, kcap) <= 160 * 1024,
+                pq_scan_lds_bytes(idx->rot_dim_pad, idx->pq_dim, kcap) <= 160 * 1024 ||
+                pq_split_lds_bytes(idx->rot_dim_pad, (int)ceil_div(ceil_div(idx->pq_dim, 2), 16) * 16, kcap) <=
+                    160 * 1024,
             "ivf_pq: the LUT scan does not fit the 160 KB LDS for this pq_dim / pq_len", MIVS_ERR_UNSUPPORTED);
     Workspace& ws = idx->ws;
     ProfRec* pr = g_profiling.load() ? idx->prof.begin(s) : nullptr;
@@ -1302,8 +1449,15 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
     if (d_probes) HIPCHK(launch_i64_to_i32(ws.probes_i.as<int64_t>(), nq * np, d_probes, s));
     const ListSet& L = idx->lists;
     const char* tiled_env = getenv("MIVS_PQ_TILED");
+    // K9s (two LUT halves) applies when pq_len is a multiple of 4 up to 16 and each half has <= 64
+    // subspaces; K9 needs the whole LUT plus its merge area in LDS; K9b otherwise
+    const int pq_half = (int)ceil_div(ceil_div(idx->pq_dim, 2), 16) * 16;
+    const bool split_ok = (idx->pq_len & 3) == 0 && idx->pq_len <= 16 && pq_half <= 64 &&
+                          pq_split_lds_bytes(idx->rot_dim_pad, pq_half, kcap) <= 160 * 1024;
     const bool tiled = (tiled_env && tiled_env[0] == '1') ||
-                       pq_scan_lds_bytes(idx->rot_dim_pad, idx->pq_dim, kcap) > 160 * 1024;
+                       (!split_ok && pq_scan_lds_bytes(idx->rot_dim_pad, idx->pq_dim, kcap) > 160 * 1024);
+    require(!tiled || kcap <= 32, "ivf_pq: k > 32 needs the whole-LUT scan (K9/K9s), which does not fit this "
+            "pq_dim in LDS", MIVS_ERR_UNSUPPORTED);
     if (tiled && pq_tile_lds_bytes(idx->rot_dim_pad, idx->pq_len) <= 160 * 1024) {
       // K9b (used when K9's whole-LUT LDS does not fit, or MIVS_PQ_TILED=1): probe map
       // (list -> 16-query tiles x 512-row chunks), tiled scan, K7 merge of the slots
@@ -1568,20 +1722,37 @@ int32_t mivs_index_last_search_stats(mivs_index_t idx, mivs_search_stats* out) {
     st.query_tile = idx->last_qtile;
     st.kcap = idx->last_k > 0 ? scan_kcap(idx->last_k) : 0;
     st.prefilter = idx->last_pf;
+    st.scan_kernel = idx->last_scan;
     st.overflow_queries = idx->last_ovf;
     st.window_candidates = idx->last_window;
     const ListSet& L = idx->lists;
     if (idx->last_nq > 0 && idx->kind == 0) {
       HIPCHK(hipDeviceSynchronize());
       std::vector<int> counts(L.n_lists), woff(L.n_lists + 1);
-      HIPCHK(hipMemcpy(counts.data(), idx->ws.counts.p, sizeof(int) * L.n_lists, hipMemcpyDeviceToHost));
+      // K13: its own probe map's counts (the exact fallback of unproven queries maps only those)
+      const Buf& cb = idx->last_scan == 13 ? idx->ws.stat_counts : idx->ws.counts;
+      HIPCHK(hipMemcpy(counts.data(), cb.p, sizeof(int) * L.n_lists, hipMemcpyDeviceToHost));
       HIPCHK(hipMemcpy(woff.data(), idx->ws.work_off.p, sizeof(int) * (L.n_lists + 1), hipMemcpyDeviceToHost));
       for (int l = 0; l < L.n_lists; ++l) {
         st.scanned_rows += (int64_t)counts[l] * (L.h_off[l + 1] - L.h_off[l]);
-        st.streamed_groups += ceil_div(counts[l], idx->last_qtile) * (L.h_goff[l + 1] - L.h_goff[l]);
+        // K13 streams every probed row once (the query tiles move, the rows stay in registers)
+        st.streamed_groups += (idx->last_scan == 13 ? (counts[l] > 0 ? 1 : 0) : ceil_div(counts[l], idx->last_qtile)) *
+                              (L.h_goff[l + 1] - L.h_goff[l]);
         if (counts[l] > 0) st.unique_groups += L.h_goff[l + 1] - L.h_goff[l];
       }
       st.work_items = woff[L.n_lists];
+      if (idx->last_scan == 13) {
+        st.work_items = 0;
+        for (int l = 0; l < L.n_lists; ++l)
+          if (counts[l] > 0) st.work_items += ceil_div(L.h_goff[l + 1] - L.h_goff[l], kRsBlockGroups);
+        // the candidates K13 appended (some beyond a query's buffer when it overflowed)
+        std::vector<int> cc(idx->last_nq);
+        HIPCHK(hipMemcpy(cc.data(), idx->ws.cand_cnt.p, sizeof(int) * cc.size(), hipMemcpyDeviceToHost));
+        for (int v : cc) {
+          st.candidates += v;
+          st.cand_overflow += v > kRsCap ? 1 : 0;
+        }
+      }
     } else if (idx->last_nq > 0) {
       // brute force: the pre-filter scan (K10) works in pf_G-group chunks, the exact scans in G
       const int G = idx->last_pf ? idx->pf_G : idx->G;
@@ -1725,6 +1896,36 @@ int32_t mivs_merge_topk(int32_t device, void* stream, const float* d_in_dist, co
     a.out_d = d_out_dist;
     a.out_i = d_out_ids;
     HIPCHK(launch_merge(a, static_cast<hipStream_t>(stream)));
+  });
+}
+
+int32_t mivs_refine(int32_t device, void* stream, const void* d_data, int32_t data_is_half, int64_t n, int32_t dim,
+                    const float* d_queries, int64_t nq, const int64_t* d_candidates, int32_t n_candidates, int32_t k,
+                    int32_t metric, float* d_distances, int64_t* d_neighbors) {
+  return guarded([&] {
+    require(dim >= 1 && dim_pad(dim) <= 1024, "dim must be in [1, 1024]", MIVS_ERR_UNSUPPORTED);
+    require(n >= 0 && nq >= 0 && n_candidates >= 1, "bad shape");
+    require(k >= 1 && k <= kMaxK && k <= n_candidates,
+            "k must be in [1, min(n_candidates, " + std::to_string(kMaxK) + ")]", MIVS_ERR_UNSUPPORTED);
+    require(metric == MIVS_METRIC_L2 || metric == MIVS_METRIC_IP, "unknown metric");
+    if (nq == 0) return;
+    require(d_data && d_queries && d_candidates && d_distances && d_neighbors, "null pointer");
+    DeviceGuard dg(device);
+    RefineArgs a{};
+    a.data = d_data;
+    a.n = n;
+    a.d = dim;
+    a.dp = dim_pad(dim);
+    a.half = data_is_half ? 1 : 0;
+    a.queries = d_queries;
+    a.nq = nq;
+    a.cand = d_candidates;
+    a.n_cand = n_candidates;
+    a.k = k;
+    a.metric = metric;
+    a.out_d = d_distances;
+    a.out_i = d_neighbors;
+    HIPCHK(launch_refine(a, static_cast<hipStream_t>(stream)));
   });
 }
 

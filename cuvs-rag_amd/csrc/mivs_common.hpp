@@ -193,6 +193,49 @@ struct PfScanArgs {
   int chunk_stride;           // max chunks per list
 };
 
+// K13 row-stationary pre-filter scan (rsscan.hip): work item = (list, block of
+// kRsBlockGroups groups), one group per wave held in registers, the list's queries streamed past in
+// kRsQTile-query tiles; every (approximate key <= T_q, row) goes to the query's candidate buffer.
+constexpr int kRsWaves = 8;
+constexpr int kRsQTile = 32;
+constexpr int kRsBlockGroups = kRsWaves;
+constexpr int kRsCap = 512;  // candidate buffer entries per query (more: exact fallback)
+struct RsScanArgs {
+  const uint16_t* groups_h;  // fp16 lists, group layout [g][dp/8][32][8]
+  const float* row_norms;    // pinned fp32 norms (+inf on pad rows)
+  const int64_t* list_goff;
+  int n_lists;
+  const int64_t* bucket_q;   // probe map with chunk = kRsBlockGroups groups and one query tile per list
+  const int* bucket_off;
+  const int* work_off;
+  const int4* items;         // [items] {first group, end group, first tile slot, tiles} (k_rs_items)
+  const char* tiles;         // query tile images (k_rs_tiles): per list ceil(m/32) x [dp/16 + 1] x 1 KiB
+  const float* qnorms;       // [nq] pinned fp32 query norms (exact key of a candidate)
+  int nq;
+  int metric;
+  int cap;
+  int* cand_cnt;             // [nq] zeroed before launch
+  float* cand_key;           // [nq][cap]
+  int* cand_pos;             // [nq][cap]
+  int flags;                 // timing experiments only (MIVS_RS_FLAGS): 1 skip epilogue, 2 skip staging
+};
+
+// K14 exact re-ranking of candidates (refine.hip): cuvs.neighbors.refine
+struct RefineArgs {
+  const void* data;       // [n][d] fp32, or fp16 when half
+  int64_t n;
+  int d, dp;              // dp = the contract's padded dim (multiple of 64, <= 1024)
+  int half;
+  const float* queries;   // [nq][d]
+  int64_t nq;
+  const int64_t* cand;    // [nq][n_cand] row numbers of data (-1: none)
+  int n_cand;
+  const int64_t* id_map;  // optional: reported id of row r (default r)
+  int k, metric;
+  float* out_d;
+  int64_t* out_i;
+};
+
 struct PfRefineArgs {
   const float* slot_key;
   const int* slot_pos;
@@ -216,6 +259,8 @@ struct PfRefineArgs {
   const int64_t* qrows;       // optional: query q is row qrows[q] of queries / qnorms / qres (k-means trainset)
   int labels_only;            // k = 1: a window of ONE candidate is the answer without its exact key
                               // (out_d then holds its approximate key)
+  const int* slot_cnt;        // optional (K13): entries per slot, unsorted; > slot_k: overflow. slot_bound
+                              // may then be nullptr
 };
 
 hipError_t launch_pf_scan(const PfScanArgs& a, int grid, size_t lds, hipStream_t s);
@@ -230,6 +275,18 @@ constexpr int kPrChunkGroups = 256;  // default groups (8192 rows) per K12 work 
 bool pr_scan_supported(int dp);
 hipError_t launch_pr_scan(const PfScanArgs& a, int grid, hipStream_t s);
 hipError_t launch_pf_refine(const PfRefineArgs& a, hipStream_t s);
+hipError_t launch_refine(const RefineArgs& a, hipStream_t s);
+size_t rs_scan_lds_bytes(int dp);
+bool rs_scan_supported(int dp);
+hipError_t launch_rs_scan(const RsScanArgs& a, int dp, int grid, hipStream_t s);
+int64_t rs_tiles_bytes(int64_t ne, int n_lists, int dp);
+hipError_t launch_rs_items(const int* work_off, const int* bucket_off, const int64_t* list_goff, int n_lists,
+                           int max_items, int4* items, hipStream_t s);
+hipError_t launch_rs_tiles(const int64_t* bucket_q, const int* bucket_off, int n_lists, const uint16_t* qh,
+                           const float4* qhdr, int nq, int dp, char* tiles, hipStream_t s);
+hipError_t launch_rs_headers(const float* pre_d, const int64_t* pre_i, int64_t nq, int k, const float* qscale,
+                             const float* qnorms, const float* qres, float x_norm_max, float x_res_max, int dp,
+                             int metric, float4* hdr, hipStream_t s);
 hipError_t launch_gather_ids(const int64_t* src, const int64_t* idx, int64_t n, int64_t* out, hipStream_t s);
 constexpr unsigned kPfOrdInf = 0xFF800000u;  // order mapping of +inf (qtheta's initial value)
 // fp32 groups -> fp16 groups scaled by 2^hx_exp (FTZ below the fp16 normal range), per-index maxima of
@@ -317,6 +374,7 @@ hipError_t launch_pq_unpack(const uint8_t* codes, int64_t n, const int64_t* list
                             int n_lists, int pq_dim, int pq_dim_pad, uint8_t* out, hipStream_t s);
 hipError_t launch_pq_scan(const PqScanArgs& a, int kcap, hipStream_t s);
 // K9s (split LUT, three workgroups per CU); hipErrorNotSupported when its shape limits are not met
+size_t pq_split_lds_bytes(int rot_dim_pad, int pq_half, int kcap);
 hipError_t launch_pq_scan_split(const PqScanArgs& a, int kcap, hipStream_t s);
 size_t pq_tile_lds_bytes(int rot_dim_pad, int pq_len);
 hipError_t launch_pq_scan_tiled(const PqTileArgs& a, int kcap, int grid, hipStream_t s);

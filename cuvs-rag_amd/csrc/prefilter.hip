@@ -22,6 +22,7 @@
 #include <cstdlib>
 
 #include "mivs_common.hpp"
+#include "pf_math.hpp"
 
 namespace mivs {
 
@@ -78,64 +79,6 @@ __device__ __forceinline__ void pf_insert(float (&lk)[KL], int (&lp)[KL], float 
     lk[t] = shift ? prev : (place ? key : lk[t]);
     lp[t] = shift ? prevp : (place ? pos : lp[t]);
   }
-}
-
-// approximate key of one accumulator element: the dot is acc * 2^-(row exp + query exp), exact
-template <int METRIC>
-__device__ __forceinline__ float pf_key(float acc, float qs, float xn, float qn) {
-  const float v = acc * qs;
-  if (METRIC == kL2) {
-    const float t = fmaf(-2.0f, v, xn + qn);
-    return t > 0.0f ? t : 0.0f;
-  }
-  return xn < INFINITY ? -v : INFINITY;
-}
-
-// delta >= |approximate key - pinned fp32 key| for every (row, query q) of the index:
-//   |x.q - x_h.q_h| <= |x_h||q - q_h| + |x - x_h||q|   (Cauchy-Schwarz on the fp16 rounding residuals)
-//   + 2 dp u |x_h||q_h|  (the fp16-product sum inside the MFMA, any order and rounding)
-//   + 1.01 dp u |x||q|   (the pinned fp32 fma chain);  L2 keys: x2, plus the roundings of the key itself.
-// Index-wide maxima of |x| and |x - x_h| stand in for the row's own values.
-template <int METRIC>
-__device__ __forceinline__ float pf_delta(float qn, float qres, float x_norm_max, float x_res_max, int dp) {
-  const float nq = sqrtf(qn) * (1.0f + 0x1p-12f);
-  const float nx = x_norm_max, rx = x_res_max;
-  const float nxh = nx + rx, nqh = nq + qres;
-  const float ga = 2.0f * (float)dp * 0x1p-24f;
-  const float gp = 1.01f * (float)dp * 0x1p-24f;
-  const float dd = nxh * qres + rx * nq + ga * nxh * nqh + gp * nx * nq;
-  const float delta = METRIC == kL2 ? 2.0f * dd + 4.0f * 0x1p-24f * (nx * nx + qn) : dd;
-  return delta * (1.0f + 0x1p-10f) + 1e-30f;
-}
-
-// order-preserving float <-> uint32 (atomicMin over signed keys)
-__device__ __forceinline__ unsigned pf_ord(float x) {
-  const unsigned b = __float_as_uint(x);
-  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
-}
-__device__ __forceinline__ float pf_unord(unsigned u) {
-  return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
-}
-
-// the refine window above a k-th approximate key kth: every candidate whose pinned key can reach the
-// top-k has approximate key <= pf_window(Ak). Monotone in kth, so any kth' >= Ak gives a window >= it.
-__device__ __forceinline__ float pf_window(float kth, float delta) {
-  return kth + 2.0f * delta + fabsf(kth) * 0x1p-20f;
-}
-
-// the epilogue's fast filter. The exact test keeps key < lk_last && key <= th, i.e. key < U with
-// U = min(lk_last, next float above th). The filter value of an accumulator element is ONE fma,
-//   L2: f = fl(xn - 2 acc qs)  (key = max(fl(fl(xn + qn) - 2 acc qs), 0))     IP: f = acc * -qs = key,
-// and f < pf_uf(U) for every key < U: for L2 the margin (xn_max^2 + qn + |U|) 2^-20 is 4x the sum of the
-// roundings of f, of the key and of U - qn (|2 acc qs| <= 1.01 (xn + qn)). The filter only has false
-// positives, which the exact test then rejects. -inf: the query slot is empty.
-template <int METRIC>
-__device__ __forceinline__ float pf_uf(float lk_last, float th, float qn, float xnmax2) {
-  const float U = fminf(lk_last, nextafterf(th, INFINITY));
-  if (!(U > -INFINITY) || !(qn < INFINITY)) return -INFINITY;
-  if (!(U < INFINITY)) return INFINITY;
-  if (METRIC == kL2) return (U - qn) + (xnmax2 + qn + fabsf(U)) * 0x1p-20f;
-  return U;
 }
 
 template <int METRIC>
@@ -632,7 +575,15 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
   const int k = a.k;
   int64_t sb = 0, se = 0;
   if (live) { sb = a.slot_begin[q]; se = a.slot_begin[q + 1]; }
-  const int64_t c1 = se * a.slot_k;
+  int64_t c1 = se * a.slot_k;
+  // K13 candidate buffers (slot_cnt): one slot per query holding slot_cnt[q] unsorted entries; more than
+  // slot_k of them means some were not stored: the query cannot be proven
+  bool cnt_ovf = false;
+  if (a.slot_cnt && live) {
+    const int n = a.slot_cnt[q];
+    cnt_ovf = n > a.slot_k;
+    c1 = sb * a.slot_k + (n < a.slot_k ? n : a.slot_k);
+  }
 
   // phase 1: Ak = k-th smallest approximate key (running top-k over the lanes, K7's ballot insertion)
   float mk = INFINITY, tk = INFINITY;
@@ -652,8 +603,9 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
       mask &= __ballot(ck < tk);
     }
   }
-  float bmin = INFINITY;
-  for (int64_t sl = sb + lane; sl < se; sl += 64) bmin = fminf(bmin, a.slot_bound[sl]);
+  float bmin = cnt_ovf ? -INFINITY : INFINITY;
+  if (a.slot_bound)
+    for (int64_t sl = sb + lane; sl < se; sl += 64) bmin = fminf(bmin, a.slot_bound[sl]);
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) bmin = fminf(bmin, __shfl_xor(bmin, off));
 
@@ -662,7 +614,7 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
   const float qn = live ? a.qnorms[qrow] : 0.0f;
   const float delta = pf_delta<METRIC>(qn, live ? a.qres[qrow] : 0.0f, a.x_norm_max, a.x_res_max, a.dp);
   const float T = pf_window(tk, delta);  // +inf when fewer than k candidates
-  bool ovf = bmin < INFINITY && bmin <= T;
+  bool ovf = bmin < INFINITY && (bmin <= T || bmin == -INFINITY);
 
   // phase 2: collect the window (ballot prefix, no atomics)
   int cnt = 0;
@@ -1446,7 +1398,7 @@ hipError_t launch_pr_scan(const PfScanArgs& a, int grid, hipStream_t s) {
 hipError_t launch_pf_refine(const PfRefineArgs& a, hipStream_t s) {
   if (a.k < 1 || a.k > kPfMaxK || a.dp > 1024) return hipErrorInvalidValue;
   if (a.nq <= 0) return hipSuccess;
-  if (a.k == 1 && a.slot_k % 4 == 0) {  // lane per query
+  if (a.k == 1 && a.slot_k % 4 == 0 && a.slot_cnt == nullptr && a.slot_bound != nullptr) {  // lane per query
     if (a.metric == kIP) hipLaunchKernelGGL(k_pf_refine1<kIP>, pf_grid(a.nq, 256), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_pf_refine1<kL2>, pf_grid(a.nq, 256), dim3(256), 0, s, a);
     return hipGetLastError();

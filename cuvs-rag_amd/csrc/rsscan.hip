@@ -1,0 +1,383 @@
+// K13 — row-stationary fp16 pre-filter scan for IVF search.
+//
+// Why: K10 keeps a 64-query tile in LDS and streams every list chunk once per tile, so a row of
+// a list probed by m queries crosses the L2 -> CU path ceil(m/64) times and, unless the tiles of a
+// chunk happen to run in step on one XCD, comes from the fabric (MALL / HBM) that many times: at
+// the benchmark shape 46 GB of fabric reads per launch against 15.4 GB of compulsory fp16 rows
+// (profiles/r01e_pf_pmc_scan_t64.json). K13 turns the roles round:
+//
+//   * work item = (list, block of 8 row groups = 256 rows); wave w of the CU keeps group w of the
+//     block as MFMA A operands IN REGISTERS for the whole item (NK k-steps x 16 B per lane:
+//     192 VGPRs at d = 768), so every row is read from HBM exactly once per search;
+//   * the list's queries stream past the rows in 32-query tiles: each tile's fp16 image
+//     ([NK k-steps][64 lanes] x 16 B, one conflict-free ds_read_b128 per MFMA) plus a 16-B header
+//     per query is copied global -> LDS by LDS-DMA (global_load_lds_dwordx4, no VGPRs), double
+//     buffered, one barrier per tile; the queries of a list (~0.5 MB) stay in the XCD's L2 while the
+//     XCD's 32 CUs work through the list's blocks (items are dealt from 8 per-XCD queues in list order);
+//   * the next item's rows are loaded into the A registers during the item's last tile, each
+//     k-step's registers right after their last MFMA;
+//   * no per-lane top-k: every query carries a bound T_q from a pre-pass (the exact k-th key over
+//     its nearest list) with T_q >= the refine window of the final answer; the
+//     epilogue appends every (approximate key <= T_q, row) to the query's candidate buffer, and K11
+//     ranks them exactly. Only false positives of the one-fma filter reach the exact test.
+//
+// The result is the pinned fp32 answer (K11 recomputes every window candidate in the oracle's
+// order; queries whose buffer overflows go to the exact scan).
+#include <climits>
+
+#include "mivs_common.hpp"
+#include "pf_math.hpp"
+
+namespace mivs {
+
+namespace {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+
+constexpr int kRsThreads = kRsWaves * 64;
+
+// one wave-instruction of LDS-DMA: 64 lanes x 16 B from per-lane global addresses to lds + lane * 16
+__device__ __forceinline__ void rs_glds(const void* g, char* lds) {
+  __builtin_amdgcn_global_load_lds((gbl_ptr_t)g, (lds_ptr_t)lds, 16, 0, 0);
+}
+
+// a work item: {first group, end group, first tile slot, tiles} (k_rs_items)
+struct RsItem {
+  int g0, gend, slot, ntiles;
+};
+
+__device__ __forceinline__ RsItem rs_item(const RsScanArgs& a, int w) {
+  const int4 v = a.items[w];
+  return RsItem{__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
+                __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w)};
+}
+
+// Stage one 32-query tile into an LDS buffer: the tile's image ([NK + 1] pieces x 1 KiB, built by
+// k_rs_tiles in exactly the LDS layout) is copied piece by piece by LDS-DMA, pieces dealt round-robin
+// over the 8 waves; every wave-instruction reads 1 KiB contiguous.
+template <int NK>
+__device__ __forceinline__ void rs_stage(char* buf, const char* img, int wave, int lane) {
+#pragma unroll
+  for (int p0 = 0; p0 <= NK; p0 += kRsWaves) {
+    const int p = p0 + wave;
+    if (p <= NK) rs_glds(img + p * 1024 + lane * 16, buf + p * 1024);
+  }
+}
+
+// the image of tile t of list l: tiles of list l start at bucket_off[l] / 32 + l (at most
+// floor(m_l / 32) + 1 >= ceil(m_l / 32) slots before list l + 1's first)
+__device__ __forceinline__ int64_t rs_tile_slot(const int* bucket_off, int l, int t) {
+  return (int64_t)(bucket_off[l] / kRsQTile) + l + t;
+}
+
+template <int METRIC, int NK>
+__global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BUF = NK * 1024 + 1024;
+  constexpr int NB = 2 * NK;  // 8-dim blocks of a group row
+  constexpr int64_t IMG = (int64_t)(NK + 1) * 1024;
+  float* s_norm = reinterpret_cast<float*>(smem + 2 * BUF);  // [8 waves][32] row norms of the wave's group
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int j = lane & 31;
+  const int h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // static, XCD-aware schedule: queue x (= blockIdx % 8, the XCD under round-robin placement; speed only)
+  // holds the x-th eighth of the list-ordered items and its P workgroups take every P-th item, so the
+  // CUs of an XCD work through the blocks of the same lists together (the lists' query tiles stay in
+  // that XCD's L2). Every item belongs to exactly one (queue, workgroup) whatever the placement.
+  const int total = __builtin_amdgcn_readfirstlane(a.work_off[a.n_lists]);
+  const int x = blockIdx.x & 7, P = gridDim.x >> 3;
+  const int hi = (int)((int64_t)total * (x + 1) / 8);
+  int w = (int)((int64_t)total * x / 8) + (int)(blockIdx.x >> 3);
+  if (w >= hi) return;
+  RsItem it = rs_item(a, w);
+  int g = it.g0 + wave;
+  bool gv = g < it.gend;
+  // group rows: a wave-uniform base (SGPRs) + this lane's 32-bit byte offset, so every k-step's load is
+  // the saddr form with no per-lane 64-bit address to keep (the next item's 48 addresses would not fit)
+  // Buffer loads: a per-group descriptor in SGPRs (uniform base, NB * 512 bytes), this lane's 32-bit
+  // offset in one VGPR and the k-step in soffset -- no per-lane 64-bit address per k-step to keep (the
+  // next item's 48 would not fit beside the resident rows)
+  const int lane_off = h * 512 + j * 16;
+  auto group_rsrc = [&](int grp) {
+    const uint64_t p = reinterpret_cast<uint64_t>(a.groups_h) + (uint64_t)grp * (NB * 512);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+    const uint32_t hi32 = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi32 << 32) | lo), 0, NB * 512,
+                                             0x00020000);
+  };
+  auto ld_rows = [&](__amdgpu_buffer_rsrc_t r, int s) {
+    return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(r, lane_off, s * 1024, 0));
+  };
+  h8 ra[NK];
+  {
+    const __amdgpu_buffer_rsrc_t r0 = group_rsrc(gv ? g : it.g0);
+#pragma unroll
+    for (int s = 0; s < NK; ++s) ra[s] = ld_rows(r0, s);
+  }
+  float nrm = (lane < 32 && gv) ? a.row_norms[(int64_t)g * kGroupRows + lane] : INFINITY;
+  rs_stage<NK>(smem, a.tiles + it.slot * IMG, wave, lane);
+  int par = 0;  // LDS buffer of the current tile
+  const float* wnorm = s_norm + wave * 32;
+  const f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+
+  for (;;) {
+    const int ntiles = it.ntiles;
+    const int wn = w + P;
+    const bool has_next = wn < hi;
+    RsItem nx = it;
+    if (has_next) nx = rs_item(a, wn);  // (retired by the first tile's wait, long before its use)
+    const int gnx = nx.g0 + wave;
+    const bool gvn = has_next && gnx < nx.gend;
+    for (int t = 0; t < ntiles; ++t) {
+      if (t == 0 && lane < 32) s_norm[wave * 32 + lane] = nrm;  // own slot: no other wave reads it
+      __builtin_amdgcn_s_waitcnt(0x0F70);                       // vmcnt(0): this wave's DMA of tile t landed
+      __syncthreads();                                          // ... and every other wave's
+      const bool last = t + 1 == ntiles;
+      // stage the next tile (of this item, or the next item's first) into the other buffer: every
+      // wave has finished reading it (tile t - 1) before the barrier above
+      if (!(a.flags & 2)) {
+        if (!last) rs_stage<NK>(smem + (par ^ 1) * BUF, a.tiles + (it.slot + t + 1) * IMG, wave, lane);
+        else if (has_next) rs_stage<NK>(smem + (par ^ 1) * BUF, a.tiles + nx.slot * IMG, wave, lane);
+      }
+      const bool reload = last && has_next;
+      const __amdgpu_buffer_rsrc_t nrs = group_rsrc(gvn ? gnx : nx.g0);
+      f32x16 acc = zero;
+      {
+        // (a wave without a group in this block runs the MFMAs on stale rows; its epilogue is skipped)
+        const char* bb = smem + par * BUF + lane * 16;
+        h8 b0 = *reinterpret_cast<const h8*>(bb);
+        h8 b1 = *reinterpret_cast<const h8*>(bb + 1024);
+#pragma unroll
+        for (int s = 0; s < NK; ++s) {
+          h8 b2 = b1;
+          if (s + 2 < NK) b2 = *reinterpret_cast<const h8*>(bb + (s + 2) * 1024);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s], b0, acc, 0, 0, 0);
+          // last tile: the next item's rows, right after this k-step's last use of the register
+          if (reload) ra[s] = ld_rows(nrs, s);
+          b0 = b1;
+          b1 = b2;
+        }
+      }
+      if (reload) nrm = (lane < 32 && gvn) ? a.row_norms[(int64_t)gnx * kGroupRows + lane] : INFINITY;
+      // epilogue: lane (j, h) holds the 16 dots of query j with rows (r & 3) + 8 (r >> 2) + 4 h
+      if (gv && !(a.flags & 1)) {
+        // header of query j: {qs, uf, T, q}
+        const float4 hd = *reinterpret_cast<const float4*>(smem + par * BUF + NK * 1024 + j * 16);
+        const float qs = hd.x, uf = hd.y;
+        const float mm = METRIC == kL2 ? -2.0f * qs : -qs;
+        // one-fma filter over the 16 keys (norms from LDS four at a time: registers are short); the rare
+        // survivors are then handled one at a time, picked out of the accumulator by selects
+        unsigned hits = 0;
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          const float4 v = *reinterpret_cast<const float4*>(wnorm + 8 * q4 + 4 * h);
+          const float xv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            hits |= (fmaf(acc[4 * q4 + u], mm, METRIC == kL2 ? xv[u] : 0.0f) < uf ? 1u : 0u) << (4 * q4 + u);
+        }
+        if (__ballot(hits != 0) != 0) {
+          const float T = hd.z;
+          const int bq = __float_as_int(hd.w);
+          const bool qv = bq >= 0 && bq < a.nq;  // (-1: an empty lane of the tile)
+          const float qn = qv ? a.qnorms[bq] : 0.0f;
+          if (!qv) hits = 0;
+          while (hits) {
+            const int r = __builtin_ctz(hits);
+            hits &= hits - 1;
+            float c = acc[0];
+#pragma unroll
+            for (int i = 1; i < 16; ++i) c = r == i ? acc[i] : c;
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+            const float k0 = pf_key<METRIC>(c, qs, wnorm[row], qn);
+            if (k0 <= T) {
+              const int at = atomicAdd(a.cand_cnt + bq, 1);
+              if (at < a.cap) {
+                a.cand_key[(int64_t)bq * a.cap + at] = k0;
+                a.cand_pos[(int64_t)bq * a.cap + at] = g * kGroupRows + row;
+              }
+            }
+          }
+        }
+      }
+      par ^= 1;
+    }
+    if (!has_next) break;
+    w = wn;
+    it = nx;
+    g = gnx;
+    gv = gvn;
+  }
+}
+
+// Work items of K13 from the probe map (chunk = kRsBlockGroups groups, one tile column per list):
+// item w -> {first group, end group, first tile slot of its list, tiles of its list}
+__global__ void k_rs_items(const int* __restrict__ work_off, const int* __restrict__ bucket_off,
+                           const int64_t* __restrict__ list_goff, int n_lists, int max_items, int4* __restrict__ items) {
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= max_items || w >= work_off[n_lists]) return;
+  int lo = 0, hi = n_lists - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (work_off[mid] <= w) lo = mid; else hi = mid - 1;
+  }
+  const int64_t g0 = list_goff[lo] + (int64_t)(w - work_off[lo]) * kRsBlockGroups;
+  const int64_t ge = list_goff[lo + 1] < g0 + kRsBlockGroups ? list_goff[lo + 1] : g0 + kRsBlockGroups;
+  const int m = bucket_off[lo + 1] - bucket_off[lo];
+  items[w] = make_int4((int)g0, (int)ge, (int)rs_tile_slot(bucket_off, lo, 0), (m + kRsQTile - 1) / kRsQTile);
+}
+
+// per query: {qs, uf, qn, T} for K13 from the pre-pass's exact k-th key over the query's nearest list;
+// row nq = the null header (matches nothing)
+template <int METRIC>
+__global__ void k_rs_headers(const float* __restrict__ pre_d, const int64_t* __restrict__ pre_i, int64_t nq, int k,
+                             const float* __restrict__ qscale, const float* __restrict__ qnorms,
+                             const float* __restrict__ qres, float x_norm_max, float x_res_max, int dp,
+                             float4* __restrict__ hdr) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q > nq) return;
+  if (q == nq) {  // the null header
+    hdr[q] = make_float4(0.0f, -INFINITY, -INFINITY, __int_as_float(-1));
+    return;
+  }
+  const float qn = qnorms[q];
+  const float delta = pf_delta<METRIC>(qn, qres[q], x_norm_max, x_res_max, dp);
+  float T = INFINITY;
+  if (pre_i[q * k + k - 1] >= 0) {
+    const float d = pre_d[q * k + k - 1];
+    const float kth = METRIC == kL2 ? d : -d;  // the exact key of the k-th neighbour in that list
+    // k rows have approximate keys <= kth + delta, so the final k-th approximate key Ak <= U and the
+    // final window pf_window(Ak) <= pf_window(U) (monotone); one more relative step covers the roundings
+    const float U = kth + delta;
+    T = pf_window(U, delta);
+    T = T + fabsf(T) * 0x1p-20f + 1e-30f;
+  }
+  const float uf = pf_uf<METRIC>(INFINITY, T, qn, x_norm_max * x_norm_max);
+  hdr[q] = make_float4(qscale[q], uf, T, __int_as_float((int)q));
+}
+
+// Tile images for K13: per list l with m_l queries, ceil(m_l / 32) tiles of [NK + 1] x 1 KiB: piece
+// s < NK is the MFMA B operand of k-step s (lane j + 32 h: dims 16 s + 8 h .. + 8 of the tile's j-th
+// query), piece NK the 16-B headers (lane j: query j's; lanes 32..63 repeat them). One workgroup per
+// list; a thread reads 16 contiguous bytes of a query row (the row's pieces are consecutive threads).
+template <int NK>
+__global__ __launch_bounds__(256) void k_rs_tiles(const int64_t* __restrict__ bucket_q, const int* __restrict__ bucket_off,
+                                                  const uint16_t* __restrict__ qh, const float4* __restrict__ qhdr,
+                                                  int nq, char* __restrict__ tiles) {
+  const int l = blockIdx.x;
+  const int e0 = bucket_off[l], m = bucket_off[l + 1] - e0;
+  if (m <= 0) return;
+  const int ntiles = (m + kRsQTile - 1) / kRsQTile;
+  constexpr int64_t IMG = (int64_t)(NK + 1) * 1024;
+  constexpr int PER = 2 * NK;  // 16-B pieces of one query row
+  char* base = tiles + rs_tile_slot(bucket_off, l, 0) * IMG;
+  for (int i = threadIdx.x; i < ntiles * kRsQTile * PER; i += blockDim.x) {
+    const int t = i / (kRsQTile * PER), r = i - t * (kRsQTile * PER);
+    const int jq = r / PER, u = r - jq * PER;  // query jq of tile t, 16-B piece u of its row
+    const int s = u >> 1, hh = u & 1;
+    const int e = t * kRsQTile + jq;
+    const int q = e < m ? (int)bucket_q[e0 + e] : -1;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (q >= 0) v = *reinterpret_cast<const uint4*>(qh + (int64_t)q * (NK * 16) + 8 * u);
+    *reinterpret_cast<uint4*>(base + t * IMG + s * 1024 + (jq + 32 * hh) * 16) = v;
+  }
+  for (int i = threadIdx.x; i < ntiles * 64; i += blockDim.x) {
+    const int t = i >> 6, L = i & 63, e = t * kRsQTile + (L & 31);
+    const int q = e < m ? (int)bucket_q[e0 + e] : -1;
+    *reinterpret_cast<float4*>(base + t * IMG + NK * 1024 + L * 16) = qhdr[q >= 0 ? q : nq];
+  }
+}
+
+}  // namespace
+
+size_t rs_scan_lds_bytes(int dp) {
+  const int nk = dp / 16;
+  return (size_t)2 * (nk * 1024 + 1024) + kRsWaves * 32 * sizeof(float) + 16;
+}
+
+bool rs_scan_supported(int dp) {
+  return dp % 64 == 0 && dp >= 64 && dp <= 768;
+}
+
+template <int METRIC, int NK>
+static hipError_t launch_rs_mk(const RsScanArgs& a, int grid, hipStream_t s) {
+  const size_t lds = rs_scan_lds_bytes(NK * 16);
+  hipError_t e = hipFuncSetAttribute((const void*)k_rs_scan<METRIC, NK>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_rs_scan<METRIC, NK>), dim3(grid), dim3(kRsThreads), lds, s, a);
+  return hipGetLastError();
+}
+
+template <int METRIC>
+static hipError_t launch_rs_m(const RsScanArgs& a, int dp, int grid, hipStream_t s) {
+  switch (dp / 16) {
+    case 4: return launch_rs_mk<METRIC, 4>(a, grid, s);
+    case 8: return launch_rs_mk<METRIC, 8>(a, grid, s);
+    case 12: return launch_rs_mk<METRIC, 12>(a, grid, s);
+    case 16: return launch_rs_mk<METRIC, 16>(a, grid, s);
+    case 20: return launch_rs_mk<METRIC, 20>(a, grid, s);
+    case 24: return launch_rs_mk<METRIC, 24>(a, grid, s);
+    case 28: return launch_rs_mk<METRIC, 28>(a, grid, s);
+    case 32: return launch_rs_mk<METRIC, 32>(a, grid, s);
+    case 36: return launch_rs_mk<METRIC, 36>(a, grid, s);
+    case 40: return launch_rs_mk<METRIC, 40>(a, grid, s);
+    case 44: return launch_rs_mk<METRIC, 44>(a, grid, s);
+    case 48: return launch_rs_mk<METRIC, 48>(a, grid, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_rs_scan(const RsScanArgs& a, int dp, int grid, hipStream_t s) {
+  if (!rs_scan_supported(dp)) return hipErrorInvalidValue;
+  return a.metric == kIP ? launch_rs_m<kIP>(a, dp, grid, s) : launch_rs_m<kL2>(a, dp, grid, s);
+}
+
+int64_t rs_tiles_bytes(int64_t ne, int n_lists, int dp) {
+  return (ne / kRsQTile + n_lists + 1) * (int64_t)(dp / 16 + 1) * 1024;
+}
+
+template <int NK>
+static void launch_rs_tiles_k(const int64_t* bucket_q, const int* bucket_off, int n_lists, const uint16_t* qh,
+                              const float4* qhdr, int nq, char* tiles, hipStream_t s) {
+  hipLaunchKernelGGL(k_rs_tiles<NK>, dim3((unsigned)n_lists), dim3(256), 0, s, bucket_q, bucket_off, qh, qhdr, nq,
+                     tiles);
+}
+
+hipError_t launch_rs_tiles(const int64_t* bucket_q, const int* bucket_off, int n_lists, const uint16_t* qh,
+                           const float4* qhdr, int nq, int dp, char* tiles, hipStream_t s) {
+  switch (dp / 16) {
+#define RS_T(NK) case NK: launch_rs_tiles_k<NK>(bucket_q, bucket_off, n_lists, qh, qhdr, nq, tiles, s); break;
+    RS_T(4) RS_T(8) RS_T(12) RS_T(16) RS_T(20) RS_T(24) RS_T(28) RS_T(32) RS_T(36) RS_T(40) RS_T(44) RS_T(48)
+#undef RS_T
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_rs_items(const int* work_off, const int* bucket_off, const int64_t* list_goff, int n_lists,
+                           int max_items, int4* items, hipStream_t s) {
+  if (max_items <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rs_items, dim3((unsigned)ceil_div(max_items, 256)), dim3(256), 0, s, work_off, bucket_off,
+                     list_goff, n_lists, max_items, items);
+  return hipGetLastError();
+}
+
+hipError_t launch_rs_headers(const float* pre_d, const int64_t* pre_i, int64_t nq, int k, const float* qscale,
+                             const float* qnorms, const float* qres, float x_norm_max, float x_res_max, int dp,
+                             int metric, float4* hdr, hipStream_t s) {
+  const dim3 grid((unsigned)ceil_div(nq + 1, 256));
+  if (metric == kIP)
+    hipLaunchKernelGGL(k_rs_headers<kIP>, grid, dim3(256), 0, s, pre_d, pre_i, nq, k, qscale, qnorms, qres,
+                       x_norm_max, x_res_max, dp, hdr);
+  else
+    hipLaunchKernelGGL(k_rs_headers<kL2>, grid, dim3(256), 0, s, pre_d, pre_i, nq, k, qscale, qnorms, qres,
+                       x_norm_max, x_res_max, dp, hdr);
+  return hipGetLastError();
+}
+
+}  // namespace mivs

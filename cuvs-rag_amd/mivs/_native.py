@@ -85,6 +85,9 @@ class SearchStats(ctypes.Structure):
         ("overflow_queries", c_int64),
         ("window_candidates", c_int64),
         ("unique_groups", c_int64),
+        ("scan_kernel", c_int32),
+        ("candidates", c_int64),
+        ("cand_overflow", c_int64),
     ]
 
     def as_dict(self) -> dict:
@@ -152,6 +155,8 @@ _SIGS = {
     "mivs_merge_topk_allgather": (c_int32, [c_void_p, POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), c_int64,
                                             c_int32, c_int32, c_int32, POINTER(c_void_p), POINTER(c_void_p)]),
     "mivs_comm_destroy": (None, [c_void_p]),
+    "mivs_refine": (c_int32, [c_int32, c_void_p, c_void_p, c_int32, c_int64, c_int32, c_void_p, c_int64, c_void_p,
+                              c_int32, c_int32, c_int32, c_void_p, c_void_p]),
     "mivs_row_norms": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int32, c_void_p]),
     "mivs_normalize_rows": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int32, c_void_p]),
     "mivs_synth_mixture": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int64, c_int32, c_uint64, c_int32,

@@ -12,7 +12,8 @@ residuals x - c_list of min(n, 256 * max_train_points_per_pq_code) strided rows;
 as pq_dim one-byte codes. Search builds a pq_dim x 256 fp32 LUT per (query, probed list) in LDS
 and sums LUT entries over the list's codes (hand-written HIP, cuvs-rag_amd/csrc/pq.hip).
 
-This build: L2 metric, pq_bits = 8, k <= 32, identity rotation (dims past ``dim`` read as 0).
+This build: L2 metric, pq_bits = 8, k <= 64, identity rotation (dims past ``dim`` read as 0). For an exact
+ranking of the PQ candidates use ``mivs.neighbors.refine`` (cuVS's IVF-PQ + refine pattern).
 fp16 datasets (BASELINE config 5) are widened to fp32 on the device before training.
 """
 from __future__ import annotations

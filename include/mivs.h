@@ -83,6 +83,9 @@ typedef struct {
   int64_t overflow_queries; /* queries the refine could not prove, re-run through the exact fp32 scan */
   int64_t window_candidates;/* candidates recomputed in fp32 by the refine (sum over queries) */
   int64_t unique_groups;    /* 32-row groups of the lists probed by at least one query (compulsory bytes) */
+  int32_t scan_kernel;      /* fine scan that served it: 3 K3, 31 K3w, 10 K10, 12 K12, 13 K13 */
+  int64_t candidates;       /* K13: (approximate key <= T_q, row) pairs appended, all queries */
+  int64_t cand_overflow;    /* K13: queries with more candidates than their buffer holds */
 } mivs_search_stats;
 
 /* device time of the searches issued since the last collect while profiling was on
@@ -156,7 +159,7 @@ int32_t mivs_index_get_prefilter(mivs_index_t index, int32_t* enabled);
 void mivs_index_free(mivs_index_t index);
 
 /* ---- IVF-PQ: replaces ivf_pq.build (index_building_coordinator.py:404, improved_multi_gpu_rag.py:137)
- * and ivf_pq.search (improved_multi_gpu_rag.py:228-230). L2, pq_bits 8, k <= 32. Codes live on the
+ * and ivf_pq.search (improved_multi_gpu_rag.py:228-230). L2, pq_bits 8, k <= 64. Codes live on the
  * device (pq_dim bytes per row); the dataset is only read during build. */
 int32_t mivs_ivf_pq_build(int32_t device, void* stream, const float* d_data, int64_t n, int32_t dim,
                           const mivs_ivf_pq_params* params, int64_t id_offset, mivs_index_t* out);
@@ -209,6 +212,14 @@ int32_t mivs_merge_topk_allgather(mivs_comm_t comm, void* const* streams, const 
                                   const int64_t* const* d_ids, int64_t nq, int32_t k_in, int32_t k,
                                   int32_t metric, float* const* d_out_dist, int64_t* const* d_out_ids);
 void mivs_comm_destroy(mivs_comm_t comm);
+
+/* ---- exact re-ranking: replaces cuvs.neighbors.refine(dataset, queries, candidates, k) (cuvs 25.06), the
+ * step that makes an IVF-PQ search (improved_multi_gpu_rag.py:228-230) exact over its top-(r*k)
+ * candidates. d_data [n][dim] fp32 (or fp16 when data_is_half), d_candidates [nq][n_candidates] row
+ * numbers (-1: none); outputs [nq][k] by (distance, id) in the contract's pinned arithmetic. k <= 64. */
+int32_t mivs_refine(int32_t device, void* stream, const void* d_data, int32_t data_is_half, int64_t n, int32_t dim,
+                    const float* d_queries, int64_t nq, const int64_t* d_candidates, int32_t n_candidates, int32_t k,
+                    int32_t metric, float* d_distances, int64_t* d_neighbors);
 
 /* ---- helpers exposed for parity tests and the bench ---- */
 int32_t mivs_row_norms(int32_t device, void* stream, const float* d_x, int64_t n, int32_t dim, float* d_out);

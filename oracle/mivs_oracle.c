@@ -128,6 +128,30 @@ void orc_knn(const float* x, int64_t n, const float* q, int64_t nq, int d, int k
   free(xn);
 }
 
+/* Exact re-ranking of candidate rows -- cuvs.neighbors.refine(dataset, queries, candidates, k)
+ * (cuvs 25.06, third-party; the step after an IVF-PQ search, improved_multi_gpu_rag.py:228-230):
+ * per query the pinned key of every candidate row (id -1 or out of range: skipped), top-k by
+ * (key, id). */
+void orc_refine(const float* x, int64_t n, int d, const float* q, int64_t nq, const int64_t* cand, int nc, int k,
+                int metric, float* out_d, int64_t* out_i) {
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int64_t qi = 0; qi < nq; ++qi) {
+    kv_t* h = (kv_t*)malloc(sizeof(kv_t) * (size_t)(k > 0 ? k : 1));
+    int sz = 0;
+    const float* qq = q + qi * d;
+    const float qn = orc_dot(qq, qq, d);
+    for (int c = 0; c < nc; ++c) {
+      const int64_t r = cand[qi * nc + c];
+      if (r < 0 || r >= n) continue;
+      const float* xr = x + r * d;
+      kv_t v = {orc_key(orc_dot(xr, qq, d), orc_dot(xr, xr, d), qn, metric), r};
+      heap_push(h, &sz, k, v);
+    }
+    heap_emit(h, sz, k, metric, out_d + qi * k, out_i + qi * k);
+    free(h);
+  }
+}
+
 /* Global top-k merge of per-shard / per-probe candidate lists — the contract of
  * SearchResultAggregator.merge_search_results (test_search_result_aggregator.py:308-358)
  * and the notebook merge (cuvs-2gpu-main.ipynb:1820-1834), ties by id. */

@@ -35,6 +35,8 @@ void orc_normalize_rows(const float* x, int64_t n, int d, float* out);
 float orc_key(float dot, float xn, float qn, int metric);
 
 /* exact brute-force kNN (rows of x carry ids = row index + id_offset) */
+void orc_refine(const float* x, int64_t n, int d, const float* q, int64_t nq, const int64_t* cand, int nc, int k,
+                int metric, float* out_d, int64_t* out_i);
 void orc_knn(const float* x, int64_t n, const float* q, int64_t nq, int d, int k, int metric,
              int64_t id_offset, float* out_d, int64_t* out_i);
 

@@ -38,6 +38,7 @@ def lib():
             "orc_norms": (None, [P, i64, i32, P]),
             "orc_normalize_rows": (None, [P, i64, i32, P]),
             "orc_knn": (None, [P, i64, P, i64, i32, i32, i32, i64, P, P]),
+            "orc_refine": (None, [P, i64, i32, P, i64, P, i32, i32, i32, P, P]),
             "orc_merge": (None, [P, P, i64, i32, i32, i32, i32, P, P]),
             "orc_kmeans_assign": (None, [P, P, i64, P, i32, i32, i32, P]),
             "orc_kmeans_update": (None, [P, P, i64, P, i32, i32, P]),
@@ -120,6 +121,17 @@ def knn(x, q, k, metric="sqeuclidean", id_offset=0):
     od = np.empty((nq, k), np.float32)
     oi = np.empty((nq, k), np.int64)
     lib().orc_knn(_p(x), x.shape[0], _p(q), nq, x.shape[1], k, metric_code(metric), id_offset, _p(od), _p(oi))
+    return od, oi
+
+
+def refine(x, q, candidates, k, metric="sqeuclidean"):
+    """Exact top-k over each query's candidate rows (cuvs.neighbors.refine semantics, ties by id)."""
+    x, q, c = _f32(x), _f32(q), _i64(candidates)
+    nq = q.shape[0]
+    od = np.empty((nq, k), np.float32)
+    oi = np.empty((nq, k), np.int64)
+    lib().orc_refine(_p(x), x.shape[0], x.shape[1], _p(q), nq, _p(np.ascontiguousarray(c)), c.shape[1], k,
+                     metric_code(metric), _p(od), _p(oi))
     return od, oi
 
 

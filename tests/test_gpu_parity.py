@@ -399,6 +399,8 @@ PQ_CASES = [
     (5000, 96, 12, 40, 2, 29, 5, 32),     # pq_len 3, rot_dim 120 > d: zero-padded dims
     (12000, 768, 32, 96, 2, 20, 6, 10),   # the reference's pq_dim = 96 at d = 768
     (9000, 32, 2, 8, 3, 15, 2, 10),       # lists > 4096 rows (K9s row blocks), one LUT half only
+    (8000, 768, 16, 96, 2, 21, 6, 64),    # k = 64: the candidate pool of IVF-PQ + refine
+    (7000, 64, 16, 16, 3, 19, 5, 40),
 ]
 
 

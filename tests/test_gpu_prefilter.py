@@ -88,7 +88,8 @@ def test_prefilter_overflow_falls_back_exactly(mivs_lib):
     """Many exact duplicates: the window holds more candidates than the refine capacity, so the
     pre-filter must hand those queries to the exact scan — and the answer must not change."""
     base = _data(500, 64, seed=12, normalize=True)
-    x = np.concatenate([base] * 40)            # every row 40 times: 40 equal keys per neighbour
+    # every row 80 times: 80 equal keys per neighbour, more than the refine's 64-candidate window
+    x = np.concatenate([base] * 80)
     q = np.concatenate([base[:20], _data(20, 64, seed=13, normalize=True)])
     idx, st = _check_vs_oracle(x, q, 8, 8, 10)
     assert st["overflow_queries"] > 0, st
