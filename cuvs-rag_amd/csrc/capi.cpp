@@ -87,7 +87,7 @@ struct Workspace {
   // fp16 pre-filter path (K10 / K11) and its exact-scan fallback
   Buf qh, qscale, qres, qtheta, pf_key, pf_pos, pf_bound, pf_stats, ovf_q, ovf_rows, ovf_d, ovf_i;
   // K13 row-stationary scan: the full probe list, the pre-pass result, per-query headers and candidates
-  Buf probes_full, pre_d, pre_i, qhdr, cand_cnt, cand_key, cand_pos, slot_iota, rs_tiles;
+  Buf probes_full, pre_d, pre_i, pre_goff, qhdr, cand_cnt, cand_key, cand_pos, slot_iota, rs_tiles;
   // per-list query counts of the last search's own probe map (an exact fallback re-maps its queries)
   Buf stat_counts, rs_ovf_q, rs_ovf_rows, rs_ovf_d, rs_ovf_i, rs_items;
 };
@@ -654,7 +654,7 @@ void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t 
                       bool allow_rs = true);
 void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                        int64_t* out_i, bool pf, ProfRec* pr, bool prof, const int64_t* probes = nullptr,
-                       bool allow_rs = true);
+                       bool allow_rs = true, const int64_t* goff_ov = nullptr, int n_lists_ov = 0);
 
 void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                         int64_t* out_i, const float* slot_key, const int* slot_pos, const float* slot_bound,
@@ -662,8 +662,9 @@ void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_
 
 // K10 scan + K11 refine for a probe map built with (kPfChunkGroups, kPfQTile); queries the refine
 // could not prove are re-run through the exact scan and scattered back.
+// (goff / n_lists: another split of the same groups into lists -- K13's pre-pass samples)
 void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
-                    int64_t* out_i, ProfRec* pr, bool use_r) {
+                    int64_t* out_i, ProfRec* pr, bool use_r, const int64_t* goff, int n_lists) {
   Workspace& ws = idx->ws;
   const ListSet& L = idx->lists;
   const int dp = idx->dp;
@@ -684,7 +685,7 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   // the 8 queue counters, then (K10) one convoy position per (list, chunk)
   const char* cve = getenv("MIVS_PF_CONVOY");
   const bool convoy = !use_r && !(cve && cve[0] == '0');
-  const int64_t n_cpos = convoy ? (int64_t)L.n_lists * tcp[1] : 0;
+  const int64_t n_cpos = convoy ? (int64_t)n_lists * tcp[1] : 0;
   ws.counter.reserve(sizeof(int) * (8 * 16 + n_cpos));
   HIPCHK(hipMemsetAsync(ws.counter.p, 0, sizeof(int) * (8 * 16 + n_cpos), s));
   PfScanArgs a{};
@@ -694,8 +695,8 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   }
   a.groups_h = idx->groups_h.as<uint16_t>();
   a.row_norms = L.norms.as<float>();
-  a.list_goff = L.goff.as<int64_t>();
-  a.n_lists = L.n_lists;
+  a.list_goff = goff;
+  a.n_lists = n_lists;
   a.chunk_groups = use_r ? idx->pr_G : idx->pf_G;
   a.qh = ws.qh.as<uint16_t>();
   a.qscale = ws.qscale.as<float>();
@@ -826,6 +827,15 @@ void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_
   }
 }
 
+// Centroid chunk of the coarse probe: enough (query tile, chunk) work items for >= 4 per CU -- a 10k-query
+// batch over 1024 centroids is only 313 query tiles -- with K7 merging the chunks' top-n_probes
+int coarse_groups(const mivs_index_s* idx, int64_t nq) {
+  const int64_t ng = std::max<int64_t>(1, idx->cents.n_groups);
+  const int64_t tiles = std::max<int64_t>(1, ceil_div(nq, kQTile));
+  const int64_t chunks = std::min<int64_t>(ng, std::max<int64_t>(1, ceil_div(4LL * cu_count(idx->device), tiles)));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(idx->G, ceil_div(ng, chunks)));
+}
+
 void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                       int64_t* out_i, int32_t* out_probes, bool allow_pf, bool prof, bool allow_rs) {
   Workspace& ws = idx->ws;
@@ -836,7 +846,7 @@ void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t 
   // coarse: top-n_probes centroids per query
   ws.probes_d.reserve(sizeof(float) * nq * np);
   ws.probes_i.reserve(sizeof(int64_t) * nq * np);
-  single_list_topk(idx->cents, idx->G, q, ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, np, idx->metric,
+  single_list_topk(idx->cents, coarse_groups(idx, nq), q, ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, np, idx->metric,
                    ws.probes_d.as<float>(), ws.probes_i.as<int64_t>(), idx->device, ws, s);
   if (out_probes) HIPCHK(launch_i64_to_i32(ws.probes_i.as<int64_t>(), nq * np, out_probes, s));
   ivf_search_probed(idx, s, q, nq, k, np, out_d, out_i, pf, pr, prof, nullptr, allow_rs);
@@ -865,14 +875,18 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   const int64_t ne = nq * np;
   ws.probes_full.reserve(sizeof(int64_t) * ne);
   HIPCHK(hipMemcpyAsync(ws.probes_full.p, ws.probes_i.p, sizeof(int64_t) * ne, hipMemcpyDeviceToDevice, s));
-  // 1. the nearest list of every query (probe 0): an n_probes = 1 search through K10 / K11
+  // 1. a sample of the nearest list of every query (probe 0): its first 1/div groups (the rows of a list
+  // are in no particular order), an n_probes = 1 search through K10 / K11 over the split lists
   ws.pre_d.reserve(sizeof(float) * nq * k);
   ws.pre_i.reserve(sizeof(int64_t) * nq * k);
-  HIPCHK(hipMemcpy2DAsync(ws.probes_i.p, sizeof(int64_t), ws.probes_full.p, sizeof(int64_t) * np, sizeof(int64_t), nq,
-                          hipMemcpyDeviceToDevice, s));
+  ws.pre_goff.reserve(sizeof(int64_t) * (2 * (size_t)L.n_lists + 1));
+  const char* pde = getenv("MIVS_RS_PRE_DIV");
+  const int pre_div = std::max(1, pde ? atoi(pde) : kRsPreDiv);
+  HIPCHK(launch_rs_pre_lists(L.goff.as<int64_t>(), L.n_lists, pre_div, ceil_div(k, kGroupRows), ws.probes_full.as<int64_t>(),
+                             nq, np, ws.pre_goff.as<int64_t>(), ws.probes_i.as<int64_t>(), s));
   const int64_t keep_ovf = idx->last_ovf, keep_window = idx->last_window;  // stats count the main pass only
   ivf_search_probed(idx, s, q, nq, k, 1, ws.pre_d.as<float>(), ws.pre_i.as<int64_t>(), true, nullptr, false,
-                    ws.probes_i.as<int64_t>(), false);
+                    ws.probes_i.as<int64_t>(), false, ws.pre_goff.as<int64_t>(), 2 * L.n_lists);
   idx->last_ovf = keep_ovf;
   idx->last_window = keep_window;
   // the pre-pass's own exact fallback may have reused the norm / fp16 query buffers for its rows
@@ -928,9 +942,34 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   a.cand_pos = ws.cand_pos.as<int>();
   a.flags = getenv("MIVS_RS_FLAGS") ? atoi(getenv("MIVS_RS_FLAGS")) : 0;
   if (a.flags & 2) a.flags |= 1;  // stale LDS tiles: never run an epilogue on them
+  const int grid = std::max(8, cu_count(idx->device) / 8 * 8);
+  Buf pbuf;
+  if (a.flags & 8) {  // diagnostic: per-block clocks to stderr
+    pbuf.reserve(sizeof(unsigned long long) * 3 * grid);
+    HIPCHK(hipMemsetAsync(pbuf.p, 0, sizeof(unsigned long long) * 3 * grid, s));
+    a.prof = pbuf.as<unsigned long long>();
+  }
   if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
-  HIPCHK(launch_rs_scan(a, dp, std::max(8, cu_count(idx->device) / 8 * 8), s));
+  HIPCHK(launch_rs_scan(a, dp, grid, s));
   if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
+  if (a.flags & 8) {
+    std::vector<unsigned long long> h(3 * (size_t)grid);
+    HIPCHK(hipMemcpyAsync(h.data(), pbuf.p, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    unsigned long long t0 = ~0ull, t1 = 0, tiles_max = 0, tiles_sum = 0;
+    double busy_sum = 0, busy_max = 0;
+    for (int b = 0; b < grid; ++b) {
+      t0 = std::min(t0, h[3 * b]);
+      t1 = std::max(t1, h[3 * b + 1]);
+      const double busy = (double)(h[3 * b + 1] - h[3 * b]);
+      busy_sum += busy;
+      busy_max = std::max(busy_max, busy);
+      tiles_sum += h[3 * b + 2];
+      tiles_max = std::max(tiles_max, h[3 * b + 2]);
+    }
+    fprintf(stderr, "[k13 blocks] span %.1f us | busy mean %.1f max %.1f us | tiles mean %.1f max %llu\n",
+            (t1 - t0) / 100.0, busy_sum / grid / 100.0, busy_max / 100.0, (double)tiles_sum / grid, tiles_max);
+  }
   // 5. exact ranking of the candidates (one slot per query)
   ws.slot_iota.reserve(sizeof(int64_t) * (nq + 1));
   HIPCHK(launch_iota_i64(ws.slot_iota.as<int64_t>(), nq + 1, 0, 1, s));
@@ -939,16 +978,21 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
 }
 
 void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
-                       int64_t* out_i, bool pf, ProfRec* pr, bool prof, const int64_t* probes, bool allow_rs) {
+                       int64_t* out_i, bool pf, ProfRec* pr, bool prof, const int64_t* probes, bool allow_rs,
+                       const int64_t* goff_ov, int n_lists_ov) {
   Workspace& ws = idx->ws;
   if (!probes) probes = ws.probes_i.as<int64_t>();
   // probe map
   const ListSet& L = idx->lists;
   const int64_t ne = nq * np;
-  ws.counts.reserve(sizeof(int) * L.n_lists);
-  ws.fill.reserve(sizeof(int) * L.n_lists);
-  ws.bucket_off.reserve(sizeof(int) * (L.n_lists + 1));
-  ws.work_off.reserve(sizeof(int) * (L.n_lists + 1));
+  // (a list split overriding the index's: the pre-filter scan only, n_probes = 1)
+  require(!goff_ov || (pf && np == 1), "list override outside the pre-pass", MIVS_ERR_INVALID);
+  const int n_lists = goff_ov ? n_lists_ov : L.n_lists;
+  const int64_t* goff = goff_ov ? goff_ov : L.goff.as<int64_t>();
+  ws.counts.reserve(sizeof(int) * n_lists);
+  ws.fill.reserve(sizeof(int) * n_lists);
+  ws.bucket_off.reserve(sizeof(int) * (n_lists + 1));
+  ws.work_off.reserve(sizeof(int) * (n_lists + 1));
   ws.bucket_q.reserve(sizeof(int64_t) * ne);
   ws.bucket_slot.reserve(sizeof(int64_t) * ne);
   ws.qp_slots.reserve(sizeof(int64_t) * ne);
@@ -962,7 +1006,7 @@ void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t
     idx->last_qtile = qtile;
     idx->last_pf = pf ? 1 : 0;
   }
-  if (pf && allow_rs && rs_use(idx, np)) {
+  if (pf && allow_rs && !goff_ov && rs_use(idx, np)) {
     if (prof) {
       idx->last_qtile = kRsQTile;
       idx->last_scan = 13;
@@ -972,13 +1016,13 @@ void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t
     return;
   }
   if (prof) idx->last_scan = pf ? (use_r ? 12 : 10) : (qtile == 64 ? 31 : 3);
-  HIPCHK(launch_probe_map(probes, nq, np, L.n_lists, L.goff.as<int64_t>(),
+  HIPCHK(launch_probe_map(probes, nq, np, n_lists, goff,
                           pf ? (use_r ? idx->pr_G : idx->pf_G) : idx->G, qtile, ws.counts.as<int>(), ws.fill.as<int>(),
                           ws.bucket_off.as<int>(), ws.work_off.as<int>(), ws.bucket_q.as<int64_t>(),
                           ws.bucket_slot.as<int64_t>(), ws.qp_slots.as<int64_t>(), ws.slot_begin.as<int64_t>(),
                           ws.scan_tmp.p, stb, s));
   if (pf) {
-    pf_scan_refine(idx, s, q, nq, k, np, out_d, out_i, pr, use_r);
+    pf_scan_refine(idx, s, q, nq, k, np, out_d, out_i, pr, use_r, goff, n_lists);
     if (pr) HIPCHK(hipEventRecord(pr->e[3], s));
     return;
   }
@@ -1444,7 +1488,7 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
     HIPCHK(launch_row_norms(d_q, nq, idx->d, ws.qn.as<float>(), s));
     ws.probes_d.reserve(sizeof(float) * nq * np);
     ws.probes_i.reserve(sizeof(int64_t) * nq * np);
-    single_list_topk(idx->cents, idx->G, d_q, ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, np, kL2,
+    single_list_topk(idx->cents, coarse_groups(idx, nq), d_q, ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, np, kL2,
                      ws.probes_d.as<float>(), ws.probes_i.as<int64_t>(), idx->device, ws, s);
     if (d_probes) HIPCHK(launch_i64_to_i32(ws.probes_i.as<int64_t>(), nq * np, d_probes, s));
     const ListSet& L = idx->lists;

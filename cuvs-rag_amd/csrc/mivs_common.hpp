@@ -199,7 +199,9 @@ struct PfScanArgs {
 constexpr int kRsWaves = 8;
 constexpr int kRsQTile = 32;
 constexpr int kRsBlockGroups = kRsWaves;
-constexpr int kRsCap = 512;  // candidate buffer entries per query (more: exact fallback)
+// K13's pre-pass scans the first 1 / kRsPreDiv of each query's nearest list (MIVS_RS_PRE_DIV)
+constexpr int kRsPreDiv = 4;
+constexpr int kRsCap = 4096;  // candidate buffer entries per query (more: the K10 fallback)
 struct RsScanArgs {
   const uint16_t* groups_h;  // fp16 lists, group layout [g][dp/8][32][8]
   const float* row_norms;    // pinned fp32 norms (+inf on pad rows)
@@ -217,7 +219,9 @@ struct RsScanArgs {
   int* cand_cnt;             // [nq] zeroed before launch
   float* cand_key;           // [nq][cap]
   int* cand_pos;             // [nq][cap]
-  int flags;                 // timing experiments only (MIVS_RS_FLAGS): 1 skip epilogue, 2 skip staging
+  int flags;                 // timing experiments only (MIVS_RS_FLAGS): 1 skip epilogue, 2 skip staging,
+                             // 8 per-block clocks into prof
+  unsigned long long* prof;  // flags & 8: [grid][3] {start, end, tiles}
 };
 
 // K14 exact re-ranking of candidates (refine.hip): cuvs.neighbors.refine
@@ -280,6 +284,8 @@ size_t rs_scan_lds_bytes(int dp);
 bool rs_scan_supported(int dp);
 hipError_t launch_rs_scan(const RsScanArgs& a, int dp, int grid, hipStream_t s);
 int64_t rs_tiles_bytes(int64_t ne, int n_lists, int dp);
+hipError_t launch_rs_pre_lists(const int64_t* goff, int n_lists, int div, int min_groups, const int64_t* probes,
+                               int64_t nq, int np, int64_t* goff2, int64_t* probes2, hipStream_t s);
 hipError_t launch_rs_items(const int* work_off, const int* bucket_off, const int64_t* list_goff, int n_lists,
                            int max_items, int4* items, hipStream_t s);
 hipError_t launch_rs_tiles(const int64_t* bucket_q, const int* bucket_off, int n_lists, const uint16_t* qh,

@@ -57,6 +57,14 @@ __device__ __forceinline__ RsItem rs_item(const RsScanArgs& a, int w) {
 // Stage one 32-query tile into an LDS buffer: the tile's image ([NK + 1] pieces x 1 KiB, built by
 // k_rs_tiles in exactly the LDS layout) is copied piece by piece by LDS-DMA, pieces dealt round-robin
 // over the 8 waves; every wave-instruction reads 1 KiB contiguous.
+// a buffer descriptor over [p, p + bytes) for a wave-uniform p (loads past `bytes` return zeros)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const char* p, int bytes) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
+}
+
 template <int NK>
 __device__ __forceinline__ void rs_stage(char* buf, const char* img, int wave, int lane) {
 #pragma unroll
@@ -78,7 +86,10 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   constexpr int BUF = NK * 1024 + 1024;
   constexpr int NB = 2 * NK;  // 8-dim blocks of a group row
   constexpr int64_t IMG = (int64_t)(NK + 1) * 1024;
-  float* s_norm = reinterpret_cast<float*>(smem + 2 * BUF);  // [8 waves][32] row norms of the wave's group
+  static_assert((NK + kRsWaves) / kRsWaves < NK, "the image's pieces are issued over k-steps 1..");
+  // [2 item parities][8 waves][64] row norms of the wave's group (lanes 32..63 repeat 0..31), filled by
+  // LDS-DMA so the next item's are in flight with its rows and nothing waits on them in registers
+  float* s_norm = reinterpret_cast<float*>(smem + 2 * BUF);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int j = lane & 31;
@@ -92,7 +103,19 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   const int x = blockIdx.x & 7, P = gridDim.x >> 3;
   const int hi = (int)((int64_t)total * (x + 1) / 8);
   int w = (int)((int64_t)total * x / 8) + (int)(blockIdx.x >> 3);
-  if (w >= hi) return;
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+  int n_tiles_done = 0;
+  auto block_prof = [&]() {  // flags & 8 (timing only): per block {start, end, tiles} in 100 MHz ticks
+    if ((a.flags & 8) && a.prof && tid == 0) {
+      a.prof[3 * blockIdx.x] = t_start;
+      a.prof[3 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+      a.prof[3 * blockIdx.x + 2] = (unsigned long long)n_tiles_done;
+    }
+  };
+  if (w >= hi) {
+    block_prof();
+    return;
+  }
   RsItem it = rs_item(a, w);
   int g = it.g0 + wave;
   bool gv = g < it.gend;
@@ -103,25 +126,25 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   // next item's 48 would not fit beside the resident rows)
   const int lane_off = h * 512 + j * 16;
   auto group_rsrc = [&](int grp) {
-    const uint64_t p = reinterpret_cast<uint64_t>(a.groups_h) + (uint64_t)grp * (NB * 512);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
-    const uint32_t hi32 = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
-    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi32 << 32) | lo), 0, NB * 512,
-                                             0x00020000);
+    return uniform_rsrc(reinterpret_cast<const char*>(a.groups_h) + (int64_t)grp * (NB * 512), NB * 512);
   };
   auto ld_rows = [&](__amdgpu_buffer_rsrc_t r, int s) {
     return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(r, lane_off, s * 1024, 0));
   };
+  auto load_norms = [&](int grp, int ip) {
+    __builtin_amdgcn_global_load_lds((gbl_ptr_t)(a.row_norms + (int64_t)grp * kGroupRows + j),
+                                     (lds_ptr_t)(s_norm + (ip * kRsWaves + wave) * 64), 4, 0, 0);
+  };
+  rs_stage<NK>(smem, a.tiles + it.slot * IMG, wave, lane);
+  load_norms(gv ? g : it.g0, 0);
   h8 ra[NK];
   {
     const __amdgpu_buffer_rsrc_t r0 = group_rsrc(gv ? g : it.g0);
 #pragma unroll
     for (int s = 0; s < NK; ++s) ra[s] = ld_rows(r0, s);
   }
-  float nrm = (lane < 32 && gv) ? a.row_norms[(int64_t)g * kGroupRows + lane] : INFINITY;
-  rs_stage<NK>(smem, a.tiles + it.slot * IMG, wave, lane);
   int par = 0;  // LDS buffer of the current tile
-  const float* wnorm = s_norm + wave * 32;
+  int ipar = 0;           // item parity: the s_norm half of this item
   const f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
   for (;;) {
@@ -133,16 +156,22 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
     const int gnx = nx.g0 + wave;
     const bool gvn = has_next && gnx < nx.gend;
     for (int t = 0; t < ntiles; ++t) {
-      if (t == 0 && lane < 32) s_norm[wave * 32 + lane] = nrm;  // own slot: no other wave reads it
-      __builtin_amdgcn_s_waitcnt(0x0F70);                       // vmcnt(0): this wave's DMA of tile t landed
-      __syncthreads();                                          // ... and every other wave's
+      // this wave's DMA of tile t has landed (and, at an item's first tile, its rows: the compiler waits
+      // for them before the first MFMA anyway), then every other wave's
+      __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
+      // raw barrier: __syncthreads()'s fence is the same wait, spelled out above
+      __builtin_amdgcn_s_barrier();
       const bool last = t + 1 == ntiles;
-      // stage the next tile (of this item, or the next item's first) into the other buffer: every
-      // wave has finished reading it (tile t - 1) before the barrier above
-      if (!(a.flags & 2)) {
-        if (!last) rs_stage<NK>(smem + (par ^ 1) * BUF, a.tiles + (it.slot + t + 1) * IMG, wave, lane);
-        else if (has_next) rs_stage<NK>(smem + (par ^ 1) * BUF, a.tiles + nx.slot * IMG, wave, lane);
-      }
+      // the next tile (of this item, or the next item's first) goes into the other buffer: every wave
+      // has finished reading it (tile t - 1) before the barrier above. Its pieces are issued one per
+      // k-step from the second on: issued before the first MFMA, the compiler's wait for the rows there
+      // (vmcnt(0): it cannot order them across the loop) would wait for this DMA too
+      // (a buffer descriptor over the image: no branch per piece; with nothing to stage -- the block's
+      // last tile -- its size is 0 and the loads write zeros to the buffer no tile reads again)
+      const char* simg = !last ? a.tiles + (it.slot + t + 1) * IMG : a.tiles + nx.slot * IMG;
+      const bool stage = (!last || has_next) && !(a.flags & 2);
+      const __amdgpu_buffer_rsrc_t srs = uniform_rsrc(simg, stage ? (int)IMG : 0);
+      char* sbuf = smem + (par ^ 1) * BUF;
       const bool reload = last && has_next;
       const __amdgpu_buffer_rsrc_t nrs = group_rsrc(gvn ? gnx : nx.g0);
       f32x16 acc = zero;
@@ -156,17 +185,24 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
           h8 b2 = b1;
           if (s + 2 < NK) b2 = *reinterpret_cast<const h8*>(bb + (s + 2) * 1024);
           acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s], b0, acc, 0, 0, 0);
-          // last tile: the next item's rows, right after this k-step's last use of the register
+          // last tile: the next item's rows, right after this k-step's last use of the register (its
+          // norms first, with the first k-step)
+          if (s == 0 && reload) load_norms(gvn ? gnx : nx.g0, ipar ^ 1);
           if (reload) ra[s] = ld_rows(nrs, s);
+          if (s >= 1 && (s - 1) * kRsWaves <= NK) {
+            // (past the last piece a wave loads the last one again: the same bytes to the same place)
+            const int p = min((s - 1) * kRsWaves + wave, NK);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(srs, (lds_ptr_t)(sbuf + p * 1024), 16, lane * 16, p * 1024, 0, 0);
+          }
           b0 = b1;
           b1 = b2;
         }
       }
-      if (reload) nrm = (lane < 32 && gvn) ? a.row_norms[(int64_t)gnx * kGroupRows + lane] : INFINITY;
       // epilogue: lane (j, h) holds the 16 dots of query j with rows (r & 3) + 8 (r >> 2) + 4 h
       if (gv && !(a.flags & 1)) {
         // header of query j: {qs, uf, T, q}
         const float4 hd = *reinterpret_cast<const float4*>(smem + par * BUF + NK * 1024 + j * 16);
+        const float* wnorm = s_norm + (ipar * kRsWaves + wave) * 64;
         const float qs = hd.x, uf = hd.y;
         const float mm = METRIC == kL2 ? -2.0f * qs : -qs;
         // one-fma filter over the 16 keys (norms from LDS four at a time: registers are short); the rare
@@ -181,11 +217,16 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
             hits |= (fmaf(acc[4 * q4 + u], mm, METRIC == kL2 ? xv[u] : 0.0f) < uf ? 1u : 0u) << (4 * q4 + u);
         }
         if (__ballot(hits != 0) != 0) {
-          const float T = hd.z;
+          // every filter hit is appended (a superset of the keys <= T_q; the refine's window is below
+          // T_q): one atomic per lane reserves its run of entries, so the latency is paid once per tile
           const int bq = __float_as_int(hd.w);
           const bool qv = bq >= 0 && bq < a.nq;  // (-1: an empty lane of the tile)
-          const float qn = qv ? a.qnorms[bq] : 0.0f;
           if (!qv) hits = 0;
+          const int nh = __popc(hits);
+          int at = 0;
+          if (nh) at = atomicAdd(a.cand_cnt + bq, nh);
+          const float qn = qv ? a.qnorms[bq] : 0.0f;
+          const int64_t base = (int64_t)bq * a.cap;
           while (hits) {
             const int r = __builtin_ctz(hits);
             hits &= hits - 1;
@@ -193,25 +234,25 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
 #pragma unroll
             for (int i = 1; i < 16; ++i) c = r == i ? acc[i] : c;
             const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-            const float k0 = pf_key<METRIC>(c, qs, wnorm[row], qn);
-            if (k0 <= T) {
-              const int at = atomicAdd(a.cand_cnt + bq, 1);
-              if (at < a.cap) {
-                a.cand_key[(int64_t)bq * a.cap + at] = k0;
-                a.cand_pos[(int64_t)bq * a.cap + at] = g * kGroupRows + row;
-              }
+            if (at < a.cap) {
+              a.cand_key[base + at] = pf_key<METRIC>(c, qs, wnorm[row], qn);
+              a.cand_pos[base + at] = g * kGroupRows + row;
             }
+            ++at;
           }
         }
       }
       par ^= 1;
     }
+    n_tiles_done += ntiles;
     if (!has_next) break;
     w = wn;
     it = nx;
     g = gnx;
     gv = gvn;
+    ipar ^= 1;
   }
+  block_prof();
 }
 
 // Work items of K13 from the probe map (chunk = kRsBlockGroups groups, one tile column per list):
@@ -296,7 +337,7 @@ __global__ __launch_bounds__(256) void k_rs_tiles(const int64_t* __restrict__ bu
 
 size_t rs_scan_lds_bytes(int dp) {
   const int nk = dp / 16;
-  return (size_t)2 * (nk * 1024 + 1024) + kRsWaves * 32 * sizeof(float) + 16;
+  return (size_t)2 * (nk * 1024 + 1024) + 2 * kRsWaves * 64 * sizeof(float) + 16;
 }
 
 bool rs_scan_supported(int dp) {
@@ -364,6 +405,40 @@ hipError_t launch_rs_items(const int* work_off, const int* bucket_off, const int
   if (max_items <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_rs_items, dim3((unsigned)ceil_div(max_items, 256)), dim3(256), 0, s, work_off, bucket_off,
                      list_goff, n_lists, max_items, items);
+  return hipGetLastError();
+}
+
+// The pre-pass's lists: list l split into 2l = its first ceil(groups / div) groups (at least min_groups,
+// at most all) and 2l + 1 = the rest, so the n_probes = 1 search of probe 2 p0 scans a sample of the
+// nearest list p0 with the unchanged K10 / probe map (the sample's rows are still rows of the probed
+// lists, so its k-th exact key bounds the final k-th from above)
+__global__ void k_rs_pre_goff(const int64_t* __restrict__ goff, int n_lists, int div, int min_groups,
+                              int64_t* __restrict__ goff2) {
+  const int l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l > n_lists) return;
+  const int64_t b = goff[l];
+  goff2[2 * l] = b;
+  if (l == n_lists) return;
+  const int64_t ng = goff[l + 1] - b;
+  int64_t t = (ng + div - 1) / div;
+  t = t < min_groups ? min_groups : t;
+  goff2[2 * l + 1] = b + (t < ng ? t : ng);
+}
+
+__global__ void k_rs_pre_probes(const int64_t* __restrict__ probes, int64_t nq, int np, int64_t* __restrict__ out) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  const int64_t p = probes[q * np];
+  out[q] = p < 0 ? p : 2 * p;
+}
+
+hipError_t launch_rs_pre_lists(const int64_t* goff, int n_lists, int div, int min_groups, const int64_t* probes,
+                               int64_t nq, int np, int64_t* goff2, int64_t* probes2, hipStream_t s) {
+  if (div < 1 || min_groups < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_rs_pre_goff, dim3((unsigned)ceil_div(n_lists + 1, 256)), dim3(256), 0, s, goff, n_lists, div,
+                     min_groups, goff2);
+  if (nq > 0)
+    hipLaunchKernelGGL(k_rs_pre_probes, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, s, probes, nq, np, probes2);
   return hipGetLastError();
 }
 
