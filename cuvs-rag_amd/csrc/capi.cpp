@@ -87,7 +87,8 @@ struct Workspace {
   // fp16 pre-filter path (K10 / K11) and its exact-scan fallback
   Buf qh, qscale, qres, qtheta, pf_key, pf_pos, pf_bound, pf_stats, ovf_q, ovf_rows, ovf_d, ovf_i;
   // K13 row-stationary scan: the full probe list, the pre-pass result, per-query headers and candidates
-  Buf probes_full, pre_d, pre_i, pre_goff, qhdr, cand_cnt, cand_key, cand_pos, slot_iota, rs_tiles;
+  Buf probes_full, pre_kth, pre_goff, qhdr, cand_off, cand_key, cand_pos, rs_bucket_tmp, rs_tiles, rs_wave_buf,
+      rs_wave_cnt;
   // per-list query counts of the last search's own probe map (an exact fallback re-maps its queries)
   Buf stat_counts, rs_ovf_q, rs_ovf_rows, rs_ovf_d, rs_ovf_i, rs_items;
 };
@@ -144,6 +145,7 @@ struct mivs_index_s {
   int last_np = 0, last_k = 0, last_qtile = kQTile;
   int last_pf = 0;
   int last_scan = 0;  // fine-scan kernel of the last search: 3 K3, 31 K3w, 10 K10, 12 K12, 13 K13
+  int last_rs_waves = 0;  // K13: candidate streams of the last search (the lost flag follows their counts)
   int64_t last_ovf = 0, last_window = 0;
 };
 
@@ -654,17 +656,20 @@ void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t 
                       bool allow_rs = true);
 void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                        int64_t* out_i, bool pf, ProfRec* pr, bool prof, const int64_t* probes = nullptr,
-                       bool allow_rs = true, const int64_t* goff_ov = nullptr, int n_lists_ov = 0);
+                       bool allow_rs = true);
 
 void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                         int64_t* out_i, const float* slot_key, const int* slot_pos, const float* slot_bound,
-                        const int* slot_cnt, const int64_t* slot_begin, int slot_k, bool fallback_pf = false);
+                        const int* force_ovf, const int64_t* slot_begin, int slot_k, bool fallback_pf = false,
+                        float* kth_out = nullptr);
 
 // K10 scan + K11 refine for a probe map built with (kPfChunkGroups, kPfQTile); queries the refine
 // could not prove are re-run through the exact scan and scattered back.
 // (goff / n_lists: another split of the same groups into lists -- K13's pre-pass samples)
+// kth_out: K13's pre-pass -- only the k-th smallest approximate key per query (no refine, no fallback)
 void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
-                    int64_t* out_i, ProfRec* pr, bool use_r, const int64_t* goff, int n_lists) {
+                    int64_t* out_i, ProfRec* pr, bool use_r, const int64_t* goff, int n_lists,
+                    float* kth_out = nullptr) {
   Workspace& ws = idx->ws;
   const ListSet& L = idx->lists;
   const int dp = idx->dp;
@@ -747,14 +752,15 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
               hp[0] / w, hp[1] / w, hp[2] / w, hp[3] / w, hp[4] / w, hp[5], hp[5] ? (double)hp[6] / hp[5] : 0.0);
   }
   pf_refine_fallback(idx, s, q, nq, k, np, out_d, out_i, ws.pf_key.as<float>(), ws.pf_pos.as<int>(),
-                     ws.pf_bound.as<float>(), nullptr, ws.slot_begin.as<int64_t>(), slot_k);
+                     ws.pf_bound.as<float>(), nullptr, ws.slot_begin.as<int64_t>(), slot_k, false, kth_out);
 }
 
 // K11 over the scan's candidate slots, then the exact scan for the queries the refine could not prove
-// (scattered back into out_d / out_i). slot_cnt: K13's per-query candidate counts (slot_bound unused).
+// (scattered back into out_d / out_i). force_ovf (K13): device flag, nonzero -> every query falls back.
 void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                         int64_t* out_i, const float* slot_key, const int* slot_pos, const float* slot_bound,
-                        const int* slot_cnt, const int64_t* slot_begin, int slot_k, bool fallback_pf) {
+                        const int* force_ovf, const int64_t* slot_begin, int slot_k, bool fallback_pf,
+                        float* kth_out) {
   Workspace& ws = idx->ws;
   const ListSet& L = idx->lists;
   const int dp = idx->dp;
@@ -765,7 +771,8 @@ void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_
   r.slot_key = slot_key;
   r.slot_pos = slot_pos;
   r.slot_bound = slot_bound;
-  r.slot_cnt = slot_cnt;
+  r.force_ovf = force_ovf;
+  r.kth_out = kth_out;
   r.slot_begin = slot_begin;
   r.slot_k = slot_k;
   r.nq = nq;
@@ -787,6 +794,7 @@ void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_
   r.ovf_q = ws.ovf_q.as<int64_t>();
   r.n_window = reinterpret_cast<int64_t*>(ws.pf_stats.as<char>() + 8);
   HIPCHK(launch_pf_refine(r, s));
+  if (kth_out) return;
   int64_t h[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(h, ws.pf_stats.p, 16, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));  // the only host sync of the search: the fallback size
@@ -863,9 +871,9 @@ bool rs_use(const mivs_index_s* idx, int np) {
 
 // The K13 search of queries whose probes are in ws.probes_i and norms in ws.qn:
 //   1. pre-pass: each query's nearest list through K10 + K11 -> the exact k-th key there;
-//   2. per-query header {qs, uf, qn, T_q}, T_q >= the final refine window;
+//   2. per-query header {qs, uf, qn, q}: uf is the filter bound for T_q >= the final refine window;
 //   3. probe map in (list, 8-group block) items, one query tile column per list;
-//   4. K13 appends every (approximate key <= T_q, row) to the query's candidate buffer;
+//   4. K13 streams every one-fma filter hit (a superset of the approximate keys <= T_q) per wave;
 //   5. K11 over the buffers + the exact fallback.
 void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                int64_t* out_i, ProfRec* pr) {
@@ -876,28 +884,37 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   ws.probes_full.reserve(sizeof(int64_t) * ne);
   HIPCHK(hipMemcpyAsync(ws.probes_full.p, ws.probes_i.p, sizeof(int64_t) * ne, hipMemcpyDeviceToDevice, s));
   // 1. a sample of the nearest list of every query (probe 0): its first 1/div groups (the rows of a list
-  // are in no particular order), an n_probes = 1 search through K10 / K11 over the split lists
-  ws.pre_d.reserve(sizeof(float) * nq * k);
-  ws.pre_i.reserve(sizeof(int64_t) * nq * k);
+  // are in no particular order) through K10 over the split lists, and the k-th smallest approximate key
+  // of each query's candidates there (K11's first phase only)
   ws.pre_goff.reserve(sizeof(int64_t) * (2 * (size_t)L.n_lists + 1));
   const char* pde = getenv("MIVS_RS_PRE_DIV");
   const int pre_div = std::max(1, pde ? atoi(pde) : kRsPreDiv);
   HIPCHK(launch_rs_pre_lists(L.goff.as<int64_t>(), L.n_lists, pre_div, ceil_div(k, kGroupRows), ws.probes_full.as<int64_t>(),
                              nq, np, ws.pre_goff.as<int64_t>(), ws.probes_i.as<int64_t>(), s));
-  const int64_t keep_ovf = idx->last_ovf, keep_window = idx->last_window;  // stats count the main pass only
-  ivf_search_probed(idx, s, q, nq, k, 1, ws.pre_d.as<float>(), ws.pre_i.as<int64_t>(), true, nullptr, false,
-                    ws.probes_i.as<int64_t>(), false, ws.pre_goff.as<int64_t>(), 2 * L.n_lists);
-  idx->last_ovf = keep_ovf;
-  idx->last_window = keep_window;
-  // the pre-pass's own exact fallback may have reused the norm / fp16 query buffers for its rows
-  HIPCHK(launch_row_norms(q, nq, idx->d, ws.qn.as<float>(), s));
-  HIPCHK(launch_queries_to_half(q, nq, idx->d, dp, idx->hx_exp, ws.qh.as<uint16_t>(), ws.qscale.as<float>(),
-                                ws.qres.as<float>(), s));
-  // 2. headers
+  {
+    const int nl2 = 2 * L.n_lists;
+    ws.counts.reserve(sizeof(int) * nl2);
+    ws.fill.reserve(sizeof(int) * nl2);
+    ws.bucket_off.reserve(sizeof(int) * (nl2 + 1));
+    ws.work_off.reserve(sizeof(int) * (nl2 + 1));
+    ws.bucket_q.reserve(sizeof(int64_t) * nq);
+    ws.bucket_slot.reserve(sizeof(int64_t) * nq);
+    ws.qp_slots.reserve(sizeof(int64_t) * nq);
+    ws.slot_begin.reserve(sizeof(int64_t) * (nq + 1));
+    const size_t stb = scan_tmp_bytes(nq) + sizeof(int64_t) * (size_t)nq;
+    ws.scan_tmp.reserve(stb);
+    HIPCHK(launch_probe_map(ws.probes_i.as<int64_t>(), nq, 1, nl2, ws.pre_goff.as<int64_t>(), idx->pf_G, kPfQTile,
+                            ws.counts.as<int>(), ws.fill.as<int>(), ws.bucket_off.as<int>(), ws.work_off.as<int>(),
+                            ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(), ws.qp_slots.as<int64_t>(),
+                            ws.slot_begin.as<int64_t>(), ws.scan_tmp.p, stb, s));
+    ws.pre_kth.reserve(sizeof(float) * nq);
+    pf_scan_refine(idx, s, q, nq, k, 1, nullptr, nullptr, nullptr, false, ws.pre_goff.as<int64_t>(), nl2,
+                   ws.pre_kth.as<float>());
+  }
+  // 2. headers (pf_scan_refine left the fp16 queries, their scales and residuals in ws.qh / qscale / qres)
   ws.qhdr.reserve(sizeof(float4) * (nq + 1));
-  HIPCHK(launch_rs_headers(ws.pre_d.as<float>(), ws.pre_i.as<int64_t>(), nq, k, ws.qscale.as<float>(),
-                           ws.qn.as<float>(), ws.qres.as<float>(), idx->x_norm_max, idx->x_res_max, dp, idx->metric,
-                           ws.qhdr.as<float4>(), s));
+  HIPCHK(launch_rs_headers(ws.pre_kth.as<float>(), nq, ws.qscale.as<float>(), ws.qn.as<float>(), ws.qres.as<float>(),
+                           idx->x_norm_max, idx->x_res_max, dp, idx->metric, ws.qhdr.as<float4>(), s));
   // 3. probe map: items = (list, block of kRsBlockGroups groups); every query of a list in one tile column
   const size_t stb = scan_tmp_bytes(ne) + sizeof(int64_t) * (size_t)ne;
   ws.scan_tmp.reserve(stb);
@@ -914,10 +931,6 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   HIPCHK(launch_rs_tiles(ws.bucket_q.as<int64_t>(), ws.bucket_off.as<int>(), L.n_lists, ws.qh.as<uint16_t>(),
                          ws.qhdr.as<float4>(), (int)nq, dp, ws.rs_tiles.as<char>(), s));
   // 4. K13
-  ws.cand_cnt.reserve(sizeof(int) * nq);
-  ws.cand_key.reserve(sizeof(float) * (size_t)nq * kRsCap);
-  ws.cand_pos.reserve(sizeof(int) * (size_t)nq * kRsCap);
-  HIPCHK(hipMemsetAsync(ws.cand_cnt.p, 0, sizeof(int) * nq, s));
   int64_t max_items = 0;  // every list probed: the item table's bound (the probe map decides the count)
   for (int l = 0; l < L.n_lists; ++l) max_items += ceil_div(L.h_goff[l + 1] - L.h_goff[l], kRsBlockGroups);
   ws.rs_items.reserve(sizeof(int4) * (size_t)std::max<int64_t>(max_items, 1));
@@ -936,24 +949,27 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   a.qnorms = ws.qn.as<float>();
   a.nq = (int)nq;
   a.metric = idx->metric;
-  a.cap = kRsCap;
-  a.cand_cnt = ws.cand_cnt.as<int>();
-  a.cand_key = ws.cand_key.as<float>();
-  a.cand_pos = ws.cand_pos.as<int>();
+  const int grid = std::max(8, cu_count(idx->device) / 8 * 8);
+  const int n_waves = grid * kRsWaves;
+  idx->last_rs_waves = n_waves;
+  a.wave_cap = (int)std::min<int64_t>(kRsWaveCapMax, std::max<int64_t>(1024, 2 * nq));
+  ws.rs_wave_buf.reserve(sizeof(int4) * (size_t)n_waves * a.wave_cap);
+  ws.rs_wave_cnt.reserve(sizeof(int) * (n_waves + 1));
+  a.wave_buf = ws.rs_wave_buf.as<int4>();
+  a.wave_cnt = ws.rs_wave_cnt.as<int>();
   a.flags = getenv("MIVS_RS_FLAGS") ? atoi(getenv("MIVS_RS_FLAGS")) : 0;
   if (a.flags & 2) a.flags |= 1;  // stale LDS tiles: never run an epilogue on them
-  const int grid = std::max(8, cu_count(idx->device) / 8 * 8);
   Buf pbuf;
-  if (a.flags & 8) {  // diagnostic: per-block clocks to stderr
-    pbuf.reserve(sizeof(unsigned long long) * 3 * grid);
-    HIPCHK(hipMemsetAsync(pbuf.p, 0, sizeof(unsigned long long) * 3 * grid, s));
+  if (a.flags & 24) {  // diagnostic: per-block clocks (8) / per-phase wave-cycles (16) to stderr
+    pbuf.reserve(sizeof(unsigned long long) * (3 * grid + 4));
+    HIPCHK(hipMemsetAsync(pbuf.p, 0, sizeof(unsigned long long) * (3 * grid + 4), s));
     a.prof = pbuf.as<unsigned long long>();
   }
   if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
   HIPCHK(launch_rs_scan(a, dp, grid, s));
   if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
-  if (a.flags & 8) {
-    std::vector<unsigned long long> h(3 * (size_t)grid);
+  if (a.flags & 24) {
+    std::vector<unsigned long long> h(3 * (size_t)grid + 4);
     HIPCHK(hipMemcpyAsync(h.data(), pbuf.p, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     unsigned long long t0 = ~0ull, t1 = 0, tiles_max = 0, tiles_sum = 0;
@@ -969,26 +985,35 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
     }
     fprintf(stderr, "[k13 blocks] span %.1f us | busy mean %.1f max %.1f us | tiles mean %.1f max %llu\n",
             (t1 - t0) / 100.0, busy_sum / grid / 100.0, busy_max / 100.0, (double)tiles_sum / grid, tiles_max);
+    const double wc = (double)(h[3 * grid] + h[3 * grid + 1] + h[3 * grid + 2]);
+    if (wc > 0)
+      fprintf(stderr, "[k13 phases] wave-cycles %.4g | wait+barrier %.3f mfma-loop %.3f epilogue %.3f | "
+              "cycles/tile/wave %.0f\n", wc, h[3 * grid] / wc, h[3 * grid + 1] / wc, h[3 * grid + 2] / wc,
+              tiles_sum ? wc / ((double)tiles_sum * kRsWaves) : 0.0);
   }
-  // 5. exact ranking of the candidates (one slot per query)
-  ws.slot_iota.reserve(sizeof(int64_t) * (nq + 1));
-  HIPCHK(launch_iota_i64(ws.slot_iota.as<int64_t>(), nq + 1, 0, 1, s));
+  // the streams into per-query CSR runs (every stream entry fits: at most n_waves * wave_cap of them)
+  const size_t max_cand = (size_t)n_waves * a.wave_cap;
+  ws.cand_off.reserve(sizeof(int64_t) * (nq + 1));
+  ws.cand_key.reserve(sizeof(float) * max_cand);
+  ws.cand_pos.reserve(sizeof(int) * max_cand);
+  ws.rs_bucket_tmp.reserve(rs_bucket_tmp_bytes((int)nq));
+  HIPCHK(hipMemsetAsync(a.wave_cnt + n_waves, 0, sizeof(int), s));
+  HIPCHK(launch_rs_bucket(a.wave_buf, a.wave_cap, a.wave_cnt, n_waves, (int)nq, ws.cand_off.as<int64_t>(),
+                          ws.cand_key.as<float>(), ws.cand_pos.as<int>(), ws.rs_bucket_tmp.p, a.wave_cnt + n_waves, s));
+  // 5. exact ranking of every query's run (slot = one entry)
   pf_refine_fallback(idx, s, q, nq, k, np, out_d, out_i, ws.cand_key.as<float>(), ws.cand_pos.as<int>(), nullptr,
-                     ws.cand_cnt.as<int>(), ws.slot_iota.as<int64_t>(), kRsCap, true);
+                     a.wave_cnt + n_waves, ws.cand_off.as<int64_t>(), 1, true);
 }
 
 void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
-                       int64_t* out_i, bool pf, ProfRec* pr, bool prof, const int64_t* probes, bool allow_rs,
-                       const int64_t* goff_ov, int n_lists_ov) {
+                       int64_t* out_i, bool pf, ProfRec* pr, bool prof, const int64_t* probes, bool allow_rs) {
   Workspace& ws = idx->ws;
   if (!probes) probes = ws.probes_i.as<int64_t>();
   // probe map
   const ListSet& L = idx->lists;
   const int64_t ne = nq * np;
-  // (a list split overriding the index's: the pre-filter scan only, n_probes = 1)
-  require(!goff_ov || (pf && np == 1), "list override outside the pre-pass", MIVS_ERR_INVALID);
-  const int n_lists = goff_ov ? n_lists_ov : L.n_lists;
-  const int64_t* goff = goff_ov ? goff_ov : L.goff.as<int64_t>();
+  const int n_lists = L.n_lists;
+  const int64_t* goff = L.goff.as<int64_t>();
   ws.counts.reserve(sizeof(int) * n_lists);
   ws.fill.reserve(sizeof(int) * n_lists);
   ws.bucket_off.reserve(sizeof(int) * (n_lists + 1));
@@ -1006,7 +1031,7 @@ void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t
     idx->last_qtile = qtile;
     idx->last_pf = pf ? 1 : 0;
   }
-  if (pf && allow_rs && !goff_ov && rs_use(idx, np)) {
+  if (pf && allow_rs && rs_use(idx, np)) {
     if (prof) {
       idx->last_qtile = kRsQTile;
       idx->last_scan = 13;
@@ -1789,13 +1814,14 @@ int32_t mivs_index_last_search_stats(mivs_index_t idx, mivs_search_stats* out) {
         st.work_items = 0;
         for (int l = 0; l < L.n_lists; ++l)
           if (counts[l] > 0) st.work_items += ceil_div(L.h_goff[l + 1] - L.h_goff[l], kRsBlockGroups);
-        // the candidates K13 appended (some beyond a query's buffer when it overflowed)
-        std::vector<int> cc(idx->last_nq);
-        HIPCHK(hipMemcpy(cc.data(), idx->ws.cand_cnt.p, sizeof(int) * cc.size(), hipMemcpyDeviceToHost));
-        for (int v : cc) {
-          st.candidates += v;
-          st.cand_overflow += v > kRsCap ? 1 : 0;
-        }
+        // the candidates K13 appended; a lost stream entry sends every query to the fallback
+        int64_t total = 0;
+        int lost = 0;
+        HIPCHK(hipMemcpy(&total, idx->ws.cand_off.as<int64_t>() + idx->last_nq, sizeof(int64_t),
+                         hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&lost, idx->ws.rs_wave_cnt.as<int>() + idx->last_rs_waves, sizeof(int), hipMemcpyDeviceToHost));
+        st.candidates = total;
+        st.cand_overflow = lost ? idx->last_nq : 0;
       }
     } else if (idx->last_nq > 0) {
       // brute force: the pre-filter scan (K10) works in pf_G-group chunks, the exact scans in G

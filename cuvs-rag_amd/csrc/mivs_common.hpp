@@ -201,7 +201,8 @@ constexpr int kRsQTile = 32;
 constexpr int kRsBlockGroups = kRsWaves;
 // K13's pre-pass scans the first 1 / kRsPreDiv of each query's nearest list (MIVS_RS_PRE_DIV)
 constexpr int kRsPreDiv = 4;
-constexpr int kRsCap = 4096;  // candidate buffer entries per query (more: the K10 fallback)
+constexpr int kRsWaveCapMax = 16384;  // entries of a K13 wave's candidate stream (more: all queries fall back)
+
 struct RsScanArgs {
   const uint16_t* groups_h;  // fp16 lists, group layout [g][dp/8][32][8]
   const float* row_norms;    // pinned fp32 norms (+inf on pad rows)
@@ -215,10 +216,9 @@ struct RsScanArgs {
   const float* qnorms;       // [nq] pinned fp32 query norms (exact key of a candidate)
   int nq;
   int metric;
-  int cap;
-  int* cand_cnt;             // [nq] zeroed before launch
-  float* cand_key;           // [nq][cap]
-  int* cand_pos;             // [nq][cap]
+  int4* wave_buf;            // [grid * kRsWaves][wave_cap] per-wave candidate streams {key bits, pos, query, 0}
+  int wave_cap;
+  int* wave_cnt;             // [grid * kRsWaves] stream lengths (may exceed wave_cap: entries lost)
   int flags;                 // timing experiments only (MIVS_RS_FLAGS): 1 skip epilogue, 2 skip staging,
                              // 8 per-block clocks into prof
   unsigned long long* prof;  // flags & 8: [grid][3] {start, end, tiles}
@@ -263,8 +263,9 @@ struct PfRefineArgs {
   const int64_t* qrows;       // optional: query q is row qrows[q] of queries / qnorms / qres (k-means trainset)
   int labels_only;            // k = 1: a window of ONE candidate is the answer without its exact key
                               // (out_d then holds its approximate key)
-  const int* slot_cnt;        // optional (K13): entries per slot, unsorted; > slot_k: overflow. slot_bound
-                              // may then be nullptr
+  const int* force_ovf;       // optional (K13): nonzero -> no query is provable (candidates were lost)
+  float* kth_out;             // optional (K13's pre-pass): only the k-th smallest approximate key per query
+                              // (+inf: fewer than k candidates), no refine
 };
 
 hipError_t launch_pf_scan(const PfScanArgs& a, int grid, size_t lds, hipStream_t s);
@@ -284,15 +285,20 @@ size_t rs_scan_lds_bytes(int dp);
 bool rs_scan_supported(int dp);
 hipError_t launch_rs_scan(const RsScanArgs& a, int dp, int grid, hipStream_t s);
 int64_t rs_tiles_bytes(int64_t ne, int n_lists, int dp);
+// K13's per-wave candidate streams -> per-query CSR runs (cand_off [nq + 1]); work: [nq + 1] int64 counts,
+// [nq] int fill, scan tmp (scan_tmp_bytes(nq + 1)); lost: set when a stream overflowed
+size_t rs_bucket_tmp_bytes(int nq);
+hipError_t launch_rs_bucket(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
+                            int64_t* cand_off, float* cand_key, int* cand_pos, void* tmp, int* lost, hipStream_t s);
 hipError_t launch_rs_pre_lists(const int64_t* goff, int n_lists, int div, int min_groups, const int64_t* probes,
                                int64_t nq, int np, int64_t* goff2, int64_t* probes2, hipStream_t s);
 hipError_t launch_rs_items(const int* work_off, const int* bucket_off, const int64_t* list_goff, int n_lists,
                            int max_items, int4* items, hipStream_t s);
 hipError_t launch_rs_tiles(const int64_t* bucket_q, const int* bucket_off, int n_lists, const uint16_t* qh,
                            const float4* qhdr, int nq, int dp, char* tiles, hipStream_t s);
-hipError_t launch_rs_headers(const float* pre_d, const int64_t* pre_i, int64_t nq, int k, const float* qscale,
-                             const float* qnorms, const float* qres, float x_norm_max, float x_res_max, int dp,
-                             int metric, float4* hdr, hipStream_t s);
+hipError_t launch_rs_headers(const float* pre_kth, int64_t nq, const float* qscale, const float* qnorms,
+                             const float* qres, float x_norm_max, float x_res_max, int dp, int metric, float4* hdr,
+                             hipStream_t s);
 hipError_t launch_gather_ids(const int64_t* src, const int64_t* idx, int64_t n, int64_t* out, hipStream_t s);
 constexpr unsigned kPfOrdInf = 0xFF800000u;  // order mapping of +inf (qtheta's initial value)
 // fp32 groups -> fp16 groups scaled by 2^hx_exp (FTZ below the fp16 normal range), per-index maxima of

@@ -575,15 +575,9 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
   const int k = a.k;
   int64_t sb = 0, se = 0;
   if (live) { sb = a.slot_begin[q]; se = a.slot_begin[q + 1]; }
-  int64_t c1 = se * a.slot_k;
-  // K13 candidate buffers (slot_cnt): one slot per query holding slot_cnt[q] unsorted entries; more than
-  // slot_k of them means some were not stored: the query cannot be proven
-  bool cnt_ovf = false;
-  if (a.slot_cnt && live) {
-    const int n = a.slot_cnt[q];
-    cnt_ovf = n > a.slot_k;
-    c1 = sb * a.slot_k + (n < a.slot_k ? n : a.slot_k);
-  }
+  const int64_t c1 = se * a.slot_k;
+  // (K13: slot_k = 1 and slot_begin the per-query CSR runs of unsorted candidates)
+  const bool cnt_ovf = a.force_ovf && *a.force_ovf;
 
   // phase 1: Ak = k-th smallest approximate key (running top-k over the lanes, K7's ballot insertion)
   float mk = INFINITY, tk = INFINITY;
@@ -602,6 +596,10 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
       mask &= ~(1ull << b);
       mask &= __ballot(ck < tk);
     }
+  }
+  if (a.kth_out) {  // (kernel-uniform: every wave of the block leaves here)
+    if (live && lane == 0) a.kth_out[q] = tk;
+    return;
   }
   float bmin = cnt_ovf ? -INFINITY : INFINITY;
   if (a.slot_bound)
@@ -1398,7 +1396,7 @@ hipError_t launch_pr_scan(const PfScanArgs& a, int grid, hipStream_t s) {
 hipError_t launch_pf_refine(const PfRefineArgs& a, hipStream_t s) {
   if (a.k < 1 || a.k > kPfMaxK || a.dp > 1024) return hipErrorInvalidValue;
   if (a.nq <= 0) return hipSuccess;
-  if (a.k == 1 && a.slot_k % 4 == 0 && a.slot_cnt == nullptr && a.slot_bound != nullptr) {  // lane per query
+  if (a.k == 1 && a.slot_k % 4 == 0 && a.force_ovf == nullptr && a.slot_bound != nullptr) {  // lane per query
     if (a.metric == kIP) hipLaunchKernelGGL(k_pf_refine1<kIP>, pf_grid(a.nq, 256), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_pf_refine1<kL2>, pf_grid(a.nq, 256), dim3(256), 0, s, a);
     return hipGetLastError();

@@ -65,6 +65,39 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const char* p, in
   return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
 }
 
+// LDS-DMA the compiler does not see. Its wait-count pass puts vmcnt(0) before any LDS read that follows
+// an LDS-DMA it knows of (it cannot tell the DMA's target from the buffer being read), which made every
+// epilogue wait for the NEXT tile's DMA and, at an item's last tile, for the next item's rows. These
+// copies are ordered by the kernel's own s_waitcnt vmcnt(0) + barrier at each tile start instead (the
+// only point where their data is read). The hardware counter still counts them, so the compiler's own
+// counted waits can only wait longer, never less.
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+// buffer descriptor (raw, 4 SGPRs) over [p, p + bytes) for a wave-uniform p
+__device__ __forceinline__ v4i uniform_desc(const void* p, int bytes) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  v4i r;
+  r.x = (int)__builtin_amdgcn_readfirstlane((uint32_t)v);
+  r.y = (int)(__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) & 0xFFFFu);
+  r.z = __builtin_amdgcn_readfirstlane(bytes);
+  r.w = 0x00020000;
+  return r;
+}
+
+// 64 lanes x 16 B from desc + voff (per lane) + soff to LDS lds + 16 lane
+__device__ __forceinline__ void dma_b128(v4i desc, const void* lds, int voff, int soff) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(lds));
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               :: "s"(m0), "v"(voff), "s"(desc), "s"(soff) : "memory");
+}
+
+// 64 lanes x 4 B from desc + voff (per lane) to LDS lds + 4 lane
+__device__ __forceinline__ void dma_b32(v4i desc, const void* lds, int voff) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(lds));
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds"
+               :: "s"(m0), "v"(voff), "s"(desc) : "memory");
+}
+
 template <int NK>
 __device__ __forceinline__ void rs_stage(char* buf, const char* img, int wave, int lane) {
 #pragma unroll
@@ -79,6 +112,11 @@ __device__ __forceinline__ void rs_stage(char* buf, const char* img, int wave, i
 __device__ __forceinline__ int64_t rs_tile_slot(const int* bucket_off, int l, int t) {
   return (int64_t)(bucket_off[l] / kRsQTile) + l + t;
 }
+
+template <bool B>
+struct BoolC {
+  static constexpr bool value = B;
+};
 
 template <int METRIC, int NK>
 __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
@@ -105,11 +143,22 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   int w = (int)((int64_t)total * x / 8) + (int)(blockIdx.x >> 3);
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
   int n_tiles_done = 0;
-  auto block_prof = [&]() {  // flags & 8 (timing only): per block {start, end, tiles} in 100 MHz ticks
+  uint64_t pw_wait = 0, pw_loop = 0, pw_epi = 0;  // flags & 16: this wave's cycles per tile phase
+  const int widx = blockIdx.x * kRsWaves + wave;
+  int4* const wstream = a.wave_buf + (int64_t)widx * a.wave_cap;
+  int wcnt = 0;  // entries of this wave's candidate stream
+  auto block_prof = [&]() {
+    if (lane == 0) a.wave_cnt[widx] = wcnt;  // (timing only) flags & 8: per block {start, end, tiles} in 100 MHz ticks
     if ((a.flags & 8) && a.prof && tid == 0) {
       a.prof[3 * blockIdx.x] = t_start;
       a.prof[3 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
       a.prof[3 * blockIdx.x + 2] = (unsigned long long)n_tiles_done;
+    }
+    if ((a.flags & 16) && a.prof && lane == 0) {  // flags & 16: [3 grid + 0..2] wave-cycles summed
+      unsigned long long* p = a.prof + 3 * gridDim.x;
+      atomicAdd(p + 0, (unsigned long long)pw_wait);
+      atomicAdd(p + 1, (unsigned long long)pw_loop);
+      atomicAdd(p + 2, (unsigned long long)pw_epi);
     }
   };
   if (w >= hi) {
@@ -132,8 +181,8 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
     return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(r, lane_off, s * 1024, 0));
   };
   auto load_norms = [&](int grp, int ip) {
-    __builtin_amdgcn_global_load_lds((gbl_ptr_t)(a.row_norms + (int64_t)grp * kGroupRows + j),
-                                     (lds_ptr_t)(s_norm + (ip * kRsWaves + wave) * 64), 4, 0, 0);
+    dma_b32(uniform_desc(a.row_norms + (int64_t)grp * kGroupRows, kGroupRows * 4), s_norm + (ip * kRsWaves + wave) * 64,
+            j * 4);
   };
   rs_stage<NK>(smem, a.tiles + it.slot * IMG, wave, lane);
   load_norms(gv ? g : it.g0, 0);
@@ -158,9 +207,11 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
     for (int t = 0; t < ntiles; ++t) {
       // this wave's DMA of tile t has landed (and, at an item's first tile, its rows: the compiler waits
       // for them before the first MFMA anyway), then every other wave's
+      const uint64_t ph0 = (a.flags & 16) ? __builtin_amdgcn_s_memtime() : 0;
       __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
       // raw barrier: __syncthreads()'s fence is the same wait, spelled out above
       __builtin_amdgcn_s_barrier();
+      const uint64_t ph1 = (a.flags & 16) ? __builtin_amdgcn_s_memtime() : 0;
       const bool last = t + 1 == ntiles;
       // the next tile (of this item, or the next item's first) goes into the other buffer: every wave
       // has finished reading it (tile t - 1) before the barrier above. Its pieces are issued one per
@@ -170,38 +221,47 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
       // last tile -- its size is 0 and the loads write zeros to the buffer no tile reads again)
       const char* simg = !last ? a.tiles + (it.slot + t + 1) * IMG : a.tiles + nx.slot * IMG;
       const bool stage = (!last || has_next) && !(a.flags & 2);
-      const __amdgpu_buffer_rsrc_t srs = uniform_rsrc(simg, stage ? (int)IMG : 0);
+      const v4i sdesc = uniform_desc(simg, stage ? (int)IMG : 0);
       char* sbuf = smem + (par ^ 1) * BUF;
       const bool reload = last && has_next;
       const __amdgpu_buffer_rsrc_t nrs = group_rsrc(gvn ? gnx : nx.g0);
       f32x16 acc = zero;
-      {
-        // (a wave without a group in this block runs the MFMAs on stale rows; its epilogue is skipped)
+      float4 hd;  // this tile's header for query j, read during the last k-steps
+      // (a wave without a group in this block runs the MFMAs on stale rows; its epilogue is skipped).
+      // Two copies of the k-loop, with and without the next item's row loads, so no k-step branches.
+      auto kloop = [&](auto reload_c) __attribute__((always_inline)) {
+        constexpr bool RL = decltype(reload_c)::value;
         const char* bb = smem + par * BUF + lane * 16;
-        h8 b0 = *reinterpret_cast<const h8*>(bb);
-        h8 b1 = *reinterpret_cast<const h8*>(bb + 1024);
+        h8 b[4];  // B operands three k-steps ahead
+#pragma unroll
+        for (int u = 0; u < 3; ++u) b[u] = *reinterpret_cast<const h8*>(bb + (u < NK ? u : 0) * 1024);
 #pragma unroll
         for (int s = 0; s < NK; ++s) {
-          h8 b2 = b1;
-          if (s + 2 < NK) b2 = *reinterpret_cast<const h8*>(bb + (s + 2) * 1024);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s], b0, acc, 0, 0, 0);
-          // last tile: the next item's rows, right after this k-step's last use of the register (its
-          // norms first, with the first k-step)
-          if (s == 0 && reload) load_norms(gvn ? gnx : nx.g0, ipar ^ 1);
-          if (reload) ra[s] = ld_rows(nrs, s);
+          if (s + 3 < NK) b[(s + 3) & 3] = *reinterpret_cast<const h8*>(bb + (s + 3) * 1024);
+          if (s == (NK > 3 ? NK - 3 : 0)) hd = *reinterpret_cast<const float4*>(smem + par * BUF + NK * 1024 + j * 16);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s], b[s & 3], acc, 0, 0, 0);
+          if constexpr (RL) {
+            // the next item's rows, right after this k-step's last use of the register (its norms
+            // first, with the first k-step)
+            if (s == 0) load_norms(gvn ? gnx : nx.g0, ipar ^ 1);
+            ra[s] = ld_rows(nrs, s);
+          }
           if (s >= 1 && (s - 1) * kRsWaves <= NK) {
             // (past the last piece a wave loads the last one again: the same bytes to the same place)
             const int p = min((s - 1) * kRsWaves + wave, NK);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(srs, (lds_ptr_t)(sbuf + p * 1024), 16, lane * 16, p * 1024, 0, 0);
+            dma_b128(sdesc, sbuf + p * 1024, lane * 16, p * 1024);
           }
-          b0 = b1;
-          b1 = b2;
+          // keep each k-step's operations in their k-step: left alone, the scheduler sinks the B reads
+          // next to their MFMAs (one exposed LDS latency per k-step)
+          __builtin_amdgcn_sched_barrier(0);
         }
-      }
+      };
+      if (reload) kloop(BoolC<true>{});
+      else kloop(BoolC<false>{});
+      const uint64_t ph2 = (a.flags & 16) ? __builtin_amdgcn_s_memtime() : 0;
       // epilogue: lane (j, h) holds the 16 dots of query j with rows (r & 3) + 8 (r >> 2) + 4 h
       if (gv && !(a.flags & 1)) {
-        // header of query j: {qs, uf, T, q}
-        const float4 hd = *reinterpret_cast<const float4*>(smem + par * BUF + NK * 1024 + j * 16);
+        // header of query j: {qs, uf, qn, q}
         const float* wnorm = s_norm + (ipar * kRsWaves + wave) * 64;
         const float qs = hd.x, uf = hd.y;
         const float mm = METRIC == kL2 ? -2.0f * qs : -qs;
@@ -217,30 +277,36 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
             hits |= (fmaf(acc[4 * q4 + u], mm, METRIC == kL2 ? xv[u] : 0.0f) < uf ? 1u : 0u) << (4 * q4 + u);
         }
         if (__ballot(hits != 0) != 0) {
-          // every filter hit is appended (a superset of the keys <= T_q; the refine's window is below
-          // T_q): one atomic per lane reserves its run of entries, so the latency is paid once per tile
+          // every filter hit (a superset of the keys <= T_q; the refine's window is below T_q) goes to
+          // this wave's stream -- positions by ballot prefix, no atomics; k_rs_bucket sorts the
+          // streams into per-query buffers
           const int bq = __float_as_int(hd.w);
           const bool qv = bq >= 0 && bq < a.nq;  // (-1: an empty lane of the tile)
           if (!qv) hits = 0;
-          const int nh = __popc(hits);
-          int at = 0;
-          if (nh) at = atomicAdd(a.cand_cnt + bq, nh);
-          const float qn = qv ? a.qnorms[bq] : 0.0f;
-          const int64_t base = (int64_t)bq * a.cap;
-          while (hits) {
-            const int r = __builtin_ctz(hits);
+          const float qn = hd.z;
+          while (__ballot(hits != 0) != 0) {
+            const bool has = hits != 0;
+            const int r = has ? __builtin_ctz(hits) : 0;
             hits &= hits - 1;
             float c = acc[0];
 #pragma unroll
             for (int i = 1; i < 16; ++i) c = r == i ? acc[i] : c;
             const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (at < a.cap) {
-              a.cand_key[base + at] = pf_key<METRIC>(c, qs, wnorm[row], qn);
-              a.cand_pos[base + at] = g * kGroupRows + row;
-            }
-            ++at;
+            const uint64_t m = __ballot(has);
+            const int at = wcnt + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (has && at < a.wave_cap)
+              wstream[at] = make_int4(__float_as_int(pf_key<METRIC>(c, qs, wnorm[row], qn)), g * kGroupRows + row,
+                                      bq, 0);
+            wcnt += __popcll(m);
           }
         }
+      }
+      if (a.flags & 16) {
+        const uint64_t ph3 = __builtin_amdgcn_s_memtime();
+        pw_wait += ph1 - ph0;
+        pw_loop += ph2 - ph1;
+        pw_epi += ph3 - ph2;
       }
       par ^= 1;
     }
@@ -272,13 +338,12 @@ __global__ void k_rs_items(const int* __restrict__ work_off, const int* __restri
   items[w] = make_int4((int)g0, (int)ge, (int)rs_tile_slot(bucket_off, lo, 0), (m + kRsQTile - 1) / kRsQTile);
 }
 
-// per query: {qs, uf, qn, T} for K13 from the pre-pass's exact k-th key over the query's nearest list;
-// row nq = the null header (matches nothing)
+// per query: {qs, uf, qn, q} for K13 (uf carries T_q: the one-fma filter bound for the exact k-th key over the
+// sample of the nearest list from the pre-pass, widened by the refine window); row nq = the null header
 template <int METRIC>
-__global__ void k_rs_headers(const float* __restrict__ pre_d, const int64_t* __restrict__ pre_i, int64_t nq, int k,
-                             const float* __restrict__ qscale, const float* __restrict__ qnorms,
-                             const float* __restrict__ qres, float x_norm_max, float x_res_max, int dp,
-                             float4* __restrict__ hdr) {
+__global__ void k_rs_headers(const float* __restrict__ pre_kth, int64_t nq, const float* __restrict__ qscale,
+                             const float* __restrict__ qnorms, const float* __restrict__ qres, float x_norm_max,
+                             float x_res_max, int dp, float4* __restrict__ hdr) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q > nq) return;
   if (q == nq) {  // the null header
@@ -288,17 +353,18 @@ __global__ void k_rs_headers(const float* __restrict__ pre_d, const int64_t* __r
   const float qn = qnorms[q];
   const float delta = pf_delta<METRIC>(qn, qres[q], x_norm_max, x_res_max, dp);
   float T = INFINITY;
-  if (pre_i[q * k + k - 1] >= 0) {
-    const float d = pre_d[q * k + k - 1];
-    const float kth = METRIC == kL2 ? d : -d;  // the exact key of the k-th neighbour in that list
-    // k rows have approximate keys <= kth + delta, so the final k-th approximate key Ak <= U and the
-    // final window pf_window(Ak) <= pf_window(U) (monotone); one more relative step covers the roundings
-    const float U = kth + delta;
+  const float kth = pre_kth[q];  // the k-th smallest approximate key (K10's) over the sample rows
+  if (kth < INFINITY) {
+    // those k rows are probed rows: their pinned keys are <= kth + delta, so the final k-th approximate key
+    // (K13's sums may round differently from K10's: each is within delta of the pinned key) is
+    // Ak <= U = kth + 2 delta, and the final window pf_window(Ak) <= pf_window(U) (monotone); one more
+    // relative step covers the roundings of U and T
+    const float U = kth + 2.0f * delta;
     T = pf_window(U, delta);
     T = T + fabsf(T) * 0x1p-20f + 1e-30f;
   }
   const float uf = pf_uf<METRIC>(INFINITY, T, qn, x_norm_max * x_norm_max);
-  hdr[q] = make_float4(qscale[q], uf, T, __int_as_float((int)q));
+  hdr[q] = make_float4(qscale[q], uf, qn, __int_as_float((int)q));  // (T itself is only in uf)
 }
 
 // Tile images for K13: per list l with m_l queries, ceil(m_l / 32) tiles of [NK + 1] x 1 KiB: piece
@@ -337,6 +403,7 @@ __global__ __launch_bounds__(256) void k_rs_tiles(const int64_t* __restrict__ bu
 
 size_t rs_scan_lds_bytes(int dp) {
   const int nk = dp / 16;
+  // two tile buffers + the norms: [2 items][8 waves][64]
   return (size_t)2 * (nk * 1024 + 1024) + 2 * kRsWaves * 64 * sizeof(float) + 16;
 }
 
@@ -408,6 +475,60 @@ hipError_t launch_rs_items(const int* work_off, const int* bucket_off, const int
   return hipGetLastError();
 }
 
+constexpr int kRsBucketSplit = 8;
+
+// K13's per-wave candidate streams -> per-query CSR runs for K11 (count, scan, scatter). A stream longer
+// than its capacity lost entries of unknown queries: `lost` is then set and K11 proves no query (every
+// query goes to the fallback search).
+__global__ __launch_bounds__(256) void k_rs_count(const int4* __restrict__ wave_buf, int wave_cap,
+                                                  const int* __restrict__ wave_cnt,
+                                                  unsigned long long* __restrict__ qcnt, int* __restrict__ lost) {
+  // (kRsBucketSplit blocks per stream: the streams' lengths differ by orders of magnitude)
+  const int w = blockIdx.x / kRsBucketSplit, sub = blockIdx.x % kRsBucketSplit;
+  const int n = wave_cnt[w];
+  if (n > wave_cap && sub == 0 && threadIdx.x == 0) atomicOr(lost, 1);
+  const int4* ws = wave_buf + (int64_t)w * wave_cap;
+  for (int i = sub * blockDim.x + threadIdx.x; i < (n < wave_cap ? n : wave_cap); i += kRsBucketSplit * blockDim.x)
+    atomicAdd(qcnt + ws[i].z, 1ull);
+}
+
+__global__ __launch_bounds__(256) void k_rs_scatter(const int4* __restrict__ wave_buf, int wave_cap,
+                                                    const int* __restrict__ wave_cnt, const int64_t* __restrict__ off,
+                                                    int* __restrict__ fill, float* __restrict__ key,
+                                                    int* __restrict__ pos) {
+  const int w = blockIdx.x / kRsBucketSplit, sub = blockIdx.x % kRsBucketSplit;
+  const int n = wave_cnt[w];
+  const int4* ws = wave_buf + (int64_t)w * wave_cap;
+  for (int i = sub * blockDim.x + threadIdx.x; i < (n < wave_cap ? n : wave_cap); i += kRsBucketSplit * blockDim.x) {
+    const int4 e = ws[i];
+    const int64_t at = off[e.z] + atomicAdd(fill + e.z, 1);
+    key[at] = __int_as_float(e.x);
+    pos[at] = e.y;
+  }
+}
+
+size_t rs_bucket_tmp_bytes(int nq) {
+  return sizeof(int64_t) * ((size_t)nq + 1) + sizeof(int) * (size_t)nq + scan_tmp_bytes(nq + 1) + 64;
+}
+
+hipError_t launch_rs_bucket(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
+                            int64_t* cand_off, float* cand_key, int* cand_pos, void* tmp, int* lost, hipStream_t s) {
+  int64_t* qcnt = static_cast<int64_t*>(tmp);
+  int* fill = reinterpret_cast<int*>(qcnt + nq + 1);
+  void* stmp = reinterpret_cast<char*>(tmp) + ((sizeof(int64_t) * ((size_t)nq + 1) + sizeof(int) * (size_t)nq + 15) & ~(size_t)15);
+  hipError_t e = hipMemsetAsync(qcnt, 0, sizeof(int64_t) * ((size_t)nq + 1) + sizeof(int) * (size_t)nq, s);
+  if (e != hipSuccess) return e;
+  if (n_waves > 0)
+    hipLaunchKernelGGL(k_rs_count, dim3((unsigned)n_waves * kRsBucketSplit), dim3(256), 0, s, wave_buf, wave_cap, wave_cnt,
+                       reinterpret_cast<unsigned long long*>(qcnt), lost);
+  e = launch_exclusive_scan_i64(qcnt, cand_off, nq + 1, stmp, s);
+  if (e != hipSuccess) return e;
+  if (n_waves > 0)
+    hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)n_waves * kRsBucketSplit), dim3(256), 0, s, wave_buf, wave_cap, wave_cnt, cand_off,
+                       fill, cand_key, cand_pos);
+  return hipGetLastError();
+}
+
 // The pre-pass's lists: list l split into 2l = its first ceil(groups / div) groups (at least min_groups,
 // at most all) and 2l + 1 = the rest, so the n_probes = 1 search of probe 2 p0 scans a sample of the
 // nearest list p0 with the unchanged K10 / probe map (the sample's rows are still rows of the probed
@@ -442,16 +563,16 @@ hipError_t launch_rs_pre_lists(const int64_t* goff, int n_lists, int div, int mi
   return hipGetLastError();
 }
 
-hipError_t launch_rs_headers(const float* pre_d, const int64_t* pre_i, int64_t nq, int k, const float* qscale,
-                             const float* qnorms, const float* qres, float x_norm_max, float x_res_max, int dp,
-                             int metric, float4* hdr, hipStream_t s) {
+hipError_t launch_rs_headers(const float* pre_kth, int64_t nq, const float* qscale, const float* qnorms,
+                             const float* qres, float x_norm_max, float x_res_max, int dp, int metric, float4* hdr,
+                             hipStream_t s) {
   const dim3 grid((unsigned)ceil_div(nq + 1, 256));
   if (metric == kIP)
-    hipLaunchKernelGGL(k_rs_headers<kIP>, grid, dim3(256), 0, s, pre_d, pre_i, nq, k, qscale, qnorms, qres,
-                       x_norm_max, x_res_max, dp, hdr);
+    hipLaunchKernelGGL(k_rs_headers<kIP>, grid, dim3(256), 0, s, pre_kth, nq, qscale, qnorms, qres, x_norm_max,
+                       x_res_max, dp, hdr);
   else
-    hipLaunchKernelGGL(k_rs_headers<kL2>, grid, dim3(256), 0, s, pre_d, pre_i, nq, k, qscale, qnorms, qres,
-                       x_norm_max, x_res_max, dp, hdr);
+    hipLaunchKernelGGL(k_rs_headers<kL2>, grid, dim3(256), 0, s, pre_kth, nq, qscale, qnorms, qres, x_norm_max,
+                       x_res_max, dp, hdr);
   return hipGetLastError();
 }
 
