@@ -1396,7 +1396,7 @@ hipError_t launch_pr_scan(const PfScanArgs& a, int grid, hipStream_t s) {
 hipError_t launch_pf_refine(const PfRefineArgs& a, hipStream_t s) {
   if (a.k < 1 || a.k > kPfMaxK || a.dp > 1024) return hipErrorInvalidValue;
   if (a.nq <= 0) return hipSuccess;
-  if (a.k == 1 && a.slot_k % 4 == 0 && a.force_ovf == nullptr && a.slot_bound != nullptr) {  // lane per query
+  if (a.k == 1 && a.slot_k % 4 == 0 && a.force_ovf == nullptr && a.kth_out == nullptr && a.slot_bound != nullptr) {  // lane per query
     if (a.metric == kIP) hipLaunchKernelGGL(k_pf_refine1<kIP>, pf_grid(a.nq, 256), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_pf_refine1<kL2>, pf_grid(a.nq, 256), dim3(256), 0, s, a);
     return hipGetLastError();

@@ -38,10 +38,6 @@ typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 
 constexpr int kRsThreads = kRsWaves * 64;
 
-// one wave-instruction of LDS-DMA: 64 lanes x 16 B from per-lane global addresses to lds + lane * 16
-__device__ __forceinline__ void rs_glds(const void* g, char* lds) {
-  __builtin_amdgcn_global_load_lds((gbl_ptr_t)g, (lds_ptr_t)lds, 16, 0, 0);
-}
 
 // a work item: {first group, end group, first tile slot, tiles} (k_rs_items)
 struct RsItem {
@@ -98,20 +94,52 @@ __device__ __forceinline__ void dma_b32(v4i desc, const void* lds, int voff) {
                :: "s"(m0), "v"(voff), "s"(desc) : "memory");
 }
 
-template <int NK>
-__device__ __forceinline__ void rs_stage(char* buf, const char* img, int wave, int lane) {
-#pragma unroll
-  for (int p0 = 0; p0 <= NK; p0 += kRsWaves) {
-    const int p = p0 + wave;
-    if (p <= NK) rs_glds(img + p * 1024 + lane * 16, buf + p * 1024);
-  }
-}
 
 // the image of tile t of list l: tiles of list l start at bucket_off[l] / 32 + l (at most
 // floor(m_l / 32) + 1 >= ceil(m_l / 32) slots before list l + 1's first)
 __device__ __forceinline__ int64_t rs_tile_slot(const int* bucket_off, int l, int t) {
   return (int64_t)(bucket_off[l] / kRsQTile) + l + t;
 }
+
+// s_waitcnt vmcnt(v') lgkmcnt(0) for the largest v' <= v in a short ladder (the count is an immediate)
+__device__ __forceinline__ void rs_wait_vm(int v) {
+#define RS_VM(n) ((n & 15) | (0x7 << 4) | ((n >> 4) << 14))
+  if (v >= 48) __builtin_amdgcn_s_waitcnt(RS_VM(48));
+  else if (v >= 40) __builtin_amdgcn_s_waitcnt(RS_VM(40));
+  else if (v >= 32) __builtin_amdgcn_s_waitcnt(RS_VM(32));
+  else if (v >= 24) __builtin_amdgcn_s_waitcnt(RS_VM(24));
+  else if (v >= 16) __builtin_amdgcn_s_waitcnt(RS_VM(16));
+  else if (v >= 12) __builtin_amdgcn_s_waitcnt(RS_VM(12));
+  else if (v >= 8) __builtin_amdgcn_s_waitcnt(RS_VM(8));
+  else if (v >= 6) __builtin_amdgcn_s_waitcnt(RS_VM(6));
+  else if (v >= 4) __builtin_amdgcn_s_waitcnt(RS_VM(4));
+  else if (v >= 3) __builtin_amdgcn_s_waitcnt(RS_VM(3));
+  else if (v >= 2) __builtin_amdgcn_s_waitcnt(RS_VM(2));
+  else if (v >= 1) __builtin_amdgcn_s_waitcnt(RS_VM(1));
+  else __builtin_amdgcn_s_waitcnt(RS_VM(0));
+#undef RS_VM
+}
+
+// the workgroup's tiles-ready counter (LDS): wait until it reaches target; false if it never did
+// within the cap (a safety valve: every wave signals every tile, so the count always arrives)
+__device__ __forceinline__ bool rs_spin(int* ctr, int target) {
+  for (int i = 0; i < (1 << 20); ++i) {  // (~40 ms: a tile takes ~3 us)
+    if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) {
+      asm volatile("" ::: "memory");  // (no LDS read of the tile moves above the wait)
+      return true;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return false;
+}
+
+__device__ __forceinline__ void rs_signal(int* ctr) {
+  asm volatile("" ::: "memory");
+  if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0)
+    __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+constexpr int kRsBPrefetch = 2;  // k-steps between a B operand's LDS read and its MFMA
 
 template <bool B>
 struct BoolC {
@@ -124,10 +152,14 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   constexpr int BUF = NK * 1024 + 1024;
   constexpr int NB = 2 * NK;  // 8-dim blocks of a group row
   constexpr int64_t IMG = (int64_t)(NK + 1) * 1024;
+  static_assert(NK / kRsWaves + 1 < NK, "DMA pieces within the k-loop");
   static_assert((NK + kRsWaves) / kRsWaves < NK, "the image's pieces are issued over k-steps 1..");
   // [2 item parities][8 waves][64] row norms of the wave's group (lanes 32..63 repeat 0..31), filled by
   // LDS-DMA so the next item's are in flight with its rows and nothing waits on them in registers
   float* s_norm = reinterpret_cast<float*>(smem + 2 * BUF);
+  // tiles-ready counter: every wave adds 1 per tile once it has finished reading the previous tile and its
+  // DMA pieces of this one have landed (see the tile loop); no workgroup barrier per tile
+  int* s_ready = reinterpret_cast<int*>(smem + 2 * BUF + 2 * kRsWaves * 64 * sizeof(float));
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int j = lane & 31;
@@ -143,12 +175,15 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   int w = (int)((int64_t)total * x / 8) + (int)(blockIdx.x >> 3);
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
   int n_tiles_done = 0;
+  int tt = 0;               // tiles this workgroup has started
+  bool spun_out = false;    // a ready-wait gave up (never expected): the results are then not trusted
   uint64_t pw_wait = 0, pw_loop = 0, pw_epi = 0;  // flags & 16: this wave's cycles per tile phase
   const int widx = blockIdx.x * kRsWaves + wave;
   int4* const wstream = a.wave_buf + (int64_t)widx * a.wave_cap;
   int wcnt = 0;  // entries of this wave's candidate stream
   auto block_prof = [&]() {
-    if (lane == 0) a.wave_cnt[widx] = wcnt;  // (timing only) flags & 8: per block {start, end, tiles} in 100 MHz ticks
+    // (a wave that gave up waiting reports a lost stream: every query then takes the fallback search)
+    if (lane == 0) a.wave_cnt[widx] = spun_out ? a.wave_cap + 1 : wcnt;  // (timing only) flags & 8: per block {start, end, tiles} in 100 MHz ticks
     if ((a.flags & 8) && a.prof && tid == 0) {
       a.prof[3 * blockIdx.x] = t_start;
       a.prof[3 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
@@ -184,7 +219,14 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
     dma_b32(uniform_desc(a.row_norms + (int64_t)grp * kGroupRows, kGroupRows * 4), s_norm + (ip * kRsWaves + wave) * 64,
             j * 4);
   };
-  rs_stage<NK>(smem, a.tiles + it.slot * IMG, wave, lane);
+  if (tid == 0) *s_ready = 0;
+  __syncthreads();  // (the only workgroup barrier: the counter is zero before any wave signals)
+  {
+    const v4i d0 = uniform_desc(a.tiles + it.slot * IMG, (int)IMG);
+#pragma unroll
+    for (int p0 = 0; p0 <= NK; p0 += kRsWaves)
+      if (p0 + wave <= NK) dma_b128(d0, smem + (p0 + wave) * 1024, lane * 16, (p0 + wave) * 1024);
+  }
   load_norms(gv ? g : it.g0, 0);
   h8 ra[NK];
   {
@@ -204,15 +246,18 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
     if (has_next) nx = rs_item(a, wn);  // (retired by the first tile's wait, long before its use)
     const int gnx = nx.g0 + wave;
     const bool gvn = has_next && gnx < nx.gend;
-    for (int t = 0; t < ntiles; ++t) {
-      // this wave's DMA of tile t has landed (and, at an item's first tile, its rows: the compiler waits
-      // for them before the first MFMA anyway), then every other wave's
+    // One tile. The item's rows have landed (the wait at the item start); this wave's DMA of tile t lands
+    // by the counted wait below, which leaves the candidate stores issued after it in flight. The last
+    // tile (LAST) is a separate copy, the only one that loads the next item's rows: in a loop shared by
+    // all tiles the compiler would wait for every vector-memory operation before the first MFMA.
+    auto tile = [&](int t, auto last_c) __attribute__((always_inline)) {
+      constexpr bool LAST = decltype(last_c)::value;
       const uint64_t ph0 = (a.flags & 16) ? __builtin_amdgcn_s_memtime() : 0;
-      __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
-      // raw barrier: __syncthreads()'s fence is the same wait, spelled out above
-      __builtin_amdgcn_s_barrier();
+      // every wave's pieces of this tile have landed and every wave is done with the previous tile
+      if (!spun_out && !rs_spin(s_ready, kRsWaves * (tt + 1))) spun_out = true;
+      ++tt;
       const uint64_t ph1 = (a.flags & 16) ? __builtin_amdgcn_s_memtime() : 0;
-      const bool last = t + 1 == ntiles;
+      const bool last = LAST;
       // the next tile (of this item, or the next item's first) goes into the other buffer: every wave
       // has finished reading it (tile t - 1) before the barrier above. Its pieces are issued one per
       // k-step from the second on: issued before the first MFMA, the compiler's wait for the rows there
@@ -223,23 +268,23 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
       const bool stage = (!last || has_next) && !(a.flags & 2);
       const v4i sdesc = uniform_desc(simg, stage ? (int)IMG : 0);
       char* sbuf = smem + (par ^ 1) * BUF;
-      const bool reload = last && has_next;
+      const bool reload = LAST && has_next;
       const __amdgpu_buffer_rsrc_t nrs = group_rsrc(gvn ? gnx : nx.g0);
       f32x16 acc = zero;
-      float4 hd;  // this tile's header for query j, read during the last k-steps
+      float4 hd;  // this tile's header for query j
       // (a wave without a group in this block runs the MFMAs on stale rows; its epilogue is skipped).
       // Two copies of the k-loop, with and without the next item's row loads, so no k-step branches.
       auto kloop = [&](auto reload_c) __attribute__((always_inline)) {
         constexpr bool RL = decltype(reload_c)::value;
         const char* bb = smem + par * BUF + lane * 16;
-        h8 b[4];  // B operands three k-steps ahead
+        constexpr int PD = kRsBPrefetch;  // B operands PD k-steps ahead (ring of PD + 1)
+        h8 b[PD + 1];
 #pragma unroll
-        for (int u = 0; u < 3; ++u) b[u] = *reinterpret_cast<const h8*>(bb + (u < NK ? u : 0) * 1024);
+        for (int u = 0; u < PD; ++u) b[u] = *reinterpret_cast<const h8*>(bb + (u < NK ? u : 0) * 1024);
 #pragma unroll
         for (int s = 0; s < NK; ++s) {
-          if (s + 3 < NK) b[(s + 3) & 3] = *reinterpret_cast<const h8*>(bb + (s + 3) * 1024);
-          if (s == (NK > 3 ? NK - 3 : 0)) hd = *reinterpret_cast<const float4*>(smem + par * BUF + NK * 1024 + j * 16);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s], b[s & 3], acc, 0, 0, 0);
+          if (s + PD < NK) b[(s + PD) % (PD + 1)] = *reinterpret_cast<const h8*>(bb + (s + PD) * 1024);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s], b[s % (PD + 1)], acc, 0, 0, 0);
           if constexpr (RL) {
             // the next item's rows, right after this k-step's last use of the register (its norms
             // first, with the first k-step)
@@ -256,9 +301,21 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
           __builtin_amdgcn_sched_barrier(0);
         }
       };
-      if (reload) kloop(BoolC<true>{});
-      else kloop(BoolC<false>{});
+      if constexpr (LAST) {
+        if (reload) kloop(BoolC<true>{});
+        else kloop(BoolC<false>{});
+      } else {
+        kloop(BoolC<false>{});
+      }
       const uint64_t ph2 = (a.flags & 16) ? __builtin_amdgcn_s_memtime() : 0;
+      // (the header piece holds query j's header at lanes j and j + 32: lane * 16 like the B pieces)
+      hd = *reinterpret_cast<const float4*>(smem + par * BUF + NK * 1024 + lane * 16);
+      // signal the next tile: this wave's reads of this one are done (lgkmcnt(0): the header is in) and
+      // its DMA pieces of the next have landed -- vmcnt counts, in issue order, only the next item's rows
+      // issued after its last piece (k-step NK / 8 + 1) beyond them
+      // (one fewer than counted: the order of a k-step's row load and DMA piece is the compiler's)
+      rs_wait_vm(LAST && has_next ? NK - 3 - NK / kRsWaves : 0);
+      rs_signal(s_ready);
       // epilogue: lane (j, h) holds the 16 dots of query j with rows (r & 3) + 8 (r >> 2) + 4 h
       if (gv && !(a.flags & 1)) {
         // header of query j: {qs, uf, qn, q}
@@ -267,16 +324,26 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
         const float mm = METRIC == kL2 ? -2.0f * qs : -qs;
         // one-fma filter over the 16 keys (norms from LDS four at a time: registers are short); the rare
         // survivors are then handled one at a time, picked out of the accumulator by selects
-        unsigned hits = 0;
+        // common case first: the smallest filter value of the lane against uf (fma + min per key); the
+        // hit mask is formed only when some lane of the wave has a hit
+        float fmin = INFINITY;
 #pragma unroll
         for (int q4 = 0; q4 < 4; ++q4) {
           const float4 v = *reinterpret_cast<const float4*>(wnorm + 8 * q4 + 4 * h);
           const float xv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-          for (int u = 0; u < 4; ++u)
-            hits |= (fmaf(acc[4 * q4 + u], mm, METRIC == kL2 ? xv[u] : 0.0f) < uf ? 1u : 0u) << (4 * q4 + u);
+          for (int u = 0; u < 4; ++u) fmin = fminf(fmin, fmaf(acc[4 * q4 + u], mm, METRIC == kL2 ? xv[u] : 0.0f));
         }
-        if (__ballot(hits != 0) != 0) {
+        if (__ballot(fmin < uf) != 0) {
+          unsigned hits = 0;
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4) {
+            const float4 v = *reinterpret_cast<const float4*>(wnorm + 8 * q4 + 4 * h);
+            const float xv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              hits |= (fmaf(acc[4 * q4 + u], mm, METRIC == kL2 ? xv[u] : 0.0f) < uf ? 1u : 0u) << (4 * q4 + u);
+          }
           // every filter hit (a superset of the keys <= T_q; the refine's window is below T_q) goes to
           // this wave's stream -- positions by ballot prefix, no atomics; k_rs_bucket sorts the
           // streams into per-query buffers
@@ -309,7 +376,13 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
         pw_epi += ph3 - ph2;
       }
       par ^= 1;
-    }
+    };
+    // the item's rows (loaded during the previous item's last tile) and everything before them; at the
+    // first item, the prologue's DMA pieces too, which this wave then signals as tile 0's
+    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
+    if (tt == 0) rs_signal(s_ready);
+    for (int t = 0; t + 1 < ntiles; ++t) tile(t, BoolC<false>{});
+    tile(ntiles - 1, BoolC<true>{});
     n_tiles_done += ntiles;
     if (!has_next) break;
     w = wn;
@@ -403,7 +476,7 @@ __global__ __launch_bounds__(256) void k_rs_tiles(const int64_t* __restrict__ bu
 
 size_t rs_scan_lds_bytes(int dp) {
   const int nk = dp / 16;
-  // two tile buffers + the norms: [2 items][8 waves][64]
+  // two tile buffers + the norms: [2 items][8 waves][64] + the tiles-ready counter
   return (size_t)2 * (nk * 1024 + 1024) + 2 * kRsWaves * 64 * sizeof(float) + 16;
 }
 
