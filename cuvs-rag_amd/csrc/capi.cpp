@@ -1365,7 +1365,7 @@ int32_t mivs_ivf_pq_build(int32_t device, void* stream, const float* d_data, int
   return guarded([&] {
     require(p != nullptr && out != nullptr, "params/out is NULL");
     check_common(device, d_data, n, dim);
-    require(p->metric == MIVS_METRIC_L2, "ivf_pq: only the L2 metric is supported by this build", MIVS_ERR_UNSUPPORTED);
+    require(p->metric == MIVS_METRIC_L2 || p->metric == MIVS_METRIC_IP, "unknown metric");
     require(p->pq_bits == 8, "ivf_pq: pq_bits must be 8 in this build", MIVS_ERR_UNSUPPORTED);
     require(p->pq_dim >= 1 && p->pq_dim <= dim, "pq_dim must be in [1, dim]");
     require(p->n_lists >= 1 && p->n_lists <= 32768, "n_lists must be in [1, 32768]");
@@ -1385,7 +1385,9 @@ int32_t mivs_ivf_pq_build(int32_t device, void* stream, const float* d_data, int
     idx->device = device;
     idx->d = dim;
     idx->dp = dim_pad(dim);
-    idx->metric = MIVS_METRIC_L2;
+    // (the coarse lists and the codebooks are trained in L2 for both metrics, as for ivf_flat; the
+    // metric is the search's ranking)
+    idx->metric = p->metric;
     idx->id_offset = id_offset;
     idx->pq_dim = p->pq_dim;
     idx->pq_bits = p->pq_bits;
@@ -1490,7 +1492,7 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
   return guarded([&] {
     require(idx != nullptr && idx->kind == 2, "not an ivf_pq index");
     require(nq >= 0, "nq must be >= 0");
-    require(k >= 1 && k <= kMaxK, "ivf_pq: k must be in [1, " + std::to_string(kMaxK) + "] in this build",
+    require(k >= 1 && k <= kMaxSelectK, "ivf_pq: k must be in [1, " + std::to_string(kMaxSelectK) + "]",
             MIVS_ERR_UNSUPPORTED);
     require(n_probes >= 1, "n_probes must be >= 1");
     require(nq == 0 || (d_q && d_dist && d_ids), "NULL query/output pointer");
@@ -1501,8 +1503,8 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
     const int np = std::min<int>(n_probes, idx->lists.n_lists);
     require(np <= kMaxSelectK, "n_probes must be <= " + std::to_string(kMaxSelectK), MIVS_ERR_UNSUPPORTED);
     require(np == n_probes || d_probes == nullptr, "n_probes > n_lists with a probes output");
-    const int kcap = scan_kcap(k);
-    require(pq_tile_lds_bytes(idx->rot_dim_pad, idx->pq_len) <= 160 * 1024 ||
+    const int kcap = scan_kcap(k);  // (0: k > 64, the DUMP scan + K8)
+    require(k > kMaxK || pq_tile_lds_bytes(idx->rot_dim_pad, idx->pq_len) <= 160 * 1024 ||
                 pq_scan_lds_bytes(idx->rot_dim_pad, idx->pq_dim, kcap) <= 160 * 1024 ||
                 pq_split_lds_bytes(idx->rot_dim_pad, (int)ceil_div(ceil_div(idx->pq_dim, 2), 16) * 16, kcap) <=
                     160 * 1024,
@@ -1513,10 +1515,72 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
     HIPCHK(launch_row_norms(d_q, nq, idx->d, ws.qn.as<float>(), s));
     ws.probes_d.reserve(sizeof(float) * nq * np);
     ws.probes_i.reserve(sizeof(int64_t) * nq * np);
-    single_list_topk(idx->cents, coarse_groups(idx, nq), d_q, ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, np, kL2,
-                     ws.probes_d.as<float>(), ws.probes_i.as<int64_t>(), idx->device, ws, s);
+    single_list_topk(idx->cents, coarse_groups(idx, nq), d_q, ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, np,
+                     idx->metric, ws.probes_d.as<float>(), ws.probes_i.as<int64_t>(), idx->device, ws, s);
     if (d_probes) HIPCHK(launch_i64_to_i32(ws.probes_i.as<int64_t>(), nq * np, d_probes, s));
     const ListSet& L = idx->lists;
+    // k > 16 (the candidate pools of IVF-PQ + refine): K9 in DUMP mode writes every probed row's key and
+    // K8 selects per query, in query batches bounded by the select workspace -- measured 3x faster than
+    // the 32/64-entry register lists at 40 candidates (profiles/r02_ivf_pq_refine_bench.log);
+    // MIVS_PQ_DUMP_K raises the threshold (up to 64) for the register path
+    const char* dke = getenv("MIVS_PQ_DUMP_K");
+    const int dump_k = std::min(kMaxK, std::max(16, dke ? atoi(dke) : 16));
+    if (k > dump_k) {
+      require(pq_scan_lds_bytes(idx->rot_dim_pad, idx->pq_dim, 0) <= 160 * 1024,
+              "ivf_pq: k > 64 needs the whole LUT in LDS, which does not fit this pq_dim", MIVS_ERR_UNSUPPORTED);
+      int64_t slot_rows = 1;
+      for (int l = 0; l < L.n_lists; ++l) slot_rows = std::max<int64_t>(slot_rows, L.h_off[l + 1] - L.h_off[l]);
+      require(slot_rows < INT32_MAX, "ivf_pq: list too long for the DUMP scan", MIVS_ERR_UNSUPPORTED);
+      const int64_t qb = select_batch(nq, (size_t)np * ((size_t)slot_rows * 4 + 16));
+      ws.part_d.reserve(sizeof(float) * (size_t)(qb * np * slot_rows));
+      ws.part_i.reserve(sizeof(int64_t) * (size_t)(qb * np * 2));
+      if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
+      for (int64_t b0 = 0; b0 < nq; b0 += qb) {
+        const int64_t nb = std::min<int64_t>(qb, nq - b0);
+        PqScanArgs a{};
+        a.queries = d_q + b0 * (int64_t)idx->d;
+        a.cents = idx->centroids_rm.as<float>();
+        a.books = idx->pq_books.as<float>();
+        a.codes = static_cast<const uint8_t*>(idx->pq_codes.p);
+        a.row_ids = L.ids.as<int64_t>();
+        a.list_off = L.off.as<int64_t>();
+        a.list_goff = L.goff.as<int64_t>();
+        a.probes = ws.probes_i.as<int64_t>() + b0 * np;
+        a.probes_d = ws.probes_d.as<float>() + b0 * np;
+        a.n_slots = nb * np;
+        a.n_probes = np;
+        a.d = idx->d;
+        a.rot_dim_pad = idx->rot_dim_pad;
+        a.pq_dim = idx->pq_dim;
+        a.pq_dim_pad = idx->pq_dim_pad;
+        a.pq_len = idx->pq_len;
+        a.k = k;
+        a.ip = idx->metric == MIVS_METRIC_IP ? 1 : 0;
+        a.out_d = ws.part_d.as<float>();
+        a.dump_rows = (int)slot_rows;
+        a.slot_info = ws.part_i.as<int64_t>();
+        HIPCHK(launch_pq_scan(a, 0, s));
+        SelectArgs sa{};
+        sa.keys = ws.part_d.as<float>();
+        sa.row_ids = L.ids.as<int64_t>();
+        sa.slot_info = ws.part_i.as<int64_t>();
+        sa.slot_begin = nullptr;
+        sa.slots_per_q = np;
+        sa.slot_rows = (int)slot_rows;
+        sa.nq = nb;
+        sa.k = k;
+        sa.metric = idx->metric;
+        sa.out_d = d_dist + b0 * k;
+        sa.out_i = d_ids + b0 * k;
+        HIPCHK(launch_select(sa, s));
+      }
+      if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
+      if (pr) HIPCHK(hipEventRecord(pr->e[3], s));
+      idx->last_nq = nq;
+      idx->last_np = np;
+      idx->last_k = k;
+      return;
+    }
     const char* tiled_env = getenv("MIVS_PQ_TILED");
     // K9s (two LUT halves) applies when pq_len is a multiple of 4 up to 16 and each half has <= 64
     // subspaces; K9 needs the whole LUT plus its merge area in LDS; K9b otherwise
@@ -1527,6 +1591,8 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
                        (!split_ok && pq_scan_lds_bytes(idx->rot_dim_pad, idx->pq_dim, kcap) > 160 * 1024);
     require(!tiled || kcap <= 32, "ivf_pq: k > 32 needs the whole-LUT scan (K9/K9s), which does not fit this "
             "pq_dim in LDS", MIVS_ERR_UNSUPPORTED);
+    require(!tiled || idx->metric == MIVS_METRIC_L2, "ivf_pq: inner product needs the whole-LUT scan (K9/K9s), "
+            "which does not fit this pq_dim in LDS", MIVS_ERR_UNSUPPORTED);
     if (tiled && pq_tile_lds_bytes(idx->rot_dim_pad, idx->pq_len) <= 160 * 1024) {
       // K9b (used when K9's whole-LUT LDS does not fit, or MIVS_PQ_TILED=1): probe map
       // (list -> 16-query tiles x 512-row chunks), tiled scan, K7 merge of the slots
@@ -1646,6 +1712,8 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
         a.n_lists = L.n_lists;
       }
       a.pq_half = (int)ceil_div(ceil_div(idx->pq_dim, 2), 16) * 16;
+      a.ip = idx->metric == MIVS_METRIC_IP ? 1 : 0;
+      a.probes_d = ws.probes_d.as<float>();
       const char* spe = getenv("MIVS_PQ_SPLIT");
       const bool split = !(spe && spe[0] == '0') && !(a.flags & 7);
       if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
@@ -1661,7 +1729,7 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
       m.nq = nq;
       m.k_in = k;
       m.k = k;
-      m.metric = kL2;
+      m.metric = idx->metric;
       m.out_d = d_dist;
       m.out_i = d_ids;
       HIPCHK(launch_merge(m, s));

@@ -118,6 +118,10 @@ struct PqScanArgs {
   const int* ent_off;          // [n_lists+1]
   int n_lists;
   int pq_half;                 // K9s: subspaces per LUT half (a multiple of 16, 2 * pq_half >= pq_dim)
+  int ip;                      // inner product: LUT -(q_j . B_j[c]), coarse term in subspace 0, out = -key
+  const float* probes_d;       // IP: [nq][n_probes] coarse distances q . c_l (K3, the probes' order)
+  int dump_rows;               // K9 DUMP (kcap 0, k > 64): out_d is [n_slots][dump_rows] keys
+  int64_t* slot_info;          //   and slot_info [n_slots][2] = (first row position, rows)
 };
 
 // IVF-PQ tiled scan (K9b, pq.hip): work item = (list, <= 16 queries, 512-row chunk) from the probe map.

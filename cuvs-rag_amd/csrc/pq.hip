@@ -132,21 +132,58 @@ __device__ __forceinline__ void pq_insert(float (&lk)[KCAP], int (&lp)[KCAP], fl
   }
 }
 
+// one term of a LUT entry's chain, dims ascending: L2 (r_i - b_i)^2 into acc (r = q - c_l), IP q_i b_i
+__device__ __forceinline__ float pq_lut_term(bool ip, float r, float b, float acc) {
+  if (ip) return fmaf(r, b, acc);
+  const float t = r - b;
+  return fmaf(t, t, acc);
+}
+
+// the entry: L2 acc; IP -acc, plus the probe's coarse key -(q . c_l) in subspace 0
+__device__ __forceinline__ float pq_lut_entry(bool ip, float acc, bool j0, float base0) {
+  if (!ip) return acc;
+  const float v = -acc;
+  return j0 ? v + base0 : v;
+}
+
+// Inner product (a.ip): the LUT is LUT_j[c] = -(q_j . B_j[c]) (the fmaf chain of the dims, negated) and
+// the coarse term -(q . c_l) -- the probe's coarse key, bit-equal to the oracle's -orc_dot -- is added to
+// subspace 0's row, so a row's key is the same j-ordered sum from 0 as for L2. This finds the probe's
+// coarse distance (q . c_l, K3's output for IP) by its list id among the query's probes.
+__device__ __forceinline__ float pq_ip_base(const PqScanArgs& a, int64_t q, int l) {
+  const int lane = threadIdx.x & 63;
+  for (int p0 = 0; p0 < a.n_probes; p0 += 64) {
+    const int p = p0 + lane;
+    const uint64_t m = __ballot(p < a.n_probes && a.probes[q * a.n_probes + p] == l);
+    if (m) return -a.probes_d[q * a.n_probes + p0 + __builtin_ctzll(m)];
+  }
+  return 0.0f;  // (unreachable: l is one of the query's probes)
+}
+
+// the slot's output distance: the key (L2) or the inner product (IP, -key); missing ranks +inf / -inf
+__device__ __forceinline__ float pq_out(const PqScanArgs& a, bool valid, float key) {
+  return valid ? (a.ip ? -key : key) : (a.ip ? -INFINITY : INFINITY);
+}
+
 // K9: one workgroup per (query, probe) slot. LDS: [qres d_pad][LUT pq_dim x 256 | merge area].
 //   1. residual q - c_l -> LDS;  2. LUT[j][c] = ||res_j - B_j[c]||^2 -> LDS;
 //   3. each thread scans rows tid, tid + NT, ... of the list: dist = sum_j LUT[j][code_j],
 //      register top-KCAP by (dist, row position);
 //   4. the NT lane lists -> LDS; wave w merges its 64 lists (64-lane min-reduction per rank),
 //      then wave 0 merges the NT/64 wave lists; the slot's top-k (dist, id) -> out.
+// KCAP = 0 (DUMP, k > 64): every row's key -> out_d[slot][dump_rows], (first row position, rows) ->
+// slot_info[slot]; K8 selects per query (as the IVF-Flat DUMP scan).
 template <int KCAP, int NT>
 __global__ __launch_bounds__(NT) void k_pq_scan(PqScanArgs a) {
+  constexpr bool DUMP = KCAP == 0;
+  constexpr int KR = DUMP ? 1 : KCAP;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* s_res = reinterpret_cast<float*>(smem);                 // [rot_dim]
   float* lut = s_res + a.rot_dim_pad;                            // [pq_dim][256]
   float* mkey = lut;                                             // merge area (after the scan)
-  int* mpos = reinterpret_cast<int*>(mkey + NT * KCAP);
-  float* wkey = mkey + 2 * NT * KCAP;                            // [NT/64][k] wave results
-  int* wpos = reinterpret_cast<int*>(wkey + (NT / 64) * KCAP);
+  int* mpos = reinterpret_cast<int*>(mkey + NT * KR);
+  float* wkey = mkey + 2 * NT * KR;                              // [NT/64][k] wave results
+  int* wpos = reinterpret_cast<int*>(wkey + (NT / 64) * KR);
 
   int64_t slot, q;
   int l;
@@ -174,15 +211,20 @@ __global__ __launch_bounds__(NT) void k_pq_scan(PqScanArgs a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   if (l < 0) {  // no probe (degenerate query): empty slot
+    if constexpr (DUMP) {
+      if (tid == 0) { a.slot_info[2 * slot] = 0; a.slot_info[2 * slot + 1] = 0; }
+      return;
+    }
     for (int t = tid; t < a.k; t += NT) {
-      a.out_d[slot * a.k + t] = INFINITY;
+      a.out_d[slot * a.k + t] = pq_out(a, false, 0.0f);
       a.out_i[slot * a.k + t] = -1;
     }
     return;
   }
   const int pl = a.pq_len;
   for (int i = tid; i < a.rot_dim_pad; i += NT)
-    s_res[i] = i < a.d ? a.queries[q * a.d + i] - a.cents[(int64_t)l * a.d + i] : 0.0f;
+    s_res[i] = i < a.d ? (a.ip ? a.queries[q * a.d + i] : a.queries[q * a.d + i] - a.cents[(int64_t)l * a.d + i]) : 0.0f;
+  const float base0 = a.ip ? pq_ip_base(a, q, l) : 0.0f;
   __syncthreads();
   const int nlut = a.flags & 1 ? 0 : a.pq_dim * kPqCodes;
   if ((pl & 3) == 0 && pl <= 16) {
@@ -207,17 +249,12 @@ __global__ __launch_bounds__(NT) void k_pq_scan(PqScanArgs a) {
 #pragma unroll
         for (int c4 = 0; c4 < 4; ++c4) {
           if (c4 < nv) {
-            const float t0 = r[4 * c4 + 0] - bv[v][c4].x;
-            acc = fmaf(t0, t0, acc);
-            const float t1 = r[4 * c4 + 1] - bv[v][c4].y;
-            acc = fmaf(t1, t1, acc);
-            const float t2 = r[4 * c4 + 2] - bv[v][c4].z;
-            acc = fmaf(t2, t2, acc);
-            const float t3 = r[4 * c4 + 3] - bv[v][c4].w;
-            acc = fmaf(t3, t3, acc);
+            const float b4[4] = {bv[v][c4].x, bv[v][c4].y, bv[v][c4].z, bv[v][c4].w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc = pq_lut_term(a.ip, r[4 * c4 + u], b4[u], acc);
           }
         }
-        lut[e] = acc;
+        lut[e] = pq_lut_entry(a.ip, acc, e < kPqCodes, base0);
       }
     }
   } else {
@@ -226,19 +263,16 @@ __global__ __launch_bounds__(NT) void k_pq_scan(PqScanArgs a) {
       const float* b = a.books + (int64_t)e * pl;
       const float* r = s_res + j * pl;
       float acc = 0.0f;
-      for (int i = 0; i < pl; ++i) {
-        const float t = r[i] - b[i];
-        acc = fmaf(t, t, acc);
-      }
-      lut[e] = acc;
+      for (int i = 0; i < pl; ++i) acc = pq_lut_term(a.ip, r[i], b[i], acc);
+      lut[e] = pq_lut_entry(a.ip, acc, e < kPqCodes, base0);
     }
   }
   __syncthreads();
 
-  float lk[KCAP];
-  int lp[KCAP];
+  float lk[KR];
+  int lp[KR];
 #pragma unroll
-  for (int t = 0; t < KCAP; ++t) { lk[t] = INFINITY; lp[t] = INT_MAX; }
+  for (int t = 0; t < KR; ++t) { lk[t] = INFINITY; lp[t] = INT_MAX; }
   const int64_t r0 = a.list_off[l], nrows = a.flags & 2 ? 0 : a.list_off[l + 1] - r0;
   const int64_t g0 = a.list_goff[l];
   const int nchunk = a.pq_dim_pad >> 4;
@@ -269,7 +303,8 @@ __global__ __launch_bounds__(NT) void k_pq_scan(PqScanArgs a) {
           }
         }
       }
-      if (dist < lk[KCAP - 1]) pq_insert<KCAP>(lk, lp, dist, (int)r);
+      if constexpr (DUMP) a.out_d[slot * a.dump_rows + r] = dist;
+      else if (dist < lk[KCAP - 1]) pq_insert<KCAP>(lk, lp, dist, (int)r);
 #pragma unroll
       for (int ch = 0; ch < kPqMaxChunks; ++ch) cur[ch] = nxt[ch];
     }
@@ -287,9 +322,14 @@ __global__ __launch_bounds__(NT) void k_pq_scan(PqScanArgs a) {
         }
         j += 16;
       }
-      if (dist < lk[KCAP - 1]) pq_insert<KCAP>(lk, lp, dist, (int)r);
+      if constexpr (DUMP) a.out_d[slot * a.dump_rows + r] = dist;
+      else if (dist < lk[KCAP - 1]) pq_insert<KCAP>(lk, lp, dist, (int)r);
     }
   }
+  if constexpr (DUMP) {
+    if (tid == 0) { a.slot_info[2 * slot] = g0 * kGroupRows; a.slot_info[2 * slot + 1] = nrows; }
+    return;
+  } else {
   if (a.flags & 4) {  // timing experiment: no merge, one store keeps the scan alive
     if (lk[0] < -1.0f) a.out_d[slot * a.k] = lk[0] + (float)lp[0];
     return;
@@ -347,7 +387,7 @@ __global__ __launch_bounds__(NT) void k_pq_scan(PqScanArgs a) {
       }
       if (lane == 0) {
         const bool valid = bp != INT_MAX;
-        a.out_d[slot * a.k + t] = valid ? bk : INFINITY;
+        a.out_d[slot * a.k + t] = pq_out(a, valid, bk);
         a.out_i[slot * a.k + t] = valid ? a.row_ids[g0 * kGroupRows + bp] : (int64_t)-1;
       }
       if (src && hk == bk && hp == bp && head < a.k) {
@@ -357,6 +397,7 @@ __global__ __launch_bounds__(NT) void k_pq_scan(PqScanArgs a) {
       }
     }
   }
+  }  // (not DUMP)
 }
 
 // LUT entries e < nlut (subspace e >> 8, code e & 255) of a pq_len = 4 * PL4 codebook slice: each
@@ -364,7 +405,7 @@ __global__ __launch_bounds__(NT) void k_pq_scan(PqScanArgs a) {
 // fmaf chain of K9 / the oracle
 template <int PL4, int NT>
 __device__ __forceinline__ void pq_lut_build(const float* __restrict__ books, const float* res, int nlut, int tid,
-                                             float* lut) {
+                                             float* lut, bool ip, bool with_base, float base0) {
   constexpr int pl = 4 * PL4, V = PL4 >= 4 ? 2 : 8 / PL4;
   for (int base = tid; base < nlut; base += V * NT) {
     float4 bv[V][PL4];
@@ -382,16 +423,11 @@ __device__ __forceinline__ void pq_lut_build(const float* __restrict__ books, co
       float acc = 0.0f;
 #pragma unroll
       for (int c4 = 0; c4 < PL4; ++c4) {
-        const float t0 = r[4 * c4 + 0] - bv[v][c4].x;
-        acc = fmaf(t0, t0, acc);
-        const float t1 = r[4 * c4 + 1] - bv[v][c4].y;
-        acc = fmaf(t1, t1, acc);
-        const float t2 = r[4 * c4 + 2] - bv[v][c4].z;
-        acc = fmaf(t2, t2, acc);
-        const float t3 = r[4 * c4 + 3] - bv[v][c4].w;
-        acc = fmaf(t3, t3, acc);
+        const float b4[4] = {bv[v][c4].x, bv[v][c4].y, bv[v][c4].z, bv[v][c4].w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc = pq_lut_term(ip, r[4 * c4 + u], b4[u], acc);
       }
-      lut[e] = acc;
+      lut[e] = pq_lut_entry(ip, acc, with_base && e < kPqCodes, base0);
     }
   }
 }
@@ -438,14 +474,15 @@ __global__ __launch_bounds__(256) void k_pq_scan_split(PqScanArgs a) {
   const int lane = tid & 63, wave = tid >> 6;
   if (l < 0) {
     for (int t = tid; t < a.k; t += NT) {
-      a.out_d[slot * a.k + t] = INFINITY;
+      a.out_d[slot * a.k + t] = pq_out(a, false, 0.0f);
       a.out_i[slot * a.k + t] = -1;
     }
     return;
   }
   const int pl = a.pq_len;
   for (int i = tid; i < a.rot_dim_pad; i += NT)
-    s_res[i] = i < a.d ? a.queries[q * a.d + i] - a.cents[(int64_t)l * a.d + i] : 0.0f;
+    s_res[i] = i < a.d ? (a.ip ? a.queries[q * a.d + i] : a.queries[q * a.d + i] - a.cents[(int64_t)l * a.d + i]) : 0.0f;
+  const float base0 = a.ip ? pq_ip_base(a, q, l) : 0.0f;
 
   float lk[KCAP];
   int lp[KCAP];
@@ -469,10 +506,10 @@ __global__ __launch_bounds__(256) void k_pq_scan_split(PqScanArgs a) {
       const float* books = a.books + (int64_t)j0 * kPqCodes * pl;
       const float* res = s_res + j0 * pl;
       switch (pl >> 2) {
-        case 1: pq_lut_build<1, NT>(books, res, nlut, tid, lut); break;
-        case 2: pq_lut_build<2, NT>(books, res, nlut, tid, lut); break;
-        case 3: pq_lut_build<3, NT>(books, res, nlut, tid, lut); break;
-        default: pq_lut_build<4, NT>(books, res, nlut, tid, lut); break;
+        case 1: pq_lut_build<1, NT>(books, res, nlut, tid, lut, a.ip, h == 0, base0); break;
+        case 2: pq_lut_build<2, NT>(books, res, nlut, tid, lut, a.ip, h == 0, base0); break;
+        case 3: pq_lut_build<3, NT>(books, res, nlut, tid, lut, a.ip, h == 0, base0); break;
+        default: pq_lut_build<4, NT>(books, res, nlut, tid, lut, a.ip, h == 0, base0); break;
       }
       __syncthreads();
       // this half's code chunks of each of my rows (<= 4 x 16 codes), the next row's requested first
@@ -562,7 +599,7 @@ __global__ __launch_bounds__(256) void k_pq_scan_split(PqScanArgs a) {
       }
       if (lane == 0) {
         const bool valid = bp != INT_MAX;
-        a.out_d[slot * a.k + t] = valid ? bk : INFINITY;
+        a.out_d[slot * a.k + t] = pq_out(a, valid, bk);
         a.out_i[slot * a.k + t] = valid ? a.row_ids[g0 * kGroupRows + bp] : (int64_t)-1;
       }
       if (src && hk == bk && hp == bp && head < a.k) {
@@ -870,6 +907,7 @@ hipError_t launch_pq_scan(const PqScanArgs& a, int kcap, hipStream_t s) {
   const size_t lds = pq_scan_lds_bytes(a.rot_dim_pad, a.pq_dim, kcap);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   switch (kcap) {
+    case 0: return launch_pq_scan_k<0>(a, lds, s);
     case 1: return launch_pq_scan_k<1>(a, lds, s);
     case 4: return launch_pq_scan_k<4>(a, lds, s);
     case 8: return launch_pq_scan_k<8>(a, lds, s);

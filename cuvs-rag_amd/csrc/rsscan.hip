@@ -476,7 +476,7 @@ __global__ __launch_bounds__(256) void k_rs_tiles(const int64_t* __restrict__ bu
 
 size_t rs_scan_lds_bytes(int dp) {
   const int nk = dp / 16;
-  // two tile buffers + the norms: [2 items][8 waves][64] + the tiles-ready counter
+  // two tile buffers + the norms ([2 items][8 waves][64]) + the tiles-ready counter
   return (size_t)2 * (nk * 1024 + 1024) + 2 * kRsWaves * 64 * sizeof(float) + 16;
 }
 

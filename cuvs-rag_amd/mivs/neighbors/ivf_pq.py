@@ -12,7 +12,9 @@ residuals x - c_list of min(n, 256 * max_train_points_per_pq_code) strided rows;
 as pq_dim one-byte codes. Search builds a pq_dim x 256 fp32 LUT per (query, probed list) in LDS
 and sums LUT entries over the list's codes (hand-written HIP, cuvs-rag_amd/csrc/pq.hip).
 
-This build: L2 metric, pq_bits = 8, k <= 64, identity rotation (dims past ``dim`` read as 0). For an exact
+This build: L2 and inner-product metrics (the coarse lists and codebooks are trained in L2 either way;
+inner product ranks by -(q . c_l) - sum_j q_j . B_j[code_j], distances out are the inner products),
+pq_bits = 8, k <= 64, identity rotation (dims past ``dim`` read as 0). For an exact
 ranking of the PQ candidates use ``mivs.neighbors.refine`` (cuVS's IVF-PQ + refine pattern).
 fp16 datasets (BASELINE config 5) are widened to fp32 on the device before training.
 """
@@ -38,8 +40,8 @@ class IndexParams:
                  max_train_points_per_pq_code: int = 256, kmeans_balance: bool = True):
         if int(n_lists) < 1:
             raise ValueError(f"n_lists must be >= 1, got {n_lists}")
-        if metric_code(metric) != _native.METRIC_L2:
-            raise NotImplementedError("ivf_pq: only the sqeuclidean metric is supported by this build")
+        if metric not in ("sqeuclidean", "l2", "L2Expanded", "inner_product"):
+            raise NotImplementedError("ivf_pq: the sqeuclidean and inner_product metrics are supported by this build")
         if int(pq_bits) != 8:
             raise NotImplementedError("ivf_pq: pq_bits must be 8 in this build")
         if codebook_kind not in ("subspace", "per_subspace"):

@@ -433,6 +433,13 @@ float orc_pq_l2(const float* a, const float* b, int pl) {
 }
 
 /* residual sub-vector j (pq_len dims) of row x w.r.t. centre c; dims >= d are 0 */
+/* the IP LUT entry's dot, dims ascending (the GPU K9/K9s chain): -(sum_i q_i b_i) */
+float orc_pq_ip(const float* a, const float* b, int pl) {
+  float acc = 0.0f;
+  for (int i = 0; i < pl; ++i) acc = fmaf(a[i], b[i], acc);
+  return -acc;
+}
+
 static void pq_residual(const float* x, const float* c, int d, int j, int pl, float* out) {
   for (int i = 0; i < pl; ++i) {
     const int k = j * pl + i;
@@ -517,9 +524,14 @@ void orc_ivfpq_build(const float* x, int64_t n, int d, int n_lists, int iters, d
   free(which);
 }
 
+/* IVF-PQ search (cuvs.neighbors.ivf_pq.search, improved_multi_gpu_rag.py:228-230). metric ORC_L2: a row's key
+ * is sum_j LUT_j[code_j] (j ascending, from 0) with LUT_j[c] = ||(q - c_l)_j - B_j[c]||^2. ORC_IP: LUT_j[c] =
+ * -(q_j . B_j[c]) and subspace 0's row also carries the probe's coarse key -(q . c_l) (orc_dot), so the key
+ * estimates -(q . x_hat); distances out are the inner products (-key). Probes rank by the metric's key. */
 void orc_ivfpq_search(const float* centroids, int n_lists, int d, const float* codebooks, int pq_dim, int pq_bits,
                       const int64_t* list_sizes, const int64_t* list_ids, const uint8_t* codes, const float* q,
-                      int64_t nq, int n_probes, int k, float* out_d, int64_t* out_i, int32_t* out_probes) {
+                      int64_t nq, int n_probes, int k, int metric, float* out_d, int64_t* out_i,
+                      int32_t* out_probes) {
   if (n_probes > n_lists) n_probes = n_lists;
   const int pl = orc_pq_len(d, pq_dim);
   const int nc = 1 << pq_bits;
@@ -535,7 +547,7 @@ void orc_ivfpq_search(const float* centroids, int n_lists, int d, const float* c
     kv_t* ph = (kv_t*)malloc(sizeof(kv_t) * (size_t)n_probes);
     int psz = 0;
     for (int j = 0; j < n_lists; ++j) {
-      kv_t v = {orc_key(orc_dot(centroids + (int64_t)j * d, qq, d), cn[j], qn, ORC_L2), j};
+      kv_t v = {orc_key(orc_dot(centroids + (int64_t)j * d, qq, d), cn[j], qn, metric), j};
       heap_push(ph, &psz, n_probes, v);
     }
     qsort(ph, (size_t)psz, sizeof(kv_t), kv_cmp);
@@ -547,9 +559,18 @@ void orc_ivfpq_search(const float* centroids, int n_lists, int d, const float* c
       const int l = (int)ph[p].id;
       if (out_probes) out_probes[qi * n_probes + p] = l;
       for (int j = 0; j < pq_dim; ++j) {
-        pq_residual(qq, centroids + (int64_t)l * d, d, j, pl, r);
-        for (int c = 0; c < nc; ++c)
-          lut[j * nc + c] = orc_pq_l2(r, codebooks + ((int64_t)j * nc + c) * pl, pl);
+        if (metric == ORC_IP) {
+          for (int i = 0; i < pl; ++i) r[i] = j * pl + i < d ? qq[j * pl + i] : 0.0f;
+          for (int c = 0; c < nc; ++c) {
+            float v = orc_pq_ip(r, codebooks + ((int64_t)j * nc + c) * pl, pl);
+            if (j == 0) v = v + ph[p].key; /* the probe's coarse key -(q . c_l) */
+            lut[j * nc + c] = v;
+          }
+        } else {
+          pq_residual(qq, centroids + (int64_t)l * d, d, j, pl, r);
+          for (int c = 0; c < nc; ++c)
+            lut[j * nc + c] = orc_pq_l2(r, codebooks + ((int64_t)j * nc + c) * pl, pl);
+        }
       }
       for (int64_t m = offs[l]; m < offs[l + 1]; ++m) {
         const uint8_t* cd = codes + m * pq_dim;
@@ -559,7 +580,7 @@ void orc_ivfpq_search(const float* centroids, int n_lists, int d, const float* c
         heap_push(h, &sz, k, v);
       }
     }
-    heap_emit(h, sz, k, ORC_L2, out_d + qi * k, out_i + qi * k);
+    heap_emit(h, sz, k, metric, out_d + qi * k, out_i + qi * k);
     free(h);
     free(r);
     free(lut);

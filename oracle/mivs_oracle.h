@@ -81,6 +81,7 @@ void orc_ivf_search(const float* x, int64_t id_offset, int d, const float* centr
 int orc_pq_len(int d, int pq_dim);
 int64_t orc_pq_train_count(int64_t n, int pq_bits, int64_t max_per_code);
 float orc_pq_l2(const float* a, const float* b, int pl);
+float orc_pq_ip(const float* a, const float* b, int pl);
 void orc_ivfpq_train_codebooks(const float* x, int64_t n, int d, const float* centroids, const int32_t* labels,
                                int pq_dim, int pq_bits, int iters, int balance, int64_t max_per_code,
                                float* codebooks);
@@ -91,7 +92,8 @@ void orc_ivfpq_build(const float* x, int64_t n, int d, int n_lists, int iters, d
                      float* codebooks, int64_t* list_sizes, int64_t* list_ids, uint8_t* codes);
 void orc_ivfpq_search(const float* centroids, int n_lists, int d, const float* codebooks, int pq_dim, int pq_bits,
                       const int64_t* list_sizes, const int64_t* list_ids, const uint8_t* codes, const float* q,
-                      int64_t nq, int n_probes, int k, float* out_d, int64_t* out_i, int32_t* out_probes);
+                      int64_t nq, int n_probes, int k, int metric, float* out_d, int64_t* out_i,
+                      int32_t* out_probes);
 
 /* ---- FAISS-algorithm CPU baseline (cpu_baseline.c; OpenMP, vectorised, NOT bit-exact) ---- */
 int orc_fast_threads(void);

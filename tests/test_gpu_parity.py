@@ -401,11 +401,25 @@ PQ_CASES = [
     (9000, 32, 2, 8, 3, 15, 2, 10),       # lists > 4096 rows (K9s row blocks), one LUT half only
     (8000, 768, 16, 96, 2, 21, 6, 64),    # k = 64: the candidate pool of IVF-PQ + refine
     (7000, 64, 16, 16, 3, 19, 5, 40),
+    (6000, 64, 16, 16, 4, 40, 8, 200),    # k > 64: K9 DUMP + K8 select (IVF-PQ + refine pools)
+    (12000, 768, 32, 96, 2, 20, 6, 300),
 ]
 
 
 @pytest.mark.parametrize("n,d,n_lists,pq_dim,iters,nq,n_probes,k", PQ_CASES)
 def test_ivf_pq_build_and_search_bitexact(mivs_lib, n, d, n_lists, pq_dim, iters, nq, n_probes, k):
+    _pq_case(n, d, n_lists, pq_dim, iters, nq, n_probes, k)
+
+
+@pytest.mark.parametrize("case", [c for c in PQ_CASES if 16 < c[-1] <= 64])
+def test_ivf_pq_register_lists_bitexact(mivs_lib, monkeypatch, case):
+    """k in (16, 64] through the 32/64-entry register lists of K9s (MIVS_PQ_DUMP_K=64) instead of the
+    default DUMP + K8 path: the same bits."""
+    monkeypatch.setenv("MIVS_PQ_DUMP_K", "64")
+    _pq_case(*case)
+
+
+def _pq_case(n, d, n_lists, pq_dim, iters, nq, n_probes, k):
     from mivs.neighbors import ivf_pq
 
     x = _data(n, d, seed=n + pq_dim, normalize=True)
@@ -424,6 +438,41 @@ def test_ivf_pq_build_and_search_bitexact(mivs_lib, n, d, n_lists, pq_dim, iters
     np.testing.assert_array_equal(probes.cpu().numpy(), op)
     np.testing.assert_array_equal(ids.cpu().numpy(), oi)
     np.testing.assert_array_equal(_bits(dist.cpu().numpy()), _bits(od))
+
+
+PQ_IP_CASES = [
+    # n, d, n_lists, pq_dim, iters, nq, n_probes, k, split
+    (6000, 64, 16, 16, 4, 40, 4, 10, True),
+    (12000, 768, 32, 96, 2, 20, 6, 10, True),     # K9s at the reference's pq_dim
+    (9000, 32, 2, 8, 3, 15, 2, 10, True),         # lists > 4096 rows: K9s row blocks
+    (5000, 96, 12, 40, 2, 29, 5, 32, False),      # K9 (MIVS_PQ_SPLIT=0), pq_len 3, padded dims
+    (8000, 768, 16, 96, 2, 21, 6, 64, True),      # k = 64
+    (5000, 96, 12, 40, 2, 29, 5, 150, True),      # k > 64: DUMP + K8
+]
+
+
+@pytest.mark.parametrize("n,d,n_lists,pq_dim,iters,nq,n_probes,k,split", PQ_IP_CASES)
+def test_ivf_pq_inner_product_bitexact(mivs_lib, monkeypatch, n, d, n_lists, pq_dim, iters, nq, n_probes, k, split):
+    """metric inner_product: probes by q . c_l, LUT -(q_j . B_j[c]) with the coarse key in subspace 0,
+    inner products out -- ids, probes and distance bits equal to oracle orc_ivfpq_search(ORC_IP)."""
+    from mivs.neighbors import ivf_pq
+
+    if not split:
+        monkeypatch.setenv("MIVS_PQ_SPLIT", "0")
+    x = _data(n, d, seed=n + pq_dim + 7, normalize=True)
+    q = _data(nq, d, seed=n + pq_dim + 8, normalize=True)
+    params = ivf_pq.IndexParams(n_lists=n_lists, metric="inner_product", pq_dim=pq_dim, kmeans_n_iters=iters,
+                                max_train_points_per_pq_code=32)
+    idx = ivf_pq.build(params, _gpu(x), ids_offset=5)
+    oc, ocb, osz, oids, ocodes = O.ivfpq_build(x, n_lists, pq_dim, iters=iters, max_per_code=32, id_offset=5)
+    np.testing.assert_array_equal(idx.codes().cpu().numpy(), ocodes)
+    probes = torch.empty((nq, n_probes), dtype=torch.int32, device="cuda")
+    dist, ids = ivf_pq.search(ivf_pq.SearchParams(n_probes=n_probes), idx, _gpu(q), k, probes_out=probes)
+    od, oi, op = O.ivfpq_search(oc, ocb, osz, oids, ocodes, q, n_probes, k, metric="inner_product")
+    np.testing.assert_array_equal(probes.cpu().numpy(), op)
+    np.testing.assert_array_equal(ids.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(dist.cpu().numpy()), _bits(od))
+    assert (np.diff(dist.cpu().numpy(), axis=1) <= 0).all()  # inner products, descending
 
 
 def test_ivf_pq_fp16_dataset_and_recall(mivs_lib):

@@ -42,3 +42,23 @@ def test_full_probe_search_ranks_by_pq_distance():
     order = np.argsort(ref, axis=1, kind="stable")[:, :10]
     np.testing.assert_allclose(d, np.take_along_axis(ref, order, 1), rtol=1e-4, atol=1e-4)
     assert (ids[order] == i).mean() > 0.95
+
+
+def test_full_probe_inner_product_ranks_by_q_dot_reconstruction():
+    """metric inner_product: key = -(q . c_l) - sum_j q_j . B_j[code_j] = -(q . x_hat); distances out are
+    the inner products q . x_hat, in descending order."""
+    x = _data(2500, 32, 4)
+    q = _data(15, 32, 5)
+    cents, cbs, sizes, ids, codes = O.ivfpq_build(x, 5, pq_dim=16, iters=3, max_per_code=8)
+    d, i, p = O.ivfpq_search(cents, cbs, sizes, ids, codes, q, 5, 10, metric="inner_product")
+    pl = O.pq_len(32, 16)
+    lab = np.repeat(np.arange(5), sizes)
+    recon = (cents[lab].reshape(-1, 16, pl) + cbs[np.arange(16)[None, :], codes]).reshape(-1, 32)
+    ref = q.astype(np.float64) @ recon.astype(np.float64).T
+    order = np.argsort(-ref, axis=1, kind="stable")[:, :10]
+    np.testing.assert_allclose(d, np.take_along_axis(ref, order, 1), rtol=1e-4, atol=1e-4)
+    assert (np.diff(d, axis=1) <= 0).all()
+    assert (ids[order] == i).mean() > 0.95
+    # probes rank the centroids by inner product
+    cp = np.argsort(-(q.astype(np.float64) @ cents.astype(np.float64).T), axis=1, kind="stable")
+    np.testing.assert_array_equal(p, cp[:, :5])

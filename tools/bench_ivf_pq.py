@@ -34,9 +34,9 @@ def main():
     ap.add_argument("--gt-queries", type=int, default=1000)
     ap.add_argument("--centers", type=int, default=65536)
     ap.add_argument("--sigma", type=float, default=0.75)
-    ap.add_argument("--refine-ratios", default="2,4,6",
-                    help="cuVS-style refinement: ivf_pq.search for ratio*k candidates (<= 64), then exact "
-                         "re-ranking against the fp16 rows (mivs.neighbors.refine)")
+    ap.add_argument("--refine-ratios", default="4,10,20,40",
+                    help="cuVS-style refinement: ivf_pq.search for ratio*k candidates, then exact re-ranking "
+                         "against the fp16 rows (mivs.neighbors.refine)")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     n, d, Q, k = a.rows, a.dim, a.queries, a.k
@@ -92,7 +92,7 @@ def main():
               file=sys.stderr, flush=True)
         refined = []
         for ratio in [int(r) for r in a.refine_ratios.split(",") if r.strip()]:
-            kc = min(64, ratio * k)
+            kc = ratio * k
             _, cand = ivf_pq.search(sp, idx, q, kc)
             refine(x, q, cand, k)
             torch.cuda.synchronize()
