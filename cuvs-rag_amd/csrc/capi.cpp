@@ -996,10 +996,11 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   ws.cand_off.reserve(sizeof(int64_t) * (nq + 1));
   ws.cand_key.reserve(sizeof(float) * max_cand);
   ws.cand_pos.reserve(sizeof(int) * max_cand);
-  ws.rs_bucket_tmp.reserve(rs_bucket_tmp_bytes((int)nq));
+  ws.rs_bucket_tmp.reserve(rs_bucket_tmp_bytes((int)nq, n_waves));
   HIPCHK(hipMemsetAsync(a.wave_cnt + n_waves, 0, sizeof(int), s));
   HIPCHK(launch_rs_bucket(a.wave_buf, a.wave_cap, a.wave_cnt, n_waves, (int)nq, ws.cand_off.as<int64_t>(),
-                          ws.cand_key.as<float>(), ws.cand_pos.as<int>(), ws.rs_bucket_tmp.p, a.wave_cnt + n_waves, s));
+                          ws.cand_key.as<float>(), ws.cand_pos.as<int>(), ws.rs_bucket_tmp.p, a.wave_cnt + n_waves,
+                          4 * cu_count(idx->device), s));
   // 5. exact ranking of every query's run (slot = one entry)
   pf_refine_fallback(idx, s, q, nq, k, np, out_d, out_i, ws.cand_key.as<float>(), ws.cand_pos.as<int>(), nullptr,
                      a.wave_cnt + n_waves, ws.cand_off.as<int64_t>(), 1, true);

@@ -289,11 +289,39 @@ size_t rs_scan_lds_bytes(int dp);
 bool rs_scan_supported(int dp);
 hipError_t launch_rs_scan(const RsScanArgs& a, int dp, int grid, hipStream_t s);
 int64_t rs_tiles_bytes(int64_t ne, int n_lists, int dp);
-// K13's per-wave candidate streams -> per-query CSR runs (cand_off [nq + 1]); work: [nq + 1] int64 counts,
-// [nq] int fill, scan tmp (scan_tmp_bytes(nq + 1)); lost: set when a stream overflowed
-size_t rs_bucket_tmp_bytes(int nq);
+// block-wide exclusive scan of one value per thread (returns exclusive prefix, total via *tot)
+__device__ inline int64_t block_excl_scan(int64_t v, int64_t* sh, int64_t* tot) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  int64_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sh[wave] = x;
+  __syncthreads();
+  if (wave == 0) {
+    int64_t s = lane < nw ? sh[lane] : 0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t y = __shfl_up(s, o);
+      if (lane >= o) s += y;
+    }
+    if (lane < nw) sh[lane] = s;  // inclusive wave totals
+  }
+  __syncthreads();
+  const int64_t base = wave > 0 ? sh[wave - 1] : 0;
+  if (tot) *tot = sh[nw - 1];
+  __syncthreads();
+  return base + x - v;
+}
+
+// K13's per-wave candidate streams -> per-query CSR runs (cand_off [nq + 1]); tmp >= rs_bucket_tmp_bytes;
+// lost: set when a stream overflowed; grid: workgroups of the flat count / scatter
+size_t rs_bucket_tmp_bytes(int nq, int n_waves);
 hipError_t launch_rs_bucket(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
-                            int64_t* cand_off, float* cand_key, int* cand_pos, void* tmp, int* lost, hipStream_t s);
+                            int64_t* cand_off, float* cand_key, int* cand_pos, void* tmp, int* lost, int grid,
+                            hipStream_t s);
 hipError_t launch_rs_pre_lists(const int64_t* goff, int n_lists, int div, int min_groups, const int64_t* probes,
                                int64_t nq, int np, int64_t* goff2, int64_t* probes2, hipStream_t s);
 hipError_t launch_rs_items(const int* work_off, const int* bucket_off, const int64_t* list_goff, int n_lists,

@@ -13,32 +13,6 @@ constexpr int kScanBlock = 1024;
 constexpr int kScanPerThread = 4;
 constexpr int kScanTile = kScanBlock * kScanPerThread;
 
-// block-wide exclusive scan of one value per thread (returns exclusive prefix, total via *tot)
-__device__ int64_t block_excl_scan(int64_t v, int64_t* sh, int64_t* tot) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
-  int64_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int64_t y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) sh[wave] = x;
-  __syncthreads();
-  if (wave == 0) {
-    int64_t s = lane < nw ? sh[lane] : 0;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int64_t y = __shfl_up(s, o);
-      if (lane >= o) s += y;
-    }
-    if (lane < nw) sh[lane] = s;  // inclusive wave totals
-  }
-  __syncthreads();
-  const int64_t base = wave > 0 ? sh[wave - 1] : 0;
-  if (tot) *tot = sh[nw - 1];
-  __syncthreads();
-  return base + x - v;
-}
 
 __global__ __launch_bounds__(kScanBlock) void k_scan_reduce(const int64_t* __restrict__ in, int64_t n,
                                                             int64_t* __restrict__ sums) {

@@ -548,57 +548,87 @@ hipError_t launch_rs_items(const int* work_off, const int* bucket_off, const int
   return hipGetLastError();
 }
 
-constexpr int kRsBucketSplit = 8;
-
-// K13's per-wave candidate streams -> per-query CSR runs for K11 (count, scan, scatter). A stream longer
-// than its capacity lost entries of unknown queries: `lost` is then set and K11 proves no query (every
-// query goes to the fallback search).
-__global__ __launch_bounds__(256) void k_rs_count(const int4* __restrict__ wave_buf, int wave_cap,
-                                                  const int* __restrict__ wave_cnt,
-                                                  unsigned long long* __restrict__ qcnt, int* __restrict__ lost) {
-  // (kRsBucketSplit blocks per stream: the streams' lengths differ by orders of magnitude)
-  const int w = blockIdx.x / kRsBucketSplit, sub = blockIdx.x % kRsBucketSplit;
-  const int n = wave_cnt[w];
-  if (n > wave_cap && sub == 0 && threadIdx.x == 0) atomicOr(lost, 1);
-  const int4* ws = wave_buf + (int64_t)w * wave_cap;
-  for (int i = sub * blockDim.x + threadIdx.x; i < (n < wave_cap ? n : wave_cap); i += kRsBucketSplit * blockDim.x)
-    atomicAdd(qcnt + ws[i].z, 1ull);
+// K13's per-wave candidate streams -> per-query CSR runs for K11: stream offsets (one workgroup), then
+// count and scatter over the flat index of all entries (a thread per entry, whatever the streams'
+// lengths, which differ by orders of magnitude). A stream longer than its capacity lost entries of
+// unknown queries: `lost` is then set and K11 proves no query (every query goes to the fallback search).
+__global__ __launch_bounds__(1024) void k_rs_stream_off(const int* __restrict__ wave_cnt, int n_waves, int wave_cap,
+                                                        int64_t* __restrict__ woff, int* __restrict__ lost) {
+  __shared__ int64_t sh[16];
+  int64_t base = 0;
+  for (int w0 = 0; w0 < n_waves; w0 += 1024) {
+    const int w = w0 + threadIdx.x;
+    int64_t c = 0;
+    if (w < n_waves) {
+      const int n = wave_cnt[w];
+      if (n > wave_cap) atomicOr(lost, 1);
+      c = n < wave_cap ? n : wave_cap;
+    }
+    int64_t tot;
+    const int64_t ex = block_excl_scan(c, sh, &tot);
+    if (w < n_waves) woff[w] = base + ex;
+    base += tot;
+  }
+  if (threadIdx.x == 0) woff[n_waves] = base;
 }
 
-__global__ __launch_bounds__(256) void k_rs_scatter(const int4* __restrict__ wave_buf, int wave_cap,
-                                                    const int* __restrict__ wave_cnt, const int64_t* __restrict__ off,
-                                                    int* __restrict__ fill, float* __restrict__ key,
-                                                    int* __restrict__ pos) {
-  const int w = blockIdx.x / kRsBucketSplit, sub = blockIdx.x % kRsBucketSplit;
-  const int n = wave_cnt[w];
-  const int4* ws = wave_buf + (int64_t)w * wave_cap;
-  for (int i = sub * blockDim.x + threadIdx.x; i < (n < wave_cap ? n : wave_cap); i += kRsBucketSplit * blockDim.x) {
-    const int4 e = ws[i];
-    const int64_t at = off[e.z] + atomicAdd(fill + e.z, 1);
-    key[at] = __int_as_float(e.x);
-    pos[at] = e.y;
+// entry e of the flat index -> (stream, index in the stream)
+__device__ __forceinline__ int rs_stream_of(const int64_t* woff, int n_waves, int64_t e) {
+  int lo = 0, hi = n_waves - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (woff[mid] <= e) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void k_rs_count(const int4* __restrict__ wave_buf, int wave_cap,
+                                                  const int64_t* __restrict__ woff, int n_waves,
+                                                  unsigned long long* __restrict__ qcnt) {
+  const int64_t total = woff[n_waves];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int w = rs_stream_of(woff, n_waves, e);
+    atomicAdd(qcnt + wave_buf[(int64_t)w * wave_cap + (e - woff[w])].z, 1ull);
   }
 }
 
-size_t rs_bucket_tmp_bytes(int nq) {
-  return sizeof(int64_t) * ((size_t)nq + 1) + sizeof(int) * (size_t)nq + scan_tmp_bytes(nq + 1) + 64;
+__global__ __launch_bounds__(256) void k_rs_scatter(const int4* __restrict__ wave_buf, int wave_cap,
+                                                    const int64_t* __restrict__ woff, int n_waves,
+                                                    const int64_t* __restrict__ off, int* __restrict__ fill,
+                                                    float* __restrict__ key, int* __restrict__ pos) {
+  const int64_t total = woff[n_waves];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int w = rs_stream_of(woff, n_waves, e);
+    const int4 v = wave_buf[(int64_t)w * wave_cap + (e - woff[w])];
+    const int64_t at = off[v.z] + atomicAdd(fill + v.z, 1);
+    key[at] = __int_as_float(v.x);
+    pos[at] = v.y;
+  }
+}
+
+size_t rs_bucket_tmp_bytes(int nq, int n_waves) {
+  return sizeof(int64_t) * ((size_t)nq + 1) + sizeof(int) * (size_t)nq + sizeof(int64_t) * ((size_t)n_waves + 1) +
+         scan_tmp_bytes(nq + 1) + 64;
 }
 
 hipError_t launch_rs_bucket(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
-                            int64_t* cand_off, float* cand_key, int* cand_pos, void* tmp, int* lost, hipStream_t s) {
+                            int64_t* cand_off, float* cand_key, int* cand_pos, void* tmp, int* lost, int grid,
+                            hipStream_t s) {
   int64_t* qcnt = static_cast<int64_t*>(tmp);
   int* fill = reinterpret_cast<int*>(qcnt + nq + 1);
-  void* stmp = reinterpret_cast<char*>(tmp) + ((sizeof(int64_t) * ((size_t)nq + 1) + sizeof(int) * (size_t)nq + 15) & ~(size_t)15);
+  int64_t* woff = reinterpret_cast<int64_t*>(
+      reinterpret_cast<char*>(tmp) + ((sizeof(int64_t) * ((size_t)nq + 1) + sizeof(int) * (size_t)nq + 15) & ~(size_t)15));
+  void* stmp = reinterpret_cast<char*>(woff) + ((sizeof(int64_t) * ((size_t)n_waves + 1) + 15) & ~(size_t)15);
   hipError_t e = hipMemsetAsync(qcnt, 0, sizeof(int64_t) * ((size_t)nq + 1) + sizeof(int) * (size_t)nq, s);
   if (e != hipSuccess) return e;
-  if (n_waves > 0)
-    hipLaunchKernelGGL(k_rs_count, dim3((unsigned)n_waves * kRsBucketSplit), dim3(256), 0, s, wave_buf, wave_cap, wave_cnt,
-                       reinterpret_cast<unsigned long long*>(qcnt), lost);
+  if (n_waves <= 0) return launch_exclusive_scan_i64(qcnt, cand_off, nq + 1, stmp, s);
+  hipLaunchKernelGGL(k_rs_stream_off, dim3(1), dim3(1024), 0, s, wave_cnt, n_waves, wave_cap, woff, lost);
+  hipLaunchKernelGGL(k_rs_count, dim3((unsigned)grid), dim3(256), 0, s, wave_buf, wave_cap, woff, n_waves,
+                     reinterpret_cast<unsigned long long*>(qcnt));
   e = launch_exclusive_scan_i64(qcnt, cand_off, nq + 1, stmp, s);
   if (e != hipSuccess) return e;
-  if (n_waves > 0)
-    hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)n_waves * kRsBucketSplit), dim3(256), 0, s, wave_buf, wave_cap, wave_cnt, cand_off,
-                       fill, cand_key, cand_pos);
+  hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)grid), dim3(256), 0, s, wave_buf, wave_cap, woff, n_waves, cand_off,
+                     fill, cand_key, cand_pos);
   return hipGetLastError();
 }
 

