@@ -985,10 +985,11 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
     }
     fprintf(stderr, "[k13 blocks] span %.1f us | busy mean %.1f max %.1f us | tiles mean %.1f max %llu\n",
             (t1 - t0) / 100.0, busy_sum / grid / 100.0, busy_max / 100.0, (double)tiles_sum / grid, tiles_max);
-    const double wc = (double)(h[3 * grid] + h[3 * grid + 1] + h[3 * grid + 2]);
+    const double wc = (double)(h[3 * grid] + h[3 * grid + 1] + h[3 * grid + 2] + h[3 * grid + 3]);
     if (wc > 0)
-      fprintf(stderr, "[k13 phases] wave-cycles %.4g | wait+barrier %.3f mfma-loop %.3f epilogue %.3f | "
-              "cycles/tile/wave %.0f\n", wc, h[3 * grid] / wc, h[3 * grid + 1] / wc, h[3 * grid + 2] / wc,
+      fprintf(stderr, "[k13 phases] wave-cycles %.4g | ready-wait %.3f mfma-loop %.3f own-dma-wait %.3f epilogue %.3f | "
+              "cycles/tile/wave %.0f\n", wc, h[3 * grid] / wc, h[3 * grid + 1] / wc, h[3 * grid + 3] / wc,
+              h[3 * grid + 2] / wc,
               tiles_sum ? wc / ((double)tiles_sum * kRsWaves) : 0.0);
   }
   // the streams into per-query CSR runs (every stream entry fits: at most n_waves * wave_cap of them)
@@ -1715,8 +1716,10 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
       a.pq_half = (int)ceil_div(ceil_div(idx->pq_dim, 2), 16) * 16;
       a.ip = idx->metric == MIVS_METRIC_IP ? 1 : 0;
       a.probes_d = ws.probes_d.as<float>();
+      // (MIVS_PQ_SPLIT=0 asks for K9 where its whole LUT and merge area fit LDS)
       const char* spe = getenv("MIVS_PQ_SPLIT");
-      const bool split = !(spe && spe[0] == '0') && !(a.flags & 7);
+      const bool k9_fits = pq_scan_lds_bytes(idx->rot_dim_pad, idx->pq_dim, kcap) <= 160 * 1024;
+      const bool split = (!(spe && spe[0] == '0') || !k9_fits) && !(a.flags & 7);
       if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
       hipError_t se = split ? launch_pq_scan_split(a, kcap, s) : hipErrorNotSupported;
       if (se == hipErrorNotSupported) se = launch_pq_scan(a, kcap, s);

@@ -177,7 +177,7 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   int n_tiles_done = 0;
   int tt = 0;               // tiles this workgroup has started
   bool spun_out = false;    // a ready-wait gave up (never expected): the results are then not trusted
-  uint64_t pw_wait = 0, pw_loop = 0, pw_epi = 0;  // flags & 16: this wave's cycles per tile phase
+  uint64_t pw_wait = 0, pw_loop = 0, pw_epi = 0, pw_dma = 0;  // flags & 16: this wave's cycles per tile phase
   const int widx = blockIdx.x * kRsWaves + wave;
   int4* const wstream = a.wave_buf + (int64_t)widx * a.wave_cap;
   int wcnt = 0;  // entries of this wave's candidate stream
@@ -194,6 +194,7 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
       atomicAdd(p + 0, (unsigned long long)pw_wait);
       atomicAdd(p + 1, (unsigned long long)pw_loop);
       atomicAdd(p + 2, (unsigned long long)pw_epi);
+      atomicAdd(p + 3, (unsigned long long)pw_dma);
     }
   };
   if (w >= hi) {
@@ -234,6 +235,7 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
 #pragma unroll
     for (int s = 0; s < NK; ++s) ra[s] = ld_rows(r0, s);
   }
+  float xnmin = 0.0f;  // the smallest row norm of the wave's group in the current item
   int par = 0;  // LDS buffer of the current tile
   int ipar = 0;           // item parity: the s_norm half of this item
   const f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -316,6 +318,7 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
       // (one fewer than counted: the order of a k-step's row load and DMA piece is the compiler's)
       rs_wait_vm(LAST && has_next ? NK - 3 - NK / kRsWaves : 0);
       rs_signal(s_ready);
+      const uint64_t ph2b = (a.flags & 16) ? __builtin_amdgcn_s_memtime() : 0;
       // epilogue: lane (j, h) holds the 16 dots of query j with rows (r & 3) + 8 (r >> 2) + 4 h
       if (gv && !(a.flags & 1)) {
         // header of query j: {qs, uf, qn, q}
@@ -324,17 +327,13 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
         const float mm = METRIC == kL2 ? -2.0f * qs : -qs;
         // one-fma filter over the 16 keys (norms from LDS four at a time: registers are short); the rare
         // survivors are then handled one at a time, picked out of the accumulator by selects
-        // common case first: the smallest filter value of the lane against uf (fma + min per key); the
-        // hit mask is formed only when some lane of the wave has a hit
-        float fmin = INFINITY;
+        // common case first, without the norms: mm < 0, so every filter value fma(acc_r, mm, xn_r) is
+        // >= fma(max_r acc_r, mm, min_r xn_r) (exact ordering, one monotone rounding); only when that
+        // bound reaches uf in some lane is the hit mask formed from the row norms
+        float amax = acc[0];
 #pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4) {
-          const float4 v = *reinterpret_cast<const float4*>(wnorm + 8 * q4 + 4 * h);
-          const float xv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-          for (int u = 0; u < 4; ++u) fmin = fminf(fmin, fmaf(acc[4 * q4 + u], mm, METRIC == kL2 ? xv[u] : 0.0f));
-        }
-        if (__ballot(fmin < uf) != 0) {
+        for (int r = 1; r < 16; ++r) amax = fmaxf(amax, acc[r]);
+        if (__ballot(fmaf(amax, mm, METRIC == kL2 ? xnmin : 0.0f) < uf) != 0) {
           unsigned hits = 0;
 #pragma unroll
           for (int q4 = 0; q4 < 4; ++q4) {
@@ -373,7 +372,8 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
         const uint64_t ph3 = __builtin_amdgcn_s_memtime();
         pw_wait += ph1 - ph0;
         pw_loop += ph2 - ph1;
-        pw_epi += ph3 - ph2;
+        pw_dma += ph2b - ph2;
+        pw_epi += ph3 - ph2b;
       }
       par ^= 1;
     };
@@ -381,6 +381,12 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
     // first item, the prologue's DMA pieces too, which this wave then signals as tile 0's
     __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
     if (tt == 0) rs_signal(s_ready);
+    {  // the smallest row norm of this wave's group (its norms landed with the rows; pad rows: +inf)
+      float m = s_norm[(ipar * kRsWaves + wave) * 64 + j];
+#pragma unroll
+      for (int off = 16; off >= 1; off >>= 1) m = fminf(m, __shfl_xor(m, off));
+      xnmin = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(m)));
+    }
     for (int t = 0; t + 1 < ntiles; ++t) tile(t, BoolC<false>{});
     tile(ntiles - 1, BoolC<true>{});
     n_tiles_done += ntiles;
@@ -572,6 +578,14 @@ __global__ __launch_bounds__(1024) void k_rs_stream_off(const int* __restrict__ 
   if (threadIdx.x == 0) woff[n_waves] = base;
 }
 
+// the stream offsets in LDS (binary searches there, not through L2)
+constexpr int kRsMaxStreams = 4096;
+__device__ __forceinline__ const int64_t* rs_woff_lds(const int64_t* woff, int n_waves, int64_t* sw) {
+  for (int i = threadIdx.x; i <= n_waves; i += blockDim.x) sw[i] = woff[i];
+  __syncthreads();
+  return sw;
+}
+
 // entry e of the flat index -> (stream, index in the stream)
 __device__ __forceinline__ int rs_stream_of(const int64_t* woff, int n_waves, int64_t e) {
   int lo = 0, hi = n_waves - 1;
@@ -585,6 +599,8 @@ __device__ __forceinline__ int rs_stream_of(const int64_t* woff, int n_waves, in
 __global__ __launch_bounds__(256) void k_rs_count(const int4* __restrict__ wave_buf, int wave_cap,
                                                   const int64_t* __restrict__ woff, int n_waves,
                                                   unsigned long long* __restrict__ qcnt) {
+  __shared__ int64_t sw[kRsMaxStreams + 1];
+  woff = rs_woff_lds(woff, n_waves, sw);
   const int64_t total = woff[n_waves];
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
     const int w = rs_stream_of(woff, n_waves, e);
@@ -596,6 +612,8 @@ __global__ __launch_bounds__(256) void k_rs_scatter(const int4* __restrict__ wav
                                                     const int64_t* __restrict__ woff, int n_waves,
                                                     const int64_t* __restrict__ off, int* __restrict__ fill,
                                                     float* __restrict__ key, int* __restrict__ pos) {
+  __shared__ int64_t sw[kRsMaxStreams + 1];
+  woff = rs_woff_lds(woff, n_waves, sw);
   const int64_t total = woff[n_waves];
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
     const int w = rs_stream_of(woff, n_waves, e);
@@ -622,6 +640,7 @@ hipError_t launch_rs_bucket(const int4* wave_buf, int wave_cap, const int* wave_
   hipError_t e = hipMemsetAsync(qcnt, 0, sizeof(int64_t) * ((size_t)nq + 1) + sizeof(int) * (size_t)nq, s);
   if (e != hipSuccess) return e;
   if (n_waves <= 0) return launch_exclusive_scan_i64(qcnt, cand_off, nq + 1, stmp, s);
+  if (n_waves > kRsMaxStreams) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_rs_stream_off, dim3(1), dim3(1024), 0, s, wave_cnt, n_waves, wave_cap, woff, lost);
   hipLaunchKernelGGL(k_rs_count, dim3((unsigned)grid), dim3(256), 0, s, wave_buf, wave_cap, woff, n_waves,
                      reinterpret_cast<unsigned long long*>(qcnt));
