@@ -459,17 +459,18 @@ __global__ __launch_bounds__(256) void k_rs_tiles(const int64_t* __restrict__ bu
   if (m <= 0) return;
   const int ntiles = (m + kRsQTile - 1) / kRsQTile;
   constexpr int64_t IMG = (int64_t)(NK + 1) * 1024;
-  constexpr int PER = 2 * NK;  // 16-B pieces of one query row
   char* base = tiles + rs_tile_slot(bucket_off, l, 0) * IMG;
-  for (int i = threadIdx.x; i < ntiles * kRsQTile * PER; i += blockDim.x) {
-    const int t = i / (kRsQTile * PER), r = i - t * (kRsQTile * PER);
-    const int jq = r / PER, u = r - jq * PER;  // query jq of tile t, 16-B piece u of its row
-    const int s = u >> 1, hh = u & 1;
+  // image order (lane L of piece s of tile t fastest): every wave-instruction stores 1 KiB contiguous;
+  // lanes L and L + 32 read the two adjacent 16-B halves of one query's 32 B of k-step s
+  for (int i = threadIdx.x; i < ntiles * NK * 64; i += blockDim.x) {
+    const int t = i / (NK * 64), r = i - t * (NK * 64);
+    const int s = r >> 6, L = r & 63;
+    const int jq = L & 31, hh = L >> 5;
     const int e = t * kRsQTile + jq;
     const int q = e < m ? (int)bucket_q[e0 + e] : -1;
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (q >= 0) v = *reinterpret_cast<const uint4*>(qh + (int64_t)q * (NK * 16) + 8 * u);
-    *reinterpret_cast<uint4*>(base + t * IMG + s * 1024 + (jq + 32 * hh) * 16) = v;
+    if (q >= 0) v = *reinterpret_cast<const uint4*>(qh + (int64_t)q * (NK * 16) + 8 * (2 * s + hh));
+    *reinterpret_cast<uint4*>(base + t * IMG + s * 1024 + L * 16) = v;
   }
   for (int i = threadIdx.x; i < ntiles * 64; i += blockDim.x) {
     const int t = i >> 6, L = i & 63, e = t * kRsQTile + (L & 31);
