@@ -1095,6 +1095,112 @@ void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t
   if (pr) HIPCHK(hipEventRecord(pr->e[3], s));
 }
 
+// K9r IVF-PQ search of queries whose probes are in ws.probes_i / probes_d: probe map in
+// (list, 16-query tile, kRtRows-row chunk) items, K9r, then K7 over the (query, probe, chunk) slots'
+// top-k (k <= 64) or K8 over their dumped keys (k > 64, in query batches bounded by the dump size)
+bool pq_rt_use(const mivs_index_s* idx, int k) {
+  const char* e = getenv("MIVS_PQ_RT");
+  return !(e && e[0] == '0') && pq_rt_supported(idx->rot_dim_pad, idx->pq_dim, idx->pq_len, k);
+}
+
+void pq_search_rt(mivs_index_s* idx, hipStream_t s, const float* d_q, int64_t nq, int k, int np, float* d_dist,
+                  int64_t* d_ids, ProfRec* pr) {
+  Workspace& ws = idx->ws;
+  const ListSet& L = idx->lists;
+  const bool dump = k > kMaxK;
+  int64_t max_chunks = 0;  // slots per query at most: the np longest lists' chunk counts
+  {
+    std::vector<int64_t> c(L.n_lists);
+    for (int l = 0; l < L.n_lists; ++l) c[l] = ceil_div(L.h_goff[l + 1] - L.h_goff[l], kRtGroups);
+    std::sort(c.begin(), c.end(), std::greater<int64_t>());
+    for (int l = 0; l < std::min<int>(np, L.n_lists); ++l) max_chunks += c[l];
+  }
+  max_chunks = std::max<int64_t>(max_chunks, 1);
+  const int64_t qb = dump ? select_batch(nq, (size_t)max_chunks * ((size_t)kRtRows * 4 + 16)) : nq;
+  const int flags = getenv("MIVS_PQ_FLAGS") ? atoi(getenv("MIVS_PQ_FLAGS")) : 0;
+  if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
+  for (int64_t b0 = 0; b0 < nq; b0 += qb) {
+    const int64_t nb = std::min<int64_t>(qb, nq - b0);
+    const int64_t ne = nb * np;
+    ws.counts.reserve(sizeof(int) * L.n_lists);
+    ws.fill.reserve(sizeof(int) * L.n_lists);
+    ws.bucket_off.reserve(sizeof(int) * (L.n_lists + 1));
+    ws.work_off.reserve(sizeof(int) * (L.n_lists + 1));
+    ws.bucket_q.reserve(sizeof(int64_t) * ne);
+    ws.bucket_slot.reserve(sizeof(int64_t) * ne);
+    ws.qp_slots.reserve(sizeof(int64_t) * ne);
+    ws.slot_begin.reserve(sizeof(int64_t) * (nb + 1));
+    const size_t stb = scan_tmp_bytes(ne) + sizeof(int64_t) * (size_t)ne;
+    ws.scan_tmp.reserve(stb);
+    const int64_t* probes = ws.probes_i.as<int64_t>() + b0 * np;
+    HIPCHK(launch_probe_map(probes, nb, np, L.n_lists, L.goff.as<int64_t>(), kRtGroups, kRtQ, ws.counts.as<int>(),
+                            ws.fill.as<int>(), ws.bucket_off.as<int>(), ws.work_off.as<int>(),
+                            ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(), ws.qp_slots.as<int64_t>(),
+                            ws.slot_begin.as<int64_t>(), ws.scan_tmp.p, stb, s));
+    const int64_t slots = nb * max_chunks;
+    ws.part_d.reserve(sizeof(float) * (size_t)slots * (dump ? kRtRows : k));
+    ws.part_i.reserve(sizeof(int64_t) * (size_t)slots * (dump ? 2 : k));
+    ws.counter.reserve(16);
+    HIPCHK(hipMemsetAsync(ws.counter.p, 0, sizeof(int), s));
+    PqTileArgs a{};
+    a.queries = d_q + b0 * (int64_t)idx->d;
+    a.cents = idx->centroids_rm.as<float>();
+    a.books = idx->pq_books.as<float>();
+    a.codes = static_cast<const uint8_t*>(idx->pq_codes.p);
+    a.row_ids = L.ids.as<int64_t>();
+    a.list_off = L.off.as<int64_t>();
+    a.list_goff = L.goff.as<int64_t>();
+    a.n_lists = L.n_lists;
+    a.bucket_q = ws.bucket_q.as<int64_t>();
+    a.bucket_slot = ws.bucket_slot.as<int64_t>();
+    a.bucket_off = ws.bucket_off.as<int>();
+    a.work_off = ws.work_off.as<int>();
+    a.work_counter = ws.counter.as<int>();
+    a.d = idx->d;
+    a.rot_dim_pad = idx->rot_dim_pad;
+    a.pq_dim = idx->pq_dim;
+    a.pq_dim_pad = idx->pq_dim_pad;
+    a.pq_len = idx->pq_len;
+    a.k = k;
+    a.out_d = ws.part_d.as<float>();
+    a.out_i = dump ? nullptr : ws.part_i.as<int64_t>();
+    a.slot_info = dump ? ws.part_i.as<int64_t>() : nullptr;
+    a.ip = idx->metric == MIVS_METRIC_IP ? 1 : 0;
+    a.probes = probes;
+    a.probes_d = ws.probes_d.as<float>() + b0 * np;
+    a.n_probes = np;
+    a.flags = flags;
+    HIPCHK(launch_pq_scan_rt(a, cu_count(idx->device), s));
+    if (dump) {
+      SelectArgs sa{};
+      sa.keys = ws.part_d.as<float>();
+      sa.row_ids = L.ids.as<int64_t>();
+      sa.slot_info = ws.part_i.as<int64_t>();
+      sa.slot_begin = ws.slot_begin.as<int64_t>();
+      sa.slot_rows = kRtRows;
+      sa.nq = nb;
+      sa.k = k;
+      sa.metric = idx->metric;
+      sa.out_d = d_dist + b0 * k;
+      sa.out_i = d_ids + b0 * k;
+      HIPCHK(launch_select(sa, s));
+    } else {
+      MergeArgs m{};
+      m.in_d = ws.part_d.as<float>();
+      m.in_i = ws.part_i.as<int64_t>();
+      m.slot_begin = ws.slot_begin.as<int64_t>();
+      m.nq = nb;
+      m.k_in = k;
+      m.k = k;
+      m.metric = idx->metric;
+      m.out_d = d_dist + b0 * k;
+      m.out_i = d_ids + b0 * k;
+      HIPCHK(launch_merge(m, s));
+    }
+  }
+  if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
+}
+
 void ivf_search_impl(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                      int64_t* out_i, int32_t* out_probes) {
   int64_t qb = nq;
@@ -1525,6 +1631,14 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
     // K8 selects per query, in query batches bounded by the select workspace -- measured 3x faster than
     // the 32/64-entry register lists at 40 candidates (profiles/r02_ivf_pq_refine_bench.log);
     // MIVS_PQ_DUMP_K raises the threshold (up to 64) for the register path
+    if (pq_rt_use(idx, k)) {
+      pq_search_rt(idx, s, d_q, nq, k, np, d_dist, d_ids, pr);
+      if (pr) HIPCHK(hipEventRecord(pr->e[3], s));
+      idx->last_nq = nq;
+      idx->last_np = np;
+      idx->last_k = k;
+      return;
+    }
     const char* dke = getenv("MIVS_PQ_DUMP_K");
     const int dump_k = std::min(kMaxK, std::max(16, dke ? atoi(dke) : 16));
     if (k > dump_k) {

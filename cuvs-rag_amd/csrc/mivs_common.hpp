@@ -144,7 +144,26 @@ struct PqTileArgs {
   int d, rot_dim_pad, pq_dim, pq_dim_pad, pq_len, k;
   float* out_d;     // [slots][k]
   int64_t* out_i;
+  // K9r only (k_pq_scan_rt): inner product (the probes' coarse keys by list id), DUMP mode outputs
+  int ip;
+  const int64_t* probes;    // [nq][n_probes]
+  const float* probes_d;    // [nq][n_probes]
+  int n_probes;
+  int64_t* slot_info;       // DUMP: [slots][2] = (first row position, rows); out_d is [slots][kRtRows]
+  int flags;                // timing experiments only (MIVS_PQ_FLAGS): 1 skip LUT build, 2 skip row scan
 };
+
+// K9r (k_pq_scan_rt, pq.hip): work item = (list, <= 16 queries probing it, chunk of kRtRows rows); the
+// 16 queries' LUT of one subspace ([code][query], 80-B rows) in LDS, each of 512 threads holds 8 rows x
+// 16 queries of sums in registers
+constexpr int kRtThreads = 512;
+constexpr int kRtQ = 16;
+constexpr int kRtRpt = 8;
+constexpr int kRtRows = kRtThreads * kRtRpt;  // 4096
+constexpr int kRtGroups = kRtRows / 32;
+size_t pq_rt_lds_bytes(int rot_dim_pad, int k);
+bool pq_rt_supported(int rot_dim_pad, int pq_dim, int pq_len, int k);
+hipError_t launch_pq_scan_rt(const PqTileArgs& a, int grid, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // fp16 pre-filter + exact refine (prefilter.hip).

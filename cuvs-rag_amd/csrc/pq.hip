@@ -761,6 +761,352 @@ __global__ __launch_bounds__(512) void k_pq_scan_tiled(PqTileArgs a) {
   }
 }
 
+// K9r: the IVF-PQ scan with the QUERIES of a list tiled and the ROWS register-stationary.
+//
+// K9/K9s build one query's whole LUT per (query, probe) and gather LUT_j[code] with ds_read_b32: 64
+// random 4-B addresses per wave-instruction, ~3.5-way bank-conflicted, one useful float per lane.
+// K9r turns the gather around. A work item is (list l, tile of <= 16 queries probing l, chunk of
+// kRtRows rows); per subspace j the tile's LUT_j is stored code-major -- row c holds LUT_j[c] of the 16
+// queries (64 B, padded to 80 B so that the 16-lane groups of ds_read_b128 spread over the 64 banks)
+// -- and each thread adds, for each of its 8 rows, the 16 queries' entries of the row's code: four
+// ds_read_b128 per (row, subspace), 16 useful floats per lane per 4 reads. The sums of 8 rows x 16
+// queries stay in registers across all subspaces, each row's sum running j = 0, 1, ... from 0 as in
+// K9 and the oracle. LUT_{j+1} is built (the K9 fmaf chain, thread = (code, 8 queries), its codebook
+// row prefetched from L2 a subspace ahead) into the other half of a double buffer while LUT_j is read.
+//
+// Output (CQ > 0, k <= 64): per (query, chunk) slot the exact top-k by (key, row) for K7: bound_q =
+// the k-th smallest of the 512 per-thread minima (>= k distinct rows lie at or below it, so every row
+// of the slot's top-k does too); rows <= bound_q -> LDS (at most 8 (k - 1) below it plus ties), and a
+// wave picks k by rounds of 64-lane minima. A slot whose list overflows CQ (many tied keys) is finished
+// by block-wide rounds over the registers instead. CQ == 0 (DUMP, k > 64): every row's key ->
+// out_d[slot][kRtRows] and (first row position, rows) -> slot_info for K8.
+__device__ __forceinline__ uint32_t rt_ord(float f) {  // orderable bits, -0 and +0 equal
+  const uint32_t u = __float_as_uint(f == 0.0f ? 0.0f : f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__device__ __forceinline__ bool rt_less(float ka, int ra, float kb, int rb) {
+  return ka < kb || (ka == kb && ra < rb);
+}
+
+template <int PL4, int CQ>
+__global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
+  constexpr int NT = kRtThreads, TQ = kRtQ, RPT = kRtRpt, R = kRtRows, LS = 20, PL = 4 * PL4;
+  constexpr bool DUMP = CQ == 0;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int64_t* s_q = reinterpret_cast<int64_t*>(smem);        // [TQ] query (-1: no query)
+  int64_t* s_slot = s_q + TQ;                             // [TQ] output slot
+  int* s_misc = reinterpret_cast<int*>(s_slot + TQ);      // [16]
+  int* s_cnt = s_misc + 16;                               // [TQ] candidates <= bound
+  uint32_t* s_bound = reinterpret_cast<uint32_t*>(s_cnt + TQ);  // [TQ]
+  float* s_base = reinterpret_cast<float*>(s_bound + TQ);       // [TQ] IP: the probe's coarse key
+  const int rdp = a.rot_dim_pad;
+  float* s_res = reinterpret_cast<float*>(smem + 512);    // [TQ][rdp] residuals (IP: the queries)
+  float* s_lut = s_res + TQ * rdp;                        // [2][256][LS]
+  // after the subspace loop (aliasing s_res / s_lut)
+  uint32_t* s_min = reinterpret_cast<uint32_t*>(smem + 512);   // [TQ][NT]
+  float* s_ck = reinterpret_cast<float*>(s_min + TQ * NT);     // [TQ][CQ]
+  int* s_cr = reinterpret_cast<int*>(s_ck + TQ * (CQ > 0 ? CQ : 1));
+  float* s_wk = reinterpret_cast<float*>(smem + 512);          // slow path: [NT/64] wave minima
+  int* s_wr = reinterpret_cast<int*>(s_wk + NT / 64);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c_own = tid & 255, qh = tid >> 8;  // LUT build: code, half of the tile's queries
+  const int total = a.work_off[a.n_lists];
+  for (;;) {
+    if (tid == 0) s_misc[0] = atomicAdd(a.work_counter, 1);
+    __syncthreads();
+    const int w = s_misc[0];
+    if (w >= total) break;
+    int lo = 0, hi = a.n_lists - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (a.work_off[mid] <= w) lo = mid; else hi = mid - 1;
+    }
+    const int l = lo;
+    const int m = a.bucket_off[l + 1] - a.bucket_off[l];
+    const int tiles = (m + TQ - 1) / TQ;
+    const int local = w - a.work_off[l];
+    const int chunk = local / tiles;
+    const int tile = local - chunk * tiles;
+    const int e0 = a.bucket_off[l] + tile * TQ;
+    const int nqt = m - tile * TQ < TQ ? m - tile * TQ : TQ;
+    const int64_t nrows = a.list_off[l + 1] - a.list_off[l];
+    const int64_t r0 = (int64_t)chunk * R;
+    const int nr = (int)(nrows - r0 < R ? nrows - r0 : R);
+    const int64_t g0 = a.list_goff[l];
+    if (tid < TQ) {
+      const bool v = tid < nqt;
+      s_q[tid] = v ? a.bucket_q[e0 + tid] : -1;
+      s_slot[tid] = v ? a.bucket_slot[e0 + tid] + chunk : -1;
+      s_cnt[tid] = 0;
+      s_base[tid] = 0.0f;
+    }
+    __syncthreads();
+    if (a.ip) {  // the probe's coarse key -(q . c_l), found by list id among the query's probes
+      for (int t = wave; t < TQ; t += NT / 64) {
+        const int64_t q = s_q[t];
+        if (q < 0) continue;
+        for (int p0 = 0; p0 < a.n_probes; p0 += 64) {
+          const int p = p0 + lane;
+          const uint64_t mk = __ballot(p < a.n_probes && a.probes[q * a.n_probes + p] == l);
+          if (mk) {
+            if (lane == 0) s_base[t] = -a.probes_d[q * a.n_probes + p0 + __builtin_ctzll(mk)];
+            break;
+          }
+        }
+      }
+    }
+    for (int i = tid; i < TQ * rdp; i += NT) {
+      const int t = i / rdp, c = i - t * rdp;
+      const int64_t q = s_q[t];
+      float v = 0.0f;
+      if (q >= 0 && c < a.d) v = a.ip ? a.queries[q * a.d + c] : a.queries[q * a.d + c] - a.cents[(int64_t)l * a.d + c];
+      s_res[i] = v;
+    }
+    // LUT_j (j < pq_dim) into buffer `buf`: thread (c_own, qh) computes the 8 entries (qh * 8 + u, c_own)
+    float bk[2][PL];  // codebook rows of subspaces j + 1 (parity (j + 1) & 1) and j + 2: no register copies
+    auto load_book = [&](int j, float (&b)[PL]) {
+      const float4* src = reinterpret_cast<const float4*>(a.books + ((int64_t)j * kPqCodes + c_own) * PL);
+#pragma unroll
+      for (int c4 = 0; c4 < PL4; ++c4) {
+        const float4 v = src[c4];
+        b[4 * c4] = v.x; b[4 * c4 + 1] = v.y; b[4 * c4 + 2] = v.z; b[4 * c4 + 3] = v.w;
+      }
+    };
+    auto build = [&](int j, const float (&b)[PL], int buf) {
+      float e[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int t = qh * 8 + u;
+        const float4* r4 = reinterpret_cast<const float4*>(s_res + t * rdp + j * PL);
+        float acc = 0.0f;
+#pragma unroll
+        for (int c4 = 0; c4 < PL4; ++c4) {
+          const float4 r = r4[c4];
+          acc = pq_lut_term(a.ip, r.x, b[4 * c4], acc);
+          acc = pq_lut_term(a.ip, r.y, b[4 * c4 + 1], acc);
+          acc = pq_lut_term(a.ip, r.z, b[4 * c4 + 2], acc);
+          acc = pq_lut_term(a.ip, r.w, b[4 * c4 + 3], acc);
+        }
+        e[u] = pq_lut_entry(a.ip, acc, j == 0, s_base[t]);
+        __builtin_amdgcn_sched_barrier(0);  // one entry's residual reads in flight
+      }
+      float4* dst = reinterpret_cast<float4*>(s_lut + (buf * kPqCodes + c_own) * LS + qh * 8);
+      dst[0] = make_float4(e[0], e[1], e[2], e[3]);
+      dst[1] = make_float4(e[4], e[5], e[6], e[7]);
+    };
+    load_book(0, bk[0]);
+    if (a.pq_dim > 1) load_book(1, bk[1]);
+    __syncthreads();  // s_res, s_base
+    if (!(a.flags & 1)) build(0, bk[0], 0);
+    if (a.pq_dim > 2) load_book(2, bk[0]);
+
+    // my rows: i * NT + tid of the chunk; their codes, 16 subspaces (one uint4) per chunk ch
+    float acc[RPT][TQ];
+#pragma unroll
+    for (int i = 0; i < RPT; ++i)
+#pragma unroll
+      for (int t = 0; t < TQ; ++t) acc[i][t] = 0.0f;
+    // my rows' code offsets from the list's first group (32-bit: a list's codes are < 2 GiB)
+    const uint8_t* lcodes = a.codes + g0 * (int64_t)kGroupRows * a.pq_dim_pad;
+    int coff[RPT];
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int row = i * NT + tid;
+      const int pos = (int)r0 + (row < nr ? row : 0);
+      coff[i] = (pos / kGroupRows) * kGroupRows * a.pq_dim_pad + (pos % kGroupRows) * 16;
+    }
+    // one 4-B code word (4 subspaces) per row at a time, the next word requested a word ahead
+    uint32_t cw[RPT], nw[RPT];
+    const int nwd = (a.pq_dim + 3) >> 2;
+    auto load_word = [&](int wq, uint32_t (&dst)[RPT]) {
+      const uint8_t* base = lcodes + (wq >> 2) * (kGroupRows * 16) + (wq & 3) * 4;
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) dst[i] = *reinterpret_cast<const uint32_t*>(base + coff[i]);
+    };
+    load_word(0, cw);
+    const bool skip_scan = a.flags & 2;
+    // row iterations of this wave inside the chunk (wave-uniform)
+    const int nvi = nr > wave * 64 ? (nr - wave * 64 + NT - 1) / NT : 0;
+    for (int wq = 0; wq < nwd; ++wq) {
+      if (wq + 1 < nwd) load_word(wq + 1, nw);
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {  // (pq_dim % 4 == 0: pq_rt_supported)
+        const int j = wq * 4 + b;
+        __syncthreads();  // LUT_j complete; LUT_{j-1}'s buffer free
+        if (j + 1 < a.pq_dim) {  // (b is static: j's parity is b's)
+          if (!(a.flags & 1)) build(j + 1, bk[(b + 1) & 1], (b + 1) & 1);
+          if (j + 3 < a.pq_dim) load_book(j + 3, bk[(b + 1) & 1]);
+        }
+        const float* lut = s_lut + (j & 1) * (kPqCodes * LS);
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+          if (i < nvi && !skip_scan) {
+            const int code = (cw[i] >> (8 * b)) & 0xFF;
+            const float4* p = reinterpret_cast<const float4*>(lut + code * LS);
+            const float4 v0 = p[0], v1 = p[1], v2 = p[2], v3 = p[3];
+            acc[i][0] += v0.x; acc[i][1] += v0.y; acc[i][2] += v0.z; acc[i][3] += v0.w;
+            acc[i][4] += v1.x; acc[i][5] += v1.y; acc[i][6] += v1.z; acc[i][7] += v1.w;
+            acc[i][8] += v2.x; acc[i][9] += v2.y; acc[i][10] += v2.z; acc[i][11] += v2.w;
+            acc[i][12] += v3.x; acc[i][13] += v3.y; acc[i][14] += v3.z; acc[i][15] += v3.w;
+          }
+          __builtin_amdgcn_sched_barrier(0);  // one row's 16 LUT floats in flight: bounds the VGPRs
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) cw[i] = nw[i];
+    }
+    __syncthreads();  // every wave done with the LUT / residuals (their LDS is reused below)
+
+    if constexpr (DUMP) {
+#pragma unroll
+      for (int t = 0; t < TQ; ++t) {
+        const int64_t slot = s_slot[t];
+        if (slot < 0) continue;
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+          const int row = i * NT + tid;
+          if (row < nr) a.out_d[slot * R + row] = acc[i][t];
+        }
+      }
+      if (tid < TQ && s_slot[tid] >= 0) {
+        a.slot_info[2 * s_slot[tid]] = g0 * kGroupRows + r0;
+        a.slot_info[2 * s_slot[tid] + 1] = nr;
+      }
+    } else {
+      // 1. per query the minimum of my rows
+#pragma unroll
+      for (int t = 0; t < TQ; ++t) {
+        float mn = INFINITY;
+        bool any = false;
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+          if (i * NT + tid < nr) { mn = fminf(mn, acc[i][t]); any = true; }
+        }
+        s_min[t * NT + tid] = any ? rt_ord(mn) : 0xFFFFFFFFu;
+      }
+      __syncthreads();
+      // 2. bound_q = the k-th smallest of the NT minima (wave w: queries 2w, 2w + 1), bit by bit
+      for (int t = wave; t < TQ; t += NT / 64) {
+        uint32_t v[NT / 64];
+#pragma unroll
+        for (int u = 0; u < NT / 64; ++u) v[u] = s_min[t * NT + u * 64 + lane];
+        int kk = a.k;
+        uint32_t P = 0;
+        for (int bit = 31; bit >= 0; --bit) {
+          const uint32_t hi_mask = ~((2u << bit) - 1u);  // bits above `bit` (none for bit 31)
+          int c0 = 0;
+#pragma unroll
+          for (int u = 0; u < NT / 64; ++u)
+            c0 += __popcll(__ballot((v[u] & hi_mask) == (P & hi_mask) && !((v[u] >> bit) & 1u)));
+          if (kk > c0) { kk -= c0; P |= 1u << bit; }
+        }
+        if (lane == 0) s_bound[t] = P;
+      }
+      __syncthreads();
+      // 3. rows at or below the bound -> the query's candidate list
+#pragma unroll
+      for (int t = 0; t < TQ; ++t) {
+        // rt_ord(x) <= bound  <=>  x <= the bound's float (-0 == +0 both ways); all ones: every row
+        const uint32_t bnd = s_bound[t];
+        const float fb = bnd == 0xFFFFFFFFu ? INFINITY
+                                           : __uint_as_float((bnd & 0x80000000u) ? (bnd & 0x7FFFFFFFu) : ~bnd);
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+          const int row = i * NT + tid;
+          if (row < nr && acc[i][t] <= fb) {
+            const int p = atomicAdd(&s_cnt[t], 1);
+            if (p < CQ) { s_ck[t * CQ + p] = acc[i][t]; s_cr[t * CQ + p] = row; }
+          }
+        }
+      }
+      __syncthreads();
+      // 4. per query (wave w: 2w, 2w + 1) k rounds of the 64-lane (key, row) minimum
+      for (int t = wave; t < TQ; t += NT / 64) {
+        const int64_t slot = s_slot[t];
+        const int n = s_cnt[t];
+        if (slot < 0 || n > CQ) continue;
+        constexpr int PER = CQ / 64;
+        float ck[PER];
+        int cr[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+          const int e = u * 64 + lane;
+          ck[u] = e < n ? s_ck[t * CQ + e] : INFINITY;
+          cr[u] = e < n ? s_cr[t * CQ + e] : INT_MAX;
+        }
+        for (int rk = 0; rk < a.k; ++rk) {
+          float bk = ck[0];
+          int br = cr[0];
+#pragma unroll
+          for (int u = 1; u < PER; ++u)
+            if (rt_less(ck[u], cr[u], bk, br)) { bk = ck[u]; br = cr[u]; }
+#pragma unroll
+          for (int off = 32; off >= 1; off >>= 1) {
+            const float ok = __shfl_xor(bk, off);
+            const int orr = __shfl_xor(br, off);
+            if (rt_less(ok, orr, bk, br)) { bk = ok; br = orr; }
+          }
+          const bool valid = br != INT_MAX;
+          if (lane == 0) {
+            a.out_d[slot * a.k + rk] = valid ? (a.ip ? -bk : bk) : (a.ip ? -INFINITY : INFINITY);
+            a.out_i[slot * a.k + rk] = valid ? a.row_ids[g0 * kGroupRows + r0 + br] : (int64_t)-1;
+          }
+#pragma unroll
+          for (int u = 0; u < PER; ++u)
+            if (ck[u] == bk && cr[u] == br) { ck[u] = INFINITY; cr[u] = INT_MAX; }
+        }
+      }
+      // 5. (rare) slots whose candidate list overflowed: block-wide rounds over the registers
+      for (int t = 0; t < TQ; ++t) {
+        if (s_slot[t] < 0 || s_cnt[t] <= CQ) continue;  // block-uniform
+        const int64_t slot = s_slot[t];
+        float xs[RPT];  // query t's sums of my rows (selected statically: no dynamic register indexing)
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+          xs[i] = acc[i][0];
+#pragma unroll
+          for (int u = 1; u < TQ; ++u)
+            if (u == t) xs[i] = acc[i][u];
+        }
+        float lk = -INFINITY;
+        int lr = -1;
+        for (int rk = 0; rk < a.k; ++rk) {
+          float bk = INFINITY;
+          int br = INT_MAX;
+#pragma unroll
+          for (int i = 0; i < RPT; ++i) {
+            const int row = i * NT + tid;
+            const float x = xs[i];
+            if (row < nr && rt_less(lk, lr, x, row) && rt_less(x, row, bk, br)) { bk = x; br = row; }
+          }
+#pragma unroll
+          for (int off = 32; off >= 1; off >>= 1) {
+            const float ok = __shfl_xor(bk, off);
+            const int orr = __shfl_xor(br, off);
+            if (rt_less(ok, orr, bk, br)) { bk = ok; br = orr; }
+          }
+          __syncthreads();
+          if (lane == 0) { s_wk[wave] = bk; s_wr[wave] = br; }
+          __syncthreads();
+#pragma unroll
+          for (int u = 0; u < NT / 64; ++u)
+            if (rt_less(s_wk[u], s_wr[u], bk, br)) { bk = s_wk[u]; br = s_wr[u]; }
+          const bool valid = br != INT_MAX;
+          if (tid == 0) {
+            a.out_d[slot * a.k + rk] = valid ? (a.ip ? -bk : bk) : (a.ip ? -INFINITY : INFINITY);
+            a.out_i[slot * a.k + rk] = valid ? a.row_ids[g0 * kGroupRows + r0 + br] : (int64_t)-1;
+          }
+          lk = bk;
+          lr = br;
+        }
+      }
+    }
+    __syncthreads();  // s_q / s_slot / s_cnt of the next item
+  }
+}
+
 inline dim3 gridc(int64_t n, int b) {
   const int64_t g = ceil_div(n > 0 ? n : 1, b);
   return dim3((unsigned)(g < (1 << 20) ? g : (1 << 20)));
@@ -795,6 +1141,51 @@ hipError_t launch_pq_scan_tiled(const PqTileArgs& a, int kcap, int grid, hipStre
     case 16: return launch_pq_tiled_k<16>(a, grid, lds, s);
     case 32: return launch_pq_tiled_k<32>(a, grid, lds, s);
     default: return hipErrorInvalidValue;
+  }
+}
+
+static int pq_rt_cq(int k) { return k > 64 ? 0 : (k <= 16 ? 128 : 512); }
+
+size_t pq_rt_lds_bytes(int rot_dim_pad, int k) {
+  const size_t loop = (size_t)kRtQ * rot_dim_pad * 4 + (size_t)2 * kPqCodes * 20 * 4;
+  const size_t sel = (size_t)kRtQ * kRtThreads * 4 + (size_t)kRtQ * pq_rt_cq(k) * 8;
+  return 512 + (loop > sel ? loop : sel);
+}
+
+bool pq_rt_supported(int rot_dim_pad, int pq_dim, int pq_len, int k) {
+  return (pq_len & 3) == 0 && pq_len >= 4 && pq_len <= 16 && rot_dim_pad % 4 == 0 && k >= 1 &&
+         (pq_dim & 3) == 0 &&
+         k <= kMaxSelectK && pq_rt_lds_bytes(rot_dim_pad, k) <= 160 * 1024;
+}
+
+template <int PL4, int CQ>
+static hipError_t launch_pq_rt_k(const PqTileArgs& a, int grid, size_t lds, hipStream_t s) {
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pq_scan_rt<PL4, CQ>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL((k_pq_scan_rt<PL4, CQ>), dim3((unsigned)grid), dim3(kRtThreads), lds, s, a);
+  return hipGetLastError();
+}
+
+template <int PL4>
+static hipError_t launch_pq_rt_pl(const PqTileArgs& a, int grid, size_t lds, hipStream_t s) {
+  switch (pq_rt_cq(a.k)) {
+    case 0: return launch_pq_rt_k<PL4, 0>(a, grid, lds, s);
+    case 128: return launch_pq_rt_k<PL4, 128>(a, grid, lds, s);
+    default: return launch_pq_rt_k<PL4, 512>(a, grid, lds, s);
+  }
+}
+
+hipError_t launch_pq_scan_rt(const PqTileArgs& a, int grid, hipStream_t s) {
+  if (!pq_rt_supported(a.rot_dim_pad, a.pq_dim, a.pq_len, a.k)) return hipErrorInvalidValue;
+  if (pq_rt_cq(a.k) == 0 && a.slot_info == nullptr) return hipErrorInvalidValue;
+  if (a.ip && (a.probes == nullptr || a.probes_d == nullptr)) return hipErrorInvalidValue;
+  const size_t lds = pq_rt_lds_bytes(a.rot_dim_pad, a.k);
+  switch (a.pq_len >> 2) {
+    case 1: return launch_pq_rt_pl<1>(a, grid, lds, s);
+    case 2: return launch_pq_rt_pl<2>(a, grid, lds, s);
+    case 3: return launch_pq_rt_pl<3>(a, grid, lds, s);
+    default: return launch_pq_rt_pl<4>(a, grid, lds, s);
   }
 }
 

@@ -171,9 +171,10 @@ def test_prefilter_default_switch(flat_data, mivs_lib, monkeypatch):
 
 
 @pytest.mark.parametrize("k", [10, 40])
-@pytest.mark.parametrize("env", [{"MIVS_PQ_ORDER": "0"}, {"MIVS_PQ_SPLIT": "0"}, {"MIVS_PQ_TILED": "1"}])
+@pytest.mark.parametrize("env", [{"MIVS_PQ_RT": "0"}, {"MIVS_PQ_RT": "0", "MIVS_PQ_ORDER": "0"},
+                                 {"MIVS_PQ_RT": "0", "MIVS_PQ_SPLIT": "0"}, {"MIVS_PQ_RT": "0", "MIVS_PQ_TILED": "1"}])
 def test_ivf_pq_switch_same_bits(mivs_lib, monkeypatch, k, env):
-    """IVF-PQ: slot order, K9 vs K9s, K9b (tiled; k <= 32 there) give the default's bits"""
+    """IVF-PQ: K9r (default) vs K9s, its slot order, K9 vs K9s, K9b (tiled; k <= 32 there): the same bits"""
     from mivs.neighbors import ivf_pq
 
     if env.get("MIVS_PQ_TILED") == "1" and k > 32:
@@ -183,9 +184,9 @@ def test_ivf_pq_switch_same_bits(mivs_lib, monkeypatch, k, env):
     idx = ivf_pq.build(ivf_pq.IndexParams(n_lists=32, pq_dim=32, kmeans_n_iters=3), torch.from_numpy(x).cuda())
     sp = ivf_pq.SearchParams(n_probes=6)
     qt = torch.from_numpy(q).cuda()
-    if k > 16:
-        monkeypatch.setenv("MIVS_PQ_DUMP_K", "64")  # the register lists, where the switches apply
     d0, i0 = ivf_pq.search(sp, idx, qt, k)
+    if k > 16:
+        monkeypatch.setenv("MIVS_PQ_DUMP_K", "64")  # K9s: the register lists, where the switches apply
     for kk, v in env.items():
         monkeypatch.setenv(kk, v)
     d1, i1 = ivf_pq.search(sp, idx, qt, k)

@@ -414,7 +414,8 @@ def test_ivf_pq_build_and_search_bitexact(mivs_lib, n, d, n_lists, pq_dim, iters
 @pytest.mark.parametrize("case", [c for c in PQ_CASES if 16 < c[-1] <= 64])
 def test_ivf_pq_register_lists_bitexact(mivs_lib, monkeypatch, case):
     """k in (16, 64] through the 32/64-entry register lists of K9s (MIVS_PQ_DUMP_K=64) instead of the
-    default DUMP + K8 path: the same bits."""
+    default path (K9r; K9s DUMP + K8 without it): the same bits."""
+    monkeypatch.setenv("MIVS_PQ_RT", "0")
     monkeypatch.setenv("MIVS_PQ_DUMP_K", "64")
     _pq_case(*case)
 
@@ -436,6 +437,26 @@ def _pq_case(n, d, n_lists, pq_dim, iters, nq, n_probes, k):
     dist, ids = ivf_pq.search(ivf_pq.SearchParams(n_probes=n_probes), idx, _gpu(q), k, probes_out=probes)
     od, oi, op = O.ivfpq_search(oc, ocb, osz, oids, ocodes, q, n_probes, k)
     np.testing.assert_array_equal(probes.cpu().numpy(), op)
+    np.testing.assert_array_equal(ids.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(dist.cpu().numpy()), _bits(od))
+
+
+@pytest.mark.parametrize("k", [10, 40, 100])
+def test_ivf_pq_tied_keys_bitexact(mivs_lib, k):
+    """every row 250 times: the best key of a list chunk is tied 250 times, more than K9r's 128-entry
+    candidate list at k <= 16 (its block-wide fallback rounds run), within the 512 list at k = 40, and
+    the DUMP + K8 tie order at k = 100 -- ids (ties by id) and bits equal to the oracle"""
+    from mivs.neighbors import ivf_pq
+
+    base = _data(40, 64, seed=91, normalize=True)
+    x = np.concatenate([base] * 250)
+    q = np.concatenate([base[:9], _data(9, 64, seed=92, normalize=True)])
+    params = ivf_pq.IndexParams(n_lists=4, pq_dim=16, kmeans_n_iters=3, max_train_points_per_pq_code=32)
+    idx = ivf_pq.build(params, _gpu(x), ids_offset=0)
+    oc, ocb, osz, oids, ocodes = O.ivfpq_build(x, 4, 16, iters=3, max_per_code=32, id_offset=0)
+    np.testing.assert_array_equal(idx.codes().cpu().numpy(), ocodes)
+    dist, ids = ivf_pq.search(ivf_pq.SearchParams(n_probes=2), idx, _gpu(q), k)
+    od, oi, _ = O.ivfpq_search(oc, ocb, osz, oids, ocodes, q, 2, k)
     np.testing.assert_array_equal(ids.cpu().numpy(), oi)
     np.testing.assert_array_equal(_bits(dist.cpu().numpy()), _bits(od))
 
