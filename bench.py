@@ -66,6 +66,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--flat-rows", type=int, default=1_000_000,
                     help="BASELINE configs[1] side line: brute force over this many rows (0: skip)")
+    ap.add_argument("--pq-rows", type=int, default=12_500_000,
+                    help="BASELINE configs[4] side line: IVF-PQ over this many fp16 rows, the per-GPU share of "
+                         "100M x 768 on 8 GPUs (0: skip)")
     ap.add_argument("--json-out", default="")
     return ap.parse_args()
 
@@ -229,6 +232,85 @@ def flat_side_line(a, q, k, rl):
         del xh
     bf.close()
     del xf
+    torch.cuda.empty_cache()
+    return line
+
+
+PEAK_LDS_B128_LOOKUPS = 256 * 2.4e9 * 64  # ds_read_b128: 256 B/clk/CU = 64 fp32 LUT entries / clk / CU
+
+
+def pq_side_line(a, rl):
+    """BASELINE configs[4], the per-GPU share: IVF-PQ over 12.5M x 768 fp16 rows, n_lists 4096, pq_dim 96,
+    pq_bits 8 (improved_multi_gpu_rag.py:131-137), the same query batch shape; plain PQ at n_probes 16 and
+    PQ + exact re-ranking of 10 k candidates (cuvs.neighbors.refine) -- the configuration that reaches
+    recall@10 >= 0.95 on this mixture. The scan's roofline: one fp32 LUT entry read from LDS per
+    (probed row, subspace, query), against the ds_read_b128 rate."""
+    from mivs import _native, ops
+    from mivs.neighbors import brute_force, ivf_pq, refine
+
+    dev = torch.cuda.current_device()
+    n, d, Q, k, pq_dim, n_lists, n_probes, ratio = a.pq_rows, a.dim, a.queries, a.k, 96, 4096, 16, 10
+    x = ops.synth_mixture(n, d, SEED + 11, n_centers=a.centers, sigma=a.sigma, device=dev).half()
+    torch.cuda.empty_cache()
+    q = ops.synth_mixture(Q, d, SEED + 11, n_centers=a.centers, sigma=a.sigma, row_begin=QUERY_ROW_BASE, device=dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    idx = ivf_pq.build(ivf_pq.IndexParams(n_lists=n_lists, pq_dim=pq_dim, pq_bits=8), x)
+    torch.cuda.synchronize()
+    t_build = time.perf_counter() - t0
+    ng = min(1000, Q)
+    xf = x.float()
+    bf = brute_force.build(xf)
+    _, gt = brute_force.search(bf, q[:ng], max(17, k))
+    gt = gt[:, :k].cpu().numpy()
+    bf.close()
+    del bf, xf
+    torch.cuda.empty_cache()
+    sp = ivf_pq.SearchParams(n_probes=n_probes)
+    reps = 5
+    ivf_pq.search(sp, idx, q, k)
+    _native.set_profiling(True)
+    idx.profile_collect()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        _, ids = ivf_pq.search(sp, idx, q, k)
+    torch.cuda.synchronize()
+    t_plain = (time.perf_counter() - t0) / reps
+    pr = idx.profile_collect()
+    _native.set_profiling(False)
+    rec_plain = recall_at_k(ids[:ng].cpu().numpy(), gt)
+    kc = ratio * k
+    _, cand = ivf_pq.search(sp, idx, q, kc)
+    refine(x, q, cand, k)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        _, cand = ivf_pq.search(sp, idx, q, kc)
+        _, rids = refine(x, q, cand, k)
+    torch.cuda.synchronize()
+    t_ref = (time.perf_counter() - t0) / reps
+    rec_ref = recall_at_k(rids[:ng].cpu().numpy(), gt)
+    probes = torch.empty((Q, n_probes), dtype=torch.int32, device=dev)
+    ivf_pq.search(sp, idx, q, k, probes_out=probes)
+    rows = int(idx.list_sizes.cpu()[probes.long().cpu()].sum())
+    scan_ms = pr["scan_ms"] / max(pr["n_calls"], 1)
+    lookups = float(rows) * pq_dim
+    ach = lookups / (scan_ms * 1e-3)
+    line = {"rows": n, "dim": d, "dtype_in": "fp16", "n_lists": n_lists, "pq_dim": pq_dim, "pq_bits": 8,
+            "queries": Q, "k": k, "n_probes": n_probes, "build_s": round(t_build, 3),
+            "build_vectors_per_s": round(n / t_build, 1),
+            "qps_pq": round(Q / t_plain, 1), "recall_at_10_pq": round(rec_plain, 4),
+            "qps_pq_refined": round(Q / t_ref, 1), "recall_at_10_pq_refined": round(rec_ref, 4),
+            "refine": f"{kc} PQ candidates re-ranked exactly against the fp16 rows (mivs.neighbors.refine, K14)",
+            "scan_kernel": "mivs::k_pq_scan_rt (K9r: 16-query tiles per list, code-major LUT rows in LDS)",
+            "roofline": {"bound": "lds", "achieved": round(ach / 1e9, 1), "peak": round(PEAK_LDS_B128_LOOKUPS / 1e9, 1),
+                         "unit": "G LUT entries/s", "frac": round(ach / PEAK_LDS_B128_LOOKUPS, 4),
+                         "launch_ms": round(scan_ms, 4), "lut_entries_per_launch": lookups, "rows_scanned": rows}}
+    rl(f"[pq] {n} x {d} fp16, build {n / t_build / 1e6:.2f} M vec/s; n_probes {n_probes}: {Q / t_plain:,.0f} QPS "
+       f"recall {rec_plain:.3f}; refined x{ratio}: {Q / t_ref:,.0f} QPS recall {rec_ref:.3f}")
+    idx.close()
+    del x, q, idx, cand, ids, rids
     torch.cuda.empty_cache()
     return line
 
@@ -424,6 +506,16 @@ def main():
         except Exception as e:  # the IVF line stands without it
             rl(f"[flat] side line failed: {e!r}")
 
+    pq = None
+    if rank == 0 and world == 1 and a.pq_rows > 0:
+        idx.close()
+        del x
+        torch.cuda.empty_cache()
+        try:
+            pq = pq_side_line(a, rl)
+        except Exception as e:  # the IVF-Flat line stands without it
+            rl(f"[pq] side line failed: {e!r}")
+
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -455,6 +547,7 @@ def main():
         "search_stats": stats,
         "n_probes_sweep": sweep,
         "flat_bruteforce_1m": flat,
+        "ivf_pq_12m5": pq,
     }
     if rank == 0:
         line = json.dumps(out)
@@ -462,7 +555,8 @@ def main():
         if a.json_out:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
-    idx.close()
+    if pq is None:
+        idx.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -958,18 +958,22 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   a.wave_buf = ws.rs_wave_buf.as<int4>();
   a.wave_cnt = ws.rs_wave_cnt.as<int>();
   a.flags = getenv("MIVS_RS_FLAGS") ? atoi(getenv("MIVS_RS_FLAGS")) : 0;
+  {
+    const char* e = getenv("MIVS_RS_PRIO");
+    a.prio = e ? atoi(e) : 0;
+  }
   if (a.flags & 2) a.flags |= 1;  // stale LDS tiles: never run an epilogue on them
   Buf pbuf;
   if (a.flags & 24) {  // diagnostic: per-block clocks (8) / per-phase wave-cycles (16) to stderr
-    pbuf.reserve(sizeof(unsigned long long) * (3 * grid + 4));
-    HIPCHK(hipMemsetAsync(pbuf.p, 0, sizeof(unsigned long long) * (3 * grid + 4), s));
+    pbuf.reserve(sizeof(unsigned long long) * (3 * grid + 8));
+    HIPCHK(hipMemsetAsync(pbuf.p, 0, sizeof(unsigned long long) * (3 * grid + 8), s));
     a.prof = pbuf.as<unsigned long long>();
   }
   if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
   HIPCHK(launch_rs_scan(a, dp, grid, s));
   if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
   if (a.flags & 24) {
-    std::vector<unsigned long long> h(3 * (size_t)grid + 4);
+    std::vector<unsigned long long> h(3 * (size_t)grid + 8);
     HIPCHK(hipMemcpyAsync(h.data(), pbuf.p, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     unsigned long long t0 = ~0ull, t1 = 0, tiles_max = 0, tiles_sum = 0;
@@ -985,12 +989,16 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
     }
     fprintf(stderr, "[k13 blocks] span %.1f us | busy mean %.1f max %.1f us | tiles mean %.1f max %llu\n",
             (t1 - t0) / 100.0, busy_sum / grid / 100.0, busy_max / 100.0, (double)tiles_sum / grid, tiles_max);
-    const double wc = (double)(h[3 * grid] + h[3 * grid + 1] + h[3 * grid + 2] + h[3 * grid + 3]);
+    const double wc = (double)(h[3 * grid] + h[3 * grid + 1] + h[3 * grid + 2] + h[3 * grid + 3] + h[3 * grid + 4]);
     if (wc > 0)
       fprintf(stderr, "[k13 phases] wave-cycles %.4g | ready-wait %.3f mfma-loop %.3f own-dma-wait %.3f epilogue %.3f | "
               "cycles/tile/wave %.0f\n", wc, h[3 * grid] / wc, h[3 * grid + 1] / wc, h[3 * grid + 3] / wc,
               h[3 * grid + 2] / wc,
               tiles_sum ? wc / ((double)tiles_sum * kRsWaves) : 0.0);
+    if (wc > 0)
+      fprintf(stderr, "[k13 phases] mfma-result-wait %.3f (in epilogue: hit path %.3f) | wave-tiles taking the hit path "
+              "%.4f of %llu\n", h[3 * grid + 4] / wc, h[3 * grid + 5] / wc,
+              h[3 * grid + 7] ? (double)h[3 * grid + 6] / (double)h[3 * grid + 7] : 0.0, h[3 * grid + 7]);
   }
   // the streams into per-query CSR runs (every stream entry fits: at most n_waves * wave_cap of them)
   const size_t max_cand = (size_t)n_waves * a.wave_cap;

@@ -178,6 +178,7 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   int tt = 0;               // tiles this workgroup has started
   bool spun_out = false;    // a ready-wait gave up (never expected): the results are then not trusted
   uint64_t pw_wait = 0, pw_loop = 0, pw_epi = 0, pw_dma = 0;  // flags & 16: this wave's cycles per tile phase
+  uint64_t pw_drain = 0, pw_hit = 0, n_hit_tiles = 0;  // flags & 16: MFMA-result wait, hit path, tiles taking it
   const int widx = blockIdx.x * kRsWaves + wave;
   int4* const wstream = a.wave_buf + (int64_t)widx * a.wave_cap;
   int wcnt = 0;  // entries of this wave's candidate stream
@@ -195,6 +196,10 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
       atomicAdd(p + 1, (unsigned long long)pw_loop);
       atomicAdd(p + 2, (unsigned long long)pw_epi);
       atomicAdd(p + 3, (unsigned long long)pw_dma);
+      atomicAdd(p + 4, (unsigned long long)pw_drain);
+      atomicAdd(p + 5, (unsigned long long)pw_hit);
+      atomicAdd(p + 6, (unsigned long long)n_hit_tiles);
+      atomicAdd(p + 7, (unsigned long long)n_tiles_done);
     }
   };
   if (w >= hi) {
@@ -220,6 +225,12 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
     dma_b32(uniform_desc(a.row_norms + (int64_t)grp * kGroupRows, kGroupRows * 4), s_norm + (ip * kRsWaves + wave) * 64,
             j * 4);
   };
+  // Waves w and w + 4 share a SIMD's MFMA pipe. They start every tile's k-loop together (the ready
+  // counter), so at equal priority they also reach their epilogues together and the pipe idles through
+  // both. With waves 0..3 raised, wave w's MFMAs go first: it finishes its k-loop about half a tile
+  // early and runs its epilogue while wave w + 4's MFMAs take the pipe alone, and wave w + 4's epilogue
+  // then runs under wave w's next k-loop.
+  if (a.prio && wave < 4) __builtin_amdgcn_s_setprio(1);
   if (tid == 0) *s_ready = 0;
   __syncthreads();  // (the only workgroup barrier: the counter is zero before any wave signals)
   {
@@ -319,6 +330,12 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
       rs_wait_vm(LAST && has_next ? NK - 3 - NK / kRsWaves : 0);
       rs_signal(s_ready);
       const uint64_t ph2b = (a.flags & 16) ? __builtin_amdgcn_s_memtime() : 0;
+      uint64_t ph2c = ph2b, ph2d = 0;
+      if (a.flags & 16) {  // (timing only) the wait for the k-loop's last MFMA result
+        float t = acc[15];
+        asm volatile("v_mov_b32 %0, %0" : "+v"(t));
+        ph2c = __builtin_amdgcn_s_memtime();
+      }
       // epilogue: lane (j, h) holds the 16 dots of query j with rows (r & 3) + 8 (r >> 2) + 4 h
       if (gv && !(a.flags & 1)) {
         // header of query j: {qs, uf, qn, q}
@@ -334,6 +351,10 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
 #pragma unroll
         for (int r = 1; r < 16; ++r) amax = fmaxf(amax, acc[r]);
         if (__ballot(fmaf(amax, mm, METRIC == kL2 ? xnmin : 0.0f) < uf) != 0) {
+          if (a.flags & 16) {
+            ++n_hit_tiles;
+            ph2d = __builtin_amdgcn_s_memtime();
+          }
           unsigned hits = 0;
 #pragma unroll
           for (int q4 = 0; q4 < 4; ++q4) {
@@ -373,7 +394,9 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
         pw_wait += ph1 - ph0;
         pw_loop += ph2 - ph1;
         pw_dma += ph2b - ph2;
-        pw_epi += ph3 - ph2b;
+        pw_drain += ph2c - ph2b;
+        pw_epi += ph3 - ph2c;
+        if (ph2d) pw_hit += ph3 - ph2d;
       }
       par ^= 1;
     };

@@ -162,3 +162,24 @@ def test_brute_force_prefilter_bitexact(mivs_lib, metric, k):
     np.testing.assert_array_equal(i1.cpu().numpy(), oi)
     np.testing.assert_array_equal(d1.cpu().numpy().view(np.int32), od.view(np.int32))
     assert st["overflow_queries"] <= 300
+
+
+@pytest.mark.parametrize("metric", ["sqeuclidean", "inner_product"])
+def test_brute_force_prefilter_overflow_falls_back_exactly(mivs_lib, metric):
+    """Brute force through the pre-filter with every row duplicated 80 times: the refine window of a
+    query whose neighbour is a base row holds > 64 candidates, so those queries take the exact
+    single-list fallback (rows gathered, norms recomputed, scattered back) -- and the answer is still
+    the oracle's (the brute-force overflow branch)."""
+    from mivs.neighbors import brute_force
+
+    base = _data(400, 64, seed=21, normalize=True)
+    x = np.concatenate([base] * 80)
+    q = np.concatenate([base[:24], _data(24, 64, seed=22, normalize=True)])
+    idx = brute_force.build(torch.from_numpy(x).cuda(), metric=metric, ids_offset=5)
+    d1, i1 = brute_force.search(idx, torch.from_numpy(q).cuda(), 10)
+    st = idx.last_search_stats()
+    assert st["prefilter"] == 1 and st["overflow_queries"] > 0, st
+    od, oi = O.knn(x, q, 10, metric=metric, id_offset=5)
+    np.testing.assert_array_equal(i1.cpu().numpy(), oi)
+    np.testing.assert_array_equal(d1.cpu().numpy().view(np.int32), od.view(np.int32))
+    idx.close()
