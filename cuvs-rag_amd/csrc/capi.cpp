@@ -958,10 +958,6 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   a.wave_buf = ws.rs_wave_buf.as<int4>();
   a.wave_cnt = ws.rs_wave_cnt.as<int>();
   a.flags = getenv("MIVS_RS_FLAGS") ? atoi(getenv("MIVS_RS_FLAGS")) : 0;
-  {
-    const char* e = getenv("MIVS_RS_PRIO");
-    a.prio = e ? atoi(e) : 0;
-  }
   if (a.flags & 2) a.flags |= 1;  // stale LDS tiles: never run an epilogue on them
   Buf pbuf;
   if (a.flags & 24) {  // diagnostic: per-block clocks (8) / per-phase wave-cycles (16) to stderr

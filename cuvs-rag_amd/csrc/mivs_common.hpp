@@ -245,7 +245,6 @@ struct RsScanArgs {
   int flags;                 // timing experiments only (MIVS_RS_FLAGS): 1 skip epilogue, 2 skip staging,
                              // 8 per-block clocks into prof
   unsigned long long* prof;  // flags & 8: [grid][3] {start, end, tiles}
-  int prio;                  // waves 0..3 (one of each SIMD's two waves) issue at raised priority
 };
 
 // K14 exact re-ranking of candidates (refine.hip): cuvs.neighbors.refine

@@ -10,12 +10,12 @@
 //     block as MFMA A operands IN REGISTERS for the whole item (NK k-steps x 16 B per lane:
 //     192 VGPRs at d = 768), so every row is read from HBM exactly once per search;
 //   * the list's queries stream past the rows in 32-query tiles: each tile's fp16 image
-//     ([NK k-steps][64 lanes] x 16 B, one conflict-free ds_read_b128 per MFMA) plus a 16-B header
-//     per query is copied global -> LDS by LDS-DMA (global_load_lds_dwordx4, no VGPRs), double
-//     buffered, one barrier per tile; the queries of a list (~0.5 MB) stay in the XCD's L2 while the
+//     ([NK pieces][64 lanes] x 16 B, one conflict-free ds_read_b128 per two v_mfma_f32_16x16x32_f16)
+//     plus a 16-B header per query is copied global -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds, no
+//     VGPRs), double buffered, an LDS tiles-ready counter per tile; the queries of a list (~0.5 MB) stay in the
 //     XCD's 32 CUs work through the list's blocks (items are dealt from 8 per-XCD queues in list order);
 //   * the next item's rows are loaded into the A registers during the item's last tile, each
-//     k-step's registers right after their last MFMA;
+//     register right after its last MFMA;
 //   * no per-lane top-k: every query carries a bound T_q from a pre-pass (the exact k-th key over
 //     its nearest list) with T_q >= the refine window of the final answer; the
 //     epilogue appends every (approximate key <= T_q, row) to the query's candidate buffer, and K11
@@ -146,24 +146,48 @@ struct BoolC {
   static constexpr bool value = B;
 };
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// K13 computes on v_mfma_f32_16x16x32_f16 (the chip holds a higher clock on this shape than on
+// 32x32x16 at the same cycles per flop: MI355X_MICROARCH.md 'DVFS give-back' item 7; measured 5.44 ->
+// 5.19 ms per launch). Tile piece s = 2 t + qb (1 KiB) holds queries 16 qb .. 16 qb + 15 x dims
+// 32 t .. 32 t + 31 and feeds two MFMAs, one per 16-row block rb of the wave's group (A registers
+// ra[2 t + rb]: lane (c, kq) = (lane & 15, lane >> 4) holds row 16 rb + c, dims 32 t + 8 kq .. + 7);
+// the wave ends a tile with the dots of queries c and 16 + c with rows 16 rb + 4 kq + i in
+// acc4[2 qb + rb][i].
+//
+// Tile protocol: two LDS tile buffers; every wave stages 1/8 of the next tile's pieces during its k-loop
+// and signals once its reads of the tile are done and its pieces landed; a wave starts the next k-loop
+// when all 8 signalled. (A decoupled variant -- three buffers, waves 0..3 staging, waves 4..7 a k-loop
+// behind so that each epilogue would run under the SIMD partner's MFMAs -- was correct but slower,
+// 5.41 vs 5.20 ms: the LDS-DMA issue cost, ~100+ cycles a piece, then sits on four waves.)
 template <int METRIC, int NK>
 __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int BUF = NK * 1024 + 1024;
+  constexpr int NBUF = 2;
   constexpr int NB = 2 * NK;  // 8-dim blocks of a group row
   constexpr int64_t IMG = (int64_t)(NK + 1) * 1024;
-  static_assert(NK / kRsWaves + 1 < NK, "DMA pieces within the k-loop");
-  static_assert((NK + kRsWaves) / kRsWaves < NK, "the image's pieces are issued over k-steps 1..");
+  constexpr int STAGERS = kRsWaves;  // waves that stage tile pieces
+  static_assert((NK + STAGERS) / STAGERS < NK, "the image's pieces are issued over k-steps 1..");
+  // rows of the next item loaded (two per odd k-step) after this wave's last DMA piece (k-step
+  // NK / STAGERS + 1), less two: the order of a k-step's row load and DMA piece is the compiler's
+  constexpr int ROWS_AFTER = [] {
+    int c = 0;
+    for (int s = NK / STAGERS + 2; s < NK; ++s) c += (s & 1) ? 2 : 0;
+    return c - 2 > 0 ? c - 2 : 0;
+  }();
   // [2 item parities][8 waves][64] row norms of the wave's group (lanes 32..63 repeat 0..31), filled by
   // LDS-DMA so the next item's are in flight with its rows and nothing waits on them in registers
-  float* s_norm = reinterpret_cast<float*>(smem + 2 * BUF);
+  float* s_norm = reinterpret_cast<float*>(smem + NBUF * BUF);
   // tiles-ready counter: every wave adds 1 per tile once it has finished reading the previous tile and its
-  // DMA pieces of this one have landed (see the tile loop); no workgroup barrier per tile
-  int* s_ready = reinterpret_cast<int*>(smem + 2 * BUF + 2 * kRsWaves * 64 * sizeof(float));
+  // DMA pieces of this one have landed (a sum over waves is a safe test: all of them wait on it, so none is
+  // a tile ahead of another when one starts a tile); no workgroup barrier per tile
+  int* s_ready = reinterpret_cast<int*>(smem + NBUF * BUF + 2 * kRsWaves * 64 * sizeof(float));
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int j = lane & 31;
-  const int h = lane >> 5;
+  const int kq = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // static, XCD-aware schedule: queue x (= blockIdx % 8, the XCD under round-robin placement; speed only)
   // holds the x-th eighth of the list-ordered items and its P workgroups take every P-th item, so the
@@ -175,8 +199,8 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   int w = (int)((int64_t)total * x / 8) + (int)(blockIdx.x >> 3);
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
   int n_tiles_done = 0;
-  int tt = 0;               // tiles this workgroup has started
-  bool spun_out = false;    // a ready-wait gave up (never expected): the results are then not trusted
+  int tt = 0;               // tiles this wave has started
+  bool spun_out = false;    // a wait gave up (never expected): the results are then not trusted
   uint64_t pw_wait = 0, pw_loop = 0, pw_epi = 0, pw_dma = 0;  // flags & 16: this wave's cycles per tile phase
   uint64_t pw_drain = 0, pw_hit = 0, n_hit_tiles = 0;  // flags & 16: MFMA-result wait, hit path, tiles taking it
   const int widx = blockIdx.x * kRsWaves + wave;
@@ -184,13 +208,13 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   int wcnt = 0;  // entries of this wave's candidate stream
   auto block_prof = [&]() {
     // (a wave that gave up waiting reports a lost stream: every query then takes the fallback search)
-    if (lane == 0) a.wave_cnt[widx] = spun_out ? a.wave_cap + 1 : wcnt;  // (timing only) flags & 8: per block {start, end, tiles} in 100 MHz ticks
-    if ((a.flags & 8) && a.prof && tid == 0) {
+    if (lane == 0) a.wave_cnt[widx] = spun_out ? a.wave_cap + 1 : wcnt;
+    if ((a.flags & 8) && a.prof && tid == 0) {  // (timing only) flags & 8: per block {start, end, tiles}
       a.prof[3 * blockIdx.x] = t_start;
       a.prof[3 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
       a.prof[3 * blockIdx.x + 2] = (unsigned long long)n_tiles_done;
     }
-    if ((a.flags & 16) && a.prof && lane == 0) {  // flags & 16: [3 grid + 0..2] wave-cycles summed
+    if ((a.flags & 16) && a.prof && lane == 0) {  // flags & 16: wave-cycles per phase summed
       unsigned long long* p = a.prof + 3 * gridDim.x;
       atomicAdd(p + 0, (unsigned long long)pw_wait);
       atomicAdd(p + 1, (unsigned long long)pw_loop);
@@ -209,34 +233,26 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   RsItem it = rs_item(a, w);
   int g = it.g0 + wave;
   bool gv = g < it.gend;
-  // group rows: a wave-uniform base (SGPRs) + this lane's 32-bit byte offset, so every k-step's load is
-  // the saddr form with no per-lane 64-bit address to keep (the next item's 48 addresses would not fit)
   // Buffer loads: a per-group descriptor in SGPRs (uniform base, NB * 512 bytes), this lane's 32-bit
-  // offset in one VGPR and the k-step in soffset -- no per-lane 64-bit address per k-step to keep (the
-  // next item's 48 would not fit beside the resident rows)
-  const int lane_off = h * 512 + j * 16;
+  // offset in one VGPR and the register's offset in soffset -- no per-lane 64-bit address per register to
+  // keep (the next item's 48 would not fit beside the resident rows)
+  const int lane_off = kq * 512 + (lane & 15) * 16;
   auto group_rsrc = [&](int grp) {
     return uniform_rsrc(reinterpret_cast<const char*>(a.groups_h) + (int64_t)grp * (NB * 512), NB * 512);
   };
-  auto ld_rows = [&](__amdgpu_buffer_rsrc_t r, int s) {
-    return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(r, lane_off, s * 1024, 0));
+  auto ld_rows = [&](__amdgpu_buffer_rsrc_t r, int i) {  // register i = 2 t + rb
+    return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(r, lane_off, (i >> 1) * 2048 + (i & 1) * 256, 0));
   };
   auto load_norms = [&](int grp, int ip) {
     dma_b32(uniform_desc(a.row_norms + (int64_t)grp * kGroupRows, kGroupRows * 4), s_norm + (ip * kRsWaves + wave) * 64,
             j * 4);
   };
-  // Waves w and w + 4 share a SIMD's MFMA pipe. They start every tile's k-loop together (the ready
-  // counter), so at equal priority they also reach their epilogues together and the pipe idles through
-  // both. With waves 0..3 raised, wave w's MFMAs go first: it finishes its k-loop about half a tile
-  // early and runs its epilogue while wave w + 4's MFMAs take the pipe alone, and wave w + 4's epilogue
-  // then runs under wave w's next k-loop.
-  if (a.prio && wave < 4) __builtin_amdgcn_s_setprio(1);
   if (tid == 0) *s_ready = 0;
   __syncthreads();  // (the only workgroup barrier: the counter is zero before any wave signals)
-  {
+  {  // tile 0's pieces
     const v4i d0 = uniform_desc(a.tiles + it.slot * IMG, (int)IMG);
 #pragma unroll
-    for (int p0 = 0; p0 <= NK; p0 += kRsWaves)
+    for (int p0 = 0; p0 <= NK; p0 += STAGERS)
       if (p0 + wave <= NK) dma_b128(d0, smem + (p0 + wave) * 1024, lane * 16, (p0 + wave) * 1024);
   }
   load_norms(gv ? g : it.g0, 0);
@@ -247,9 +263,9 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
     for (int s = 0; s < NK; ++s) ra[s] = ld_rows(r0, s);
   }
   float xnmin = 0.0f;  // the smallest row norm of the wave's group in the current item
-  int par = 0;  // LDS buffer of the current tile
-  int ipar = 0;           // item parity: the s_norm half of this item
-  const f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int cur = 0;         // LDS buffer of the current tile (tt % NBUF)
+  int ipar = 0;        // item parity: the s_norm half of this item
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
 
   for (;;) {
     const int ntiles = it.ntiles;
@@ -259,8 +275,70 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
     if (has_next) nx = rs_item(a, wn);  // (retired by the first tile's wait, long before its use)
     const int gnx = nx.g0 + wave;
     const bool gvn = has_next && gnx < nx.gend;
-    // One tile. The item's rows have landed (the wait at the item start); this wave's DMA of tile t lands
-    // by the counted wait below, which leaves the candidate stores issued after it in flight. The last
+    // the filter over one tile's dots; h0 / h1 = the headers {qs, uf, qn, q} of queries c and 16 + c,
+    // read before the wave signalled the tile (after that the buffer may be restaged)
+    auto epilogue = [&](const f32x4 (&acc4)[4], const float4& h0, const float4& h1, uint64_t& ph2d)
+                        __attribute__((always_inline)) {
+      const float mm0 = METRIC == kL2 ? -2.0f * h0.x : -h0.x;
+      const float mm1 = METRIC == kL2 ? -2.0f * h1.x : -h1.x;
+      // common case first, without the norms: mm < 0, so every filter value fma(acc, mm, xn) is
+      // >= fma(max acc, mm, min xn) (exact ordering, one monotone rounding); only when that bound reaches
+      // uf in some lane is the hit mask formed from the row norms
+      float am0 = fmaxf(acc4[0][0], acc4[1][0]), am1 = fmaxf(acc4[2][0], acc4[3][0]);
+#pragma unroll
+      for (int i = 1; i < 4; ++i) {
+        am0 = fmaxf(am0, fmaxf(acc4[0][i], acc4[1][i]));
+        am1 = fmaxf(am1, fmaxf(acc4[2][i], acc4[3][i]));
+      }
+      const float xb = METRIC == kL2 ? xnmin : 0.0f;
+      if (__ballot(fmaf(am0, mm0, xb) < h0.y || fmaf(am1, mm1, xb) < h1.y) == 0) return;
+      if (a.flags & 16) {
+        ++n_hit_tiles;
+        ph2d = __builtin_amdgcn_s_memtime();
+      }
+      const float* wnorm = s_norm + (ipar * kRsWaves + wave) * 64;
+      unsigned hits = 0;  // bit 8 qb + 4 rb + i (norms from LDS four at a time: registers are short)
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        const float4 nv = *reinterpret_cast<const float4*>(wnorm + 16 * rb + 4 * kq);
+        const float xn[4] = {nv.x, nv.y, nv.z, nv.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float xv = METRIC == kL2 ? xn[i] : 0.0f;
+          hits |= (fmaf(acc4[rb][i], mm0, xv) < h0.y ? 1u : 0u) << (4 * rb + i);
+          hits |= (fmaf(acc4[2 + rb][i], mm1, xv) < h1.y ? 1u : 0u) << (8 + 4 * rb + i);
+        }
+      }
+      // (-1: an empty lane of the tile)
+      const int bq0 = __float_as_int(h0.w), bq1 = __float_as_int(h1.w);
+      if (!(bq0 >= 0 && bq0 < a.nq)) hits &= 0xFF00u;
+      if (!(bq1 >= 0 && bq1 < a.nq)) hits &= 0x00FFu;
+      // every filter hit (a superset of the keys <= T_q; the refine's window is below T_q) goes to this
+      // wave's stream -- positions by ballot prefix, no atomics; k_rs_bucket sorts the streams into
+      // per-query runs. One hit per lane per round; the rare survivors are picked out of the
+      // accumulators by selects (bit r = 8 qb + 4 rb + i is element r of acc4)
+      while (__ballot(hits != 0) != 0) {
+        const bool has = hits != 0;
+        const int r = has ? __builtin_ctz(hits) : 0;
+        hits &= hits - 1;
+        float c = acc4[0][0];
+#pragma unroll
+        for (int e = 1; e < 16; ++e) c = r == e ? acc4[e >> 2][e & 3] : c;
+        const int qb = r >> 3, row = 16 * ((r >> 2) & 1) + 4 * kq + (r & 3);
+        const uint64_t m = __ballot(has);
+        const int at = wcnt + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (has && at < a.wave_cap) {
+          const float4 hq = qb ? h1 : h0;
+          wstream[at] = make_int4(__float_as_int(pf_key<METRIC>(c, hq.x, wnorm[row], hq.z)), g * kGroupRows + row,
+                                  __float_as_int(hq.w), 0);
+        }
+        wcnt += __popcll(m);
+      }
+    };
+
+    // One tile. The item's rows have landed (the wait at the item start); this wave's DMA of the next tile
+    // lands by the counted wait below, which leaves the candidate stores issued after it in flight. The last
     // tile (LAST) is a separate copy, the only one that loads the next item's rows: in a loop shared by
     // all tiles the compiler would wait for every vector-memory operation before the first MFMA.
     auto tile = [&](int t, auto last_c) __attribute__((always_inline)) {
@@ -271,124 +349,75 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
       ++tt;
       const uint64_t ph1 = (a.flags & 16) ? __builtin_amdgcn_s_memtime() : 0;
       const bool last = LAST;
-      // the next tile (of this item, or the next item's first) goes into the other buffer: every wave
-      // has finished reading it (tile t - 1) before the barrier above. Its pieces are issued one per
-      // k-step from the second on: issued before the first MFMA, the compiler's wait for the rows there
-      // (vmcnt(0): it cannot order them across the loop) would wait for this DMA too
+      // the next tile (of this item, or the next item's first) goes into the next buffer. Its pieces are
+      // issued one per k-step from the second on: issued before the first MFMA, the compiler's wait for the
+      // rows there (vmcnt(0): it cannot order them across the loop) would wait for this DMA too
       // (a buffer descriptor over the image: no branch per piece; with nothing to stage -- the block's
-      // last tile -- its size is 0 and the loads write zeros to the buffer no tile reads again)
+      // last tile -- its size is 0 and the loads write zeros to a buffer no tile reads again)
       const char* simg = !last ? a.tiles + (it.slot + t + 1) * IMG : a.tiles + nx.slot * IMG;
       const bool stage = (!last || has_next) && !(a.flags & 2);
       const v4i sdesc = uniform_desc(simg, stage ? (int)IMG : 0);
-      char* sbuf = smem + (par ^ 1) * BUF;
+      const int nxt = cur + 1 == NBUF ? 0 : cur + 1;
+      char* sbuf = smem + nxt * BUF;
       const bool reload = LAST && has_next;
       const __amdgpu_buffer_rsrc_t nrs = group_rsrc(gvn ? gnx : nx.g0);
-      f32x16 acc = zero;
-      float4 hd;  // this tile's header for query j
+      f32x4 acc4[4] = {zero4, zero4, zero4, zero4};
       // (a wave without a group in this block runs the MFMAs on stale rows; its epilogue is skipped).
-      // Two copies of the k-loop, with and without the next item's row loads, so no k-step branches.
+      // Copies of the k-loop with / without the next item's row loads and the staging, so no k-step branches.
       auto kloop = [&](auto reload_c) __attribute__((always_inline)) {
         constexpr bool RL = decltype(reload_c)::value;
-        const char* bb = smem + par * BUF + lane * 16;
-        constexpr int PD = kRsBPrefetch;  // B operands PD k-steps ahead (ring of PD + 1)
+        const char* bb = smem + cur * BUF + lane * 16;
+        constexpr int PD = kRsBPrefetch;  // B operands PD pieces ahead (ring of PD + 1)
         h8 b[PD + 1];
 #pragma unroll
         for (int u = 0; u < PD; ++u) b[u] = *reinterpret_cast<const h8*>(bb + (u < NK ? u : 0) * 1024);
 #pragma unroll
         for (int s = 0; s < NK; ++s) {
           if (s + PD < NK) b[(s + PD) % (PD + 1)] = *reinterpret_cast<const h8*>(bb + (s + PD) * 1024);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s], b[s % (PD + 1)], acc, 0, 0, 0);
+          const int t2 = 2 * (s >> 1), qb = s & 1;
+          acc4[2 * qb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[t2], b[s % (PD + 1)], acc4[2 * qb], 0, 0, 0);
+          acc4[2 * qb + 1] =
+              __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[t2 + 1], b[s % (PD + 1)], acc4[2 * qb + 1], 0, 0, 0);
           if constexpr (RL) {
-            // the next item's rows, right after this k-step's last use of the register (its norms
-            // first, with the first k-step)
+            // the next item's rows, right after the last use of the registers (registers 2 t, 2 t + 1 after
+            // piece 2 t + 1), its norms first, with the first k-step
             if (s == 0) load_norms(gvn ? gnx : nx.g0, ipar ^ 1);
-            ra[s] = ld_rows(nrs, s);
+            if (s & 1) {
+              ra[s - 1] = ld_rows(nrs, s - 1);
+              ra[s] = ld_rows(nrs, s);
+            }
           }
-          if (s >= 1 && (s - 1) * kRsWaves <= NK) {
-            // (past the last piece a wave loads the last one again: the same bytes to the same place)
-            const int p = min((s - 1) * kRsWaves + wave, NK);
-            dma_b128(sdesc, sbuf + p * 1024, lane * 16, p * 1024);
+          {
+            if (s >= 1 && (s - 1) * STAGERS <= NK) {
+              // (past the last piece a wave loads the last one again: the same bytes to the same place)
+              const int p = min((s - 1) * STAGERS + wave, NK);
+              dma_b128(sdesc, sbuf + p * 1024, lane * 16, p * 1024);
+            }
           }
           // keep each k-step's operations in their k-step: left alone, the scheduler sinks the B reads
           // next to their MFMAs (one exposed LDS latency per k-step)
           __builtin_amdgcn_sched_barrier(0);
         }
       };
-      if constexpr (LAST) {
-        if (reload) kloop(BoolC<true>{});
-        else kloop(BoolC<false>{});
-      } else {
-        kloop(BoolC<false>{});
-      }
+      if (LAST && reload) kloop(BoolC<LAST>{});
+      else kloop(BoolC<false>{});
       const uint64_t ph2 = (a.flags & 16) ? __builtin_amdgcn_s_memtime() : 0;
-      // (the header piece holds query j's header at lanes j and j + 32: lane * 16 like the B pieces)
-      hd = *reinterpret_cast<const float4*>(smem + par * BUF + NK * 1024 + lane * 16);
-      // signal the next tile: this wave's reads of this one are done (lgkmcnt(0): the header is in) and
+      // (the header piece holds query j's header at lanes j and j + 32)
+      const float4 hq0 = *reinterpret_cast<const float4*>(smem + cur * BUF + NK * 1024 + (lane & 15) * 16);
+      const float4 hq1 = *reinterpret_cast<const float4*>(smem + cur * BUF + NK * 1024 + (16 + (lane & 15)) * 16);
+      // signal the next tile: this wave's reads of this one are done (lgkmcnt(0): the headers are in) and
       // its DMA pieces of the next have landed -- vmcnt counts, in issue order, only the next item's rows
-      // issued after its last piece (k-step NK / 8 + 1) beyond them
-      // (one fewer than counted: the order of a k-step's row load and DMA piece is the compiler's)
-      rs_wait_vm(LAST && has_next ? NK - 3 - NK / kRsWaves : 0);
+      // issued after its last piece beyond them
+      rs_wait_vm(LAST && has_next ? ROWS_AFTER : 0);
       rs_signal(s_ready);
       const uint64_t ph2b = (a.flags & 16) ? __builtin_amdgcn_s_memtime() : 0;
       uint64_t ph2c = ph2b, ph2d = 0;
       if (a.flags & 16) {  // (timing only) the wait for the k-loop's last MFMA result
-        float t = acc[15];
-        asm volatile("v_mov_b32 %0, %0" : "+v"(t));
+        float tv = acc4[3][3];
+        asm volatile("v_mov_b32 %0, %0" : "+v"(tv));
         ph2c = __builtin_amdgcn_s_memtime();
       }
-      // epilogue: lane (j, h) holds the 16 dots of query j with rows (r & 3) + 8 (r >> 2) + 4 h
-      if (gv && !(a.flags & 1)) {
-        // header of query j: {qs, uf, qn, q}
-        const float* wnorm = s_norm + (ipar * kRsWaves + wave) * 64;
-        const float qs = hd.x, uf = hd.y;
-        const float mm = METRIC == kL2 ? -2.0f * qs : -qs;
-        // one-fma filter over the 16 keys (norms from LDS four at a time: registers are short); the rare
-        // survivors are then handled one at a time, picked out of the accumulator by selects
-        // common case first, without the norms: mm < 0, so every filter value fma(acc_r, mm, xn_r) is
-        // >= fma(max_r acc_r, mm, min_r xn_r) (exact ordering, one monotone rounding); only when that
-        // bound reaches uf in some lane is the hit mask formed from the row norms
-        float amax = acc[0];
-#pragma unroll
-        for (int r = 1; r < 16; ++r) amax = fmaxf(amax, acc[r]);
-        if (__ballot(fmaf(amax, mm, METRIC == kL2 ? xnmin : 0.0f) < uf) != 0) {
-          if (a.flags & 16) {
-            ++n_hit_tiles;
-            ph2d = __builtin_amdgcn_s_memtime();
-          }
-          unsigned hits = 0;
-#pragma unroll
-          for (int q4 = 0; q4 < 4; ++q4) {
-            const float4 v = *reinterpret_cast<const float4*>(wnorm + 8 * q4 + 4 * h);
-            const float xv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-              hits |= (fmaf(acc[4 * q4 + u], mm, METRIC == kL2 ? xv[u] : 0.0f) < uf ? 1u : 0u) << (4 * q4 + u);
-          }
-          // every filter hit (a superset of the keys <= T_q; the refine's window is below T_q) goes to
-          // this wave's stream -- positions by ballot prefix, no atomics; k_rs_bucket sorts the
-          // streams into per-query buffers
-          const int bq = __float_as_int(hd.w);
-          const bool qv = bq >= 0 && bq < a.nq;  // (-1: an empty lane of the tile)
-          if (!qv) hits = 0;
-          const float qn = hd.z;
-          while (__ballot(hits != 0) != 0) {
-            const bool has = hits != 0;
-            const int r = has ? __builtin_ctz(hits) : 0;
-            hits &= hits - 1;
-            float c = acc[0];
-#pragma unroll
-            for (int i = 1; i < 16; ++i) c = r == i ? acc[i] : c;
-            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-            const uint64_t m = __ballot(has);
-            const int at = wcnt + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            if (has && at < a.wave_cap)
-              wstream[at] = make_int4(__float_as_int(pf_key<METRIC>(c, qs, wnorm[row], qn)), g * kGroupRows + row,
-                                      bq, 0);
-            wcnt += __popcll(m);
-          }
-        }
-      }
+      if (gv && !(a.flags & 1)) epilogue(acc4, hq0, hq1, ph2d);
       if (a.flags & 16) {
         const uint64_t ph3 = __builtin_amdgcn_s_memtime();
         pw_wait += ph1 - ph0;
@@ -398,10 +427,10 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
         pw_epi += ph3 - ph2c;
         if (ph2d) pw_hit += ph3 - ph2d;
       }
-      par ^= 1;
+      cur = nxt;
     };
     // the item's rows (loaded during the previous item's last tile) and everything before them; at the
-    // first item, the prologue's DMA pieces too, which this wave then signals as tile 0's
+    // first item, the prologue's DMA pieces too, which the wave then signals as tile 0's
     __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
     if (tt == 0) rs_signal(s_ready);
     {  // the smallest row norm of this wave's group (its norms landed with the rows; pad rows: +inf)
@@ -473,6 +502,8 @@ __global__ void k_rs_headers(const float* __restrict__ pre_kth, int64_t nq, cons
 // s < NK is the MFMA B operand of k-step s (lane j + 32 h: dims 16 s + 8 h .. + 8 of the tile's j-th
 // query), piece NK the 16-B headers (lane j: query j's; lanes 32..63 repeat them). One workgroup per
 // list; a thread reads 16 contiguous bytes of a query row (the row's pieces are consecutive threads).
+// Piece s = 2 t + qb, lane (c, kq) = (L & 15, L >> 4): dims 32 t + 8 kq .. + 8 of query 16 qb + c (the B
+// operand of v_mfma_f32_16x16x32_f16).
 template <int NK>
 __global__ __launch_bounds__(256) void k_rs_tiles(const int64_t* __restrict__ bucket_q, const int* __restrict__ bucket_off,
                                                   const uint16_t* __restrict__ qh, const float4* __restrict__ qhdr,
@@ -488,11 +519,12 @@ __global__ __launch_bounds__(256) void k_rs_tiles(const int64_t* __restrict__ bu
   for (int i = threadIdx.x; i < ntiles * NK * 64; i += blockDim.x) {
     const int t = i / (NK * 64), r = i - t * (NK * 64);
     const int s = r >> 6, L = r & 63;
-    const int jq = L & 31, hh = L >> 5;
+    const int jq = 16 * (s & 1) + (L & 15);
+    const int dim0 = 32 * (s >> 1) + 8 * (L >> 4);
     const int e = t * kRsQTile + jq;
     const int q = e < m ? (int)bucket_q[e0 + e] : -1;
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (q >= 0) v = *reinterpret_cast<const uint4*>(qh + (int64_t)q * (NK * 16) + 8 * (2 * s + hh));
+    if (q >= 0) v = *reinterpret_cast<const uint4*>(qh + (int64_t)q * (NK * 16) + dim0);
     *reinterpret_cast<uint4*>(base + t * IMG + s * 1024 + L * 16) = v;
   }
   for (int i = threadIdx.x; i < ntiles * 64; i += blockDim.x) {
@@ -517,8 +549,8 @@ bool rs_scan_supported(int dp) {
 template <int METRIC, int NK>
 static hipError_t launch_rs_mk(const RsScanArgs& a, int grid, hipStream_t s) {
   const size_t lds = rs_scan_lds_bytes(NK * 16);
-  hipError_t e = hipFuncSetAttribute((const void*)k_rs_scan<METRIC, NK>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipError_t e = hipFuncSetAttribute((const void*)k_rs_scan<METRIC, NK>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_rs_scan<METRIC, NK>), dim3(grid), dim3(kRsThreads), lds, s, a);
   return hipGetLastError();
