@@ -165,6 +165,7 @@ struct ScanJob {
   float* out_d;
   int64_t* out_i;
   int qtile;  // 32: K3, 64: K3w (must match the work decomposition of the probe map / single job)
+  bool dump = false;  // DUMP mode (raw keys per slot for K8) whatever k: set by every caller that runs K8
 };
 
 // Query tile of the fine scan for k: K3w (64 queries, slab-staged) where it applies, else K3.
@@ -177,7 +178,9 @@ int pick_qtile(int k, int d, int G) {
 }
 
 void run_scan(const ScanJob& j, int device, Workspace& ws, hipStream_t s) {
-  const int kcap = scan_kcap(j.k);  // 0 = DUMP mode (k > kMaxK): raw keys per slot for K8
+  // 0 = DUMP mode (k > kMaxK, or asked for): raw keys per slot + (first row, rows) slot info for K8
+  const int kcap = j.dump ? 0 : scan_kcap(j.k);
+  require(!(j.dump && j.qtile == 64), "internal: DUMP runs the 32-query K3", MIVS_ERR_UNSUPPORTED);
   require(j.k >= 1 && j.k <= kMaxSelectK, "k must be in [1, " + std::to_string(kMaxSelectK) + "]",
           MIVS_ERR_UNSUPPORTED);
   require(j.dp <= 1024, "dim > 1024 is not supported by this build", MIVS_ERR_UNSUPPORTED);
@@ -240,10 +243,10 @@ int64_t select_batch(int64_t nq, size_t per_query_bytes) {
 // Writes [nq][k] results into (out_d, out_i) (merging chunk partials if needed).
 void single_list_topk(const ListSet& ls, int G, const float* queries, const float* qnorms, const int64_t* rows,
                       int64_t nq, int d, int dp, int k, int metric, float* out_d, int64_t* out_i, int device,
-                      Workspace& ws, hipStream_t s) {
+                      Workspace& ws, hipStream_t s, bool dump = false) {
   const int64_t chunks = std::max<int64_t>(1, ceil_div(ls.n_groups, G));
   require(ceil_div(nq, kQTile) * chunks < (int64_t)INT32_MAX, "too many work items", MIVS_ERR_UNSUPPORTED);
-  if (k > kMaxK) {  // DUMP scan + K8 select, in query batches
+  if (k > kMaxK || dump) {  // DUMP scan + K8 select, in query batches
     const int64_t slot_rows = (int64_t)G * kGroupRows;
     const int64_t qb = select_batch(nq, (size_t)(chunks * (slot_rows * 4 + 16)));
     for (int64_t b0 = 0; b0 < nq; b0 += qb) {
@@ -263,6 +266,7 @@ void single_list_topk(const ListSet& ls, int G, const float* queries, const floa
       ScanJob j{&ls, G, qb_ptr, qn_ptr, d, dp, k, metric, ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(),
                 ws.bucket_off.as<int>(), ws.work_off.as<int>(), ws.part_d.as<float>(), ws.part_i.as<int64_t>(),
                 kQTile};
+      j.dump = true;
       run_scan(j, device, ws, s);
       SelectArgs sa{};
       sa.keys = ws.part_d.as<float>();
@@ -835,6 +839,15 @@ void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_
   }
 }
 
+// The coarse probe for n_probes > 16 (beyond K3w's register top-k): K3 in DUMP mode (every key of the
+// centroid list, written as computed) + K8 per query, instead of K3's 32- or 64-entry register top-k per
+// lane + K7 over the chunks (same keys, same (key, id) order: bit-identical probes). MIVS_COARSE_DUMP=0
+// keeps the register top-k.
+bool coarse_dump(int np) {
+  const char* e = getenv("MIVS_COARSE_DUMP");
+  return np > 16 && !(e && e[0] == '0');
+}
+
 // Centroid chunk of the coarse probe: enough (query tile, chunk) work items for >= 4 per CU -- a 10k-query
 // batch over 1024 centroids is only 313 query tiles -- with K7 merging the chunks' top-n_probes
 int coarse_groups(const mivs_index_s* idx, int64_t nq) {
@@ -855,7 +868,7 @@ void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t 
   ws.probes_d.reserve(sizeof(float) * nq * np);
   ws.probes_i.reserve(sizeof(int64_t) * nq * np);
   single_list_topk(idx->cents, coarse_groups(idx, nq), q, ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, np, idx->metric,
-                   ws.probes_d.as<float>(), ws.probes_i.as<int64_t>(), idx->device, ws, s);
+                   ws.probes_d.as<float>(), ws.probes_i.as<int64_t>(), idx->device, ws, s, coarse_dump(np));
   if (out_probes) HIPCHK(launch_i64_to_i32(ws.probes_i.as<int64_t>(), nq * np, out_probes, s));
   ivf_search_probed(idx, s, q, nq, k, np, out_d, out_i, pf, pr, prof, nullptr, allow_rs);
 }
@@ -1067,6 +1080,7 @@ void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t
   ScanJob j{&L, idx->G, q, ws.qn.as<float>(), idx->d, idx->dp, k, idx->metric, ws.bucket_q.as<int64_t>(),
             ws.bucket_slot.as<int64_t>(), ws.bucket_off.as<int>(), ws.work_off.as<int>(), ws.part_d.as<float>(),
             ws.part_i.as<int64_t>(), qtile};
+  j.dump = dump;
   if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
   run_scan(j, idx->device, ws, s);
   if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
@@ -1628,7 +1642,8 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
     ws.probes_d.reserve(sizeof(float) * nq * np);
     ws.probes_i.reserve(sizeof(int64_t) * nq * np);
     single_list_topk(idx->cents, coarse_groups(idx, nq), d_q, ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, np,
-                     idx->metric, ws.probes_d.as<float>(), ws.probes_i.as<int64_t>(), idx->device, ws, s);
+                     idx->metric, ws.probes_d.as<float>(), ws.probes_i.as<int64_t>(), idx->device, ws, s,
+                     coarse_dump(np));
     if (d_probes) HIPCHK(launch_i64_to_i32(ws.probes_i.as<int64_t>(), nq * np, d_probes, s));
     const ListSet& L = idx->lists;
     // k > 16 (the candidate pools of IVF-PQ + refine): K9 in DUMP mode writes every probed row's key and

@@ -278,6 +278,134 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
   }
 }
 
+// K8s: the same selection for small k over few DUMP keys (k <= 64, slots x slot_rows <= 1024 per query: the
+// coarse probe's top-n_probes of the centroid list), one WAVE per query instead of a 1024-thread block
+// with 2048-bin histograms and a 1024-wide bitonic sort. Each lane holds <= 16 candidates in registers:
+//   1. T = the need-th smallest orderable key: binary search over the 32 key bits, counts by wave sums;
+//   2. among keys equal to T, the (need - #(key < T)) smallest ids: binary search over the id bits (only
+//      when the tie is larger than what is needed);
+//   3. the need chosen (key, id) pairs -> one per lane (ballot prefix into LDS) -> 64-lane bitonic sort
+//      by (key, id) -> the first k, the missing ranks (id -1, +inf / IP -inf) as in K8.
+constexpr int kSmallPer = 16;
+constexpr int kSmallWaves = 4;
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+template <int METRIC>
+__global__ __launch_bounds__(64 * kSmallWaves) void k_select_small(SelectArgs a) {
+  __shared__ uint32_t s_u[kSmallWaves][64];
+  __shared__ int64_t s_i[kSmallWaves][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t q = (int64_t)blockIdx.x * kSmallWaves + wv;
+  if (q >= a.nq) return;
+  const int k = a.k;
+  const int64_t base = q * a.slots_per_q;
+  const int n_total = (int)(a.slots_per_q * a.slot_rows);
+  uint32_t u[kSmallPer];
+  int nv = 0;
+#pragma unroll
+  for (int i = 0; i < kSmallPer; ++i) {
+    const int t = lane + 64 * i;
+    u[i] = 0xFFFFFFFFu;
+    if (t < n_total) {
+      const Cand c = cand_key<false, METRIC>(a, base, t);
+      if (c.valid) {
+        u[i] = c.u;
+        ++nv;
+      }
+    }
+  }
+  nv = wave_sum(nv);
+  const int need = nv < k ? nv : k;
+  auto count_le = [&](uint32_t m) {
+    int c = 0;
+#pragma unroll
+    for (int i = 0; i < kSmallPer; ++i) c += u[i] <= m ? 1 : 0;  // (invalid = 0xFFFFFFFF > every valid m)
+    return wave_sum(c);
+  };
+  uint32_t T = 0;
+  int64_t I = LLONG_MAX;  // among keys == T: ids <= I are chosen
+  if (need > 0) {
+    uint32_t lo = 0, hi = kOrdInf - 1;  // the need-th smallest valid key lies in [lo, hi]
+    while (lo < hi) {
+      const uint32_t mid = lo + ((hi - lo) >> 1);
+      if (count_le(mid) >= need) hi = mid; else lo = mid + 1;
+    }
+    T = lo;
+    const int c_lt = T > 0 ? count_le(T - 1) : 0;
+    const int c_eq = count_le(T) - c_lt;
+    const int m = need - c_lt;
+    if (c_eq > m) {  // a tie larger than needed: the m smallest ids among keys == T (ids are distinct)
+      auto count_id = [&](int64_t x) {
+        int c = 0;
+#pragma unroll
+        for (int i = 0; i < kSmallPer; ++i)
+          if (u[i] == T && cand_id<false>(a, base, lane + 64 * i) <= x) ++c;
+        return wave_sum(c);
+      };
+      int64_t ilo = 0, ihi = LLONG_MAX;  // (valid candidates have ids >= 0; count_id(LLONG_MAX) = c_eq >= m)
+      while (ilo < ihi) {
+        const int64_t mid = ilo + ((ihi - ilo) >> 1);
+        if (count_id(mid) >= m) ihi = mid; else ilo = mid + 1;
+      }
+      I = ilo;
+    }
+  }
+  // the chosen pairs, one per lane
+  int nsel = 0;
+#pragma unroll
+  for (int i = 0; i < kSmallPer; ++i) {
+    const int t = lane + 64 * i;
+    bool take = need > 0 && u[i] <= T && u[i] != 0xFFFFFFFFu;
+    int64_t id = 0;
+    if (take) {
+      id = cand_id<false>(a, base, t);
+      if (u[i] == T && id > I) take = false;
+    }
+    const uint64_t bm = __ballot(take);
+    if (take) {
+      const int at = nsel + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+      if (at < 64) {
+        s_u[wv][at] = u[i];
+        s_i[wv][at] = id;
+      }
+    }
+    nsel += __popcll(bm);
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  uint32_t ku = lane < need ? s_u[wv][lane] : 0xFFFFFFFFu;
+  int64_t ki = lane < need ? s_i[wv][lane] : LLONG_MAX;
+  // bitonic sort of the 64 lanes by (key, id), ascending
+#pragma unroll
+  for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const uint32_t ou = __shfl_xor(ku, stride);
+      const int64_t oi = __shfl_xor(ki, stride);
+      const bool lower = (lane & stride) == 0;
+      const bool up = (lane & size) == 0;
+      const bool o_less = ou < ku || (ou == ku && oi < ki);
+      // the lower lane of a pair keeps the smaller in an ascending block, the larger in a descending one
+      const bool take_o = (lower == up) ? o_less : !o_less && !(ou == ku && oi == ki);
+      if (take_o) {
+        ku = ou;
+        ki = oi;
+      }
+    }
+  }
+  if (lane < k) {
+    const bool valid = lane < need;
+    const float key = valid ? from_ord(ku) : INFINITY;
+    a.out_d[q * k + lane] = valid ? (METRIC == kIP ? -key : key) : (METRIC == kIP ? -INFINITY : INFINITY);
+    a.out_i[q * k + lane] = valid ? ki : (int64_t)-1;
+  }
+}
+
 template <int CAP>
 hipError_t launch_cap(const SelectArgs& a, bool expl, hipStream_t s) {
   const dim3 grid((unsigned)a.nq), block(kSelThreads);
@@ -298,6 +426,12 @@ hipError_t launch_select(const SelectArgs& a, hipStream_t s) {
   if (a.nq <= 0) return hipSuccess;
   if (a.nq > 0x7FFFFFFF) return hipErrorInvalidValue;
   const bool expl = a.slot_info == nullptr;
+  if (!expl && a.k <= 64 && a.slots_per_q * a.slot_rows <= 64 * kSmallPer) {  // K8s
+    const dim3 grid((unsigned)ceil_div(a.nq, (int64_t)kSmallWaves)), block(64 * kSmallWaves);
+    if (a.metric == kIP) hipLaunchKernelGGL(k_select_small<kIP>, grid, block, 0, s, a);
+    else hipLaunchKernelGGL(k_select_small<kL2>, grid, block, 0, s, a);
+    return hipGetLastError();
+  }
   if (a.k <= 512) return launch_cap<1024>(a, expl, s);
   if (a.k <= 1024) return launch_cap<2048>(a, expl, s);
   if (a.k <= 2048) return launch_cap<4096>(a, expl, s);

@@ -193,3 +193,23 @@ def test_ivf_pq_switch_same_bits(mivs_lib, monkeypatch, k, env):
     np.testing.assert_array_equal(i1.cpu().numpy(), i0.cpu().numpy())
     np.testing.assert_array_equal(_bits(d1.cpu().numpy()), _bits(d0.cpu().numpy()))
     idx.close()
+
+
+@pytest.mark.parametrize("n_probes", [17, 32, 48])
+def test_coarse_probe_dump_switch_same_bits(ivf, flat_data, monkeypatch, n_probes):
+    """n_probes > 16: the coarse probe through K3 DUMP + K8 (default) and through K3's register top-k
+    (MIVS_COARSE_DUMP=0) give the same probes (order and ids) and the same search result"""
+    from mivs.neighbors import ivf_flat
+
+    idx, _ = ivf
+    _, q = flat_data
+    qd = torch.from_numpy(q).cuda()
+    sp = ivf_flat.SearchParams(n_probes=n_probes)
+    p0 = torch.empty((q.shape[0], n_probes), dtype=torch.int32, device="cuda")
+    d0, i0 = ivf_flat.search(sp, idx, qd, 10, probes_out=p0)
+    monkeypatch.setenv("MIVS_COARSE_DUMP", "0")
+    p1 = torch.empty_like(p0)
+    d1, i1 = ivf_flat.search(sp, idx, qd, 10, probes_out=p1)
+    np.testing.assert_array_equal(p1.cpu().numpy(), p0.cpu().numpy())
+    np.testing.assert_array_equal(i1.cpu().numpy(), i0.cpu().numpy())
+    np.testing.assert_array_equal(_bits(d1.cpu().numpy()), _bits(d0.cpu().numpy()))
