@@ -321,6 +321,20 @@ __global__ __launch_bounds__(64 * kSmallWaves) void k_select_small(SelectArgs a)
   }
   nv = wave_sum(nv);
   const int need = nv < k ? nv : k;
+  // the valid keys' range bounds the search (a few of the 32 bits once the keys share an exponent)
+  uint32_t umin = 0xFFFFFFFFu, umax = 0u;
+#pragma unroll
+  for (int i = 0; i < kSmallPer; ++i)
+    if (u[i] != 0xFFFFFFFFu) {
+      umin = u[i] < umin ? u[i] : umin;
+      umax = u[i] > umax ? u[i] : umax;
+    }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint32_t a0 = __shfl_xor(umin, o), a1 = __shfl_xor(umax, o);
+    umin = a0 < umin ? a0 : umin;
+    umax = a1 > umax ? a1 : umax;
+  }
   auto count_le = [&](uint32_t m) {
     int c = 0;
 #pragma unroll
@@ -330,7 +344,7 @@ __global__ __launch_bounds__(64 * kSmallWaves) void k_select_small(SelectArgs a)
   uint32_t T = 0;
   int64_t I = LLONG_MAX;  // among keys == T: ids <= I are chosen
   if (need > 0) {
-    uint32_t lo = 0, hi = kOrdInf - 1;  // the need-th smallest valid key lies in [lo, hi]
+    uint32_t lo = umin, hi = umax;  // the need-th smallest valid key lies in [lo, hi]
     while (lo < hi) {
       const uint32_t mid = lo + ((hi - lo) >> 1);
       if (count_le(mid) >= need) hi = mid; else lo = mid + 1;
