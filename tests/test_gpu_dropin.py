@@ -101,3 +101,46 @@ def test_coordinator_ivf_pq_seam(mivs_lib):
     np.testing.assert_array_equal(out.final_distances.view(np.int32), od.view(np.int32))
     co.cleanup_all_indices()
     dm.cleanup_distribution()
+
+
+def test_parallel_index_builder_and_search_engine_bitexact_vs_oracle(mivs_lib):
+    """§8 row a2: ParallelIndexBuilder.build_indices_parallel (one build per GPU on the thread pool,
+    improved_multi_gpu_rag.py:108-190 upstream) and ParallelSearchEngine.parallel_search through the
+    engine equal the oracle's IVF-Flat build (centroids, list sizes, list ids) and search (ids, distance
+    bits), and the brute-force seam equals the oracle's exact kNN -- on every GPU of the box (one here)."""
+    import improved_multi_gpu_rag as imr
+
+    n_gpus = torch.cuda.device_count()
+    rng = np.random.default_rng(31)
+    n, d, nq, k = 6000 * n_gpus, 96, 40, 15
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    q = rng.standard_normal((nq, d)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    parts = np.array_split(x, n_gpus)
+    builder = imr.ParallelIndexBuilder(num_gpus=n_gpus)
+    res = builder.build_indices_parallel([torch.from_numpy(p) for p in parts], imr.IndexType.IVF_FLAT,
+                                         {"n_lists": 24, "kmeans_n_iters": 5})
+    assert not res.get("failed_gpus"), res
+    offs = np.concatenate([[0], np.cumsum([p.shape[0] for p in parts])])
+    oracle_shards = [O.ivf_build(p, 24, iters=5, id_offset=int(offs[g])) for g, p in enumerate(parts)]
+    for g, (oc, osz, oids) in enumerate(oracle_shards):
+        idx = res["indexes"][g]
+        np.testing.assert_array_equal(idx.centers.cpu().numpy().view(np.int32), oc.view(np.int32))
+        np.testing.assert_array_equal(idx.list_sizes.numpy(), osz)
+        np.testing.assert_array_equal(idx.list_ids().cpu().numpy(), oids)
+    cfg = imr.SearchConfig(top_k=k, n_probes=6)
+    eng = imr.ParallelSearchEngine(res["indexes"], imr.IndexType.IVF_FLAT, cfg)
+    dd, ii = eng.parallel_search(torch.from_numpy(q).cuda())
+    # the oracle: every shard's top-k, merged by (distance, id)
+    per = [O.ivf_search(p, *oracle_shards[g], q, 6, k, id_offset=int(offs[g]))[:2] for g, p in enumerate(parts)]
+    md, mi = O.merge(np.stack([r[0] for r in per], axis=1), np.stack([r[1] for r in per], axis=1), k)
+    np.testing.assert_array_equal(np.asarray(ii), mi)
+    np.testing.assert_array_equal(np.asarray(dd, dtype=np.float32).view(np.int32), md.view(np.int32))
+    # brute-force seam
+    resb = builder.build_indices_parallel([torch.from_numpy(p) for p in parts], imr.IndexType.BRUTE_FORCE, {})
+    engb = imr.ParallelSearchEngine(resb["indexes"], imr.IndexType.BRUTE_FORCE, cfg)
+    bd, bi = engb.parallel_search(torch.from_numpy(q).cuda())
+    ed, ei = O.knn(x, q, k)
+    np.testing.assert_array_equal(np.asarray(bi), ei)
+    np.testing.assert_array_equal(np.asarray(bd, dtype=np.float32).view(np.int32), ed.view(np.int32))
