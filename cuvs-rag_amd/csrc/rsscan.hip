@@ -680,6 +680,64 @@ __global__ __launch_bounds__(256) void k_rs_scatter(const int4* __restrict__ wav
   }
 }
 
+// The same bucketing with an LDS histogram per group of streams. Group b holds the streams of J K13
+// workgroups of one item queue (x = b % 8, workgroups x + 8 (J (b / 8) + t), t < J). Those workgroups take
+// consecutive items of the same lists, so their hits fall on the same lists' queries, and the ~2M
+// contended global atomics of the flat kernels become one per (group, query) with a hit.
+constexpr int kRsLdsMaxQ = 32768;  // 128 KiB of int bins
+__device__ __forceinline__ int rs_group_stream(int b, int t, int J) {
+  return ((b & 7) + 8 * (J * (b >> 3) + t / kRsWaves)) * kRsWaves + t % kRsWaves;
+}
+
+__device__ __forceinline__ void rs_group_hist(const int4* __restrict__ wave_buf, int wave_cap,
+                                              const int* __restrict__ wave_cnt, int J, int nq, int* bins) {
+  for (int i = threadIdx.x; i < nq; i += blockDim.x) bins[i] = 0;
+  __syncthreads();
+  for (int t = 0; t < kRsWaves * J; ++t) {
+    const int w = rs_group_stream(blockIdx.x, t, J);
+    const int n = min(wave_cnt[w], wave_cap);
+    const int4* sb = wave_buf + (int64_t)w * wave_cap;
+    for (int e = threadIdx.x; e < n; e += blockDim.x) atomicAdd(bins + sb[e].z, 1);
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(1024) void k_rs_count_lds(const int4* __restrict__ wave_buf, int wave_cap,
+                                                       const int* __restrict__ wave_cnt, int J, int nq,
+                                                       unsigned long long* __restrict__ qcnt) {
+  extern __shared__ int bins[];
+  rs_group_hist(wave_buf, wave_cap, wave_cnt, J, nq, bins);
+  for (int i = threadIdx.x; i < nq; i += blockDim.x) {
+    const int c = bins[i];
+    if (c) atomicAdd(qcnt + i, (unsigned long long)c);
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_rs_scatter_lds(const int4* __restrict__ wave_buf, int wave_cap,
+                                                         const int* __restrict__ wave_cnt, int J, int nq,
+                                                         const int64_t* __restrict__ off, int* __restrict__ fill,
+                                                         float* __restrict__ key, int* __restrict__ pos) {
+  extern __shared__ int bins[];
+  rs_group_hist(wave_buf, wave_cap, wave_cnt, J, nq, bins);
+  // this group's range of each query's run (< n_waves * wave_cap entries in all: fits an int)
+  for (int i = threadIdx.x; i < nq; i += blockDim.x) {
+    const int c = bins[i];
+    if (c) bins[i] = (int)(off[i] + atomicAdd(fill + i, c));
+  }
+  __syncthreads();
+  for (int t = 0; t < kRsWaves * J; ++t) {
+    const int w = rs_group_stream(blockIdx.x, t, J);
+    const int n = min(wave_cnt[w], wave_cap);
+    const int4* sb = wave_buf + (int64_t)w * wave_cap;
+    for (int e = threadIdx.x; e < n; e += blockDim.x) {
+      const int4 v = sb[e];
+      const int at = atomicAdd(bins + v.z, 1);
+      key[at] = __int_as_float(v.x);
+      pos[at] = v.y;
+    }
+  }
+}
+
 size_t rs_bucket_tmp_bytes(int nq, int n_waves) {
   return sizeof(int64_t) * ((size_t)nq + 1) + sizeof(int) * (size_t)nq + sizeof(int64_t) * ((size_t)n_waves + 1) +
          scan_tmp_bytes(nq + 1) + 64;
@@ -698,7 +756,33 @@ hipError_t launch_rs_bucket(const int4* wave_buf, int wave_cap, const int* wave_
   if (n_waves <= 0) return launch_exclusive_scan_i64(qcnt, cand_off, nq + 1, stmp, s);
   if (n_waves > kRsMaxStreams) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_rs_stream_off, dim3(1), dim3(1024), 0, s, wave_cnt, n_waves, wave_cap, woff, lost);
-  hipLaunchKernelGGL(k_rs_count, dim3((unsigned)grid), dim3(256), 0, s, wave_buf, wave_cap, woff, n_waves,
+  // grouped LDS-histogram form when the streams come from K13's 8 item queues (n_waves = 8 queues x P
+  // workgroups x kRsWaves) and the bins fit LDS; J = workgroups of a queue per group
+  const int P = n_waves / (8 * kRsWaves);
+  int J = 0;
+  const char* fe = getenv("MIVS_RS_BUCKET_FLAT");
+  if (nq <= kRsLdsMaxQ && n_waves == 8 * kRsWaves * P && P > 0 && !(fe && fe[0] == '1'))
+    J = P % 4 == 0 ? 4 : P % 2 == 0 ? 2 : 1;
+  if (J > 0) {
+    const size_t lds = sizeof(int) * (size_t)nq;
+    static const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rs_count_lds),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)(sizeof(int) * kRsLdsMaxQ));
+    static const hipError_t a2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rs_scatter_lds),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)(sizeof(int) * kRsLdsMaxQ));
+    if (a1 != hipSuccess) return a1;
+    if (a2 != hipSuccess) return a2;
+    const unsigned nb = (unsigned)(8 * (P / J));
+    hipLaunchKernelGGL(k_rs_count_lds, dim3(nb), dim3(1024), lds, s, wave_buf, wave_cap, wave_cnt, J, nq,
+                       reinterpret_cast<unsigned long long*>(qcnt));
+    e = launch_exclusive_scan_i64(qcnt, cand_off, nq + 1, stmp, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_rs_scatter_lds, dim3(nb), dim3(1024), lds, s, wave_buf, wave_cap, wave_cnt, J, nq,
+                       cand_off, fill, cand_key, cand_pos);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(k_rs_count,dim3((unsigned)grid), dim3(256), 0, s, wave_buf, wave_cap, woff, n_waves,
                      reinterpret_cast<unsigned long long*>(qcnt));
   e = launch_exclusive_scan_i64(qcnt, cand_off, nq + 1, stmp, s);
   if (e != hipSuccess) return e;
