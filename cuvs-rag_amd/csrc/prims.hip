@@ -151,6 +151,57 @@ __global__ void k_probe_fill(const int64_t* __restrict__ probes, int64_t n, int 
   qp_slots[i] = ceil_div(list_goff[l + 1] - list_goff[l], G);
 }
 
+// The same count and fill with an LDS histogram per chunk of kPmChunk entries: a list probed by m queries
+// took m contended global atomics per pass, now one per (chunk, list). The order of the queries inside a
+// bucket was the atomics' order before and still is (nothing downstream depends on it).
+constexpr int kPmChunk = 8192;
+constexpr int kPmMaxLists = 32768;  // 128 KiB of int bins
+
+__device__ __forceinline__ void pm_chunk_hist(const int64_t* __restrict__ probes, int64_t n, int n_lists, int* bins) {
+  for (int l = threadIdx.x; l < n_lists; l += blockDim.x) bins[l] = 0;
+  __syncthreads();
+  const int64_t i0 = (int64_t)blockIdx.x * kPmChunk;
+  const int64_t i1 = i0 + kPmChunk < n ? i0 + kPmChunk : n;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const int64_t l = probes[i];
+    if (l >= 0) atomicAdd(bins + l, 1);
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(1024) void k_probe_count_lds(const int64_t* __restrict__ probes, int64_t n, int n_lists,
+                                                          int* __restrict__ counts) {
+  extern __shared__ int bins[];
+  pm_chunk_hist(probes, n, n_lists, bins);
+  for (int l = threadIdx.x; l < n_lists; l += blockDim.x)
+    if (bins[l]) atomicAdd(counts + l, bins[l]);
+}
+
+__global__ __launch_bounds__(1024) void k_probe_fill_lds(const int64_t* __restrict__ probes, int64_t n, int np,
+                                                         int n_lists, const int* __restrict__ bucket_off,
+                                                         int* __restrict__ fill, int64_t* __restrict__ bucket_q,
+                                                         int64_t* __restrict__ bucket_qp,
+                                                         const int64_t* __restrict__ list_goff, int G,
+                                                         int64_t* __restrict__ qp_slots) {
+  extern __shared__ int bins[];
+  pm_chunk_hist(probes, n, n_lists, bins);
+  for (int l = threadIdx.x; l < n_lists; l += blockDim.x) {
+    const int c = bins[l];
+    if (c) bins[l] = bucket_off[l] + atomicAdd(fill + l, c);  // this chunk's range of list l's bucket
+  }
+  __syncthreads();
+  const int64_t i0 = (int64_t)blockIdx.x * kPmChunk;
+  const int64_t i1 = i0 + kPmChunk < n ? i0 + kPmChunk : n;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const int l = (int)probes[i];
+    if (l < 0) { qp_slots[i] = 0; continue; }
+    const int e = atomicAdd(bins + l, 1);
+    bucket_q[e] = i / np;
+    bucket_qp[e] = i;
+    qp_slots[i] = ceil_div(list_goff[l + 1] - list_goff[l], G);
+  }
+}
+
 __global__ void k_bucket_slot(int64_t* __restrict__ bucket_slot, int64_t n, const int64_t* __restrict__ qp_base) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e < n) bucket_slot[e] = qp_base[bucket_slot[e]];
@@ -287,11 +338,30 @@ hipError_t launch_probe_map(const int64_t* probes, int64_t nq, int np, int n_lis
   void* stmp = qp_base + n;
   hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * n_lists, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_probe_count, grid1(n, 256), dim3(256), 0, s, probes, n, counts);
+  // LDS-histogram form once the entries outnumber the lists (a chunk then repeats lists)
+  const bool lds = n_lists <= kPmMaxLists && n >= 2 * (int64_t)n_lists;
+  const size_t lds_bytes = sizeof(int) * (size_t)n_lists;
+  if (lds) {
+    static const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_probe_count_lds),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)(sizeof(int) * kPmMaxLists));
+    static const hipError_t a2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_probe_fill_lds),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)(sizeof(int) * kPmMaxLists));
+    if (a1 != hipSuccess) return a1;
+    if (a2 != hipSuccess) return a2;
+    hipLaunchKernelGGL(k_probe_count_lds, grid1(n, kPmChunk), dim3(1024), lds_bytes, s, probes, n, n_lists, counts);
+  } else {
+    hipLaunchKernelGGL(k_probe_count, grid1(n, 256), dim3(256), 0, s, probes, n, counts);
+  }
   hipLaunchKernelGGL(k_probe_prefix, dim3(1), dim3(1024), 0, s, counts, n_lists, list_goff, chunk_groups, qtile,
                      bucket_off, work_off, fill);
-  hipLaunchKernelGGL(k_probe_fill, grid1(n, 256), dim3(256), 0, s, probes, n, np, bucket_off, fill, bucket_q,
-                     bucket_slot, list_goff, chunk_groups, qp_slots);
+  if (lds)
+    hipLaunchKernelGGL(k_probe_fill_lds, grid1(n, kPmChunk), dim3(1024), lds_bytes, s, probes, n, np, n_lists,
+                       bucket_off, fill, bucket_q, bucket_slot, list_goff, chunk_groups, qp_slots);
+  else
+    hipLaunchKernelGGL(k_probe_fill, grid1(n, 256), dim3(256), 0, s, probes, n, np, bucket_off, fill, bucket_q,
+                       bucket_slot, list_goff, chunk_groups, qp_slots);
   e = launch_exclusive_scan_i64(qp_slots, qp_base, n, stmp, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_bucket_slot, grid1(n, 256), dim3(256), 0, s, bucket_slot, n, qp_base);

@@ -501,11 +501,12 @@ __global__ void k_rs_headers(const float* __restrict__ pre_kth, int64_t nq, cons
 // Tile images for K13: per list l with m_l queries, ceil(m_l / 32) tiles of [NK + 1] x 1 KiB: piece
 // s < NK is the MFMA B operand of k-step s (lane j + 32 h: dims 16 s + 8 h .. + 8 of the tile's j-th
 // query), piece NK the 16-B headers (lane j: query j's; lanes 32..63 repeat them). One workgroup per
-// list; a thread reads 16 contiguous bytes of a query row (the row's pieces are consecutive threads).
+// list (1024 threads: the stores of a list's ~0.5 MB keep more requests in flight); a thread reads 16
+// contiguous bytes of a query row (the row's pieces are consecutive threads).
 // Piece s = 2 t + qb, lane (c, kq) = (L & 15, L >> 4): dims 32 t + 8 kq .. + 8 of query 16 qb + c (the B
 // operand of v_mfma_f32_16x16x32_f16).
 template <int NK>
-__global__ __launch_bounds__(256) void k_rs_tiles(const int64_t* __restrict__ bucket_q, const int* __restrict__ bucket_off,
+__global__ __launch_bounds__(1024) void k_rs_tiles(const int64_t* __restrict__ bucket_q, const int* __restrict__ bucket_off,
                                                   const uint16_t* __restrict__ qh, const float4* __restrict__ qhdr,
                                                   int nq, char* __restrict__ tiles) {
   const int l = blockIdx.x;
@@ -587,7 +588,7 @@ int64_t rs_tiles_bytes(int64_t ne, int n_lists, int dp) {
 template <int NK>
 static void launch_rs_tiles_k(const int64_t* bucket_q, const int* bucket_off, int n_lists, const uint16_t* qh,
                               const float4* qhdr, int nq, char* tiles, hipStream_t s) {
-  hipLaunchKernelGGL(k_rs_tiles<NK>, dim3((unsigned)n_lists), dim3(256), 0, s, bucket_q, bucket_off, qh, qhdr, nq,
+  hipLaunchKernelGGL(k_rs_tiles<NK>, dim3((unsigned)n_lists), dim3(1024), 0, s, bucket_q, bucket_off, qh, qhdr, nq,
                      tiles);
 }
 
