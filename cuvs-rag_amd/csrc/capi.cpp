@@ -88,7 +88,7 @@ struct Workspace {
   Buf qh, qscale, qres, qtheta, pf_key, pf_pos, pf_bound, pf_stats, ovf_q, ovf_rows, ovf_d, ovf_i;
   // K13 row-stationary scan: the full probe list, the pre-pass result, per-query headers and candidates
   Buf probes_full, pre_kth, pre_goff, qhdr, cand_off, cand_key, cand_pos, rs_bucket_tmp, rs_tiles, rs_wave_buf,
-      rs_wave_cnt;
+      rs_wave_cnt, rs_bounds;
   // per-list query counts of the last search's own probe map (an exact fallback re-maps its queries)
   Buf stat_counts, rs_ovf_q, rs_ovf_rows, rs_ovf_d, rs_ovf_i, rs_items;
 };
@@ -947,8 +947,13 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   int64_t max_items = 0;  // every list probed: the item table's bound (the probe map decides the count)
   for (int l = 0; l < L.n_lists; ++l) max_items += ceil_div(L.h_goff[l + 1] - L.h_goff[l], kRsBlockGroups);
   ws.rs_items.reserve(sizeof(int4) * (size_t)std::max<int64_t>(max_items, 1));
+  // items dealt from 8 queues of equal tile work, dynamically inside a queue (MIVS_RS_STATIC_DEAL=1: the
+  // round-1 deal -- equal item counts, every P-th item -- for A/B runs)
+  const char* dde = getenv("MIVS_RS_STATIC_DEAL");
+  const bool static_deal = dde && dde[0] == '1';
+  ws.rs_bounds.reserve(sizeof(int) * 9);
   HIPCHK(launch_rs_items(ws.work_off.as<int>(), ws.bucket_off.as<int>(), L.goff.as<int64_t>(), L.n_lists,
-                         (int)max_items, ws.rs_items.as<int4>(), s));
+                         (int)max_items, ws.rs_items.as<int4>(), static_deal ? nullptr : ws.rs_bounds.as<int>(), s));
   RsScanArgs a{};
   a.groups_h = idx->groups_h.as<uint16_t>();
   a.row_norms = L.norms.as<float>();
@@ -967,9 +972,12 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   idx->last_rs_waves = n_waves;
   a.wave_cap = (int)std::min<int64_t>(kRsWaveCapMax, std::max<int64_t>(1024, 2 * nq));
   ws.rs_wave_buf.reserve(sizeof(int4) * (size_t)n_waves * a.wave_cap);
-  ws.rs_wave_cnt.reserve(sizeof(int) * (n_waves + 1));
+  ws.rs_wave_cnt.reserve(sizeof(int) * (n_waves + 1 + 8));  // + the lost flag, the 8 item-queue counters
   a.wave_buf = ws.rs_wave_buf.as<int4>();
   a.wave_cnt = ws.rs_wave_cnt.as<int>();
+  a.queue = static_deal ? nullptr : a.wave_cnt + n_waves + 1;
+  a.bounds = static_deal ? nullptr : ws.rs_bounds.as<int>();
+  HIPCHK(hipMemsetAsync(a.wave_cnt + n_waves, 0, sizeof(int) * 9, s));  // lost flag + queue counters
   a.flags = getenv("MIVS_RS_FLAGS") ? atoi(getenv("MIVS_RS_FLAGS")) : 0;
   if (a.flags & 2) a.flags |= 1;  // stale LDS tiles: never run an epilogue on them
   Buf pbuf;
@@ -1015,7 +1023,6 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   ws.cand_key.reserve(sizeof(float) * max_cand);
   ws.cand_pos.reserve(sizeof(int) * max_cand);
   ws.rs_bucket_tmp.reserve(rs_bucket_tmp_bytes((int)nq, n_waves));
-  HIPCHK(hipMemsetAsync(a.wave_cnt + n_waves, 0, sizeof(int), s));
   HIPCHK(launch_rs_bucket(a.wave_buf, a.wave_cap, a.wave_cnt, n_waves, (int)nq, ws.cand_off.as<int64_t>(),
                           ws.cand_key.as<float>(), ws.cand_pos.as<int>(), ws.rs_bucket_tmp.p, a.wave_cnt + n_waves,
                           4 * cu_count(idx->device), s));

@@ -242,6 +242,8 @@ struct RsScanArgs {
   int4* wave_buf;            // [grid * kRsWaves][wave_cap] per-wave candidate streams {key bits, pos, query, 0}
   int wave_cap;
   int* wave_cnt;             // [grid * kRsWaves] stream lengths (may exceed wave_cap: entries lost)
+  int* queue;                // [8] per-queue item counters, zero at launch (dynamic dealing)
+  const int* bounds;         // [9] the queues' item ranges by tile work (k_rs_bounds); null: equal item counts
   int flags;                 // timing experiments only (MIVS_RS_FLAGS): 1 skip epilogue, 2 skip staging,
                              // 8 per-block clocks into prof
   unsigned long long* prof;  // flags & 8: [grid][3] {start, end, tiles}
@@ -344,7 +346,7 @@ hipError_t launch_rs_bucket(const int4* wave_buf, int wave_cap, const int* wave_
 hipError_t launch_rs_pre_lists(const int64_t* goff, int n_lists, int div, int min_groups, const int64_t* probes,
                                int64_t nq, int np, int64_t* goff2, int64_t* probes2, hipStream_t s);
 hipError_t launch_rs_items(const int* work_off, const int* bucket_off, const int64_t* list_goff, int n_lists,
-                           int max_items, int4* items, hipStream_t s);
+                           int max_items, int4* items, int* bounds, hipStream_t s);
 hipError_t launch_rs_tiles(const int64_t* bucket_q, const int* bucket_off, int n_lists, const uint16_t* qh,
                            const float4* qhdr, int nq, int dp, char* tiles, hipStream_t s);
 hipError_t launch_rs_headers(const float* pre_kth, int64_t nq, const float* qscale, const float* qnorms,

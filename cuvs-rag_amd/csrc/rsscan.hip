@@ -189,14 +189,27 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   const int j = lane & 31;
   const int kq = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // static, XCD-aware schedule: queue x (= blockIdx % 8, the XCD under round-robin placement; speed only)
-  // holds the x-th eighth of the list-ordered items and its P workgroups take every P-th item, so the
-  // CUs of an XCD work through the blocks of the same lists together (the lists' query tiles stay in
-  // that XCD's L2). Every item belongs to exactly one (queue, workgroup) whatever the placement.
+  // XCD-aware schedule: queue x (= blockIdx % 8, the XCD under round-robin placement; speed only) holds
+  // the x-th eighth of the list-ordered items, so the CUs of an XCD work through the blocks of the same
+  // lists together (the lists' query tiles stay in that XCD's L2). Its P workgroups take the first P
+  // items, then deal the rest dynamically from the queue's counter (a.queue[x]): a static deal left the
+  // last workgroup 6.6 % behind the mean (phase clocks: busy mean 5.03 ms, max 5.36 ms). Lane 0 of
+  // wave 0 grabs three items ahead into an LDS ring (s_next): grabbed during item j's first tile (after
+  // its wait, published before its signal), an index is read at the start of item j + 2, when every
+  // wave has seen that signal -- every item has at least one tile. Every item is taken exactly once
+  // (indices past the queue's end read as -1, and once -1 always -1).
   const int total = __builtin_amdgcn_readfirstlane(a.work_off[a.n_lists]);
   const int x = blockIdx.x & 7, P = gridDim.x >> 3;
-  const int hi = (int)((int64_t)total * (x + 1) / 8);
-  int w = (int)((int64_t)total * x / 8) + (int)(blockIdx.x >> 3);
+  const int hi = a.bounds ? __builtin_amdgcn_readfirstlane(a.bounds[x + 1]) : (int)((int64_t)total * (x + 1) / 8);
+  const int lo_x = a.bounds ? __builtin_amdgcn_readfirstlane(a.bounds[x]) : (int)((int64_t)total * x / 8);
+  int w = lo_x + (int)(blockIdx.x >> 3);
+  const int w0 = w;
+  int* const s_next = s_ready + 4;  // [4] ring of upcoming item indices
+  auto grab = [&](int ord) {  // this workgroup's item of ordinal ord (a.queue null: the static deal)
+    const int v = a.queue ? lo_x + P + atomicAdd(a.queue + x, 1) : w0 + ord * P;
+    return v < hi ? v : -1;
+  };
+  int ii = 0;  // this workgroup's item ordinal
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
   int n_tiles_done = 0;
   int tt = 0;               // tiles this wave has started
@@ -247,7 +260,11 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
     dma_b32(uniform_desc(a.row_norms + (int64_t)grp * kGroupRows, kGroupRows * 4), s_norm + (ip * kRsWaves + wave) * 64,
             j * 4);
   };
-  if (tid == 0) *s_ready = 0;
+  if (tid == 0) {
+    *s_ready = 0;
+    s_next[1] = grab(1);
+    s_next[2] = grab(2);
+  }
   __syncthreads();  // (the only workgroup barrier: the counter is zero before any wave signals)
   {  // tile 0's pieces
     const v4i d0 = uniform_desc(a.tiles + it.slot * IMG, (int)IMG);
@@ -269,8 +286,8 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
 
   for (;;) {
     const int ntiles = it.ntiles;
-    const int wn = w + P;
-    const bool has_next = wn < hi;
+    const int wn = s_next[(ii + 1) & 3];
+    const bool has_next = wn >= 0;
     RsItem nx = it;
     if (has_next) nx = rs_item(a, wn);  // (retired by the first tile's wait, long before its use)
     const int gnx = nx.g0 + wave;
@@ -347,6 +364,9 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
       // every wave's pieces of this tile have landed and every wave is done with the previous tile
       if (!spun_out && !rs_spin(s_ready, kRsWaves * (tt + 1))) spun_out = true;
       ++tt;
+      const bool grabber = t == 0 && wave == 0 && lane == 0;
+      int grabbed = -1;
+      if (grabber) grabbed = grab(ii + 3);  // (its result is waited for at the signal below)
       const uint64_t ph1 = (a.flags & 16) ? __builtin_amdgcn_s_memtime() : 0;
       const bool last = LAST;
       // the next tile (of this item, or the next item's first) goes into the next buffer. Its pieces are
@@ -409,6 +429,7 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
       // its DMA pieces of the next have landed -- vmcnt counts, in issue order, only the next item's rows
       // issued after its last piece beyond them
       rs_wait_vm(LAST && has_next ? ROWS_AFTER : 0);
+      if (grabber) s_next[(ii + 3) & 3] = grabbed;
       rs_signal(s_ready);
       const uint64_t ph2b = (a.flags & 16) ? __builtin_amdgcn_s_memtime() : 0;
       uint64_t ph2c = ph2b, ph2d = 0;
@@ -443,6 +464,7 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
     tile(ntiles - 1, BoolC<true>{});
     n_tiles_done += ntiles;
     if (!has_next) break;
+    ++ii;
     w = wn;
     it = nx;
     g = gnx;
@@ -467,6 +489,58 @@ __global__ void k_rs_items(const int* __restrict__ work_off, const int* __restri
   const int64_t ge = list_goff[lo + 1] < g0 + kRsBlockGroups ? list_goff[lo + 1] : g0 + kRsBlockGroups;
   const int m = bucket_off[lo + 1] - bucket_off[lo];
   items[w] = make_int4((int)g0, (int)ge, (int)rs_tile_slot(bucket_off, lo, 0), (m + kRsQTile - 1) / kRsQTile);
+}
+
+// The 8 item queues of K13 as ranges of equal TILE work (bounds [9]): an item costs its list's tile count,
+// and lists differ in queries, so equal item counts left one queue ~3 % heavier than the mean. Item
+// weights are uniform inside a list: queue x starts at the first item whose work prefix reaches
+// W x / 8 (W = all items' tiles).
+__global__ __launch_bounds__(1024) void k_rs_bounds(const int* __restrict__ work_off, const int* __restrict__ bucket_off,
+                                                    int n_lists, int* __restrict__ bounds) {
+  __shared__ int64_t sh[16];
+  __shared__ int64_t s_total;
+  // pass 1: W
+  int64_t tot = 0;
+  for (int l0 = 0; l0 < n_lists; l0 += 1024) {
+    const int l = l0 + threadIdx.x;
+    int64_t wl = 0;
+    if (l < n_lists)
+      wl = (int64_t)(work_off[l + 1] - work_off[l]) * ((bucket_off[l + 1] - bucket_off[l] + kRsQTile - 1) / kRsQTile);
+    int64_t t;
+    block_excl_scan(wl, sh, &t);
+    tot += t;
+  }
+  if (threadIdx.x == 0) s_total = tot;
+  __syncthreads();
+  const int64_t W = s_total;
+  const int n_items = work_off[n_lists];
+  if (W == 0) {  // nothing to weigh: equal item counts
+    if (threadIdx.x <= 8) bounds[threadIdx.x] = (int)((int64_t)n_items * threadIdx.x / 8);
+    return;
+  }
+  if (threadIdx.x == 0) { bounds[0] = 0; bounds[8] = n_items; }
+  // pass 2: the list holding each target W x / 8 (x = 1..7) sets bounds[x]
+  int64_t cum = 0;
+  for (int l0 = 0; l0 < n_lists; l0 += 1024) {
+    const int l = l0 + threadIdx.x;
+    int64_t wl = 0, nt = 1;
+    if (l < n_lists) {
+      nt = (bucket_off[l + 1] - bucket_off[l] + kRsQTile - 1) / kRsQTile;
+      wl = (int64_t)(work_off[l + 1] - work_off[l]) * nt;
+    }
+    int64_t t;
+    const int64_t c = cum + block_excl_scan(wl, sh, &t);
+    if (wl > 0) {
+      for (int x = 1; x < 8; ++x) {
+        const int64_t target = W * x / 8;
+        if (target >= c && target < c + wl) {
+          const int64_t b = work_off[l] + (target - c + nt - 1) / nt;
+          bounds[x] = (int)(b < work_off[l + 1] ? b : work_off[l + 1]);
+        }
+      }
+    }
+    cum += t;
+  }
 }
 
 // per query: {qs, uf, qn, q} for K13 (uf carries T_q: the one-fma filter bound for the exact k-th key over the
@@ -539,8 +613,8 @@ __global__ __launch_bounds__(1024) void k_rs_tiles(const int64_t* __restrict__ b
 
 size_t rs_scan_lds_bytes(int dp) {
   const int nk = dp / 16;
-  // two tile buffers + the norms ([2 items][8 waves][64]) + the tiles-ready counter
-  return (size_t)2 * (nk * 1024 + 1024) + 2 * kRsWaves * 64 * sizeof(float) + 16;
+  // two tile buffers + the norms ([2 items][8 waves][64]) + the tiles-ready counter and the item ring
+  return (size_t)2 * (nk * 1024 + 1024) + 2 * kRsWaves * 64 * sizeof(float) + 64;
 }
 
 bool rs_scan_supported(int dp) {
@@ -604,10 +678,11 @@ hipError_t launch_rs_tiles(const int64_t* bucket_q, const int* bucket_off, int n
 }
 
 hipError_t launch_rs_items(const int* work_off, const int* bucket_off, const int64_t* list_goff, int n_lists,
-                           int max_items, int4* items, hipStream_t s) {
+                           int max_items, int4* items, int* bounds, hipStream_t s) {
   if (max_items <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_rs_items, dim3((unsigned)ceil_div(max_items, 256)), dim3(256), 0, s, work_off, bucket_off,
                      list_goff, n_lists, max_items, items);
+  if (bounds) hipLaunchKernelGGL(k_rs_bounds, dim3(1), dim3(1024), 0, s, work_off, bucket_off, n_lists, bounds);
   return hipGetLastError();
 }
 

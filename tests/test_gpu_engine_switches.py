@@ -63,6 +63,7 @@ SEARCH_SWITCHES = [
     {"MIVS_RS_PRE_DIV": "1"},
     {"MIVS_RS_PRE_DIV": "16"},
     {"MIVS_RS_BUCKET_FLAT": "1"},                                     # K13 streams bucketed by flat atomics
+    {"MIVS_RS_STATIC_DEAL": "1"},                                     # K13 items dealt statically
     {"MIVS_RS_FLAGS": "24"},                                          # K13 clocks (stderr only)
     {"MIVS_PF_ROWSTAT": "0", "MIVS_PF_FLAGS": "32"},                  # K10 phase clocks (stderr only)
 ]
