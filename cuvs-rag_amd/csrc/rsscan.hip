@@ -197,7 +197,7 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   // wave 0 grabs three items ahead into an LDS ring (s_next): grabbed during item j's first tile (after
   // its wait, published before its signal), an index is read at the start of item j + 2, when every
   // wave has seen that signal -- every item has at least one tile. Every item is taken exactly once
-  // (indices past the queue's end read as -1, and once -1 always -1).
+  // (indices past the queues' ends read as -1, and once -1 always -1).
   const int total = __builtin_amdgcn_readfirstlane(a.work_off[a.n_lists]);
   const int x = blockIdx.x & 7, P = gridDim.x >> 3;
   const int hi = a.bounds ? __builtin_amdgcn_readfirstlane(a.bounds[x + 1]) : (int)((int64_t)total * (x + 1) / 8);
@@ -205,9 +205,22 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   int w = lo_x + (int)(blockIdx.x >> 3);
   const int w0 = w;
   int* const s_next = s_ready + 4;  // [4] ring of upcoming item indices
-  auto grab = [&](int ord) {  // this workgroup's item of ordinal ord (a.queue null: the static deal)
-    const int v = a.queue ? lo_x + P + atomicAdd(a.queue + x, 1) : w0 + ord * P;
-    return v < hi ? v : -1;
+  // this workgroup's item of ordinal ord (a.queue null: the static deal); once its own queue is dry it
+  // takes items from the other queues in turn (the tail of a launch), so no CU idles while any item is left
+  auto grab = [&](int ord) {
+    if (!a.queue) {
+      const int v = w0 + ord * P;
+      return v < hi ? v : -1;
+    }
+    int v = lo_x + P + atomicAdd(a.queue + x, 1);
+    if (v < hi) return v;
+    if (a.bounds)
+      for (int k = 1; k < 8; ++k) {
+        const int xq = (x + k) & 7;
+        v = a.bounds[xq] + P + atomicAdd(a.queue + xq, 1);
+        if (v < a.bounds[xq + 1]) return v;
+      }
+    return -1;
   };
   int ii = 0;  // this workgroup's item ordinal
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
