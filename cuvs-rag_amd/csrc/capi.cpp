@@ -87,7 +87,7 @@ struct Workspace {
   // fp16 pre-filter path (K10 / K11) and its exact-scan fallback
   Buf qh, qscale, qres, qtheta, pf_key, pf_pos, pf_bound, pf_stats, ovf_q, ovf_rows, ovf_d, ovf_i;
   // K13 row-stationary scan: the full probe list, the pre-pass result, per-query headers and candidates
-  Buf probes_full, pre_kth, pre_goff, qhdr, cand_off, cand_key, cand_pos, rs_bucket_tmp, rs_tiles, rs_wave_buf,
+  Buf probes_full, pre_kth, pre_goff, qhdr, rs_tq, cand_off, cand_key, cand_pos, rs_bucket_tmp, rs_tiles, rs_wave_buf,
       rs_wave_cnt, rs_bounds;
   // per-list query counts of the last search's own probe map (an exact fallback re-maps its queries)
   Buf stat_counts, rs_ovf_q, rs_ovf_rows, rs_ovf_d, rs_ovf_i, rs_items;
@@ -131,6 +131,7 @@ struct mivs_index_s {
   Buf pq_codes, pq_books;
   // fp16 copy of the lists for the K10 pre-filter; empty = exact scan only
   Buf groups_h;
+  Buf group_nmin;  // K13: the smallest row norm of every 32-row group (built with groups_h)
   int hx_exp = 0;
   float x_norm_max = 0.0f, x_res_max = 0.0f;
   int pf_G = kPfChunkGroups;                  // groups per K10 work item
@@ -146,6 +147,7 @@ struct mivs_index_s {
   int last_pf = 0;
   int last_scan = 0;  // fine-scan kernel of the last search: 3 K3, 31 K3w, 10 K10, 12 K12, 13 K13
   int last_rs_waves = 0;  // K13: candidate streams of the last search (the lost flag follows their counts)
+  int64_t last_rs_nq = 0; // K13: queries of the last search batch (its cand_off holds last_rs_nq + 1 offsets)
   int64_t last_ovf = 0, last_window = 0;
 };
 
@@ -532,10 +534,14 @@ void assign_rows(const float* data, const float* data_norms, const int64_t* rows
 }
 
 // n_iters Lloyd iterations on trainset rows; centroids_rm in/out [nc][d]
+// iterations it_begin .. it_begin + iters - 1 of a Lloyd run of it_total iterations (-1: iters); the balancing
+// step runs on all but the run's last kBalanceKeepLast. labels_out: the last iteration's assignment.
 void kmeans_fit_impl(const float* data, const float* data_norms, const int64_t* rows, int64_t n_train, int d, int dp,
                      int nc, int iters, float* centroids_rm, int G, int device, Workspace& ws, hipStream_t s,
-                     bool balance = false, const PfAssign* pfa = nullptr) {
+                     bool balance = false, const PfAssign* pfa = nullptr, int it_begin = 0, int it_total = -1,
+                     int64_t* labels_out = nullptr) {
   if (iters <= 0) return;
+  if (it_total < 0) it_total = it_begin + iters;
   Buf labels, perm, off, partial, chunk_off, tmp, ctmp;
   labels.reserve(sizeof(int64_t) * n_train);
   perm.reserve(sizeof(int64_t) * n_train);
@@ -545,15 +551,17 @@ void kmeans_fit_impl(const float* data, const float* data_norms, const int64_t* 
   tmp.reserve(sizeof(int64_t) * (nc + 1) + scan_tmp_bytes(nc + 1));
   const size_t cb = csort_tmp_bytes(n_train, nc);
   ctmp.reserve(cb);
-  for (int it = 0; it < iters; ++it) {
+  for (int it = it_begin; it < it_begin + iters; ++it) {
     ListSet cents;
     make_single_list(cents, centroids_rm, nc, d, dp, 0, G, s);
     assign_rows(data, data_norms, rows, n_train, d, dp, cents, G, kL2, labels.as<int64_t>(), device, ws, s, pfa);
+    if (labels_out && it == it_begin + iters - 1)
+      HIPCHK(hipMemcpyAsync(labels_out, labels.p, sizeof(int64_t) * n_train, hipMemcpyDeviceToDevice, s));
     HIPCHK(launch_counting_sort(labels.as<int64_t>(), n_train, nc, perm.as<int64_t>(), off.as<int64_t>(), ctmp.p,
                                 cb, s));
     HIPCHK(launch_km_update(data, d, rows, perm.as<int64_t>(), off.as<int64_t>(), nc, n_train,
                             partial.as<double>(), chunk_off.as<int64_t>(), tmp.p, centroids_rm, s));
-    if (balance && it < iters - kBalanceKeepLast)
+    if (balance && it < it_total - kBalanceKeepLast)
       HIPCHK(launch_km_rebalance(data, d, rows, labels.as<int64_t>(), off.as<int64_t>(), nc, n_train, it,
                                  centroids_rm, s));
   }
@@ -621,6 +629,8 @@ void pf_enable(mivs_index_s* idx, hipStream_t s) {
   std::memcpy(&normmax, &h[1], 4);
   idx->hx_exp = pf_hx_exp(absmax);
   idx->groups_h.reserve(sizeof(uint16_t) * (size_t)nslot * idx->dp);
+  idx->group_nmin.reserve(sizeof(float) * (size_t)L.n_groups);
+  HIPCHK(launch_group_nmin(L.norms.as<float>(), L.n_groups, idx->group_nmin.as<float>(), s));
   HIPCHK(launch_groups_to_half(L.groups.as<float>(), L.n_groups, idx->dp, idx->hx_exp, idx->groups_h.as<uint16_t>(),
                                st.as<unsigned>() + 2, s));
   HIPCHK(hipMemcpyAsync(&h[2], st.as<unsigned>() + 2, sizeof(unsigned), hipMemcpyDeviceToHost, s));
@@ -665,7 +675,7 @@ void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t
 void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                         int64_t* out_i, const float* slot_key, const int* slot_pos, const float* slot_bound,
                         const int* force_ovf, const int64_t* slot_begin, int slot_k, bool fallback_pf = false,
-                        float* kth_out = nullptr);
+                        float* kth_out = nullptr, const float* window_cap = nullptr);
 
 // K10 scan + K11 refine for a probe map built with (kPfChunkGroups, kPfQTile); queries the refine
 // could not prove are re-run through the exact scan and scattered back.
@@ -764,7 +774,7 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
 void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                         int64_t* out_i, const float* slot_key, const int* slot_pos, const float* slot_bound,
                         const int* force_ovf, const int64_t* slot_begin, int slot_k, bool fallback_pf,
-                        float* kth_out) {
+                        float* kth_out, const float* window_cap) {
   Workspace& ws = idx->ws;
   const ListSet& L = idx->lists;
   const int dp = idx->dp;
@@ -776,6 +786,7 @@ void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_
   r.slot_pos = slot_pos;
   r.slot_bound = slot_bound;
   r.force_ovf = force_ovf;
+  r.window_cap = window_cap;
   r.kth_out = kth_out;
   r.slot_begin = slot_begin;
   r.slot_k = slot_k;
@@ -882,6 +893,15 @@ bool rs_use(const mivs_index_s* idx, int np) {
   return idx->kind == 0 && np >= 2 && rs_scan_supported(idx->dp) && !(e && e[0] == '0');
 }
 
+// records per K13 stream: twice the batch's queries, at most kRsWaveCapMax (MIVS_RS_WAVE_CAP overrides it: the
+// lost-stream path is then testable at small sizes). Batches are at most kRsMaxBatch queries (ivf_search_impl),
+// so a stream's mean length (~160 records per 1,000 queries at the benchmark shape) stays far below the cap.
+int rs_wave_cap(int64_t nq) {
+  const char* e = getenv("MIVS_RS_WAVE_CAP");
+  if (e && atoi(e) > 0) return atoi(e);
+  return (int)std::min<int64_t>(kRsWaveCapMax, std::max<int64_t>(1024, 2 * nq));
+}
+
 // The K13 search of queries whose probes are in ws.probes_i and norms in ws.qn:
 //   1. pre-pass: each query's nearest list through K10 + K11 -> the exact k-th key there;
 //   2. per-query header {qs, uf, qn, q}: uf is the filter bound for T_q >= the final refine window;
@@ -926,8 +946,10 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   }
   // 2. headers (pf_scan_refine left the fp16 queries, their scales and residuals in ws.qh / qscale / qres)
   ws.qhdr.reserve(sizeof(float4) * (nq + 1));
+  ws.rs_tq.reserve(sizeof(float) * nq);
   HIPCHK(launch_rs_headers(ws.pre_kth.as<float>(), nq, ws.qscale.as<float>(), ws.qn.as<float>(), ws.qres.as<float>(),
-                           idx->x_norm_max, idx->x_res_max, dp, idx->metric, ws.qhdr.as<float4>(), s));
+                           idx->x_norm_max, idx->x_res_max, dp, idx->metric, ws.qhdr.as<float4>(), ws.rs_tq.as<float>(),
+                           s));
   // 3. probe map: items = (list, block of kRsBlockGroups groups); every query of a list in one tile column
   const size_t stb = scan_tmp_bytes(ne) + sizeof(int64_t) * (size_t)ne;
   ws.scan_tmp.reserve(stb);
@@ -965,32 +987,36 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   a.items = ws.rs_items.as<int4>();
   a.tiles = ws.rs_tiles.as<char>();
   a.qnorms = ws.qn.as<float>();
+  a.group_nmin = idx->group_nmin.as<float>();
   a.nq = (int)nq;
   a.metric = idx->metric;
   const int grid = std::max(8, cu_count(idx->device) / 8 * 8);
   const int n_waves = grid * kRsWaves;
   idx->last_rs_waves = n_waves;
-  a.wave_cap = (int)std::min<int64_t>(kRsWaveCapMax, std::max<int64_t>(1024, 2 * nq));
-  ws.rs_wave_buf.reserve(sizeof(int4) * (size_t)n_waves * a.wave_cap);
-  ws.rs_wave_cnt.reserve(sizeof(int) * (n_waves + 1 + 8));  // + the lost flag, the 8 item-queue counters
+  idx->last_rs_nq = nq;
+  a.wave_cap = rs_wave_cap(nq);
+  ws.rs_wave_buf.reserve(sizeof(int4) * kRsRecInt4 * (size_t)n_waves * a.wave_cap);
+  // + the lost flag, the 8 item-queue counters, the spun-out wave count
+  ws.rs_wave_cnt.reserve(sizeof(int) * (n_waves + 1 + 8 + 1));
   a.wave_buf = ws.rs_wave_buf.as<int4>();
   a.wave_cnt = ws.rs_wave_cnt.as<int>();
   a.queue = static_deal ? nullptr : a.wave_cnt + n_waves + 1;
   a.bounds = static_deal ? nullptr : ws.rs_bounds.as<int>();
-  HIPCHK(hipMemsetAsync(a.wave_cnt + n_waves, 0, sizeof(int) * 9, s));  // lost flag + queue counters
+  HIPCHK(hipMemsetAsync(a.wave_cnt + n_waves, 0, sizeof(int) * 10, s));  // lost flag, queue counters, spun-out
   a.flags = getenv("MIVS_RS_FLAGS") ? atoi(getenv("MIVS_RS_FLAGS")) : 0;
   if (a.flags & 2) a.flags |= 1;  // stale LDS tiles: never run an epilogue on them
+  if (getenv("MIVS_RS_ROWWAIT") && getenv("MIVS_RS_ROWWAIT")[0] == '1') a.flags |= 32;  // one vmcnt(0) per item
   Buf pbuf;
   if (a.flags & 24) {  // diagnostic: per-block clocks (8) / per-phase wave-cycles (16) to stderr
-    pbuf.reserve(sizeof(unsigned long long) * (3 * grid + 8));
-    HIPCHK(hipMemsetAsync(pbuf.p, 0, sizeof(unsigned long long) * (3 * grid + 8), s));
+    pbuf.reserve(sizeof(unsigned long long) * (3 * grid + 16));
+    HIPCHK(hipMemsetAsync(pbuf.p, 0, sizeof(unsigned long long) * (3 * grid + 16), s));
     a.prof = pbuf.as<unsigned long long>();
   }
   if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
   HIPCHK(launch_rs_scan(a, dp, grid, s));
   if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
   if (a.flags & 24) {
-    std::vector<unsigned long long> h(3 * (size_t)grid + 8);
+    std::vector<unsigned long long> h(3 * (size_t)grid + 16);
     HIPCHK(hipMemcpyAsync(h.data(), pbuf.p, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     unsigned long long t0 = ~0ull, t1 = 0, tiles_max = 0, tiles_sum = 0;
@@ -1016,19 +1042,24 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
       fprintf(stderr, "[k13 phases] mfma-result-wait %.3f (in epilogue: hit path %.3f) | wave-tiles taking the hit path "
               "%.4f of %llu\n", h[3 * grid + 4] / wc, h[3 * grid + 5] / wc,
               h[3 * grid + 7] ? (double)h[3 * grid + 6] / (double)h[3 * grid + 7] : 0.0, h[3 * grid + 7]);
+    if (wc > 0 && h[3 * grid + 9] && h[3 * grid + 7] > h[3 * grid + 9])
+      fprintf(stderr, "[k13 phases] k-loop cycles: items' first tile %.0f, other tiles %.0f | wave lifetime %.4g cycles "
+              "(tile phases %.3f of it)\n", (double)h[3 * grid + 8] / h[3 * grid + 9],
+              (double)(h[3 * grid + 1] - h[3 * grid + 8]) / (double)(h[3 * grid + 7] - h[3 * grid + 9]),
+              (double)h[3 * grid + 10], wc / (double)h[3 * grid + 10]);
   }
-  // the streams into per-query CSR runs (every stream entry fits: at most n_waves * wave_cap of them)
-  const size_t max_cand = (size_t)n_waves * a.wave_cap;
+  // the streams into per-query CSR runs (a record expands to at most 8 candidates)
+  const size_t max_cand = (size_t)n_waves * a.wave_cap * 8;
   ws.cand_off.reserve(sizeof(int64_t) * (nq + 1));
   ws.cand_key.reserve(sizeof(float) * max_cand);
   ws.cand_pos.reserve(sizeof(int) * max_cand);
   ws.rs_bucket_tmp.reserve(rs_bucket_tmp_bytes((int)nq, n_waves));
-  HIPCHK(launch_rs_bucket(a.wave_buf, a.wave_cap, a.wave_cnt, n_waves, (int)nq, ws.cand_off.as<int64_t>(),
-                          ws.cand_key.as<float>(), ws.cand_pos.as<int>(), ws.rs_bucket_tmp.p, a.wave_cnt + n_waves,
-                          4 * cu_count(idx->device), s));
-  // 5. exact ranking of every query's run (slot = one entry)
+  HIPCHK(launch_rs_bucket(a.wave_buf, a.wave_cap, a.wave_cnt, n_waves, (int)nq, ws.qhdr.as<float4>(), a.row_norms,
+                          idx->metric, ws.cand_off.as<int64_t>(), ws.cand_key.as<float>(), ws.cand_pos.as<int>(),
+                          ws.rs_bucket_tmp.p, a.wave_cnt + n_waves, 4 * cu_count(idx->device), s));
+  // 5. exact ranking of every query's run (slot = one entry); a window above T_q is not proven
   pf_refine_fallback(idx, s, q, nq, k, np, out_d, out_i, ws.cand_key.as<float>(), ws.cand_pos.as<int>(), nullptr,
-                     a.wave_cnt + n_waves, ws.cand_off.as<int64_t>(), 1, true);
+                     a.wave_cnt + n_waves, ws.cand_off.as<int64_t>(), 1, true, nullptr, ws.rs_tq.as<float>());
 }
 
 void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
@@ -1233,15 +1264,18 @@ void ivf_search_impl(mivs_index_s* idx, hipStream_t s, const float* q, int64_t n
     const ListSet& L = idx->lists;
     const int64_t per_q_slots = std::max<int64_t>(1, L.top_chunks_prefix[std::min<int64_t>(np, L.n_lists)]);
     qb = select_batch(nq, (size_t)per_q_slots * ((size_t)idx->G * kGroupRows * 4 + 16));
+  } else if (idx->groups_h.p != nullptr && k <= kPfMaxK && rs_use(idx, np)) {
+    qb = std::min<int64_t>(nq, kRsMaxBatch);  // K13: bounded record streams and LDS-histogram bucketing
   }
   idx->last_ovf = 0;
   idx->last_window = 0;
+  int64_t nb = 0;
   for (int64_t b0 = 0; b0 < nq; b0 += qb) {
-    const int64_t nb = std::min<int64_t>(qb, nq - b0);
+    nb = std::min<int64_t>(qb, nq - b0);
     ivf_search_batch(idx, s, q + b0 * (int64_t)idx->d, nb, k, np, out_d + b0 * k, out_i + b0 * k,
                      out_probes ? out_probes + b0 * np : nullptr);
   }
-  idx->last_nq = nq;
+  idx->last_nq = nb;  // (the stats describe the last batch)
   idx->last_np = np;
   idx->last_k = k;
 }
@@ -2028,12 +2062,13 @@ int32_t mivs_index_last_search_stats(mivs_index_t idx, mivs_search_stats* out) {
           if (counts[l] > 0) st.work_items += ceil_div(L.h_goff[l + 1] - L.h_goff[l], kRsBlockGroups);
         // the candidates K13 appended; a lost stream entry sends every query to the fallback
         int64_t total = 0;
-        int lost = 0;
-        HIPCHK(hipMemcpy(&total, idx->ws.cand_off.as<int64_t>() + idx->last_nq, sizeof(int64_t),
+        int lost[10] = {};
+        HIPCHK(hipMemcpy(&total, idx->ws.cand_off.as<int64_t>() + idx->last_rs_nq, sizeof(int64_t),
                          hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(&lost, idx->ws.rs_wave_cnt.as<int>() + idx->last_rs_waves, sizeof(int), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(lost, idx->ws.rs_wave_cnt.as<int>() + idx->last_rs_waves, sizeof(lost), hipMemcpyDeviceToHost));
         st.candidates = total;
-        st.cand_overflow = lost ? idx->last_nq : 0;
+        st.spun_out_waves = lost[9];
+        st.cand_overflow = lost[0] && !lost[9] ? idx->last_rs_nq : 0;
       }
     } else if (idx->last_nq > 0) {
       // brute force: the pre-filter scan (K10) works in pf_G-group chunks, the exact scans in G
@@ -2121,6 +2156,28 @@ int32_t mivs_kmeans_fit(int32_t device, void* stream, const float* d_data, int64
     HIPCHK(launch_row_norms(d_data, n, dim, norms.as<float>(), s));
     kmeans_fit_impl(d_data, norms.as<float>(), d_rows, n_train, dim, dim_pad(dim), n_clusters, n_iters, d_centroids,
                     kDefaultChunkGroups, device, ws, s);
+  });
+}
+
+int32_t mivs_kmeans_steps(int32_t device, void* stream, const float* d_data, int64_t n, int32_t dim,
+                          const int64_t* d_rows, int64_t n_train, int32_t n_clusters, int32_t it_begin, int32_t n_steps,
+                          int32_t it_total, int32_t balance, float* d_centroids, int64_t* d_labels) {
+  return guarded([&] {
+    check_common(device, d_data, n, dim);
+    require(n_clusters >= 1 && n_clusters <= 32768, "n_clusters must be in [1, 32768]");
+    require(n_train >= 1 && (d_rows != nullptr || n_train <= n), "bad trainset");
+    require(it_begin >= 0 && n_steps >= 0 && it_total >= it_begin + n_steps, "bad iteration range");
+    if (n_steps == 0) return;
+    DeviceGuard dg(device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    Workspace ws;
+    Buf norms;
+    norms.reserve(sizeof(float) * std::max<int64_t>(n, 1));
+    HIPCHK(launch_row_norms(d_data, n, dim, norms.as<float>(), s));
+    PfAssign pfa;  // the assign of the IVF build, as ivf_flat_build runs it
+    pf_assign_prepare(pfa, d_data, n, dim, dim_pad(dim), s);
+    kmeans_fit_impl(d_data, norms.as<float>(), d_rows, n_train, dim, dim_pad(dim), n_clusters, n_steps, d_centroids,
+                    kDefaultChunkGroups, device, ws, s, balance != 0, &pfa, it_begin, it_total, d_labels);
   });
 }
 

@@ -224,7 +224,9 @@ constexpr int kRsQTile = 32;
 constexpr int kRsBlockGroups = kRsWaves;
 // K13's pre-pass scans the first 1 / kRsPreDiv of each query's nearest list (MIVS_RS_PRE_DIV)
 constexpr int kRsPreDiv = 4;
-constexpr int kRsWaveCapMax = 16384;  // entries of a K13 wave's candidate stream (more: all queries fall back)
+constexpr int kRsWaveCapMax = 16384;  // records of a K13 wave's candidate stream (more: all queries fall back)
+constexpr int kRsRecInt4 = 3;         // a record: 8 dots of one lane and query half + {first row position, query}
+constexpr int kRsMaxBatch = 32768;    // queries per K13 search batch (the LDS-histogram bucketing's bins)
 
 struct RsScanArgs {
   const uint16_t* groups_h;  // fp16 lists, group layout [g][dp/8][32][8]
@@ -239,9 +241,10 @@ struct RsScanArgs {
   const float* qnorms;       // [nq] pinned fp32 query norms (exact key of a candidate)
   int nq;
   int metric;
-  int4* wave_buf;            // [grid * kRsWaves][wave_cap] per-wave candidate streams {key bits, pos, query, 0}
-  int wave_cap;
-  int* wave_cnt;             // [grid * kRsWaves] stream lengths (may exceed wave_cap: entries lost)
+  const float* group_nmin;   // [groups] the smallest row norm of each group (L2 filter bound)
+  int4* wave_buf;            // [grid * kRsWaves][wave_cap][kRsRecInt4] per-wave record streams
+  int wave_cap;              // records per stream
+  int* wave_cnt;             // [grid * kRsWaves] stream lengths (may exceed wave_cap: records lost)
   int* queue;                // [8] per-queue item counters, zero at launch (dynamic dealing)
   const int* bounds;         // [9] the queues' item ranges by tile work (k_rs_bounds); null: equal item counts
   int flags;                 // timing experiments only (MIVS_RS_FLAGS): 1 skip epilogue, 2 skip staging,
@@ -289,6 +292,7 @@ struct PfRefineArgs {
   int labels_only;            // k = 1: a window of ONE candidate is the answer without its exact key
                               // (out_d then holds its approximate key)
   const int* force_ovf;       // optional (K13): nonzero -> no query is provable (candidates were lost)
+  const float* window_cap;    // optional (K13): [nq] T_q -- a query whose window exceeds it is not proven
   float* kth_out;             // optional (K13's pre-pass): only the k-th smallest approximate key per query
                               // (+inf: fewer than k candidates), no refine
 };
@@ -337,21 +341,24 @@ __device__ inline int64_t block_excl_scan(int64_t v, int64_t* sh, int64_t* tot) 
   return base + x - v;
 }
 
-// K13's per-wave candidate streams -> per-query CSR runs (cand_off [nq + 1]); tmp >= rs_bucket_tmp_bytes;
-// lost: set when a stream overflowed; grid: workgroups of the flat count / scatter
+// K13's per-wave record streams -> per-query CSR runs (cand_off [nq + 1]) of (approximate key, row position);
+// tmp >= rs_bucket_tmp_bytes; lost: set when a stream overflowed; grid: workgroups of the flat count / scatter
 size_t rs_bucket_tmp_bytes(int nq, int n_waves);
 hipError_t launch_rs_bucket(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
-                            int64_t* cand_off, float* cand_key, int* cand_pos, void* tmp, int* lost, int grid,
-                            hipStream_t s);
+                            const float4* qhdr, const float* row_norms, int metric, int64_t* cand_off,
+                            float* cand_key, int* cand_pos, void* tmp, int* lost, int grid, hipStream_t s);
+// per group of 32 rows the smallest row norm (K13's filter bound)
+hipError_t launch_group_nmin(const float* norms, int64_t n_groups, float* out, hipStream_t s);
 hipError_t launch_rs_pre_lists(const int64_t* goff, int n_lists, int div, int min_groups, const int64_t* probes,
                                int64_t nq, int np, int64_t* goff2, int64_t* probes2, hipStream_t s);
 hipError_t launch_rs_items(const int* work_off, const int* bucket_off, const int64_t* list_goff, int n_lists,
                            int max_items, int4* items, int* bounds, hipStream_t s);
 hipError_t launch_rs_tiles(const int64_t* bucket_q, const int* bucket_off, int n_lists, const uint16_t* qh,
                            const float4* qhdr, int nq, int dp, char* tiles, hipStream_t s);
+// tq (optional): T_q per query, the bound K11 checks its final window against
 hipError_t launch_rs_headers(const float* pre_kth, int64_t nq, const float* qscale, const float* qnorms,
                              const float* qres, float x_norm_max, float x_res_max, int dp, int metric, float4* hdr,
-                             hipStream_t s);
+                             float* tq, hipStream_t s);
 hipError_t launch_gather_ids(const int64_t* src, const int64_t* idx, int64_t n, int64_t* out, hipStream_t s);
 constexpr unsigned kPfOrdInf = 0xFF800000u;  // order mapping of +inf (qtheta's initial value)
 // fp32 groups -> fp16 groups scaled by 2^hx_exp (FTZ below the fp16 normal range), per-index maxima of

@@ -613,6 +613,9 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
   const float delta = pf_delta<METRIC>(qn, live ? a.qres[qrow] : 0.0f, a.x_norm_max, a.x_res_max, a.dp);
   const float T = pf_window(tk, delta);  // +inf when fewer than k candidates
   bool ovf = bmin < INFINITY && (bmin <= T || bmin == -INFINITY);
+  // K13: its candidates are every row whose approximate key is <= T_q (a superset); the window is complete
+  // only if it lies below T_q, which the analysis of T_q guarantees -- checked here, not assumed
+  if (live && a.window_cap && !(T <= a.window_cap[q])) ovf = true;
 
   // phase 2: collect the window (ballot prefix, no atomics)
   int cnt = 0;

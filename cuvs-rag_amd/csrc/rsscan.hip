@@ -17,9 +17,13 @@
 //   * the next item's rows are loaded into the A registers during the item's last tile, each
 //     register right after its last MFMA;
 //   * no per-lane top-k: every query carries a bound T_q from a pre-pass (the exact k-th key over
-//     its nearest list) with T_q >= the refine window of the final answer; the
-//     epilogue appends every (approximate key <= T_q, row) to the query's candidate buffer, and K11
-//     ranks them exactly. Only false positives of the one-fma filter reach the exact test.
+//     its nearest list) with T_q >= the refine window of the final answer. The epilogue
+//     tests, per lane and query half, ONE filter value bounding the lane's 8 rows from below (largest dot,
+//     smallest row norm of the group); a lane that may hold a row with approximate key <= T_q writes its 8
+//     dots as a 48-B record to the wave's stream (ballot positions, no atomics, no per-hit loop). The
+//     bucketing kernels expand the records with the exact per-row filter into per-query candidate runs,
+//     and K11 ranks them exactly. So a wave with hits costs three stores, not a per-hit loop that holds
+//     every other wave at the next tile's ready counter.
 //
 // The result is the pinned fp32 answer (K11 recomputes every window candidate in the oracle's
 // order; queries whose buffer overflows go to the exact scan).
@@ -85,13 +89,6 @@ __device__ __forceinline__ void dma_b128(v4i desc, const void* lds, int voff, in
   const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(lds));
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
                :: "s"(m0), "v"(voff), "s"(desc), "s"(soff) : "memory");
-}
-
-// 64 lanes x 4 B from desc + voff (per lane) to LDS lds + 4 lane
-__device__ __forceinline__ void dma_b32(v4i desc, const void* lds, int voff) {
-  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(lds));
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds"
-               :: "s"(m0), "v"(voff), "s"(desc) : "memory");
 }
 
 
@@ -177,16 +174,12 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
     for (int s = NK / STAGERS + 2; s < NK; ++s) c += (s & 1) ? 2 : 0;
     return c - 2 > 0 ? c - 2 : 0;
   }();
-  // [2 item parities][8 waves][64] row norms of the wave's group (lanes 32..63 repeat 0..31), filled by
-  // LDS-DMA so the next item's are in flight with its rows and nothing waits on them in registers
-  float* s_norm = reinterpret_cast<float*>(smem + NBUF * BUF);
   // tiles-ready counter: every wave adds 1 per tile once it has finished reading the previous tile and its
   // DMA pieces of this one have landed (a sum over waves is a safe test: all of them wait on it, so none is
   // a tile ahead of another when one starts a tile); no workgroup barrier per tile
-  int* s_ready = reinterpret_cast<int*>(smem + NBUF * BUF + 2 * kRsWaves * 64 * sizeof(float));
+  int* s_ready = reinterpret_cast<int*>(smem + NBUF * BUF);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int j = lane & 31;
   const int kq = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // XCD-aware schedule: queue x (= blockIdx % 8, the XCD under round-robin placement; speed only) holds
@@ -205,6 +198,10 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   int w = lo_x + (int)(blockIdx.x >> 3);
   const int w0 = w;
   int* const s_next = s_ready + 4;  // [4] ring of upcoming item indices
+  // [4] their descriptors: the grabber loads item j + 2's during item j's first tile and publishes it with that
+  // tile's signal, so no wave waits on a global load of the item table at an item boundary (it read
+  // items[w] there before: one L2 / HBM round trip, ~4.7k cycles per item and wave)
+  int4* const s_desc = reinterpret_cast<int4*>(s_ready + 8);
   // this workgroup's item of ordinal ord (a.queue null: the static deal); once its own queue is dry it
   // takes items from the other queues in turn (the tail of a launch), so no CU idles while any item is left
   auto grab = [&](int ord) {
@@ -229,12 +226,18 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   bool spun_out = false;    // a wait gave up (never expected): the results are then not trusted
   uint64_t pw_wait = 0, pw_loop = 0, pw_epi = 0, pw_dma = 0;  // flags & 16: this wave's cycles per tile phase
   uint64_t pw_drain = 0, pw_hit = 0, n_hit_tiles = 0;  // flags & 16: MFMA-result wait, hit path, tiles taking it
+  uint64_t pw_first = 0, n_items = 0;  // flags & 16: k-loop cycles of items' first tiles, items
+  const uint64_t pw_t0 = __builtin_amdgcn_s_memtime();
   const int widx = blockIdx.x * kRsWaves + wave;
-  int4* const wstream = a.wave_buf + (int64_t)widx * a.wave_cap;
-  int wcnt = 0;  // entries of this wave's candidate stream
+  int4* const wstream = a.wave_buf + (int64_t)widx * a.wave_cap * kRsRecInt4;
+  int wcnt = 0;  // records of this wave's candidate stream
   auto block_prof = [&]() {
-    // (a wave that gave up waiting reports a lost stream: every query then takes the fallback search)
-    if (lane == 0) a.wave_cnt[widx] = spun_out ? a.wave_cap + 1 : wcnt;
+    // (a wave that gave up waiting reports a lost stream, so every query takes the fallback search, and counts
+    // itself in wave_cnt[waves + 9] so that the stats tell it from a stream overflow)
+    if (lane == 0) {
+      a.wave_cnt[widx] = spun_out ? a.wave_cap + 1 : wcnt;
+      if (spun_out) atomicAdd(a.wave_cnt + gridDim.x * kRsWaves + 9, 1);
+    }
     if ((a.flags & 8) && a.prof && tid == 0) {  // (timing only) flags & 8: per block {start, end, tiles}
       a.prof[3 * blockIdx.x] = t_start;
       a.prof[3 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
@@ -250,6 +253,9 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
       atomicAdd(p + 5, (unsigned long long)pw_hit);
       atomicAdd(p + 6, (unsigned long long)n_hit_tiles);
       atomicAdd(p + 7, (unsigned long long)n_tiles_done);
+      atomicAdd(p + 8, (unsigned long long)pw_first);
+      atomicAdd(p + 9, (unsigned long long)n_items);
+      atomicAdd(p + 10, (unsigned long long)(__builtin_amdgcn_s_memtime() - pw_t0));
     }
   };
   if (w >= hi) {
@@ -269,14 +275,11 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   auto ld_rows = [&](__amdgpu_buffer_rsrc_t r, int i) {  // register i = 2 t + rb
     return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(r, lane_off, (i >> 1) * 2048 + (i & 1) * 256, 0));
   };
-  auto load_norms = [&](int grp, int ip) {
-    dma_b32(uniform_desc(a.row_norms + (int64_t)grp * kGroupRows, kGroupRows * 4), s_norm + (ip * kRsWaves + wave) * 64,
-            j * 4);
-  };
   if (tid == 0) {
     *s_ready = 0;
     s_next[1] = grab(1);
     s_next[2] = grab(2);
+    if (s_next[1] >= 0) s_desc[1] = a.items[s_next[1]];
   }
   __syncthreads();  // (the only workgroup barrier: the counter is zero before any wave signals)
   {  // tile 0's pieces
@@ -285,7 +288,8 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
     for (int p0 = 0; p0 <= NK; p0 += STAGERS)
       if (p0 + wave <= NK) dma_b128(d0, smem + (p0 + wave) * 1024, lane * 16, (p0 + wave) * 1024);
   }
-  load_norms(gv ? g : it.g0, 0);
+  // the smallest row norm of the wave's group (the filter's lower bound; pad rows: +inf, so a real row's)
+  float xn_next = METRIC == kL2 ? a.group_nmin[gv ? g : it.g0] : 0.0f;
   h8 ra[NK];
   {
     const __amdgpu_buffer_rsrc_t r0 = group_rsrc(gv ? g : it.g0);
@@ -294,26 +298,27 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   }
   float xnmin = 0.0f;  // the smallest row norm of the wave's group in the current item
   int cur = 0;         // LDS buffer of the current tile (tt % NBUF)
-  int ipar = 0;        // item parity: the s_norm half of this item
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
 
   for (;;) {
     const int ntiles = it.ntiles;
     const int wn = s_next[(ii + 1) & 3];
     const bool has_next = wn >= 0;
+    // the next item's descriptor: read in this item's LAST tile, after its ready wait (the grabber wrote it
+    // with its signal of the previous item's first tile; an item may have a single tile, so the item start
+    // itself is too early)
     RsItem nx = it;
-    if (has_next) nx = rs_item(a, wn);  // (retired by the first tile's wait, long before its use)
-    const int gnx = nx.g0 + wave;
-    const bool gvn = has_next && gnx < nx.gend;
+    int gnx = 0;
+    bool gvn = false;
     // the filter over one tile's dots; h0 / h1 = the headers {qs, uf, qn, q} of queries c and 16 + c,
-    // read before the wave signalled the tile (after that the buffer may be restaged)
+    // read before the wave signalled the tile (after that the buffer may be restaged). Lane (c, kq) holds the
+    // dots of query 16 qb + c with rows 4 kq + i and 16 + 4 kq + i in acc4[2 qb] / acc4[2 qb + 1].
     auto epilogue = [&](const f32x4 (&acc4)[4], const float4& h0, const float4& h1, uint64_t& ph2d)
                         __attribute__((always_inline)) {
       const float mm0 = METRIC == kL2 ? -2.0f * h0.x : -h0.x;
       const float mm1 = METRIC == kL2 ? -2.0f * h1.x : -h1.x;
-      // common case first, without the norms: mm < 0, so every filter value fma(acc, mm, xn) is
-      // >= fma(max acc, mm, min xn) (exact ordering, one monotone rounding); only when that bound reaches
-      // uf in some lane is the hit mask formed from the row norms
+      // mm < 0, so every row's filter value fma(acc, mm, xn) is >= fma(max acc, mm, min xn) (exact ordering,
+      // one monotone rounding): a lane whose bound does not reach uf holds no hit of that query
       float am0 = fmaxf(acc4[0][0], acc4[1][0]), am1 = fmaxf(acc4[2][0], acc4[3][0]);
 #pragma unroll
       for (int i = 1; i < 4; ++i) {
@@ -321,50 +326,38 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
         am1 = fmaxf(am1, fmaxf(acc4[2][i], acc4[3][i]));
       }
       const float xb = METRIC == kL2 ? xnmin : 0.0f;
-      if (__ballot(fmaf(am0, mm0, xb) < h0.y || fmaf(am1, mm1, xb) < h1.y) == 0) return;
+      // (an empty slot of the tile has the null header: uf = -inf, never passes)
+      const bool p0 = fmaf(am0, mm0, xb) < h0.y, p1 = fmaf(am1, mm1, xb) < h1.y;
+      const uint64_t m0 = __ballot(p0), m1 = __ballot(p1);
+      if ((m0 | m1) == 0) return;
       if (a.flags & 16) {
         ++n_hit_tiles;
         ph2d = __builtin_amdgcn_s_memtime();
       }
-      const float* wnorm = s_norm + (ipar * kRsWaves + wave) * 64;
-      unsigned hits = 0;  // bit 8 qb + 4 rb + i (norms from LDS four at a time: registers are short)
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb) {
-        const float4 nv = *reinterpret_cast<const float4*>(wnorm + 16 * rb + 4 * kq);
-        const float xn[4] = {nv.x, nv.y, nv.z, nv.w};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float xv = METRIC == kL2 ? xn[i] : 0.0f;
-          hits |= (fmaf(acc4[rb][i], mm0, xv) < h0.y ? 1u : 0u) << (4 * rb + i);
-          hits |= (fmaf(acc4[2 + rb][i], mm1, xv) < h1.y ? 1u : 0u) << (8 + 4 * rb + i);
+      // one 48-B record per (lane, query half) that passes: the 8 dots, then {first row position, query}
+      const int pos0 = g * kGroupRows + 4 * kq;
+      const int n0 = __popcll(m0);
+      if (p0) {
+        const int at = wcnt + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u));
+        if (at < a.wave_cap) {
+          int4* r = wstream + (int64_t)at * kRsRecInt4;
+          r[0] = __builtin_bit_cast(int4, acc4[0]);
+          r[1] = __builtin_bit_cast(int4, acc4[1]);
+          r[2] = make_int4(pos0, __float_as_int(h0.w), 0, 0);
         }
       }
-      // (-1: an empty lane of the tile)
-      const int bq0 = __float_as_int(h0.w), bq1 = __float_as_int(h1.w);
-      if (!(bq0 >= 0 && bq0 < a.nq)) hits &= 0xFF00u;
-      if (!(bq1 >= 0 && bq1 < a.nq)) hits &= 0x00FFu;
-      // every filter hit (a superset of the keys <= T_q; the refine's window is below T_q) goes to this
-      // wave's stream -- positions by ballot prefix, no atomics; k_rs_bucket sorts the streams into
-      // per-query runs. One hit per lane per round; the rare survivors are picked out of the
-      // accumulators by selects (bit r = 8 qb + 4 rb + i is element r of acc4)
-      while (__ballot(hits != 0) != 0) {
-        const bool has = hits != 0;
-        const int r = has ? __builtin_ctz(hits) : 0;
-        hits &= hits - 1;
-        float c = acc4[0][0];
-#pragma unroll
-        for (int e = 1; e < 16; ++e) c = r == e ? acc4[e >> 2][e & 3] : c;
-        const int qb = r >> 3, row = 16 * ((r >> 2) & 1) + 4 * kq + (r & 3);
-        const uint64_t m = __ballot(has);
-        const int at = wcnt + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        if (has && at < a.wave_cap) {
-          const float4 hq = qb ? h1 : h0;
-          wstream[at] = make_int4(__float_as_int(pf_key<METRIC>(c, hq.x, wnorm[row], hq.z)), g * kGroupRows + row,
-                                  __float_as_int(hq.w), 0);
+      if (p1) {
+        const int at = wcnt + n0 + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
+        if (at < a.wave_cap) {
+          int4* r = wstream + (int64_t)at * kRsRecInt4;
+          r[0] = __builtin_bit_cast(int4, acc4[2]);
+          r[1] = __builtin_bit_cast(int4, acc4[3]);
+          r[2] = make_int4(pos0, __float_as_int(h1.w), 0, 0);
         }
-        wcnt += __popcll(m);
       }
+      wcnt += n0 + __popcll(m1);
     };
 
     // One tile. The item's rows have landed (the wait at the item start); this wave's DMA of the next tile
@@ -377,9 +370,21 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
       // every wave's pieces of this tile have landed and every wave is done with the previous tile
       if (!spun_out && !rs_spin(s_ready, kRsWaves * (tt + 1))) spun_out = true;
       ++tt;
+      if (LAST && has_next) {
+        const int4 v = s_desc[(ii + 1) & 3];
+        nx = RsItem{__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
+                    __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w)};
+        gnx = nx.g0 + wave;
+        gvn = gnx < nx.gend;
+      }
       const bool grabber = t == 0 && wave == 0 && lane == 0;
       int grabbed = -1;
-      if (grabber) grabbed = grab(ii + 3);  // (its result is waited for at the signal below)
+      int4 desc2 = make_int4(0, 0, 0, 0);
+      if (grabber) {
+        grabbed = grab(ii + 3);  // (its result is waited for at the signal below)
+        const int w2 = s_next[(ii + 2) & 3];  // (grabbed during the previous item's first tile)
+        if (w2 >= 0) desc2 = a.items[w2];
+      }
       const uint64_t ph1 = (a.flags & 16) ? __builtin_amdgcn_s_memtime() : 0;
       const bool last = LAST;
       // the next tile (of this item, or the next item's first) goes into the next buffer. Its pieces are
@@ -413,8 +418,8 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
               __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[t2 + 1], b[s % (PD + 1)], acc4[2 * qb + 1], 0, 0, 0);
           if constexpr (RL) {
             // the next item's rows, right after the last use of the registers (registers 2 t, 2 t + 1 after
-            // piece 2 t + 1), its norms first, with the first k-step
-            if (s == 0) load_norms(gvn ? gnx : nx.g0, ipar ^ 1);
+            // piece 2 t + 1), its group's smallest row norm first, with the first k-step
+            if (s == 0 && METRIC == kL2) xn_next = a.group_nmin[gvn ? gnx : nx.g0];
             if (s & 1) {
               ra[s - 1] = ld_rows(nrs, s - 1);
               ra[s] = ld_rows(nrs, s);
@@ -442,7 +447,10 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
       // its DMA pieces of the next have landed -- vmcnt counts, in issue order, only the next item's rows
       // issued after its last piece beyond them
       rs_wait_vm(LAST && has_next ? ROWS_AFTER : 0);
-      if (grabber) s_next[(ii + 3) & 3] = grabbed;
+      if (grabber) {
+        s_next[(ii + 3) & 3] = grabbed;
+        s_desc[(ii + 2) & 3] = desc2;
+      }
       rs_signal(s_ready);
       const uint64_t ph2b = (a.flags & 16) ? __builtin_amdgcn_s_memtime() : 0;
       uint64_t ph2c = ph2b, ph2d = 0;
@@ -456,6 +464,10 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
         const uint64_t ph3 = __builtin_amdgcn_s_memtime();
         pw_wait += ph1 - ph0;
         pw_loop += ph2 - ph1;
+        if (t == 0) {
+          pw_first += ph2 - ph1;
+          ++n_items;
+        }
         pw_dma += ph2b - ph2;
         pw_drain += ph2c - ph2b;
         pw_epi += ph3 - ph2c;
@@ -465,14 +477,16 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
     };
     // the item's rows (loaded during the previous item's last tile) and everything before them; at the
     // first item, the prologue's DMA pieces too, which the wave then signals as tile 0's
-    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
+    // The first item: wait for everything (the prologue's DMA pieces, which the wave then signals as tile 0's,
+    // and the rows). Later items: the rows were issued during the previous item's last tile, in k-step order;
+    // each is waited for where the first tile's k-loop first reads it (the compiler's counted vmcnt before
+    // that MFMA: every DMA piece and record store it cannot see is YOUNGER, so its count only waits longer),
+    // which gives every row load about one more tile of latency than one vmcnt(0) here (MIVS_RS_ROWWAIT=1
+    // restores that for A/B runs).
+    if (tt == 0 || (a.flags & 32)) __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
+    else __builtin_amdgcn_s_waitcnt(0xC07F);                             // lgkmcnt(0)
     if (tt == 0) rs_signal(s_ready);
-    {  // the smallest row norm of this wave's group (its norms landed with the rows; pad rows: +inf)
-      float m = s_norm[(ipar * kRsWaves + wave) * 64 + j];
-#pragma unroll
-      for (int off = 16; off >= 1; off >>= 1) m = fminf(m, __shfl_xor(m, off));
-      xnmin = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(m)));
-    }
+    xnmin = xn_next;
     for (int t = 0; t + 1 < ntiles; ++t) tile(t, BoolC<false>{});
     tile(ntiles - 1, BoolC<true>{});
     n_tiles_done += ntiles;
@@ -482,7 +496,6 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
     it = nx;
     g = gnx;
     gv = gvn;
-    ipar ^= 1;
   }
   block_prof();
 }
@@ -561,7 +574,7 @@ __global__ __launch_bounds__(1024) void k_rs_bounds(const int* __restrict__ work
 template <int METRIC>
 __global__ void k_rs_headers(const float* __restrict__ pre_kth, int64_t nq, const float* __restrict__ qscale,
                              const float* __restrict__ qnorms, const float* __restrict__ qres, float x_norm_max,
-                             float x_res_max, int dp, float4* __restrict__ hdr) {
+                             float x_res_max, int dp, float4* __restrict__ hdr, float* __restrict__ tq) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q > nq) return;
   if (q == nq) {  // the null header
@@ -582,7 +595,8 @@ __global__ void k_rs_headers(const float* __restrict__ pre_kth, int64_t nq, cons
     T = T + fabsf(T) * 0x1p-20f + 1e-30f;
   }
   const float uf = pf_uf<METRIC>(INFINITY, T, qn, x_norm_max * x_norm_max);
-  hdr[q] = make_float4(qscale[q], uf, qn, __int_as_float((int)q));  // (T itself is only in uf)
+  hdr[q] = make_float4(qscale[q], uf, qn, __int_as_float((int)q));
+  if (tq) tq[q] = T;
 }
 
 // Tile images for K13: per list l with m_l queries, ceil(m_l / 32) tiles of [NK + 1] x 1 KiB: piece
@@ -626,8 +640,8 @@ __global__ __launch_bounds__(1024) void k_rs_tiles(const int64_t* __restrict__ b
 
 size_t rs_scan_lds_bytes(int dp) {
   const int nk = dp / 16;
-  // two tile buffers + the norms ([2 items][8 waves][64]) + the tiles-ready counter and the item ring
-  return (size_t)2 * (nk * 1024 + 1024) + 2 * kRsWaves * 64 * sizeof(float) + 64;
+  // two tile buffers + the tiles-ready counter, the item ring and its descriptors
+  return (size_t)2 * (nk * 1024 + 1024) + 128;
 }
 
 bool rs_scan_supported(int dp) {
@@ -699,10 +713,11 @@ hipError_t launch_rs_items(const int* work_off, const int* bucket_off, const int
   return hipGetLastError();
 }
 
-// K13's per-wave candidate streams -> per-query CSR runs for K11: stream offsets (one workgroup), then
-// count and scatter over the flat index of all entries (a thread per entry, whatever the streams'
-// lengths, which differ by orders of magnitude). A stream longer than its capacity lost entries of
-// unknown queries: `lost` is then set and K11 proves no query (every query goes to the fallback search).
+// K13's per-wave record streams -> per-query CSR runs for K11: stream offsets (one workgroup), then
+// count and scatter. A record {8 dots of one lane, first row position, query} expands to the rows whose
+// exact filter value fma(acc, mm, xn) passes uf -- the same test, on the same values, as a per-row test in
+// K13's epilogue would make -- each with its approximate key. A stream longer than its capacity lost
+// records of unknown queries: `lost` is then set and K11 proves no query (every query goes to the fallback).
 __global__ __launch_bounds__(1024) void k_rs_stream_off(const int* __restrict__ wave_cnt, int n_waves, int wave_cap,
                                                         int64_t* __restrict__ woff, int* __restrict__ lost) {
   __shared__ int64_t sh[16];
@@ -723,6 +738,40 @@ __global__ __launch_bounds__(1024) void k_rs_stream_off(const int* __restrict__ 
   if (threadIdx.x == 0) woff[n_waves] = base;
 }
 
+// one record: its query, and the rows among its 8 that pass the query's filter (bit i: row pos0 + i for i < 4,
+// pos0 + 12 + i for i >= 4 -- rows 4 kq + i and 16 + 4 kq + i - 4 of the group)
+struct RsRec {
+  f32x4 c0, c1;
+  int pos0, q;
+};
+
+__device__ __forceinline__ RsRec rs_rec_load(const int4* __restrict__ r) {
+  RsRec v;
+  v.c0 = __builtin_bit_cast(f32x4, r[0]);
+  v.c1 = __builtin_bit_cast(f32x4, r[1]);
+  const int4 m = r[2];
+  v.pos0 = m.x;
+  v.q = m.y;
+  return v;
+}
+
+__device__ __forceinline__ int rs_rec_row(int pos0, int i) { return pos0 + (i < 4 ? i : 12 + i); }
+
+template <int METRIC>
+__device__ __forceinline__ unsigned rs_rec_hits(const RsRec& r, const float4& h, const float* __restrict__ row_norms,
+                                                float (&xn)[8]) {
+  const float mm = METRIC == kL2 ? -2.0f * h.x : -h.x;
+  unsigned m = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    xn[i] = row_norms[rs_rec_row(r.pos0, i)];
+    const float c = i < 4 ? r.c0[i] : r.c1[i - 4];
+    const float xv = METRIC == kL2 ? xn[i] : 0.0f;
+    m |= (fmaf(c, mm, xv) < h.y ? 1u : 0u) << i;
+  }
+  return m;
+}
+
 // the stream offsets in LDS (binary searches there, not through L2)
 constexpr int kRsMaxStreams = 4096;
 __device__ __forceinline__ const int64_t* rs_woff_lds(const int64_t* woff, int n_waves, int64_t* sw) {
@@ -731,7 +780,7 @@ __device__ __forceinline__ const int64_t* rs_woff_lds(const int64_t* woff, int n
   return sw;
 }
 
-// entry e of the flat index -> (stream, index in the stream)
+// record e of the flat index -> (stream, index in the stream)
 __device__ __forceinline__ int rs_stream_of(const int64_t* woff, int n_waves, int64_t e) {
   int lo = 0, hi = n_waves - 1;
   while (lo < hi) {
@@ -741,20 +790,40 @@ __device__ __forceinline__ int rs_stream_of(const int64_t* woff, int n_waves, in
   return lo;
 }
 
+template <int METRIC>
 __global__ __launch_bounds__(256) void k_rs_count(const int4* __restrict__ wave_buf, int wave_cap,
                                                   const int64_t* __restrict__ woff, int n_waves,
+                                                  const float4* __restrict__ qhdr, const float* __restrict__ row_norms,
                                                   unsigned long long* __restrict__ qcnt) {
   __shared__ int64_t sw[kRsMaxStreams + 1];
   woff = rs_woff_lds(woff, n_waves, sw);
   const int64_t total = woff[n_waves];
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
     const int w = rs_stream_of(woff, n_waves, e);
-    atomicAdd(qcnt + wave_buf[(int64_t)w * wave_cap + (e - woff[w])].z, 1ull);
+    const RsRec r = rs_rec_load(wave_buf + ((int64_t)w * wave_cap + (e - woff[w])) * kRsRecInt4);
+    float xn[8];
+    const unsigned m = rs_rec_hits<METRIC>(r, qhdr[r.q], row_norms, xn);
+    if (m) atomicAdd(qcnt + r.q, (unsigned long long)__popc(m));
   }
 }
 
+template <int METRIC>
+__device__ __forceinline__ void rs_rec_emit(const RsRec& r, unsigned m, const float4& h, const float (&xn)[8], int at,
+                                            float* __restrict__ key, int* __restrict__ pos) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (m & (1u << i)) {
+      const float c = i < 4 ? r.c0[i] : r.c1[i - 4];
+      key[at] = pf_key<METRIC>(c, h.x, xn[i], h.z);
+      pos[at] = rs_rec_row(r.pos0, i);
+      ++at;
+    }
+}
+
+template <int METRIC>
 __global__ __launch_bounds__(256) void k_rs_scatter(const int4* __restrict__ wave_buf, int wave_cap,
                                                     const int64_t* __restrict__ woff, int n_waves,
+                                                    const float4* __restrict__ qhdr, const float* __restrict__ row_norms,
                                                     const int64_t* __restrict__ off, int* __restrict__ fill,
                                                     float* __restrict__ key, int* __restrict__ pos) {
   __shared__ int64_t sw[kRsMaxStreams + 1];
@@ -762,53 +831,67 @@ __global__ __launch_bounds__(256) void k_rs_scatter(const int4* __restrict__ wav
   const int64_t total = woff[n_waves];
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
     const int w = rs_stream_of(woff, n_waves, e);
-    const int4 v = wave_buf[(int64_t)w * wave_cap + (e - woff[w])];
-    const int64_t at = off[v.z] + atomicAdd(fill + v.z, 1);
-    key[at] = __int_as_float(v.x);
-    pos[at] = v.y;
+    const RsRec r = rs_rec_load(wave_buf + ((int64_t)w * wave_cap + (e - woff[w])) * kRsRecInt4);
+    const float4 h = qhdr[r.q];
+    float xn[8];
+    const unsigned m = rs_rec_hits<METRIC>(r, h, row_norms, xn);
+    if (m) rs_rec_emit<METRIC>(r, m, h, xn, (int)(off[r.q] + atomicAdd(fill + r.q, __popc(m))), key, pos);
   }
 }
 
 // The same bucketing with an LDS histogram per group of streams. Group b holds the streams of J K13
 // workgroups of one item queue (x = b % 8, workgroups x + 8 (J (b / 8) + t), t < J). Those workgroups take
-// consecutive items of the same lists, so their hits fall on the same lists' queries, and the ~2M
-// contended global atomics of the flat kernels become one per (group, query) with a hit.
+// consecutive items of the same lists, so their hits fall on the same lists' queries, and the contended
+// global atomics of the flat kernels become one per (group, query) with a hit.
 constexpr int kRsLdsMaxQ = 32768;  // 128 KiB of int bins
 __device__ __forceinline__ int rs_group_stream(int b, int t, int J) {
   return ((b & 7) + 8 * (J * (b >> 3) + t / kRsWaves)) * kRsWaves + t % kRsWaves;
 }
 
+template <int METRIC>
 __device__ __forceinline__ void rs_group_hist(const int4* __restrict__ wave_buf, int wave_cap,
-                                              const int* __restrict__ wave_cnt, int J, int nq, int* bins) {
+                                              const int* __restrict__ wave_cnt, int J, int nq,
+                                              const float4* __restrict__ qhdr, const float* __restrict__ row_norms,
+                                              int* bins) {
   for (int i = threadIdx.x; i < nq; i += blockDim.x) bins[i] = 0;
   __syncthreads();
   for (int t = 0; t < kRsWaves * J; ++t) {
     const int w = rs_group_stream(blockIdx.x, t, J);
     const int n = min(wave_cnt[w], wave_cap);
-    const int4* sb = wave_buf + (int64_t)w * wave_cap;
-    for (int e = threadIdx.x; e < n; e += blockDim.x) atomicAdd(bins + sb[e].z, 1);
+    const int4* sb = wave_buf + (int64_t)w * wave_cap * kRsRecInt4;
+    for (int e = threadIdx.x; e < n; e += blockDim.x) {
+      const RsRec r = rs_rec_load(sb + (int64_t)e * kRsRecInt4);
+      float xn[8];
+      const unsigned m = rs_rec_hits<METRIC>(r, qhdr[r.q], row_norms, xn);
+      if (m) atomicAdd(bins + r.q, __popc(m));
+    }
   }
   __syncthreads();
 }
 
+template <int METRIC>
 __global__ __launch_bounds__(1024) void k_rs_count_lds(const int4* __restrict__ wave_buf, int wave_cap,
                                                        const int* __restrict__ wave_cnt, int J, int nq,
+                                                       const float4* __restrict__ qhdr, const float* __restrict__ row_norms,
                                                        unsigned long long* __restrict__ qcnt) {
   extern __shared__ int bins[];
-  rs_group_hist(wave_buf, wave_cap, wave_cnt, J, nq, bins);
+  rs_group_hist<METRIC>(wave_buf, wave_cap, wave_cnt, J, nq, qhdr, row_norms, bins);
   for (int i = threadIdx.x; i < nq; i += blockDim.x) {
     const int c = bins[i];
     if (c) atomicAdd(qcnt + i, (unsigned long long)c);
   }
 }
 
+template <int METRIC>
 __global__ __launch_bounds__(1024) void k_rs_scatter_lds(const int4* __restrict__ wave_buf, int wave_cap,
                                                          const int* __restrict__ wave_cnt, int J, int nq,
+                                                         const float4* __restrict__ qhdr,
+                                                         const float* __restrict__ row_norms,
                                                          const int64_t* __restrict__ off, int* __restrict__ fill,
                                                          float* __restrict__ key, int* __restrict__ pos) {
   extern __shared__ int bins[];
-  rs_group_hist(wave_buf, wave_cap, wave_cnt, J, nq, bins);
-  // this group's range of each query's run (< n_waves * wave_cap entries in all: fits an int)
+  rs_group_hist<METRIC>(wave_buf, wave_cap, wave_cnt, J, nq, qhdr, row_norms, bins);
+  // this group's range of each query's run (< 2^31 entries in all: fits an int)
   for (int i = threadIdx.x; i < nq; i += blockDim.x) {
     const int c = bins[i];
     if (c) bins[i] = (int)(off[i] + atomicAdd(fill + i, c));
@@ -817,12 +900,13 @@ __global__ __launch_bounds__(1024) void k_rs_scatter_lds(const int4* __restrict_
   for (int t = 0; t < kRsWaves * J; ++t) {
     const int w = rs_group_stream(blockIdx.x, t, J);
     const int n = min(wave_cnt[w], wave_cap);
-    const int4* sb = wave_buf + (int64_t)w * wave_cap;
+    const int4* sb = wave_buf + (int64_t)w * wave_cap * kRsRecInt4;
     for (int e = threadIdx.x; e < n; e += blockDim.x) {
-      const int4 v = sb[e];
-      const int at = atomicAdd(bins + v.z, 1);
-      key[at] = __int_as_float(v.x);
-      pos[at] = v.y;
+      const RsRec r = rs_rec_load(sb + (int64_t)e * kRsRecInt4);
+      const float4 h = qhdr[r.q];
+      float xn[8];
+      const unsigned m = rs_rec_hits<METRIC>(r, h, row_norms, xn);
+      if (m) rs_rec_emit<METRIC>(r, m, h, xn, atomicAdd(bins + r.q, __popc(m)), key, pos);
     }
   }
 }
@@ -832,9 +916,48 @@ size_t rs_bucket_tmp_bytes(int nq, int n_waves) {
          scan_tmp_bytes(nq + 1) + 64;
 }
 
+template <int METRIC>
+static hipError_t rs_bucket_m(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
+                              const float4* qhdr, const float* row_norms, int64_t* cand_off, float* cand_key,
+                              int* cand_pos, int64_t* qcnt, int* fill, int64_t* woff, void* stmp, int grid, bool flat,
+                              hipStream_t s) {
+  hipError_t e;
+  // grouped LDS-histogram form when the streams come from K13's 8 item queues (n_waves = 8 queues x P
+  // workgroups x kRsWaves) and the bins fit LDS; J = workgroups of a queue per group
+  const int P = n_waves / (8 * kRsWaves);
+  int J = 0;
+  if (nq <= kRsLdsMaxQ && n_waves == 8 * kRsWaves * P && P > 0 && !flat) J = P % 4 == 0 ? 4 : P % 2 == 0 ? 2 : 1;
+  if (J > 0) {
+    const size_t lds = sizeof(int) * (size_t)nq;
+    static const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rs_count_lds<METRIC>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)(sizeof(int) * kRsLdsMaxQ));
+    static const hipError_t a2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rs_scatter_lds<METRIC>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)(sizeof(int) * kRsLdsMaxQ));
+    if (a1 != hipSuccess) return a1;
+    if (a2 != hipSuccess) return a2;
+    const unsigned nb = (unsigned)(8 * (P / J));
+    hipLaunchKernelGGL(k_rs_count_lds<METRIC>, dim3(nb), dim3(1024), lds, s, wave_buf, wave_cap, wave_cnt, J, nq, qhdr,
+                       row_norms, reinterpret_cast<unsigned long long*>(qcnt));
+    e = launch_exclusive_scan_i64(qcnt, cand_off, nq + 1, stmp, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_rs_scatter_lds<METRIC>, dim3(nb), dim3(1024), lds, s, wave_buf, wave_cap, wave_cnt, J, nq,
+                       qhdr, row_norms, cand_off, fill, cand_key, cand_pos);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(k_rs_count<METRIC>, dim3((unsigned)grid), dim3(256), 0, s, wave_buf, wave_cap, woff, n_waves, qhdr,
+                     row_norms, reinterpret_cast<unsigned long long*>(qcnt));
+  e = launch_exclusive_scan_i64(qcnt, cand_off, nq + 1, stmp, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_rs_scatter<METRIC>, dim3((unsigned)grid), dim3(256), 0, s, wave_buf, wave_cap, woff, n_waves,
+                     qhdr, row_norms, cand_off, fill, cand_key, cand_pos);
+  return hipGetLastError();
+}
+
 hipError_t launch_rs_bucket(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
-                            int64_t* cand_off, float* cand_key, int* cand_pos, void* tmp, int* lost, int grid,
-                            hipStream_t s) {
+                            const float4* qhdr, const float* row_norms, int metric, int64_t* cand_off,
+                            float* cand_key, int* cand_pos, void* tmp, int* lost, int grid, hipStream_t s) {
   int64_t* qcnt = static_cast<int64_t*>(tmp);
   int* fill = reinterpret_cast<int*>(qcnt + nq + 1);
   int64_t* woff = reinterpret_cast<int64_t*>(
@@ -845,38 +968,27 @@ hipError_t launch_rs_bucket(const int4* wave_buf, int wave_cap, const int* wave_
   if (n_waves <= 0) return launch_exclusive_scan_i64(qcnt, cand_off, nq + 1, stmp, s);
   if (n_waves > kRsMaxStreams) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_rs_stream_off, dim3(1), dim3(1024), 0, s, wave_cnt, n_waves, wave_cap, woff, lost);
-  // grouped LDS-histogram form when the streams come from K13's 8 item queues (n_waves = 8 queues x P
-  // workgroups x kRsWaves) and the bins fit LDS; J = workgroups of a queue per group
-  const int P = n_waves / (8 * kRsWaves);
-  int J = 0;
   const char* fe = getenv("MIVS_RS_BUCKET_FLAT");
-  if (nq <= kRsLdsMaxQ && n_waves == 8 * kRsWaves * P && P > 0 && !(fe && fe[0] == '1'))
-    J = P % 4 == 0 ? 4 : P % 2 == 0 ? 2 : 1;
-  if (J > 0) {
-    const size_t lds = sizeof(int) * (size_t)nq;
-    static const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rs_count_lds),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                     (int)(sizeof(int) * kRsLdsMaxQ));
-    static const hipError_t a2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rs_scatter_lds),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                     (int)(sizeof(int) * kRsLdsMaxQ));
-    if (a1 != hipSuccess) return a1;
-    if (a2 != hipSuccess) return a2;
-    const unsigned nb = (unsigned)(8 * (P / J));
-    hipLaunchKernelGGL(k_rs_count_lds, dim3(nb), dim3(1024), lds, s, wave_buf, wave_cap, wave_cnt, J, nq,
-                       reinterpret_cast<unsigned long long*>(qcnt));
-    e = launch_exclusive_scan_i64(qcnt, cand_off, nq + 1, stmp, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_rs_scatter_lds, dim3(nb), dim3(1024), lds, s, wave_buf, wave_cap, wave_cnt, J, nq,
-                       cand_off, fill, cand_key, cand_pos);
-    return hipGetLastError();
-  }
-  hipLaunchKernelGGL(k_rs_count,dim3((unsigned)grid), dim3(256), 0, s, wave_buf, wave_cap, woff, n_waves,
-                     reinterpret_cast<unsigned long long*>(qcnt));
-  e = launch_exclusive_scan_i64(qcnt, cand_off, nq + 1, stmp, s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)grid), dim3(256), 0, s, wave_buf, wave_cap, woff, n_waves, cand_off,
-                     fill, cand_key, cand_pos);
+  const bool flat = fe && fe[0] == '1';
+  return metric == kIP ? rs_bucket_m<kIP>(wave_buf, wave_cap, wave_cnt, n_waves, nq, qhdr, row_norms, cand_off, cand_key,
+                                          cand_pos, qcnt, fill, woff, stmp, grid, flat, s)
+                       : rs_bucket_m<kL2>(wave_buf, wave_cap, wave_cnt, n_waves, nq, qhdr, row_norms, cand_off, cand_key,
+                                          cand_pos, qcnt, fill, woff, stmp, grid, flat, s);
+}
+
+// the smallest row norm of every group (K13's filter bound; pad rows are +inf, every group has a real row)
+__global__ void k_group_nmin(const float* __restrict__ norms, int64_t n_groups, float* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t g = t >> 5;
+  float m = g < n_groups ? norms[t] : INFINITY;
+#pragma unroll
+  for (int off = 16; off >= 1; off >>= 1) m = fminf(m, __shfl_xor(m, off));
+  if (g < n_groups && (t & 31) == 0) out[g] = m;
+}
+
+hipError_t launch_group_nmin(const float* norms, int64_t n_groups, float* out, hipStream_t s) {
+  if (n_groups <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_group_nmin, dim3((unsigned)ceil_div(n_groups * 32, 256)), dim3(256), 0, s, norms, n_groups, out);
   return hipGetLastError();
 }
 
@@ -916,14 +1028,14 @@ hipError_t launch_rs_pre_lists(const int64_t* goff, int n_lists, int div, int mi
 
 hipError_t launch_rs_headers(const float* pre_kth, int64_t nq, const float* qscale, const float* qnorms,
                              const float* qres, float x_norm_max, float x_res_max, int dp, int metric, float4* hdr,
-                             hipStream_t s) {
+                             float* tq, hipStream_t s) {
   const dim3 grid((unsigned)ceil_div(nq + 1, 256));
   if (metric == kIP)
     hipLaunchKernelGGL(k_rs_headers<kIP>, grid, dim3(256), 0, s, pre_kth, nq, qscale, qnorms, qres, x_norm_max,
-                       x_res_max, dp, hdr);
+                       x_res_max, dp, hdr, tq);
   else
     hipLaunchKernelGGL(k_rs_headers<kL2>, grid, dim3(256), 0, s, pre_kth, nq, qscale, qnorms, qres, x_norm_max,
-                       x_res_max, dp, hdr);
+                       x_res_max, dp, hdr, tq);
   return hipGetLastError();
 }
 

@@ -88,6 +88,7 @@ class SearchStats(ctypes.Structure):
         ("scan_kernel", c_int32),
         ("candidates", c_int64),
         ("cand_overflow", c_int64),
+        ("spun_out_waves", c_int64),
     ]
 
     def as_dict(self) -> dict:
@@ -146,6 +147,8 @@ _SIGS = {
                                   c_void_p]),
     "mivs_kmeans_predict": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_int32, c_int32,
                                       c_void_p]),
+    "mivs_kmeans_steps": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32,
+                                    c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p]),
     "mivs_merge_topk": (c_int32, [c_int32, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_int32,
                                   c_void_p, c_void_p]),
     "mivs_merge_topk_gathered": (c_int32, [c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_int64, c_int32, c_int32,

@@ -50,6 +50,25 @@ def fit(params: KMeansParams, X, centroids=None, rows: torch.Tensor | None = Non
     return c, params.max_iter
 
 
+def build_steps(X, centroids, rows: torch.Tensor | None, it_begin: int, n_steps: int, it_total: int,
+                balance: bool = True, return_labels: bool = False):
+    """Iterations it_begin .. it_begin + n_steps - 1 of the IVF build's k-means (mivs_kmeans_steps: the assign
+    through the fp16 pre-filter, the fp64 update, the re-seed on all but the last 2 of it_total iterations),
+    from `centroids` (updated in place). Returns (centroids, labels of the last step or None)."""
+    x = as_device_f32(X, name="X")
+    dev = x.device.index
+    n, d = x.shape
+    c = as_device_f32(centroids, device=dev, name="centroids")
+    rows_t = None if rows is None else rows.to(device=x.device, dtype=torch.int64).contiguous()
+    n_train = n if rows_t is None else rows_t.shape[0]
+    labels = torch.empty(n_train, dtype=torch.int64, device=x.device) if return_labels else None
+    with torch.cuda.device(dev):
+        _native.check(_native.lib().mivs_kmeans_steps(dev, stream_ptr(dev), ptr(x), n, d, ptr(rows_t), n_train,
+                                                      c.shape[0], it_begin, n_steps, it_total, int(balance), ptr(c),
+                                                      ptr(labels)))
+    return c, labels
+
+
 def predict(params: KMeansParams, centroids, X) -> torch.Tensor:
     x = as_device_f32(X, name="X")
     dev = x.device.index

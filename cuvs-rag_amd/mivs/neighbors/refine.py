@@ -16,10 +16,14 @@ from .._tensors import as_device_f32, emit, out_tensor, ptr, stream_ptr
 from .ivf_flat import _SQRT_METRICS, metric_code
 
 
-def refine(dataset, queries, candidates, k: int, metric: str = "sqeuclidean", indices=None, distances=None,
+def refine(dataset, queries, candidates, k=None, indices=None, distances=None, metric: str = "sqeuclidean",
            resources=None):
     """-> (distances [nq, k] f32, neighbors [nq, k] i64): the exact top-k of each query's candidate rows
-    (row numbers of ``dataset``; -1 entries are skipped)."""
+    (row numbers of ``dataset``; -1 entries are skipped).
+
+    cuVS's parameter order: ``k`` may be omitted when ``indices`` (the output buffer) is given -- it is then
+    ``indices.shape[1]``. This build serves k <= 64 (one wave per query ranks the candidates); larger k
+    raises ValueError."""
     ds = dataset.tensor if hasattr(dataset, "tensor") else dataset
     if not isinstance(ds, torch.Tensor):
         ds = torch.as_tensor(ds)
@@ -39,6 +43,10 @@ def refine(dataset, queries, candidates, k: int, metric: str = "sqeuclidean", in
     c = torch.as_tensor(c).to(device=f"cuda:{dev}", dtype=torch.int64).contiguous()
     if c.dim() != 2 or c.shape[0] != q.shape[0]:
         raise ValueError("candidates must be [n_queries, n_candidates]")
+    if k is None:
+        if indices is None:
+            raise ValueError("k is required when no indices output is given")
+        k = (indices.tensor if hasattr(indices, "tensor") else indices).shape[1]
     k = int(k)
     if not 1 <= k <= min(c.shape[1], 64):
         raise ValueError(f"k must be in [1, min(n_candidates, 64)], got {k}")

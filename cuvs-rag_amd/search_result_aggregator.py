@@ -10,11 +10,14 @@ DesignDocument.md:119-137,174-189``. This is that contract, written for MI355X:
   * the per-shard [Q, k] tiles stay on their devices and are merged over RCCL: one grouped
     all-gather on xGMI (``mivs.comm.LocalComm`` -> ``mivs_merge_topk_allgather``) and the K7 wave
     merge on the device, replacing the reference's host numpy argsort
-    (improved_multi_gpu_rag.py:266-275, cuvs-2gpu-main.ipynb:1820-1834). Under torch.distributed
-    (one process per GPU) the local result is then merged across ranks with
-    ``mivs.distributed.merge_across_ranks`` (RCCL all-gather, same K7 merge). Rows merge
+    (improved_multi_gpu_rag.py:266-275, cuvs-2gpu-main.ipynb:1820-1834). Rows merge
     independently, so the ``(P, k)`` concat + axis-0 fancy-index bug (``index 2 is out of bounds``,
     RequirementsDocument.md:5) cannot occur;
+  * opt-in (``SearchConfig.merge_across_ranks``), under torch.distributed with one process per GPU:
+    the local result is then merged across ranks (``mivs.distributed.merge_across_ranks``, RCCL
+    all-gather + K7). That is a collective: EVERY rank must call ``perform_distributed_search`` at the
+    same point with the same query batch and the same k, or rows of different queries would be merged
+    (or the collective would hang). Off by default, so a rank serving its own batches never blocks;
   * the merge order follows the indices' metric (ascending L2 / cosine distance, descending inner
     product), ties by id;
   * shards built by the coordinator carry GLOBAL ids (``ids_offset = start_index``), so no
@@ -108,6 +111,9 @@ class SearchConfig:
     # of this process when there are several, the K7 merge alone for one; "rccl": always the RCCL
     # exchange (also for one GPU); "peer": peer copies to the first GPU, then K7
     exchange: str = "auto"
+    # mivs extension: also merge across torch.distributed ranks (a collective: every rank must search the
+    # same query batch with the same k at the same point; see the module docstring). Default off.
+    merge_across_ranks: bool = False
 
     def __post_init__(self):
         if self.k <= 0:
@@ -181,17 +187,34 @@ def _rccl_merge(tiles: Dict[int, Tuple[torch.Tensor, torch.Tensor]], k: int, met
     return out[devs[0]]
 
 
+def _ranks_active() -> bool:
+    import torch.distributed as tdist
+
+    return tdist.is_available() and tdist.is_initialized() and tdist.get_world_size() > 1
+
+
 def _rank_merge(d: torch.Tensor, i: torch.Tensor, k: int, metric: str):
     """Under torch.distributed (one process per GPU): merge this rank's result with every other rank's
     over the RCCL all-gather (``mivs.distributed.merge_across_ranks``); identity otherwise."""
-    import torch.distributed as tdist
-
-    if not (tdist.is_available() and tdist.is_initialized() and tdist.get_world_size() > 1):
+    if not _ranks_active():
         return d, i
     from mivs.distributed import merge_across_ranks
 
     with torch.cuda.device(d.device.index):
         return merge_across_ranks(d.contiguous(), i.contiguous(), k, metric)
+
+
+def _rank_merge_host(d: np.ndarray, i: np.ndarray, k: int, metric: str) -> Tuple[np.ndarray, np.ndarray]:
+    """The same cross-rank merge for host results (no engine on this host: the contract's simulation),
+    over the process group's own backend (gloo on CPU)."""
+    if not _ranks_active():
+        return d, i
+    from mivs.distributed import all_gather_topk
+
+    gd, gi = all_gather_topk(torch.from_numpy(np.ascontiguousarray(d, np.float32)),
+                             torch.from_numpy(np.ascontiguousarray(i, np.int64)))
+    q = gd.shape[0]
+    return _host_merge(gd.reshape(q, -1).numpy(), gi.reshape(q, -1).numpy(), k, metric)
 
 
 def combine_search_results(results: List[SearchResult], k: int) -> Tuple[np.ndarray, np.ndarray]:
@@ -340,7 +363,7 @@ class SearchResultAggregator:
                 with torch.cuda.device(order[0]):
                     fd, fi = _device_merge([raw[g][0] for g in order], [raw[g][1] for g in order], kk, metric,
                                            torch.device(f"cuda:{order[0]}"))
-            final_dev = _rank_merge(fd, fi, kk, metric)
+            final_dev = _rank_merge(fd, fi, kk, metric) if config.merge_across_ranks else (fd, fi)
         gpu_results = [SearchResult(distances=raw[g][0].detach().cpu().numpy().astype(np.float32, copy=False),
                                     indices=raw[g][1].detach().cpu().numpy().astype(np.int64, copy=False),
                                     gpu_id=g, query_time=raw[g][2], k_requested=config.k,
@@ -351,6 +374,8 @@ class SearchResultAggregator:
             final_d, final_i = final_dev[0].cpu().numpy(), final_dev[1].cpu().numpy()
         else:
             final_d, final_i = self.merge_search_results(gpu_results, config.k, metric)
+            if config.merge_across_ranks:
+                final_d, final_i = _rank_merge_host(final_d, final_i, int(final_d.shape[1]), metric)
         result = AggregatedSearchResult(final_distances=final_d, final_indices=final_i,
                                         total_query_time=time.time() - t0, gpu_results=gpu_results,
                                         k_requested=config.k, k_returned=int(final_d.shape[1]), num_queries=nq)

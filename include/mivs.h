@@ -69,7 +69,8 @@ typedef struct {
   int32_t add_data_on_build;        /* 1: encode the dataset during build */
 } mivs_ivf_pq_params;
 
-/* what the last search on an index did (algorithmic counts for the bench roofline) */
+/* what the last search on an index did (algorithmic counts for the bench roofline). Searches that run in
+ * query batches (K13 above 32,768 queries, large k) report the last batch: n_queries is its size. */
 typedef struct {
   int64_t n_queries;
   int32_t n_probes;
@@ -85,7 +86,9 @@ typedef struct {
   int64_t unique_groups;    /* 32-row groups of the lists probed by at least one query (compulsory bytes) */
   int32_t scan_kernel;      /* fine scan that served it: 3 K3, 31 K3w, 10 K10, 12 K12, 13 K13 */
   int64_t candidates;       /* K13: (approximate key <= T_q, row) pairs appended, all queries */
-  int64_t cand_overflow;    /* K13: queries with more candidates than their buffer holds */
+  int64_t cand_overflow;    /* K13: queries sent to the fallback because a record stream overflowed */
+  int64_t spun_out_waves;   /* K13: waves that gave up waiting for a tile (~40 ms; never expected): their
+                               batch took the fallback search, as for a stream overflow */
 } mivs_search_stats;
 
 /* device time of the searches issued since the last collect while profiling was on
@@ -180,6 +183,13 @@ int32_t mivs_kmeans_fit(int32_t device, void* stream, const float* d_data, int64
                         float* d_centroids);
 int32_t mivs_kmeans_predict(int32_t device, void* stream, const float* d_data, int64_t n, int32_t dim,
                             const float* d_centroids, int32_t n_clusters, int32_t metric, int64_t* d_labels);
+/* iterations it_begin .. it_begin + n_steps - 1 of the IVF build's k-means (its assign through the fp16
+ * pre-filter, the fp64 update and, when balance != 0, the re-seed on all but the last 2 of it_total
+ * iterations): the build's trainer one step at a time, for full-size parity checks. d_centroids in/out;
+ * d_labels (optional, [n_train] int64): the last step's assignment. */
+int32_t mivs_kmeans_steps(int32_t device, void* stream, const float* d_data, int64_t n, int32_t dim,
+                          const int64_t* d_rows, int64_t n_train, int32_t n_clusters, int32_t it_begin, int32_t n_steps,
+                          int32_t it_total, int32_t balance, float* d_centroids, int64_t* d_labels);
 
 /* ---- K7: merge m sorted candidate lists per query -> top-k (cross-shard merge after the
  *      RCCL all-gather; replaces the host numpy merge at improved_multi_gpu_rag.py:266-275) ----

@@ -217,23 +217,31 @@ void orc_kmeans_update(const float* x, const int64_t* rows, int64_t nr, const in
   int64_t* order = (int64_t*)malloc(sizeof(int64_t) * (size_t)(nr > 0 ? nr : 1));
   int64_t* offs = (int64_t*)malloc(sizeof(int64_t) * (size_t)(nc + 1));
   stable_by_label(labels, nr, nc, order, offs);
-#pragma omp parallel for schedule(dynamic, 1)
-  for (int j = 0; j < nc; ++j) {
-    const int64_t b = offs[j], e = offs[j + 1], cnt = e - b;
-    if (cnt == 0) continue;
-    for (int kk = 0; kk < d; ++kk) {
-      double total = 0.0;
+#pragma omp parallel
+  {
+    /* per dim kk: s = sum of the chunk's members in member order, total += s in chunk order (the loops run
+     * member-outer so that each row is read contiguously; every (kk) sum sees the same sequence) */
+    double* total = (double*)malloc(sizeof(double) * (size_t)d);
+    double* s = (double*)malloc(sizeof(double) * (size_t)d);
+#pragma omp for schedule(dynamic, 1)
+    for (int j = 0; j < nc; ++j) {
+      const int64_t b = offs[j], e = offs[j + 1], cnt = e - b;
+      if (cnt == 0) continue;
+      for (int kk = 0; kk < d; ++kk) total[kk] = 0.0;
       for (int64_t cb = b; cb < e; cb += ORC_KM_CHUNK) {
         const int64_t ce = cb + ORC_KM_CHUNK < e ? cb + ORC_KM_CHUNK : e;
-        double s = 0.0;
+        for (int kk = 0; kk < d; ++kk) s[kk] = 0.0;
         for (int64_t m = cb; m < ce; ++m) {
           const int64_t t = order[m];
-          s += (double)x[(rows ? rows[t] : t) * (int64_t)d + kk];
+          const float* xr = x + (rows ? rows[t] : t) * (int64_t)d;
+          for (int kk = 0; kk < d; ++kk) s[kk] += (double)xr[kk];
         }
-        total += s;
+        for (int kk = 0; kk < d; ++kk) total[kk] += s[kk];
       }
-      c[(int64_t)j * d + kk] = (float)(total / (double)cnt);
+      for (int kk = 0; kk < d; ++kk) c[(int64_t)j * d + kk] = (float)(total[kk] / (double)cnt);
     }
+    free(total);
+    free(s);
   }
   free(order);
   free(offs);

@@ -42,6 +42,7 @@ def lib():
             "orc_merge": (None, [P, P, i64, i32, i32, i32, i32, P, P]),
             "orc_kmeans_assign": (None, [P, P, i64, P, i32, i32, i32, P]),
             "orc_kmeans_update": (None, [P, P, i64, P, i32, i32, P]),
+            "orc_kmeans_rebalance": (None, [P, P, i64, P, i32, i32, i32, P]),
             "orc_kmeans_fit": (None, [P, P, i64, i32, i32, i32, i32, P]),
             "orc_kmeans_fit_ex": (None, [P, P, i64, i32, i32, i32, i32, i32, P]),
             "orc_train_count": (i64, [i64, i32, f64, i64]),
@@ -155,6 +156,28 @@ def kmeans_assign(x, c, rows=None, metric="sqeuclidean"):
     out = np.empty(nr, np.int32)
     lib().orc_kmeans_assign(_p(x), _p(r), nr, _p(c), c.shape[0], x.shape[1], metric_code(metric), _p(out))
     return out
+
+
+def kmeans_update(x, labels, c, rows=None):
+    """One Lloyd centroid update from given labels (orc_kmeans_update: fp64 sums over fixed 256-member
+    chunks in ascending train position); c is updated in place and returned. Empty clusters keep c."""
+    x = _f32(x)
+    lab = np.ascontiguousarray(labels, dtype=np.int32)
+    r = None if rows is None else _i64(rows)
+    assert c.dtype == np.float32 and c.flags.c_contiguous
+    lib().orc_kmeans_update(_p(x), _p(r), lab.shape[0], _p(lab), c.shape[0], x.shape[1], _p(c))
+    return c
+
+
+def kmeans_rebalance(x, labels, it, c, rows=None):
+    """The IVF build's balancing step of iteration `it` (orc_kmeans_rebalance, cuVS adjust_centers
+    restated); c is updated in place and returned."""
+    x = _f32(x)
+    lab = np.ascontiguousarray(labels, dtype=np.int32)
+    r = None if rows is None else _i64(rows)
+    assert c.dtype == np.float32 and c.flags.c_contiguous
+    lib().orc_kmeans_rebalance(_p(x), _p(r), lab.shape[0], _p(lab), c.shape[0], x.shape[1], int(it), _p(c))
+    return c
 
 
 def kmeans_fit(x, c0, iters, rows=None, metric="sqeuclidean", balance=False):

@@ -24,7 +24,7 @@ def header_functions():
 def test_header_declares_the_hot_path_entry_points():
     fns = header_functions()
     for required in ("mivs_ivf_flat_build", "mivs_ivf_flat_search", "mivs_brute_force_build",
-                     "mivs_brute_force_search", "mivs_kmeans_fit", "mivs_merge_topk", "mivs_index_free",
+                     "mivs_brute_force_search", "mivs_kmeans_fit", "mivs_kmeans_steps", "mivs_merge_topk", "mivs_index_free",
                      "mivs_last_error"):
         assert required in fns
 

@@ -1,9 +1,12 @@
 """N>1 path on CPU: one process per rank (gloo, world_size 2), corpus sharded with the reference's
 'even' split, per-shard top-k with global ids, one all-gather, then the global merge.
 
-The device merge (K7) needs a GPU, so the ranks here pass a host merge_fn; everything else — the
-exchange layout, id offsets, and the result being identical on every rank — is the production
-code path of mivs.distributed.
+``merge_across_ranks`` runs its DEFAULT branch (``all_gather_raw`` + ``ops.merge_topk_gathered`` over
+the rank-major receive buffer, read in place): only the K7 kernel call inside
+``merge_topk_gathered`` needs a GPU, so the ranks replace that one function with a host stand-in
+that reads the same [parts, nq, k_in] layout (the kernel itself is pinned by the -m gpu exchange
+tests). The aggregator's opt-in cross-rank merge (``SearchConfig.merge_across_ranks``) runs over
+the same process group.
 """
 import os
 import socket
@@ -34,6 +37,18 @@ def _host_merge(d, i, k, metric="sqeuclidean"):
     return torch.from_numpy(od), torch.from_numpy(oi)
 
 
+def _host_gathered(d, i, k, metric="sqeuclidean"):
+    """Host stand-in for K7's gathered form: [parts, nq, k_in] rank-major, read without a transpose."""
+    parts, nq, kin = d.shape
+    od, oi = np.empty((nq, k), np.float32), np.empty((nq, k), np.int64)
+    for r in range(nq):
+        dd = np.concatenate([d[p, r].numpy() for p in range(parts)])
+        ii = np.concatenate([i[p, r].numpy() for p in range(parts)])
+        o = np.lexsort((ii, dd))[:k]
+        od[r], oi[r] = dd[o], ii[o]
+    return torch.from_numpy(od), torch.from_numpy(oi)
+
+
 def _rank(rank, world, port, out):
     import sys
 
@@ -42,7 +57,10 @@ def _rank(rank, world, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from gpu_resource_manager import GPUResourceManager
+    from mivs import ops
     from mivs.distributed import all_gather_raw, allreduce_max, merge_across_ranks
+
+    ops.merge_topk_gathered = _host_gathered  # the K7 call only: the default branch runs as in production
 
     rng = np.random.default_rng(0)
     x = rng.standard_normal((1003, 16)).astype(np.float32)
@@ -55,7 +73,9 @@ def _rank(rank, world, port, out):
     loc = np.argsort(d, axis=1, kind="stable")[:, :5]
     ld = torch.from_numpy(np.take_along_axis(d, loc, 1).astype(np.float32))
     li = torch.from_numpy((loc + start).astype(np.int64))  # global ids = start_index + local id
-    gd, gi = merge_across_ranks(ld, li, 5, merge_fn=_host_merge)
+    gd, gi = merge_across_ranks(ld, li, 5)  # default branch: all_gather_raw + merge_topk_gathered
+    hd, hi = merge_across_ranks(ld, li, 5, merge_fn=_host_merge)  # the merge_fn hook gives the same
+    assert torch.equal(hi, gi) and torch.equal(hd, gd)
     t = allreduce_max(float(rank + 1))
     # the rank-major receive buffer the device merge (mivs_merge_topk_gathered) reads in place
     rd, ri = all_gather_raw(ld, li)
@@ -90,3 +110,51 @@ def test_single_process_merge_is_identity():
     i = torch.arange(12).reshape(3, 4)
     od, oi = merge_across_ranks(d, i, 4)
     assert od is d and oi is i
+
+
+def _agg_rank(rank, world, port, out):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "cuvs-rag_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import search_result_aggregator as sra
+    from gpu_resource_manager import GPUResourceManager
+
+    assert not sra.CUVS_AVAILABLE  # no engine on this host: the contract's simulation answers
+    m = GPUResourceManager.__new__(GPUResourceManager)
+    m.available_gpus = [0]
+    m.validate_gpu_index = lambda g: True
+    agg = sra.SearchResultAggregator(m)
+    torch.manual_seed(100 + rank)
+    q = torch.zeros((6, 8))
+    local = agg.perform_distributed_search(q, {0: object()}, sra.SearchConfig(k=4))  # default: no collective
+    merged = agg.perform_distributed_search(q, {0: object()}, sra.SearchConfig(k=4, merge_across_ranks=True))
+    out[rank] = (local.final_distances.tolist(), local.final_indices.tolist(),
+                 merged.gpu_results[0].distances.tolist(), merged.gpu_results[0].indices.tolist(),
+                 merged.final_distances.tolist(), merged.final_indices.tolist())
+    dist.destroy_process_group()
+
+
+def test_two_rank_aggregator_merge_is_opt_in_and_global():
+    """ADVICE r2: the aggregator merges across ranks only when SearchConfig.merge_across_ranks is set;
+    then every rank holds the global top-k of all ranks' shard results"""
+    world = 2
+    port = _free_port()
+    with mp.Manager() as man:
+        out = man.dict()
+        mp.spawn(_agg_rank, args=(world, port, out), nprocs=world, join=True)
+        res = dict(out)
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "cuvs-rag_amd"))
+    from search_result_aggregator import _host_merge
+
+    d = np.concatenate([np.asarray(res[r][2], np.float32) for r in range(world)], axis=1)
+    i = np.concatenate([np.asarray(res[r][3], np.int64) for r in range(world)], axis=1)
+    ed, ei = _host_merge(d, i, 4)
+    for r in range(world):
+        assert np.asarray(res[r][0]).shape == (6, 4)  # the local-only search returned its own merge
+        np.testing.assert_array_equal(np.asarray(res[r][5]), ei)
+        np.testing.assert_array_equal(np.asarray(res[r][4], np.float32), ed)

@@ -12,7 +12,8 @@ The bench measures these shapes; these tests make its numbers evidence:
   queries, (ii) the oracle over the exported centroids and lists == the GPU for 200 sampled queries
   (ids, distance bits and probes), (iii) the build's labels are the same with the fp16 pre-filter assign
   (default) and the fp32 assign (MIVS_PF_ASSIGN=0), and the oracle's assign of a 100k-row sample at the
-  GPU's final centroids gives the GPU's lists.
+  GPU's final centroids gives the GPU's lists, (iv) one full-size Lloyd step of the build's trainer (5M train
+  rows) is bit-exact with the oracle's update + re-seed, and stepping on to 20 iterations gives the build.
 * configs[4], the per-GPU share -- 12.5M x 768 fp16 IVF-PQ, n_lists 4096, pq_dim 96: the oracle's PQ
   search over the exported centroids, codebooks and codes == the GPU for a query sample.
 
@@ -177,6 +178,49 @@ def test_config2_ivf_10m_build_labels_fp16_assign_equal_fp32_and_oracle(ivf_10m)
     rows = _sample(n, 100_000, 3)
     xs = x[torch.from_numpy(rows).to("cuda:0")].cpu().numpy()
     np.testing.assert_array_equal(O.kmeans_assign(xs, cents), lab_pf[rows])
+
+
+def test_config2_kmeans_lloyd_step_full_size_bitexact_vs_oracle(ivf_10m):
+    """steps of the 10M build's trainer at full size. The GPU runs the build's k-means
+    (mivs_kmeans_steps = kmeans_fit_impl of ivf_flat_build: pre-filter assign, fp64 chunked update, re-seed)
+    from the build's strided init over the 5M strided train rows. For steps t = 0 (the first, from the init,
+    where lists are least even) and t = 4 the oracle (orc_kmeans_update + orc_kmeans_rebalance, on the host's
+    cores) takes the GPU's labels of step t and the centroids before it: the centroids after step t must be
+    bit-equal -- 5M x 768 fp64 member sums over ~20k 256-member chunks, and the re-seed wherever a list is
+    under-filled at that step. The labels are checked against the oracle's assign on a 100k-row sample.
+    Stepping on to iteration 20 must give the build's own centroids. Matches
+    Attempt_1/index_building_coordinator.py:392-396 (ivf_flat.build with n_lists 1024, 20 iterations)."""
+    from mivs.cluster import kmeans
+
+    x, _, idx = ivf_10m
+    n, dim, nl, total = x.shape[0], x.shape[1], 1024, 20
+    nt = O.train_count(n, nl, 0.5)
+    assert nt == 5_000_000
+    rows = torch.from_numpy(O.train_rows(n, nt)).to("cuda:0")
+    init = (((np.arange(nl, dtype=np.int64) * nt) // nl) * n) // nt  # ivf_flat_build's init rows
+    c = x[torch.from_numpy(init).to("cuda:0")].contiguous()
+    xt = x[rows].cpu().numpy()  # the 5M train rows (15.4 GB), rows in train order
+    done = 0
+    for t in (0, 4):
+        if t > done:
+            kmeans.build_steps(x, c, rows, done, t - done, total, balance=True)
+        c_t = c.cpu().numpy().copy()
+        _, lab = kmeans.build_steps(x, c, rows, t, 1, total, balance=True, return_labels=True)
+        done = t + 1
+        c_gpu = c.cpu().numpy()
+        lab = lab.cpu().numpy().astype(np.int32)
+        s_ = _sample(nt, 100_000, 5 + t)
+        np.testing.assert_array_equal(O.kmeans_assign(xt[s_], c_t), lab[s_])
+        sizes = np.bincount(lab, minlength=nl)
+        print(f"step {t}: list sizes min {sizes.min()} max {sizes.max()}, under-filled (re-seeded) "
+              f"{int((sizes < 0.25 * nt / nl).sum())}")
+        c_orc = O.kmeans_update(xt, lab, c_t.copy())
+        O.kmeans_rebalance(xt, lab, t, c_orc)
+        np.testing.assert_array_equal(_bits(c_gpu), _bits(c_orc))
+    del xt
+    # and the build's own 20 iterations land where the steps do (the index fixture is that build)
+    kmeans.build_steps(x, c, rows, done, total - done, total, balance=True)
+    np.testing.assert_array_equal(_bits(c.cpu().numpy()), _bits(idx.centers.cpu().numpy()))
 
 
 def test_config4_share_ivf_pq_12m5_fp16_oracle_on_query_sample(mivs_lib):

@@ -65,6 +65,8 @@ SEARCH_SWITCHES = [
     {"MIVS_RS_BUCKET_FLAT": "1"},                                     # K13 streams bucketed by flat atomics
     {"MIVS_RS_STATIC_DEAL": "1"},                                     # K13 items dealt statically
     {"MIVS_RS_FLAGS": "24"},                                          # K13 clocks (stderr only)
+    {"MIVS_RS_WAVE_CAP": "2"},                                        # K13 streams overflow: the fallback
+    {"MIVS_RS_ROWWAIT": "1"},                                         # K13 rows waited at item start
     {"MIVS_PF_ROWSTAT": "0", "MIVS_PF_FLAGS": "32"},                  # K10 phase clocks (stderr only)
 ]
 
@@ -215,3 +217,34 @@ def test_coarse_probe_dump_switch_same_bits(ivf, flat_data, monkeypatch, n_probe
     np.testing.assert_array_equal(p1.cpu().numpy(), p0.cpu().numpy())
     np.testing.assert_array_equal(i1.cpu().numpy(), i0.cpu().numpy())
     np.testing.assert_array_equal(_bits(d1.cpu().numpy()), _bits(d0.cpu().numpy()))
+
+
+def test_k13_lost_stream_fallback_is_exact_and_reported(ivf, flat_data, monkeypatch):
+    """force K13's record streams to overflow (2 records per wave): every query of the batch takes
+    the fallback search, the stats say so, and the answer is the default one bit for bit"""
+    idx, _ = ivf
+    _, q = flat_data
+    d0, i0 = _search(idx, q)
+    st0 = idx.last_search_stats()
+    assert st0["scan_kernel"] == 13 and st0["cand_overflow"] == 0 and st0["spun_out_waves"] == 0
+    monkeypatch.setenv("MIVS_RS_WAVE_CAP", "2")
+    d1, i1 = _search(idx, q)
+    st1 = idx.last_search_stats()
+    assert st1["cand_overflow"] == q.shape[0] and st1["overflow_queries"] >= q.shape[0]
+    assert st1["spun_out_waves"] == 0
+    np.testing.assert_array_equal(i1, i0)
+    np.testing.assert_array_equal(_bits(d1), _bits(d0))
+
+
+def test_k13_query_batches_same_bits(ivf, flat_data):
+    """more queries than one K13 batch (kRsMaxBatch = 32768): the batched search equals per-slice searches"""
+    idx, _ = ivf
+    x, _ = flat_data
+    rng = np.random.default_rng(9)
+    q = x[rng.integers(0, x.shape[0], 33_000)] + 0.01 * rng.standard_normal((33_000, x.shape[1])).astype(np.float32)
+    d, i = _search(idx, q)
+    assert idx.last_search_stats()["n_queries"] == 33_000 - 32_768  # the last batch
+    for lo, hi in ((0, 5000), (32_000, 33_000)):
+        ds, is_ = _search(idx, q[lo:hi])
+        np.testing.assert_array_equal(i[lo:hi], is_)
+        np.testing.assert_array_equal(_bits(d[lo:hi]), _bits(ds))

@@ -77,3 +77,21 @@ def test_ivf_pq_then_refine_recall(mivs_lib):
     rec = lambda f: np.mean([len(set(a) & set(b)) / 10 for a, b in zip(f, gt)])  # noqa: E731
     assert rec(ri.cpu().numpy()) >= rec(pq10.cpu().numpy())
     assert rec(ri.cpu().numpy()) > 0.8
+
+
+def test_refine_cuvs_argument_order_and_k_from_indices(mivs_lib):
+    """cuVS's order refine(dataset, queries, candidates, k=None, indices=None, distances=None,
+    metric=...); k omitted -> indices.shape[1]; k > 64 is refused rather than silently capped"""
+    from mivs.neighbors import refine
+
+    rng = np.random.default_rng(4)
+    x = torch.from_numpy(rng.standard_normal((3000, 64)).astype(np.float32)).cuda()
+    q = torch.from_numpy(rng.standard_normal((9, 64)).astype(np.float32)).cuda()
+    cand = torch.from_numpy(np.stack([rng.choice(3000, 80, replace=False) for _ in range(9)])).cuda()
+    d0, i0 = refine(x, q, cand, 8)
+    ib = torch.empty((9, 8), dtype=torch.int64, device="cuda")
+    db = torch.empty((9, 8), dtype=torch.float32, device="cuda")
+    d1, i1 = refine(x, q, cand, None, ib, db)
+    assert torch.equal(i1, i0) and torch.equal(ib, i0) and torch.equal(db, d0)
+    with pytest.raises(ValueError):
+        refine(x, q, cand, 65)

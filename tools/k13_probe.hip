@@ -1,0 +1,223 @@
+// K13 k-loop probe (tools/, not part of the product): what the row-stationary loop shape of k_rs_scan can
+// sustain on its own, without the search around it. Each wave holds 32 fp16 rows x 768 dims in registers
+// (48 x h8 = 192 VGPRs) and runs 32-query tiles from LDS through v_mfma_f32_16x16x32_f16 (one ds_read_b128
+// per two MFMAs, B read PD k-steps ahead), as K13 does. Variants (VAR bits):
+//   1  per-tile all-wave sync through an LDS counter (K13's rs_spin / rs_signal)
+//   2  LDS-DMA staging of the next tile (6-7 pieces of 1 KiB per wave per tile, L2-resident source)
+//   4  the common-case epilogue (16 fmax + 2 fma + ballot) instead of a plain fold
+//   8  items of 10 tiles: the next item's rows (48 KiB per wave) loaded from a large HBM buffer during an
+//      item's last tile, waited for at the next item's start (K13's item transition)
+//   16 tile images from a 540 MB pool (11k tiles, HBM/MALL): the 32 blocks of one XCD walk one range of it
+//      together, as the items of one list do (otherwise 64 L2-resident tiles)
+// Reports TF/s, the in-kernel clock (s_memtime / s_memrealtime) and the MFMA pipe's busy fraction.
+// Build: hipcc -O3 --offload-arch=gfx950 -ffp-contract=off tools/k13_probe.hip -o tools/k13_probe
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+#define CHECK(x)                                                                             \
+  do {                                                                                       \
+    hipError_t e_ = (x);                                                                     \
+    if (e_ != hipSuccess) {                                                                  \
+      printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__);          \
+      return 1;                                                                              \
+    }                                                                                        \
+  } while (0)
+
+constexpr int NK = 48;
+constexpr int BUF = NK * 1024 + 1024;
+
+__device__ __forceinline__ v4i uniform_desc(const void* p, int bytes) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  v4i r;
+  r.x = (int)__builtin_amdgcn_readfirstlane((uint32_t)v);
+  r.y = (int)(__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) & 0xFFFFu);
+  r.z = __builtin_amdgcn_readfirstlane(bytes);
+  r.w = 0x00020000;
+  return r;
+}
+
+__device__ __forceinline__ void dma_b128(v4i desc, const void* lds, int voff, int soff) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(lds));
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               :: "s"(m0), "v"(voff), "s"(desc), "s"(soff) : "memory");
+}
+
+template <int VAR, int PD, int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 1) void probe(const h8* __restrict__ rows, const char* __restrict__ src,
+                                                       int src_tiles, int ntiles, float* out,
+                                                       unsigned long long* clk, const h8* __restrict__ big_rows,
+                                                       long long big_items) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* s_ready = reinterpret_cast<int*>(smem + 2 * BUF);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int i = tid; i < 2 * BUF / 16; i += WAVES * 64) {
+    const int v = (i * 2654435761u) >> 7;
+    reinterpret_cast<uint4*>(smem)[i] = make_uint4(v & 0x3BFF3BFF, (v >> 3) & 0x3BFF3BFF, v & 0x37FF37FF, 0x3C003C00 ^ (v & 0x03FF03FF));
+  }
+  if (tid == 0) *s_ready = 0;
+  __syncthreads();
+  h8 ra[NK];
+  const h8* rp = rows + ((size_t)(blockIdx.x * WAVES + wave) * NK) * 64 + lane;
+#pragma unroll
+  for (int s = 0; s < NK; ++s) ra[s] = rp[s * 64];
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  float sink = 0.f;
+  int cur = 0;
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  if (VAR & 1) {
+    if (lane == 0) __hip_atomic_fetch_add(s_ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  for (int t = 0; t < ntiles; ++t) {
+    if (VAR & 1) {
+      for (int i = 0; i < (1 << 20); ++i) {
+        if (__hip_atomic_load(s_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= WAVES * (t + 1)) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      asm volatile("" ::: "memory");
+    }
+    const char* bb = smem + cur * BUF + lane * 16;
+    const int nxt = cur ^ 1;
+    char* sbuf = smem + nxt * BUF;
+    const int tsrc = (VAR & 16) ? (int)(((blockIdx.x & 7) * 1375 + t + 1) % src_tiles) : (int)((blockIdx.x + t) % src_tiles);
+    const v4i sdesc = uniform_desc(src + (size_t)tsrc * (NK + 1) * 1024, (NK + 1) * 1024);
+    const bool reload = (VAR & 8) && (t % 10 == 9);
+    const h8* nr = big_rows + ((size_t)(((long long)blockIdx.x * 7919 + t * 131) % big_items) * WAVES + wave) * NK * 64 + lane;
+    if ((VAR & 8) && t % 10 == 0) __builtin_amdgcn_s_waitcnt(0x0070);
+    f32x4 acc[4] = {z, z, z, z};
+    h8 b[PD + 1];
+#pragma unroll
+    for (int u = 0; u < PD; ++u) b[u] = *reinterpret_cast<const h8*>(bb + u * 1024);
+#pragma unroll
+    for (int s = 0; s < NK; ++s) {
+      if (s + PD < NK) b[(s + PD) % (PD + 1)] = *reinterpret_cast<const h8*>(bb + (s + PD) * 1024);
+      const int t2 = 2 * (s >> 1), qb = s & 1;
+      acc[2 * qb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[t2], b[s % (PD + 1)], acc[2 * qb], 0, 0, 0);
+      acc[2 * qb + 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[t2 + 1], b[s % (PD + 1)], acc[2 * qb + 1], 0, 0, 0);
+      if ((VAR & 8) && reload && (s & 1)) {
+        ra[s - 1] = nr[(s - 1) * 64];
+        ra[s] = nr[s * 64];
+      }
+      if (VAR & 2) {
+        if (s >= 1 && (s - 1) * WAVES <= NK) {
+          const int p = min((s - 1) * WAVES + wave, NK);
+          dma_b128(sdesc, sbuf + p * 1024, lane * 16, p * 1024);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if ((VAR & 2) && !((VAR & 8) && reload)) __builtin_amdgcn_s_waitcnt(0x0070);
+    if ((VAR & 2) && (VAR & 8) && reload) __builtin_amdgcn_s_waitcnt(0x0070);  // (conservative: rows too)
+    if (VAR & 1) {
+      asm volatile("" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(s_ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (VAR & 4) {
+      float am0 = fmaxf(acc[0][0], acc[1][0]), am1 = fmaxf(acc[2][0], acc[3][0]);
+#pragma unroll
+      for (int i = 1; i < 4; ++i) {
+        am0 = fmaxf(am0, fmaxf(acc[0][i], acc[1][i]));
+        am1 = fmaxf(am1, fmaxf(acc[2][i], acc[3][i]));
+      }
+      if (__ballot(fmaf(am0, -2.f, 0.5f) < -1e30f || fmaf(am1, -2.f, 0.5f) < -1e30f)) sink += 1.f;
+      sink += am0 * 1e-30f;
+    } else {
+      sink += acc[0][0] + acc[1][1] + acc[2][2] + acc[3][3];
+    }
+    cur = nxt;
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0 && wave == 0) {
+    clk[2 * blockIdx.x] = t1 - t0;
+    clk[2 * blockIdx.x + 1] = r1 - r0;
+  }
+  out[(size_t)(blockIdx.x * WAVES + wave) * 64 + lane] = sink;
+}
+
+const h8* g_big = nullptr;
+long long g_big_items = 1;
+
+template <int VAR, int PD, int WAVES>
+int run(const char* name, const h8* rows, const char* src, int src_tiles, float* out, unsigned long long* clk,
+        int grid, int ntiles) {
+  const size_t lds = 2 * BUF + 64;
+  CHECK(hipFuncSetAttribute((const void*)probe<VAR, PD, WAVES>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  for (int rep = 0; rep < 3; ++rep)  // warm: >= 2 s of back-to-back launches before the timed one
+    hipLaunchKernelGGL((probe<VAR, PD, WAVES>), dim3(grid), dim3(WAVES * 64), lds, 0, rows, src, src_tiles, ntiles, out, clk, g_big, g_big_items);
+  CHECK(hipEventRecord(e0));
+  hipLaunchKernelGGL((probe<VAR, PD, WAVES>), dim3(grid), dim3(WAVES * 64), lds, 0, rows, src, src_tiles, ntiles, out, clk, g_big, g_big_items);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  float ms = 0;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  std::vector<unsigned long long> h(2 * grid);
+  CHECK(hipMemcpy(h.data(), clk, sizeof(unsigned long long) * 2 * grid, hipMemcpyDeviceToHost));
+  double ghz = 0;
+  for (int b = 0; b < grid; ++b) ghz += (double)h[2 * b] / (double)h[2 * b + 1] * 0.1;
+  ghz /= grid;
+  const double n_mfma = (double)grid * WAVES * ntiles * 2 * NK;
+  const double tf = n_mfma * 16 * 16 * 32 * 2 / (ms * 1e-3) / 1e12;
+  const double pipe = n_mfma / (grid * 4.0) * 16 / (ms * 1e-3 * ghz * 1e9);
+  printf("%-34s %8.3f ms  %7.1f TF/s  clock %.3f GHz  pipe busy %.3f  frac-of-2.5PF %.3f\n", name, ms, tf, ghz, pipe,
+         tf / 2500.0);
+  CHECK(hipEventDestroy(e0));
+  CHECK(hipEventDestroy(e1));
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  const int grid = 256;
+  const int ntiles = argc > 1 ? atoi(argv[1]) : 4000;
+  const int src_tiles = 64;  // 3.1 MB of tile images: L2/MALL-resident
+  const int big_tiles = 11000;  // 540 MB of tile images (VAR 16)
+  h8* rows;
+  char* src;
+  float* out;
+  unsigned long long* clk;
+  const size_t nrows = (size_t)grid * 8 * NK * 64;
+  CHECK(hipMalloc(&rows, nrows * sizeof(h8)));
+  CHECK(hipMalloc(&src, (size_t)big_tiles * (NK + 1) * 1024));
+  {
+    h8* big;
+    const size_t big_bytes = (size_t)8 << 30;  // 8 GiB of rows: the item reloads come from HBM
+    CHECK(hipMalloc(&big, big_bytes));
+    CHECK(hipMemset(big, 0x35, big_bytes));
+    g_big = big;
+    g_big_items = (long long)(big_bytes / ((size_t)8 * NK * 1024));
+  }
+  CHECK(hipMalloc(&out, (size_t)grid * 8 * 64 * sizeof(float)));
+  CHECK(hipMalloc(&clk, sizeof(unsigned long long) * 2 * grid));
+  {
+    std::vector<uint16_t> hr(nrows * 8);
+    uint32_t x = 12345;
+    for (auto& v : hr) {
+      x = x * 1664525u + 1013904223u;
+      v = (uint16_t)(0x3000 + ((x >> 9) & 0x0BFF)) ^ ((x >> 3) & 0x8000);
+    }
+    CHECK(hipMemcpy(rows, hr.data(), hr.size() * 2, hipMemcpyHostToDevice));
+    std::vector<uint16_t> hs((size_t)big_tiles * (NK + 1) * 512);
+    for (auto& v : hs) {
+      x = x * 1664525u + 1013904223u;
+      v = (uint16_t)(0x3000 + ((x >> 9) & 0x0BFF)) ^ ((x >> 3) & 0x8000);
+    }
+    CHECK(hipMemcpy(src, hs.data(), hs.size() * 2, hipMemcpyHostToDevice));
+  }
+  printf("grid %d, %d tiles per wave, 16x16x32 f16, 32 rows x 768 dims per wave in registers\n", grid, ntiles);
+  run<0, 2, 8>("loop only, PD 2, 8 waves", rows, src, src_tiles, out, clk, grid, ntiles);
+  run<7, 2, 8>("+sync +dma +epi", rows, src, src_tiles, out, clk, grid, ntiles);
+  run<15, 2, 8>("+sync +dma +epi +items", rows, src, src_tiles, out, clk, grid, ntiles);
+  run<23, 2, 8>("+sync +dma +epi +hbm tiles", rows, src, big_tiles, out, clk, grid, ntiles);
+  run<31, 2, 8>("+sync +dma +epi +items +hbm tiles", rows, src, big_tiles, out, clk, grid, ntiles);
+  run<10, 2, 8>("+dma +items (no sync)", rows, src, src_tiles, out, clk, grid, ntiles);
+  run<26, 2, 8>("+dma +items +hbm tiles (no sync)", rows, src, big_tiles, out, clk, grid, ntiles);
+  return 0;
+}
