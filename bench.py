@@ -67,8 +67,15 @@ def parse():
     ap.add_argument("--flat-rows", type=int, default=1_000_000,
                     help="BASELINE configs[1] side line: brute force over this many rows (0: skip)")
     ap.add_argument("--pq-rows", type=int, default=12_500_000,
-                    help="BASELINE configs[4] side line: IVF-PQ over this many fp16 rows, the per-GPU share of "
-                         "100M x 768 on 8 GPUs (0: skip)")
+                    help="BASELINE configs[4] line: IVF-PQ over this many fp16 rows PER RANK (the per-GPU share of "
+                         "100M x 768 on 8 GPUs), refined top-k merged across ranks over RCCL (0: skip)")
+    ap.add_argument("--large-k", default="2000,4000",
+                    help="side line (rank 0, N=1): the reference's large-k requests at configs[2] "
+                         "(top_k 2000, k*2 per shard: improved_multi_gpu_rag.py:40,247); '' to skip")
+    ap.add_argument("--single-process", type=int, default=1,
+                    help="side line (N=1 launch): the reference's one-process shape -- every visible GPU holds a "
+                         "rows-per-GPU shard, ParallelIndexBuilder threads build them, SearchResultAggregator "
+                         "searches them and merges over RCCL (LocalComm); 0 to skip")
     ap.add_argument("--json-out", default="")
     return ap.parse_args()
 
@@ -236,60 +243,185 @@ def flat_side_line(a, q, k, rl):
     return line
 
 
+def large_k_side_line(a, idx, q, rl, scanned_rows):
+    """The reference's large-k default at configs[2]: its driver asks for top_k = 2000 and each shard for
+    k * 2 (improved_multi_gpu_rag.py:40,247,416). Every k > 16 takes the exact fp32 scan in DUMP mode (K3,
+    raw keys per (query, probe, chunk) slot) + the K8 radix select, query-batched by the select workspace.
+    QPS over the full 10k-query batch, the scan kernel's time and its fp32 MFMA roofline."""
+    from mivs import _native
+    from mivs.neighbors import ivf_flat
+
+    out = []
+    sp = ivf_flat.SearchParams(n_probes=a.n_probes)
+    for kk in [int(v) for v in a.large_k.split(",") if v.strip()]:
+        ivf_flat.search(sp, idx, q, kk)
+        torch.cuda.synchronize()
+        _native.set_profiling(True)
+        idx.profile_collect()
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            d, i = ivf_flat.search(sp, idx, q, kk)
+        torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) / reps
+        pr = idx.profile_collect()
+        _native.set_profiling(False)
+        # the scan runs once per query batch (the select workspace bounds a batch): its time per search call
+        # is the sum over the batches; the algorithmic flops are the k = 10 search's (same probes, all queries)
+        batches = max(1, pr["n_calls"] // reps)
+        scan_ms = pr["scan_ms"] / reps
+        flops = 2.0 * a.dim * scanned_rows
+        tf = flops / (scan_ms * 1e-3) / 1e12
+        ok = bool((i[:, 0] >= 0).all()) and bool((d[:, 1:] >= d[:, :-1]).all())
+        out.append({"k": kk, "queries": q.shape[0], "qps": round(q.shape[0] / t, 1), "ms_per_batch": round(t * 1e3, 3),
+                    "scan_kernel": "mivs::k_scan<DUMP> (K3 exact fp32, raw keys) + mivs::k_select (K8)",
+                    "query_batches": batches, "scan_ms_per_search": round(scan_ms, 4),
+                    "select_and_rest_ms_per_search": round(t * 1e3 - scan_ms, 3), "well_formed": ok,
+                    "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_F32_MFMA_TFS,
+                                 "unit": "TFLOP/s", "frac": round(tf / PEAK_F32_MFMA_TFS, 4)}})
+        rl(f"[large-k] k={kk}: {q.shape[0] / t:,.0f} QPS ({t * 1e3:.1f} ms per {q.shape[0]} queries), scan "
+           f"{scan_ms:.2f} ms = {tf:.1f} TF/s fp32")
+        del d, i
+        torch.cuda.empty_cache()
+    return out
+
+
+def single_process_side_line(a, idx, q, res_i, rl):
+    """The reference's own multi-GPU shape (improved_multi_gpu_rag.py:105,206,239-277; merge contract
+    Attempt_1/test_search_result_aggregator.py:405-457): ONE process drives every visible GPU -- a
+    rows-per-GPU shard on each (the main index on GPU 0, the others generated on their devices and built
+    by ParallelIndexBuilder threads with global ids), SearchResultAggregator searches them in parallel
+    threads and merges over RCCL (exchange='rccl': mivs_comm_init_all + grouped all-gather + K7)."""
+    from gpu_resource_manager import GPUResourceManager
+    from improved_multi_gpu_rag import GPUConfig, IndexType, ParallelIndexBuilder
+    from search_result_aggregator import SearchConfig, SearchResultAggregator
+
+    from mivs import ops
+
+    G = torch.cuda.device_count()
+    n = a.rows
+    indexes = {0: idx}
+    extra = {}
+    t_build = 0.0
+    if G > 1:
+        b = ParallelIndexBuilder(G)
+        params = {"n_lists": a.n_lists, "kmeans_n_iters": a.kmeans_iters,
+                  "kmeans_trainset_fraction": a.trainset_fraction}
+
+        def one(g):
+            with torch.cuda.device(g):
+                xg = ops.synth_mixture(n, a.dim, SEED, n_centers=a.centers, sigma=a.sigma, row_begin=g * n, device=g)
+                torch.cuda.synchronize(g)
+                ix, tb = b.build_index_on_gpu(GPUConfig(g), xg, IndexType.IVF_FLAT, params, ids_offset=g * n)
+                del xg
+                torch.cuda.empty_cache()
+                return g, ix, tb
+
+        t0 = time.perf_counter()
+        futs = [b.executor.submit(one, g) for g in range(1, G)]
+        for f in futs:
+            g, ix, _ = f.result()
+            indexes[g] = extra[g] = ix
+        t_build = time.perf_counter() - t0
+    agg = SearchResultAggregator(GPUResourceManager())
+    cfg = SearchConfig(k=a.k, search_params={"nprobe": a.n_probes}, exchange="rccl")
+    r = agg.perform_distributed_search(q, indexes, cfg)  # warm (communicators, threads)
+    reps = max(3, a.steps // 4)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        r = agg.perform_distributed_search(q, indexes, cfg)
+    t = (time.perf_counter() - t0) / reps
+    line = {"devices": G, "rows_per_gpu": n, "rows_total": n * G, "queries": q.shape[0], "k": a.k,
+            "n_probes": a.n_probes, "qps_full_corpus": round(q.shape[0] / t, 1),
+            "shard_searches_per_s": round(q.shape[0] * G / t, 1), "ms_per_batch": round(t * 1e3, 3),
+            "extra_shards_build_s": round(t_build, 3),
+            "path": "SearchResultAggregator (one thread per GPU) -> mivs.comm.LocalComm RCCL all-gather + K7; "
+                    "results copied to host as the reference's contract returns them"}
+    if G == 1:
+        line["final_ids_equal_main_search"] = bool(np.array_equal(r.final_indices, res_i.cpu().numpy()))
+    rl(f"[single-process] {G} GPU(s), {n * G} rows: {q.shape[0] / t:,.0f} QPS through the aggregator + RCCL merge")
+    for ix in extra.values():
+        ix.close()
+    torch.cuda.empty_cache()
+    return line
+
+
 PEAK_LDS_B128_LOOKUPS = 256 * 2.4e9 * 64  # ds_read_b128: 256 B/clk/CU = 64 fp32 LUT entries / clk / CU
 
 
-def pq_side_line(a, rl):
-    """BASELINE configs[4], the per-GPU share: IVF-PQ over 12.5M x 768 fp16 rows, n_lists 4096, pq_dim 96,
-    pq_bits 8 (improved_multi_gpu_rag.py:131-137), the same query batch shape; plain PQ at n_probes 16 and
-    PQ + exact re-ranking of 10 k candidates (cuvs.neighbors.refine) -- the configuration that reaches
-    recall@10 >= 0.95 on this mixture. The scan's roofline: one fp32 LUT entry read from LDS per
-    (probed row, subspace, query), against the ds_read_b128 rate."""
+def pq_side_line(a, rl, rank=0, world=1, dev=None):
+    """BASELINE configs[4]: IVF-PQ over 12.5M x 768 fp16 rows PER RANK (100M over 8 GPUs), n_lists 4096,
+    pq_dim 96, pq_bits 8 (improved_multi_gpu_rag.py:131-137), the same query batch shape; plain PQ at
+    n_probes 16 and PQ + exact re-ranking of 10 k candidates (cuvs.neighbors.refine) -- the configuration
+    that reaches recall@10 >= 0.95 on this mixture. With N ranks every rank builds its own shard (rows
+    rank*n..), and one step = each rank's search (+ refine) and the RCCL all-gather + K7 merge of the
+    per-shard top-k (mivs.distributed.merge_across_ranks), timed between barriers, max over ranks. The
+    scan's roofline: one fp32 LUT entry read from LDS per (probed row, subspace, query), against the
+    ds_read_b128 rate."""
     from mivs import _native, ops
+    from mivs.distributed import merge_across_ranks
     from mivs.neighbors import brute_force, ivf_pq, refine
 
-    dev = torch.cuda.current_device()
+    dev = torch.cuda.current_device() if dev is None else dev
     n, d, Q, k, pq_dim, n_lists, n_probes, ratio = a.pq_rows, a.dim, a.queries, a.k, 96, 4096, 16, 10
-    x = ops.synth_mixture(n, d, SEED + 11, n_centers=a.centers, sigma=a.sigma, device=dev).half()
+    start = rank * n
+    x = ops.synth_mixture(n, d, SEED + 11, n_centers=a.centers, sigma=a.sigma, row_begin=start, device=dev).half()
     torch.cuda.empty_cache()
     q = ops.synth_mixture(Q, d, SEED + 11, n_centers=a.centers, sigma=a.sigma, row_begin=QUERY_ROW_BASE, device=dev)
-    torch.cuda.synchronize()
+    sync_all(world)
+    _native.set_profiling(True)
     t0 = time.perf_counter()
     idx = ivf_pq.build(ivf_pq.IndexParams(n_lists=n_lists, pq_dim=pq_dim, pq_bits=8), x)
     torch.cuda.synchronize()
-    t_build = time.perf_counter() - t0
+    t_build = max_over_ranks(time.perf_counter() - t0, world, dev)
+    phases = idx.build_phases()
+    _native.set_profiling(False)
     ng = min(1000, Q)
     xf = x.float()
-    bf = brute_force.build(xf)
-    _, gt = brute_force.search(bf, q[:ng], max(17, k))
-    gt = gt[:, :k].cpu().numpy()
+    bf = brute_force.build(xf, ids_offset=start)
+    gd, gi = brute_force.search(bf, q[:ng], max(17, k))
+    gd, gi = gd[:, :k].contiguous(), gi[:, :k].contiguous()
     bf.close()
     del bf, xf
     torch.cuda.empty_cache()
+    if world > 1:
+        gd, gi = merge_across_ranks(gd, gi, k)
+    gt = gi.cpu().numpy()
     sp = ivf_pq.SearchParams(n_probes=n_probes)
     reps = 5
-    ivf_pq.search(sp, idx, q, k)
+
+    def plain():
+        dd, ii = ivf_pq.search(sp, idx, q, k)
+        ii = ii + start if start else ii  # (the shard's row numbers -> global ids)
+        return merge_across_ranks(dd, ii, k) if world > 1 else (dd, ii)
+
+    kc = ratio * k
+
+    def refined():
+        _, cand = ivf_pq.search(sp, idx, q, kc)
+        dd, ii = refine(x, q, cand, k)
+        ii = ii + start if start else ii
+        return merge_across_ranks(dd, ii, k) if world > 1 else (dd, ii)
+
+    plain()
     _native.set_profiling(True)
     idx.profile_collect()
-    torch.cuda.synchronize()
+    sync_all(world)
     t0 = time.perf_counter()
     for _ in range(reps):
-        _, ids = ivf_pq.search(sp, idx, q, k)
+        _, ids = plain()
     torch.cuda.synchronize()
-    t_plain = (time.perf_counter() - t0) / reps
+    t_plain = max_over_ranks(time.perf_counter() - t0, world, dev) / reps
     pr = idx.profile_collect()
     _native.set_profiling(False)
     rec_plain = recall_at_k(ids[:ng].cpu().numpy(), gt)
-    kc = ratio * k
-    _, cand = ivf_pq.search(sp, idx, q, kc)
-    refine(x, q, cand, k)
-    torch.cuda.synchronize()
+    refined()
+    sync_all(world)
     t0 = time.perf_counter()
     for _ in range(reps):
-        _, cand = ivf_pq.search(sp, idx, q, kc)
-        _, rids = refine(x, q, cand, k)
+        _, rids = refined()
     torch.cuda.synchronize()
-    t_ref = (time.perf_counter() - t0) / reps
+    t_ref = max_over_ranks(time.perf_counter() - t0, world, dev) / reps
     rec_ref = recall_at_k(rids[:ng].cpu().numpy(), gt)
     probes = torch.empty((Q, n_probes), dtype=torch.int32, device=dev)
     ivf_pq.search(sp, idx, q, k, probes_out=probes)
@@ -297,20 +429,25 @@ def pq_side_line(a, rl):
     scan_ms = pr["scan_ms"] / max(pr["n_calls"], 1)
     lookups = float(rows) * pq_dim
     ach = lookups / (scan_ms * 1e-3)
-    line = {"rows": n, "dim": d, "dtype_in": "fp16", "n_lists": n_lists, "pq_dim": pq_dim, "pq_bits": 8,
-            "queries": Q, "k": k, "n_probes": n_probes, "build_s": round(t_build, 3),
-            "build_vectors_per_s": round(n / t_build, 1),
+    line = {"rows_per_gpu": n, "rows_total": n * world, "n_gpus": world, "dim": d, "dtype_in": "fp16",
+            "n_lists": n_lists, "pq_dim": pq_dim, "pq_bits": 8, "queries": Q, "k": k, "n_probes": n_probes,
+            "build_s": round(t_build, 3), "build_vectors_per_s": round(n * world / t_build, 1),
+            "build_phases_s": phases,
             "qps_pq": round(Q / t_plain, 1), "recall_at_10_pq": round(rec_plain, 4),
             "qps_pq_refined": round(Q / t_ref, 1), "recall_at_10_pq_refined": round(rec_ref, 4),
-            "refine": f"{kc} PQ candidates re-ranked exactly against the fp16 rows (mivs.neighbors.refine, K14)",
+            "shard_searches_per_s_refined": round(Q * world / t_ref, 1),
+            "refine": f"{kc} PQ candidates re-ranked exactly against the fp16 rows (mivs.neighbors.refine, K14)"
+                      + ("; per-shard top-k merged across ranks (RCCL all-gather + K7) inside the step"
+                         if world > 1 else ""),
             "scan_kernel": "mivs::k_pq_scan_rt (K9r: 16-query tiles per list, code-major LUT rows in LDS)",
             "roofline": {"bound": "lds", "achieved": round(ach / 1e9, 1), "peak": round(PEAK_LDS_B128_LOOKUPS / 1e9, 1),
                          "unit": "G LUT entries/s", "frac": round(ach / PEAK_LDS_B128_LOOKUPS, 4),
                          "launch_ms": round(scan_ms, 4), "lut_entries_per_launch": lookups, "rows_scanned": rows}}
-    rl(f"[pq] {n} x {d} fp16, build {n / t_build / 1e6:.2f} M vec/s; n_probes {n_probes}: {Q / t_plain:,.0f} QPS "
-       f"recall {rec_plain:.3f}; refined x{ratio}: {Q / t_ref:,.0f} QPS recall {rec_ref:.3f}")
+    rl(f"[pq] {n * world} x {d} fp16 on {world} GPU(s), build {n * world / t_build / 1e6:.2f} M vec/s {phases}; "
+       f"n_probes {n_probes}: {Q / t_plain:,.0f} QPS recall {rec_plain:.3f}; refined x{ratio}: {Q / t_ref:,.0f} QPS "
+       f"recall {rec_ref:.3f}")
     idx.close()
-    del x, q, idx, cand, ids, rids
+    del x, q, idx, ids, rids
     torch.cuda.empty_cache()
     return line
 
@@ -347,10 +484,13 @@ def main():
     params = ivf_flat.IndexParams(n_lists=a.n_lists, kmeans_n_iters=a.kmeans_iters,
                                   kmeans_trainset_fraction=a.trainset_fraction)
     sync_all(world)
+    _native.set_profiling(True)  # (the build's phase clocks: one stream sync per phase)
     t0 = time.perf_counter()
     idx = ivf_flat.build(params, x, ids_offset=start)
     torch.cuda.synchronize()
     t_build = max_over_ranks(time.perf_counter() - t0, world, dev)
+    _native.set_profiling(False)
+    build_phases = idx.build_phases()
     build_vps = n * world / t_build
     sizes = idx.list_sizes.numpy()
     rl(f"[build] {n * world} rows in {t_build:.2f} s -> {build_vps / 1e6:.2f} M vec/s; lists min/med/max "
@@ -506,15 +646,31 @@ def main():
         except Exception as e:  # the IVF line stands without it
             rl(f"[flat] side line failed: {e!r}")
 
+    large_k = None
+    if rank == 0 and world == 1 and a.large_k.strip():
+        try:
+            large_k = large_k_side_line(a, idx, q, rl, stats["scanned_rows"])
+        except Exception as e:  # the IVF line stands without it
+            rl(f"[large-k] side line failed: {e!r}")
+
+    single = None
+    if rank == 0 and world == 1 and a.single_process:
+        try:
+            single = single_process_side_line(a, idx, q, res_i, rl)
+        except Exception as e:  # the IVF line stands without it
+            rl(f"[single-process] side line failed: {e!r}")
+
     pq = None
-    if rank == 0 and world == 1 and a.pq_rows > 0:
+    if a.pq_rows > 0:  # every rank: configs[4] is this line at N = 8
         idx.close()
         del x
         torch.cuda.empty_cache()
         try:
-            pq = pq_side_line(a, rl)
+            pq = pq_side_line(a, rl, rank, world, local)
         except Exception as e:  # the IVF-Flat line stands without it
             rl(f"[pq] side line failed: {e!r}")
+            if world > 1:
+                raise  # a rank that left the collective would hang the others
 
     out = {
         "metric": METRIC,
@@ -542,11 +698,14 @@ def main():
         "recall_at_10": round(rec, 4),
         "build_vectors_per_s": round(build_vps, 1),
         "build_s": round(t_build, 3),
+        "build_phases_s": build_phases,
         "roofline": roof,
         "cpu_baseline": cpu,
         "search_stats": stats,
         "n_probes_sweep": sweep,
         "flat_bruteforce_1m": flat,
+        "large_k": large_k,
+        "single_process_aggregator": single,
         "ivf_pq_12m5": pq,
     }
     if rank == 0:

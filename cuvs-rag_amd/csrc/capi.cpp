@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <memory>
 #include <cstring>
@@ -149,6 +150,8 @@ struct mivs_index_s {
   int last_rs_waves = 0;  // K13: candidate streams of the last search (the lost flag follows their counts)
   int64_t last_rs_nq = 0; // K13: queries of the last search batch (its cand_off holds last_rs_nq + 1 offsets)
   int64_t last_ovf = 0, last_window = 0;
+  // host wall time of the build's phases (mivs_index_build_phases; recorded while profiling is on)
+  std::vector<double> build_phase_s;
 };
 
 namespace {
@@ -946,10 +949,10 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   }
   // 2. headers (pf_scan_refine left the fp16 queries, their scales and residuals in ws.qh / qscale / qres)
   ws.qhdr.reserve(sizeof(float4) * (nq + 1));
+  float4* qhdr = ws.qhdr.as<float4>();
   ws.rs_tq.reserve(sizeof(float) * nq);
   HIPCHK(launch_rs_headers(ws.pre_kth.as<float>(), nq, ws.qscale.as<float>(), ws.qn.as<float>(), ws.qres.as<float>(),
-                           idx->x_norm_max, idx->x_res_max, dp, idx->metric, ws.qhdr.as<float4>(), ws.rs_tq.as<float>(),
-                           s));
+                           idx->x_norm_max, idx->x_res_max, dp, idx->metric, qhdr, ws.rs_tq.as<float>(), s));
   // 3. probe map: items = (list, block of kRsBlockGroups groups); every query of a list in one tile column
   const size_t stb = scan_tmp_bytes(ne) + sizeof(int64_t) * (size_t)ne;
   ws.scan_tmp.reserve(stb);
@@ -961,10 +964,12 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
     ws.stat_counts.reserve(sizeof(int) * L.n_lists);
     HIPCHK(hipMemcpyAsync(ws.stat_counts.p, ws.counts.p, sizeof(int) * L.n_lists, hipMemcpyDeviceToDevice, s));
   }
-  // the query tiles in the LDS image layout (one contiguous 1 KiB per DMA wave-instruction)
+  // the query tiles in the LDS image layout (one contiguous 1 KiB per DMA wave-instruction; a per-lane gather
+  // straight from the fp16 query matrix was measured 0.45 ms slower per launch: 16 separate 64-B segments per
+  // DMA instruction)
   ws.rs_tiles.reserve((size_t)rs_tiles_bytes(ne, L.n_lists, dp));
-  HIPCHK(launch_rs_tiles(ws.bucket_q.as<int64_t>(), ws.bucket_off.as<int>(), L.n_lists, ws.qh.as<uint16_t>(),
-                         ws.qhdr.as<float4>(), (int)nq, dp, ws.rs_tiles.as<char>(), s));
+  HIPCHK(launch_rs_tiles(ws.bucket_q.as<int64_t>(), ws.bucket_off.as<int>(), L.n_lists, ws.qh.as<uint16_t>(), qhdr,
+                         (int)nq, dp, ws.rs_tiles.as<char>(), s));
   // 4. K13
   int64_t max_items = 0;  // every list probed: the item table's bound (the probe map decides the count)
   for (int l = 0; l < L.n_lists; ++l) max_items += ceil_div(L.h_goff[l + 1] - L.h_goff[l], kRsBlockGroups);
@@ -1054,7 +1059,7 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   ws.cand_key.reserve(sizeof(float) * max_cand);
   ws.cand_pos.reserve(sizeof(int) * max_cand);
   ws.rs_bucket_tmp.reserve(rs_bucket_tmp_bytes((int)nq, n_waves));
-  HIPCHK(launch_rs_bucket(a.wave_buf, a.wave_cap, a.wave_cnt, n_waves, (int)nq, ws.qhdr.as<float4>(), a.row_norms,
+  HIPCHK(launch_rs_bucket(a.wave_buf, a.wave_cap, a.wave_cnt, n_waves, (int)nq, qhdr, a.row_norms,
                           idx->metric, ws.cand_off.as<int64_t>(), ws.cand_key.as<float>(), ws.cand_pos.as<int>(),
                           ws.rs_bucket_tmp.p, a.wave_cnt + n_waves, 4 * cu_count(idx->device), s));
   // 5. exact ranking of every query's run (slot = one entry); a window above T_q is not proven
@@ -1329,17 +1334,31 @@ int32_t mivs_ivf_flat_build(int32_t device, void* stream, const float* d_data, i
     norms.reserve(sizeof(float) * n);
     HIPCHK(launch_row_norms(d_data, n, dim, norms.as<float>(), s));
     HIPCHK(hipStreamSynchronize(s));
+    // phase clock (profiling on): prepare | coarse k-means | assign + pack | fp16 copy
+    const bool clk = g_profiling.load();
+    auto t_ph = std::chrono::steady_clock::now();
+    auto phase = [&]() {
+      if (!clk) return;
+      HIPCHK(hipStreamSynchronize(s));
+      const auto t1 = std::chrono::steady_clock::now();
+      idx->build_phase_s.push_back(std::chrono::duration<double>(t1 - t_ph).count());
+      t_ph = t1;
+    };
     PfAssign pfa;  // the data's fp16 copy: k-means assign + list fill through the pre-filter
     pf_assign_prepare(pfa, d_data, n, dim, idx->dp, s);
+    phase();
     kmeans_fit_impl(d_data, norms.as<float>(), rows.as<int64_t>(), nt, dim, idx->dp, nl, p->kmeans_n_iters,
                     idx->centroids_rm.as<float>(), idx->G, device, idx->ws, s, p->kmeans_balance != 0, &pfa);
     make_single_list(idx->cents, idx->centroids_rm.as<float>(), nl, dim, idx->dp, 0, idx->G, s);
+    phase();
     if (p->add_data_on_build) {
       build_lists(idx.get(), d_data, norms.as<float>(), n, s, &pfa);
     } else {
       build_lists(idx.get(), d_data, norms.as<float>(), 0, s);
     }
+    phase();
     if (p->prefilter && pf_default_on()) pf_enable(idx.get(), s);
+    phase();
     HIPCHK(hipStreamSynchronize(s));
     *out = idx.release();
   });
@@ -1563,6 +1582,17 @@ int32_t mivs_ivf_pq_build(int32_t device, void* stream, const float* d_data, int
     idx->rot_dim_pad = (p->pq_dim * pl + 3) / 4 * 4;
     const int nl = p->n_lists;
     const int nc = 1 << p->pq_bits;
+    // phase clock (profiling on): prepare | coarse k-means | assign + sort | codebooks | encode
+    const bool clk = g_profiling.load();
+    auto tnow = [] { return std::chrono::steady_clock::now(); };
+    auto t_ph = tnow();
+    auto phase = [&]() {
+      if (!clk) return;
+      HIPCHK(hipStreamSynchronize(s));
+      const auto t1 = tnow();
+      idx->build_phase_s.push_back(std::chrono::duration<double>(t1 - t_ph).count());
+      t_ph = t1;
+    };
     // ---- coarse k-means (as ivf_flat: trainset, strided init) ----
     int64_t nt = (int64_t)((double)n * p->kmeans_trainset_fraction);
     nt = std::min<int64_t>(std::max<int64_t>(nt, nl), n);
@@ -1581,9 +1611,11 @@ int32_t mivs_ivf_pq_build(int32_t device, void* stream, const float* d_data, int
     {
       PfAssign pfa;  // coarse k-means + list assign through the fp16 pre-filter
       pf_assign_prepare(pfa, d_data, n, dim, idx->dp, s);
+      phase();
       kmeans_fit_impl(d_data, norms.as<float>(), rows.as<int64_t>(), nt, dim, idx->dp, nl, p->kmeans_n_iters,
                       idx->centroids_rm.as<float>(), idx->G, device, idx->ws, s, p->kmeans_balance != 0, &pfa);
       make_single_list(idx->cents, idx->centroids_rm.as<float>(), nl, dim, idx->dp, 0, idx->G, s);
+      phase();
       // ---- lists: L2 assignment of every row, stable order by label ----
       labels.reserve(sizeof(int64_t) * n);
       perm.reserve(sizeof(int64_t) * n);
@@ -1608,6 +1640,7 @@ int32_t mivs_ivf_pq_build(int32_t device, void* stream, const float* d_data, int
     HIPCHK(hipMemcpyAsync(L.off.p, L.h_off.data(), sizeof(int64_t) * (nl + 1), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(L.goff.p, L.h_goff.data(), sizeof(int64_t) * (nl + 1), hipMemcpyHostToDevice, s));
     L.finalize_host(idx->G);
+    phase();
     // ---- codebooks: per subspace k-means on residual sub-vectors of a strided trainset ----
     Buf prow, resid, rnorm;
     prow.reserve(sizeof(int64_t) * n_pq);
@@ -1628,6 +1661,7 @@ int32_t mivs_ivf_pq_build(int32_t device, void* stream, const float* d_data, int
       kmeans_fit_impl(rj, rnorm.as<float>(), nullptr, n_pq, pl, dim_pad(pl), nc, p->kmeans_n_iters, bj, idx->G,
                       device, idx->ws, s, p->kmeans_balance != 0);
     }
+    phase();
     // ---- encode + ids into the interleaved layout ----
     const int64_t slots = std::max<int64_t>(L.n_groups, 1) * kGroupRows;
     idx->pq_codes.reserve((size_t)slots * idx->pq_dim_pad);
@@ -1640,6 +1674,7 @@ int32_t mivs_ivf_pq_build(int32_t device, void* stream, const float* d_data, int
                               idx->pq_dim_pad, static_cast<uint8_t*>(idx->pq_codes.p), s));
       HIPCHK(launch_pq_ids(perm.as<int64_t>(), n, L.off.as<int64_t>(), L.goff.as<int64_t>(), nl, id_offset,
                            L.ids.as<int64_t>(), s));
+      phase();
     } else {
       L.n_rows = 0;
       std::fill(L.h_off.begin(), L.h_off.end(), 0);
@@ -2079,6 +2114,15 @@ int32_t mivs_index_last_search_stats(mivs_index_t idx, mivs_search_stats* out) {
       st.work_items = ceil_div(idx->last_nq, idx->last_qtile) * std::max<int64_t>(1, ceil_div(L.n_groups, G));
     }
     *out = st;
+  });
+}
+
+int32_t mivs_index_build_phases(mivs_index_t idx, double* out_s, int32_t n_max, int32_t* n_out) {
+  return guarded([&] {
+    require(idx != nullptr && n_out != nullptr, "NULL argument");
+    const int n = (int)idx->build_phase_s.size();
+    for (int i = 0; i < n && i < n_max && out_s; ++i) out_s[i] = idx->build_phase_s[i];
+    *n_out = n;
   });
 }
 

@@ -635,11 +635,16 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
     const int at = atomicAdd(a.ovf_count, 1);
     a.ovf_q[at] = q;
   }
-  if (live && !ovf && lane == 0 && a.n_window) atomicAdd(reinterpret_cast<unsigned long long*>(a.n_window),
-                                                          (unsigned long long)cnt);
+  // window-size stats: one atomic per workgroup (10k same-address atomics per launch were a serial tail)
+  __shared__ int s_win[4];
+  if (lane == 0) s_win[wv] = live && !ovf ? cnt : 0;
   // the query row in LDS (zero past d), for the exact recompute
   for (int i = lane; i < a.dp; i += 64) s_qv[wv][i] = (live && i < a.d) ? a.queries[qrow * a.d + i] : 0.0f;
   __syncthreads();
+  if (threadIdx.x == 0 && a.n_window) {
+    const int w = s_win[0] + s_win[1] + s_win[2] + s_win[3];
+    if (w) atomicAdd(reinterpret_cast<unsigned long long*>(a.n_window), (unsigned long long)w);
+  }
 
   // phase 3: exact keys in the pinned order (oracle orc_dot), then a bitonic sort by (key, id)
   float P = INFINITY;

@@ -761,10 +761,14 @@ template <int METRIC>
 __device__ __forceinline__ unsigned rs_rec_hits(const RsRec& r, const float4& h, const float* __restrict__ row_norms,
                                                 float (&xn)[8]) {
   const float mm = METRIC == kL2 ? -2.0f * h.x : -h.x;
+  // the record's rows are pos0 .. pos0 + 3 and pos0 + 16 .. + 19 (pos0 = 32 g + 4 kq): two 16-B loads
+  const float4 n0 = *reinterpret_cast<const float4*>(row_norms + r.pos0);
+  const float4 n1 = *reinterpret_cast<const float4*>(row_norms + r.pos0 + 16);
+  xn[0] = n0.x; xn[1] = n0.y; xn[2] = n0.z; xn[3] = n0.w;
+  xn[4] = n1.x; xn[5] = n1.y; xn[6] = n1.z; xn[7] = n1.w;
   unsigned m = 0;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    xn[i] = row_norms[rs_rec_row(r.pos0, i)];
     const float c = i < 4 ? r.c0[i] : r.c1[i - 4];
     const float xv = METRIC == kL2 ? xn[i] : 0.0f;
     m |= (fmaf(c, mm, xv) < h.y ? 1u : 0u) << i;

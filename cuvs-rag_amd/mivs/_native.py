@@ -140,6 +140,7 @@ _SIGS = {
                                   POINTER(c_int32)]),
     "mivs_index_last_search_stats": (c_int32, [c_void_p, POINTER(SearchStats)]),
     "mivs_index_profile_collect": (c_int32, [c_void_p, POINTER(Profile)]),
+    "mivs_index_build_phases": (c_int32, [c_void_p, c_void_p, c_int32, POINTER(c_int32)]),
     "mivs_index_set_prefilter": (c_int32, [c_void_p, c_void_p, c_int32]),
     "mivs_index_get_prefilter": (c_int32, [c_void_p, POINTER(c_int32)]),
     "mivs_index_free": (None, [c_void_p]),
@@ -219,5 +220,30 @@ def check(rc: int) -> None:
     raise MivsError(rc, msg)
 
 
+_PROFILING = False
+
+
 def set_profiling(on: bool) -> None:
+    global _PROFILING
+    _PROFILING = bool(on)
     load().mivs_set_profiling(1 if on else 0)
+
+
+def profiling() -> bool:
+    """Whether set_profiling(True) is in effect (build phase clocks, search hipEvents)."""
+    return _PROFILING
+
+
+BUILD_PHASES = {0: ("prepare", "coarse_kmeans", "assign_pack", "fp16_copy"),
+                2: ("prepare", "coarse_kmeans", "assign_sort", "codebooks", "encode")}
+
+
+def build_phases(handle, kind: int) -> dict:
+    """{phase: seconds} of an index's build (recorded only while profiling was on)."""
+    import ctypes
+
+    buf = (ctypes.c_double * 16)()
+    n = c_int32(0)
+    check(lib().mivs_index_build_phases(handle, buf, 16, ctypes.byref(n)))
+    names = BUILD_PHASES.get(kind, ())
+    return {(names[i] if i < len(names) else f"phase{i}"): round(buf[i], 4) for i in range(min(n.value, 16))}

@@ -156,6 +156,13 @@ class Index:
         _native.check(_native.lib().mivs_index_last_search_stats(self.handle, ctypes.byref(st)))
         return st.as_dict()
 
+    def build_phases(self) -> dict:
+        """Host wall time (s) of this index's build phases (recorded only while profiling was on)."""
+        ph = _native.build_phases(self.handle, 0)
+        if getattr(self, "_to_f32_s", None) is not None:
+            ph = {"to_fp32": round(self._to_f32_s, 4), **ph}
+        return ph
+
     def profile_collect(self) -> dict:
         """Device time of the searches since the last collect (needs mivs._native.set_profiling(True))."""
         pr = _native.Profile()

@@ -21,6 +21,7 @@ fp16 datasets (BASELINE config 5) are widened to fp32 on the device before train
 from __future__ import annotations
 
 import ctypes
+import time
 
 import numpy as np
 import torch
@@ -154,6 +155,13 @@ class Index:
         _native.check(_native.lib().mivs_ivf_pq_get_codes(self.handle, stream_ptr(self.device), ptr(out)))
         return out
 
+    def build_phases(self) -> dict:
+        """Host wall time (s) of this index's build phases (recorded only while profiling was on)."""
+        ph = _native.build_phases(self.handle, 2)
+        if getattr(self, "_to_f32_s", None) is not None:
+            ph = {"to_fp32": round(self._to_f32_s, 4), **ph}
+        return ph
+
     def profile_collect(self) -> dict:
         pr = _native.Profile()
         _native.check(_native.lib().mivs_index_profile_collect(self.handle, ctypes.byref(pr)))
@@ -181,8 +189,13 @@ def build(index_params: IndexParams, dataset, resources=None, ids_offset: int = 
     """Coarse k-means, list assignment, per-subspace codebooks and encoding, on the GPU holding `dataset`."""
     if not isinstance(index_params, IndexParams):
         raise TypeError("index_params must be an ivf_pq.IndexParams")
-    x = as_device_f32(dataset, name="dataset")
+    prof = _native.profiling()
+    t0 = time.perf_counter()
+    x = as_device_f32(dataset, name="dataset")  # (fp16 input is widened exactly; the kernels read fp32)
     dev = x.device.index
+    if prof:
+        torch.cuda.synchronize(dev)
+    t_conv = time.perf_counter() - t0
     n, d = x.shape
     if n < index_params.n_lists:
         raise ValueError(f"dataset has {n} rows, fewer than n_lists={index_params.n_lists}")
@@ -191,7 +204,9 @@ def build(index_params: IndexParams, dataset, resources=None, ids_offset: int = 
     with torch.cuda.device(dev):
         _native.check(_native.lib().mivs_ivf_pq_build(dev, stream_ptr(dev), ptr(x), n, d, ctypes.byref(p),
                                                       int(ids_offset), ctypes.byref(h)))
-    return Index(h.value, index_params.metric)
+    idx = Index(h.value, index_params.metric)
+    idx._to_f32_s = t_conv if prof else None
+    return idx
 
 
 def _search(search_params, index, queries, k: int, neighbors=None, distances=None, probes_out=None):

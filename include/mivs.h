@@ -154,6 +154,10 @@ int32_t mivs_index_info(mivs_index_t index, int64_t* n_rows, int32_t* dim, int32
                         int32_t* device);
 int32_t mivs_index_last_search_stats(mivs_index_t index, mivs_search_stats* out);
 int32_t mivs_index_profile_collect(mivs_index_t index, mivs_profile* out);
+/* host wall time (s) of the build's phases, recorded when profiling was on during the build (stream syncs
+ * between phases): ivf_flat {prepare, coarse k-means, assign + pack, fp16 copy}; ivf_pq {prepare, coarse
+ * k-means, assign + sort, codebooks, encode}. *n_out = phases recorded (0: profiling was off). */
+int32_t mivs_index_build_phases(mivs_index_t index, double* out_s, int32_t n_max, int32_t* n_out);
 /* keep (1) or drop (0) the fp16 copy of the lists that the pre-filter search uses (ivf_flat, brute force).
  * Results are identical either way (the refine recomputes every candidate that can reach the top-k in
  * the pinned fp32 order); the copy costs 2 bytes per padded dimension per row of HBM. */

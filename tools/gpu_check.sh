@@ -14,7 +14,7 @@ if [ "${TESTS:-1}" = "1" ]; then
   tail -3 $OUT/tests.log
   [ $rc -eq 0 ] || { echo "pytest rc=$rc"; exit $rc; }
 fi
-QB="--steps 10 --warmup 2 --no-cpu-baseline --sweep '' --flat-rows 0 --pq-rows 0 --gt-queries 500"
+QB="--steps 10 --warmup 2 --no-cpu-baseline --sweep '' --flat-rows 0 --pq-rows 0 --large-k '' --single-process 0 --gt-queries 500"
 eval timeout -k 10 300 python -u bench.py $QB --json-out $OUT/bench.json > $OUT/bench.log 2>&1 || { echo "bench failed"; tail -5 $OUT/bench.log; exit 3; }
 python3 -c "import json;j=json.load(open('$OUT/bench.json'));r=j['roofline'];print('value',j['value'],'ms',j['ms_per_step'],'recall',j['recall_at_10'],'k13_ms',r['launch_ms'],'frac',r['frac'],'cand',j['search_stats']['candidates'])"
 if [ "${PHASE:-1}" = "1" ]; then
