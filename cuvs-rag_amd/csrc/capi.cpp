@@ -137,8 +137,6 @@ struct mivs_index_s {
   float x_norm_max = 0.0f, x_res_max = 0.0f;
   int pf_G = kPfChunkGroups;                  // groups per K10 work item
   std::vector<int64_t> pf_top_chunks_prefix;  // as ListSet::top_chunks_prefix, for pf_G
-  int pr_G = kPrChunkGroups;                  // groups per K12 work item
-  std::vector<int64_t> pr_top_chunks_prefix;  // as ListSet::top_chunks_prefix, for pr_G
   std::mutex mu;
   Workspace ws;
   Profiler prof;
@@ -655,17 +653,6 @@ void pf_enable(mivs_index_s* idx, hipStream_t s) {
     for (int l = 0; l < L.n_lists; ++l) out[l + 1] = out[l] + c[l];
   };
   top_prefix(idx->pf_G, idx->pf_top_chunks_prefix);
-  // K12 items: the LDS holds a ring of groups, not the chunk's norms, so any chunk length fits
-  const char* re = getenv("MIVS_PR_CHUNK_ROWS");
-  idx->pr_G = std::max(1, re ? atoi(re) / kGroupRows : kPrChunkGroups);
-  top_prefix(idx->pr_G, idx->pr_top_chunks_prefix);
-}
-
-// K12 (register-resident 128-query tiles) serves the pre-filter scan only on request
-// (MIVS_PF_REG=1): at d = 768 its 4-entry lane lists send too many queries to the exact fallback
-bool pr_use(const mivs_index_s* idx) {
-  const char* e = getenv("MIVS_PF_REG");
-  return e && e[0] == '1' && pr_scan_supported(idx->dp);
 }
 
 void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
@@ -685,8 +672,7 @@ void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_
 // (goff / n_lists: another split of the same groups into lists -- K13's pre-pass samples)
 // kth_out: K13's pre-pass -- only the k-th smallest approximate key per query (no refine, no fallback)
 void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
-                    int64_t* out_i, ProfRec* pr, bool use_r, const int64_t* goff, int n_lists,
-                    float* kth_out = nullptr) {
+                    int64_t* out_i, ProfRec* pr, const int64_t* goff, int n_lists, float* kth_out = nullptr) {
   Workspace& ws = idx->ws;
   const ListSet& L = idx->lists;
   const int dp = idx->dp;
@@ -695,18 +681,17 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   ws.qres.reserve(sizeof(float) * nq);
   HIPCHK(launch_queries_to_half(q, nq, idx->d, dp, idx->hx_exp, ws.qh.as<uint16_t>(), ws.qscale.as<float>(),
                                 ws.qres.as<float>(), s));
-  const std::vector<int64_t>& tcp = use_r ? idx->pr_top_chunks_prefix : idx->pf_top_chunks_prefix;
+  const std::vector<int64_t>& tcp = idx->pf_top_chunks_prefix;
   const int64_t max_slots = std::max<int64_t>(1, nq * tcp[std::min<int64_t>(np, L.n_lists)]);
   // per-slot candidates: room above k so that a neighbourhood packed into one chunk does not overflow
-  // (K12: the query's four lane lists of 4)
   const char* ske = getenv("MIVS_PF_SLOT_K");  // K10 slot size override (16 or 32)
-  const int slot_k = use_r ? kPrSlotK : (ske ? (atoi(ske) > 16 ? kPfSlotKMax : 16) : kPfSlotKMax);
+  const int slot_k = ske ? (atoi(ske) > 16 ? kPfSlotKMax : 16) : kPfSlotKMax;
   ws.pf_key.reserve(sizeof(float) * (size_t)max_slots * slot_k);
   ws.pf_pos.reserve(sizeof(int) * (size_t)max_slots * slot_k);
   ws.pf_bound.reserve(sizeof(float) * (size_t)max_slots);
   // the 8 queue counters, then (K10) one convoy position per (list, chunk)
   const char* cve = getenv("MIVS_PF_CONVOY");
-  const bool convoy = !use_r && !(cve && cve[0] == '0');
+  const bool convoy = !(cve && cve[0] == '0');
   const int64_t n_cpos = convoy ? (int64_t)n_lists * tcp[1] : 0;
   ws.counter.reserve(sizeof(int) * (8 * 16 + n_cpos));
   HIPCHK(hipMemsetAsync(ws.counter.p, 0, sizeof(int) * (8 * 16 + n_cpos), s));
@@ -719,7 +704,7 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   a.row_norms = L.norms.as<float>();
   a.list_goff = goff;
   a.n_lists = n_lists;
-  a.chunk_groups = use_r ? idx->pr_G : idx->pf_G;
+  a.chunk_groups = idx->pf_G;
   a.qh = ws.qh.as<uint16_t>();
   a.qscale = ws.qscale.as<float>();
   a.qnorms = ws.qn.as<float>();
@@ -750,21 +735,14 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   }
   if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
   const int grid = std::max(8, cu_count(idx->device) / 8 * 8);
-  if (use_r) HIPCHK(launch_pr_scan(a, grid, s));
-  else HIPCHK(launch_pf_scan(a, grid, pf_scan_lds_bytes(dp, idx->pf_G), s));
+  HIPCHK(launch_pf_scan(a, grid, pf_scan_lds_bytes(dp, idx->pf_G), s));
   if (pr) HIPCHK(hipEventRecord(pr->e[2], s));
   if (a.flags & 32) {
     unsigned long long hp[16];
     HIPCHK(hipMemcpyAsync(hp, pbuf.p, sizeof(hp), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     const double w = (double)hp[7];
-    if (use_r)
-      fprintf(stderr, "[k12 phases] waves-cycles %.4g clock %.3f GHz | fetch %.3f setup %.3f loop %.3f tail %.3f | "
-              "groups/wave %.1f cycles/group %.0f slow %.4f\n", w, hp[8] ? (double)hp[7] / hp[8] * 0.1 : 0.0,
-              hp[0] / w, hp[1] / w, hp[2] / w, hp[3] / w, hp[5] / 4.0 / (w / (double)(hp[7] ? hp[7] : 1)),
-              hp[5] ? (double)hp[2] / hp[5] : 0.0, hp[5] ? (double)hp[6] / hp[5] : 0.0);
-    else
-      fprintf(stderr, "[k10 phases] waves-cycles %.4g clock %.3f GHz | fetch %.3f staging %.3f loop %.3f "
+    fprintf(stderr, "[k10 phases] waves-cycles %.4g clock %.3f GHz | fetch %.3f staging %.3f loop %.3f "
               "barrier %.3f merge %.3f | epilogues %llu slow %.4f\n", w, hp[8] ? (double)hp[7] / hp[8] * 0.1 : 0.0,
               hp[0] / w, hp[1] / w, hp[2] / w, hp[3] / w, hp[4] / w, hp[5], hp[5] ? (double)hp[6] / hp[5] : 0.0);
   }
@@ -944,7 +922,7 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
                             ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(), ws.qp_slots.as<int64_t>(),
                             ws.slot_begin.as<int64_t>(), ws.scan_tmp.p, stb, s));
     ws.pre_kth.reserve(sizeof(float) * nq);
-    pf_scan_refine(idx, s, q, nq, k, 1, nullptr, nullptr, nullptr, false, ws.pre_goff.as<int64_t>(), nl2,
+    pf_scan_refine(idx, s, q, nq, k, 1, nullptr, nullptr, nullptr, ws.pre_goff.as<int64_t>(), nl2,
                    ws.pre_kth.as<float>());
   }
   // 2. headers (pf_scan_refine left the fp16 queries, their scales and residuals in ws.qh / qscale / qres)
@@ -974,13 +952,10 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   int64_t max_items = 0;  // every list probed: the item table's bound (the probe map decides the count)
   for (int l = 0; l < L.n_lists; ++l) max_items += ceil_div(L.h_goff[l + 1] - L.h_goff[l], kRsBlockGroups);
   ws.rs_items.reserve(sizeof(int4) * (size_t)std::max<int64_t>(max_items, 1));
-  // items dealt from 8 queues of equal tile work, dynamically inside a queue (MIVS_RS_STATIC_DEAL=1: the
-  // round-1 deal -- equal item counts, every P-th item -- for A/B runs)
-  const char* dde = getenv("MIVS_RS_STATIC_DEAL");
-  const bool static_deal = dde && dde[0] == '1';
+  // items dealt from 8 queues of equal tile work, dynamically inside a queue
   ws.rs_bounds.reserve(sizeof(int) * 9);
   HIPCHK(launch_rs_items(ws.work_off.as<int>(), ws.bucket_off.as<int>(), L.goff.as<int64_t>(), L.n_lists,
-                         (int)max_items, ws.rs_items.as<int4>(), static_deal ? nullptr : ws.rs_bounds.as<int>(), s));
+                         (int)max_items, ws.rs_items.as<int4>(), ws.rs_bounds.as<int>(), s));
   RsScanArgs a{};
   a.groups_h = idx->groups_h.as<uint16_t>();
   a.row_norms = L.norms.as<float>();
@@ -1005,12 +980,11 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   ws.rs_wave_cnt.reserve(sizeof(int) * (n_waves + 1 + 8 + 1));
   a.wave_buf = ws.rs_wave_buf.as<int4>();
   a.wave_cnt = ws.rs_wave_cnt.as<int>();
-  a.queue = static_deal ? nullptr : a.wave_cnt + n_waves + 1;
-  a.bounds = static_deal ? nullptr : ws.rs_bounds.as<int>();
+  a.queue = a.wave_cnt + n_waves + 1;
+  a.bounds = ws.rs_bounds.as<int>();
   HIPCHK(hipMemsetAsync(a.wave_cnt + n_waves, 0, sizeof(int) * 10, s));  // lost flag, queue counters, spun-out
   a.flags = getenv("MIVS_RS_FLAGS") ? atoi(getenv("MIVS_RS_FLAGS")) : 0;
   if (a.flags & 2) a.flags |= 1;  // stale LDS tiles: never run an epilogue on them
-  if (getenv("MIVS_RS_ROWWAIT") && getenv("MIVS_RS_ROWWAIT")[0] == '1') a.flags |= 32;  // one vmcnt(0) per item
   Buf pbuf;
   if (a.flags & 24) {  // diagnostic: per-block clocks (8) / per-phase wave-cycles (16) to stderr
     pbuf.reserve(sizeof(unsigned long long) * (3 * grid + 16));
@@ -1087,8 +1061,7 @@ void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t
   const size_t stb = scan_tmp_bytes(ne) + sizeof(int64_t) * (size_t)ne;
   ws.scan_tmp.reserve(stb);
   const bool dump = k > kMaxK;
-  const bool use_r = pf && pr_use(idx);
-  const int qtile = pf ? (use_r ? kPrQTile : kPfQTile) : (dump ? kQTile : pick_qtile(k, idx->d, idx->G));
+  const int qtile = pf ? kPfQTile : (dump ? kQTile : pick_qtile(k, idx->d, idx->G));
   if (prof) {
     idx->last_qtile = qtile;
     idx->last_pf = pf ? 1 : 0;
@@ -1102,14 +1075,14 @@ void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t
     if (pr) HIPCHK(hipEventRecord(pr->e[3], s));
     return;
   }
-  if (prof) idx->last_scan = pf ? (use_r ? 12 : 10) : (qtile == 64 ? 31 : 3);
+  if (prof) idx->last_scan = pf ? 10 : (qtile == 64 ? 31 : 3);
   HIPCHK(launch_probe_map(probes, nq, np, n_lists, goff,
-                          pf ? (use_r ? idx->pr_G : idx->pf_G) : idx->G, qtile, ws.counts.as<int>(), ws.fill.as<int>(),
+                          pf ? idx->pf_G : idx->G, qtile, ws.counts.as<int>(), ws.fill.as<int>(),
                           ws.bucket_off.as<int>(), ws.work_off.as<int>(), ws.bucket_q.as<int64_t>(),
                           ws.bucket_slot.as<int64_t>(), ws.qp_slots.as<int64_t>(), ws.slot_begin.as<int64_t>(),
                           ws.scan_tmp.p, stb, s));
   if (pf) {
-    pf_scan_refine(idx, s, q, nq, k, np, out_d, out_i, pr, use_r, goff, n_lists);
+    pf_scan_refine(idx, s, q, nq, k, np, out_d, out_i, pr, goff, n_lists);
     if (pr) HIPCHK(hipEventRecord(pr->e[3], s));
     return;
   }

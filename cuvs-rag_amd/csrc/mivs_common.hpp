@@ -246,7 +246,7 @@ struct RsScanArgs {
   int wave_cap;              // records per stream
   int* wave_cnt;             // [grid * kRsWaves] stream lengths (may exceed wave_cap: records lost)
   int* queue;                // [8] per-queue item counters, zero at launch (dynamic dealing)
-  const int* bounds;         // [9] the queues' item ranges by tile work (k_rs_bounds); null: equal item counts
+  const int* bounds;         // [9] the queues' item ranges by tile work (k_rs_bounds)
   int flags;                 // timing experiments only (MIVS_RS_FLAGS): 1 skip epilogue, 2 skip staging,
                              // 8 per-block clocks into prof
   unsigned long long* prof;  // flags & 8: [grid][3] {start, end, tiles}

@@ -191,32 +191,25 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   // its wait, published before its signal), an index is read at the start of item j + 2, when every
   // wave has seen that signal -- every item has at least one tile. Every item is taken exactly once
   // (indices past the queues' ends read as -1, and once -1 always -1).
-  const int total = __builtin_amdgcn_readfirstlane(a.work_off[a.n_lists]);
   const int x = blockIdx.x & 7, P = gridDim.x >> 3;
-  const int hi = a.bounds ? __builtin_amdgcn_readfirstlane(a.bounds[x + 1]) : (int)((int64_t)total * (x + 1) / 8);
-  const int lo_x = a.bounds ? __builtin_amdgcn_readfirstlane(a.bounds[x]) : (int)((int64_t)total * x / 8);
+  const int hi = __builtin_amdgcn_readfirstlane(a.bounds[x + 1]);
+  const int lo_x = __builtin_amdgcn_readfirstlane(a.bounds[x]);
   int w = lo_x + (int)(blockIdx.x >> 3);
-  const int w0 = w;
   int* const s_next = s_ready + 4;  // [4] ring of upcoming item indices
   // [4] their descriptors: the grabber loads item j + 2's during item j's first tile and publishes it with that
   // tile's signal, so no wave waits on a global load of the item table at an item boundary (it read
   // items[w] there before: one L2 / HBM round trip, ~4.7k cycles per item and wave)
   int4* const s_desc = reinterpret_cast<int4*>(s_ready + 8);
-  // this workgroup's item of ordinal ord (a.queue null: the static deal); once its own queue is dry it
-  // takes items from the other queues in turn (the tail of a launch), so no CU idles while any item is left
-  auto grab = [&](int ord) {
-    if (!a.queue) {
-      const int v = w0 + ord * P;
-      return v < hi ? v : -1;
-    }
+  // this workgroup's next item; once its own queue is dry it takes items from the other queues in turn (the
+  // tail of a launch), so no CU idles while any item is left
+  auto grab = [&](int) {
     int v = lo_x + P + atomicAdd(a.queue + x, 1);
     if (v < hi) return v;
-    if (a.bounds)
-      for (int k = 1; k < 8; ++k) {
-        const int xq = (x + k) & 7;
-        v = a.bounds[xq] + P + atomicAdd(a.queue + xq, 1);
-        if (v < a.bounds[xq + 1]) return v;
-      }
+    for (int k = 1; k < 8; ++k) {
+      const int xq = (x + k) & 7;
+      v = a.bounds[xq] + P + atomicAdd(a.queue + xq, 1);
+      if (v < a.bounds[xq + 1]) return v;
+    }
     return -1;
   };
   int ii = 0;  // this workgroup's item ordinal
@@ -480,10 +473,9 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
     // The first item: wait for everything (the prologue's DMA pieces, which the wave then signals as tile 0's,
     // and the rows). Later items: the rows were issued during the previous item's last tile, in k-step order;
     // each is waited for where the first tile's k-loop first reads it (the compiler's counted vmcnt before
-    // that MFMA: every DMA piece and record store it cannot see is YOUNGER, so its count only waits longer),
-    // which gives every row load about one more tile of latency than one vmcnt(0) here (MIVS_RS_ROWWAIT=1
-    // restores that for A/B runs).
-    if (tt == 0 || (a.flags & 32)) __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
+    // that MFMA: every DMA piece and record store it cannot see is YOUNGER, so its count only waits longer;
+    // measured equal to one vmcnt(0) here, profiles/r03_k13_experiments.txt).
+    if (tt == 0) __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
     else __builtin_amdgcn_s_waitcnt(0xC07F);                             // lgkmcnt(0)
     if (tt == 0) rs_signal(s_ready);
     xnmin = xn_next;
@@ -776,41 +768,6 @@ __device__ __forceinline__ unsigned rs_rec_hits(const RsRec& r, const float4& h,
   return m;
 }
 
-// the stream offsets in LDS (binary searches there, not through L2)
-constexpr int kRsMaxStreams = 4096;
-__device__ __forceinline__ const int64_t* rs_woff_lds(const int64_t* woff, int n_waves, int64_t* sw) {
-  for (int i = threadIdx.x; i <= n_waves; i += blockDim.x) sw[i] = woff[i];
-  __syncthreads();
-  return sw;
-}
-
-// record e of the flat index -> (stream, index in the stream)
-__device__ __forceinline__ int rs_stream_of(const int64_t* woff, int n_waves, int64_t e) {
-  int lo = 0, hi = n_waves - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (woff[mid] <= e) lo = mid; else hi = mid - 1;
-  }
-  return lo;
-}
-
-template <int METRIC>
-__global__ __launch_bounds__(256) void k_rs_count(const int4* __restrict__ wave_buf, int wave_cap,
-                                                  const int64_t* __restrict__ woff, int n_waves,
-                                                  const float4* __restrict__ qhdr, const float* __restrict__ row_norms,
-                                                  unsigned long long* __restrict__ qcnt) {
-  __shared__ int64_t sw[kRsMaxStreams + 1];
-  woff = rs_woff_lds(woff, n_waves, sw);
-  const int64_t total = woff[n_waves];
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int w = rs_stream_of(woff, n_waves, e);
-    const RsRec r = rs_rec_load(wave_buf + ((int64_t)w * wave_cap + (e - woff[w])) * kRsRecInt4);
-    float xn[8];
-    const unsigned m = rs_rec_hits<METRIC>(r, qhdr[r.q], row_norms, xn);
-    if (m) atomicAdd(qcnt + r.q, (unsigned long long)__popc(m));
-  }
-}
-
 template <int METRIC>
 __device__ __forceinline__ void rs_rec_emit(const RsRec& r, unsigned m, const float4& h, const float (&xn)[8], int at,
                                             float* __restrict__ key, int* __restrict__ pos) {
@@ -824,29 +781,10 @@ __device__ __forceinline__ void rs_rec_emit(const RsRec& r, unsigned m, const fl
     }
 }
 
-template <int METRIC>
-__global__ __launch_bounds__(256) void k_rs_scatter(const int4* __restrict__ wave_buf, int wave_cap,
-                                                    const int64_t* __restrict__ woff, int n_waves,
-                                                    const float4* __restrict__ qhdr, const float* __restrict__ row_norms,
-                                                    const int64_t* __restrict__ off, int* __restrict__ fill,
-                                                    float* __restrict__ key, int* __restrict__ pos) {
-  __shared__ int64_t sw[kRsMaxStreams + 1];
-  woff = rs_woff_lds(woff, n_waves, sw);
-  const int64_t total = woff[n_waves];
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int w = rs_stream_of(woff, n_waves, e);
-    const RsRec r = rs_rec_load(wave_buf + ((int64_t)w * wave_cap + (e - woff[w])) * kRsRecInt4);
-    const float4 h = qhdr[r.q];
-    float xn[8];
-    const unsigned m = rs_rec_hits<METRIC>(r, h, row_norms, xn);
-    if (m) rs_rec_emit<METRIC>(r, m, h, xn, (int)(off[r.q] + atomicAdd(fill + r.q, __popc(m))), key, pos);
-  }
-}
-
-// The same bucketing with an LDS histogram per group of streams. Group b holds the streams of J K13
+// The bucketing with an LDS histogram per group of streams. Group b holds the streams of J K13
 // workgroups of one item queue (x = b % 8, workgroups x + 8 (J (b / 8) + t), t < J). Those workgroups take
-// consecutive items of the same lists, so their hits fall on the same lists' queries, and the contended
-// global atomics of the flat kernels become one per (group, query) with a hit.
+// consecutive items of the same lists, so their hits fall on the same lists' queries: one global atomic per
+// (group, query) with a hit instead of one per candidate (the round-2 flat kernels: 329 -> 119 us per step).
 constexpr int kRsLdsMaxQ = 32768;  // 128 KiB of int bins
 __device__ __forceinline__ int rs_group_stream(int b, int t, int J) {
   return ((b & 7) + 8 * (J * (b >> 3) + t / kRsWaves)) * kRsWaves + t % kRsWaves;
@@ -923,15 +861,14 @@ size_t rs_bucket_tmp_bytes(int nq, int n_waves) {
 template <int METRIC>
 static hipError_t rs_bucket_m(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
                               const float4* qhdr, const float* row_norms, int64_t* cand_off, float* cand_key,
-                              int* cand_pos, int64_t* qcnt, int* fill, int64_t* woff, void* stmp, int grid, bool flat,
-                              hipStream_t s) {
+                              int* cand_pos, int64_t* qcnt, int* fill, void* stmp, hipStream_t s) {
   hipError_t e;
-  // grouped LDS-histogram form when the streams come from K13's 8 item queues (n_waves = 8 queues x P
-  // workgroups x kRsWaves) and the bins fit LDS; J = workgroups of a queue per group
+  // the streams come from K13's 8 item queues (n_waves = 8 queues x P workgroups x kRsWaves) and a batch's
+  // bins fit LDS (K13 batches are at most kRsMaxBatch = kRsLdsMaxQ queries); J = workgroups of a queue per group
   const int P = n_waves / (8 * kRsWaves);
-  int J = 0;
-  if (nq <= kRsLdsMaxQ && n_waves == 8 * kRsWaves * P && P > 0 && !flat) J = P % 4 == 0 ? 4 : P % 2 == 0 ? 2 : 1;
-  if (J > 0) {
+  if (!(nq <= kRsLdsMaxQ && n_waves == 8 * kRsWaves * P && P > 0)) return hipErrorInvalidValue;
+  const int J = P % 4 == 0 ? 4 : P % 2 == 0 ? 2 : 1;
+  {
     const size_t lds = sizeof(int) * (size_t)nq;
     static const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rs_count_lds<METRIC>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -950,13 +887,6 @@ static hipError_t rs_bucket_m(const int4* wave_buf, int wave_cap, const int* wav
                        qhdr, row_norms, cand_off, fill, cand_key, cand_pos);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(k_rs_count<METRIC>, dim3((unsigned)grid), dim3(256), 0, s, wave_buf, wave_cap, woff, n_waves, qhdr,
-                     row_norms, reinterpret_cast<unsigned long long*>(qcnt));
-  e = launch_exclusive_scan_i64(qcnt, cand_off, nq + 1, stmp, s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_rs_scatter<METRIC>, dim3((unsigned)grid), dim3(256), 0, s, wave_buf, wave_cap, woff, n_waves,
-                     qhdr, row_norms, cand_off, fill, cand_key, cand_pos);
-  return hipGetLastError();
 }
 
 hipError_t launch_rs_bucket(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
@@ -970,14 +900,12 @@ hipError_t launch_rs_bucket(const int4* wave_buf, int wave_cap, const int* wave_
   hipError_t e = hipMemsetAsync(qcnt, 0, sizeof(int64_t) * ((size_t)nq + 1) + sizeof(int) * (size_t)nq, s);
   if (e != hipSuccess) return e;
   if (n_waves <= 0) return launch_exclusive_scan_i64(qcnt, cand_off, nq + 1, stmp, s);
-  if (n_waves > kRsMaxStreams) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_rs_stream_off, dim3(1), dim3(1024), 0, s, wave_cnt, n_waves, wave_cap, woff, lost);
-  const char* fe = getenv("MIVS_RS_BUCKET_FLAT");
-  const bool flat = fe && fe[0] == '1';
+  (void)grid;
   return metric == kIP ? rs_bucket_m<kIP>(wave_buf, wave_cap, wave_cnt, n_waves, nq, qhdr, row_norms, cand_off, cand_key,
-                                          cand_pos, qcnt, fill, woff, stmp, grid, flat, s)
+                                          cand_pos, qcnt, fill, stmp, s)
                        : rs_bucket_m<kL2>(wave_buf, wave_cap, wave_cnt, n_waves, nq, qhdr, row_norms, cand_off, cand_key,
-                                          cand_pos, qcnt, fill, woff, stmp, grid, flat, s);
+                                          cand_pos, qcnt, fill, stmp, s);
 }
 
 // the smallest row norm of every group (K13's filter bound; pad rows are +inf, every group has a real row)

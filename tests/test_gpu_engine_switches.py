@@ -59,14 +59,10 @@ SEARCH_SWITCHES = [
     {"MIVS_PF_ROWSTAT": "0", "MIVS_PF_PAIR": "0", "MIVS_PF_DEPTH": "8"},
     {"MIVS_PF_ROWSTAT": "0", "MIVS_PF_CONVOY": "0"},
     {"MIVS_PF_ROWSTAT": "0", "MIVS_PF_SLOT_K": "16"},
-    {"MIVS_PF_ROWSTAT": "0", "MIVS_PF_REG": "1"},                     # K12 search
     {"MIVS_RS_PRE_DIV": "1"},
     {"MIVS_RS_PRE_DIV": "16"},
-    {"MIVS_RS_BUCKET_FLAT": "1"},                                     # K13 streams bucketed by flat atomics
-    {"MIVS_RS_STATIC_DEAL": "1"},                                     # K13 items dealt statically
     {"MIVS_RS_FLAGS": "24"},                                          # K13 clocks (stderr only)
     {"MIVS_RS_WAVE_CAP": "2"},                                        # K13 streams overflow: the fallback
-    {"MIVS_RS_ROWWAIT": "1"},                                         # K13 rows waited at item start
     {"MIVS_PF_ROWSTAT": "0", "MIVS_PF_FLAGS": "32"},                  # K10 phase clocks (stderr only)
 ]
 
@@ -93,8 +89,7 @@ def test_ivf_default_matches_oracle(ivf, flat_data):
     np.testing.assert_array_equal(_bits(d), _bits(od))
 
 
-@pytest.mark.parametrize("env", [{"MIVS_PF_CHUNK_ROWS": "2048"}, {"MIVS_PR_CHUNK_ROWS": "1024", "MIVS_PF_REG": "1",
-                                                                    "MIVS_PF_ROWSTAT": "0"}])
+@pytest.mark.parametrize("env", [{"MIVS_PF_CHUNK_ROWS": "2048"}])
 def test_ivf_chunk_rows_switch_same_bits(ivf, flat_data, monkeypatch, env):
     """work-item sizes are fixed when the fp16 copy is made (build / set_prefilter(True))"""
     idx, _ = ivf
