@@ -12,6 +12,6 @@ for r in $(seq 1 $REPS); do
   for e in "$@"; do
     i=$((i+1))
     eval env $e timeout -k 10 300 python -u bench.py $QB --json-out $OUT/v${i}_$r.json > $OUT/v${i}_$r.log 2>&1 || { echo "run v$i failed"; tail -3 $OUT/v${i}_$r.log; exit 3; }
-    python3 -c "import json;j=json.load(open('$OUT/v${i}_$r.json'));r=j['roofline'];print('v$i [$e] rep $r: value',j['value'],'ms',j['ms_per_step'],'k13',r['launch_ms'],'frac',r['frac'])"
+    python3 -c "import json;j=json.load(open('$OUT/v${i}_$r.json'));r=j['roofline'];print('v$i [$e] rep $r: value',j['value'],'ms',j['ms_per_step'],'k13',r['launch_ms'],'frac',r['frac'],'cand',j['search_stats']['candidates'],'ovf',j['search_stats']['overflow_queries'])"
   done
 done
