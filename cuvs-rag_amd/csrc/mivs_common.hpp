@@ -248,7 +248,7 @@ struct RsScanArgs {
   int* queue;                // [8] per-queue item counters, zero at launch (dynamic dealing)
   const int* bounds;         // [9] the queues' item ranges by tile work (k_rs_bounds)
   int flags;                 // timing experiments only (MIVS_RS_FLAGS): 1 skip epilogue, 2 skip staging,
-                             // 8 per-block clocks into prof
+                             // 4 keep the rows at item transitions, 8 per-block clocks into prof, 16 phase clocks
   unsigned long long* prof;  // flags & 8: [grid][3] {start, end, tiles}
 };
 

@@ -265,8 +265,10 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   auto group_rsrc = [&](int grp) {
     return uniform_rsrc(reinterpret_cast<const char*>(a.groups_h) + (int64_t)grp * (NB * 512), NB * 512);
   };
+  // the rows are read once per search: non-temporal policy (aux = 2), 1.5-2.5 % shorter launches than the default
+  // policy in alternating same-box runs (profiles/r03_k13_experiments.txt)
   auto ld_rows = [&](__amdgpu_buffer_rsrc_t r, int i) {  // register i = 2 t + rb
-    return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(r, lane_off, (i >> 1) * 2048 + (i & 1) * 256, 0));
+    return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(r, lane_off, (i >> 1) * 2048 + (i & 1) * 256, 2));
   };
   if (tid == 0) {
     *s_ready = 0;
@@ -390,7 +392,8 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
       const v4i sdesc = uniform_desc(simg, stage ? (int)IMG : 0);
       const int nxt = cur + 1 == NBUF ? 0 : cur + 1;
       char* sbuf = smem + nxt * BUF;
-      const bool reload = LAST && has_next;
+      // (flags & 4, timing only: keep the rows, i.e. measure the item transitions' cost)
+      const bool reload = LAST && has_next && !(a.flags & 4);
       const __amdgpu_buffer_rsrc_t nrs = group_rsrc(gvn ? gnx : nx.g0);
       f32x4 acc4[4] = {zero4, zero4, zero4, zero4};
       // (a wave without a group in this block runs the MFMAs on stale rows; its epilogue is skipped).
@@ -439,7 +442,7 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
       // signal the next tile: this wave's reads of this one are done (lgkmcnt(0): the headers are in) and
       // its DMA pieces of the next have landed -- vmcnt counts, in issue order, only the next item's rows
       // issued after its last piece beyond them
-      rs_wait_vm(LAST && has_next ? ROWS_AFTER : 0);
+      rs_wait_vm(reload ? ROWS_AFTER : 0);
       if (grabber) {
         s_next[(ii + 3) & 3] = grabbed;
         s_desc[(ii + 2) & 3] = desc2;
