@@ -726,6 +726,10 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   HIPCHK(launch_fill_i32(ws.qtheta.as<int>(), nq, (int)kPfOrdInf, s));
   a.qtheta = ws.qtheta.as<unsigned>();
   a.k = k;
+  // K13's pre-pass (kth_out): each list sample is scanned by one tile -- its rows are read once
+  // (MIVS_PF_PRE_NT=0: the default policy, A/B runs)
+  const char* pne = getenv("MIVS_PF_PRE_NT");
+  a.rows_nt = kth_out != nullptr && !(pne && pne[0] == '0');
   a.flags = getenv("MIVS_PF_FLAGS") ? atoi(getenv("MIVS_PF_FLAGS")) : 0;
   Buf pbuf;
   if (a.flags & 32) {  // diagnostic: K10 phase clocks to stderr

@@ -214,6 +214,8 @@ struct PfScanArgs {
   int* chunk_pos;             // [n_lists * chunk_stride] K10 convoy: the pair a chunk's tiles are scanning
                               // (zeroed before launch), or nullptr (every tile scans from pair 0)
   int chunk_stride;           // max chunks per list
+  int rows_nt;                // 1: the rows are read once (K13's pre-pass: one tile per list sample) -- load them
+                              // with the non-temporal policy (pair mode only)
 };
 
 // K13 row-stationary pre-filter scan (rsscan.hip): work item = (list, block of

@@ -36,6 +36,12 @@ constexpr int kPfSmall = kPfQTile * 8 * 2 + kPfQTile * 4 * 2 + 16;  // s_q, s_sl
 constexpr int kPfMergeBytes = kPfQTile * 16 * kPfLaneK * 8;          // [64 queries][16 lane lists][KL] (key, pos)
 
 __device__ __forceinline__ h8 ld_h8(const uint16_t* p) { return *reinterpret_cast<const h8*>(p); }
+// a row operand; NT: non-temporal policy (rows read once)
+template <bool NT>
+__device__ __forceinline__ h8 ld_row_h8(const uint16_t* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const h8*>(p));
+  else return *reinterpret_cast<const h8*>(p);
+}
 
 // ---- 16-lane (DPP row) reductions: a butterfly over quad_perm [1,0,3,2], quad_perm [2,3,0,1],
 // row_half_mirror, row_mirror -- every lane of the row ends with the row's result, without the LDS
@@ -150,7 +156,7 @@ __device__ __forceinline__ float pf_theta(const float* __restrict__ l8, float de
 // eighth of the (list, chunk, tile)-ordered items, so the query tiles of one chunk run at the same
 // time on CUs sharing an L2 and all but the first read the chunk's rows as L2 hits. A workgroup
 // whose queue is empty takes items from the next queues.
-template <int METRIC, int D, int R>
+template <int METRIC, int D, int R, bool NT = false>
 __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int64_t* s_q = reinterpret_cast<int64_t*>(smem);          // [64] query ids (-1: empty)
@@ -337,8 +343,8 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
         h8 ra[D], rb[D];
 #pragma unroll
         for (int u = 0; u < D; ++u) {
-          ra[u] = ld_h8(na + (ls + u) * 512);
-          rb[u] = ld_h8(nbp + (ls + u) * 512);
+          ra[u] = ld_row_h8<NT>(na + (ls + u) * 512);
+          rb[u] = ld_row_h8<NT>(nbp + (ls + u) * 512);
           __builtin_amdgcn_sched_barrier(0);
         }
         ls += D;
@@ -360,8 +366,8 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
             a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[u], bq1[u & 1], a1, 0, 0, 0);
             b0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(rb[u], bq0[u & 1], b0, 0, 0, 0);
             b1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(rb[u], bq1[u & 1], b1, 0, 0, 0);
-            ra[u] = ld_h8(na + (ls + u) * 512);
-            rb[u] = ld_h8(nbp + (ls + u) * 512);
+            ra[u] = ld_row_h8<NT>(na + (ls + u) * 512);
+            rb[u] = ld_row_h8<NT>(nbp + (ls + u) * 512);
             __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
             __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // MFMA
             __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);  // VMEM read
@@ -1335,12 +1341,12 @@ size_t pf_scan_lds_bytes(int dp, int chunk_groups) {
   return kPfSmall + (size_t)kPfQTile * 18 * 4 + norms + (b > (size_t)kPfMergeBytes ? b : (size_t)kPfMergeBytes);
 }
 
-template <int METRIC, int D, int R>
+template <int METRIC, int D, int R, bool NT = false>
 static hipError_t launch_pf_scan_md(const PfScanArgs& a, int grid, size_t lds, hipStream_t s) {
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pf_scan<METRIC, D, R>),
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pf_scan<METRIC, D, R, NT>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL((k_pf_scan<METRIC, D, R>), dim3(grid), dim3(kPfThreads), lds, s, a);
+  hipLaunchKernelGGL((k_pf_scan<METRIC, D, R, NT>), dim3(grid), dim3(kPfThreads), lds, s, a);
   return hipGetLastError();
 }
 
@@ -1349,8 +1355,10 @@ static hipError_t launch_pf_scan_m(const PfScanArgs& a, int grid, size_t lds, hi
   // default: two groups per pass with 6-deep rings (half the LDS operand traffic per flop: the kernel is
   // power-bound); MIVS_PF_PAIR=0: one group per pass with MIVS_PF_DEPTH (16) k-steps in flight
   const int nk = a.dp / 16;
-  if (pf_pair_mode()) return nk % 6 == 0 ? launch_pf_scan_md<METRIC, 6, 2>(a, grid, lds, s)
-                               : launch_pf_scan_md<METRIC, 4, 2>(a, grid, lds, s);
+  if (pf_pair_mode()) {
+    if (a.rows_nt && nk % 6 == 0) return launch_pf_scan_md<METRIC, 6, 2, true>(a, grid, lds, s);
+    return nk % 6 == 0 ? launch_pf_scan_md<METRIC, 6, 2>(a, grid, lds, s) : launch_pf_scan_md<METRIC, 4, 2>(a, grid, lds, s);
+  }
   const int dsel = getenv("MIVS_PF_DEPTH") ? atoi(getenv("MIVS_PF_DEPTH")) : 16;
   if (dsel >= 16 && nk % 16 == 0) return launch_pf_scan_md<METRIC, 16, 1>(a, grid, lds, s);
   if (dsel >= 8 && nk % 8 == 0) return launch_pf_scan_md<METRIC, 8, 1>(a, grid, lds, s);

@@ -788,30 +788,58 @@ __device__ __forceinline__ void rs_rec_emit(const RsRec& r, unsigned m, const fl
 // workgroups of one item queue (x = b % 8, workgroups x + 8 (J (b / 8) + t), t < J). Those workgroups take
 // consecutive items of the same lists, so their hits fall on the same lists' queries: one global atomic per
 // (group, query) with a hit instead of one per candidate (the round-2 flat kernels: 329 -> 119 us per step).
+// The group's records are one flat index space (a stream's ~100 records would leave most of a 1024-thread
+// block idle if the streams were walked one after another): record e of the group is record e - pre[t] of
+// its stream t, found in an LDS prefix of the kRsWaves * J stream lengths.
 constexpr int kRsLdsMaxQ = 32768;  // 128 KiB of int bins
+constexpr int kRsMaxGroupStreams = 64;
 __device__ __forceinline__ int rs_group_stream(int b, int t, int J) {
   return ((b & 7) + 8 * (J * (b >> 3) + t / kRsWaves)) * kRsWaves + t % kRsWaves;
 }
 
-template <int METRIC>
-__device__ __forceinline__ void rs_group_hist(const int4* __restrict__ wave_buf, int wave_cap,
-                                              const int* __restrict__ wave_cnt, int J, int nq,
-                                              const float4* __restrict__ qhdr, const float* __restrict__ row_norms,
-                                              int* bins) {
-  for (int i = threadIdx.x; i < nq; i += blockDim.x) bins[i] = 0;
-  __syncthreads();
-  for (int t = 0; t < kRsWaves * J; ++t) {
-    const int w = rs_group_stream(blockIdx.x, t, J);
-    const int n = min(wave_cnt[w], wave_cap);
-    const int4* sb = wave_buf + (int64_t)w * wave_cap * kRsRecInt4;
-    for (int e = threadIdx.x; e < n; e += blockDim.x) {
-      const RsRec r = rs_rec_load(sb + (int64_t)e * kRsRecInt4);
-      float xn[8];
-      const unsigned m = rs_rec_hits<METRIC>(r, qhdr[r.q], row_norms, xn);
-      if (m) atomicAdd(bins + r.q, __popc(m));
+// the group's stream prefix in LDS (pre[0..S], S = kRsWaves * J); returns the group's record count
+__device__ __forceinline__ int rs_group_prefix(const int* __restrict__ wave_cnt, int wave_cap, int J, int* pre) {
+  const int S = kRsWaves * J;
+  if (threadIdx.x < 64) {
+    const int t = threadIdx.x;
+    int n = t < S ? min(wave_cnt[rs_group_stream(blockIdx.x, t, J)], wave_cap) : 0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(n, o);
+      if (t >= o) n += y;
     }
+    if (t < S) pre[t + 1] = n;
+    if (t == 0) pre[0] = 0;
   }
   __syncthreads();
+  return pre[S];
+}
+
+// record e of the group: its stream's base pointer
+__device__ __forceinline__ const int4* rs_group_rec(const int4* __restrict__ wave_buf, int wave_cap, int J,
+                                                    const int* pre, int e) {
+  const int S = kRsWaves * J;
+  int t = 0;
+  while (t + 1 < S && pre[t + 1] <= e) ++t;  // (S <= 64: a short scan of LDS-resident prefixes)
+  const int w = rs_group_stream(blockIdx.x, t, J);
+  return wave_buf + ((int64_t)w * wave_cap + (e - pre[t])) * kRsRecInt4;
+}
+
+template <int METRIC>
+__device__ __forceinline__ int rs_group_hist(const int4* __restrict__ wave_buf, int wave_cap,
+                                             const int* __restrict__ wave_cnt, int J, int nq,
+                                             const float4* __restrict__ qhdr, const float* __restrict__ row_norms,
+                                             int* bins, int* pre) {
+  for (int i = threadIdx.x; i < nq; i += blockDim.x) bins[i] = 0;
+  const int n = rs_group_prefix(wave_cnt, wave_cap, J, pre);  // (its barrier also orders the zeroing)
+  for (int e = threadIdx.x; e < n; e += blockDim.x) {
+    const RsRec r = rs_rec_load(rs_group_rec(wave_buf, wave_cap, J, pre, e));
+    float xn[8];
+    const unsigned m = rs_rec_hits<METRIC>(r, qhdr[r.q], row_norms, xn);
+    if (m) atomicAdd(bins + r.q, __popc(m));
+  }
+  __syncthreads();
+  return n;
 }
 
 template <int METRIC>
@@ -820,7 +848,8 @@ __global__ __launch_bounds__(1024) void k_rs_count_lds(const int4* __restrict__ 
                                                        const float4* __restrict__ qhdr, const float* __restrict__ row_norms,
                                                        unsigned long long* __restrict__ qcnt) {
   extern __shared__ int bins[];
-  rs_group_hist<METRIC>(wave_buf, wave_cap, wave_cnt, J, nq, qhdr, row_norms, bins);
+  __shared__ int pre[kRsMaxGroupStreams + 1];
+  rs_group_hist<METRIC>(wave_buf, wave_cap, wave_cnt, J, nq, qhdr, row_norms, bins, pre);
   for (int i = threadIdx.x; i < nq; i += blockDim.x) {
     const int c = bins[i];
     if (c) atomicAdd(qcnt + i, (unsigned long long)c);
@@ -835,24 +864,20 @@ __global__ __launch_bounds__(1024) void k_rs_scatter_lds(const int4* __restrict_
                                                          const int64_t* __restrict__ off, int* __restrict__ fill,
                                                          float* __restrict__ key, int* __restrict__ pos) {
   extern __shared__ int bins[];
-  rs_group_hist<METRIC>(wave_buf, wave_cap, wave_cnt, J, nq, qhdr, row_norms, bins);
+  __shared__ int pre[kRsMaxGroupStreams + 1];
+  const int n = rs_group_hist<METRIC>(wave_buf, wave_cap, wave_cnt, J, nq, qhdr, row_norms, bins, pre);
   // this group's range of each query's run (< 2^31 entries in all: fits an int)
   for (int i = threadIdx.x; i < nq; i += blockDim.x) {
     const int c = bins[i];
     if (c) bins[i] = (int)(off[i] + atomicAdd(fill + i, c));
   }
   __syncthreads();
-  for (int t = 0; t < kRsWaves * J; ++t) {
-    const int w = rs_group_stream(blockIdx.x, t, J);
-    const int n = min(wave_cnt[w], wave_cap);
-    const int4* sb = wave_buf + (int64_t)w * wave_cap * kRsRecInt4;
-    for (int e = threadIdx.x; e < n; e += blockDim.x) {
-      const RsRec r = rs_rec_load(sb + (int64_t)e * kRsRecInt4);
-      const float4 h = qhdr[r.q];
-      float xn[8];
-      const unsigned m = rs_rec_hits<METRIC>(r, h, row_norms, xn);
-      if (m) rs_rec_emit<METRIC>(r, m, h, xn, atomicAdd(bins + r.q, __popc(m)), key, pos);
-    }
+  for (int e = threadIdx.x; e < n; e += blockDim.x) {
+    const RsRec r = rs_rec_load(rs_group_rec(wave_buf, wave_cap, J, pre, e));
+    const float4 h = qhdr[r.q];
+    float xn[8];
+    const unsigned m = rs_rec_hits<METRIC>(r, h, row_norms, xn);
+    if (m) rs_rec_emit<METRIC>(r, m, h, xn, atomicAdd(bins + r.q, __popc(m)), key, pos);
   }
 }
 
@@ -870,7 +895,11 @@ static hipError_t rs_bucket_m(const int4* wave_buf, int wave_cap, const int* wav
   // bins fit LDS (K13 batches are at most kRsMaxBatch = kRsLdsMaxQ queries); J = workgroups of a queue per group
   const int P = n_waves / (8 * kRsWaves);
   if (!(nq <= kRsLdsMaxQ && n_waves == 8 * kRsWaves * P && P > 0)) return hipErrorInvalidValue;
-  const int J = P % 4 == 0 ? 4 : P % 2 == 0 ? 2 : 1;
+  // J: K13 workgroups per bucketing group (MIVS_RS_BUCKET_J, A/B runs: fewer means more groups and more global
+  // atomics per query, more means fewer, longer groups)
+  const char* je = getenv("MIVS_RS_BUCKET_J");
+  const int jw = je ? atoi(je) : 1;
+  const int J = (jw >= 4 && P % 4 == 0) ? 4 : (jw >= 2 && P % 2 == 0) ? 2 : 1;
   {
     const size_t lds = sizeof(int) * (size_t)nq;
     static const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rs_count_lds<METRIC>),
