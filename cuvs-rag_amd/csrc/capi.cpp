@@ -132,6 +132,7 @@ struct mivs_index_s {
   Buf pq_codes, pq_books;
   // fp16 copy of the lists for the K10 pre-filter; empty = exact scan only
   Buf groups_h;
+  Buf rows_rm;     // K11: the fp32 lists row-major (built with groups_h when HBM has room; MIVS_PF_ROWMAJOR=0: off)
   Buf group_nmin;  // K13: the smallest row norm of every 32-row group (built with groups_h)
   int hx_exp = 0;
   float x_norm_max = 0.0f, x_res_max = 0.0f;
@@ -615,6 +616,7 @@ bool pf_default_on() {
 void pf_enable(mivs_index_s* idx, hipStream_t s) {
   const ListSet& L = idx->lists;
   idx->groups_h.release();
+  idx->rows_rm.release();
   if (L.n_groups == 0 || idx->dp % 64 != 0) return;
   const int64_t nslot = L.n_groups * (int64_t)kGroupRows;
   Buf st;
@@ -640,6 +642,16 @@ void pf_enable(mivs_index_s* idx, hipStream_t s) {
   std::memcpy(&resmax, &h[2], 4);
   idx->x_norm_max = sqrtf(normmax) * (1.0f + 0x1p-12f);
   idx->x_res_max = resmax;
+  {  // K11's row-major copy (+ the fp32 lists' size again): only with a quarter of it (>= 4 GiB) to spare beside it
+    const char* rme = getenv("MIVS_PF_ROWMAJOR");
+    const size_t bytes = sizeof(float) * (size_t)nslot * idx->dp;
+    size_t fr = 0, tot = 0;
+    if (!(rme && rme[0] == '0') && hipMemGetInfo(&fr, &tot) == hipSuccess &&
+        fr > bytes + std::max<size_t>(bytes / 4, (size_t)4 << 30)) {
+      idx->rows_rm.reserve(bytes);
+      HIPCHK(launch_groups_to_rows(L.groups.as<float>(), L.n_groups, idx->dp, idx->rows_rm.as<float>(), s));
+    }
+  }
   std::vector<int64_t> c(L.n_lists);
   const char* ce = getenv("MIVS_PF_CHUNK_ROWS");
   // rows per work item: as many as the LDS holds the norms of beside the query tile (the tile's
@@ -781,6 +793,7 @@ void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_
   r.dp = dp;
   r.metric = idx->metric;
   r.groups = L.groups.as<float>();
+  r.rows_rm = idx->rows_rm.p ? idx->rows_rm.as<float>() : nullptr;
   r.row_norms = L.norms.as<float>();
   r.row_ids = L.ids.as<int64_t>();
   r.queries = q;
@@ -1462,6 +1475,7 @@ int32_t mivs_ivf_flat_extend(mivs_index_t idx, void* stream, const float* d_new,
     HIPCHK(hipStreamSynchronize(s));
     const bool had_pf = idx->groups_h.p != nullptr;
     idx->groups_h.release();
+    idx->rows_rm.release();
     pack_lists(L, rows.as<float>(), d, idx->dp, perm.as<int64_t>(), h_off, 0, ids.as<int64_t>(), idx->G, s);
     if (had_pf) pf_enable(idx, s);
     HIPCHK(hipStreamSynchronize(s));
@@ -2142,6 +2156,7 @@ int32_t mivs_index_set_prefilter(mivs_index_t idx, void* stream, int32_t enable)
       if (!idx->groups_h.p) pf_enable(idx, s);
     } else {
       idx->groups_h.release();
+      idx->rows_rm.release();
     }
   });
 }

@@ -279,6 +279,7 @@ struct PfRefineArgs {
   int64_t nq;
   int k, d, dp, metric;
   const float* groups;        // fp32 lists (group layout) for the exact recompute
+  const float* rows_rm;       // optional: the same rows row-major ([slot][dp], launch_groups_to_rows)
   const float* row_norms;
   const int64_t* row_ids;
   const float* queries;       // fp32 [nq][d]
@@ -365,6 +366,9 @@ hipError_t launch_gather_ids(const int64_t* src, const int64_t* idx, int64_t n, 
 constexpr unsigned kPfOrdInf = 0xFF800000u;  // order mapping of +inf (qtheta's initial value)
 // fp32 groups -> fp16 groups scaled by 2^hx_exp (FTZ below the fp16 normal range), per-index maxima of
 // ||x - x_h|| and max |x| (as float bits, atomicMax) into stats[0..1] (zeroed by the caller)
+// the fp32 lists row-major ([n_groups * 32][dp], group-row order): K11's exact recompute reads a candidate's 3 KiB
+// contiguously instead of 32 B from each of 96 lines shared with three other rows
+hipError_t launch_groups_to_rows(const float* groups, int64_t n_groups, int dp, float* out, hipStream_t s);
 hipError_t launch_groups_to_half(const float* groups, int64_t n_groups, int dp, int hx_exp, uint16_t* out,
                                  unsigned* stats, hipStream_t s);
 hipError_t launch_abs_max(const float* x, int64_t n, unsigned* out, hipStream_t s);

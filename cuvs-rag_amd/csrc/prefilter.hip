@@ -658,13 +658,16 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
   if (live && !ovf && lane < cnt) {
     const int pos = s_cp[wv][lane];
     const int nb = a.dp >> 3;
-    const float* rowp = a.groups + ((int64_t)(pos >> 5) * nb * kGroupRows + (pos & 31)) * 8;
+    // the row's block b: 8 floats at rowp + b * bstride (row-major copy: contiguous; group layout: 1 KiB apart)
+    const float* rowp = a.rows_rm ? a.rows_rm + (int64_t)pos * a.dp
+                                  : a.groups + ((int64_t)(pos >> 5) * nb * kGroupRows + (pos & 31)) * 8;
+    const int64_t bstride = a.rows_rm ? 8 : 256;
     const float* qv = s_qv[wv];
     float acc = 0.0f;
-#pragma unroll 4
+#pragma unroll 12
     for (int b = 0; b < nb; ++b) {
-      const float4 x0 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * 256);
-      const float4 x1 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * 256 + 4);
+      const float4 x0 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride);
+      const float4 x1 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride + 4);
       const float4 y0 = *reinterpret_cast<const float4*>(qv + 8 * b);
       const float4 y1 = *reinterpret_cast<const float4*>(qv + 8 * b + 4);
       acc = fmaf(x0.x, y0.x, acc); acc = fmaf(x1.x, y1.x, acc);
@@ -1419,6 +1422,28 @@ hipError_t launch_pf_refine(const PfRefineArgs& a, hipStream_t s) {
   }
   if (a.metric == kIP) hipLaunchKernelGGL(k_pf_refine<kIP>, pf_grid(a.nq, 4), dim3(256), 0, s, a);
   else hipLaunchKernelGGL(k_pf_refine<kL2>, pf_grid(a.nq, 4), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+// thread = (row slot, 8-dim block), block fastest: every store is 32 B of one row, consecutive threads contiguous
+__global__ void k_groups_to_rows(const float* __restrict__ groups, int64_t n_groups, int dp, float* __restrict__ out) {
+  const int nb = dp >> 3;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_groups * kGroupRows * nb) return;
+  const int64_t slot = t / nb;
+  const int b = (int)(t - slot * nb);
+  const int64_t g = slot / kGroupRows;
+  const int r = (int)(slot - g * kGroupRows);
+  const float4* src = reinterpret_cast<const float4*>(groups + ((g * nb + b) * kGroupRows + r) * 8);
+  float4* dst = reinterpret_cast<float4*>(out + slot * dp + 8 * b);
+  dst[0] = src[0];
+  dst[1] = src[1];
+}
+
+hipError_t launch_groups_to_rows(const float* groups, int64_t n_groups, int dp, float* out, hipStream_t s) {
+  const int64_t n = n_groups * kGroupRows * (dp >> 3);
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_groups_to_rows, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, groups, n_groups, dp, out);
   return hipGetLastError();
 }
 
