@@ -181,6 +181,7 @@ constexpr int kPfLaneK = 8;      // per-lane approximate list length in K10
 constexpr int kPfSlotKMax = 32;  // approximate candidates kept per slot: 16 for k <= 10, else 32
 constexpr int kPfMaxK = 16;      // largest k served by the pre-filter path
 constexpr int kPfCap = 64;       // refine capacity (window candidates per query)
+constexpr int kPfSelRegs = 8;    // K11 phase 1: candidates per query held in registers (x 64) for the radix select
 constexpr int kPfChunkGroups = 512;  // default groups (16384 rows) per K10 work item (MIVS_PF_CHUNK_ROWS)
 
 struct PfScanArgs {

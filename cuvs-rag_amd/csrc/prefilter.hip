@@ -585,8 +585,32 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
   // (K13: slot_k = 1 and slot_begin the per-query CSR runs of unsorted candidates)
   const bool cnt_ovf = a.force_ovf && *a.force_ovf;
 
-  // phase 1: Ak = k-th smallest approximate key (running top-k over the lanes, K7's ballot insertion)
+  // phase 1: Ak = k-th smallest approximate key. Up to kPfSelRegs * 64 candidates (K13's runs: ~200 per query at the
+  // benchmark shape): held in registers, a 32-step radix select over their orderable bits -- the largest u with
+  // fewer than k keys below it is the k-th smallest (ties counted), no shuffles; more: the running top-k
+  // (K7's ballot insertion). Both return the same value.
   float mk = INFINITY, tk = INFINITY;
+  const int64_t n_c = c1 - sb * a.slot_k;
+  if (n_c <= kPfSelRegs * 64) {
+    uint32_t u[kPfSelRegs];
+#pragma unroll
+    for (int i = 0; i < kPfSelRegs; ++i) {
+      const int64_t cc = sb * a.slot_k + i * 64 + lane;
+      const float f = cc < c1 ? a.slot_key[cc] : INFINITY;
+      const uint32_t b = __float_as_uint(f == 0.0f ? 0.0f : f);  // (-0 and +0: one key)
+      u[i] = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    }
+    uint32_t ans = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+      const uint32_t t = ans | (1u << bit);
+      int below = 0;
+#pragma unroll
+      for (int i = 0; i < kPfSelRegs; ++i) below += __popcll(__ballot(u[i] < t));
+      if (below < k) ans = t;
+    }
+    const uint32_t b = (ans & 0x80000000u) ? (ans & 0x7FFFFFFFu) : ~ans;
+    tk = __uint_as_float(b);
+  } else
   for (int64_t c = sb * a.slot_k; c < c1; c += 64) {
     const int64_t cc = c + lane;
     const float ck = cc < c1 ? a.slot_key[cc] : INFINITY;

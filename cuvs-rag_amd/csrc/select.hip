@@ -289,12 +289,6 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
 constexpr int kSmallPer = 16;
 constexpr int kSmallWaves = 4;
 
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-
 template <int METRIC>
 __global__ __launch_bounds__(64 * kSmallWaves) void k_select_small(SelectArgs a) {
   __shared__ uint32_t s_u[kSmallWaves][64];
@@ -311,15 +305,16 @@ __global__ __launch_bounds__(64 * kSmallWaves) void k_select_small(SelectArgs a)
   for (int i = 0; i < kSmallPer; ++i) {
     const int t = lane + 64 * i;
     u[i] = 0xFFFFFFFFu;
+    bool ok = false;
     if (t < n_total) {
       const Cand c = cand_key<false, METRIC>(a, base, t);
       if (c.valid) {
         u[i] = c.u;
-        ++nv;
+        ok = true;
       }
     }
+    nv += __popcll(__ballot(ok));
   }
-  nv = wave_sum(nv);
   const int need = nv < k ? nv : k;
   // the valid keys' range bounds the search (a few of the 32 bits once the keys share an exponent)
   uint32_t umin = 0xFFFFFFFFu, umax = 0u;
@@ -335,11 +330,13 @@ __global__ __launch_bounds__(64 * kSmallWaves) void k_select_small(SelectArgs a)
     umin = a0 < umin ? a0 : umin;
     umax = a1 > umax ? a1 : umax;
   }
+  // counts over the wave by ballot + popcount (scalar): a shuffle reduction per count put six LDS round trips
+  // on every step of the searches below
   auto count_le = [&](uint32_t m) {
     int c = 0;
 #pragma unroll
-    for (int i = 0; i < kSmallPer; ++i) c += u[i] <= m ? 1 : 0;  // (invalid = 0xFFFFFFFF > every valid m)
-    return wave_sum(c);
+    for (int i = 0; i < kSmallPer; ++i) c += __popcll(__ballot(u[i] <= m));  // (invalid = 0xFFFFFFFF > every valid m)
+    return c;
   };
   uint32_t T = 0;
   int64_t I = LLONG_MAX;  // among keys == T: ids <= I are chosen
@@ -358,8 +355,8 @@ __global__ __launch_bounds__(64 * kSmallWaves) void k_select_small(SelectArgs a)
         int c = 0;
 #pragma unroll
         for (int i = 0; i < kSmallPer; ++i)
-          if (u[i] == T && cand_id<false>(a, base, lane + 64 * i) <= x) ++c;
-        return wave_sum(c);
+          c += __popcll(__ballot(u[i] == T && cand_id<false>(a, base, lane + 64 * i) <= x));
+        return c;
       };
       int64_t ilo = 0, ihi = LLONG_MAX;  // (valid candidates have ids >= 0; count_id(LLONG_MAX) = c_eq >= m)
       while (ilo < ihi) {
