@@ -185,7 +185,12 @@ def cpu_baseline(idx, q_host, gt, n_probes, k, target_s, rank_log):
     nr = min(ns, gt.shape[0])
     rec = recall_at_k(ci[:nr], gt[:nr]) if nr > 0 else None
     del rows
-    return {"value": ns / dt, "unit": "QPS", "cores": threads, "kind": "port", "host": host_cpu_info(),
+    host = host_cpu_info()
+    return {"value": ns / dt, "unit": "QPS", "cores": threads, "kind": "port", "host": host,
+            "cores_note": f"{threads} threads = this job's CPU share (the harness's OMP_NUM_THREADS: one GPU's share of "
+                          f"a {host.get('physical_cores')}-core / {host.get('logical_cpus')}-thread node); the "
+                          f"search is OpenMP over queries, so the whole node's cores would scale it by at most "
+                          f"{host.get('logical_cpus') or 0} / {threads}",
             "sample": f"{ns} of the {q_host.shape[0]} benchmark queries, same index (copied to host), n_probes="
                       f"{n_probes}, k={k}; FAISS IndexIVFFlat search algorithm restated in oracle/cpu_baseline.c "
                       f"(faiss not installed); {dt:.1f} s",
