@@ -25,6 +25,7 @@ import glob
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -76,6 +77,8 @@ def parse():
                     help="side line (N=1 launch): the reference's one-process shape -- every visible GPU holds a "
                          "rows-per-GPU shard, ParallelIndexBuilder threads build them, SearchResultAggregator "
                          "searches them and merges over RCCL (LocalComm); 0 to skip")
+    ap.add_argument("--single-process-timeout", type=float, default=240.0,
+                    help="seconds the one-process multi-GPU side line may take before it is abandoned")
     ap.add_argument("--json-out", default="")
     return ap.parse_args()
 
@@ -659,14 +662,32 @@ def main():
             rl(f"[large-k] side line failed: {e!r}")
 
     single = None
+    single_hung = False
     if rank == 0 and world == 1 and a.single_process:
-        try:
-            single = single_process_side_line(a, idx, q, res_i, rl)
-        except Exception as e:  # the IVF line stands without it
-            rl(f"[single-process] side line failed: {e!r}")
+        # on a multi-GPU node this is the only place the one-process RCCL path (ncclCommInitAll over every local
+        # device) runs at P > 1: a watchdog keeps a hang there from taking the IVF-Flat line with it
+        box = {}
+
+        def _side():
+            try:
+                box["r"] = single_process_side_line(a, idx, q, res_i, rl)
+            except Exception as e:  # the IVF line stands without it
+                box["e"] = e
+
+        th = threading.Thread(target=_side, daemon=True)
+        th.start()
+        th.join(timeout=a.single_process_timeout)
+        if th.is_alive():
+            single_hung = True
+            single = {"error": f"did not finish within {a.single_process_timeout} s (abandoned)"}
+            rl(f"[single-process] side line did not finish within {a.single_process_timeout} s: abandoned")
+        elif "e" in box:
+            rl(f"[single-process] side line failed: {box['e']!r}")
+        else:
+            single = box.get("r")
 
     pq = None
-    if a.pq_rows > 0:  # every rank: configs[4] is this line at N = 8
+    if a.pq_rows > 0 and not single_hung:  # every rank: configs[4] is this line at N = 8
         idx.close()
         del x
         torch.cuda.empty_cache()
@@ -719,6 +740,10 @@ def main():
         if a.json_out:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
+    if single_hung:  # a thread is stuck in a collective: leave without the teardown that would wait for it
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
     if pq is None:
         idx.close()
     if world > 1:
