@@ -136,7 +136,7 @@ __device__ __forceinline__ void rs_signal(int* ctr) {
     __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-constexpr int kRsBPrefetch = 2;  // k-steps between a B operand's LDS read and its MFMA
+constexpr int kRsBPrefetch = 3;  // k-steps between a B operand's LDS read and its MFMA
 
 template <bool B>
 struct BoolC {
