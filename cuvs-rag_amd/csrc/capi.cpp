@@ -329,6 +329,18 @@ void make_single_list(ListSet& ls, const float* src, int64_t n, int d, int dp, i
   pack_lists(ls, src, d, dp, nullptr, off, id_offset, nullptr, G, s);
 }
 
+// k-means' centroid list, refreshed every iteration: after the first pack only the groups and norms are
+// rewritten (same shape: no allocation, no host copy, no stream sync -- the codebook training runs ~2,000 of
+// these, and their hipMalloc / hipFree / syncs were most of its time)
+void repack_single_list(ListSet& ls, const float* src, int64_t n, int d, int dp, int G, hipStream_t s) {
+  if (ls.n_lists != 1 || ls.n_rows != n || ls.groups.p == nullptr) {
+    make_single_list(ls, src, n, d, dp, 0, G, s);
+    return;
+  }
+  HIPCHK(launch_pack_groups(src, 0, d, dp, nullptr, ls.off.as<int64_t>(), ls.goff.as<int64_t>(), nullptr, ls.n_groups,
+                            ls.groups.as<float>(), ls.norms.as<float>(), ls.ids.as<int64_t>(), nullptr, 0, s));
+}
+
 // ---- fp16 pre-filter assign: k-means assign and list fill as a one-list K10 scan
 // (queries = data rows, rows = centroids, k = 1) + the K11 exact refine; labels equal the fp32 K4's ----
 struct PfAssign {
@@ -524,15 +536,16 @@ void pf_assign_rows(const PfAssign& P, const float* data, const float* data_norm
 // when `pfa` holds the data's fp16 copy (L2 only)
 void assign_rows(const float* data, const float* data_norms, const int64_t* rows, int64_t nr, int d, int dp,
                  const ListSet& cents, int G, int metric, int64_t* labels, int device, Workspace& ws,
-                 hipStream_t s, const PfAssign* pfa = nullptr) {
+                 hipStream_t s, const PfAssign* pfa = nullptr, Buf* dist_buf = nullptr) {
   if (pfa && pfa->ok && metric == kL2 && nr > 0) {
     pf_assign_rows(*pfa, data, data_norms, rows, nr, d, dp, cents, G, labels, device, ws, s);
     return;
   }
-  Buf dist;
+  Buf local;
+  Buf& dist = dist_buf ? *dist_buf : local;  // (a caller's buffer outlives the launch: no sync)
   dist.reserve(sizeof(float) * (size_t)std::max<int64_t>(nr, 1));
   single_list_topk(cents, G, data, data_norms, rows, nr, d, dp, 1, metric, dist.as<float>(), labels, device, ws, s);
-  HIPCHK(hipStreamSynchronize(s));  // `dist` is freed on return
+  if (!dist_buf) HIPCHK(hipStreamSynchronize(s));  // `dist` is freed on return
 }
 
 // n_iters Lloyd iterations on trainset rows; centroids_rm in/out [nc][d]
@@ -544,7 +557,8 @@ void kmeans_fit_impl(const float* data, const float* data_norms, const int64_t* 
                      int64_t* labels_out = nullptr) {
   if (iters <= 0) return;
   if (it_total < 0) it_total = it_begin + iters;
-  Buf labels, perm, off, partial, chunk_off, tmp, ctmp;
+  Buf labels, perm, off, partial, chunk_off, tmp, ctmp, dist;
+  ListSet cents;  // (one allocation for every iteration)
   labels.reserve(sizeof(int64_t) * n_train);
   perm.reserve(sizeof(int64_t) * n_train);
   off.reserve(sizeof(int64_t) * (nc + 1));
@@ -554,9 +568,9 @@ void kmeans_fit_impl(const float* data, const float* data_norms, const int64_t* 
   const size_t cb = csort_tmp_bytes(n_train, nc);
   ctmp.reserve(cb);
   for (int it = it_begin; it < it_begin + iters; ++it) {
-    ListSet cents;
-    make_single_list(cents, centroids_rm, nc, d, dp, 0, G, s);
-    assign_rows(data, data_norms, rows, n_train, d, dp, cents, G, kL2, labels.as<int64_t>(), device, ws, s, pfa);
+    repack_single_list(cents, centroids_rm, nc, d, dp, G, s);
+    assign_rows(data, data_norms, rows, n_train, d, dp, cents, G, kL2, labels.as<int64_t>(), device, ws, s, pfa,
+                &dist);
     if (labels_out && it == it_begin + iters - 1)
       HIPCHK(hipMemcpyAsync(labels_out, labels.p, sizeof(int64_t) * n_train, hipMemcpyDeviceToDevice, s));
     HIPCHK(launch_counting_sort(labels.as<int64_t>(), n_train, nc, perm.as<int64_t>(), off.as<int64_t>(), ctmp.p,
