@@ -77,6 +77,7 @@ def parse():
                     help="side line (N=1 launch): the reference's one-process shape -- every visible GPU holds a "
                          "rows-per-GPU shard, ParallelIndexBuilder threads build them, SearchResultAggregator "
                          "searches them and merges over RCCL (LocalComm); 0 to skip")
+    ap.add_argument("--build-warmup", type=int, default=1, help="untimed builds before the timed one (allocator warm-up)")
     ap.add_argument("--single-process-timeout", type=float, default=240.0,
                     help="seconds the one-process multi-GPU side line may take before it is abandoned")
     ap.add_argument("--json-out", default="")
@@ -377,6 +378,10 @@ def pq_side_line(a, rl, rank=0, world=1, dev=None):
     torch.cuda.empty_cache()
     q = ops.synth_mixture(Q, d, SEED + 11, n_centers=a.centers, sigma=a.sigma, row_begin=QUERY_ROW_BASE, device=dev)
     sync_all(world)
+    if a.build_warmup:  # (as for the IVF-Flat build: an untimed first build warms the allocator)
+        ivf_pq.build(ivf_pq.IndexParams(n_lists=n_lists, pq_dim=pq_dim, pq_bits=8), x).close()
+        torch.cuda.synchronize()
+        sync_all(world)
     _native.set_profiling(True)
     t0 = time.perf_counter()
     idx = ivf_pq.build(ivf_pq.IndexParams(n_lists=n_lists, pq_dim=pq_dim, pq_bits=8), x)
@@ -492,6 +497,11 @@ def main():
     params = ivf_flat.IndexParams(n_lists=a.n_lists, kmeans_n_iters=a.kmeans_iters,
                                   kmeans_trainset_fraction=a.trainset_fraction)
     sync_all(world)
+    if a.build_warmup:  # an untimed first build: a process's first ~100 GB of device allocations can stall for
+        # seconds (once seen: 2.96 s in the copies' phase against 0.03 s), as the search's warmup steps do for it
+        ivf_flat.build(params, x, ids_offset=start).close()
+        torch.cuda.synchronize()
+        sync_all(world)
     _native.set_profiling(True)  # (the build's phase clocks: one stream sync per phase)
     t0 = time.perf_counter()
     idx = ivf_flat.build(params, x, ids_offset=start)

@@ -346,6 +346,7 @@ void repack_single_list(ListSet& ls, const float* src, int64_t n, int d, int dp,
 struct PfAssign {
   Buf qh, qscale, qres;  // fp16 copy of every data row: 2^hx x a per-row power of two (k_queries_to_half)
   int hx = 0;
+  int64_t n = 0;         // data rows
   bool ok = false;
 };
 
@@ -382,12 +383,91 @@ void pf_assign_prepare(PfAssign& P, const float* data, int64_t n, int d, int dp,
   P.qres.reserve(sizeof(float) * n);
   HIPCHK(launch_queries_to_half(data, n, d, dp, P.hx, P.qh.as<uint16_t>(), P.qscale.as<float>(),
                                 P.qres.as<float>(), s));
+  P.n = n;
   P.ok = true;
+}
+
+void pf_assign_k12(const PfAssign& P, const float* data, const float* data_norms, const int64_t* rows, int64_t nr,
+                   int d, int dp, const ListSet& cents, int G, int64_t* labels, int device, Workspace& ws,
+                   hipStream_t s);
+
+bool as_assign_on() {
+  const char* e = getenv("MIVS_PF_ASSIGN_RS");
+  return !(e && e[0] == '0');
+}
+
+// K13a (assign.hip): the centroids' tile images, the row-stationary scan, then K12 + the window refine for the
+// rows it could not prove (a wait that gave up: every row through the exact scan)
+void as_assign_rows(const PfAssign& P, const float* data, const float* data_norms, const int64_t* rows, int64_t nr,
+                    int d, int dp, const ListSet& cents, int G, int64_t* labels, int device, Workspace& ws,
+                    hipStream_t s) {
+  Buf ct, st, cnt, dist;
+  ct.reserve(as_ctiles_bytes(cents.n_groups, dp));
+  st.reserve(16);
+  cnt.reserve(16);
+  HIPCHK(hipMemsetAsync(st.p, 0, 16, s));
+  HIPCHK(hipMemsetAsync(cnt.p, 0, 16, s));
+  HIPCHK(launch_as_ctiles(cents.groups.as<float>(), cents.norms.as<float>(), cents.n_groups, dp, P.hx, ct.as<char>(),
+                          st.as<unsigned>(), s));
+  ws.ovf_q.reserve(sizeof(int64_t) * std::max<int64_t>(nr, 1));
+  AsScanArgs a{};
+  a.qh = P.qh.as<uint16_t>();
+  a.qscale = P.qscale.as<float>();
+  a.qnorms = data_norms;
+  a.qres = P.qres.as<float>();
+  a.rows = rows;
+  a.nr = nr;
+  a.ctiles = ct.as<char>();
+  a.n_ctiles = (int)cents.n_groups;
+  a.cstat = st.as<unsigned>();
+  a.dp = dp;
+  a.labels = labels;
+  a.ovf_count = cnt.as<int>();
+  a.ovf_rows = ws.ovf_q.as<int64_t>();
+  a.queue = cnt.as<int>() + 2;
+  a.flags = getenv("MIVS_AS_FLAGS") ? atoi(getenv("MIVS_AS_FLAGS")) : 0;
+  HIPCHK(launch_as_scan(a, cu_count(device), s));
+  int h[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(h, cnt.p, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  dist.reserve(sizeof(float) * std::max<int64_t>(nr, 1));  // (the fallback's distances, unused)
+  if (h[1] != 0) {  // never expected: every row through the exact scan
+    single_list_topk(cents, G, data, data_norms, rows, nr, d, dp, 1, kL2, dist.as<float>(), labels, device, ws, s);
+    HIPCHK(hipStreamSynchronize(s));
+    return;
+  }
+  if (h[0] == 0) return;
+  // the near ties (a second centroid inside the refine window): K12 + the window refine on those rows alone,
+  // scattered back (its own unprovable rows take the exact scan)
+  const int64_t hn = h[0];
+  Buf ovf, drow, lab;
+  ovf.reserve(sizeof(int64_t) * hn);
+  drow.reserve(sizeof(int64_t) * hn);
+  lab.reserve(sizeof(int64_t) * hn);
+  HIPCHK(hipMemcpyAsync(ovf.p, ws.ovf_q.p, sizeof(int64_t) * hn, hipMemcpyDeviceToDevice, s));
+  if (rows) HIPCHK(launch_gather_ids(rows, ovf.as<int64_t>(), hn, drow.as<int64_t>(), s));
+  else HIPCHK(hipMemcpyAsync(drow.p, ovf.p, sizeof(int64_t) * hn, hipMemcpyDeviceToDevice, s));
+  pf_assign_k12(P, data, data_norms, drow.as<int64_t>(), hn, d, dp, cents, G, lab.as<int64_t>(), device, ws, s);
+  HIPCHK(launch_scatter_results(dist.as<float>(), lab.as<int64_t>(), ovf.as<int64_t>(), hn, 1, dist.as<float>(),
+                                labels, s));
+  HIPCHK(hipStreamSynchronize(s));
 }
 
 void pf_assign_rows(const PfAssign& P, const float* data, const float* data_norms, const int64_t* rows, int64_t nr,
                     int d, int dp, const ListSet& cents, int G, int64_t* labels, int device, Workspace& ws,
                     hipStream_t s) {
+  if (as_assign_on() && as_scan_supported(dp, cents.n_rows) && cents.n_lists == 1) {
+    as_assign_rows(P, data, data_norms, rows, nr, d, dp, cents, G, labels, device, ws, s);
+    return;
+  }
+  pf_assign_k12(P, data, data_norms, rows, nr, d, dp, cents, G, labels, device, ws, s);
+}
+
+// K12 (register-resident rows, the centroids streamed) + K11's one-lane refine of each row's window candidates;
+// rows the refine cannot prove: the exact K4 scan. `rows` may be in any order (qtheta spans every data row).
+void pf_assign_k12(const PfAssign& P, const float* data, const float* data_norms, const int64_t* rows, int64_t nr,
+                   int d, int dp, const ListSet& cents, int G, int64_t* labels, int device, Workspace& ws,
+                   hipStream_t s) {
   // the centroids' fp16 copy (scale 2^hx) and the maxima the refine window needs
   const int64_t nslot = cents.n_groups * (int64_t)kGroupRows;
   Buf ch, st;
@@ -423,13 +503,7 @@ void pf_assign_rows(const PfAssign& P, const float* data, const float* data_norm
   ws.pf_bound.reserve(sizeof(float) * (size_t)nslots);
   ws.counter.reserve(8 * 16 * sizeof(int));
   HIPCHK(hipMemsetAsync(ws.counter.p, 0, 8 * 16 * sizeof(int), s));
-  int64_t n_ids = nr;  // qtheta is indexed by data row: as many entries as the largest row id + 1
-  if (rows) {
-    int64_t last = 0;
-    HIPCHK(hipMemcpyAsync(&last, rows + nr - 1, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    n_ids = last + 1;  // the trainset rows are increasing (launch_train_rows)
-  }
+  const int64_t n_ids = rows ? P.n : nr;  // qtheta is indexed by data row
   ws.qtheta.reserve(sizeof(unsigned) * n_ids);
   HIPCHK(launch_fill_i32(ws.qtheta.as<int>(), n_ids, (int)kPfOrdInf, s));
   HIPCHK(hipStreamSynchronize(s));

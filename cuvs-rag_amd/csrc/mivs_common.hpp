@@ -255,6 +255,30 @@ struct RsScanArgs {
   unsigned long long* prof;  // flags & 8: [grid][3] {start, end, tiles}
 };
 
+// K13a k-means assign on the row-stationary loop (assign.hip)
+struct AsScanArgs {
+  const uint16_t* qh;        // data rows fp16 [n][dp], row r scaled by its own power of two (k_queries_to_half)
+  const float* qscale;       // [n] 2^-(hx + row exp): the fp16 dot -> approximate fp32 dot
+  const float* qnorms;       // [n] pinned fp32 norms of the data rows
+  const float* qres;         // [n] ||x - x_h|| of the data rows
+  const int64_t* rows;       // optional: assign row r is data row rows[r] (the k-means trainset), else r
+  int64_t nr;                // rows to assign
+  const char* ctiles;        // centroid tile images (k_as_ctiles): [n_ctiles][dp/16 + 1] x 1 KiB
+  int n_ctiles;              // tiles of 32 centroids (> 1)
+  const unsigned* cstat;     // {max pinned centroid norm, max ||c - c_h||} as float bits (k_as_ctiles)
+  int dp;
+  int64_t* labels;           // [nr] the argmin of every proven row
+  int* ovf_count;            // [2] rows handed to the exact scan; [1] != 0: a wait gave up (rerun every row)
+  int64_t* ovf_rows;         // [nr] those rows (assign-row indices)
+  int* queue;                // item counter, zero at launch
+  int flags;                 // timing only: 2 skip staging
+};
+bool as_scan_supported(int dp, int64_t n_centroids);
+size_t as_ctiles_bytes(int64_t n_groups, int dp);
+hipError_t launch_as_ctiles(const float* groups, const float* norms, int64_t n_groups, int dp, int hx, char* tiles,
+                            unsigned* stat, hipStream_t s);
+hipError_t launch_as_scan(const AsScanArgs& a, int grid, hipStream_t s);
+
 // K14 exact re-ranking of candidates (refine.hip): cuvs.neighbors.refine
 struct RefineArgs {
   const void* data;       // [n][d] fp32, or fp16 when half

@@ -129,15 +129,17 @@ def test_exact_scan_switch_same_bits(ivf, flat_data, monkeypatch, k, env):
 
 
 def test_build_assign_switches_same_index(flat_data, mivs_lib, monkeypatch):
-    """the build's assign through K12 (default), through K10 (MIVS_PF_ASSIGN_REG=0) and in fp32
-    (MIVS_PF_ASSIGN=0): the same centroids, list sizes and list order"""
+    """the build's assign through K13a (default), through K12 (MIVS_PF_ASSIGN_RS=0), through K10
+    (MIVS_PF_ASSIGN_RS=0 MIVS_PF_ASSIGN_REG=0) and in fp32 (MIVS_PF_ASSIGN=0): the same centroids, list sizes
+    and list order"""
     from mivs.neighbors import ivf_flat
 
     x, _ = flat_data
     xt = torch.from_numpy(x).cuda()
     p = ivf_flat.IndexParams(n_lists=48, kmeans_n_iters=4)
     ref = ivf_flat.build(p, xt)
-    for env in ({"MIVS_PF_ASSIGN_REG": "0"}, {"MIVS_PF_ASSIGN": "0"}):
+    for env in ({"MIVS_PF_ASSIGN_RS": "0"}, {"MIVS_PF_ASSIGN_RS": "0", "MIVS_PF_ASSIGN_REG": "0"},
+                {"MIVS_PF_ASSIGN": "0"}):
         for kk, v in env.items():
             monkeypatch.setenv(kk, v)
         other = ivf_flat.build(p, xt)
@@ -148,6 +150,27 @@ def test_build_assign_switches_same_index(flat_data, mivs_lib, monkeypatch):
         np.testing.assert_array_equal(other.list_ids().cpu().numpy(), ref.list_ids().cpu().numpy())
         other.close()
     ref.close()
+
+
+@pytest.mark.parametrize("d,dup", [(128, "exact"), (768, "exact"), (768, "near")])
+def test_build_assign_k13a_near_ties(mivs_lib, d, dup):
+    """K13a's rows it cannot prove (a second centroid inside the refine window) go through K12 + the window
+    refine: centroids 32..63 duplicate 0..31 exactly (every row a tie, resolved to the lower id) or up to a
+    1e-6 nudge (inside the window, decided by the exact fp32 keys); labels equal the oracle's assign"""
+    from mivs.cluster import kmeans
+
+    x = _data(20_000, d, 7)
+    rng = np.random.default_rng(3)
+    c = x[rng.choice(x.shape[0], 64, replace=False)].copy()
+    c[32:] = c[:32]
+    if dup == "near":
+        c[32:] += (1e-6 * rng.standard_normal((32, d))).astype(np.float32)
+    _, lab = kmeans.build_steps(torch.from_numpy(x).cuda(), torch.from_numpy(c).cuda(), None, 0, 1, 1,
+                                balance=False, return_labels=True)
+    exp = O.kmeans_assign(x, c)
+    if dup == "exact":
+        assert exp.max() < 32
+    np.testing.assert_array_equal(lab.cpu().numpy(), exp)
 
 
 def test_prefilter_default_switch(flat_data, mivs_lib, monkeypatch):
