@@ -134,6 +134,8 @@ struct mivs_index_s {
   Buf groups_h;
   Buf rows_rm;     // K11: the fp32 lists row-major (built with groups_h when HBM has room; MIVS_PF_ROWMAJOR=0: off)
   Buf group_nmin;  // K13: the smallest row norm of every 32-row group (built with groups_h)
+  Buf pre_norms;   // K13's pre-pass: every row's norm over its first pre_norms_dims dims (0: not built)
+  int pre_norms_dims = 0;
   int hx_exp = 0;
   float x_norm_max = 0.0f, x_res_max = 0.0f;
   int pf_G = kPfChunkGroups;                  // groups per K10 work item
@@ -705,6 +707,8 @@ void pf_enable(mivs_index_s* idx, hipStream_t s) {
   const ListSet& L = idx->lists;
   idx->groups_h.release();
   idx->rows_rm.release();
+  idx->pre_norms.release();
+  idx->pre_norms_dims = 0;
   if (L.n_groups == 0 || idx->dp % 64 != 0) return;
   const int64_t nslot = L.n_groups * (int64_t)kGroupRows;
   Buf st;
@@ -765,14 +769,17 @@ void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t
 void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                         int64_t* out_i, const float* slot_key, const int* slot_pos, const float* slot_bound,
                         const int* force_ovf, const int64_t* slot_begin, int slot_k, bool fallback_pf = false,
-                        float* kth_out = nullptr, const float* window_cap = nullptr);
+                        float* kth_out = nullptr, const float* window_cap = nullptr, int verify_sel = 0);
 
 // K10 scan + K11 refine for a probe map built with (kPfChunkGroups, kPfQTile); queries the refine
 // could not prove are re-run through the exact scan and scattered back.
 // (goff / n_lists: another split of the same groups into lists -- K13's pre-pass samples)
-// kth_out: K13's pre-pass -- only the k-th smallest approximate key per query (no refine, no fallback)
+// kth_out: K13's pre-pass -- only the k-th smallest approximate key per query (no refine, no fallback);
+// with nk_scan > 0 the scan scores the first 16 nk_scan dims against scan_norms (nomination), and verify_sel
+// > 0 makes kth_out the k-th smallest pinned key of each query's verify_sel best-scored rows
 void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
-                    int64_t* out_i, ProfRec* pr, const int64_t* goff, int n_lists, float* kth_out = nullptr) {
+                    int64_t* out_i, ProfRec* pr, const int64_t* goff, int n_lists, float* kth_out = nullptr,
+                    int nk_scan = 0, const float* scan_norms = nullptr, int verify_sel = 0) {
   Workspace& ws = idx->ws;
   const ListSet& L = idx->lists;
   const int dp = idx->dp;
@@ -801,7 +808,8 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
     a.chunk_stride = (int)tcp[1];
   }
   a.groups_h = idx->groups_h.as<uint16_t>();
-  a.row_norms = L.norms.as<float>();
+  a.row_norms = scan_norms ? scan_norms : L.norms.as<float>();
+  a.nk_scan = nk_scan;
   a.list_goff = goff;
   a.n_lists = n_lists;
   a.chunk_groups = idx->pf_G;
@@ -825,7 +833,7 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   ws.qtheta.reserve(sizeof(unsigned) * nq);
   HIPCHK(launch_fill_i32(ws.qtheta.as<int>(), nq, (int)kPfOrdInf, s));
   a.qtheta = ws.qtheta.as<unsigned>();
-  a.k = k;
+  a.k = verify_sel > 0 ? std::min(verify_sel, kPfMaxK) : k;  // (nomination: the slots keep the verify_sel best)
   // K13's pre-pass (kth_out): each list sample is scanned by one tile -- its rows are read once
   // (MIVS_PF_PRE_NT=0: the default policy, A/B runs)
   const char* pne = getenv("MIVS_PF_PRE_NT");
@@ -851,7 +859,8 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
               hp[0] / w, hp[1] / w, hp[2] / w, hp[3] / w, hp[4] / w, hp[5], hp[5] ? (double)hp[6] / hp[5] : 0.0);
   }
   pf_refine_fallback(idx, s, q, nq, k, np, out_d, out_i, ws.pf_key.as<float>(), ws.pf_pos.as<int>(),
-                     ws.pf_bound.as<float>(), nullptr, ws.slot_begin.as<int64_t>(), slot_k, false, kth_out);
+                     ws.pf_bound.as<float>(), nullptr, ws.slot_begin.as<int64_t>(), slot_k, false, kth_out, nullptr,
+                     verify_sel);
 }
 
 // K11 over the scan's candidate slots, then the exact scan for the queries the refine could not prove
@@ -859,7 +868,7 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
 void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                         int64_t* out_i, const float* slot_key, const int* slot_pos, const float* slot_bound,
                         const int* force_ovf, const int64_t* slot_begin, int slot_k, bool fallback_pf,
-                        float* kth_out, const float* window_cap) {
+                        float* kth_out, const float* window_cap, int verify_sel) {
   Workspace& ws = idx->ws;
   const ListSet& L = idx->lists;
   const int dp = idx->dp;
@@ -873,6 +882,7 @@ void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_
   r.force_ovf = force_ovf;
   r.window_cap = window_cap;
   r.kth_out = kth_out;
+  r.verify_sel = verify_sel;
   r.slot_begin = slot_begin;
   r.slot_k = slot_k;
   r.nq = nq;
@@ -979,6 +989,16 @@ bool rs_use(const mivs_index_s* idx, int np) {
   return idx->kind == 0 && np >= 2 && rs_scan_supported(idx->dp) && !(e && e[0] == '0');
 }
 
+// K13's pre-pass nomination dims (MIVS_RS_PRE_DIMS; 0 or >= dp: the full-dims sample of round 2): a multiple
+// of 64 or 96 (K10's 4- or 6-deep rings of 16-dim k-steps) below dp
+int rs_pre_dims(int dp) {
+  const char* e = getenv("MIVS_RS_PRE_DIMS");
+  const int v = e ? atoi(e) : kRsPreDims;
+  if (v <= 0 || v >= dp) return 0;
+  if (v % 96 == 0) return v;
+  return std::max(64, v / 64 * 64);
+}
+
 // records per K13 stream: twice the batch's queries, at most kRsWaveCapMax (MIVS_RS_WAVE_CAP overrides it: the
 // lost-stream path is then testable at small sizes). Batches are at most kRsMaxBatch queries (ivf_search_impl),
 // so a stream's mean length (~160 records per 1,000 queries at the benchmark shape) stays far below the cap.
@@ -1006,8 +1026,19 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   // are in no particular order) through K10 over the split lists, and the k-th smallest approximate key
   // of each query's candidates there (K11's first phase only)
   ws.pre_goff.reserve(sizeof(int64_t) * (2 * (size_t)L.n_lists + 1));
+  // nomination (MIVS_RS_PRE_DIMS > 0): the sample scored on its first pre_dims dims only (against the rows' norms
+  // over those dims), then the MIVS_RS_PRE_SEL best-scored rows of each query verified with pinned keys
+  const int pre_dims = rs_pre_dims(dp);
+  const char* pse = getenv("MIVS_RS_PRE_SEL");
+  const int pre_sel = pre_dims > 0 ? std::min(kPfMaxK, std::max(k, pse ? atoi(pse) : kRsPreSel)) : 0;
   const char* pde = getenv("MIVS_RS_PRE_DIV");
-  const int pre_div = std::max(1, pde ? atoi(pde) : kRsPreDiv);
+  const int pre_div = std::max(1, pde ? atoi(pde) : (pre_dims > 0 ? kRsPreDivNominate : kRsPreDiv));
+  if (pre_dims > 0 && idx->pre_norms_dims != pre_dims) {
+    idx->pre_norms.reserve(sizeof(float) * (size_t)L.n_groups * kGroupRows);
+    HIPCHK(launch_partial_norms(L.groups.as<float>(), L.norms.as<float>(), L.n_groups, dp, pre_dims,
+                                idx->pre_norms.as<float>(), s));
+    idx->pre_norms_dims = pre_dims;
+  }
   HIPCHK(launch_rs_pre_lists(L.goff.as<int64_t>(), L.n_lists, pre_div, ceil_div(k, kGroupRows), ws.probes_full.as<int64_t>(),
                              nq, np, ws.pre_goff.as<int64_t>(), ws.probes_i.as<int64_t>(), s));
   {
@@ -1028,14 +1059,36 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
                             ws.slot_begin.as<int64_t>(), ws.scan_tmp.p, stb, s));
     ws.pre_kth.reserve(sizeof(float) * nq);
     pf_scan_refine(idx, s, q, nq, k, 1, nullptr, nullptr, nullptr, ws.pre_goff.as<int64_t>(), nl2,
-                   ws.pre_kth.as<float>());
+                   ws.pre_kth.as<float>(), pre_dims / 16, pre_dims > 0 ? idx->pre_norms.as<float>() : nullptr,
+                   pre_sel);
   }
   // 2. headers (pf_scan_refine left the fp16 queries, their scales and residuals in ws.qh / qscale / qres)
   ws.qhdr.reserve(sizeof(float4) * (nq + 1));
   float4* qhdr = ws.qhdr.as<float4>();
   ws.rs_tq.reserve(sizeof(float) * nq);
   HIPCHK(launch_rs_headers(ws.pre_kth.as<float>(), nq, ws.qscale.as<float>(), ws.qn.as<float>(), ws.qres.as<float>(),
-                           idx->x_norm_max, idx->x_res_max, dp, idx->metric, qhdr, ws.rs_tq.as<float>(), s));
+                           idx->x_norm_max, idx->x_res_max, dp, idx->metric, pre_sel > 0 ? 1 : 0, qhdr,
+                           ws.rs_tq.as<float>(), s));
+  if (getenv("MIVS_RS_PRE_STATS")) {  // diagnostic: the pre-pass's k-th keys and T_q (stderr)
+    std::vector<float> hk(nq), ht(nq);
+    HIPCHK(hipMemcpyAsync(hk.data(), ws.pre_kth.p, sizeof(float) * nq, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(ht.data(), ws.rs_tq.p, sizeof(float) * nq, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    double sk = 0, st = 0;
+    int64_t ninf = 0;
+    for (int64_t i = 0; i < nq; ++i) {
+      if (!(hk[i] < INFINITY)) { ++ninf; continue; }
+      sk += hk[i];
+      st += ht[i];
+    }
+    const double nf = std::max<double>(1.0, (double)(nq - ninf));
+    std::vector<float> sorted = ht;
+    std::sort(sorted.begin(), sorted.end());
+    auto pc = [&](double f) { return sorted[std::min<int64_t>(nq - 1, (int64_t)(f * nq))]; };
+    fprintf(stderr, "[rs pre] dims %d div %d sel %d | mean kth %.6f mean T_q %.6f | inf %lld of %lld | T_q p10 %.4f "
+            "p50 %.4f p90 %.4f p99 %.4f max %.4f\n", pre_dims, pre_div, pre_sel, sk / nf, st / nf, (long long)ninf,
+            (long long)nq, pc(0.1), pc(0.5), pc(0.9), pc(0.99), sorted[nq - 1]);
+  }
   // 3. probe map: items = (list, block of kRsBlockGroups groups); every query of a list in one tile column
   const size_t stb = scan_tmp_bytes(ne) + sizeof(int64_t) * (size_t)ne;
   ws.scan_tmp.reserve(stb);

@@ -176,7 +176,8 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
 
   const int dp = a.dp;
   const int nb = dp >> 3;  // 8-dim blocks
-  const int nk = dp >> 4;  // 16-dim k-steps (a multiple of D)
+  // 16-dim k-steps (a multiple of D); nk_scan: only the first 16 nk_scan dims (K13's pre-pass nomination)
+  const int nk = a.nk_scan > 0 ? a.nk_scan : dp >> 4;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: the k-loop is a scalar loop
@@ -268,7 +269,7 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
           const int qg = gb / nb, b = gb - qg * nb;
           const int64_t q = (i0 + u < per) ? s_q[qg * 32 + (i & 31)] : -1;
           v[u] = make_uint4(0u, 0u, 0u, 0u);
-          if (q >= 0) v[u] = *reinterpret_cast<const uint4*>(a.qh + q * dp + 8 * b);
+          if (q >= 0 && b < 2 * nk) v[u] = *reinterpret_cast<const uint4*>(a.qh + q * dp + 8 * b);
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u)
@@ -568,6 +569,33 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
   }
 }
 
+// the pinned fp32 key of row slot pos (oracle orc_dot order) against the query row qv (zero past d)
+template <int METRIC>
+__device__ __forceinline__ float pf_pinned_key(const PfRefineArgs& a, int pos, const float* qv, float qn) {
+  const int nb = a.dp >> 3;
+  // the row's block b: 8 floats at rowp + b * bstride (row-major copy: contiguous; group layout: 1 KiB apart)
+  const float* rowp = a.rows_rm ? a.rows_rm + (int64_t)pos * a.dp
+                                : a.groups + ((int64_t)(pos >> 5) * nb * kGroupRows + (pos & 31)) * 8;
+  const int64_t bstride = a.rows_rm ? 8 : 256;
+  float acc = 0.0f;
+#pragma unroll 12
+  for (int b = 0; b < nb; ++b) {
+    const float4 x0 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride);
+    const float4 x1 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride + 4);
+    const float4 y0 = *reinterpret_cast<const float4*>(qv + 8 * b);
+    const float4 y1 = *reinterpret_cast<const float4*>(qv + 8 * b + 4);
+    acc = fmaf(x0.x, y0.x, acc); acc = fmaf(x1.x, y1.x, acc);
+    acc = fmaf(x0.y, y0.y, acc); acc = fmaf(x1.y, y1.y, acc);
+    acc = fmaf(x0.z, y0.z, acc); acc = fmaf(x1.z, y1.z, acc);
+    acc = fmaf(x0.w, y0.w, acc); acc = fmaf(x1.w, y1.w, acc);
+  }
+  if (METRIC == kL2) {
+    const float v = fmaf(-2.0f, acc, a.row_norms[pos] + qn);
+    return v > 0.0f ? v : 0.0f;
+  }
+  return -acc;
+}
+
 // K11. One wave per query (4 per workgroup; every wave reaches every barrier).
 template <int METRIC>
 __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
@@ -590,6 +618,7 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
   // fewer than k keys below it is the k-th smallest (ties counted), no shuffles; more: the running top-k
   // (K7's ballot insertion). Both return the same value.
   float mk = INFINITY, tk = INFINITY;
+  const int ksel = a.kth_out && a.verify_sel > 0 ? a.verify_sel : k;  // (verify: the nominees' count)
   const int64_t n_c = c1 - sb * a.slot_k;
   if (n_c <= kPfSelRegs * 64) {
     uint32_t u[kPfSelRegs];
@@ -606,7 +635,7 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
       int below = 0;
 #pragma unroll
       for (int i = 0; i < kPfSelRegs; ++i) below += __popcll(__ballot(u[i] < t));
-      if (below < k) ans = t;
+      if (below < ksel) ans = t;
     }
     const uint32_t b = (ans & 0x80000000u) ? (ans & 0x7FFFFFFFu) : ~ans;
     tk = __uint_as_float(b);
@@ -618,17 +647,51 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
     while (mask) {
       const int b = __ffsll((unsigned long long)mask) - 1;
       const float nk = __shfl(ck, b);
-      const int pos = __popcll(__ballot(lane < k && mk <= nk));
+      const int pos = __popcll(__ballot(lane < ksel && mk <= nk));
       const float pk = __shfl_up(mk, 1);
       if (lane == pos) mk = nk;
       else if (lane > pos) mk = pk;
-      tk = __shfl(mk, k - 1);
+      tk = __shfl(mk, ksel - 1);
       mask &= ~(1ull << b);
       mask &= __ballot(ck < tk);
     }
   }
   if (a.kth_out) {  // (kernel-uniform: every wave of the block leaves here)
-    if (live && lane == 0) a.kth_out[q] = tk;
+    if (a.verify_sel <= 0) {
+      if (live && lane == 0) a.kth_out[q] = tk;
+      return;
+    }
+    // verify: the nominees (key <= the verify_sel-th smallest; ties beyond 64 dropped: any probed rows bound the
+    // final k-th key) get their pinned fp32 keys; kth_out = the k-th smallest of those (+inf: fewer than k)
+    int cnt = 0;
+    for (int64_t c = sb * a.slot_k; c < c1; c += 64) {
+      const int64_t cc = c + lane;
+      const float ck = cc < c1 ? a.slot_key[cc] : INFINITY;
+      const bool take = ck <= tk && ck < INFINITY;
+      const uint64_t msk = __ballot(take);
+      if (take) {
+        const int at = cnt + __popcll(msk & ((1ull << lane) - 1));
+        if (at < 64) s_cp[wv][at] = a.slot_pos[cc];
+      }
+      cnt += __popcll(msk);
+    }
+    const int64_t qrow = live && a.qrows ? a.qrows[q] : q;
+    const float qn = live ? a.qnorms[qrow] : 0.0f;
+    for (int i = lane; i < a.dp; i += 64) s_qv[wv][i] = (live && i < a.d) ? a.queries[qrow * a.d + i] : 0.0f;
+    __syncthreads();
+    float P = INFINITY;
+    if (live && lane < cnt && lane < 64) P = pf_pinned_key<METRIC>(a, s_cp[wv][lane], s_qv[wv], qn);
+#pragma unroll
+    for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        const float oP = __shfl_xor(P, stride);
+        const bool want_min = ((lane & stride) == 0) == ((lane & size) == 0);
+        if (want_min ? oP < P : oP > P) P = oP;
+      }
+    }
+    const float kx = __shfl(P, k - 1);
+    if (live && lane == 0) a.kth_out[q] = kx;
     return;
   }
   float bmin = cnt_ovf ? -INFINITY : INFINITY;
@@ -681,30 +744,7 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
   int64_t id = LLONG_MAX;
   if (live && !ovf && lane < cnt) {
     const int pos = s_cp[wv][lane];
-    const int nb = a.dp >> 3;
-    // the row's block b: 8 floats at rowp + b * bstride (row-major copy: contiguous; group layout: 1 KiB apart)
-    const float* rowp = a.rows_rm ? a.rows_rm + (int64_t)pos * a.dp
-                                  : a.groups + ((int64_t)(pos >> 5) * nb * kGroupRows + (pos & 31)) * 8;
-    const int64_t bstride = a.rows_rm ? 8 : 256;
-    const float* qv = s_qv[wv];
-    float acc = 0.0f;
-#pragma unroll 12
-    for (int b = 0; b < nb; ++b) {
-      const float4 x0 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride);
-      const float4 x1 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride + 4);
-      const float4 y0 = *reinterpret_cast<const float4*>(qv + 8 * b);
-      const float4 y1 = *reinterpret_cast<const float4*>(qv + 8 * b + 4);
-      acc = fmaf(x0.x, y0.x, acc); acc = fmaf(x1.x, y1.x, acc);
-      acc = fmaf(x0.y, y0.y, acc); acc = fmaf(x1.y, y1.y, acc);
-      acc = fmaf(x0.z, y0.z, acc); acc = fmaf(x1.z, y1.z, acc);
-      acc = fmaf(x0.w, y0.w, acc); acc = fmaf(x1.w, y1.w, acc);
-    }
-    if (METRIC == kL2) {
-      const float v = fmaf(-2.0f, acc, a.row_norms[pos] + qn);
-      P = v > 0.0f ? v : 0.0f;
-    } else {
-      P = -acc;
-    }
+    P = pf_pinned_key<METRIC>(a, pos, s_qv[wv], qn);
     id = a.row_ids[pos];
   }
 #pragma unroll
@@ -1381,7 +1421,9 @@ template <int METRIC>
 static hipError_t launch_pf_scan_m(const PfScanArgs& a, int grid, size_t lds, hipStream_t s) {
   // default: two groups per pass with 6-deep rings (half the LDS operand traffic per flop: the kernel is
   // power-bound); MIVS_PF_PAIR=0: one group per pass with MIVS_PF_DEPTH (16) k-steps in flight
-  const int nk = a.dp / 16;
+  const int nk = a.nk_scan > 0 ? a.nk_scan : a.dp / 16;
+  if (a.nk_scan > 0 && (a.nk_scan > a.dp / 16 || (a.nk_scan % 4 != 0 && a.nk_scan % 6 != 0)))
+    return hipErrorInvalidValue;
   if (pf_pair_mode()) {
     if (a.rows_nt && nk % 6 == 0) return launch_pf_scan_md<METRIC, 6, 2, true>(a, grid, lds, s);
     return nk % 6 == 0 ? launch_pf_scan_md<METRIC, 6, 2>(a, grid, lds, s) : launch_pf_scan_md<METRIC, 4, 2>(a, grid, lds, s);

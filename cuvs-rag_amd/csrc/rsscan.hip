@@ -569,7 +569,8 @@ __global__ __launch_bounds__(1024) void k_rs_bounds(const int* __restrict__ work
 template <int METRIC>
 __global__ void k_rs_headers(const float* __restrict__ pre_kth, int64_t nq, const float* __restrict__ qscale,
                              const float* __restrict__ qnorms, const float* __restrict__ qres, float x_norm_max,
-                             float x_res_max, int dp, float4* __restrict__ hdr, float* __restrict__ tq) {
+                             float x_res_max, int dp, int pre_exact, float4* __restrict__ hdr,
+                             float* __restrict__ tq) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q > nq) return;
   if (q == nq) {  // the null header
@@ -579,13 +580,15 @@ __global__ void k_rs_headers(const float* __restrict__ pre_kth, int64_t nq, cons
   const float qn = qnorms[q];
   const float delta = pf_delta<METRIC>(qn, qres[q], x_norm_max, x_res_max, dp);
   float T = INFINITY;
-  const float kth = pre_kth[q];  // the k-th smallest approximate key (K10's) over the sample rows
+  // the k-th smallest approximate key (K10's) over the sample rows, or (pre_exact) the k-th smallest PINNED key
+  // over the verified nominees
+  const float kth = pre_kth[q];
   if (kth < INFINITY) {
-    // those k rows are probed rows: their pinned keys are <= kth + delta, so the final k-th approximate key
-    // (K13's sums may round differently from K10's: each is within delta of the pinned key) is
-    // Ak <= U = kth + 2 delta, and the final window pf_window(Ak) <= pf_window(U) (monotone); one more
-    // relative step covers the roundings of U and T
-    const float U = kth + 2.0f * delta;
+    // those k rows are probed rows: their pinned keys are <= kth + delta (pre_exact: <= kth), so the final k-th
+    // approximate key (K13's sums may round differently from K10's: each is within delta of the pinned key) is
+    // Ak <= U = kth + 2 delta (pre_exact: kth + delta), and the final window pf_window(Ak) <= pf_window(U)
+    // (monotone); one more relative step covers the roundings of U and T
+    const float U = kth + (pre_exact ? 1.0f : 2.0f) * delta;
     T = pf_window(U, delta);
     T = T + fabsf(T) * 0x1p-20f + 1e-30f;
   }
@@ -956,6 +959,35 @@ hipError_t launch_group_nmin(const float* norms, int64_t n_groups, float* out, h
   return hipGetLastError();
 }
 
+// the squared norm of every row slot over its first `dims` dims (K13's pre-pass nomination score: the partial
+// distance needs the partial norm); pad rows (+inf full norm) stay +inf
+__global__ void k_partial_norms(const float* __restrict__ groups, const float* __restrict__ norms, int64_t n_groups,
+                                int dp, int dims, float* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_groups * kGroupRows) return;
+  const int64_t g = t >> 5;
+  const int j = (int)(t & 31);
+  const int nb = dp >> 3;
+  const float* p = groups + (g * nb * kGroupRows + j) * 8;
+  float acc = 0.0f;
+  for (int b = 0; b < (dims >> 3); ++b) {
+    const float4 x0 = *reinterpret_cast<const float4*>(p + (int64_t)b * 256);
+    const float4 x1 = *reinterpret_cast<const float4*>(p + (int64_t)b * 256 + 4);
+    acc = fmaf(x0.x, x0.x, acc); acc = fmaf(x0.y, x0.y, acc); acc = fmaf(x0.z, x0.z, acc); acc = fmaf(x0.w, x0.w, acc);
+    acc = fmaf(x1.x, x1.x, acc); acc = fmaf(x1.y, x1.y, acc); acc = fmaf(x1.z, x1.z, acc); acc = fmaf(x1.w, x1.w, acc);
+  }
+  out[t] = norms[t] < INFINITY ? acc : INFINITY;
+}
+
+hipError_t launch_partial_norms(const float* groups, const float* norms, int64_t n_groups, int dp, int dims,
+                                float* out, hipStream_t s) {
+  if (n_groups <= 0) return hipSuccess;
+  if (dims % 8 != 0 || dims > dp) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_partial_norms, dim3((unsigned)ceil_div(n_groups * kGroupRows, 256)), dim3(256), 0, s, groups,
+                     norms, n_groups, dp, dims, out);
+  return hipGetLastError();
+}
+
 // The pre-pass's lists: list l split into 2l = its first ceil(groups / div) groups (at least min_groups,
 // at most all) and 2l + 1 = the rest, so the n_probes = 1 search of probe 2 p0 scans a sample of the
 // nearest list p0 with the unchanged K10 / probe map (the sample's rows are still rows of the probed
@@ -991,15 +1023,15 @@ hipError_t launch_rs_pre_lists(const int64_t* goff, int n_lists, int div, int mi
 }
 
 hipError_t launch_rs_headers(const float* pre_kth, int64_t nq, const float* qscale, const float* qnorms,
-                             const float* qres, float x_norm_max, float x_res_max, int dp, int metric, float4* hdr,
-                             float* tq, hipStream_t s) {
+                             const float* qres, float x_norm_max, float x_res_max, int dp, int metric, int pre_exact,
+                             float4* hdr, float* tq, hipStream_t s) {
   const dim3 grid((unsigned)ceil_div(nq + 1, 256));
   if (metric == kIP)
     hipLaunchKernelGGL(k_rs_headers<kIP>, grid, dim3(256), 0, s, pre_kth, nq, qscale, qnorms, qres, x_norm_max,
-                       x_res_max, dp, hdr, tq);
+                       x_res_max, dp, pre_exact, hdr, tq);
   else
     hipLaunchKernelGGL(k_rs_headers<kL2>, grid, dim3(256), 0, s, pre_kth, nq, qscale, qnorms, qres, x_norm_max,
-                       x_res_max, dp, hdr, tq);
+                       x_res_max, dp, pre_exact, hdr, tq);
   return hipGetLastError();
 }
 
