@@ -87,6 +87,7 @@ struct Workspace {
       counts, fill, qp_slots, scan_tmp, gmerge;
   // fp16 pre-filter path (K10 / K11) and its exact-scan fallback
   Buf qh, qscale, qres, qtheta, pf_key, pf_pos, pf_bound, pf_stats, ovf_q, ovf_rows, ovf_d, ovf_i;
+  Buf q8, qscale8;  // K13's fp8 nomination: the queries' fp8 copy and scales
   // K13 row-stationary scan: the full probe list, the pre-pass result, per-query headers and candidates
   Buf probes_full, pre_kth, pre_goff, qhdr, rs_tq, cand_off, cand_key, cand_pos, rs_bucket_tmp, rs_tiles, rs_wave_buf,
       rs_wave_cnt, rs_bounds;
@@ -136,6 +137,8 @@ struct mivs_index_s {
   Buf group_nmin;  // K13: the smallest row norm of every 32-row group (built with groups_h)
   Buf pre_norms;   // K13's pre-pass: every row's norm over its first pre_norms_dims dims (0: not built)
   int pre_norms_dims = 0;
+  Buf groups_f8;   // K13's pre-pass: the lists' fp8 copy at 2^hx8 (built on first use when HBM has room)
+  int hx8 = 0;
   int hx_exp = 0;
   float x_norm_max = 0.0f, x_res_max = 0.0f;
   int pf_G = kPfChunkGroups;                  // groups per K10 work item
@@ -709,6 +712,7 @@ void pf_enable(mivs_index_s* idx, hipStream_t s) {
   idx->rows_rm.release();
   idx->pre_norms.release();
   idx->pre_norms_dims = 0;
+  idx->groups_f8.release();
   if (L.n_groups == 0 || idx->dp % 64 != 0) return;
   const int64_t nslot = L.n_groups * (int64_t)kGroupRows;
   Buf st;
@@ -779,7 +783,7 @@ void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_
 // > 0 makes kth_out the k-th smallest pinned key of each query's verify_sel best-scored rows
 void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                     int64_t* out_i, ProfRec* pr, const int64_t* goff, int n_lists, float* kth_out = nullptr,
-                    int nk_scan = 0, const float* scan_norms = nullptr, int verify_sel = 0) {
+                    int nk_scan = 0, const float* scan_norms = nullptr, int verify_sel = 0, bool f8 = false) {
   Workspace& ws = idx->ws;
   const ListSet& L = idx->lists;
   const int dp = idx->dp;
@@ -810,6 +814,14 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   a.groups_h = idx->groups_h.as<uint16_t>();
   a.row_norms = scan_norms ? scan_norms : L.norms.as<float>();
   a.nk_scan = nk_scan;
+  if (f8) {  // K13's fp8 nomination: the fp8 queries beside the fp16 ones (the headers and tiles use those)
+    ws.q8.reserve((size_t)nq * dp);
+    ws.qscale8.reserve(sizeof(float) * nq);
+    HIPCHK(launch_queries_to_f8(q, nq, idx->d, dp, idx->hx8, ws.q8.as<uint8_t>(), ws.qscale8.as<float>(), s));
+    a.groups_f8 = idx->groups_f8.as<uint8_t>();
+    a.q8 = ws.q8.as<uint8_t>();
+    a.qscale8 = ws.qscale8.as<float>();
+  }
   a.list_goff = goff;
   a.n_lists = n_lists;
   a.chunk_groups = idx->pf_G;
@@ -989,6 +1001,24 @@ bool rs_use(const mivs_index_s* idx, int np) {
   return idx->kind == 0 && np >= 2 && rs_scan_supported(idx->dp) && !(e && e[0] == '0');
 }
 
+// K13's fp8 pre-pass nomination (MIVS_RS_PRE_F8=0: off): the rows' fp8 copy is built on first use if the
+// HBM has room for it beside a 4 GiB margin; dp / 32 must be a multiple of 4 or 6 (K10's rings)
+bool rs_pre_f8(mivs_index_s* idx, hipStream_t s) {
+  const char* e = getenv("MIVS_RS_PRE_F8");
+  if (e && e[0] == '0') return false;
+  const int nsb = idx->dp / 32;
+  if (idx->dp % 32 != 0 || (nsb % 6 != 0 && nsb % 4 != 0) || !pf_pair_mode()) return false;
+  if (idx->groups_f8.p) return true;
+  const ListSet& L = idx->lists;
+  const size_t bytes = (size_t)L.n_groups * kGroupRows * idx->dp;
+  size_t fr = 0, tot = 0;
+  if (bytes == 0 || hipMemGetInfo(&fr, &tot) != hipSuccess || fr < bytes + ((size_t)4 << 30)) return false;
+  idx->hx8 = idx->hx_exp - 7;  // |x| max 2^hx_exp in [2^14, 2^15) -> [128, 256) under e4m3's 448
+  idx->groups_f8.reserve(bytes);
+  HIPCHK(launch_groups_to_f8(L.groups.as<float>(), L.n_groups, idx->dp, idx->hx8, idx->groups_f8.as<uint8_t>(), s));
+  return true;
+}
+
 // K13's pre-pass nomination dims (MIVS_RS_PRE_DIMS; 0 or >= dp: the full-dims sample of round 2): a multiple
 // of 64 or 96 (K10's 4- or 6-deep rings of 16-dim k-steps) below dp
 int rs_pre_dims(int dp) {
@@ -1028,11 +1058,14 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   ws.pre_goff.reserve(sizeof(int64_t) * (2 * (size_t)L.n_lists + 1));
   // nomination (MIVS_RS_PRE_DIMS > 0): the sample scored on its first pre_dims dims only (against the rows' norms
   // over those dims), then the MIVS_RS_PRE_SEL best-scored rows of each query verified with pinned keys
-  const int pre_dims = rs_pre_dims(dp);
+  // fp8 nomination (MIVS_RS_PRE_F8, default on where it applies): the sample scored on fp8 copies over every dim,
+  // the MIVS_RS_PRE_SEL best rows verified with pinned keys
+  const bool pre_f8 = rs_pre_f8(idx, s);
+  const int pre_dims = pre_f8 ? 0 : rs_pre_dims(dp);
   const char* pse = getenv("MIVS_RS_PRE_SEL");
-  const int pre_sel = pre_dims > 0 ? std::min(kPfMaxK, std::max(k, pse ? atoi(pse) : kRsPreSel)) : 0;
+  const int pre_sel = (pre_dims > 0 || pre_f8) ? std::min(kPfMaxK, std::max(k, pse ? atoi(pse) : kRsPreSel)) : 0;
   const char* pde = getenv("MIVS_RS_PRE_DIV");
-  const int pre_div = std::max(1, pde ? atoi(pde) : (pre_dims > 0 ? kRsPreDivNominate : kRsPreDiv));
+  const int pre_div = std::max(1, pde ? atoi(pde) : (pre_f8 ? kRsPreDivF8 : (pre_dims > 0 ? kRsPreDivNominate : kRsPreDiv)));
   if (pre_dims > 0 && idx->pre_norms_dims != pre_dims) {
     idx->pre_norms.reserve(sizeof(float) * (size_t)L.n_groups * kGroupRows);
     HIPCHK(launch_partial_norms(L.groups.as<float>(), L.norms.as<float>(), L.n_groups, dp, pre_dims,
@@ -1060,15 +1093,14 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
     ws.pre_kth.reserve(sizeof(float) * nq);
     pf_scan_refine(idx, s, q, nq, k, 1, nullptr, nullptr, nullptr, ws.pre_goff.as<int64_t>(), nl2,
                    ws.pre_kth.as<float>(), pre_dims / 16, pre_dims > 0 ? idx->pre_norms.as<float>() : nullptr,
-                   pre_sel);
+                   pre_sel, pre_f8);
   }
   // 2. headers (pf_scan_refine left the fp16 queries, their scales and residuals in ws.qh / qscale / qres)
   ws.qhdr.reserve(sizeof(float4) * (nq + 1));
   float4* qhdr = ws.qhdr.as<float4>();
   ws.rs_tq.reserve(sizeof(float) * nq);
   HIPCHK(launch_rs_headers(ws.pre_kth.as<float>(), nq, ws.qscale.as<float>(), ws.qn.as<float>(), ws.qres.as<float>(),
-                           idx->x_norm_max, idx->x_res_max, dp, idx->metric, pre_sel > 0 ? 1 : 0, qhdr,
-                           ws.rs_tq.as<float>(), s));
+                           idx->x_norm_max, idx->x_res_max, dp, idx->metric, qhdr, ws.rs_tq.as<float>(), s));
   if (getenv("MIVS_RS_PRE_STATS")) {  // diagnostic: the pre-pass's k-th keys and T_q (stderr)
     std::vector<float> hk(nq), ht(nq);
     HIPCHK(hipMemcpyAsync(hk.data(), ws.pre_kth.p, sizeof(float) * nq, hipMemcpyDeviceToHost, s));
@@ -1085,8 +1117,8 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
     std::vector<float> sorted = ht;
     std::sort(sorted.begin(), sorted.end());
     auto pc = [&](double f) { return sorted[std::min<int64_t>(nq - 1, (int64_t)(f * nq))]; };
-    fprintf(stderr, "[rs pre] dims %d div %d sel %d | mean kth %.6f mean T_q %.6f | inf %lld of %lld | T_q p10 %.4f "
-            "p50 %.4f p90 %.4f p99 %.4f max %.4f\n", pre_dims, pre_div, pre_sel, sk / nf, st / nf, (long long)ninf,
+    fprintf(stderr, "[rs pre] f8 %d dims %d div %d sel %d | mean kth %.6f mean T_q %.6f | inf %lld of %lld | T_q p10 %.4f "
+            "p50 %.4f p90 %.4f p99 %.4f max %.4f\n", (int)pre_f8, pre_dims, pre_div, pre_sel, sk / nf, st / nf, (long long)ninf,
             (long long)nq, pc(0.1), pc(0.5), pc(0.9), pc(0.99), sorted[nq - 1]);
   }
   // 3. probe map: items = (list, block of kRsBlockGroups groups); every query of a list in one tile column

@@ -219,6 +219,9 @@ struct PfScanArgs {
                               // with the non-temporal policy (pair mode only)
   int nk_scan;                // 0: every dim; else only dims [0, 16 nk_scan) (a multiple of 4 or 6 k-steps) with
                               // row_norms = the rows' norms over those dims: K13's pre-pass nomination score
+  const uint8_t* groups_f8;   // optional (K13's pre-pass nomination, pair mode): fp8 rows (launch_groups_to_f8);
+  const uint8_t* q8;          //   then the fp8 queries (launch_queries_to_f8) and their scales replace groups_h,
+  const float* qscale8;       //   qh and qscale
 };
 
 // K13 row-stationary pre-filter scan (rsscan.hip): work item = (list, block of
@@ -232,8 +235,11 @@ constexpr int kRsBlockGroups = kRsWaves;
 // MIVS_RS_PRE_DIMS dims, and the kRsPreSel best-scored rows of each query get their pinned keys (MIVS_RS_PRE_SEL)
 constexpr int kRsPreDiv = 4;
 constexpr int kRsPreDims = 0;
+// the fp8 nomination (MIVS_RS_PRE_F8): the first 1 / kRsPreDivF8 of the nearest list scored on fp8 copies of the
+// rows and queries over every dim, the kRsPreSel best rows of each query verified with pinned keys
+constexpr int kRsPreDivF8 = 4;
 constexpr int kRsPreDivNominate = 1;
-constexpr int kRsPreSel = 16;
+constexpr int kRsPreSel = 10;
 constexpr int kRsWaveCapMax = 16384;  // records of a K13 wave's candidate stream (more: all queries fall back)
 constexpr int kRsRecInt4 = 3;         // a record: 8 dots of one lane and query half + {first row position, query}
 constexpr int kRsMaxBatch = 32768;    // queries per K13 search batch (the LDS-histogram bucketing's bins)
@@ -331,7 +337,8 @@ struct PfRefineArgs {
   float* kth_out;             // optional (K13's pre-pass): only the k-th smallest approximate key per query
                               // (+inf: fewer than k candidates), no refine
   int verify_sel;             // with kth_out: > 0 -> the candidates with the verify_sel smallest keys (nomination
-                              // scores) get their pinned fp32 keys, and kth_out is the k-th smallest of THOSE
+                              // scores) get fp32 keys (within delta of their pinned keys), and kth_out is the k-th
+                              // smallest of THOSE
 };
 
 hipError_t launch_pf_scan(const PfScanArgs& a, int grid, size_t lds, hipStream_t s);
@@ -384,6 +391,11 @@ size_t rs_bucket_tmp_bytes(int nq, int n_waves);
 hipError_t launch_rs_bucket(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
                             const float4* qhdr, const float* row_norms, int metric, int64_t* cand_off,
                             float* cand_key, int* cand_pos, void* tmp, int* lost, int grid, hipStream_t s);
+// fp8 (e4m3) copies for K13's pre-pass nomination: rows at scale 2^hx8 in the operand layout of
+// k_pf_scan<.., F8> (dp % 32 == 0), queries at their own power of two (qscale8[q] = the fp8 dot -> fp32 dot)
+hipError_t launch_groups_to_f8(const float* groups, int64_t n_groups, int dp, int hx8, uint8_t* out, hipStream_t s);
+hipError_t launch_queries_to_f8(const float* q, int64_t nq, int d, int dp, int hx8, uint8_t* out, float* qscale8,
+                                hipStream_t s);
 // every row slot's squared norm over its first dims dims (+inf on pad rows): K13's pre-pass nomination
 hipError_t launch_partial_norms(const float* groups, const float* norms, int64_t n_groups, int dp, int dims,
                                 float* out, hipStream_t s);
@@ -395,11 +407,10 @@ hipError_t launch_rs_items(const int* work_off, const int* bucket_off, const int
                            int max_items, int4* items, int* bounds, hipStream_t s);
 hipError_t launch_rs_tiles(const int64_t* bucket_q, const int* bucket_off, int n_lists, const uint16_t* qh,
                            const float4* qhdr, int nq, int dp, char* tiles, hipStream_t s);
-// tq (optional): T_q per query, the bound K11 checks its final window against; pre_exact: pre_kth holds pinned
-// keys (the pre-pass's verified nominees), not approximate ones
+// tq (optional): T_q per query, the bound K11 checks its final window against
 hipError_t launch_rs_headers(const float* pre_kth, int64_t nq, const float* qscale, const float* qnorms,
-                             const float* qres, float x_norm_max, float x_res_max, int dp, int metric, int pre_exact,
-                             float4* hdr, float* tq, hipStream_t s);
+                             const float* qres, float x_norm_max, float x_res_max, int dp, int metric, float4* hdr,
+                             float* tq, hipStream_t s);
 hipError_t launch_gather_ids(const int64_t* src, const int64_t* idx, int64_t n, int64_t* out, hipStream_t s);
 constexpr unsigned kPfOrdInf = 0xFF800000u;  // order mapping of +inf (qtheta's initial value)
 // fp32 groups -> fp16 groups scaled by 2^hx_exp (FTZ below the fp16 normal range), per-index maxima of

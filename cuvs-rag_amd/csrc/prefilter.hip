@@ -156,7 +156,10 @@ __device__ __forceinline__ float pf_theta(const float* __restrict__ l8, float de
 // eighth of the (list, chunk, tile)-ordered items, so the query tiles of one chunk run at the same
 // time on CUs sharing an L2 and all but the first read the chunk's rows as L2 hits. A workgroup
 // whose queue is empty takes items from the next queues.
-template <int METRIC, int D, int R, bool NT = false>
+// F8 (K13's pre-pass nomination, pair mode only): the rows and queries are fp8 copies (groups_f8 / q8, the
+// [32-dim superblock][32 rows][2 halves][16 B] operand layout of k_groups_to_f8), each 16-B load feeds two
+// v_mfma_f32_32x32x16_fp8_fp8 k-steps; the keys only nominate rows whose pinned keys K11 then computes
+template <int METRIC, int D, int R, bool NT = false, bool F8 = false>
 __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int64_t* s_q = reinterpret_cast<int64_t*>(smem);          // [64] query ids (-1: empty)
@@ -177,7 +180,9 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
   const int dp = a.dp;
   const int nb = dp >> 3;  // 8-dim blocks
   // 16-dim k-steps (a multiple of D); nk_scan: only the first 16 nk_scan dims (K13's pre-pass nomination)
-  const int nk = a.nk_scan > 0 ? a.nk_scan : dp >> 4;
+  const int nk = F8 ? dp >> 5 : (a.nk_scan > 0 ? a.nk_scan : dp >> 4);
+  static_assert(!F8 || R == 2, "fp8 rows: pair mode only");
+  const int bq1off = F8 ? dp * 32 : nb * 512;  // B image: query group 1's bytes after group 0's
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: the k-loop is a scalar loop
@@ -185,7 +190,8 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
   const int h = lane >> 5;
   const int total = a.work_off[a.n_lists];
   const int grp = blockIdx.x & 7;
-  const int64_t pstride = (int64_t)kPfWaves * nb * 256;  // halves between a wave's consecutive groups
+  // halves between a wave's consecutive groups (F8: a group is 32 dp bytes)
+  const int64_t pstride = F8 ? (int64_t)kPfWaves * 16 * dp : (int64_t)kPfWaves * nb * 256;
   const float xnmax2 = a.x_norm_max * a.x_norm_max;       // >= every row's pinned norm
   if (tid == 0) s_misc[1] = 0;                            // queues exhausted so far
   // diagnostic phase clocks (a.prof != nullptr only under MIVS_PF_FLAGS & 32)
@@ -237,8 +243,9 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
         s_slot[tid] = a.bucket_slot[e0 + tid] + chunk;
         const float qn = a.qnorms[q];
         s_qn[tid] = qn;
-        s_qs[tid] = a.qscale[q];
-        s_dl[tid] = pf_delta<METRIC>(qn, a.qres[q], a.x_norm_max, a.x_res_max, dp);
+        s_qs[tid] = F8 ? a.qscale8[q] : a.qscale[q];
+        // (F8: the window only widens which nominees a slot keeps; 2^7 x the fp16 bound)
+        s_dl[tid] = pf_delta<METRIC>(qn, a.qres[q], a.x_norm_max, a.x_res_max, dp) * (F8 ? 128.0f : 1.0f);
         s_th[tid] = pf_unord(__hip_atomic_load(a.qtheta + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
       } else {
         s_q[tid] = -1;
@@ -258,7 +265,28 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
     // 1 KiB wave read (conflict-free) at an immediate offset per k-step. Piece i of the image is
     // written by thread i mod 512 (linear, conflict-free); its source is a 16-B piece of query row
     // (i/32/nb)*32 + i%32. nb/8 pieces per thread (dp % 64 == 0), loads batched by 4.
-    if (!(a.flags & 8)) {
+    if (F8 && !(a.flags & 8)) {
+      // fp8 B image: [2 query groups][dp/32 superblocks][64 lanes (j, h)] x 16 B, piece (S, j, h) = bytes
+      // 32 S + 16 h .. + 16 of query j's fp8 row (k_queries_to_f8 lays them out as the operands)
+      const int nsb = dp >> 5;
+      const int per = dp >> 7;  // 4 dp pieces over 512 threads
+      for (int i0 = 0; i0 < per; i0 += 2) {
+        uint4 v[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int i = tid + (i0 + u) * kPfThreads;
+          const int qg = i / (nsb * 64), rem = i - qg * (nsb * 64);
+          const int S = rem >> 6, L = rem & 63;
+          const int64_t q = (i0 + u < per) ? s_q[qg * 32 + (L & 31)] : -1;
+          v[u] = make_uint4(0u, 0u, 0u, 0u);
+          if (q >= 0) v[u] = *reinterpret_cast<const uint4*>(a.q8 + q * dp + S * 32 + (L >> 5) * 16);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          if (i0 + u < per) *reinterpret_cast<uint4*>(s_b + (size_t)(tid + (i0 + u) * kPfThreads) * 16) = v[u];
+      }
+    }
+    if (!F8 && !(a.flags & 8)) {
       const int per = nb >> 3;
       for (int i0 = 0; i0 < per; i0 += 4) {
         uint4 v[4];
@@ -323,7 +351,8 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
       if (npw > 0) {
         const int rot = s_misc[2] % npair;
         auto phys = [&](int pr) { return pr + rot < npair ? pr + rot : pr + rot - npair; };
-        const uint16_t* abase = a.groups_h + ((g_begin + wave) * nb + h) * 256 + j * 8;
+        const uint16_t* abase = F8 ? reinterpret_cast<const uint16_t*>(a.groups_f8) + (g_begin + wave) * 16 * dp + j * 16 + h * 8
+                                   : a.groups_h + ((g_begin + wave) * nb + h) * 256 + j * 8;
         int lp_ = 0, ls = 0;  // pair / k-step of the next load (past the end: re-read the last pair)
         auto pair_ptr = [&](int pr, int which) {
           int gi = 2 * phys(pr) + which;
@@ -355,23 +384,36 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
         int p = 0, s = 0;
         h8 bq0[2], bq1[2];
         bq0[0] = *reinterpret_cast<const h8*>(s_bl);
-        bq1[0] = *reinterpret_cast<const h8*>(s_bl + nb * 512);
+        bq1[0] = *reinterpret_cast<const h8*>(s_bl + bq1off);
         for (int t0 = 0; t0 < npair * nk; t0 += D) {
 #pragma unroll
           for (int u = 0; u < D; ++u) {
             int sn = s + u + 1;
             if (sn >= nk) sn -= nk;
             bq0[(u + 1) & 1] = *reinterpret_cast<const h8*>(s_bl + sn * 1024);
-            bq1[(u + 1) & 1] = *reinterpret_cast<const h8*>(s_bl + nb * 512 + sn * 1024);
-            a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[u], bq0[u & 1], a0, 0, 0, 0);
-            a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[u], bq1[u & 1], a1, 0, 0, 0);
-            b0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(rb[u], bq0[u & 1], b0, 0, 0, 0);
-            b1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(rb[u], bq1[u & 1], b1, 0, 0, 0);
+            bq1[(u + 1) & 1] = *reinterpret_cast<const h8*>(s_bl + bq1off + sn * 1024);
+            if constexpr (F8) {
+              typedef long l2 __attribute__((ext_vector_type(2)));
+              const l2 xa = __builtin_bit_cast(l2, ra[u]), xb = __builtin_bit_cast(l2, rb[u]);
+              const l2 y0 = __builtin_bit_cast(l2, bq0[u & 1]), y1 = __builtin_bit_cast(l2, bq1[u & 1]);
+#pragma unroll
+              for (int e = 0; e < 2; ++e) {
+                a0 = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(xa[e], y0[e], a0, 0, 0, 0);
+                a1 = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(xa[e], y1[e], a1, 0, 0, 0);
+                b0 = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(xb[e], y0[e], b0, 0, 0, 0);
+                b1 = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(xb[e], y1[e], b1, 0, 0, 0);
+              }
+            } else {
+              a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[u], bq0[u & 1], a0, 0, 0, 0);
+              a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[u], bq1[u & 1], a1, 0, 0, 0);
+              b0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(rb[u], bq0[u & 1], b0, 0, 0, 0);
+              b1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(rb[u], bq1[u & 1], b1, 0, 0, 0);
+            }
             ra[u] = ld_row_h8<NT>(na + (ls + u) * 512);
             rb[u] = ld_row_h8<NT>(nbp + (ls + u) * 512);
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
-            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // MFMA
-            __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);  // VMEM read
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);            // DS read
+            __builtin_amdgcn_sched_group_barrier(0x008, F8 ? 8 : 4, 0);   // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);            // VMEM read
           }
           ls += D;
           if (ls == nk) { ls = 0; if (++lp_ < npair) { na = pair_ptr(lp_, 0); nbp = pair_ptr(lp_, 1); } }
@@ -662,7 +704,9 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
       return;
     }
     // verify: the nominees (key <= the verify_sel-th smallest; ties beyond 64 dropped: any probed rows bound the
-    // final k-th key) get their pinned fp32 keys; kth_out = the k-th smallest of those (+inf: fewer than k)
+    // final k-th key) get fp32 keys, the wave summing each row's dot in parallel (not the pinned order: the key is
+    // within the pinned one's summation-error term of delta, so kth + 2 delta still bounds the final window's
+    // k-th approximate key, k_rs_headers); kth_out = the k-th smallest (+inf: fewer than k)
     int cnt = 0;
     for (int64_t c = sb * a.slot_k; c < c1; c += 64) {
       const int64_t cc = c + lane;
@@ -680,7 +724,33 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
     for (int i = lane; i < a.dp; i += 64) s_qv[wv][i] = (live && i < a.d) ? a.queries[qrow * a.d + i] : 0.0f;
     __syncthreads();
     float P = INFINITY;
-    if (live && lane < cnt && lane < 64) P = pf_pinned_key<METRIC>(a, s_cp[wv][lane], s_qv[wv], qn);
+    const int nvf = live ? (cnt < 64 ? cnt : 64) : 0;
+    const int nb = a.dp >> 3;
+    for (int n = 0; n < nvf; ++n) {
+      const int pos = s_cp[wv][n];
+      const float* rowp = a.rows_rm ? a.rows_rm + (int64_t)pos * a.dp
+                                    : a.groups + ((int64_t)(pos >> 5) * nb * kGroupRows + (pos & 31)) * 8;
+      const int64_t bstride = a.rows_rm ? 8 : 256;
+      float acc = 0.0f;
+      for (int b = lane; b < nb; b += 64) {
+        const float4 x0 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride);
+        const float4 x1 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride + 4);
+        const float4 y0 = *reinterpret_cast<const float4*>(s_qv[wv] + 8 * b);
+        const float4 y1 = *reinterpret_cast<const float4*>(s_qv[wv] + 8 * b + 4);
+        acc = fmaf(x0.x, y0.x, acc); acc = fmaf(x0.y, y0.y, acc); acc = fmaf(x0.z, y0.z, acc); acc = fmaf(x0.w, y0.w, acc);
+        acc = fmaf(x1.x, y1.x, acc); acc = fmaf(x1.y, y1.y, acc); acc = fmaf(x1.z, y1.z, acc); acc = fmaf(x1.w, y1.w, acc);
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+      if (lane == n) {
+        if (METRIC == kL2) {
+          const float v = fmaf(-2.0f, acc, a.row_norms[pos] + qn);
+          P = v > 0.0f ? v : 0.0f;
+        } else {
+          P = -acc;
+        }
+      }
+    }
 #pragma unroll
     for (int size = 2; size <= 64; size <<= 1) {
 #pragma unroll
@@ -1408,12 +1478,12 @@ size_t pf_scan_lds_bytes(int dp, int chunk_groups) {
   return kPfSmall + (size_t)kPfQTile * 18 * 4 + norms + (b > (size_t)kPfMergeBytes ? b : (size_t)kPfMergeBytes);
 }
 
-template <int METRIC, int D, int R, bool NT = false>
+template <int METRIC, int D, int R, bool NT = false, bool F8 = false>
 static hipError_t launch_pf_scan_md(const PfScanArgs& a, int grid, size_t lds, hipStream_t s) {
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pf_scan<METRIC, D, R, NT>),
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pf_scan<METRIC, D, R, NT, F8>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL((k_pf_scan<METRIC, D, R, NT>), dim3(grid), dim3(kPfThreads), lds, s, a);
+  hipLaunchKernelGGL((k_pf_scan<METRIC, D, R, NT, F8>), dim3(grid), dim3(kPfThreads), lds, s, a);
   return hipGetLastError();
 }
 
@@ -1421,6 +1491,13 @@ template <int METRIC>
 static hipError_t launch_pf_scan_m(const PfScanArgs& a, int grid, size_t lds, hipStream_t s) {
   // default: two groups per pass with 6-deep rings (half the LDS operand traffic per flop: the kernel is
   // power-bound); MIVS_PF_PAIR=0: one group per pass with MIVS_PF_DEPTH (16) k-steps in flight
+  if (a.groups_f8) {  // fp8 nomination (pair mode): superblocks of 32 dims, a ring of 6 or 4
+    const int nsb = a.dp / 32;
+    if (a.q8 == nullptr || a.qscale8 == nullptr || a.nk_scan > 0) return hipErrorInvalidValue;
+    if (nsb % 6 == 0) return launch_pf_scan_md<METRIC, 6, 2, true, true>(a, grid, lds, s);
+    if (nsb % 4 == 0) return launch_pf_scan_md<METRIC, 4, 2, true, true>(a, grid, lds, s);
+    return hipErrorInvalidValue;
+  }
   const int nk = a.nk_scan > 0 ? a.nk_scan : a.dp / 16;
   if (a.nk_scan > 0 && (a.nk_scan > a.dp / 16 || (a.nk_scan % 4 != 0 && a.nk_scan % 6 != 0)))
     return hipErrorInvalidValue;
@@ -1518,6 +1595,83 @@ hipError_t launch_groups_to_half(const float* groups, int64_t n_groups, int dp, 
   if (n_groups <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_groups_to_half, pf_grid(n_groups * kGroupRows, 256), dim3(256), 0, s, groups, n_groups, dp,
                      hx_exp, out, stats);
+  return hipGetLastError();
+}
+
+// fp8 (e4m3) copies for K13's pre-pass nomination (k_pf_scan<.., F8>): rows at 2^hx8, a query at its own
+// 2^qexp (its |q| max in [128, 256)); piece (S, j, h) of a group = dims 32 S + 8 h .. + 7 and 32 S + 16 + 8 h ..
+// + 7 of row j: the A operands of k-steps 2 S and 2 S + 1 of v_mfma_f32_32x32x16_fp8_fp8 for lane (j, h)
+__device__ __forceinline__ uint4 f8_pack16(const float (&v)[16], float sc) {
+  int w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int x = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * i] * sc, v[4 * i + 1] * sc, 0, false);
+    w[i] = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * i + 2] * sc, v[4 * i + 3] * sc, x, true);
+  }
+  return make_uint4((unsigned)w[0], (unsigned)w[1], (unsigned)w[2], (unsigned)w[3]);
+}
+
+__global__ void k_groups_to_f8(const float* __restrict__ groups, int64_t n_groups, int dp, int hx8,
+                               uint8_t* __restrict__ out) {
+  const int nsb = dp >> 5, nb = dp >> 3;
+  const int64_t n = n_groups * nsb * 64;
+  const float sc = ldexpf(1.0f, hx8);
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t g = t / (nsb * 64);
+    const int rem = (int)(t - g * (nsb * 64));
+    const int S = rem >> 6, jj = (rem & 63) >> 1, hh = rem & 1;
+    float v[16];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const float* src = groups + ((g * nb + 4 * S + 2 * e + hh) * kGroupRows + jj) * 8;
+      const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
+      v[8 * e + 0] = x0.x; v[8 * e + 1] = x0.y; v[8 * e + 2] = x0.z; v[8 * e + 3] = x0.w;
+      v[8 * e + 4] = x1.x; v[8 * e + 5] = x1.y; v[8 * e + 6] = x1.z; v[8 * e + 7] = x1.w;
+    }
+    *reinterpret_cast<uint4*>(out + t * 16) = f8_pack16(v, sc);
+  }
+}
+
+// one wave per query: its |q| max, then the pieces (S, h) of its fp8 row (zero past d) and qscale8 = 2^-(hx8 + qexp)
+__global__ __launch_bounds__(256) void k_queries_to_f8(const float* __restrict__ q, int64_t nq, int d, int dp, int hx8,
+                                                       uint8_t* __restrict__ out, float* __restrict__ qscale8) {
+  const int lane = threadIdx.x & 63;
+  const int64_t qi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (qi >= nq) return;
+  const float* row = q + qi * d;
+  float m = 0.0f;
+  for (int i = lane; i < d; i += 64) m = fmaxf(m, fabsf(row[i]));
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  const int e = (m > 0.0f && m < INFINITY) ? 7 - ilogbf(m) : 0;  // m 2^e in [128, 256)
+  const float sc = ldexpf(1.0f, e);
+  for (int pc = lane; pc < (dp >> 4); pc += 64) {  // piece pc = (S, h): 16 B
+    const int S = pc >> 1, hh = pc & 1;
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = 32 * S + 16 * (i >> 3) + 8 * hh + (i & 7);
+      v[i] = c < d ? row[c] : 0.0f;
+    }
+    *reinterpret_cast<uint4*>(out + qi * dp + pc * 16) = f8_pack16(v, sc);
+  }
+  if (lane == 0) qscale8[qi] = ldexpf(1.0f, -(hx8 + e));
+}
+
+hipError_t launch_groups_to_f8(const float* groups, int64_t n_groups, int dp, int hx8, uint8_t* out, hipStream_t s) {
+  if (n_groups <= 0) return hipSuccess;
+  if (dp % 32 != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_groups_to_f8, pf_grid(n_groups * (dp / 32) * 64, 256), dim3(256), 0, s, groups, n_groups, dp,
+                     hx8, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_queries_to_f8(const float* q, int64_t nq, int d, int dp, int hx8, uint8_t* out, float* qscale8,
+                                hipStream_t s) {
+  if (nq <= 0) return hipSuccess;
+  if (dp % 32 != 0 || d > dp) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_queries_to_f8, dim3((unsigned)ceil_div(nq, (int64_t)4)), dim3(256), 0, s, q, nq, d, dp, hx8,
+                     out, qscale8);
   return hipGetLastError();
 }
 

@@ -569,8 +569,7 @@ __global__ __launch_bounds__(1024) void k_rs_bounds(const int* __restrict__ work
 template <int METRIC>
 __global__ void k_rs_headers(const float* __restrict__ pre_kth, int64_t nq, const float* __restrict__ qscale,
                              const float* __restrict__ qnorms, const float* __restrict__ qres, float x_norm_max,
-                             float x_res_max, int dp, int pre_exact, float4* __restrict__ hdr,
-                             float* __restrict__ tq) {
+                             float x_res_max, int dp, float4* __restrict__ hdr, float* __restrict__ tq) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q > nq) return;
   if (q == nq) {  // the null header
@@ -580,15 +579,15 @@ __global__ void k_rs_headers(const float* __restrict__ pre_kth, int64_t nq, cons
   const float qn = qnorms[q];
   const float delta = pf_delta<METRIC>(qn, qres[q], x_norm_max, x_res_max, dp);
   float T = INFINITY;
-  // the k-th smallest approximate key (K10's) over the sample rows, or (pre_exact) the k-th smallest PINNED key
-  // over the verified nominees
+  // the k-th smallest approximate key (K10's) over the sample rows, or the k-th smallest fp32 key of the verified
+  // nominees (K11's verify mode: each within delta of its pinned key, as an approximate key is)
   const float kth = pre_kth[q];
   if (kth < INFINITY) {
-    // those k rows are probed rows: their pinned keys are <= kth + delta (pre_exact: <= kth), so the final k-th
-    // approximate key (K13's sums may round differently from K10's: each is within delta of the pinned key) is
-    // Ak <= U = kth + 2 delta (pre_exact: kth + delta), and the final window pf_window(Ak) <= pf_window(U)
-    // (monotone); one more relative step covers the roundings of U and T
-    const float U = kth + (pre_exact ? 1.0f : 2.0f) * delta;
+    // those k rows are probed rows: their pinned keys are <= kth + delta, so the final k-th approximate key
+    // (K13's sums may round differently from K10's: each is within delta of the pinned key) is
+    // Ak <= U = kth + 2 delta, and the final window pf_window(Ak) <= pf_window(U) (monotone); one more
+    // relative step covers the roundings of U and T
+    const float U = kth + 2.0f * delta;
     T = pf_window(U, delta);
     T = T + fabsf(T) * 0x1p-20f + 1e-30f;
   }
@@ -1023,15 +1022,15 @@ hipError_t launch_rs_pre_lists(const int64_t* goff, int n_lists, int div, int mi
 }
 
 hipError_t launch_rs_headers(const float* pre_kth, int64_t nq, const float* qscale, const float* qnorms,
-                             const float* qres, float x_norm_max, float x_res_max, int dp, int metric, int pre_exact,
-                             float4* hdr, float* tq, hipStream_t s) {
+                             const float* qres, float x_norm_max, float x_res_max, int dp, int metric, float4* hdr,
+                             float* tq, hipStream_t s) {
   const dim3 grid((unsigned)ceil_div(nq + 1, 256));
   if (metric == kIP)
     hipLaunchKernelGGL(k_rs_headers<kIP>, grid, dim3(256), 0, s, pre_kth, nq, qscale, qnorms, qres, x_norm_max,
-                       x_res_max, dp, pre_exact, hdr, tq);
+                       x_res_max, dp, hdr, tq);
   else
     hipLaunchKernelGGL(k_rs_headers<kL2>, grid, dim3(256), 0, s, pre_kth, nq, qscale, qnorms, qres, x_norm_max,
-                       x_res_max, dp, pre_exact, hdr, tq);
+                       x_res_max, dp, hdr, tq);
   return hipGetLastError();
 }
 

@@ -61,8 +61,10 @@ SEARCH_SWITCHES = [
     {"MIVS_PF_ROWSTAT": "0", "MIVS_PF_SLOT_K": "16"},
     {"MIVS_RS_PRE_DIV": "1"},
     {"MIVS_RS_PRE_DIV": "16"},
-    {"MIVS_RS_PRE_DIMS": "96"},                                       # pre-pass: nominate on 96 dims + verify
-    {"MIVS_RS_PRE_DIMS": "64", "MIVS_RS_PRE_DIV": "2", "MIVS_RS_PRE_SEL": "10"},
+    {"MIVS_RS_PRE_F8": "0"},                                          # pre-pass: the fp16 sample (round 2)
+    {"MIVS_RS_PRE_F8": "0", "MIVS_RS_PRE_DIMS": "96"},                # pre-pass: nominate on 96 dims + verify
+    {"MIVS_RS_PRE_F8": "0", "MIVS_RS_PRE_DIMS": "64", "MIVS_RS_PRE_DIV": "2", "MIVS_RS_PRE_SEL": "10"},
+    {"MIVS_RS_PRE_DIV": "1", "MIVS_RS_PRE_SEL": "10"},                # fp8 nomination over the whole list
     {"MIVS_RS_PRE_STATS": "1"},                                       # pre-pass T_q stats (stderr only)
     {"MIVS_RS_FLAGS": "24"},                                          # K13 clocks (stderr only)
     {"MIVS_RS_WAVE_CAP": "2"},                                        # K13 streams overflow: the fallback
