@@ -289,7 +289,10 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
 constexpr int kSmallPer = 16;
 constexpr int kSmallWaves = 4;
 
-template <int METRIC>
+// V2 (default; MIVS_SELECT_SMALL_V2=0 keeps the bit search only): T0 = the need-th smallest of the 64 lanes' minima bounds the need-th
+// smallest key from above (need <= 64 lanes, each minimum a distinct key at or below it); when at most 64 keys lie
+// at or below T0 they are the candidates -- one per lane, bitonic-sorted by (key, id) -- without the bit search
+template <int METRIC, bool V2>
 __global__ __launch_bounds__(64 * kSmallWaves) void k_select_small(SelectArgs a) {
   __shared__ uint32_t s_u[kSmallWaves][64];
   __shared__ int64_t s_i[kSmallWaves][64];
@@ -340,7 +343,28 @@ __global__ __launch_bounds__(64 * kSmallWaves) void k_select_small(SelectArgs a)
   };
   uint32_t T = 0;
   int64_t I = LLONG_MAX;  // among keys == T: ids <= I are chosen
-  if (need > 0) {
+  bool searched = false;
+  if (V2 && need > 0) {
+    uint32_t lm = 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 0; i < kSmallPer; ++i) lm = u[i] < lm ? u[i] : lm;
+    // bitonic sort of the 64 lane minima, ascending
+#pragma unroll
+    for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        const uint32_t o = __shfl_xor(lm, stride);
+        const bool lower = (lane & stride) == 0, up = (lane & size) == 0;
+        lm = (lower == up) ? (o < lm ? o : lm) : (o > lm ? o : lm);
+      }
+    }
+    const uint32_t T0 = __shfl(lm, need - 1);
+    if (T0 != 0xFFFFFFFFu && count_le(T0) <= 64) {
+      T = T0;  // every key <= T0 is taken (I = +inf): at most 64, the need smallest among them
+      searched = true;
+    }
+  }
+  if (need > 0 && !searched) {
     uint32_t lo = umin, hi = umax;  // the need-th smallest valid key lies in [lo, hi]
     while (lo < hi) {
       const uint32_t mid = lo + ((hi - lo) >> 1);
@@ -389,8 +413,9 @@ __global__ __launch_bounds__(64 * kSmallWaves) void k_select_small(SelectArgs a)
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  uint32_t ku = lane < need ? s_u[wv][lane] : 0xFFFFFFFFu;
-  int64_t ki = lane < need ? s_i[wv][lane] : LLONG_MAX;
+  const int ncand = searched ? (nsel < 64 ? nsel : 64) : need;
+  uint32_t ku = lane < ncand ? s_u[wv][lane] : 0xFFFFFFFFu;
+  int64_t ki = lane < ncand ? s_i[wv][lane] : LLONG_MAX;
   // bitonic sort of the 64 lanes by (key, id), ascending
 #pragma unroll
   for (int size = 2; size <= 64; size <<= 1) {
@@ -439,8 +464,15 @@ hipError_t launch_select(const SelectArgs& a, hipStream_t s) {
   const bool expl = a.slot_info == nullptr;
   if (!expl && a.k <= 64 && a.slots_per_q * a.slot_rows <= 64 * kSmallPer) {  // K8s
     const dim3 grid((unsigned)ceil_div(a.nq, (int64_t)kSmallWaves)), block(64 * kSmallWaves);
-    if (a.metric == kIP) hipLaunchKernelGGL(k_select_small<kIP>, grid, block, 0, s, a);
-    else hipLaunchKernelGGL(k_select_small<kL2>, grid, block, 0, s, a);
+    const char* v2e = getenv("MIVS_SELECT_SMALL_V2");
+    const bool v2 = !(v2e && v2e[0] == '0');  // 122 -> 72 us for the coarse probe's 10k x 1024 keys
+    if (v2) {
+      if (a.metric == kIP) hipLaunchKernelGGL((k_select_small<kIP, true>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((k_select_small<kL2, true>), grid, block, 0, s, a);
+    } else {
+      if (a.metric == kIP) hipLaunchKernelGGL((k_select_small<kIP, false>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((k_select_small<kL2, false>), grid, block, 0, s, a);
+    }
     return hipGetLastError();
   }
   if (a.k <= 512) return launch_cap<1024>(a, expl, s);

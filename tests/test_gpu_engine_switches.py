@@ -62,6 +62,7 @@ SEARCH_SWITCHES = [
     {"MIVS_RS_PRE_DIV": "1"},
     {"MIVS_RS_PRE_DIV": "16"},
     {"MIVS_RS_PRE_F8": "0"},                                          # pre-pass: the fp16 sample (round 2)
+    {"MIVS_SELECT_SMALL_V2": "0"},                                    # K8s by the bit search alone
     {"MIVS_RS_PRE_F8": "0", "MIVS_RS_PRE_DIMS": "96"},                # pre-pass: nominate on 96 dims + verify
     {"MIVS_RS_PRE_F8": "0", "MIVS_RS_PRE_DIMS": "64", "MIVS_RS_PRE_DIV": "2", "MIVS_RS_PRE_SEL": "10"},
     {"MIVS_RS_PRE_DIV": "1", "MIVS_RS_PRE_SEL": "10"},                # fp8 nomination over the whole list
