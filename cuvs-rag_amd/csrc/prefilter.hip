@@ -611,33 +611,6 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
   }
 }
 
-// the pinned fp32 key of row slot pos (oracle orc_dot order) against the query row qv (zero past d)
-template <int METRIC>
-__device__ __forceinline__ float pf_pinned_key(const PfRefineArgs& a, int pos, const float* qv, float qn) {
-  const int nb = a.dp >> 3;
-  // the row's block b: 8 floats at rowp + b * bstride (row-major copy: contiguous; group layout: 1 KiB apart)
-  const float* rowp = a.rows_rm ? a.rows_rm + (int64_t)pos * a.dp
-                                : a.groups + ((int64_t)(pos >> 5) * nb * kGroupRows + (pos & 31)) * 8;
-  const int64_t bstride = a.rows_rm ? 8 : 256;
-  float acc = 0.0f;
-#pragma unroll 12
-  for (int b = 0; b < nb; ++b) {
-    const float4 x0 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride);
-    const float4 x1 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride + 4);
-    const float4 y0 = *reinterpret_cast<const float4*>(qv + 8 * b);
-    const float4 y1 = *reinterpret_cast<const float4*>(qv + 8 * b + 4);
-    acc = fmaf(x0.x, y0.x, acc); acc = fmaf(x1.x, y1.x, acc);
-    acc = fmaf(x0.y, y0.y, acc); acc = fmaf(x1.y, y1.y, acc);
-    acc = fmaf(x0.z, y0.z, acc); acc = fmaf(x1.z, y1.z, acc);
-    acc = fmaf(x0.w, y0.w, acc); acc = fmaf(x1.w, y1.w, acc);
-  }
-  if (METRIC == kL2) {
-    const float v = fmaf(-2.0f, acc, a.row_norms[pos] + qn);
-    return v > 0.0f ? v : 0.0f;
-  }
-  return -acc;
-}
-
 // K11. One wave per query (4 per workgroup; every wave reaches every barrier).
 template <int METRIC>
 __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
@@ -660,7 +633,161 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
   // fewer than k keys below it is the k-th smallest (ties counted), no shuffles; more: the running top-k
   // (K7's ballot insertion). Both return the same value.
   float mk = INFINITY, tk = INFINITY;
-  const int ksel = a.kth_out && a.verify_sel > 0 ? a.verify_sel : k;  // (verify: the nominees' count)
+  const int64_t n_c = c1 - sb * a.slot_k;
+  if (n_c <= kPfSelRegs * 64) {
+    uint32_t u[kPfSelRegs];
+#pragma unroll
+    for (int i = 0; i < kPfSelRegs; ++i) {
+      const int64_t cc = sb * a.slot_k + i * 64 + lane;
+      const float f = cc < c1 ? a.slot_key[cc] : INFINITY;
+      const uint32_t b = __float_as_uint(f == 0.0f ? 0.0f : f);  // (-0 and +0: one key)
+      u[i] = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    }
+    uint32_t ans = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+      const uint32_t t = ans | (1u << bit);
+      int below = 0;
+#pragma unroll
+      for (int i = 0; i < kPfSelRegs; ++i) below += __popcll(__ballot(u[i] < t));
+      if (below < k) ans = t;
+    }
+    const uint32_t b = (ans & 0x80000000u) ? (ans & 0x7FFFFFFFu) : ~ans;
+    tk = __uint_as_float(b);
+  } else
+  for (int64_t c = sb * a.slot_k; c < c1; c += 64) {
+    const int64_t cc = c + lane;
+    const float ck = cc < c1 ? a.slot_key[cc] : INFINITY;
+    uint64_t mask = __ballot(ck < tk);
+    while (mask) {
+      const int b = __ffsll((unsigned long long)mask) - 1;
+      const float nk = __shfl(ck, b);
+      const int pos = __popcll(__ballot(lane < k && mk <= nk));
+      const float pk = __shfl_up(mk, 1);
+      if (lane == pos) mk = nk;
+      else if (lane > pos) mk = pk;
+      tk = __shfl(mk, k - 1);
+      mask &= ~(1ull << b);
+      mask &= __ballot(ck < tk);
+    }
+  }
+  if (a.kth_out) {  // (kernel-uniform: every wave of the block leaves here)
+    if (live && lane == 0) a.kth_out[q] = tk;
+    return;
+  }
+  float bmin = cnt_ovf ? -INFINITY : INFINITY;
+  if (a.slot_bound)
+    for (int64_t sl = sb + lane; sl < se; sl += 64) bmin = fminf(bmin, a.slot_bound[sl]);
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) bmin = fminf(bmin, __shfl_xor(bmin, off));
+
+  // the window: delta >= |approx key - pinned key| for every candidate of this query
+  const int64_t qrow = live && a.qrows ? a.qrows[q] : q;  // the query's row in queries / qnorms / qres
+  const float qn = live ? a.qnorms[qrow] : 0.0f;
+  const float delta = pf_delta<METRIC>(qn, live ? a.qres[qrow] : 0.0f, a.x_norm_max, a.x_res_max, a.dp);
+  const float T = pf_window(tk, delta);  // +inf when fewer than k candidates
+  bool ovf = bmin < INFINITY && (bmin <= T || bmin == -INFINITY);
+  // K13: its candidates are every row whose approximate key is <= T_q (a superset); the window is complete
+  // only if it lies below T_q, which the analysis of T_q guarantees -- checked here, not assumed
+  if (live && a.window_cap && !(T <= a.window_cap[q])) ovf = true;
+
+  // phase 2: collect the window (ballot prefix, no atomics)
+  int cnt = 0;
+  for (int64_t c = sb * a.slot_k; c < c1; c += 64) {
+    const int64_t cc = c + lane;
+    const float ck = cc < c1 ? a.slot_key[cc] : INFINITY;
+    const bool take = ck <= T && ck < INFINITY;  // +inf: an empty slot entry (fewer than k candidates: T = +inf)
+    const uint64_t msk = __ballot(take);
+    if (take) {
+      const int at = cnt + __popcll(msk & ((1ull << lane) - 1));
+      if (at < kPfCap) { s_ck[wv][at] = ck; s_cp[wv][at] = a.slot_pos[cc]; }
+    }
+    cnt += __popcll(msk);
+  }
+  ovf = ovf || cnt > kPfCap;
+  if (live && ovf && lane == 0) {
+    const int at = atomicAdd(a.ovf_count, 1);
+    a.ovf_q[at] = q;
+  }
+  // window-size stats: one atomic per workgroup (10k same-address atomics per launch were a serial tail)
+  __shared__ int s_win[4];
+  if (lane == 0) s_win[wv] = live && !ovf ? cnt : 0;
+  // the query row in LDS (zero past d), for the exact recompute
+  for (int i = lane; i < a.dp; i += 64) s_qv[wv][i] = (live && i < a.d) ? a.queries[qrow * a.d + i] : 0.0f;
+  __syncthreads();
+  if (threadIdx.x == 0 && a.n_window) {
+    const int w = s_win[0] + s_win[1] + s_win[2] + s_win[3];
+    if (w) atomicAdd(reinterpret_cast<unsigned long long*>(a.n_window), (unsigned long long)w);
+  }
+
+  // phase 3: exact keys in the pinned order (oracle orc_dot), then a bitonic sort by (key, id)
+  float P = INFINITY;
+  int64_t id = LLONG_MAX;
+  if (live && !ovf && lane < cnt) {
+    const int pos = s_cp[wv][lane];
+    const int nb = a.dp >> 3;
+    // the row's block b: 8 floats at rowp + b * bstride (row-major copy: contiguous; group layout: 1 KiB apart)
+    const float* rowp = a.rows_rm ? a.rows_rm + (int64_t)pos * a.dp
+                                  : a.groups + ((int64_t)(pos >> 5) * nb * kGroupRows + (pos & 31)) * 8;
+    const int64_t bstride = a.rows_rm ? 8 : 256;
+    const float* qv = s_qv[wv];
+    float acc = 0.0f;
+#pragma unroll 12
+    for (int b = 0; b < nb; ++b) {
+      const float4 x0 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride);
+      const float4 x1 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride + 4);
+      const float4 y0 = *reinterpret_cast<const float4*>(qv + 8 * b);
+      const float4 y1 = *reinterpret_cast<const float4*>(qv + 8 * b + 4);
+      acc = fmaf(x0.x, y0.x, acc); acc = fmaf(x1.x, y1.x, acc);
+      acc = fmaf(x0.y, y0.y, acc); acc = fmaf(x1.y, y1.y, acc);
+      acc = fmaf(x0.z, y0.z, acc); acc = fmaf(x1.z, y1.z, acc);
+      acc = fmaf(x0.w, y0.w, acc); acc = fmaf(x1.w, y1.w, acc);
+    }
+    if (METRIC == kL2) {
+      const float v = fmaf(-2.0f, acc, a.row_norms[pos] + qn);
+      P = v > 0.0f ? v : 0.0f;
+    } else {
+      P = -acc;
+    }
+    id = a.row_ids[pos];
+  }
+#pragma unroll
+  for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const float oP = __shfl_xor(P, stride);
+      const int64_t oid = __shfl_xor(id, stride);
+      const bool want_min = ((lane & stride) == 0) == ((lane & size) == 0);  // ascending blocks keep min low
+      const bool o_lt = oP < P || (oP == P && oid < id);
+      const bool o_gt = oP > P || (oP == P && oid > id);
+      if (want_min ? o_lt : o_gt) { P = oP; id = oid; }
+    }
+  }
+  if (live && !ovf && lane < k) {
+    const bool valid = id != LLONG_MAX;
+    a.out_d[q * k + lane] = valid ? (METRIC == kIP ? -P : P) : (METRIC == kIP ? -INFINITY : INFINITY);
+    a.out_i[q * k + lane] = valid ? id : (int64_t)-1;
+  }
+}
+
+// K11v: K13's pre-pass verification (verify_sel > 0, kth_out): phase 1 of K11 at rank verify_sel, then fp32 keys of
+// the nominees and the k-th smallest of them (a kernel of its own: inside K11 its code changed how the compiler
+// unrolled K11's exact recompute, 0.18 -> 0.33 ms per final refine)
+template <int METRIC>
+__global__ __launch_bounds__(256) void k_pf_verify(PfRefineArgs a) {
+  __shared__ int s_cp[4][kPfCap];
+  __shared__ __attribute__((aligned(16))) float s_qv[4][1024];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int64_t q = (int64_t)blockIdx.x * 4 + wv;
+  const bool live = q < a.nq;
+  const int k = a.k;
+  int64_t sb = 0, se = 0;
+  if (live) { sb = a.slot_begin[q]; se = a.slot_begin[q + 1]; }
+  const int64_t c1 = se * a.slot_k;
+
+  // K11's phase 1 at rank ksel: tk = the ksel-th smallest nomination score
+  float mk = INFINITY, tk = INFINITY;
+  const int ksel = a.verify_sel;
   const int64_t n_c = c1 - sb * a.slot_k;
   if (n_c <= kPfSelRegs * 64) {
     uint32_t u[kPfSelRegs];
@@ -698,11 +825,7 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
       mask &= __ballot(ck < tk);
     }
   }
-  if (a.kth_out) {  // (kernel-uniform: every wave of the block leaves here)
-    if (a.verify_sel <= 0) {
-      if (live && lane == 0) a.kth_out[q] = tk;
-      return;
-    }
+  {
     // verify: the nominees (key <= the verify_sel-th smallest; ties beyond 64 dropped: any probed rows bound the
     // final k-th key) get fp32 keys, the wave summing each row's dot in parallel (not the pinned order: the key is
     // within the pinned one's summation-error term of delta, so kth + 2 delta still bounds the final window's
@@ -763,76 +886,6 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
     const float kx = __shfl(P, k - 1);
     if (live && lane == 0) a.kth_out[q] = kx;
     return;
-  }
-  float bmin = cnt_ovf ? -INFINITY : INFINITY;
-  if (a.slot_bound)
-    for (int64_t sl = sb + lane; sl < se; sl += 64) bmin = fminf(bmin, a.slot_bound[sl]);
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) bmin = fminf(bmin, __shfl_xor(bmin, off));
-
-  // the window: delta >= |approx key - pinned key| for every candidate of this query
-  const int64_t qrow = live && a.qrows ? a.qrows[q] : q;  // the query's row in queries / qnorms / qres
-  const float qn = live ? a.qnorms[qrow] : 0.0f;
-  const float delta = pf_delta<METRIC>(qn, live ? a.qres[qrow] : 0.0f, a.x_norm_max, a.x_res_max, a.dp);
-  const float T = pf_window(tk, delta);  // +inf when fewer than k candidates
-  bool ovf = bmin < INFINITY && (bmin <= T || bmin == -INFINITY);
-  // K13: its candidates are every row whose approximate key is <= T_q (a superset); the window is complete
-  // only if it lies below T_q, which the analysis of T_q guarantees -- checked here, not assumed
-  if (live && a.window_cap && !(T <= a.window_cap[q])) ovf = true;
-
-  // phase 2: collect the window (ballot prefix, no atomics)
-  int cnt = 0;
-  for (int64_t c = sb * a.slot_k; c < c1; c += 64) {
-    const int64_t cc = c + lane;
-    const float ck = cc < c1 ? a.slot_key[cc] : INFINITY;
-    const bool take = ck <= T && ck < INFINITY;  // +inf: an empty slot entry (fewer than k candidates: T = +inf)
-    const uint64_t msk = __ballot(take);
-    if (take) {
-      const int at = cnt + __popcll(msk & ((1ull << lane) - 1));
-      if (at < kPfCap) { s_ck[wv][at] = ck; s_cp[wv][at] = a.slot_pos[cc]; }
-    }
-    cnt += __popcll(msk);
-  }
-  ovf = ovf || cnt > kPfCap;
-  if (live && ovf && lane == 0) {
-    const int at = atomicAdd(a.ovf_count, 1);
-    a.ovf_q[at] = q;
-  }
-  // window-size stats: one atomic per workgroup (10k same-address atomics per launch were a serial tail)
-  __shared__ int s_win[4];
-  if (lane == 0) s_win[wv] = live && !ovf ? cnt : 0;
-  // the query row in LDS (zero past d), for the exact recompute
-  for (int i = lane; i < a.dp; i += 64) s_qv[wv][i] = (live && i < a.d) ? a.queries[qrow * a.d + i] : 0.0f;
-  __syncthreads();
-  if (threadIdx.x == 0 && a.n_window) {
-    const int w = s_win[0] + s_win[1] + s_win[2] + s_win[3];
-    if (w) atomicAdd(reinterpret_cast<unsigned long long*>(a.n_window), (unsigned long long)w);
-  }
-
-  // phase 3: exact keys in the pinned order (oracle orc_dot), then a bitonic sort by (key, id)
-  float P = INFINITY;
-  int64_t id = LLONG_MAX;
-  if (live && !ovf && lane < cnt) {
-    const int pos = s_cp[wv][lane];
-    P = pf_pinned_key<METRIC>(a, pos, s_qv[wv], qn);
-    id = a.row_ids[pos];
-  }
-#pragma unroll
-  for (int size = 2; size <= 64; size <<= 1) {
-#pragma unroll
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      const float oP = __shfl_xor(P, stride);
-      const int64_t oid = __shfl_xor(id, stride);
-      const bool want_min = ((lane & stride) == 0) == ((lane & size) == 0);  // ascending blocks keep min low
-      const bool o_lt = oP < P || (oP == P && oid < id);
-      const bool o_gt = oP > P || (oP == P && oid > id);
-      if (want_min ? o_lt : o_gt) { P = oP; id = oid; }
-    }
-  }
-  if (live && !ovf && lane < k) {
-    const bool valid = id != LLONG_MAX;
-    a.out_d[q * k + lane] = valid ? (METRIC == kIP ? -P : P) : (METRIC == kIP ? -INFINITY : INFINITY);
-    a.out_i[q * k + lane] = valid ? id : (int64_t)-1;
   }
 }
 
@@ -1561,6 +1614,11 @@ hipError_t launch_pf_refine(const PfRefineArgs& a, hipStream_t s) {
   if (a.k == 1 && a.slot_k % 4 == 0 && a.force_ovf == nullptr && a.kth_out == nullptr && a.slot_bound != nullptr) {  // lane per query
     if (a.metric == kIP) hipLaunchKernelGGL(k_pf_refine1<kIP>, pf_grid(a.nq, 256), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_pf_refine1<kL2>, pf_grid(a.nq, 256), dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
+  if (a.kth_out && a.verify_sel > 0) {
+    if (a.metric == kIP) hipLaunchKernelGGL(k_pf_verify<kIP>, pf_grid(a.nq, 4), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_pf_verify<kL2>, pf_grid(a.nq, 4), dim3(256), 0, s, a);
     return hipGetLastError();
   }
   if (a.metric == kIP) hipLaunchKernelGGL(k_pf_refine<kIP>, pf_grid(a.nq, 4), dim3(256), 0, s, a);
