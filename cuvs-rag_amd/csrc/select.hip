@@ -81,6 +81,32 @@ __device__ __forceinline__ int64_t cand_id(const SelectArgs& a, int64_t base, in
   return a.row_ids[a.slot_info[2 * s] + rr];
 }
 
+// every candidate of a query, strided over the block: f(cand, id_of) with id_of() its id. DUMP slots are walked
+// slot by slot over their valid rows, so no key pays cand_key's division of its flat index by slot_rows (a 64-bit
+// division per key and pass: K8 over a k = 100 IVF-PQ dump of ~75k keys per query was bound by them)
+template <bool EXPLICIT, int METRIC, class F>
+__device__ __forceinline__ void visit_cands(const SelectArgs& a, int64_t base, int64_t ncand, int64_t nslots, F&& f) {
+  if constexpr (EXPLICIT) {
+    for (int64_t t = threadIdx.x; t < ncand; t += kSelThreads) {
+      const Cand c = cand_key<true, METRIC>(a, base, t);
+      f(c, [&]() { return a.ids[base + t]; });
+    }
+  } else {
+    for (int64_t sq = 0; sq < nslots; ++sq) {
+      const int64_t sl = base + sq;
+      const int nr = (int)a.slot_info[2 * sl + 1];
+      const int64_t r0 = a.slot_info[2 * sl];
+      const float* kp = a.keys + sl * a.slot_rows;
+      for (int rr = threadIdx.x; rr < nr; rr += kSelThreads) {
+        Cand c;
+        c.u = ord_bits(kp[rr]);
+        c.valid = c.u < kOrdInf;  // pad rows carry +inf
+        f(c, [&]() { return a.row_ids[r0 + rr]; });
+      }
+    }
+  }
+}
+
 // Linear bins of width bw = ceil(w / 2048) over a range [lo, lo + w): bin = (v - lo) / bw.
 // Key ranges are < 2^32 wide, so the hot key passes use 32-bit division.
 __device__ __forceinline__ uint64_t bin_width(uint64_t w) { return (w + kBins - 1) / kBins; }
@@ -144,7 +170,7 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
 
   const int64_t q = blockIdx.x;
   const int tid = threadIdx.x;
-  int64_t base, ncand;
+  int64_t base, ncand, nslots = 0;
   if (EXPLICIT) {
     base = q * a.n_in;
     ncand = a.n_in;
@@ -152,20 +178,20 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
     const int64_t sb = a.slot_begin ? a.slot_begin[q] : q * a.slots_per_q;
     const int64_t se = a.slot_begin ? a.slot_begin[q + 1] : sb + a.slots_per_q;
     base = sb;
-    ncand = (se - sb) * a.slot_rows;
+    nslots = se - sb;
+    ncand = nslots * a.slot_rows;
   }
   const int k = a.k;
 
   // ---- pass 0: valid count + key range ----
   uint64_t cnt = 0, mn = 0xFFFFFFFFull, mx = 0;
-  for (int64_t t = tid; t < ncand; t += kSelThreads) {
-    const Cand c = cand_key<EXPLICIT, METRIC>(a, base, t);
+  visit_cands<EXPLICIT, METRIC>(a, base, ncand, nslots, [&](const Cand& c, auto) {
     if (c.valid) {
       ++cnt;
       mn = c.u < mn ? c.u : mn;
       mx = c.u > mx ? c.u : mx;
     }
-  }
+  });
   const int64_t n_valid = (int64_t)block_reduce<uint64_t>(cnt, s_red, 0);
   uint64_t klo = block_reduce<uint64_t>(mn, s_red, 1);
   uint64_t khi = block_reduce<uint64_t>(mx, s_red, 2);
@@ -182,14 +208,13 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
     // range exhausted on the key: refine by id among the tied candidates
     if (!id_phase && klo == khi) {
       uint64_t imn = ~0ull, imx = 0;
-      for (int64_t t = tid; t < ncand; t += kSelThreads) {
-        const Cand c = cand_key<EXPLICIT, METRIC>(a, base, t);
+      visit_cands<EXPLICIT, METRIC>(a, base, ncand, nslots, [&](const Cand& c, auto id_of) {
         if (c.valid && c.u == klo) {
-          const uint64_t id = (uint64_t)cand_id<EXPLICIT>(a, base, t);
+          const uint64_t id = (uint64_t)id_of();
           imn = id < imn ? id : imn;
           imx = id > imx ? id : imx;
         }
-      }
+      });
       ilo = block_reduce<uint64_t>(imn, s_red, 1);
       ihi = block_reduce<uint64_t>(imx, s_red, 2);
       id_phase = true;
@@ -200,16 +225,15 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
     const uint64_t bw = bin_width(w);
     for (int i = tid; i < kBins; i += kSelThreads) hist[i] = 0;
     __syncthreads();
-    for (int64_t t = tid; t < ncand; t += kSelThreads) {
-      const Cand c = cand_key<EXPLICIT, METRIC>(a, base, t);
-      if (!c.valid) continue;
+    visit_cands<EXPLICIT, METRIC>(a, base, ncand, nslots, [&](const Cand& c, auto id_of) {
+      if (!c.valid) return;
       if (!id_phase) {
         if (c.u >= klo && c.u <= khi) atomicAdd(&hist[bin_of_key(c.u, (uint32_t)klo, (uint32_t)bw)], 1);
       } else if (c.u == klo) {
-        const uint64_t id = (uint64_t)cand_id<EXPLICIT>(a, base, t);
+        const uint64_t id = (uint64_t)id_of();
         if (id >= ilo && id <= ihi) atomicAdd(&hist[bin_of_id(id, ilo, bw)], 1);
       }
-    }
+    });
     __syncthreads();
     find_bin(hist, need - (int)below, s_res);
     const int b = s_res[0];
@@ -228,21 +252,20 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
   // ---- collect: everything at or below the bound ----
   if (tid == 0) s_res[2] = 0;
   __syncthreads();
-  for (int64_t t = tid; t < ncand; t += kSelThreads) {
-    const Cand c = cand_key<EXPLICIT, METRIC>(a, base, t);
-    if (!c.valid) continue;
+  visit_cands<EXPLICIT, METRIC>(a, base, ncand, nslots, [&](const Cand& c, auto id_of) {
+    if (!c.valid) return;
     bool take;
     if (select_all) take = true;
     else if (!id_phase) take = c.u <= khi;
-    else take = c.u < klo || (c.u == klo && (uint64_t)cand_id<EXPLICIT>(a, base, t) <= ihi);
+    else take = c.u < klo || (c.u == klo && (uint64_t)id_of() <= ihi);
     if (take) {
       const int pos = atomicAdd(&s_res[2], 1);
       if (pos < CAP) {
         sk[pos] = c.u;
-        si[pos] = cand_id<EXPLICIT>(a, base, t);
+        si[pos] = id_of();
       }
     }
-  }
+  });
   __syncthreads();
   const int n_sel = s_res[2] < CAP ? s_res[2] : CAP;
   int p2 = 1;
