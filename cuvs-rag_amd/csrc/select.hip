@@ -61,8 +61,10 @@ __device__ __forceinline__ Cand cand_key(const SelectArgs& a, int64_t base, int6
     r.u = ord_bits(key);
     r.valid = id >= 0 && r.u < kOrdInf;
   } else {
-    const int64_t s = base + t / a.slot_rows;
-    const int rr = (int)(t - (t / a.slot_rows) * a.slot_rows);
+    // (t < a query's slots x slot_rows < 2^31: a 32-bit division, not the 64-bit one)
+    const uint32_t sq = (uint32_t)t / (uint32_t)a.slot_rows;
+    const int64_t s = base + sq;
+    const int rr = (int)((uint32_t)t - sq * (uint32_t)a.slot_rows);
     r.valid = false;
     r.u = 0xFFFFFFFFu;
     if (rr < (int)a.slot_info[2 * s + 1]) {
@@ -76,8 +78,9 @@ __device__ __forceinline__ Cand cand_key(const SelectArgs& a, int64_t base, int6
 template <bool EXPLICIT>
 __device__ __forceinline__ int64_t cand_id(const SelectArgs& a, int64_t base, int64_t t) {
   if (EXPLICIT) return a.ids[base + t];
-  const int64_t s = base + t / a.slot_rows;
-  const int rr = (int)(t - (t / a.slot_rows) * a.slot_rows);
+  const uint32_t sq = (uint32_t)t / (uint32_t)a.slot_rows;
+  const int64_t s = base + sq;
+  const int rr = (int)((uint32_t)t - sq * (uint32_t)a.slot_rows);
   return a.row_ids[a.slot_info[2 * s] + rr];
 }
 
