@@ -139,6 +139,9 @@ struct mivs_index_s {
   int pre_norms_dims = 0;
   Buf groups_f8;   // K13's pre-pass: the lists' fp8 copy at 2^hx8 (built on first use when HBM has room)
   int hx8 = 0;
+  // IVF: the coarse probe as a brute-force pre-filter search over the centroids (built on first use from
+  // centroids_rm; every writer of centroids_rm drops it)
+  std::unique_ptr<mivs_index_s> coarse_bf;
   int hx_exp = 0;
   float x_norm_max = 0.0f, x_res_max = 0.0f;
   int pf_G = kPfChunkGroups;                  // groups per K10 work item
@@ -796,7 +799,7 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   const int64_t max_slots = std::max<int64_t>(1, nq * tcp[std::min<int64_t>(np, L.n_lists)]);
   // per-slot candidates: room above k so that a neighbourhood packed into one chunk does not overflow
   const char* ske = getenv("MIVS_PF_SLOT_K");  // K10 slot size override (16 or 32)
-  const int slot_k = ske ? (atoi(ske) > 16 ? kPfSlotKMax : 16) : kPfSlotKMax;
+  const int slot_k = (ske && atoi(ske) <= 16 && k <= 16) ? 16 : kPfSlotKMax;  // (k > 16: the coarse probe)
   ws.pf_key.reserve(sizeof(float) * (size_t)max_slots * slot_k);
   ws.pf_pos.reserve(sizeof(int) * (size_t)max_slots * slot_k);
   ws.pf_bound.reserve(sizeof(float) * (size_t)max_slots);
@@ -976,6 +979,32 @@ int coarse_groups(const mivs_index_s* idx, int64_t nq) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(idx->G, ceil_div(ng, chunks)));
 }
 
+// The coarse probe through the fp16 pre-filter (MIVS_COARSE_PF=0: the exact K3 DUMP + K8s): n_probes <= 32 over an
+// ivf_flat index whose lists have the fp16 copy. The centroids form a brute-force index (K10 with k = n_probes,
+// K11 the exact window refine, its own fallback the exact scan): the same keys in the same (key, id) order as K3.
+bool coarse_pf_default(const char* e) { return e ? e[0] != '0' : kCoarsePfDefault; }
+mivs_index_s* coarse_index(mivs_index_s* idx, int np, hipStream_t s) {
+  const char* e = getenv("MIVS_COARSE_PF");
+  if (!coarse_pf_default(e) || idx->kind != 0 || np > kCoarsePfMaxK || idx->groups_h.p == nullptr ||
+      idx->centroids_rm.p == nullptr || idx->cents.n_rows < 2)
+    return nullptr;
+  if (!idx->coarse_bf) {
+    auto cb = std::make_unique<mivs_index_s>();
+    const int nl = idx->cents.n_lists == 1 ? (int)idx->cents.n_rows : idx->cents.n_lists;
+    cb->kind = 1;
+    cb->device = idx->device;
+    cb->d = idx->d;
+    cb->dp = idx->dp;
+    cb->metric = idx->metric;
+    cb->id_offset = 0;
+    make_single_list(cb->lists, idx->centroids_rm.as<float>(), nl, idx->d, cb->dp, 0, cb->G, s);
+    pf_enable(cb.get(), s);
+    if (cb->groups_h.p == nullptr) return nullptr;
+    idx->coarse_bf = std::move(cb);
+  }
+  return idx->coarse_bf.get();
+}
+
 void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                       int64_t* out_i, int32_t* out_probes, bool allow_pf, bool prof, bool allow_rs) {
   Workspace& ws = idx->ws;
@@ -986,8 +1015,20 @@ void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t 
   // coarse: top-n_probes centroids per query
   ws.probes_d.reserve(sizeof(float) * nq * np);
   ws.probes_i.reserve(sizeof(int64_t) * nq * np);
-  single_list_topk(idx->cents, coarse_groups(idx, nq), q, ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, np, idx->metric,
-                   ws.probes_d.as<float>(), ws.probes_i.as<int64_t>(), idx->device, ws, s, coarse_dump(np));
+  mivs_index_s* cb = pf ? coarse_index(idx, np, s) : nullptr;
+  if (cb) {  // every query probes the centroid list: K10 + K11 with k = n_probes
+    Workspace& cw = cb->ws;
+    cw.qn.reserve(sizeof(float) * nq);
+    HIPCHK(hipMemcpyAsync(cw.qn.p, ws.qn.p, sizeof(float) * nq, hipMemcpyDeviceToDevice, s));
+    cw.probes_i.reserve(sizeof(int64_t) * nq);
+    HIPCHK(hipMemsetAsync(cw.probes_i.p, 0, sizeof(int64_t) * nq, s));
+    ivf_search_probed(cb, s, q, nq, np, 1, ws.probes_d.as<float>(), ws.probes_i.as<int64_t>(), true, nullptr, false,
+                      nullptr, false);
+  } else {
+    single_list_topk(idx->cents, coarse_groups(idx, nq), q, ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, np,
+                     idx->metric, ws.probes_d.as<float>(), ws.probes_i.as<int64_t>(), idx->device, ws, s,
+                     coarse_dump(np));
+  }
   if (out_probes) HIPCHK(launch_i64_to_i32(ws.probes_i.as<int64_t>(), nq * np, out_probes, s));
   ivf_search_probed(idx, s, q, nq, k, np, out_d, out_i, pf, pr, prof, nullptr, allow_rs);
 }
@@ -1493,6 +1534,7 @@ int32_t mivs_ivf_flat_build(int32_t device, void* stream, const float* d_data, i
     init_rows.reserve(sizeof(int64_t) * nl);
     HIPCHK(hipMemcpyAsync(init_rows.p, h_init.data(), sizeof(int64_t) * nl, hipMemcpyHostToDevice, s));
     idx->centroids_rm.reserve(sizeof(float) * (size_t)nl * dim);
+    idx->coarse_bf.reset();
     HIPCHK(launch_gather_rows(d_data, dim, init_rows.as<int64_t>(), nl, idx->centroids_rm.as<float>(), s));
     norms.reserve(sizeof(float) * n);
     HIPCHK(launch_row_norms(d_data, n, dim, norms.as<float>(), s));
@@ -1547,6 +1589,7 @@ int32_t mivs_ivf_flat_build_from_centroids(int32_t device, void* stream, const f
     idx->G = chunk_groups_from_rows(chunk_rows);
     idx->id_offset = id_offset;
     idx->centroids_rm.reserve(sizeof(float) * (size_t)n_lists * dim);
+    idx->coarse_bf.reset();
     HIPCHK(hipMemcpyAsync(idx->centroids_rm.p, d_centroids, sizeof(float) * (size_t)n_lists * dim,
                           hipMemcpyDeviceToDevice, s));
     make_single_list(idx->cents, idx->centroids_rm.as<float>(), n_lists, dim, idx->dp, 0, idx->G, s);
@@ -1586,6 +1629,7 @@ int32_t mivs_ivf_flat_build_from_lists(int32_t device, void* stream, const float
     idx->metric = metric;
     idx->G = chunk_groups_from_rows(chunk_rows);
     idx->centroids_rm.reserve(sizeof(float) * (size_t)n_lists * dim);
+    idx->coarse_bf.reset();
     HIPCHK(hipMemcpyAsync(idx->centroids_rm.p, d_centroids, sizeof(float) * (size_t)n_lists * dim,
                           hipMemcpyDeviceToDevice, s));
     make_single_list(idx->cents, idx->centroids_rm.as<float>(), n_lists, dim, idx->dp, 0, idx->G, s);
@@ -1768,6 +1812,7 @@ int32_t mivs_ivf_pq_build(int32_t device, void* stream, const float* d_data, int
     init_rows.reserve(sizeof(int64_t) * std::max(nl, nc));
     HIPCHK(hipMemcpyAsync(init_rows.p, h_init.data(), sizeof(int64_t) * nl, hipMemcpyHostToDevice, s));
     idx->centroids_rm.reserve(sizeof(float) * (size_t)nl * dim);
+    idx->coarse_bf.reset();
     HIPCHK(launch_gather_rows(d_data, dim, init_rows.as<int64_t>(), nl, idx->centroids_rm.as<float>(), s));
     norms.reserve(sizeof(float) * n);
     HIPCHK(launch_row_norms(d_data, n, dim, norms.as<float>(), s));

@@ -180,6 +180,8 @@ constexpr int kPfQTile = 64;     // queries per K10 work item
 constexpr int kPfLaneK = 8;      // per-lane approximate list length in K10
 constexpr int kPfSlotKMax = 32;  // approximate candidates kept per slot: 16 for k <= 10, else 32
 constexpr int kPfMaxK = 16;      // largest k served by the pre-filter path
+constexpr bool kCoarsePfDefault = false;  // the coarse probe through the pre-filter unless MIVS_COARSE_PF says otherwise
+constexpr int kCoarsePfMaxK = 32;  // largest n_probes of the coarse probe through the pre-filter (K10's theta: 4 lane lists)
 constexpr int kPfCap = 64;       // refine capacity (window candidates per query)
 constexpr int kPfSelRegs = 8;    // K11 phase 1: candidates per query held in registers (x 64) for the radix select
 constexpr int kPfChunkGroups = 512;  // default groups (16384 rows) per K10 work item (MIVS_PF_CHUNK_ROWS)

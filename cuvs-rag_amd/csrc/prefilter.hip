@@ -128,22 +128,26 @@ __device__ __forceinline__ bool pf_epilogue(const f32x16& c0, const f32x16& c1, 
   return true;
 }
 
-// theta of a query from its 16 lane lists' last entries (s_l8[16]): with two full lists whose last
-// entries are v1 <= v2, at least 16 >= k kept keys are <= v2, so the query's k-th approximate key over
-// the whole search is <= v2 and the refine window is <= pf_window(v2).
-__device__ __forceinline__ float pf_theta(const float* __restrict__ l8, float delta) {
-  float m1 = INFINITY, m2 = INFINITY;
+// theta of a query from its 16 lane lists' last entries (s_l8[16]): with m full lists whose last entries are
+// v1 <= .. <= vm, at least 8 m >= k kept keys are <= vm, so the query's k-th approximate key over the whole
+// search is <= vm and the refine window is <= pf_window(vm). m = 2 for k <= 16, ceil(k / 8) <= 4 for k <= 32.
+__device__ __forceinline__ float pf_theta(const float* __restrict__ l8, float delta, int m) {
+  float v0 = INFINITY, v1 = INFINITY, v2 = INFINITY, v3 = INFINITY;  // the 4 smallest, ascending
 #pragma unroll
   for (int i = 0; i < 16; i += 4) {
     const float4 v = *reinterpret_cast<const float4*>(l8 + i);
     const float e[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      m2 = fminf(m2, fmaxf(m1, e[t]));
-      m1 = fminf(m1, e[t]);
+      const float x = e[t];
+      v3 = fminf(v3, fmaxf(v2, x));
+      v2 = fminf(v2, fmaxf(v1, x));
+      v1 = fminf(v1, fmaxf(v0, x));
+      v0 = fminf(v0, x);
     }
   }
-  return m2 < INFINITY ? pf_window(m2, delta) : INFINITY;
+  const float vm = m <= 2 ? v1 : (m == 3 ? v2 : v3);
+  return vm < INFINITY ? pf_window(vm, delta) : INFINITY;
 }
 
 // K10. One workgroup (8 waves) per CU, persistent over (list, chunk, 64-query tile) work items.
@@ -193,6 +197,7 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
   // halves between a wave's consecutive groups (F8: a group is 32 dp bytes)
   const int64_t pstride = F8 ? (int64_t)kPfWaves * 16 * dp : (int64_t)kPfWaves * nb * 256;
   const float xnmax2 = a.x_norm_max * a.x_norm_max;       // >= every row's pinned norm
+  const int mth = a.k > 16 ? (a.k + kPfLaneK - 1) / kPfLaneK : 2;  // lane lists theta needs (pf_theta)
   if (tid == 0) s_misc[1] = 0;                            // queues exhausted so far
   // diagnostic phase clocks (a.prof != nullptr only under MIVS_PF_FLAGS & 32)
   unsigned long long pr_top = 0, pr_item = 0, pr_stage = 0, pr_loop = 0, pr_bar = 0, pr_slow = 0, pr_epi = 0;
@@ -335,8 +340,8 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
       // stored is the end of a real list, so a stale read only gives a looser, still valid theta)
       s_l8[j * 16 + src] = lk0[kPfLaneK - 1];
       s_l8[(32 + j) * 16 + src] = lk1[kPfLaneK - 1];
-      th0 = fminf(th0, pf_theta(s_l8 + j * 16, dl0));
-      th1 = fminf(th1, pf_theta(s_l8 + (32 + j) * 16, dl1));
+      th0 = fminf(th0, pf_theta(s_l8 + j * 16, dl0, mth));
+      th1 = fminf(th1, pf_theta(s_l8 + (32 + j) * 16, dl1, mth));
       uf0 = pf_uf<METRIC>(lk0[kPfLaneK - 1], th0, qn0, xnmax2);
       uf1 = pf_uf<METRIC>(lk1[kPfLaneK - 1], th1, qn1, xnmax2);
     };
@@ -532,7 +537,7 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
       float bnd = myk[kPfLaneK - 1];
       // (theta drops are keys > theta: the bound is the next float up, so a theta equal to the
       // refine's window -- the common case when one slot holds the whole top-k -- is no overflow)
-      if (src == 0) bnd = fminf(bnd, nextafterf(fminf(s_th[qi], pf_theta(s_l8 + qi * 16, s_dl[qi])), INFINITY));
+      if (src == 0) bnd = fminf(bnd, nextafterf(fminf(s_th[qi], pf_theta(s_l8 + qi * 16, s_dl[qi], mth)), INFINITY));
       bnd = pf_row_fmin(bnd);
       // fast path (the common case once theta is tight): fewer than k kept keys in all 16 lists
       // -> compact them unsorted into the slot (the refine needs no order), pad with +inf
@@ -1567,6 +1572,7 @@ static hipError_t launch_pf_scan_m(const PfScanArgs& a, int grid, size_t lds, hi
 // grid: a multiple of 8 (one queue per XCD group); the work counters (8 x 16 ints) are zeroed by the caller
 hipError_t launch_pf_scan(const PfScanArgs& a, int grid, size_t lds, hipStream_t s) {
   if (a.dp % 64 != 0 || a.dp > 1024 || lds > 160 * 1024) return hipErrorInvalidValue;
+  if (a.k < 1 || a.k > 4 * kPfLaneK || a.k > a.slot_k) return hipErrorInvalidValue;  // (pf_theta: 4 lane lists)
   return a.metric == kIP ? launch_pf_scan_m<kIP>(a, grid, lds, s) : launch_pf_scan_m<kL2>(a, grid, lds, s);
 }
 
@@ -1609,7 +1615,7 @@ hipError_t launch_pr_scan(const PfScanArgs& a, int grid, hipStream_t s) {
 }
 
 hipError_t launch_pf_refine(const PfRefineArgs& a, hipStream_t s) {
-  if (a.k < 1 || a.k > kPfMaxK || a.dp > 1024) return hipErrorInvalidValue;
+  if (a.k < 1 || a.k > kCoarsePfMaxK || a.dp > 1024) return hipErrorInvalidValue;  // (k > 16: the coarse probe)
   if (a.nq <= 0) return hipSuccess;
   if (a.k == 1 && a.slot_k % 4 == 0 && a.force_ovf == nullptr && a.kth_out == nullptr && a.slot_bound != nullptr) {  // lane per query
     if (a.metric == kIP) hipLaunchKernelGGL(k_pf_refine1<kIP>, pf_grid(a.nq, 256), dim3(256), 0, s, a);

@@ -63,6 +63,7 @@ SEARCH_SWITCHES = [
     {"MIVS_RS_PRE_DIV": "16"},
     {"MIVS_RS_PRE_F8": "0"},                                          # pre-pass: the fp16 sample (round 2)
     {"MIVS_SELECT_SMALL_V2": "0"},                                    # K8s by the bit search alone
+    {"MIVS_COARSE_PF": "1"},                                          # coarse probe: centroids' pre-filter
     {"MIVS_RS_PRE_F8": "0", "MIVS_RS_PRE_DIMS": "96"},                # pre-pass: nominate on 96 dims + verify
     {"MIVS_RS_PRE_F8": "0", "MIVS_RS_PRE_DIMS": "64", "MIVS_RS_PRE_DIV": "2", "MIVS_RS_PRE_SEL": "10"},
     {"MIVS_RS_PRE_DIV": "1", "MIVS_RS_PRE_SEL": "10"},                # fp8 nomination over the whole list
@@ -223,10 +224,16 @@ def test_ivf_pq_switch_same_bits(mivs_lib, monkeypatch, k, env):
     idx.close()
 
 
-@pytest.mark.parametrize("n_probes", [17, 32, 48])
-def test_coarse_probe_dump_switch_same_bits(ivf, flat_data, monkeypatch, n_probes):
-    """n_probes > 16: the coarse probe through K3 DUMP + K8 (default) and through K3's register top-k
-    (MIVS_COARSE_DUMP=0) give the same probes (order and ids) and the same search result"""
+@pytest.mark.parametrize("n_probes,env", [(17, {"MIVS_COARSE_PF": "1"}),
+                                           (17, {"MIVS_COARSE_DUMP": "0"}),
+                                           (32, {"MIVS_COARSE_PF": "1"}),
+                                           (32, {"MIVS_COARSE_DUMP": "0"}),
+                                           (8, {"MIVS_COARSE_PF": "1"}), (2, {"MIVS_COARSE_PF": "1"}),
+                                           (48, {"MIVS_COARSE_DUMP": "0"})])
+def test_coarse_probe_switches_same_bits(ivf, flat_data, monkeypatch, n_probes, env):
+    """the coarse probe through the centroids' fp16 pre-filter (K10 + K11 with k = n_probes <= 32, default),
+    through K3 DUMP + K8s (MIVS_COARSE_PF=0; > 32 probes always) and through K3's register top-k
+    (MIVS_COARSE_DUMP=0): the same probes (order and ids) and the same search result"""
     from mivs.neighbors import ivf_flat
 
     idx, _ = ivf
@@ -235,7 +242,8 @@ def test_coarse_probe_dump_switch_same_bits(ivf, flat_data, monkeypatch, n_probe
     sp = ivf_flat.SearchParams(n_probes=n_probes)
     p0 = torch.empty((q.shape[0], n_probes), dtype=torch.int32, device="cuda")
     d0, i0 = ivf_flat.search(sp, idx, qd, 10, probes_out=p0)
-    monkeypatch.setenv("MIVS_COARSE_DUMP", "0")
+    for kk, v in env.items():
+        monkeypatch.setenv(kk, v)
     p1 = torch.empty_like(p0)
     d1, i1 = ivf_flat.search(sp, idx, qd, 10, probes_out=p1)
     np.testing.assert_array_equal(p1.cpu().numpy(), p0.cpu().numpy())
