@@ -87,12 +87,25 @@ __device__ __forceinline__ int64_t cand_id(const SelectArgs& a, int64_t base, in
 // every candidate of a query, strided over the block: f(cand, id_of) with id_of() its id. DUMP slots are walked
 // slot by slot over their valid rows, so no key pays cand_key's division of its flat index by slot_rows (a 64-bit
 // division per key and pass: K8 over a k = 100 IVF-PQ dump of ~75k keys per query was bound by them)
+// (four keys per thread and step, loaded before any is used: one at a time a pass waited on memory latency)
 template <bool EXPLICIT, int METRIC, class F>
 __device__ __forceinline__ void visit_cands(const SelectArgs& a, int64_t base, int64_t ncand, int64_t nslots, F&& f) {
+  constexpr int U = 4;
   if constexpr (EXPLICIT) {
-    for (int64_t t = threadIdx.x; t < ncand; t += kSelThreads) {
-      const Cand c = cand_key<true, METRIC>(a, base, t);
-      f(c, [&]() { return a.ids[base + t]; });
+    for (int64_t t0 = threadIdx.x; t0 < ncand; t0 += U * kSelThreads) {
+      Cand c[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t t = t0 + (int64_t)u * kSelThreads;
+        c[u].valid = false;
+        c[u].u = 0xFFFFFFFFu;
+        if (t < ncand) c[u] = cand_key<true, METRIC>(a, base, t);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t t = t0 + (int64_t)u * kSelThreads;
+        if (t < ncand) f(c[u], [&]() { return a.ids[base + t]; });
+      }
     }
   } else {
     for (int64_t sq = 0; sq < nslots; ++sq) {
@@ -100,11 +113,23 @@ __device__ __forceinline__ void visit_cands(const SelectArgs& a, int64_t base, i
       const int nr = (int)a.slot_info[2 * sl + 1];
       const int64_t r0 = a.slot_info[2 * sl];
       const float* kp = a.keys + sl * a.slot_rows;
-      for (int rr = threadIdx.x; rr < nr; rr += kSelThreads) {
-        Cand c;
-        c.u = ord_bits(kp[rr]);
-        c.valid = c.u < kOrdInf;  // pad rows carry +inf
-        f(c, [&]() { return a.row_ids[r0 + rr]; });
+      for (int rr0 = threadIdx.x; rr0 < nr; rr0 += U * kSelThreads) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int rr = rr0 + u * kSelThreads;
+          v[u] = rr < nr ? kp[rr] : INFINITY;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int rr = rr0 + u * kSelThreads;
+          if (rr < nr) {
+            Cand c;
+            c.u = ord_bits(v[u]);
+            c.valid = c.u < kOrdInf;  // pad rows carry +inf
+            f(c, [&]() { return a.row_ids[r0 + rr]; });
+          }
+        }
       }
     }
   }
