@@ -1693,6 +1693,9 @@ int32_t mivs_ivf_flat_extend(mivs_index_t idx, void* stream, const float* d_new,
     const bool had_pf = idx->groups_h.p != nullptr;
     idx->groups_h.release();
     idx->rows_rm.release();
+    idx->groups_f8.release();  // (copies of the old lists; pf_enable would drop them too)
+    idx->pre_norms.release();
+    idx->pre_norms_dims = 0;
     pack_lists(L, rows.as<float>(), d, idx->dp, perm.as<int64_t>(), h_off, 0, ids.as<int64_t>(), idx->G, s);
     if (had_pf) pf_enable(idx, s);
     HIPCHK(hipStreamSynchronize(s));
@@ -2375,6 +2378,9 @@ int32_t mivs_index_set_prefilter(mivs_index_t idx, void* stream, int32_t enable)
     } else {
       idx->groups_h.release();
       idx->rows_rm.release();
+      idx->groups_f8.release();
+      idx->pre_norms.release();
+      idx->pre_norms_dims = 0;
     }
   });
 }
