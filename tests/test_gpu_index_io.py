@@ -86,6 +86,25 @@ def test_extend_equals_one_shot_build_and_oracle(mivs_lib, split):
     np.testing.assert_array_equal(_bits(dist.cpu().numpy()), _bits(od))
 
 
+@pytest.mark.parametrize("dim", [128, 768])
+def test_search_extend_search_rebuilds_prepass_copies(mivs_lib, dim):
+    """a search builds K13's fp8 pre-pass copy of the lists on first use; extend changes the lists, so the next
+    search must score the new lists' copy (the old one is released with the fp16 copy): results equal the
+    oracle's after the extend"""
+    from mivs.neighbors import ivf_flat
+
+    x, q = _data(6000, dim, 7), _data(40, dim, 8)
+    cents = _data(16, dim, 9)
+    part = ivf_flat.build_from_centroids(_gpu(cents), _gpu(x[:2000]))
+    ivf_flat.search(ivf_flat.SearchParams(n_probes=5), part, _gpu(q), 10)  # (builds the copies)
+    ivf_flat.extend(part, _gpu(x[2000:]))
+    full = ivf_flat.build_from_centroids(_gpu(cents), _gpu(x))
+    od, oi, _ = O.ivf_search(x, cents, full.list_sizes.numpy(), full.list_ids().cpu().numpy(), q, 5, 10)
+    dist, ids = ivf_flat.search(ivf_flat.SearchParams(n_probes=5), part, _gpu(q), 10)
+    np.testing.assert_array_equal(ids.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(dist.cpu().numpy()), _bits(od))
+
+
 def test_extend_with_explicit_ids(mivs_lib):
     from mivs.neighbors import ivf_flat
 
