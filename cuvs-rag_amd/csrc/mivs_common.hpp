@@ -76,9 +76,7 @@ struct SelectArgs {
   int k, metric;
   float* out_d;
   int64_t* out_i;
-  int cap_search;  // (set by launch_select) K8: cap the search range at the threads' m-th smallest keys
 };
-constexpr bool kSelectCapDefault = false;
 
 // Merge job: per query q, candidates = slots [slot_begin[q], slot_begin[q+1])
 // (or [q*slots_per_q, (q+1)*slots_per_q) when slot_begin == nullptr), each of

@@ -211,37 +211,18 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
   }
   const int k = a.k;
 
-  // ---- pass 0: valid count + key range, and each thread's m = ceil(k / threads) smallest keys: if every thread
-  // holds m, at least m x threads >= k keys lie at or below the largest of their m-th smallest, so the search
-  // range ends there (the bulk of the keys above it never reaches a histogram atomic; they clustered in a few
-  // hot bins) ----
-  constexpr int kSelM = 4;
-  const int m_own = (k + kSelThreads - 1) / kSelThreads;
+  // ---- pass 0: valid count + key range ----
   uint64_t cnt = 0, mn = 0xFFFFFFFFull, mx = 0;
-  uint32_t sm[kSelM] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};  // ascending
   visit_cands<EXPLICIT, METRIC>(a, base, ncand, nslots, [&](const Cand& c, auto) {
     if (c.valid) {
       ++cnt;
       mn = c.u < mn ? c.u : mn;
       mx = c.u > mx ? c.u : mx;
-      uint32_t x = c.u;
-#pragma unroll
-      for (int i = 0; i < kSelM; ++i) {
-        const uint32_t lo = x < sm[i] ? x : sm[i];
-        x = x < sm[i] ? sm[i] : x;
-        sm[i] = lo;
-      }
     }
   });
   const int64_t n_valid = (int64_t)block_reduce<uint64_t>(cnt, s_red, 0);
   uint64_t klo = block_reduce<uint64_t>(mn, s_red, 1);
   uint64_t khi = block_reduce<uint64_t>(mx, s_red, 2);
-  if (a.cap_search && m_own <= kSelM) {
-    // (a thread with fewer than m valid keys has sm[m - 1] = 0xFFFFFFFF: the cap is then the full range)
-    const uint32_t own = m_own == 1 ? sm[0] : (m_own == 2 ? sm[1] : (m_own == 3 ? sm[2] : sm[3]));
-    const uint64_t cap = block_reduce<uint64_t>((uint64_t)own, s_red, 2);
-    if (cap < khi) khi = cap;
-  }
 
   // selection bound: key u < klo always selected; u in [klo, khi] selected (key phase) or,
   // in the id phase (klo == khi), with id in [ilo, ihi]
@@ -527,12 +508,7 @@ hipError_t launch_cap(const SelectArgs& a, bool expl, hipStream_t s) {
 
 }  // namespace
 
-hipError_t launch_select(const SelectArgs& a_in, hipStream_t s) {
-  SelectArgs a = a_in;
-  {  // (MIVS_SELECT_CAP: K8's search range capped by the threads' m smallest keys)
-    const char* ce = getenv("MIVS_SELECT_CAP");
-    a.cap_search = ce ? (ce[0] != '0') : kSelectCapDefault;
-  }
+hipError_t launch_select(const SelectArgs& a, hipStream_t s) {
   if (a.k < 1 || a.k > kMaxSelectK) return hipErrorInvalidValue;
   if (a.nq <= 0) return hipSuccess;
   if (a.nq > 0x7FFFFFFF) return hipErrorInvalidValue;

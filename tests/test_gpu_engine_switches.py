@@ -118,8 +118,7 @@ def test_ivf_chunk_rows_switch_same_bits(ivf, flat_data, monkeypatch, env):
 
 
 @pytest.mark.parametrize("k,env", [(10, {"MIVS_SCAN_WIDE": "0"}), (10, {"MIVS_SCAN_WIDE_WAVES": "8"}),
-                                   (100, {"MIVS_SCAN_WAVES": "8"}), (100, {"MIVS_SELECT_CAP": "1"}),
-                                   (1500, {"MIVS_SELECT_CAP": "1"}), (1500, {"MIVS_SELECT_CAP": "0"})])
+                                   (100, {"MIVS_SCAN_WAVES": "8"})])
 def test_exact_scan_switch_same_bits(ivf, flat_data, monkeypatch, k, env):
     """the exact fp32 scans: K3 vs K3w, K3w with 8 waves, the DUMP scan (k > 64) with 8 waves"""
     idx, _ = ivf
