@@ -81,6 +81,12 @@ def parse():
     ap.add_argument("--single-process-timeout", type=float, default=240.0,
                     help="seconds the one-process multi-GPU side line may take before it is abandoned")
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--ids-out", default="", help="(set by the launcher) rank 0 saves the merged ids of the timed "
+                                                  "search here (.npy)")
+    ap.add_argument("--launch-timeout", type=float, default=1500.0,
+                    help="seconds the self-launched ranks may take (--gpus N > 1 without WORLD_SIZE)")
+    ap.add_argument("--launcher-dry-run", action="store_true",
+                    help="print the command --gpus N > 1 would start its ranks with, and exit")
     return ap.parse_args()
 
 
@@ -201,6 +207,49 @@ def cpu_baseline(idx, q_host, gt, n_probes, k, target_s, rank_log):
             "recall_at_10": rec}
 
 
+def faiss_blas_knn(x, qb, k, bs_x=65536):
+    """FAISS exhaustive_L2sqr_blas restated on torch-CPU tensors: the database's squared norms (computed inside
+    every search, as FAISS does), then per database block one MKL sgemm of the query block against it,
+    ||q||^2 + ||x||^2 - 2 q.x, and a running top-k per query (FAISS: a max-heap per query)."""
+    xn = (x * x).sum(1)
+    qn = (qb * qb).sum(1)
+    best_d = torch.full((qb.shape[0], k), float("inf"))
+    best_i = torch.full((qb.shape[0], k), -1, dtype=torch.int64)
+    for b0 in range(0, x.shape[0], bs_x):
+        xb = x[b0:b0 + bs_x]
+        dd = torch.addmm(qn[:, None] + xn[None, b0:b0 + bs_x], qb, xb.t(), beta=1.0, alpha=-2.0).clamp_min_(0)
+        kk = min(k, dd.shape[1])
+        bd, bi = torch.topk(dd, kk, dim=1, largest=False)
+        cd = torch.cat([best_d, bd], 1)
+        ci = torch.cat([best_i, bi + b0], 1)
+        o = torch.topk(cd, k, dim=1, largest=False).indices
+        best_d, best_i = cd.gather(1, o), ci.gather(1, o)
+    return best_d, best_i
+
+
+def faiss_blas_knn_timed(xh, qh, k, threads, target_s=6.0):
+    """The BLAS form timed on `threads` threads over a query sample sized for ~target_s seconds (queries in blocks of
+    FAISS's distance_compute_blas_query_bs = 4096)."""
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        x = torch.from_numpy(xh)
+        q = torch.from_numpy(qh)
+        faiss_blas_knn(x[:200_000], q[:64], k)  # warm MKL / pages
+        t0 = time.perf_counter()
+        faiss_blas_knn(x, q[:64], k)
+        per_q = (time.perf_counter() - t0) / 64
+        n = int(max(64, min(q.shape[0], target_s / max(per_q, 1e-9))))
+        t0 = time.perf_counter()
+        ids = []
+        for b0 in range(0, n, 4096):
+            ids.append(faiss_blas_knn(x, q[b0:min(n, b0 + 4096)], k)[1])
+        dt = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(prev)
+    return {"qps": n / dt, "n": n, "s": dt, "ids": torch.cat(ids).numpy(), "bs_q": min(n, 4096), "bs_x": 65536}
+
+
 def flat_side_line(a, q, k, rl):
     """BASELINE configs[1]: exact k-NN over a 1M x 768 fp32 corpus of the same mixture on the GPU (the
     fp16 pre-filter + exact refine path, k <= 16), next to the FAISS IndexFlatL2 algorithm on this host's
@@ -230,21 +279,34 @@ def flat_side_line(a, q, k, rl):
         threads = cpu_threads()
         O.fast_set_threads(threads)
         xh = xf.cpu().numpy()
-        qh = q[:512].cpu().numpy()
+        qh = q[:4096].cpu().numpy()
+        # 1. FAISS's own path at this batch size: IndexFlatL2.search takes the BLAS form for nq >= 20
+        # (distance_compute_blas_threshold; exhaustive_L2sqr_blas: row norms, sgemm of query x database blocks,
+        # ||q||^2 + ||x||^2 - 2 q.x, a per-query top-k) -- restated with torch-CPU (MKL sgemm) on the same threads
+        blas = faiss_blas_knn_timed(xh, qh, k, threads, target_s=6.0)
+        agree = float(np.mean(blas["ids"] == fi[:blas["n"]].cpu().numpy()))
+        # 2. the per-query scalar form (FAISS's path below 20 queries; oracle/cpu_baseline.c orc_fast_knn)
         O.fast_knn(xh, qh[:4], k)
         t0 = time.perf_counter()
         O.fast_knn(xh, qh[:16], k)
         per_q = (time.perf_counter() - t0) / 16
-        ns = int(max(16, min(qh.shape[0], 6.0 / max(per_q, 1e-9))))
+        ns = int(max(16, min(512, 4.0 / max(per_q, 1e-9))))
         t0 = time.perf_counter()
         _, ci = O.fast_knn(xh, qh[:ns], k)
         dt = time.perf_counter() - t0
-        agree = float(np.mean(ci == fi[:ns].cpu().numpy()))
-        line["cpu_baseline"] = {"value": round(ns / dt, 2), "unit": "QPS", "cores": threads, "kind": "port",
-                                "sample": f"{ns} queries, FAISS IndexFlatL2 algorithm (oracle/cpu_baseline.c); {dt:.1f} s",
-                                "ids_equal_to_gpu_frac": round(agree, 4)}
-        line["gpu_over_cpu"] = round(gpu_qps / (ns / dt), 1)
-        rl(f"[flat] CPU {ns / dt:.1f} QPS on {threads} threads")
+        agree_port = float(np.mean(ci == fi[:ns].cpu().numpy()))
+        line["cpu_baseline"] = {
+            "value": round(blas["qps"], 2), "unit": "QPS", "cores": threads, "kind": "port",
+            "sample": f"{blas['n']} queries in one batch (FAISS IndexFlatL2 BLAS path for nq >= 20: sgemm of "
+                      f"{blas['bs_q']}-query x {blas['bs_x']}-row blocks + ||q||^2 + ||x||^2 - 2 q.x + per-query "
+                      f"top-k, torch-CPU MKL on {threads} threads; faiss not installed); {blas['s']:.1f} s",
+            "ids_equal_to_gpu_frac": round(agree, 4),
+            "per_query_form": {"value": round(ns / dt, 2), "unit": "QPS", "cores": threads,
+                               "sample": f"{ns} queries, FAISS fvec_L2sqr per (query, row) (its path for nq < 20; "
+                                         f"oracle/cpu_baseline.c); {dt:.1f} s",
+                               "ids_equal_to_gpu_frac": round(agree_port, 4)}}
+        line["gpu_over_cpu"] = round(gpu_qps / blas["qps"], 1)
+        rl(f"[flat] CPU {blas['qps']:.1f} QPS (BLAS form), {ns / dt:.1f} QPS (per-query form) on {threads} threads")
         del xh
     bf.close()
     del xf
@@ -295,24 +357,28 @@ def large_k_side_line(a, idx, q, rl, scanned_rows):
     return out
 
 
-def single_process_side_line(a, idx, q, res_i, rl):
+def single_process_side_line(a, q, ref_ids, rl, devices, indexes=None):
     """The reference's own multi-GPU shape (improved_multi_gpu_rag.py:105,206,239-277; merge contract
-    Attempt_1/test_search_result_aggregator.py:405-457): ONE process drives every visible GPU -- a
-    rows-per-GPU shard on each (the main index on GPU 0, the others generated on their devices and built
-    by ParallelIndexBuilder threads with global ids), SearchResultAggregator searches them in parallel
-    threads and merges over RCCL (exchange='rccl': mivs_comm_init_all + grouped all-gather + K7)."""
+    Attempt_1/test_search_result_aggregator.py:405-457): ONE process drives `devices` -- a rows-per-GPU
+    shard on each (shard g = rows [g n, (g + 1) n) of the same corpus, generated on its device and built by
+    ParallelIndexBuilder threads with global ids; `indexes` may hold shards already built), and
+    SearchResultAggregator searches them in parallel threads and merges over RCCL (exchange='rccl':
+    mivs_comm_init_all + grouped all-gather + K7). `ref_ids` (host [Q, k]): the same search's merged ids from
+    the one-process-per-GPU run (torch.distributed), which the aggregator's final ids must equal."""
     from gpu_resource_manager import GPUResourceManager
     from improved_multi_gpu_rag import GPUConfig, IndexType, ParallelIndexBuilder
     from search_result_aggregator import SearchConfig, SearchResultAggregator
 
     from mivs import ops
 
-    G = torch.cuda.device_count()
+    devices = list(devices)
+    G = len(devices)
     n = a.rows
-    indexes = {0: idx}
+    indexes = dict(indexes or {})
     extra = {}
     t_build = 0.0
-    if G > 1:
+    todo = [g for g in devices if g not in indexes]
+    if todo:
         b = ParallelIndexBuilder(G)
         params = {"n_lists": a.n_lists, "kmeans_n_iters": a.kmeans_iters,
                   "kmeans_trainset_fraction": a.trainset_fraction}
@@ -327,7 +393,7 @@ def single_process_side_line(a, idx, q, res_i, rl):
                 return g, ix, tb
 
         t0 = time.perf_counter()
-        futs = [b.executor.submit(one, g) for g in range(1, G)]
+        futs = [b.executor.submit(one, g) for g in todo]
         for f in futs:
             g, ix, _ = f.result()
             indexes[g] = extra[g] = ix
@@ -343,16 +409,134 @@ def single_process_side_line(a, idx, q, res_i, rl):
     line = {"devices": G, "rows_per_gpu": n, "rows_total": n * G, "queries": q.shape[0], "k": a.k,
             "n_probes": a.n_probes, "qps_full_corpus": round(q.shape[0] / t, 1),
             "shard_searches_per_s": round(q.shape[0] * G / t, 1), "ms_per_batch": round(t * 1e3, 3),
-            "extra_shards_build_s": round(t_build, 3),
+            "shards_built_here": len(todo), "shards_build_s": round(t_build, 3),
             "path": "SearchResultAggregator (one thread per GPU) -> mivs.comm.LocalComm RCCL all-gather + K7; "
                     "results copied to host as the reference's contract returns them"}
-    if G == 1:
-        line["final_ids_equal_main_search"] = bool(np.array_equal(r.final_indices, res_i.cpu().numpy()))
-    rl(f"[single-process] {G} GPU(s), {n * G} rows: {q.shape[0] / t:,.0f} QPS through the aggregator + RCCL merge")
+    if ref_ids is not None:
+        line["final_ids_equal_main_search"] = bool(np.array_equal(r.final_indices, np.asarray(ref_ids)))
+    rl(f"[single-process] {G} GPU(s), {n * G} rows: {q.shape[0] / t:,.0f} QPS through the aggregator + RCCL merge"
+       + (f"; ids equal to the per-rank run: {line['final_ids_equal_main_search']}" if ref_ids is not None
+          else ""))
     for ix in extra.values():
         ix.close()
     torch.cuda.empty_cache()
     return line
+
+
+def run_with_watchdog(fn, timeout_s):
+    """fn() on a daemon thread: (result, error, hung). A hung thread is abandoned (the caller must then leave
+    with os._exit, since the interpreter's teardown would wait for a thread stuck in a collective)."""
+    box = {}
+
+    def _run():
+        try:
+            box["r"] = fn()
+        except Exception as e:  # reported by the caller
+            box["e"] = e
+
+    th = threading.Thread(target=_run, daemon=True)
+    th.start()
+    th.join(timeout=timeout_s)
+    if th.is_alive():
+        return None, None, True
+    return box.get("r"), box.get("e"), False
+
+
+EXIT_HUNG = 3  # a side line hung (a stuck collective): the JSON line is printed, the exit status says so
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_argv(a, argv, port, ids_out):
+    """The child command for `bench.py --gpus N` (N > 1) started without WORLD_SIZE: N ranks, one per GPU,
+    under torch.distributed.run on this node (the same command the driver may use itself); rank 0 writes the
+    merged ids of the timed search to `ids_out` for the one-process check."""
+    fwd = [v for v in argv if v != "--launcher-dry-run"]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + fwd + \
+        ["--single-process", "0", "--ids-out", ids_out]
+
+
+def self_launch(a, argv):
+    """`python bench.py --gpus N` with N > 1 and no torch.distributed environment: start the N rank processes
+    as ONE child (torch.distributed.run) before anything in this process touches a GPU, forward their stderr,
+    take rank 0's JSON line, then -- the ranks gone and their HBM free -- run the reference's one-process shape
+    (single_process_aggregator: every shard on its own device in this process, aggregator threads + the RCCL
+    merge of mivs.comm.LocalComm) over the same N devices and check its final ids against the ranks' merged
+    ids. Prints one JSON line and exits with the ranks' status (EXIT_HUNG if the one-process line hung)."""
+    import subprocess
+    import tempfile
+
+    tmpd = tempfile.mkdtemp(prefix="mivs_bench_")
+    ids_out = os.path.join(tmpd, "merged_ids.npy")
+    port = free_port()
+    cmd = launcher_argv(a, argv, port, ids_out)
+    if a.launcher_dry_run:
+        print(json.dumps({"launcher": {"argv": cmd, "gpus": a.gpus}}), flush=True)
+        return 0
+    print(f"[launcher] {a.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    t0 = time.perf_counter()
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, start_new_session=True)
+    line = None
+    try:
+        for ln in p.stdout:
+            s = ln.strip()
+            if s.startswith("{") and '"metric"' in s:
+                line = s
+            elif s:
+                print(s, file=sys.stderr, flush=True)
+        rc = p.wait(timeout=a.launch_timeout)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, 9)
+        rc = 124
+    if line is None:
+        print(f"[launcher] the ranks exited with {rc} and no result line", file=sys.stderr, flush=True)
+        return rc or 1
+    out = json.loads(line)
+    out["launcher"] = {"mode": "bench.py started its ranks (torch.distributed.run child)", "ranks_rc": rc,
+                       "ranks_wall_s": round(time.perf_counter() - t0, 2)}
+    hung = False
+    if rc == 0 and a.single_process and os.path.exists(ids_out):
+        ref = np.load(ids_out, allow_pickle=False)
+
+        def _side():
+            import mivs
+            from mivs import ops
+
+            mivs.load()
+            torch.cuda.set_device(0)
+            q = ops.synth_mixture(a.queries, a.dim, SEED, n_centers=a.centers, sigma=a.sigma,
+                                  row_begin=QUERY_ROW_BASE, device=0)
+            return single_process_side_line(a, q, ref, lambda *m: log(0, *m), range(a.gpus))
+
+        single, err, hung = run_with_watchdog(_side, a.single_process_timeout)
+        if hung:
+            single = {"error": f"did not finish within {a.single_process_timeout} s (abandoned)"}
+        elif err is not None:
+            single = {"error": repr(err)}
+        out["single_process_aggregator"] = single
+    print(json.dumps(out), flush=True)
+    if a.json_out:
+        with open(a.json_out, "w") as f:
+            f.write(json.dumps(out) + "\n")
+    try:
+        os.remove(ids_out)
+        os.rmdir(tmpd)
+    except OSError:
+        pass
+    if hung:
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(EXIT_HUNG)
+    return rc
 
 
 PEAK_LDS_B128_LOOKUPS = 256 * 2.4e9 * 64  # ds_read_b128: 256 B/clk/CU = 64 fp32 LUT entries / clk / CU
@@ -467,17 +651,24 @@ def pq_side_line(a, rl, rank=0, world=1, dev=None):
 
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        # one process per GPU is how the scan scales: start the ranks as a child (never exec: nothing here has
+        # touched a GPU yet, and the child is a new process either way)
+        return self_launch(a, sys.argv[1:])
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
-        if world == 1 and a.gpus > 1:
-            raise SystemExit("for --gpus N>1 launch with: python -m torch.distributed.run --nproc-per-node N "
-                             "--master-addr 127.0.0.1 bench.py --gpus N")
+        rl0 = f"[bench] --gpus {a.gpus} but WORLD_SIZE {world}: measuring the {world} launched ranks"
+        print(rl0, file=sys.stderr, flush=True) if rank == 0 else None
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    dist_info = {"backend": dist.get_backend() if world > 1 else None,
+                 "world_size": dist.get_world_size() if world > 1 else 1,
+                 "launched_by": "torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ or world > 1
+                 else "single process"}
     import mivs
     from mivs import _native, ops
     from mivs.distributed import merge_across_ranks
@@ -671,33 +862,29 @@ def main():
         except Exception as e:  # the IVF line stands without it
             rl(f"[large-k] side line failed: {e!r}")
 
+    if a.ids_out and rank == 0:  # (the launcher's one-process check compares against these)
+        np.save(a.ids_out, res_i.cpu().numpy())
+
     single = None
     single_hung = False
     if rank == 0 and world == 1 and a.single_process:
-        # on a multi-GPU node this is the only place the one-process RCCL path (ncclCommInitAll over every local
-        # device) runs at P > 1: a watchdog keeps a hang there from taking the IVF-Flat line with it
-        box = {}
-
-        def _side():
-            try:
-                box["r"] = single_process_side_line(a, idx, q, res_i, rl)
-            except Exception as e:  # the IVF line stands without it
-                box["e"] = e
-
-        th = threading.Thread(target=_side, daemon=True)
-        th.start()
-        th.join(timeout=a.single_process_timeout)
-        if th.is_alive():
-            single_hung = True
+        # on a multi-GPU node this runs the one-process RCCL path (ncclCommInitAll over every local device) at
+        # P > 1: a watchdog keeps a hang there from taking the IVF-Flat line with it (and the exit status says so)
+        G = torch.cuda.device_count()
+        single, err, single_hung = run_with_watchdog(
+            lambda: single_process_side_line(a, q, res_i.cpu().numpy() if G == 1 else None, rl, range(G), {0: idx}),
+            a.single_process_timeout)
+        if single_hung:
             single = {"error": f"did not finish within {a.single_process_timeout} s (abandoned)"}
             rl(f"[single-process] side line did not finish within {a.single_process_timeout} s: abandoned")
-        elif "e" in box:
-            rl(f"[single-process] side line failed: {box['e']!r}")
-        else:
-            single = box.get("r")
+        elif err is not None:
+            single = {"error": repr(err)}
+            rl(f"[single-process] side line failed: {err!r}")
 
     pq = None
-    if a.pq_rows > 0 and not single_hung:  # every rank: configs[4] is this line at N = 8
+    if single_hung:
+        pq = {"skipped": "not run: the one-process RCCL side line hung and holds the devices"}
+    elif a.pq_rows > 0:  # every rank: configs[4] is this line at N = 8
         idx.close()
         del x
         torch.cuda.empty_cache()
@@ -743,6 +930,7 @@ def main():
         "large_k": large_k,
         "single_process_aggregator": single,
         "ivf_pq_12m5": pq,
+        "distributed": dist_info,
     }
     if rank == 0:
         line = json.dumps(out)
@@ -750,10 +938,11 @@ def main():
         if a.json_out:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
-    if single_hung:  # a thread is stuck in a collective: leave without the teardown that would wait for it
+    if single_hung:  # a thread is stuck in a collective: leave without the teardown that would wait for it, and
+        # say so in the exit status (the line above still carries every measured number)
         sys.stdout.flush()
         sys.stderr.flush()
-        os._exit(0)
+        os._exit(EXIT_HUNG)
     if pq is None:
         idx.close()
     if world > 1:
@@ -762,4 +951,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -135,13 +135,8 @@ struct mivs_index_s {
   Buf groups_h;
   Buf rows_rm;     // K11: the fp32 lists row-major (built with groups_h when HBM has room; MIVS_PF_ROWMAJOR=0: off)
   Buf group_nmin;  // K13: the smallest row norm of every 32-row group (built with groups_h)
-  Buf pre_norms;   // K13's pre-pass: every row's norm over its first pre_norms_dims dims (0: not built)
-  int pre_norms_dims = 0;
   Buf groups_f8;   // K13's pre-pass: the lists' fp8 copy at 2^hx8 (built on first use when HBM has room)
   int hx8 = 0;
-  // IVF: the coarse probe as a brute-force pre-filter search over the centroids (built on first use from
-  // centroids_rm; every writer of centroids_rm drops it)
-  std::unique_ptr<mivs_index_s> coarse_bf;
   int hx_exp = 0;
   float x_norm_max = 0.0f, x_res_max = 0.0f;
   int pf_G = kPfChunkGroups;                  // groups per K10 work item
@@ -713,8 +708,6 @@ void pf_enable(mivs_index_s* idx, hipStream_t s) {
   const ListSet& L = idx->lists;
   idx->groups_h.release();
   idx->rows_rm.release();
-  idx->pre_norms.release();
-  idx->pre_norms_dims = 0;
   idx->groups_f8.release();
   if (L.n_groups == 0 || idx->dp % 64 != 0) return;
   const int64_t nslot = L.n_groups * (int64_t)kGroupRows;
@@ -782,11 +775,11 @@ void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_
 // could not prove are re-run through the exact scan and scattered back.
 // (goff / n_lists: another split of the same groups into lists -- K13's pre-pass samples)
 // kth_out: K13's pre-pass -- only the k-th smallest approximate key per query (no refine, no fallback);
-// with nk_scan > 0 the scan scores the first 16 nk_scan dims against scan_norms (nomination), and verify_sel
-// > 0 makes kth_out the k-th smallest pinned key of each query's verify_sel best-scored rows
+// verify_sel > 0 (with the fp8 scan, f8) makes kth_out the k-th smallest fp32 key of each query's verify_sel
+// best-scored rows
 void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                     int64_t* out_i, ProfRec* pr, const int64_t* goff, int n_lists, float* kth_out = nullptr,
-                    int nk_scan = 0, const float* scan_norms = nullptr, int verify_sel = 0, bool f8 = false) {
+                    int verify_sel = 0, bool f8 = false) {
   Workspace& ws = idx->ws;
   const ListSet& L = idx->lists;
   const int dp = idx->dp;
@@ -815,8 +808,7 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
     a.chunk_stride = (int)tcp[1];
   }
   a.groups_h = idx->groups_h.as<uint16_t>();
-  a.row_norms = scan_norms ? scan_norms : L.norms.as<float>();
-  a.nk_scan = nk_scan;
+  a.row_norms = L.norms.as<float>();
   if (f8) {  // K13's fp8 nomination: the fp8 queries beside the fp16 ones (the headers and tiles use those)
     ws.q8.reserve((size_t)nq * dp);
     ws.qscale8.reserve(sizeof(float) * nq);
@@ -979,32 +971,6 @@ int coarse_groups(const mivs_index_s* idx, int64_t nq) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(idx->G, ceil_div(ng, chunks)));
 }
 
-// The coarse probe through the fp16 pre-filter (MIVS_COARSE_PF=0: the exact K3 DUMP + K8s): n_probes <= 32 over an
-// ivf_flat index whose lists have the fp16 copy. The centroids form a brute-force index (K10 with k = n_probes,
-// K11 the exact window refine, its own fallback the exact scan): the same keys in the same (key, id) order as K3.
-bool coarse_pf_default(const char* e) { return e ? e[0] != '0' : kCoarsePfDefault; }
-mivs_index_s* coarse_index(mivs_index_s* idx, int np, hipStream_t s) {
-  const char* e = getenv("MIVS_COARSE_PF");
-  if (!coarse_pf_default(e) || idx->kind != 0 || np > kCoarsePfMaxK || idx->groups_h.p == nullptr ||
-      idx->centroids_rm.p == nullptr || idx->cents.n_rows < 2)
-    return nullptr;
-  if (!idx->coarse_bf) {
-    auto cb = std::make_unique<mivs_index_s>();
-    const int nl = idx->cents.n_lists == 1 ? (int)idx->cents.n_rows : idx->cents.n_lists;
-    cb->kind = 1;
-    cb->device = idx->device;
-    cb->d = idx->d;
-    cb->dp = idx->dp;
-    cb->metric = idx->metric;
-    cb->id_offset = 0;
-    make_single_list(cb->lists, idx->centroids_rm.as<float>(), nl, idx->d, cb->dp, 0, cb->G, s);
-    pf_enable(cb.get(), s);
-    if (cb->groups_h.p == nullptr) return nullptr;
-    idx->coarse_bf = std::move(cb);
-  }
-  return idx->coarse_bf.get();
-}
-
 void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                       int64_t* out_i, int32_t* out_probes, bool allow_pf, bool prof, bool allow_rs) {
   Workspace& ws = idx->ws;
@@ -1015,20 +981,9 @@ void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t 
   // coarse: top-n_probes centroids per query
   ws.probes_d.reserve(sizeof(float) * nq * np);
   ws.probes_i.reserve(sizeof(int64_t) * nq * np);
-  mivs_index_s* cb = pf ? coarse_index(idx, np, s) : nullptr;
-  if (cb) {  // every query probes the centroid list: K10 + K11 with k = n_probes
-    Workspace& cw = cb->ws;
-    cw.qn.reserve(sizeof(float) * nq);
-    HIPCHK(hipMemcpyAsync(cw.qn.p, ws.qn.p, sizeof(float) * nq, hipMemcpyDeviceToDevice, s));
-    cw.probes_i.reserve(sizeof(int64_t) * nq);
-    HIPCHK(hipMemsetAsync(cw.probes_i.p, 0, sizeof(int64_t) * nq, s));
-    ivf_search_probed(cb, s, q, nq, np, 1, ws.probes_d.as<float>(), ws.probes_i.as<int64_t>(), true, nullptr, false,
-                      nullptr, false);
-  } else {
-    single_list_topk(idx->cents, coarse_groups(idx, nq), q, ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, np,
-                     idx->metric, ws.probes_d.as<float>(), ws.probes_i.as<int64_t>(), idx->device, ws, s,
-                     coarse_dump(np));
-  }
+  single_list_topk(idx->cents, coarse_groups(idx, nq), q, ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, np,
+                   idx->metric, ws.probes_d.as<float>(), ws.probes_i.as<int64_t>(), idx->device, ws, s,
+                   coarse_dump(np));
   if (out_probes) HIPCHK(launch_i64_to_i32(ws.probes_i.as<int64_t>(), nq * np, out_probes, s));
   ivf_search_probed(idx, s, q, nq, k, np, out_d, out_i, pf, pr, prof, nullptr, allow_rs);
 }
@@ -1060,16 +1015,6 @@ bool rs_pre_f8(mivs_index_s* idx, hipStream_t s) {
   return true;
 }
 
-// K13's pre-pass nomination dims (MIVS_RS_PRE_DIMS; 0 or >= dp: the full-dims sample of round 2): a multiple
-// of 64 or 96 (K10's 4- or 6-deep rings of 16-dim k-steps) below dp
-int rs_pre_dims(int dp) {
-  const char* e = getenv("MIVS_RS_PRE_DIMS");
-  const int v = e ? atoi(e) : kRsPreDims;
-  if (v <= 0 || v >= dp) return 0;
-  if (v % 96 == 0) return v;
-  return std::max(64, v / 64 * 64);
-}
-
 // records per K13 stream: twice the batch's queries, at most kRsWaveCapMax (MIVS_RS_WAVE_CAP overrides it: the
 // lost-stream path is then testable at small sizes). Batches are at most kRsMaxBatch queries (ivf_search_impl),
 // so a stream's mean length (~160 records per 1,000 queries at the benchmark shape) stays far below the cap.
@@ -1097,22 +1042,12 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   // are in no particular order) through K10 over the split lists, and the k-th smallest approximate key
   // of each query's candidates there (K11's first phase only)
   ws.pre_goff.reserve(sizeof(int64_t) * (2 * (size_t)L.n_lists + 1));
-  // nomination (MIVS_RS_PRE_DIMS > 0): the sample scored on its first pre_dims dims only (against the rows' norms
-  // over those dims), then the MIVS_RS_PRE_SEL best-scored rows of each query verified with pinned keys
   // fp8 nomination (MIVS_RS_PRE_F8, default on where it applies): the sample scored on fp8 copies over every dim,
-  // the MIVS_RS_PRE_SEL best rows verified with pinned keys
+  // the kRsPreSel best rows of each query verified with fp32 keys
   const bool pre_f8 = rs_pre_f8(idx, s);
-  const int pre_dims = pre_f8 ? 0 : rs_pre_dims(dp);
-  const char* pse = getenv("MIVS_RS_PRE_SEL");
-  const int pre_sel = (pre_dims > 0 || pre_f8) ? std::min(kPfMaxK, std::max(k, pse ? atoi(pse) : kRsPreSel)) : 0;
+  const int pre_sel = pre_f8 ? std::min(kPfMaxK, std::max(k, kRsPreSel)) : 0;
   const char* pde = getenv("MIVS_RS_PRE_DIV");
-  const int pre_div = std::max(1, pde ? atoi(pde) : (pre_f8 ? kRsPreDivF8 : (pre_dims > 0 ? kRsPreDivNominate : kRsPreDiv)));
-  if (pre_dims > 0 && idx->pre_norms_dims != pre_dims) {
-    idx->pre_norms.reserve(sizeof(float) * (size_t)L.n_groups * kGroupRows);
-    HIPCHK(launch_partial_norms(L.groups.as<float>(), L.norms.as<float>(), L.n_groups, dp, pre_dims,
-                                idx->pre_norms.as<float>(), s));
-    idx->pre_norms_dims = pre_dims;
-  }
+  const int pre_div = std::max(1, pde ? atoi(pde) : (pre_f8 ? kRsPreDivF8 : kRsPreDiv));
   HIPCHK(launch_rs_pre_lists(L.goff.as<int64_t>(), L.n_lists, pre_div, ceil_div(k, kGroupRows), ws.probes_full.as<int64_t>(),
                              nq, np, ws.pre_goff.as<int64_t>(), ws.probes_i.as<int64_t>(), s));
   {
@@ -1133,8 +1068,7 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
                             ws.slot_begin.as<int64_t>(), ws.scan_tmp.p, stb, s));
     ws.pre_kth.reserve(sizeof(float) * nq);
     pf_scan_refine(idx, s, q, nq, k, 1, nullptr, nullptr, nullptr, ws.pre_goff.as<int64_t>(), nl2,
-                   ws.pre_kth.as<float>(), pre_dims / 16, pre_dims > 0 ? idx->pre_norms.as<float>() : nullptr,
-                   pre_sel, pre_f8);
+                   ws.pre_kth.as<float>(), pre_sel, pre_f8);
   }
   // 2. headers (pf_scan_refine left the fp16 queries, their scales and residuals in ws.qh / qscale / qres)
   ws.qhdr.reserve(sizeof(float4) * (nq + 1));
@@ -1158,8 +1092,8 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
     std::vector<float> sorted = ht;
     std::sort(sorted.begin(), sorted.end());
     auto pc = [&](double f) { return sorted[std::min<int64_t>(nq - 1, (int64_t)(f * nq))]; };
-    fprintf(stderr, "[rs pre] f8 %d dims %d div %d sel %d | mean kth %.6f mean T_q %.6f | inf %lld of %lld | T_q p10 %.4f "
-            "p50 %.4f p90 %.4f p99 %.4f max %.4f\n", (int)pre_f8, pre_dims, pre_div, pre_sel, sk / nf, st / nf, (long long)ninf,
+    fprintf(stderr, "[rs pre] f8 %d div %d sel %d | mean kth %.6f mean T_q %.6f | inf %lld of %lld | T_q p10 %.4f "
+            "p50 %.4f p90 %.4f p99 %.4f max %.4f\n", (int)pre_f8, pre_div, pre_sel, sk / nf, st / nf, (long long)ninf,
             (long long)nq, pc(0.1), pc(0.5), pc(0.9), pc(0.99), sorted[nq - 1]);
   }
   // 3. probe map: items = (list, block of kRsBlockGroups groups); every query of a list in one tile column
@@ -1476,11 +1410,11 @@ void ivf_search_impl(mivs_index_s* idx, hipStream_t s, const float* q, int64_t n
   } else if (idx->groups_h.p != nullptr && k <= kPfMaxK && rs_use(idx, np)) {
     qb = std::min<int64_t>(nq, kRsMaxBatch);  // K13: bounded record streams and LDS-histogram bucketing
   }
-  idx->last_ovf = 0;
-  idx->last_window = 0;
   int64_t nb = 0;
   for (int64_t b0 = 0; b0 < nq; b0 += qb) {
     nb = std::min<int64_t>(qb, nq - b0);
+    idx->last_ovf = 0;  // (every stat describes the last batch, as n_queries does)
+    idx->last_window = 0;
     ivf_search_batch(idx, s, q + b0 * (int64_t)idx->d, nb, k, np, out_d + b0 * k, out_i + b0 * k,
                      out_probes ? out_probes + b0 * np : nullptr);
   }
@@ -1534,7 +1468,6 @@ int32_t mivs_ivf_flat_build(int32_t device, void* stream, const float* d_data, i
     init_rows.reserve(sizeof(int64_t) * nl);
     HIPCHK(hipMemcpyAsync(init_rows.p, h_init.data(), sizeof(int64_t) * nl, hipMemcpyHostToDevice, s));
     idx->centroids_rm.reserve(sizeof(float) * (size_t)nl * dim);
-    idx->coarse_bf.reset();
     HIPCHK(launch_gather_rows(d_data, dim, init_rows.as<int64_t>(), nl, idx->centroids_rm.as<float>(), s));
     norms.reserve(sizeof(float) * n);
     HIPCHK(launch_row_norms(d_data, n, dim, norms.as<float>(), s));
@@ -1589,7 +1522,6 @@ int32_t mivs_ivf_flat_build_from_centroids(int32_t device, void* stream, const f
     idx->G = chunk_groups_from_rows(chunk_rows);
     idx->id_offset = id_offset;
     idx->centroids_rm.reserve(sizeof(float) * (size_t)n_lists * dim);
-    idx->coarse_bf.reset();
     HIPCHK(hipMemcpyAsync(idx->centroids_rm.p, d_centroids, sizeof(float) * (size_t)n_lists * dim,
                           hipMemcpyDeviceToDevice, s));
     make_single_list(idx->cents, idx->centroids_rm.as<float>(), n_lists, dim, idx->dp, 0, idx->G, s);
@@ -1629,7 +1561,6 @@ int32_t mivs_ivf_flat_build_from_lists(int32_t device, void* stream, const float
     idx->metric = metric;
     idx->G = chunk_groups_from_rows(chunk_rows);
     idx->centroids_rm.reserve(sizeof(float) * (size_t)n_lists * dim);
-    idx->coarse_bf.reset();
     HIPCHK(hipMemcpyAsync(idx->centroids_rm.p, d_centroids, sizeof(float) * (size_t)n_lists * dim,
                           hipMemcpyDeviceToDevice, s));
     make_single_list(idx->cents, idx->centroids_rm.as<float>(), n_lists, dim, idx->dp, 0, idx->G, s);
@@ -1694,8 +1625,6 @@ int32_t mivs_ivf_flat_extend(mivs_index_t idx, void* stream, const float* d_new,
     idx->groups_h.release();
     idx->rows_rm.release();
     idx->groups_f8.release();  // (copies of the old lists; pf_enable would drop them too)
-    idx->pre_norms.release();
-    idx->pre_norms_dims = 0;
     pack_lists(L, rows.as<float>(), d, idx->dp, perm.as<int64_t>(), h_off, 0, ids.as<int64_t>(), idx->G, s);
     if (had_pf) pf_enable(idx, s);
     HIPCHK(hipStreamSynchronize(s));
@@ -1815,7 +1744,6 @@ int32_t mivs_ivf_pq_build(int32_t device, void* stream, const float* d_data, int
     init_rows.reserve(sizeof(int64_t) * std::max(nl, nc));
     HIPCHK(hipMemcpyAsync(init_rows.p, h_init.data(), sizeof(int64_t) * nl, hipMemcpyHostToDevice, s));
     idx->centroids_rm.reserve(sizeof(float) * (size_t)nl * dim);
-    idx->coarse_bf.reset();
     HIPCHK(launch_gather_rows(d_data, dim, init_rows.as<int64_t>(), nl, idx->centroids_rm.as<float>(), s));
     norms.reserve(sizeof(float) * n);
     HIPCHK(launch_row_norms(d_data, n, dim, norms.as<float>(), s));
@@ -2379,8 +2307,6 @@ int32_t mivs_index_set_prefilter(mivs_index_t idx, void* stream, int32_t enable)
       idx->groups_h.release();
       idx->rows_rm.release();
       idx->groups_f8.release();
-      idx->pre_norms.release();
-      idx->pre_norms_dims = 0;
     }
   });
 }

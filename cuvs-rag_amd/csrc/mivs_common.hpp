@@ -180,8 +180,7 @@ constexpr int kPfQTile = 64;     // queries per K10 work item
 constexpr int kPfLaneK = 8;      // per-lane approximate list length in K10
 constexpr int kPfSlotKMax = 32;  // approximate candidates kept per slot: 16 for k <= 10, else 32
 constexpr int kPfMaxK = 16;      // largest k served by the pre-filter path
-constexpr bool kCoarsePfDefault = false;  // the coarse probe through the pre-filter unless MIVS_COARSE_PF says otherwise
-constexpr int kCoarsePfMaxK = 32;  // largest n_probes of the coarse probe through the pre-filter (K10's theta: 4 lane lists)
+constexpr int kPfRefineMaxK = 32;  // largest k K11 ranks (the pre-filter search itself serves k <= kPfMaxK)
 constexpr int kPfCap = 64;       // refine capacity (window candidates per query)
 constexpr int kPfSelRegs = 8;    // K11 phase 1: candidates per query held in registers (x 64) for the radix select
 constexpr int kPfChunkGroups = 512;  // default groups (16384 rows) per K10 work item (MIVS_PF_CHUNK_ROWS)
@@ -219,8 +218,6 @@ struct PfScanArgs {
   int chunk_stride;           // max chunks per list
   int rows_nt;                // 1: the rows are read once (K13's pre-pass: one tile per list sample) -- load them
                               // with the non-temporal policy (pair mode only)
-  int nk_scan;                // 0: every dim; else only dims [0, 16 nk_scan) (a multiple of 4 or 6 k-steps) with
-                              // row_norms = the rows' norms over those dims: K13's pre-pass nomination score
   const uint8_t* groups_f8;   // optional (K13's pre-pass nomination, pair mode): fp8 rows (launch_groups_to_f8);
   const uint8_t* q8;          //   then the fp8 queries (launch_queries_to_f8) and their scales replace groups_h,
   const float* qscale8;       //   qh and qscale
@@ -232,15 +229,11 @@ struct PfScanArgs {
 constexpr int kRsWaves = 8;
 constexpr int kRsQTile = 32;
 constexpr int kRsBlockGroups = kRsWaves;
-// K13's pre-pass scans the first 1 / kRsPreDiv of each query's nearest list (MIVS_RS_PRE_DIV) -- or, nominating
-// (MIVS_RS_PRE_DIMS > 0; off by default), the first 1 / kRsPreDivNominate of it on its first
-// MIVS_RS_PRE_DIMS dims, and the kRsPreSel best-scored rows of each query get their pinned keys (MIVS_RS_PRE_SEL)
+// K13's pre-pass scans the first 1 / kRsPreDiv of each query's nearest list (MIVS_RS_PRE_DIV); with the fp8 copies
+// (MIVS_RS_PRE_F8, default) the sample is scored on fp8 rows and queries over every dim and the kRsPreSel best rows
+// of each query are verified with fp32 keys
 constexpr int kRsPreDiv = 4;
-constexpr int kRsPreDims = 0;
-// the fp8 nomination (MIVS_RS_PRE_F8): the first 1 / kRsPreDivF8 of the nearest list scored on fp8 copies of the
-// rows and queries over every dim, the kRsPreSel best rows of each query verified with pinned keys
 constexpr int kRsPreDivF8 = 4;
-constexpr int kRsPreDivNominate = 1;
 constexpr int kRsPreSel = 10;
 constexpr int kRsWaveCapMax = 16384;  // records of a K13 wave's candidate stream (more: all queries fall back)
 constexpr int kRsRecInt4 = 3;         // a record: 8 dots of one lane and query half + {first row position, query}
@@ -398,9 +391,6 @@ hipError_t launch_rs_bucket(const int4* wave_buf, int wave_cap, const int* wave_
 hipError_t launch_groups_to_f8(const float* groups, int64_t n_groups, int dp, int hx8, uint8_t* out, hipStream_t s);
 hipError_t launch_queries_to_f8(const float* q, int64_t nq, int d, int dp, int hx8, uint8_t* out, float* qscale8,
                                 hipStream_t s);
-// every row slot's squared norm over its first dims dims (+inf on pad rows): K13's pre-pass nomination
-hipError_t launch_partial_norms(const float* groups, const float* norms, int64_t n_groups, int dp, int dims,
-                                float* out, hipStream_t s);
 // per group of 32 rows the smallest row norm (K13's filter bound)
 hipError_t launch_group_nmin(const float* norms, int64_t n_groups, float* out, hipStream_t s);
 hipError_t launch_rs_pre_lists(const int64_t* goff, int n_lists, int div, int min_groups, const int64_t* probes,

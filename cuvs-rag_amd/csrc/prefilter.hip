@@ -183,8 +183,8 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
 
   const int dp = a.dp;
   const int nb = dp >> 3;  // 8-dim blocks
-  // 16-dim k-steps (a multiple of D); nk_scan: only the first 16 nk_scan dims (K13's pre-pass nomination)
-  const int nk = F8 ? dp >> 5 : (a.nk_scan > 0 ? a.nk_scan : dp >> 4);
+  // 16-dim k-steps (a multiple of D)
+  const int nk = F8 ? dp >> 5 : dp >> 4;
   static_assert(!F8 || R == 2, "fp8 rows: pair mode only");
   const int bq1off = F8 ? dp * 32 : nb * 512;  // B image: query group 1's bytes after group 0's
   const int tid = threadIdx.x;
@@ -1551,14 +1551,12 @@ static hipError_t launch_pf_scan_m(const PfScanArgs& a, int grid, size_t lds, hi
   // power-bound); MIVS_PF_PAIR=0: one group per pass with MIVS_PF_DEPTH (16) k-steps in flight
   if (a.groups_f8) {  // fp8 nomination (pair mode): superblocks of 32 dims, a ring of 6 or 4
     const int nsb = a.dp / 32;
-    if (a.q8 == nullptr || a.qscale8 == nullptr || a.nk_scan > 0) return hipErrorInvalidValue;
+    if (a.q8 == nullptr || a.qscale8 == nullptr) return hipErrorInvalidValue;
     if (nsb % 6 == 0) return launch_pf_scan_md<METRIC, 6, 2, true, true>(a, grid, lds, s);
     if (nsb % 4 == 0) return launch_pf_scan_md<METRIC, 4, 2, true, true>(a, grid, lds, s);
     return hipErrorInvalidValue;
   }
-  const int nk = a.nk_scan > 0 ? a.nk_scan : a.dp / 16;
-  if (a.nk_scan > 0 && (a.nk_scan > a.dp / 16 || (a.nk_scan % 4 != 0 && a.nk_scan % 6 != 0)))
-    return hipErrorInvalidValue;
+  const int nk = a.dp / 16;
   if (pf_pair_mode()) {
     if (a.rows_nt && nk % 6 == 0) return launch_pf_scan_md<METRIC, 6, 2, true>(a, grid, lds, s);
     return nk % 6 == 0 ? launch_pf_scan_md<METRIC, 6, 2>(a, grid, lds, s) : launch_pf_scan_md<METRIC, 4, 2>(a, grid, lds, s);
@@ -1615,7 +1613,7 @@ hipError_t launch_pr_scan(const PfScanArgs& a, int grid, hipStream_t s) {
 }
 
 hipError_t launch_pf_refine(const PfRefineArgs& a, hipStream_t s) {
-  if (a.k < 1 || a.k > kCoarsePfMaxK || a.dp > 1024) return hipErrorInvalidValue;  // (k > 16: the coarse probe)
+  if (a.k < 1 || a.k > kPfRefineMaxK || a.dp > 1024) return hipErrorInvalidValue;  // (k > 16: the coarse probe)
   if (a.nq <= 0) return hipSuccess;
   if (a.k == 1 && a.slot_k % 4 == 0 && a.force_ovf == nullptr && a.kth_out == nullptr && a.slot_bound != nullptr) {  // lane per query
     if (a.metric == kIP) hipLaunchKernelGGL(k_pf_refine1<kIP>, pf_grid(a.nq, 256), dim3(256), 0, s, a);

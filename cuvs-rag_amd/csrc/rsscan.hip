@@ -225,10 +225,13 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   int4* const wstream = a.wave_buf + (int64_t)widx * a.wave_cap * kRsRecInt4;
   int wcnt = 0;  // records of this wave's candidate stream
   auto block_prof = [&]() {
-    // (a wave that gave up waiting reports a lost stream, so every query takes the fallback search, and counts
-    // itself in wave_cnt[waves + 9] so that the stats tell it from a stream overflow)
+    // The stream length is the count of records actually written (at most wave_cap), so the bucketing never reads
+    // a slot this search did not fill. A stream that overflowed, or a wave that gave up waiting (its records may
+    // come from a stale LDS tile: it reports none), raises the lost flag wave_cnt[waves]: every query of the batch
+    // then takes the fallback search. A spun-out wave also counts itself in wave_cnt[waves + 9] for the stats.
     if (lane == 0) {
-      a.wave_cnt[widx] = spun_out ? a.wave_cap + 1 : wcnt;
+      a.wave_cnt[widx] = spun_out ? 0 : min(wcnt, a.wave_cap);
+      if (spun_out || wcnt > a.wave_cap) atomicOr(a.wave_cnt + gridDim.x * kRsWaves, 1);
       if (spun_out) atomicAdd(a.wave_cnt + gridDim.x * kRsWaves + 9, 1);
     }
     if ((a.flags & 8) && a.prof && tid == 0) {  // (timing only) flags & 8: per block {start, end, tiles}
@@ -722,10 +725,10 @@ __global__ __launch_bounds__(1024) void k_rs_stream_off(const int* __restrict__ 
   for (int w0 = 0; w0 < n_waves; w0 += 1024) {
     const int w = w0 + threadIdx.x;
     int64_t c = 0;
-    if (w < n_waves) {
+    if (w < n_waves) {  // (K13 reports at most wave_cap records per stream and raises `lost` itself)
       const int n = wave_cnt[w];
       if (n > wave_cap) atomicOr(lost, 1);
-      c = n < wave_cap ? n : wave_cap;
+      c = n < 0 ? 0 : (n < wave_cap ? n : wave_cap);
     }
     int64_t tot;
     const int64_t ex = block_excl_scan(c, sh, &tot);
@@ -955,35 +958,6 @@ __global__ void k_group_nmin(const float* __restrict__ norms, int64_t n_groups, 
 hipError_t launch_group_nmin(const float* norms, int64_t n_groups, float* out, hipStream_t s) {
   if (n_groups <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_group_nmin, dim3((unsigned)ceil_div(n_groups * 32, 256)), dim3(256), 0, s, norms, n_groups, out);
-  return hipGetLastError();
-}
-
-// the squared norm of every row slot over its first `dims` dims (K13's pre-pass nomination score: the partial
-// distance needs the partial norm); pad rows (+inf full norm) stay +inf
-__global__ void k_partial_norms(const float* __restrict__ groups, const float* __restrict__ norms, int64_t n_groups,
-                                int dp, int dims, float* __restrict__ out) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_groups * kGroupRows) return;
-  const int64_t g = t >> 5;
-  const int j = (int)(t & 31);
-  const int nb = dp >> 3;
-  const float* p = groups + (g * nb * kGroupRows + j) * 8;
-  float acc = 0.0f;
-  for (int b = 0; b < (dims >> 3); ++b) {
-    const float4 x0 = *reinterpret_cast<const float4*>(p + (int64_t)b * 256);
-    const float4 x1 = *reinterpret_cast<const float4*>(p + (int64_t)b * 256 + 4);
-    acc = fmaf(x0.x, x0.x, acc); acc = fmaf(x0.y, x0.y, acc); acc = fmaf(x0.z, x0.z, acc); acc = fmaf(x0.w, x0.w, acc);
-    acc = fmaf(x1.x, x1.x, acc); acc = fmaf(x1.y, x1.y, acc); acc = fmaf(x1.z, x1.z, acc); acc = fmaf(x1.w, x1.w, acc);
-  }
-  out[t] = norms[t] < INFINITY ? acc : INFINITY;
-}
-
-hipError_t launch_partial_norms(const float* groups, const float* norms, int64_t n_groups, int dp, int dims,
-                                float* out, hipStream_t s) {
-  if (n_groups <= 0) return hipSuccess;
-  if (dims % 8 != 0 || dims > dp) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_partial_norms, dim3((unsigned)ceil_div(n_groups * kGroupRows, 256)), dim3(256), 0, s, groups,
-                     norms, n_groups, dp, dims, out);
   return hipGetLastError();
 }
 

@@ -63,10 +63,7 @@ SEARCH_SWITCHES = [
     {"MIVS_RS_PRE_DIV": "16"},
     {"MIVS_RS_PRE_F8": "0"},                                          # pre-pass: the fp16 sample (round 2)
     {"MIVS_SELECT_SMALL_V2": "0"},                                    # K8s by the bit search alone
-    {"MIVS_COARSE_PF": "1"},                                          # coarse probe: centroids' pre-filter
-    {"MIVS_RS_PRE_F8": "0", "MIVS_RS_PRE_DIMS": "96"},                # pre-pass: nominate on 96 dims + verify
-    {"MIVS_RS_PRE_F8": "0", "MIVS_RS_PRE_DIMS": "64", "MIVS_RS_PRE_DIV": "2", "MIVS_RS_PRE_SEL": "10"},
-    {"MIVS_RS_PRE_DIV": "1", "MIVS_RS_PRE_SEL": "10"},                # fp8 nomination over the whole list
+    {"MIVS_RS_PRE_DIV": "1"},                                         # fp8 nomination over the whole list
     {"MIVS_RS_PRE_STATS": "1"},                                       # pre-pass T_q stats (stderr only)
     {"MIVS_RS_FLAGS": "24"},                                          # K13 clocks (stderr only)
     {"MIVS_RS_WAVE_CAP": "2"},                                        # K13 streams overflow: the fallback
@@ -224,16 +221,14 @@ def test_ivf_pq_switch_same_bits(mivs_lib, monkeypatch, k, env):
     idx.close()
 
 
-@pytest.mark.parametrize("n_probes,env", [(17, {"MIVS_COARSE_PF": "1"}),
-                                           (17, {"MIVS_COARSE_DUMP": "0"}),
-                                           (32, {"MIVS_COARSE_PF": "1"}),
+@pytest.mark.parametrize("n_probes,env", [(17, {"MIVS_COARSE_DUMP": "0"}),
                                            (32, {"MIVS_COARSE_DUMP": "0"}),
-                                           (8, {"MIVS_COARSE_PF": "1"}), (2, {"MIVS_COARSE_PF": "1"}),
+                                           (32, {"MIVS_SELECT_SMALL_V2": "0"}),
                                            (48, {"MIVS_COARSE_DUMP": "0"})])
 def test_coarse_probe_switches_same_bits(ivf, flat_data, monkeypatch, n_probes, env):
-    """the coarse probe through the centroids' fp16 pre-filter (K10 + K11 with k = n_probes <= 32, default),
-    through K3 DUMP + K8s (MIVS_COARSE_PF=0; > 32 probes always) and through K3's register top-k
-    (MIVS_COARSE_DUMP=0): the same probes (order and ids) and the same search result"""
+    """the coarse probe through K3 DUMP + K8s (the default above 16 probes) and through K3's register top-k
+    (MIVS_COARSE_DUMP=0), K8s with the bit search alone: the same probes (order and ids) and the same search
+    result"""
     from mivs.neighbors import ivf_flat
 
     idx, _ = ivf
@@ -275,7 +270,9 @@ def test_k13_query_batches_same_bits(ivf, flat_data):
     rng = np.random.default_rng(9)
     q = x[rng.integers(0, x.shape[0], 33_000)] + 0.01 * rng.standard_normal((33_000, x.shape[1])).astype(np.float32)
     d, i = _search(idx, q)
-    assert idx.last_search_stats()["n_queries"] == 33_000 - 32_768  # the last batch
+    st = idx.last_search_stats()
+    assert st["n_queries"] == 33_000 - 32_768  # the last batch: every count describes it
+    assert st["overflow_queries"] <= st["n_queries"]
     for lo, hi in ((0, 5000), (32_000, 33_000)):
         ds, is_ = _search(idx, q[lo:hi])
         np.testing.assert_array_equal(i[lo:hi], is_)
