@@ -316,9 +316,11 @@ def flat_side_line(a, q, k, rl):
 
 def large_k_side_line(a, idx, q, rl, scanned_rows):
     """The reference's large-k default at configs[2]: its driver asks for top_k = 2000 and each shard for
-    k * 2 (improved_multi_gpu_rag.py:40,247,416). Every k > 16 takes the exact fp32 scan in DUMP mode (K3,
-    raw keys per (query, probe, chunk) slot) + the K8 radix select, query-batched by the select workspace.
-    QPS over the full 10k-query batch, the scan kernel's time and its fp32 MFMA roofline."""
+    k * 2 (improved_multi_gpu_rag.py:40,247,416). Every k > 16 runs through the fp16 pre-filter:
+    T_q from an exact scan of a 1/64 sample of the probed rows, K13 streams the rows under it, K16 proves each
+    query's window and recomputes it in the pinned fp32 order (the exact fp32 scan, K3 DUMP + K8, answers the
+    queries it cannot prove). QPS over the full 10k-query batch; the same search through the exact path
+    (MIVS_LARGE_K_PF=0) beside it, checked equal; K13's time and K16's gather of the window rows."""
     from mivs import _native
     from mivs.neighbors import ivf_flat
 
@@ -337,22 +339,36 @@ def large_k_side_line(a, idx, q, rl, scanned_rows):
         t = (time.perf_counter() - t0) / reps
         pr = idx.profile_collect()
         _native.set_profiling(False)
-        # the scan runs once per query batch (the select workspace bounds a batch): its time per search call
-        # is the sum over the batches; the algorithmic flops are the k = 10 search's (same probes, all queries)
+        st = idx.last_search_stats()
         batches = max(1, pr["n_calls"] // reps)
         scan_ms = pr["scan_ms"] / reps
-        flops = 2.0 * a.dim * scanned_rows
-        tf = flops / (scan_ms * 1e-3) / 1e12
+        # the exact fp32 path for comparison (and the check that both give the same bits)
+        os.environ["MIVS_LARGE_K_PF"] = "0"
+        try:
+            ivf_flat.search(sp, idx, q, kk)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ed, ei = ivf_flat.search(sp, idx, q, kk)
+            torch.cuda.synchronize()
+            t_ex = time.perf_counter() - t0
+        finally:
+            del os.environ["MIVS_LARGE_K_PF"]
+        same = bool(torch.equal(ei, i)) and bool(torch.equal(ed.view(torch.int32), d.view(torch.int32)))
+        # K16's floor: the window rows' fp32 values gathered once per (query, window row)
+        win_bytes = float(st["window_candidates"]) * a.dim * 4
         ok = bool((i[:, 0] >= 0).all()) and bool((d[:, 1:] >= d[:, :-1]).all())
         out.append({"k": kk, "queries": q.shape[0], "qps": round(q.shape[0] / t, 1), "ms_per_batch": round(t * 1e3, 3),
-                    "scan_kernel": "mivs::k_scan<DUMP> (K3 exact fp32, raw keys) + mivs::k_select (K8)",
-                    "query_batches": batches, "scan_ms_per_search": round(scan_ms, 4),
-                    "select_and_rest_ms_per_search": round(t * 1e3 - scan_ms, 3), "well_formed": ok,
-                    "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_F32_MFMA_TFS,
-                                 "unit": "TFLOP/s", "frac": round(tf / PEAK_F32_MFMA_TFS, 4)}})
-        rl(f"[large-k] k={kk}: {q.shape[0] / t:,.0f} QPS ({t * 1e3:.1f} ms per {q.shape[0]} queries), scan "
-           f"{scan_ms:.2f} ms = {tf:.1f} TF/s fp32")
-        del d, i
+                    "path": "K3 DUMP sample -> T_q, K13 fp16 row-stationary scan, K16 window + pinned fp32 keys + "
+                            "(key, id) sort; unproven queries -> exact K3 DUMP + K8",
+                    "query_batches": batches, "k13_ms_per_search": round(scan_ms, 4),
+                    "rest_ms_per_search": round(t * 1e3 - scan_ms, 3),
+                    "candidates": st["candidates"], "window_rows": st["window_candidates"],
+                    "window_gather_gb": round(win_bytes / 1e9, 2), "unproven_queries": st["overflow_queries"],
+                    "exact_path_qps": round(q.shape[0] / t_ex, 1), "equal_to_exact_path": same, "well_formed": ok})
+        rl(f"[large-k] k={kk}: {q.shape[0] / t:,.0f} QPS ({t * 1e3:.1f} ms per {q.shape[0]} queries; K13 {scan_ms:.2f} ms, "
+           f"{st['candidates']} candidates, {st['window_candidates']} window rows, {st['overflow_queries']} unproven); "
+           f"exact path {q.shape[0] / t_ex:,.0f} QPS, same bits: {same}")
+        del d, i, ed, ei
         torch.cuda.empty_cache()
     return out
 

@@ -93,6 +93,8 @@ struct Workspace {
       rs_wave_cnt, rs_bounds;
   // per-list query counts of the last search's own probe map (an exact fallback re-maps its queries)
   Buf stat_counts, rs_ovf_q, rs_ovf_rows, rs_ovf_d, rs_ovf_i, rs_items;
+  // K16 large-k: T_q's sample probes and selection, the per-query windows and K16r's work items
+  Buf lk_probes, lk_sel, lk_sel_i, lk_win_pos, lk_win_key, lk_win_n, lk_chunks, lk_chunk_off;
 };
 
 // hipEvent pairs recorded on the caller's stream around the pipeline stages of
@@ -173,6 +175,8 @@ struct ScanJob {
   int64_t* out_i;
   int qtile;  // 32: K3, 64: K3w (must match the work decomposition of the probe map / single job)
   bool dump = false;  // DUMP mode (raw keys per slot for K8) whatever k: set by every caller that runs K8
+  const int64_t* goff = nullptr;  // another split of ls's groups into lists (K16's sample), else ls->goff
+  int n_lists = 0;
 };
 
 // Query tile of the fine scan for k: K3w (64 queries, slab-staged) where it applies, else K3.
@@ -197,8 +201,8 @@ void run_scan(const ScanJob& j, int device, Workspace& ws, hipStream_t s) {
   a.groups = j.ls->groups.as<float>();
   a.row_norms = j.ls->norms.as<float>();
   a.row_ids = j.ls->ids.as<int64_t>();
-  a.list_goff = j.ls->goff.as<int64_t>();
-  a.n_lists = j.ls->n_lists;
+  a.list_goff = j.goff ? j.goff : j.ls->goff.as<int64_t>();
+  a.n_lists = j.goff ? j.n_lists : j.ls->n_lists;
   a.chunk_groups = j.G;
   a.queries = j.queries;
   a.qnorms = j.qnorms;
@@ -762,6 +766,8 @@ void pf_enable(mivs_index_s* idx, hipStream_t s) {
 void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                       int64_t* out_i, int32_t* out_probes, bool allow_pf = true, bool prof = true,
                       bool allow_rs = true);
+bool lk_use(const mivs_index_s* idx, int k, int np);
+int64_t lk_batch(const mivs_index_s* idx, int64_t nq, int k, int np);
 void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                        int64_t* out_i, bool pf, ProfRec* pr, bool prof, const int64_t* probes = nullptr,
                        bool allow_rs = true);
@@ -975,7 +981,7 @@ void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t 
                       int64_t* out_i, int32_t* out_probes, bool allow_pf, bool prof, bool allow_rs) {
   Workspace& ws = idx->ws;
   ProfRec* pr = prof && g_profiling.load() ? idx->prof.begin(s) : nullptr;
-  const bool pf = allow_pf && idx->groups_h.p != nullptr && k <= kPfMaxK;
+  const bool pf = allow_pf && idx->groups_h.p != nullptr && (k <= kPfMaxK || (allow_rs && lk_use(idx, k, np)));
   ws.qn.reserve(sizeof(float) * nq);
   HIPCHK(launch_row_norms(q, nq, idx->d, ws.qn.as<float>(), s));
   // coarse: top-n_probes centroids per query
@@ -1018,39 +1024,256 @@ bool rs_pre_f8(mivs_index_s* idx, hipStream_t s) {
 // records per K13 stream: twice the batch's queries, at most kRsWaveCapMax (MIVS_RS_WAVE_CAP overrides it: the
 // lost-stream path is then testable at small sizes). Batches are at most kRsMaxBatch queries (ivf_search_impl),
 // so a stream's mean length (~160 records per 1,000 queries at the benchmark shape) stays far below the cap.
-int rs_wave_cap(int64_t nq) {
+// Large k (K16): est_cand candidates per query, one record each at that hit density, twice the mean stream.
+int rs_wave_cap(int64_t nq, int k = 1, int64_t est_cand = 0, int n_waves = 1) {
   const char* e = getenv("MIVS_RS_WAVE_CAP");
   if (e && atoi(e) > 0) return atoi(e);
+  if (k > kPfMaxK)
+    return (int)std::min<int64_t>(kRsWaveCapMaxLk, std::max<int64_t>(4096, 2 * nq * est_cand / std::max(1, n_waves)));
   return (int)std::min<int64_t>(kRsWaveCapMax, std::max<int64_t>(1024, 2 * nq));
 }
 
-// The K13 search of queries whose probes are in ws.probes_i and norms in ws.qn (DESIGN.md §6d):
-//   1. pre-pass: each query's nearest list through K10 + K11 -> the exact k-th key there;
-//   2. per-query header {qs, uf, qn, q}: uf is the filter bound for T_q >= the final refine window;
+// K16 serves k in (kPfMaxK, kMaxSelectK] through K13 when the index has the fp16 copy
+// (MIVS_LARGE_K_PF=0: the exact K3 DUMP + K8 path, A/B runs)
+bool lk_use(const mivs_index_s* idx, int k, int np) {
+  const char* e = getenv("MIVS_LARGE_K_PF");
+  return k > kPfMaxK && k <= kMaxSelectK && idx->groups_h.p != nullptr && rs_use(idx, np) && !(e && e[0] == '0');
+}
+
+// T_q's sample (K16): the first 1/div groups of every list (at least one); host-side bounds over the lists of
+// the sample's rank r_max (every query's r_q is below it: r_q grows with the query's sample fraction, a weighted
+// mean of its lists' fractions) and of the candidates per query it leads to
+struct LkPlan {
+  int div = kLkSampleDiv;
+  int r_max = 1;
+  int64_t slots_per_q = 1;  // K3 DUMP slots of a query over its sample lists (at most)
+  int64_t est_cand = 1;     // candidates per query K13 is expected to stream (T_q's global rank, about r / f)
+};
+LkPlan lk_plan(const mivs_index_s* idx, int k, int np) {
+  const ListSet& L = idx->lists;
+  LkPlan p;
+  const char* de = getenv("MIVS_LK_SAMPLE_DIV");
+  p.div = std::max(1, de ? atoi(de) : kLkSampleDiv);
+  double f_max = 0.0, rows = 0.0, smp = 0.0;
+  std::vector<int64_t> ch(L.n_lists);
+  for (int l = 0; l < L.n_lists; ++l) {
+    const int64_t ng = L.h_goff[l + 1] - L.h_goff[l], nr = L.h_off[l + 1] - L.h_off[l];
+    const int64_t sg = std::min<int64_t>(ng, std::max<int64_t>(1, ceil_div(ng, p.div)));
+    const double sr = (double)std::min<int64_t>(nr, sg * kGroupRows);
+    ch[l] = ceil_div(sg, idx->G);
+    if (nr > 0) f_max = std::max(f_max, sr / (double)nr);
+    rows += (double)nr;
+    smp += sr;
+  }
+  std::sort(ch.begin(), ch.end(), std::greater<int64_t>());
+  p.slots_per_q = 0;
+  for (int l = 0; l < std::min(np, L.n_lists); ++l) p.slots_per_q += ch[l];
+  p.slots_per_q = std::max<int64_t>(1, p.slots_per_q);
+  const double mu = (double)k * f_max;
+  p.r_max = (int)std::min<double>(kMaxSelectK, std::ceil(mu + kLkSampleZ * std::sqrt(mu) + 1.0));
+  const double f_avg = rows > 0 ? smp / rows : 1.0;
+  p.est_cand = (int64_t)std::ceil(std::max((double)k, (double)p.r_max / std::max(f_avg, 1e-9)));
+  return p;
+}
+
+// queries per K16 batch: the record streams, the windows and the sample's DUMP slots within the large-k workspace
+// (MIVS_LK_WORKSPACE_MB, default 8 GiB; K13 reads every probed row once per batch, so fewer batches are better)
+int64_t lk_batch(const mivs_index_s* idx, int64_t nq, int k, int np) {
+  const LkPlan p = lk_plan(idx, k, np);
+  const char* e = getenv("MIVS_LK_WORKSPACE_MB");
+  const size_t budget = (size_t)std::max<long long>(e ? atoll(e) : 8192, 1) << 20;
+  const size_t per_q = (size_t)p.est_cand * (2 * kRsRecInt4 * 16 + 8) + (size_t)lk_cap(k) * 12 +
+                       (size_t)p.slots_per_q * ((size_t)idx->G * kGroupRows * 4 + 16);
+  return std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t)(budget / std::max<size_t>(per_q, 1))));
+}
+
+// K16 step 1: T_q per query into ws.pre_kth from an exact scan of the sample (K3 DUMP over the
+// split lists 2l = the sample of list l, + K8 top r_max by (key, id)) and the sample's r_q-th key (k_lk_rank)
+void lk_prepass(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, const LkPlan& p) {
+  Workspace& ws = idx->ws;
+  const ListSet& L = idx->lists;
+  const int nl2 = 2 * L.n_lists;
+  const int64_t ne = nq * np;
+  ws.pre_goff.reserve(sizeof(int64_t) * ((size_t)nl2 + 1));
+  HIPCHK(launch_rs_pre_lists(L.goff.as<int64_t>(), L.n_lists, p.div, 1, nullptr, 0, np, ws.pre_goff.as<int64_t>(),
+                             nullptr, s));
+  ws.lk_probes.reserve(sizeof(int64_t) * ne);
+  HIPCHK(launch_lk_sample_probes(ws.probes_full.as<int64_t>(), ne, ws.lk_probes.as<int64_t>(), s));
+  ws.counts.reserve(sizeof(int) * nl2);
+  ws.fill.reserve(sizeof(int) * nl2);
+  ws.bucket_off.reserve(sizeof(int) * (nl2 + 1));
+  ws.work_off.reserve(sizeof(int) * (nl2 + 1));
+  ws.bucket_q.reserve(sizeof(int64_t) * ne);
+  ws.bucket_slot.reserve(sizeof(int64_t) * ne);
+  ws.qp_slots.reserve(sizeof(int64_t) * ne);
+  ws.slot_begin.reserve(sizeof(int64_t) * (nq + 1));
+  const size_t stb = scan_tmp_bytes(ne) + sizeof(int64_t) * (size_t)ne;
+  ws.scan_tmp.reserve(stb);
+  HIPCHK(launch_probe_map(ws.lk_probes.as<int64_t>(), nq, np, nl2, ws.pre_goff.as<int64_t>(), idx->G, kQTile,
+                          ws.counts.as<int>(), ws.fill.as<int>(), ws.bucket_off.as<int>(), ws.work_off.as<int>(),
+                          ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(), ws.qp_slots.as<int64_t>(),
+                          ws.slot_begin.as<int64_t>(), ws.scan_tmp.p, stb, s));
+  const int64_t slot_rows = (int64_t)idx->G * kGroupRows;
+  const int64_t slots = nq * p.slots_per_q;
+  ws.part_d.reserve(sizeof(float) * (size_t)(slots * slot_rows));
+  ws.part_i.reserve(sizeof(int64_t) * (size_t)(slots * 2));
+  ScanJob j{&L, idx->G, q, ws.qn.as<float>(), idx->d, idx->dp, p.r_max, idx->metric, ws.bucket_q.as<int64_t>(),
+            ws.bucket_slot.as<int64_t>(), ws.bucket_off.as<int>(), ws.work_off.as<int>(), ws.part_d.as<float>(),
+            ws.part_i.as<int64_t>(), kQTile};
+  j.dump = true;
+  j.goff = ws.pre_goff.as<int64_t>();
+  j.n_lists = nl2;
+  run_scan(j, idx->device, ws, s);
+  ws.lk_sel.reserve(sizeof(float) * (size_t)nq * p.r_max);
+  ws.lk_sel_i.reserve(sizeof(int64_t) * (size_t)nq * p.r_max);
+  SelectArgs sa{};
+  sa.keys = ws.part_d.as<float>();
+  sa.row_ids = L.ids.as<int64_t>();
+  sa.slot_info = ws.part_i.as<int64_t>();
+  sa.slot_begin = ws.slot_begin.as<int64_t>();
+  sa.slot_rows = (int)slot_rows;
+  sa.nq = nq;
+  sa.k = p.r_max;
+  sa.metric = idx->metric;
+  sa.out_d = ws.lk_sel.as<float>();
+  sa.out_i = ws.lk_sel_i.as<int64_t>();
+  HIPCHK(launch_select(sa, s));
+  ws.pre_kth.reserve(sizeof(float) * nq);
+  HIPCHK(launch_lk_rank(ws.probes_full.as<int64_t>(), nq, np, L.off.as<int64_t>(), ws.pre_goff.as<int64_t>(), k,
+                        kLkSampleZ, ws.lk_sel.as<float>(), p.r_max, idx->metric == kIP ? 1 : 0, ws.pre_kth.as<float>(),
+                        s));
+  // the fp16 queries, their scales and residuals for the headers and tiles
+  ws.qh.reserve(sizeof(uint16_t) * (size_t)nq * idx->dp);
+  ws.qscale.reserve(sizeof(float) * nq);
+  ws.qres.reserve(sizeof(float) * nq);
+  HIPCHK(launch_queries_to_half(q, nq, idx->d, idx->dp, idx->hx_exp, ws.qh.as<uint16_t>(), ws.qscale.as<float>(),
+                                ws.qres.as<float>(), s));
+}
+
+// the exact search (K3 / K3w, or K3 DUMP + K8 for k > 64) of n query rows, in query batches bounded by the select
+// workspace (the fallback of the pre-filter paths)
+void exact_search_batched(mivs_index_s* idx, hipStream_t s, const float* rows, int64_t n, int k, int np, float* out_d,
+                          int64_t* out_i) {
+  int64_t qb = n;
+  if (k > kMaxK) {
+    const ListSet& L = idx->lists;
+    const int64_t per_q_slots = std::max<int64_t>(1, L.top_chunks_prefix[std::min<int64_t>(np, L.n_lists)]);
+    qb = select_batch(n, (size_t)per_q_slots * ((size_t)idx->G * kGroupRows * 4 + 16));
+  }
+  for (int64_t b0 = 0; b0 < n; b0 += qb) {
+    const int64_t nb = std::min<int64_t>(qb, n - b0);
+    ivf_search_batch(idx, s, rows + b0 * (int64_t)idx->d, nb, k, np, out_d + b0 * k, out_i + b0 * k, nullptr, false,
+                     false);
+  }
+}
+
+// K16 steps 3-5 over K13's candidate runs (ws.cand_off / cand_key / cand_pos, T_q in ws.rs_tq), then the exact scan
+// for the queries it could not prove
+void lk_finish(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
+               int64_t* out_i, const int* lost) {
+  Workspace& ws = idx->ws;
+  const ListSet& L = idx->lists;
+  const int cap = lk_cap(k);
+  ws.lk_win_pos.reserve(sizeof(int) * (size_t)nq * cap);
+  ws.lk_win_key.reserve(sizeof(float) * (size_t)nq * cap);
+  ws.lk_win_n.reserve(sizeof(int) * (size_t)nq);
+  ws.lk_chunks.reserve(sizeof(int64_t) * (size_t)(nq + 1));
+  ws.lk_chunk_off.reserve(sizeof(int64_t) * (size_t)(nq + 1));
+  ws.pf_stats.reserve(32);
+  HIPCHK(hipMemsetAsync(ws.pf_stats.p, 0, 32, s));
+  ws.ovf_q.reserve(sizeof(int64_t) * nq);
+  LkArgs a{};
+  a.cand_off = ws.cand_off.as<int64_t>();
+  a.cand_key = ws.cand_key.as<float>();
+  a.cand_pos = ws.cand_pos.as<int>();
+  a.tq = ws.rs_tq.as<float>();
+  a.qnorms = ws.qn.as<float>();
+  a.qres = ws.qres.as<float>();
+  a.x_norm_max = idx->x_norm_max;
+  a.x_res_max = idx->x_res_max;
+  a.d = idx->d;
+  a.dp = idx->dp;
+  a.k = k;
+  a.cap = cap;
+  a.metric = idx->metric;
+  a.nq = nq;
+  a.force_ovf = lost;
+  a.win_pos = ws.lk_win_pos.as<int>();
+  a.win_key = ws.lk_win_key.as<float>();
+  a.win_n = ws.lk_win_n.as<int>();
+  a.ovf_count = ws.pf_stats.as<int>();
+  a.ovf_q = ws.ovf_q.as<int64_t>();
+  a.n_window = reinterpret_cast<int64_t*>(ws.pf_stats.as<char>() + 8);
+  a.chunk_off = ws.lk_chunk_off.as<int64_t>();
+  a.rows_rm = idx->rows_rm.p ? idx->rows_rm.as<float>() : nullptr;
+  a.groups = L.groups.as<float>();
+  a.row_norms = L.norms.as<float>();
+  a.row_ids = L.ids.as<int64_t>();
+  a.queries = q;
+  a.out_d = out_d;
+  a.out_i = out_i;
+  HIPCHK(launch_lk_window(a, s));
+  HIPCHK(launch_lk_chunks(a.win_n, nq, ws.lk_chunks.as<int64_t>(), s));
+  ws.scan_tmp.reserve(scan_tmp_bytes(nq + 1));
+  HIPCHK(launch_exclusive_scan_i64(ws.lk_chunks.as<int64_t>(), ws.lk_chunk_off.as<int64_t>(), nq + 1, ws.scan_tmp.p, s));
+  HIPCHK(launch_lk_recompute(a, 8 * cu_count(idx->device), s));
+  HIPCHK(launch_lk_sort(a, s));
+  int64_t h[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(h, ws.pf_stats.p, 16, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));  // the fallback size
+  const int64_t novf = (int64_t)(int32_t)(h[0] & 0xFFFFFFFF);
+  idx->last_ovf += novf;
+  idx->last_window += h[1];
+  if (novf > 0) {
+    ws.rs_ovf_q.reserve(sizeof(int64_t) * (size_t)novf);
+    ws.rs_ovf_rows.reserve(sizeof(float) * (size_t)novf * idx->d);
+    ws.rs_ovf_d.reserve(sizeof(float) * (size_t)novf * k);
+    ws.rs_ovf_i.reserve(sizeof(int64_t) * (size_t)novf * k);
+    HIPCHK(hipMemcpyAsync(ws.rs_ovf_q.p, ws.ovf_q.p, sizeof(int64_t) * novf, hipMemcpyDeviceToDevice, s));
+    HIPCHK(launch_gather_rows(q, idx->d, ws.rs_ovf_q.as<int64_t>(), novf, ws.rs_ovf_rows.as<float>(), s));
+    exact_search_batched(idx, s, ws.rs_ovf_rows.as<float>(), novf, k, np, ws.rs_ovf_d.as<float>(),
+                         ws.rs_ovf_i.as<int64_t>());
+    HIPCHK(launch_scatter_results(ws.rs_ovf_d.as<float>(), ws.rs_ovf_i.as<int64_t>(), ws.rs_ovf_q.as<int64_t>(), novf,
+                                  k, out_d, out_i, s));
+  }
+}
+
+// The K13 search of queries whose probes are in ws.probes_i and norms in ws.qn (DESIGN.md §6d, §6e):
+//   1. T_q: k <= 16, a pre-pass over a sample of each query's nearest list through K10 + K11 (the k-th key there);
+//      large k, an exact scan of a uniform sample of the probed rows (lk_prepass);
+//   2. per-query header {qs, uf, qn, q}: uf is the filter bound for T_q;
 //   3. probe map in (list, 8-group block) items, one query tile column per list;
 //   4. K13 streams every one-fma filter hit (a superset of the approximate keys <= T_q) per wave;
-//   5. K11 over the buffers + the exact fallback.
+//   5. k <= 16: K11 over the buffers; large k: K16 (window, pinned keys, sort); then the exact fallback.
 void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                int64_t* out_i, ProfRec* pr) {
   Workspace& ws = idx->ws;
   const ListSet& L = idx->lists;
   const int dp = idx->dp;
   const int64_t ne = nq * np;
+  const bool large = k > kPfMaxK;
   ws.probes_full.reserve(sizeof(int64_t) * ne);
   HIPCHK(hipMemcpyAsync(ws.probes_full.p, ws.probes_i.p, sizeof(int64_t) * ne, hipMemcpyDeviceToDevice, s));
-  // 1. a sample of the nearest list of every query (probe 0): its first 1/div groups (the rows of a list
-  // are in no particular order) through K10 over the split lists, and the k-th smallest approximate key
-  // of each query's candidates there (K11's first phase only)
-  ws.pre_goff.reserve(sizeof(int64_t) * (2 * (size_t)L.n_lists + 1));
-  // fp8 nomination (MIVS_RS_PRE_F8, default on where it applies): the sample scored on fp8 copies over every dim,
-  // the kRsPreSel best rows of each query verified with fp32 keys
-  const bool pre_f8 = rs_pre_f8(idx, s);
-  const int pre_sel = pre_f8 ? std::min(kPfMaxK, std::max(k, kRsPreSel)) : 0;
-  const char* pde = getenv("MIVS_RS_PRE_DIV");
-  const int pre_div = std::max(1, pde ? atoi(pde) : (pre_f8 ? kRsPreDivF8 : kRsPreDiv));
-  HIPCHK(launch_rs_pre_lists(L.goff.as<int64_t>(), L.n_lists, pre_div, ceil_div(k, kGroupRows), ws.probes_full.as<int64_t>(),
-                             nq, np, ws.pre_goff.as<int64_t>(), ws.probes_i.as<int64_t>(), s));
-  {
+  LkPlan plan;
+  bool pre_f8 = false;
+  int pre_div = 0, pre_sel = 0;
+  if (large) {
+    plan = lk_plan(idx, k, np);
+    lk_prepass(idx, s, q, nq, k, np, plan);
+  } else {
+    // 1. a sample of the nearest list of every query (probe 0): its first 1/div groups (the rows of a list
+    // are in no particular order) through K10 over the split lists, and the k-th smallest approximate key
+    // of each query's candidates there (K11's first phase only)
+    ws.pre_goff.reserve(sizeof(int64_t) * (2 * (size_t)L.n_lists + 1));
+    // fp8 nomination (MIVS_RS_PRE_F8, default on where it applies): the sample scored on fp8 copies over every
+    // dim, the kRsPreSel best rows of each query verified with fp32 keys
+    pre_f8 = rs_pre_f8(idx, s);
+    pre_sel = pre_f8 ? std::min(kPfMaxK, std::max(k, kRsPreSel)) : 0;
+    const char* pde = getenv("MIVS_RS_PRE_DIV");
+    pre_div = std::max(1, pde ? atoi(pde) : (pre_f8 ? kRsPreDivF8 : kRsPreDiv));
+    HIPCHK(launch_rs_pre_lists(L.goff.as<int64_t>(), L.n_lists, pre_div, ceil_div(k, kGroupRows),
+                               ws.probes_full.as<int64_t>(), nq, np, ws.pre_goff.as<int64_t>(),
+                               ws.probes_i.as<int64_t>(), s));
     const int nl2 = 2 * L.n_lists;
     ws.counts.reserve(sizeof(int) * nl2);
     ws.fill.reserve(sizeof(int) * nl2);
@@ -1070,7 +1293,7 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
     pf_scan_refine(idx, s, q, nq, k, 1, nullptr, nullptr, nullptr, ws.pre_goff.as<int64_t>(), nl2,
                    ws.pre_kth.as<float>(), pre_sel, pre_f8);
   }
-  // 2. headers (pf_scan_refine left the fp16 queries, their scales and residuals in ws.qh / qscale / qres)
+  // 2. headers (the pre-pass left the fp16 queries, their scales and residuals in ws.qh / qscale / qres)
   ws.qhdr.reserve(sizeof(float4) * (nq + 1));
   float4* qhdr = ws.qhdr.as<float4>();
   ws.rs_tq.reserve(sizeof(float) * nq);
@@ -1092,11 +1315,20 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
     std::vector<float> sorted = ht;
     std::sort(sorted.begin(), sorted.end());
     auto pc = [&](double f) { return sorted[std::min<int64_t>(nq - 1, (int64_t)(f * nq))]; };
-    fprintf(stderr, "[rs pre] f8 %d div %d sel %d | mean kth %.6f mean T_q %.6f | inf %lld of %lld | T_q p10 %.4f "
-            "p50 %.4f p90 %.4f p99 %.4f max %.4f\n", (int)pre_f8, pre_div, pre_sel, sk / nf, st / nf, (long long)ninf,
-            (long long)nq, pc(0.1), pc(0.5), pc(0.9), pc(0.99), sorted[nq - 1]);
+    fprintf(stderr, "[rs pre] k %d f8 %d div %d sel %d r_max %d | mean kth %.6f mean T_q %.6f | inf %lld of %lld | "
+            "T_q p10 %.4f p50 %.4f p90 %.4f p99 %.4f max %.4f\n", k, (int)pre_f8, large ? plan.div : pre_div, pre_sel,
+            large ? plan.r_max : 0, sk / nf, st / nf, (long long)ninf, (long long)nq, pc(0.1), pc(0.5), pc(0.9),
+            pc(0.99), sorted[nq - 1]);
   }
   // 3. probe map: items = (list, block of kRsBlockGroups groups); every query of a list in one tile column
+  ws.counts.reserve(sizeof(int) * L.n_lists);
+  ws.fill.reserve(sizeof(int) * L.n_lists);
+  ws.bucket_off.reserve(sizeof(int) * (L.n_lists + 1));
+  ws.work_off.reserve(sizeof(int) * (L.n_lists + 1));
+  ws.bucket_q.reserve(sizeof(int64_t) * ne);
+  ws.bucket_slot.reserve(sizeof(int64_t) * ne);
+  ws.qp_slots.reserve(sizeof(int64_t) * ne);
+  ws.slot_begin.reserve(sizeof(int64_t) * (nq + 1));
   const size_t stb = scan_tmp_bytes(ne) + sizeof(int64_t) * (size_t)ne;
   ws.scan_tmp.reserve(stb);
   HIPCHK(launch_probe_map(ws.probes_full.as<int64_t>(), nq, np, L.n_lists, L.goff.as<int64_t>(), kRsBlockGroups,
@@ -1139,7 +1371,7 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   const int n_waves = grid * kRsWaves;
   idx->last_rs_waves = n_waves;
   idx->last_rs_nq = nq;
-  a.wave_cap = rs_wave_cap(nq);
+  a.wave_cap = rs_wave_cap(nq, k, plan.est_cand, n_waves);
   ws.rs_wave_buf.reserve(sizeof(int4) * kRsRecInt4 * (size_t)n_waves * a.wave_cap);
   // + the lost flag, the 8 item-queue counters, the spun-out wave count
   ws.rs_wave_cnt.reserve(sizeof(int) * (n_waves + 1 + 8 + 1));
@@ -1193,17 +1425,33 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
               (double)h[3 * grid + 10], wc / (double)h[3 * grid + 10]);
   }
   // the streams into per-query CSR runs (a record expands to at most 8 candidates)
-  const size_t max_cand = (size_t)n_waves * a.wave_cap * 8;
   ws.cand_off.reserve(sizeof(int64_t) * (nq + 1));
-  ws.cand_key.reserve(sizeof(float) * max_cand);
-  ws.cand_pos.reserve(sizeof(int) * max_cand);
   ws.rs_bucket_tmp.reserve(rs_bucket_tmp_bytes((int)nq, n_waves));
-  HIPCHK(launch_rs_bucket(a.wave_buf, a.wave_cap, a.wave_cnt, n_waves, (int)nq, qhdr, a.row_norms,
-                          idx->metric, ws.cand_off.as<int64_t>(), ws.cand_key.as<float>(), ws.cand_pos.as<int>(),
-                          ws.rs_bucket_tmp.p, a.wave_cnt + n_waves, 4 * cu_count(idx->device), s));
-  // 5. exact ranking of every query's run (slot = one entry); a window above T_q is not proven
-  pf_refine_fallback(idx, s, q, nq, k, np, out_d, out_i, ws.cand_key.as<float>(), ws.cand_pos.as<int>(), nullptr,
-                     a.wave_cnt + n_waves, ws.cand_off.as<int64_t>(), 1, true, nullptr, ws.rs_tq.as<float>());
+  if (!large) {
+    const size_t max_cand = (size_t)n_waves * a.wave_cap * 8;
+    ws.cand_key.reserve(sizeof(float) * max_cand);
+    ws.cand_pos.reserve(sizeof(int) * max_cand);
+    HIPCHK(launch_rs_bucket(a.wave_buf, a.wave_cap, a.wave_cnt, n_waves, (int)nq, qhdr, a.row_norms,
+                            idx->metric, ws.cand_off.as<int64_t>(), ws.cand_key.as<float>(), ws.cand_pos.as<int>(),
+                            ws.rs_bucket_tmp.p, a.wave_cnt + n_waves, 4 * cu_count(idx->device), s));
+    // 5. exact ranking of every query's run (slot = one entry); a window above T_q is not proven
+    pf_refine_fallback(idx, s, q, nq, k, np, out_d, out_i, ws.cand_key.as<float>(), ws.cand_pos.as<int>(), nullptr,
+                       a.wave_cnt + n_waves, ws.cand_off.as<int64_t>(), 1, true, nullptr, ws.rs_tq.as<float>());
+    return;
+  }
+  // large k: the candidate arrays sized by the count (one host sync: up to 8 candidates per record would be
+  // several GB at this k)
+  HIPCHK(launch_rs_bucket_count(a.wave_buf, a.wave_cap, a.wave_cnt, n_waves, (int)nq, qhdr, a.row_norms, idx->metric,
+                                ws.cand_off.as<int64_t>(), ws.rs_bucket_tmp.p, a.wave_cnt + n_waves, s));
+  int64_t total = 0;
+  HIPCHK(hipMemcpyAsync(&total, ws.cand_off.as<int64_t>() + nq, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  ws.cand_key.reserve(sizeof(float) * (size_t)std::max<int64_t>(total, 1));
+  ws.cand_pos.reserve(sizeof(int) * (size_t)std::max<int64_t>(total, 1));
+  HIPCHK(launch_rs_bucket_scatter(a.wave_buf, a.wave_cap, a.wave_cnt, n_waves, (int)nq, qhdr, a.row_norms, idx->metric,
+                                  ws.cand_off.as<int64_t>(), ws.cand_key.as<float>(), ws.cand_pos.as<int>(),
+                                  ws.rs_bucket_tmp.p, s));
+  lk_finish(idx, s, q, nq, k, np, out_d, out_i, a.wave_cnt + n_waves);
 }
 
 void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
@@ -1225,6 +1473,7 @@ void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t
   ws.slot_begin.reserve(sizeof(int64_t) * (nq + 1));
   const size_t stb = scan_tmp_bytes(ne) + sizeof(int64_t) * (size_t)ne;
   ws.scan_tmp.reserve(stb);
+  if (pf && k > kPfMaxK && !(allow_rs && lk_use(idx, k, np))) pf = false;  // (large k: K13 + K16 or the exact scan)
   const bool dump = k > kMaxK;
   const int qtile = pf ? kPfQTile : (dump ? kQTile : pick_qtile(k, idx->d, idx->G));
   if (prof) {
@@ -1403,7 +1652,9 @@ void pq_search_rt(mivs_index_s* idx, hipStream_t s, const float* d_q, int64_t nq
 void ivf_search_impl(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                      int64_t* out_i, int32_t* out_probes) {
   int64_t qb = nq;
-  if (k > kMaxK) {  // DUMP workspace: bound it by batching queries
+  if (lk_use(idx, k, np)) {  // K16: the record streams and windows bound the batch
+    qb = std::min<int64_t>(std::min<int64_t>(nq, kRsMaxBatch), lk_batch(idx, nq, k, np));
+  } else if (k > kMaxK) {  // DUMP workspace: bound it by batching queries
     const ListSet& L = idx->lists;
     const int64_t per_q_slots = std::max<int64_t>(1, L.top_chunks_prefix[std::min<int64_t>(np, L.n_lists)]);
     qb = select_batch(nq, (size_t)per_q_slots * ((size_t)idx->G * kGroupRows * 4 + 16));

@@ -1,0 +1,374 @@
+// K16 -- large-k IVF search through the fp16 pre-filter (k in (16, 4096]).
+//
+// The reference's driver asks for top_k = 2000 and each shard for k * 2 (Latest/cuVS-2-gpu/
+// improved_multi_gpu_rag.py:40,247). At that k the k-th key lies in the bulk of the distance distribution:
+// the rows near it are dense (at configs[2] ~80 probed rows per 0.001 of key), and no cheap sample bounds it
+// rigorously (the nearest list's 2000-th key is the ~24,000-th over the probed lists: tools/large_k_stats.py).
+// So the pipeline TRIES a threshold and PROVES each query's answer at run time:
+//
+//   1. T_q: a uniform sample of the probed rows (the first 1/div of every probed list; rows of a list are in
+//      no particular order) scanned exactly (K3 DUMP + K8); the sample's r_q-th key, r_q = mu + z sqrt(mu) + 1
+//      with mu = k n_sample / n_probed, lies above the k-th probed key with high probability (k_lk_rank);
+//   2. K13 streams every row whose approximate key may be <= T_q (the k <= 16 path's scan, unchanged);
+//   3. K16w (k_lk_window): per query the k-th smallest approximate key Ak of its candidates, the refine
+//      window T = Ak + 2 delta (pf_window), and the proof: at least k candidates and T <= T_q, so every row
+//      whose pinned key can reach the top-k is a candidate (the k <= 16 path's K11 argument). The window's
+//      row positions go to a fixed per-query capacity; a query that fails the proof goes to the exact scan;
+//   4. K16r (k_lk_recompute): the pinned fp32 key of every window row (oracle orc_dot's order), one lane per
+//      row, the query in scalar registers, the row read from the row-major fp32 copy -- the gather of
+//      ~(k + window) x d x 4 bytes per query is the step's floor;
+//   5. K16s (k_lk_sort): per query a bitonic sort of the window by (key, id) in LDS; the first k are the answer.
+#include <climits>
+
+#include "mivs_common.hpp"
+#include "pf_math.hpp"
+
+namespace mivs {
+
+namespace {
+
+constexpr int kLkThreads = 256;
+constexpr int kLkBins = 2048;
+
+__device__ __forceinline__ uint32_t lk_ord(float f) {
+  const uint32_t u = __float_as_uint(f == 0.0f ? 0.0f : f);  // (-0 and +0: one key)
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float lk_unord(uint32_t o) {
+  return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
+}
+
+// every probe p of query q -> sample list 2 p (the first part of the split list set, k_rs_pre_goff)
+__global__ void k_lk_sample_probes(const int64_t* __restrict__ probes, int64_t n, int64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t p = probes[i];
+  out[i] = p < 0 ? p : 2 * p;
+}
+
+// T_q's key per query: the r_q-th smallest exact key of the sample (sel: the sample's top r_max by (key, id), K8
+// output distances), or +inf when the sample cannot reach it (then every probed row is a candidate)
+__global__ void k_lk_rank(const int64_t* __restrict__ probes, int64_t nq, int np, const int64_t* __restrict__ list_off,
+                          const int64_t* __restrict__ goff2, int k, float z, const float* __restrict__ sel, int r_max,
+                          int ip, float* __restrict__ kth) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  double n_all = 0.0, n_smp = 0.0;
+  for (int p = 0; p < np; ++p) {
+    const int64_t l = probes[q * np + p];
+    if (l < 0) continue;
+    const double nl = (double)(list_off[l + 1] - list_off[l]);
+    const double ns = (double)(goff2[2 * l + 1] - goff2[2 * l]) * kGroupRows;
+    n_all += nl;
+    n_smp += ns < nl ? ns : nl;
+  }
+  float out = INFINITY;
+  if (n_all > (double)k && n_smp > 0.0) {
+    const double mu = (double)k * n_smp / n_all;
+    const double r = ceil(mu + (double)z * sqrt(mu) + 1.0);
+    if (r <= (double)r_max && r <= n_smp) {
+      const float v = sel[q * r_max + (int64_t)r - 1];
+      out = ip ? -v : v;  // (K8 reports the inner product for IP; the key is its negation)
+      if (!(out < INFINITY) || out != out) out = INFINITY;
+    }
+  }
+  kth[q] = out;
+}
+
+// block-wide exclusive scan of one int per thread (kLkThreads threads); returns the prefix, *tot the sum
+__device__ __forceinline__ int lk_block_scan(int v, int* sh, int* tot) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sh[w] = x;
+  __syncthreads();
+  int base = 0, all = 0;
+#pragma unroll
+  for (int i = 0; i < kLkThreads / 64; ++i) {
+    const int s = sh[i];
+    base += i < w ? s : 0;
+    all += s;
+  }
+  __syncthreads();
+  *tot = all;
+  return base + x - v;
+}
+
+// K16w: one workgroup per query
+template <int METRIC>
+__global__ __launch_bounds__(kLkThreads) void k_lk_window(LkArgs a) {
+  __shared__ int s_hist[kLkBins];
+  __shared__ int s_sh[kLkThreads / 64];
+  __shared__ uint32_t s_sel[2];
+  const int64_t q = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int64_t c0 = a.cand_off[q];
+  const int n_c = (int)(a.cand_off[q + 1] - c0);
+  const int k = a.k;
+  const float Tq = a.tq[q];
+  const float qn = a.qnorms[q];
+  const float delta = pf_delta<METRIC>(qn, a.qres[q], a.x_norm_max, a.x_res_max, a.dp);
+  const bool lost = a.force_ovf && *a.force_ovf;
+  // 1. Ak = the k-th smallest approximate key (orderable bits, three digits of 11 / 11 / 10 bits); +inf with < k
+  uint32_t ans = 0xFFFFFFFFu;
+  if (n_c >= k && !lost) {
+    uint32_t prefix = 0, pmask = 0;
+    int kk = k;
+    const int shifts[3] = {21, 10, 0};
+    const int widths[3] = {11, 11, 10};
+#pragma unroll 1
+    for (int d = 0; d < 3; ++d) {
+      const int sh = shifts[d], nb = 1 << widths[d];
+      for (int i = tid; i < nb; i += kLkThreads) s_hist[i] = 0;
+      __syncthreads();
+      for (int i = tid; i < n_c; i += kLkThreads) {
+        const uint32_t u = lk_ord(a.cand_key[c0 + i]);
+        if ((u & pmask) == prefix) atomicAdd(s_hist + ((u >> sh) & (nb - 1)), 1);
+      }
+      __syncthreads();
+      // the bin holding the kk-th: per-thread sums of nb / kLkThreads consecutive bins, then a scan
+      const int per = nb / kLkThreads;
+      int cs = 0;
+      for (int j = 0; j < per; ++j) cs += s_hist[tid * per + j];
+      int tot;
+      const int ex = lk_block_scan(cs, s_sh, &tot);
+      if (ex < kk && kk <= ex + cs) {
+        int c = ex;
+        for (int j = 0; j < per; ++j) {
+          const int h = s_hist[tid * per + j];
+          if (c + h >= kk) {
+            s_sel[0] = (uint32_t)(tid * per + j);
+            s_sel[1] = (uint32_t)(kk - c);
+            break;
+          }
+          c += h;
+        }
+      }
+      __syncthreads();
+      prefix |= s_sel[0] << sh;
+      pmask |= (uint32_t)(nb - 1) << sh;
+      kk = (int)s_sel[1];
+      __syncthreads();
+    }
+    ans = prefix;
+  }
+  const float Ak = ans == 0xFFFFFFFFu ? INFINITY : lk_unord(ans);
+  const float T = Ak < INFINITY ? pf_window(Ak, delta) : INFINITY;
+  // 2. the proof: every row whose pinned key can reach the top-k has approximate key <= T; the candidates hold
+  // every row with approximate key <= T_q; so T <= T_q (and >= k candidates) makes the window complete. With
+  // T_q = +inf every probed row is a candidate and fewer than k is the whole answer.
+  bool ovf = lost || !(T <= Tq) || (Tq < INFINITY && n_c < k);
+  // 3. the window's row positions (any order) into the query's fixed-capacity slot
+  int n_w = 0;
+  if (!ovf) {
+    for (int i0 = 0; i0 < n_c; i0 += kLkThreads) {
+      const int i = i0 + tid;
+      const float ck = i < n_c ? a.cand_key[c0 + i] : INFINITY;
+      const bool take = ck <= T && ck < INFINITY;
+      int tot;
+      const int at = n_w + lk_block_scan(take ? 1 : 0, s_sh, &tot);
+      if (take && at < a.cap) a.win_pos[q * a.cap + at] = a.cand_pos[c0 + i];
+      n_w += tot;
+    }
+    ovf = n_w > a.cap;
+  }
+  if (tid == 0) {
+    a.win_n[q] = ovf ? -1 : n_w;  // (-1: the exact scan answers this query)
+    if (ovf) {
+      const int at = atomicAdd(a.ovf_count, 1);
+      a.ovf_q[at] = q;
+    } else if (a.n_window) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(a.n_window), (unsigned long long)n_w);
+    }
+  }
+}
+
+// per query the number of 64-row chunks of its window (K16r's work items)
+__global__ void k_lk_chunks(const int* __restrict__ win_n, int64_t nq, int64_t* __restrict__ chunks) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < nq) chunks[q] = win_n[q] > 0 ? (win_n[q] + 63) / 64 : 0;
+  if (q == nq) chunks[q] = 0;
+}
+
+// K16r: persistent waves over the (query, 64-row chunk) items; lane i computes the pinned fp32 key of window row
+// 64 j + i: the fma chain of oracle orc_dot (per 8-dim block: dims 0/4, 1/5, 2/6, 3/7), the query's values as
+// scalar operands (the query index is wave-uniform), the row's from the row-major copy (or the group layout)
+template <int METRIC>
+__global__ __launch_bounds__(256) void k_lk_recompute(LkArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n_items = a.chunk_off[a.nq];
+  const int64_t n_waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int nb = a.dp >> 3;
+  for (int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); w < n_items; w += n_waves) {
+    // the item's query: the last q with chunk_off[q] <= w
+    int64_t lo = 0, hi = a.nq - 1;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (a.chunk_off[mid] <= w) lo = mid; else hi = mid - 1;
+    }
+    const int64_t q = __builtin_amdgcn_readfirstlane((int)lo);
+    const int j = (int)(w - a.chunk_off[q]);
+    const int i = 64 * j + lane;
+    const int n_w = a.win_n[q];
+    const bool live = i < n_w;
+    const int pos = live ? a.win_pos[q * a.cap + i] : 0;
+    const float* rowp = a.rows_rm ? a.rows_rm + (int64_t)pos * a.dp
+                                  : a.groups + ((int64_t)(pos >> 5) * nb * kGroupRows + (pos & 31)) * 8;
+    const int64_t bstride = a.rows_rm ? 8 : 256;
+    const float* qv = a.queries + q * a.d;
+    float acc = 0.0f;
+    const int nbd = a.d >> 3;  // blocks fully inside d (the padded tail is zero: neutral, the accumulator is never -0)
+#pragma unroll 8
+    for (int b = 0; b < nbd; ++b) {
+      const float4 x0 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride);
+      const float4 x1 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride + 4);
+      const float* y = qv + 8 * b;
+      acc = fmaf(x0.x, y[0], acc); acc = fmaf(x1.x, y[4], acc);
+      acc = fmaf(x0.y, y[1], acc); acc = fmaf(x1.y, y[5], acc);
+      acc = fmaf(x0.z, y[2], acc); acc = fmaf(x1.z, y[6], acc);
+      acc = fmaf(x0.w, y[3], acc); acc = fmaf(x1.w, y[7], acc);
+    }
+    if (nbd < nb) {  // d % 8 != 0: the last block's query dims past d read as zero
+      const int b = nbd;
+      const float4 x0 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride);
+      const float4 x1 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride + 4);
+      float y[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) y[t] = 8 * b + t < a.d ? qv[8 * b + t] : 0.0f;
+      acc = fmaf(x0.x, y[0], acc); acc = fmaf(x1.x, y[4], acc);
+      acc = fmaf(x0.y, y[1], acc); acc = fmaf(x1.y, y[5], acc);
+      acc = fmaf(x0.z, y[2], acc); acc = fmaf(x1.z, y[6], acc);
+      acc = fmaf(x0.w, y[3], acc); acc = fmaf(x1.w, y[7], acc);
+    }
+    if (live) {
+      float P;
+      if (METRIC == kL2) {
+        const float v = fmaf(-2.0f, acc, a.row_norms[pos] + a.qnorms[q]);
+        P = v > 0.0f ? v : 0.0f;
+      } else {
+        P = -acc;
+      }
+      a.win_key[q * a.cap + i] = P;
+    }
+  }
+}
+
+// (key, id) order with the id looked up only for equal keys (rare: duplicate rows)
+__device__ __forceinline__ bool lk_less(float ka, int pa, float kb, int pb, const int64_t* __restrict__ row_ids) {
+  if (ka != kb) return ka < kb;
+  if (pa == pb) return false;
+  if (pa < 0 || pb < 0) return pb < 0 && pa >= 0;
+  return row_ids[pa] < row_ids[pb];
+}
+
+// K16s: one workgroup per query; bitonic sort of the window's (key, position) by (key, id) in LDS, the first k out
+template <int METRIC, int CAP>
+__global__ __launch_bounds__(kLkThreads) void k_lk_sort(LkArgs a) {
+  __shared__ float s_k[CAP];
+  __shared__ int s_p[CAP];
+  const int64_t q = blockIdx.x;
+  const int n_w = a.win_n[q];
+  if (n_w < 0) return;  // (the exact scan's answer is scattered in later)
+  int N = 64;
+  while (N < n_w) N <<= 1;
+  for (int i = threadIdx.x; i < N; i += kLkThreads) {
+    const bool v = i < n_w;
+    s_k[i] = v ? a.win_key[q * a.cap + i] : INFINITY;
+    s_p[i] = v ? a.win_pos[q * a.cap + i] : -1;
+  }
+  __syncthreads();
+  for (int size = 2; size <= N; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < N / 2; t += kLkThreads) {
+        const int lo = 2 * t - (t & (stride - 1));
+        const int hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const float kl = s_k[lo], kh = s_k[hi];
+        const int pl = s_p[lo], ph = s_p[hi];
+        const bool sw = up ? lk_less(kh, ph, kl, pl, a.row_ids) : lk_less(kl, pl, kh, ph, a.row_ids);
+        if (sw) {
+          s_k[lo] = kh; s_k[hi] = kl;
+          s_p[lo] = ph; s_p[hi] = pl;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < a.k; i += kLkThreads) {
+    const bool v = i < n_w;
+    const float P = v ? s_k[i] : INFINITY;
+    a.out_d[q * a.k + i] = v ? (METRIC == kIP ? -P : P) : (METRIC == kIP ? -INFINITY : INFINITY);
+    a.out_i[q * a.k + i] = v ? a.row_ids[s_p[i]] : (int64_t)-1;
+  }
+}
+
+template <int METRIC>
+hipError_t launch_lk_sort_m(const LkArgs& a, hipStream_t s) {
+  const dim3 g((unsigned)a.nq), b(kLkThreads);
+  switch (a.cap) {
+    case 256: hipLaunchKernelGGL((k_lk_sort<METRIC, 256>), g, b, 0, s, a); break;
+    case 512: hipLaunchKernelGGL((k_lk_sort<METRIC, 512>), g, b, 0, s, a); break;
+    case 1024: hipLaunchKernelGGL((k_lk_sort<METRIC, 1024>), g, b, 0, s, a); break;
+    case 2048: hipLaunchKernelGGL((k_lk_sort<METRIC, 2048>), g, b, 0, s, a); break;
+    case 4096: hipLaunchKernelGGL((k_lk_sort<METRIC, 4096>), g, b, 0, s, a); break;
+    case 8192: hipLaunchKernelGGL((k_lk_sort<METRIC, 8192>), g, b, 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
+
+int lk_cap(int k) {
+  // the window holds the k answers plus the rows within 2 delta above the k-th (configs[2]: ~10 % of k); a query
+  // whose window exceeds the capacity takes the exact scan
+  int c = 256;
+  const int need = k + k / 2 + 256;
+  while (c < need && c < kLkMaxCap) c <<= 1;
+  return c;
+}
+
+hipError_t launch_lk_sample_probes(const int64_t* probes, int64_t n, int64_t* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_lk_sample_probes, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, probes, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_lk_rank(const int64_t* probes, int64_t nq, int np, const int64_t* list_off, const int64_t* goff2,
+                          int k, float z, const float* sel, int r_max, int ip, float* kth, hipStream_t s) {
+  if (nq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_lk_rank, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, s, probes, nq, np, list_off, goff2, k,
+                     z, sel, r_max, ip, kth);
+  return hipGetLastError();
+}
+
+hipError_t launch_lk_window(const LkArgs& a, hipStream_t s) {
+  if (a.nq <= 0) return hipSuccess;
+  if (a.k < 1 || a.k > kMaxSelectK || a.cap > kLkMaxCap || a.dp > 1024) return hipErrorInvalidValue;
+  if (a.metric == kIP) hipLaunchKernelGGL(k_lk_window<kIP>, dim3((unsigned)a.nq), dim3(kLkThreads), 0, s, a);
+  else hipLaunchKernelGGL(k_lk_window<kL2>, dim3((unsigned)a.nq), dim3(kLkThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_lk_chunks(const int* win_n, int64_t nq, int64_t* chunks, hipStream_t s) {
+  hipLaunchKernelGGL(k_lk_chunks, dim3((unsigned)ceil_div(nq + 1, 256)), dim3(256), 0, s, win_n, nq, chunks);
+  return hipGetLastError();
+}
+
+hipError_t launch_lk_recompute(const LkArgs& a, int grid, hipStream_t s) {
+  if (a.nq <= 0) return hipSuccess;
+  if (a.metric == kIP) hipLaunchKernelGGL(k_lk_recompute<kIP>, dim3((unsigned)grid), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(k_lk_recompute<kL2>, dim3((unsigned)grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_lk_sort(const LkArgs& a, hipStream_t s) {
+  if (a.nq <= 0) return hipSuccess;
+  return a.metric == kIP ? launch_lk_sort_m<kIP>(a, s) : launch_lk_sort_m<kL2>(a, s);
+}
+
+}  // namespace mivs

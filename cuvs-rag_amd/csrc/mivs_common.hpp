@@ -236,6 +236,7 @@ constexpr int kRsPreDiv = 4;
 constexpr int kRsPreDivF8 = 4;
 constexpr int kRsPreSel = 10;
 constexpr int kRsWaveCapMax = 16384;  // records of a K13 wave's candidate stream (more: all queries fall back)
+constexpr int kRsWaveCapMaxLk = 1 << 18;  // the same for large k (K16: thousands of candidates per query)
 constexpr int kRsRecInt4 = 3;         // a record: 8 dots of one lane and query half + {first row position, query}
 constexpr int kRsMaxBatch = 32768;    // queries per K13 search batch (the LDS-histogram bucketing's bins)
 
@@ -262,6 +263,46 @@ struct RsScanArgs {
                              // 4 keep the rows at item transitions, 8 per-block clocks into prof, 16 phase clocks
   unsigned long long* prof;  // flags & 8: [grid][3] {start, end, tiles}
 };
+
+// K16 large-k search through the pre-filter (largek.hip): K13's candidates -> per query the refine
+// window (K16w) -> pinned fp32 keys of the window rows (K16r) -> (key, id) sort and the first k (K16s)
+constexpr int kLkMaxCap = 8192;    // window rows per query at most (more: the exact scan)
+constexpr int kLkSampleDiv = 64;   // T_q's sample: the first 1 / kLkSampleDiv of every probed list (MIVS_LK_SAMPLE_DIV)
+constexpr float kLkSampleZ = 4.0f; // sample rank margin in standard deviations (binomial)
+struct LkArgs {
+  const int64_t* cand_off;  // [nq + 1] K13's per-query candidate runs
+  const float* cand_key;    // approximate keys
+  const int* cand_pos;      // row positions
+  const float* tq;          // [nq] T_q (+inf: every probed row is a candidate)
+  const float* qnorms;      // [nq] pinned query norms
+  const float* qres;        // [nq] ||q - q_h||
+  float x_norm_max, x_res_max;
+  int d, dp, k, cap, metric;
+  int64_t nq;
+  const int* force_ovf;     // optional: nonzero -> no query is provable (K13 lost records)
+  int* win_pos;             // [nq][cap] window row positions
+  float* win_key;           // [nq][cap] their pinned keys
+  int* win_n;               // [nq] window rows (-1: the query takes the exact scan)
+  int* ovf_count;
+  int64_t* ovf_q;
+  int64_t* n_window;        // optional: total window rows (stats)
+  const int64_t* chunk_off; // [nq + 1] exclusive prefix of the windows' 64-row chunks (K16r's items)
+  const float* rows_rm;     // fp32 rows row-major (or nullptr: the group layout below)
+  const float* groups;
+  const float* row_norms;
+  const int64_t* row_ids;
+  const float* queries;     // fp32 [nq][d]
+  float* out_d;
+  int64_t* out_i;
+};
+int lk_cap(int k);
+hipError_t launch_lk_sample_probes(const int64_t* probes, int64_t n, int64_t* out, hipStream_t s);
+hipError_t launch_lk_rank(const int64_t* probes, int64_t nq, int np, const int64_t* list_off, const int64_t* goff2,
+                          int k, float z, const float* sel, int r_max, int ip, float* kth, hipStream_t s);
+hipError_t launch_lk_window(const LkArgs& a, hipStream_t s);
+hipError_t launch_lk_chunks(const int* win_n, int64_t nq, int64_t* chunks, hipStream_t s);
+hipError_t launch_lk_recompute(const LkArgs& a, int grid, hipStream_t s);
+hipError_t launch_lk_sort(const LkArgs& a, hipStream_t s);
 
 // K13a k-means assign on the row-stationary loop (assign.hip)
 struct AsScanArgs {
@@ -386,6 +427,14 @@ size_t rs_bucket_tmp_bytes(int nq, int n_waves);
 hipError_t launch_rs_bucket(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
                             const float4* qhdr, const float* row_norms, int metric, int64_t* cand_off,
                             float* cand_key, int* cand_pos, void* tmp, int* lost, int grid, hipStream_t s);
+// the same in two halves (large k sizes the candidate arrays from cand_off[nq] between them): count -> cand_off,
+// then the scatter
+hipError_t launch_rs_bucket_count(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
+                                  const float4* qhdr, const float* row_norms, int metric, int64_t* cand_off, void* tmp,
+                                  int* lost, hipStream_t s);
+hipError_t launch_rs_bucket_scatter(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
+                                    const float4* qhdr, const float* row_norms, int metric, const int64_t* cand_off,
+                                    float* cand_key, int* cand_pos, void* tmp, hipStream_t s);
 // fp8 (e4m3) copies for K13's pre-pass nomination: rows at scale 2^hx8 in the operand layout of
 // k_pf_scan<.., F8> (dp % 32 == 0), queries at their own power of two (qscale8[q] = the fp8 dot -> fp32 dot)
 hipError_t launch_groups_to_f8(const float* groups, int64_t n_groups, int dp, int hx8, uint8_t* out, hipStream_t s);

@@ -442,6 +442,10 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
       // (the header piece holds query j's header at lanes j and j + 32)
       const float4 hq0 = *reinterpret_cast<const float4*>(smem + cur * BUF + NK * 1024 + (lane & 15) * 16);
       const float4 hq1 = *reinterpret_cast<const float4*>(smem + cur * BUF + NK * 1024 + (16 + (lane & 15)) * 16);
+      // (all four fields kept live, so each header is ONE conflict-free ds_read_b128: left alone the compiler reads
+      // the three it uses as ds_read_b64 + ds_read_b32, and ds_read_b32 banks are dword mod 32 -- lanes j and j + 8 of
+      // a group then collide, 2 extra LDS cycles per header read: r03b's 13.2M SQ_LDS_BANK_CONFLICT cycles)
+      asm volatile("" ::"v"(hq0.z), "v"(hq1.z));
       // signal the next tile: this wave's reads of this one are done (lgkmcnt(0): the headers are in) and
       // its DMA pieces of the next have landed -- vmcnt counts, in issue order, only the next item's rows
       // issued after its last piece beyond them
@@ -891,58 +895,101 @@ size_t rs_bucket_tmp_bytes(int nq, int n_waves) {
          scan_tmp_bytes(nq + 1) + 64;
 }
 
-template <int METRIC>
-static hipError_t rs_bucket_m(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
-                              const float4* qhdr, const float* row_norms, int64_t* cand_off, float* cand_key,
-                              int* cand_pos, int64_t* qcnt, int* fill, void* stmp, hipStream_t s) {
-  hipError_t e;
-  // the streams come from K13's 8 item queues (n_waves = 8 queues x P workgroups x kRsWaves) and a batch's
-  // bins fit LDS (K13 batches are at most kRsMaxBatch = kRsLdsMaxQ queries); J = workgroups of a queue per group
+// J: K13 workgroups per bucketing group (MIVS_RS_BUCKET_J, A/B runs: fewer means more groups and more global atomics
+// per query, more means fewer, longer groups); the streams come from K13's 8 item queues (n_waves = 8 queues x P
+// workgroups x kRsWaves) and a batch's bins fit LDS (K13 batches are at most kRsMaxBatch = kRsLdsMaxQ queries)
+static int rs_bucket_groups(int n_waves, int nq, int* J_out) {
   const int P = n_waves / (8 * kRsWaves);
-  if (!(nq <= kRsLdsMaxQ && n_waves == 8 * kRsWaves * P && P > 0)) return hipErrorInvalidValue;
-  // J: K13 workgroups per bucketing group (MIVS_RS_BUCKET_J, A/B runs: fewer means more groups and more global
-  // atomics per query, more means fewer, longer groups)
+  if (!(nq <= kRsLdsMaxQ && n_waves == 8 * kRsWaves * P && P > 0)) return 0;
   const char* je = getenv("MIVS_RS_BUCKET_J");
   const int jw = je ? atoi(je) : 1;
-  const int J = (jw >= 4 && P % 4 == 0) ? 4 : (jw >= 2 && P % 2 == 0) ? 2 : 1;
-  {
-    const size_t lds = sizeof(int) * (size_t)nq;
-    static const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rs_count_lds<METRIC>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                     (int)(sizeof(int) * kRsLdsMaxQ));
-    static const hipError_t a2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rs_scatter_lds<METRIC>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                     (int)(sizeof(int) * kRsLdsMaxQ));
-    if (a1 != hipSuccess) return a1;
-    if (a2 != hipSuccess) return a2;
-    const unsigned nb = (unsigned)(8 * (P / J));
-    hipLaunchKernelGGL(k_rs_count_lds<METRIC>, dim3(nb), dim3(1024), lds, s, wave_buf, wave_cap, wave_cnt, J, nq, qhdr,
-                       row_norms, reinterpret_cast<unsigned long long*>(qcnt));
-    e = launch_exclusive_scan_i64(qcnt, cand_off, nq + 1, stmp, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_rs_scatter_lds<METRIC>, dim3(nb), dim3(1024), lds, s, wave_buf, wave_cap, wave_cnt, J, nq,
-                       qhdr, row_norms, cand_off, fill, cand_key, cand_pos);
-    return hipGetLastError();
-  }
+  *J_out = (jw >= 4 && P % 4 == 0) ? 4 : (jw >= 2 && P % 2 == 0) ? 2 : 1;
+  return 8 * (P / *J_out);
+}
+
+template <int METRIC>
+static hipError_t rs_bucket_count_m(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
+                                    const float4* qhdr, const float* row_norms, int64_t* cand_off, int64_t* qcnt,
+                                    void* stmp, hipStream_t s) {
+  int J = 1;
+  const int nb = rs_bucket_groups(n_waves, nq, &J);
+  if (nb == 0) return hipErrorInvalidValue;
+  static const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rs_count_lds<METRIC>),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   (int)(sizeof(int) * kRsLdsMaxQ));
+  if (a1 != hipSuccess) return a1;
+  hipLaunchKernelGGL(k_rs_count_lds<METRIC>, dim3((unsigned)nb), dim3(1024), sizeof(int) * (size_t)nq, s, wave_buf,
+                     wave_cap, wave_cnt, J, nq, qhdr, row_norms, reinterpret_cast<unsigned long long*>(qcnt));
+  return launch_exclusive_scan_i64(qcnt, cand_off, nq + 1, stmp, s);
+}
+
+template <int METRIC>
+static hipError_t rs_bucket_scatter_m(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
+                                      const float4* qhdr, const float* row_norms, const int64_t* cand_off,
+                                      float* cand_key, int* cand_pos, int* fill, hipStream_t s) {
+  int J = 1;
+  const int nb = rs_bucket_groups(n_waves, nq, &J);
+  if (nb == 0) return hipErrorInvalidValue;
+  static const hipError_t a2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rs_scatter_lds<METRIC>),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   (int)(sizeof(int) * kRsLdsMaxQ));
+  if (a2 != hipSuccess) return a2;
+  hipLaunchKernelGGL(k_rs_scatter_lds<METRIC>, dim3((unsigned)nb), dim3(1024), sizeof(int) * (size_t)nq, s, wave_buf,
+                     wave_cap, wave_cnt, J, nq, qhdr, row_norms, cand_off, fill, cand_key, cand_pos);
+  return hipGetLastError();
+}
+
+// the temporaries of the bucketing inside tmp: qcnt [nq + 1], fill [nq], woff [n_waves + 1], the scan's
+struct RsBucketTmp {
+  int64_t* qcnt;
+  int* fill;
+  int64_t* woff;
+  void* stmp;
+};
+static RsBucketTmp rs_bucket_tmp(void* tmp, int nq, int n_waves) {
+  RsBucketTmp t;
+  t.qcnt = static_cast<int64_t*>(tmp);
+  t.fill = reinterpret_cast<int*>(t.qcnt + nq + 1);
+  t.woff = reinterpret_cast<int64_t*>(
+      reinterpret_cast<char*>(tmp) + ((sizeof(int64_t) * ((size_t)nq + 1) + sizeof(int) * (size_t)nq + 15) & ~(size_t)15));
+  t.stmp = reinterpret_cast<char*>(t.woff) + ((sizeof(int64_t) * ((size_t)n_waves + 1) + 15) & ~(size_t)15);
+  return t;
+}
+
+hipError_t launch_rs_bucket_count(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
+                                  const float4* qhdr, const float* row_norms, int metric, int64_t* cand_off, void* tmp,
+                                  int* lost, hipStream_t s) {
+  const RsBucketTmp t = rs_bucket_tmp(tmp, nq, n_waves);
+  hipError_t e = hipMemsetAsync(t.qcnt, 0, sizeof(int64_t) * ((size_t)nq + 1) + sizeof(int) * (size_t)nq, s);
+  if (e != hipSuccess) return e;
+  if (n_waves <= 0) return launch_exclusive_scan_i64(t.qcnt, cand_off, nq + 1, t.stmp, s);
+  hipLaunchKernelGGL(k_rs_stream_off, dim3(1), dim3(1024), 0, s, wave_cnt, n_waves, wave_cap, t.woff, lost);
+  return metric == kIP ? rs_bucket_count_m<kIP>(wave_buf, wave_cap, wave_cnt, n_waves, nq, qhdr, row_norms, cand_off,
+                                                t.qcnt, t.stmp, s)
+                       : rs_bucket_count_m<kL2>(wave_buf, wave_cap, wave_cnt, n_waves, nq, qhdr, row_norms, cand_off,
+                                                t.qcnt, t.stmp, s);
+}
+
+hipError_t launch_rs_bucket_scatter(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
+                                    const float4* qhdr, const float* row_norms, int metric, const int64_t* cand_off,
+                                    float* cand_key, int* cand_pos, void* tmp, hipStream_t s) {
+  if (n_waves <= 0) return hipSuccess;
+  const RsBucketTmp t = rs_bucket_tmp(tmp, nq, n_waves);
+  return metric == kIP ? rs_bucket_scatter_m<kIP>(wave_buf, wave_cap, wave_cnt, n_waves, nq, qhdr, row_norms, cand_off,
+                                                  cand_key, cand_pos, t.fill, s)
+                       : rs_bucket_scatter_m<kL2>(wave_buf, wave_cap, wave_cnt, n_waves, nq, qhdr, row_norms, cand_off,
+                                                  cand_key, cand_pos, t.fill, s);
 }
 
 hipError_t launch_rs_bucket(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
                             const float4* qhdr, const float* row_norms, int metric, int64_t* cand_off,
                             float* cand_key, int* cand_pos, void* tmp, int* lost, int grid, hipStream_t s) {
-  int64_t* qcnt = static_cast<int64_t*>(tmp);
-  int* fill = reinterpret_cast<int*>(qcnt + nq + 1);
-  int64_t* woff = reinterpret_cast<int64_t*>(
-      reinterpret_cast<char*>(tmp) + ((sizeof(int64_t) * ((size_t)nq + 1) + sizeof(int) * (size_t)nq + 15) & ~(size_t)15));
-  void* stmp = reinterpret_cast<char*>(woff) + ((sizeof(int64_t) * ((size_t)n_waves + 1) + 15) & ~(size_t)15);
-  hipError_t e = hipMemsetAsync(qcnt, 0, sizeof(int64_t) * ((size_t)nq + 1) + sizeof(int) * (size_t)nq, s);
-  if (e != hipSuccess) return e;
-  if (n_waves <= 0) return launch_exclusive_scan_i64(qcnt, cand_off, nq + 1, stmp, s);
-  hipLaunchKernelGGL(k_rs_stream_off, dim3(1), dim3(1024), 0, s, wave_cnt, n_waves, wave_cap, woff, lost);
   (void)grid;
-  return metric == kIP ? rs_bucket_m<kIP>(wave_buf, wave_cap, wave_cnt, n_waves, nq, qhdr, row_norms, cand_off, cand_key,
-                                          cand_pos, qcnt, fill, stmp, s)
-                       : rs_bucket_m<kL2>(wave_buf, wave_cap, wave_cnt, n_waves, nq, qhdr, row_norms, cand_off, cand_key,
-                                          cand_pos, qcnt, fill, stmp, s);
+  hipError_t e = launch_rs_bucket_count(wave_buf, wave_cap, wave_cnt, n_waves, nq, qhdr, row_norms, metric, cand_off,
+                                        tmp, lost, s);
+  if (e != hipSuccess) return e;
+  return launch_rs_bucket_scatter(wave_buf, wave_cap, wave_cnt, n_waves, nq, qhdr, row_norms, metric, cand_off,
+                                  cand_key, cand_pos, tmp, s);
 }
 
 // the smallest row norm of every group (K13's filter bound; pad rows are +inf, every group has a real row)

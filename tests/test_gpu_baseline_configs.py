@@ -144,6 +144,34 @@ def test_config2_ivf_10m_oracle_on_query_sample(ivf_10m):
     np.testing.assert_array_equal(_bits(d.cpu().numpy()), _bits(od))
 
 
+def test_config2_ivf_10m_large_k_equals_exact_all_queries_and_oracle_sample(ivf_10m):
+    """the reference's top_k = 2000 (improved_multi_gpu_rag.py:40,247) at configs[2]: K13 + K16 on
+    all 10k queries bit-equal to the exact fp32 path (K3 DUMP + K8), and a query sample bit-equal to the oracle"""
+    from mivs.neighbors import ivf_flat
+
+    x, q, idx = ivf_10m
+    sp = ivf_flat.SearchParams(n_probes=32)
+    k = 2000
+    d_pf, i_pf = ivf_flat.search(sp, idx, q, k)
+    st = idx.last_search_stats()
+    assert st["prefilter"] == 1 and st["scan_kernel"] == 13 and st["n_queries"] == 10_000, st
+    assert st["overflow_queries"] <= 100, st  # (the sample's margin: unproven queries take the exact scan)
+    idx.set_prefilter(False)
+    try:
+        d_ex, i_ex = ivf_flat.search(sp, idx, q, k)
+        assert idx.last_search_stats()["prefilter"] == 0
+    finally:
+        idx.set_prefilter(True)
+    np.testing.assert_array_equal(i_pf.cpu().numpy(), i_ex.cpu().numpy())
+    np.testing.assert_array_equal(_bits(d_pf.cpu().numpy()), _bits(d_ex.cpu().numpy()))
+    s = _sample(q.shape[0], 12, 5)
+    xh = x.cpu().numpy()
+    od, oi, _ = O.ivf_search(xh, idx.centers.cpu().numpy(), idx.list_sizes.numpy(), idx.list_ids().cpu().numpy(),
+                             q.cpu().numpy()[s], 32, k)
+    np.testing.assert_array_equal(i_pf.cpu().numpy()[s], oi)
+    np.testing.assert_array_equal(_bits(d_pf.cpu().numpy()[s]), _bits(od))
+
+
 def _labels_of(idx, n):
     """row -> list from the index's list order (ids are row numbers: ids_offset 0)."""
     sizes = idx.list_sizes.numpy()
