@@ -94,7 +94,7 @@ struct Workspace {
   // per-list query counts of the last search's own probe map (an exact fallback re-maps its queries)
   Buf stat_counts, rs_ovf_q, rs_ovf_rows, rs_ovf_d, rs_ovf_i, rs_items;
   // K16 large-k: T_q's sample probes and selection, the per-query windows and K16r's work items
-  Buf lk_probes, lk_sel, lk_sel_i, lk_win_pos, lk_win_key, lk_win_n, lk_chunks, lk_chunk_off;
+  Buf lk_probes, lk_win_pos, lk_win_key, lk_win_n, lk_chunks, lk_chunk_off;
 };
 
 // hipEvent pairs recorded on the caller's stream around the pipeline stages of
@@ -1088,7 +1088,7 @@ int64_t lk_batch(const mivs_index_s* idx, int64_t nq, int k, int np) {
 }
 
 // K16 step 1: T_q per query into ws.pre_kth from an exact scan of the sample (K3 DUMP over the
-// split lists 2l = the sample of list l, + K8 top r_max by (key, id)) and the sample's r_q-th key (k_lk_rank)
+// split lists 2l = the sample of list l) and the sample's r_q-th key (k_lk_sample_kth)
 void lk_prepass(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, const LkPlan& p) {
   Workspace& ws = idx->ws;
   const ListSet& L = idx->lists;
@@ -1124,24 +1124,10 @@ void lk_prepass(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, in
   j.goff = ws.pre_goff.as<int64_t>();
   j.n_lists = nl2;
   run_scan(j, idx->device, ws, s);
-  ws.lk_sel.reserve(sizeof(float) * (size_t)nq * p.r_max);
-  ws.lk_sel_i.reserve(sizeof(int64_t) * (size_t)nq * p.r_max);
-  SelectArgs sa{};
-  sa.keys = ws.part_d.as<float>();
-  sa.row_ids = L.ids.as<int64_t>();
-  sa.slot_info = ws.part_i.as<int64_t>();
-  sa.slot_begin = ws.slot_begin.as<int64_t>();
-  sa.slot_rows = (int)slot_rows;
-  sa.nq = nq;
-  sa.k = p.r_max;
-  sa.metric = idx->metric;
-  sa.out_d = ws.lk_sel.as<float>();
-  sa.out_i = ws.lk_sel_i.as<int64_t>();
-  HIPCHK(launch_select(sa, s));
   ws.pre_kth.reserve(sizeof(float) * nq);
-  HIPCHK(launch_lk_rank(ws.probes_full.as<int64_t>(), nq, np, L.off.as<int64_t>(), ws.pre_goff.as<int64_t>(), k,
-                        kLkSampleZ, ws.lk_sel.as<float>(), p.r_max, idx->metric == kIP ? 1 : 0, ws.pre_kth.as<float>(),
-                        s));
+  HIPCHK(launch_lk_sample_kth(ws.probes_full.as<int64_t>(), nq, np, L.off.as<int64_t>(), ws.pre_goff.as<int64_t>(), k,
+                              kLkSampleZ, ws.part_d.as<float>(), ws.part_i.as<int64_t>(), ws.slot_begin.as<int64_t>(),
+                              (int)slot_rows, ws.pre_kth.as<float>(), s));
   // the fp16 queries, their scales and residuals for the headers and tiles
   ws.qh.reserve(sizeof(uint16_t) * (size_t)nq * idx->dp);
   ws.qscale.reserve(sizeof(float) * nq);
@@ -1216,7 +1202,7 @@ void lk_finish(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   HIPCHK(launch_lk_chunks(a.win_n, nq, ws.lk_chunks.as<int64_t>(), s));
   ws.scan_tmp.reserve(scan_tmp_bytes(nq + 1));
   HIPCHK(launch_exclusive_scan_i64(ws.lk_chunks.as<int64_t>(), ws.lk_chunk_off.as<int64_t>(), nq + 1, ws.scan_tmp.p, s));
-  HIPCHK(launch_lk_recompute(a, 8 * cu_count(idx->device), s));
+  HIPCHK(launch_lk_recompute(a, cu_count(idx->device), s));
   HIPCHK(launch_lk_sort(a, s));
   int64_t h[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(h, ws.pf_stats.p, 16, hipMemcpyDeviceToHost, s));

@@ -7,15 +7,15 @@
 // So the pipeline TRIES a threshold and PROVES each query's answer at run time:
 //
 //   1. T_q: a uniform sample of the probed rows (the first 1/div of every probed list; rows of a list are in
-//      no particular order) scanned exactly (K3 DUMP + K8); the sample's r_q-th key, r_q = mu + z sqrt(mu) + 1
-//      with mu = k n_sample / n_probed, lies above the k-th probed key with high probability (k_lk_rank);
+//      no particular order) scanned exactly (K3 DUMP); the sample's r_q-th key, r_q = mu + z sqrt(mu) + 1
+//      with mu = k n_sample / n_probed, lies above the k-th probed key with high probability (k_lk_sample_kth);
 //   2. K13 streams every row whose approximate key may be <= T_q (the k <= 16 path's scan, unchanged);
 //   3. K16w (k_lk_window): per query the k-th smallest approximate key Ak of its candidates, the refine
 //      window T = Ak + 2 delta (pf_window), and the proof: at least k candidates and T <= T_q, so every row
 //      whose pinned key can reach the top-k is a candidate (the k <= 16 path's K11 argument). The window's
 //      row positions go to a fixed per-query capacity; a query that fails the proof goes to the exact scan;
-//   4. K16r (k_lk_recompute): the pinned fp32 key of every window row (oracle orc_dot's order), one lane per
-//      row, the query in scalar registers, the row read from the row-major fp32 copy -- the gather of
+//   4. K16r (k_lk_recompute_rm): the pinned fp32 key of every window row (oracle orc_dot's order), one lane per
+//      row, the rows gathered from the row-major fp32 copy by LDS-DMA in 64-dim chunks -- the gather of
 //      ~(k + window) x d x 4 bytes per query is the step's floor;
 //   5. K16s (k_lk_sort): per query a bitonic sort of the window by (key, id) in LDS; the first k are the answer.
 #include <climits>
@@ -46,35 +46,6 @@ __global__ void k_lk_sample_probes(const int64_t* __restrict__ probes, int64_t n
   out[i] = p < 0 ? p : 2 * p;
 }
 
-// T_q's key per query: the r_q-th smallest exact key of the sample (sel: the sample's top r_max by (key, id), K8
-// output distances), or +inf when the sample cannot reach it (then every probed row is a candidate)
-__global__ void k_lk_rank(const int64_t* __restrict__ probes, int64_t nq, int np, const int64_t* __restrict__ list_off,
-                          const int64_t* __restrict__ goff2, int k, float z, const float* __restrict__ sel, int r_max,
-                          int ip, float* __restrict__ kth) {
-  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= nq) return;
-  double n_all = 0.0, n_smp = 0.0;
-  for (int p = 0; p < np; ++p) {
-    const int64_t l = probes[q * np + p];
-    if (l < 0) continue;
-    const double nl = (double)(list_off[l + 1] - list_off[l]);
-    const double ns = (double)(goff2[2 * l + 1] - goff2[2 * l]) * kGroupRows;
-    n_all += nl;
-    n_smp += ns < nl ? ns : nl;
-  }
-  float out = INFINITY;
-  if (n_all > (double)k && n_smp > 0.0) {
-    const double mu = (double)k * n_smp / n_all;
-    const double r = ceil(mu + (double)z * sqrt(mu) + 1.0);
-    if (r <= (double)r_max && r <= n_smp) {
-      const float v = sel[q * r_max + (int64_t)r - 1];
-      out = ip ? -v : v;  // (K8 reports the inner product for IP; the key is its negation)
-      if (!(out < INFINITY) || out != out) out = INFINITY;
-    }
-  }
-  kth[q] = out;
-}
-
 // block-wide exclusive scan of one int per thread (kLkThreads threads); returns the prefix, *tot the sum
 __device__ __forceinline__ int lk_block_scan(int v, int* sh, int* tot) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -98,6 +69,104 @@ __device__ __forceinline__ int lk_block_scan(int v, int* sh, int* tot) {
   return base + x - v;
 }
 
+// the kk-th smallest orderable key among n values produced by key_at(i) (i < n), kk in [1, n], by three LDS histogram
+// digits of 11 / 11 / 10 bits (one workgroup of kLkThreads; every thread calls it)
+template <typename F>
+__device__ __forceinline__ uint32_t lk_select(int n, int kk, F&& key_at, int* s_hist, int* s_sh, uint32_t* s_sel) {
+  const int tid = threadIdx.x;
+  uint32_t prefix = 0, pmask = 0;
+  const int shifts[3] = {21, 10, 0};
+  const int widths[3] = {11, 11, 10};
+#pragma unroll 1
+  for (int d = 0; d < 3; ++d) {
+    const int sh = shifts[d], nb = 1 << widths[d];
+    for (int i = tid; i < nb; i += kLkThreads) s_hist[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += kLkThreads) {
+      const uint32_t u = key_at(i);
+      if ((u & pmask) == prefix) atomicAdd(s_hist + ((u >> sh) & (nb - 1)), 1);
+    }
+    __syncthreads();
+    // the bin holding the kk-th: per-thread sums of nb / kLkThreads consecutive bins, then a scan
+    const int per = nb / kLkThreads;
+    int cs = 0;
+    for (int j = 0; j < per; ++j) cs += s_hist[tid * per + j];
+    int tot;
+    const int ex = lk_block_scan(cs, s_sh, &tot);
+    if (ex < kk && kk <= ex + cs) {
+      int c = ex;
+      for (int j = 0; j < per; ++j) {
+        const int h = s_hist[tid * per + j];
+        if (c + h >= kk) {
+          s_sel[0] = (uint32_t)(tid * per + j);
+          s_sel[1] = (uint32_t)(kk - c);
+          break;
+        }
+        c += h;
+      }
+    }
+    __syncthreads();
+    prefix |= s_sel[0] << sh;
+    pmask |= (uint32_t)(nb - 1) << sh;
+    kk = (int)s_sel[1];
+    __syncthreads();
+  }
+  return prefix;
+}
+
+// T_q's key per query straight from the sample's DUMP slots (K3: raw keys [slot][slot_rows], slot_info = (first row,
+// rows), pad rows +inf): the r_q-th smallest (one workgroup per query; replaces a K8 top-r_max + k_lk_rank)
+__global__ __launch_bounds__(kLkThreads) void k_lk_sample_kth(const int64_t* __restrict__ probes, int np,
+                                                              const int64_t* __restrict__ list_off,
+                                                              const int64_t* __restrict__ goff2, int k, float z,
+                                                              const float* __restrict__ keys,
+                                                              const int64_t* __restrict__ slot_info,
+                                                              const int64_t* __restrict__ slot_begin, int slot_rows,
+                                                              float* __restrict__ kth) {
+  __shared__ int s_hist[kLkBins];
+  __shared__ int s_sh[kLkThreads / 64];
+  __shared__ uint32_t s_sel[2];
+  __shared__ int s_cum[kLkMaxSampleSlots + 1];
+  const int64_t q = blockIdx.x;
+  const int tid = threadIdx.x;
+  double n_all = 0.0, n_smp = 0.0;
+  for (int p = 0; p < np; ++p) {
+    const int64_t l = probes[q * np + p];
+    if (l < 0) continue;
+    const double nl = (double)(list_off[l + 1] - list_off[l]);
+    const double ns = (double)(goff2[2 * l + 1] - goff2[2 * l]) * kGroupRows;
+    n_all += nl;
+    n_smp += ns < nl ? ns : nl;
+  }
+  const int64_t s0 = slot_begin[q], ns_slots = slot_begin[q + 1] - s0;
+  float out = INFINITY;
+  if (n_all > (double)k && n_smp > 0.0 && ns_slots <= kLkMaxSampleSlots) {
+    const double mu = (double)k * n_smp / n_all;
+    const double r = ceil(mu + (double)z * sqrt(mu) + 1.0);
+    if (r <= n_smp) {
+      // the query's keys as one flat range over its slots (a prefix of the slots' row counts)
+      if (tid == 0) {
+        int c = 0;
+        for (int64_t t = 0; t < ns_slots; ++t) {
+          s_cum[t] = c;
+          c += (int)slot_info[2 * (s0 + t) + 1];
+        }
+        s_cum[ns_slots] = c;
+      }
+      __syncthreads();
+      const int n = s_cum[ns_slots];
+      auto key_at = [&](int i) {
+        int t = 0;
+        while (s_cum[t + 1] <= i) ++t;  // (a few slots per query: a short LDS scan)
+        return lk_ord(keys[(s0 + t) * (int64_t)slot_rows + (i - s_cum[t])]);
+      };
+      if ((int)r <= n) out = lk_unord(lk_select(n, (int)r, key_at, s_hist, s_sh, s_sel));
+      if (!(out < INFINITY) || out != out) out = INFINITY;
+    }
+  }
+  if (tid == 0) kth[q] = out;
+}
+
 // K16w: one workgroup per query
 template <int METRIC>
 __global__ __launch_bounds__(kLkThreads) void k_lk_window(LkArgs a) {
@@ -113,49 +182,10 @@ __global__ __launch_bounds__(kLkThreads) void k_lk_window(LkArgs a) {
   const float qn = a.qnorms[q];
   const float delta = pf_delta<METRIC>(qn, a.qres[q], a.x_norm_max, a.x_res_max, a.dp);
   const bool lost = a.force_ovf && *a.force_ovf;
-  // 1. Ak = the k-th smallest approximate key (orderable bits, three digits of 11 / 11 / 10 bits); +inf with < k
+  // 1. Ak = the k-th smallest approximate key (orderable bits); +inf with fewer than k candidates
   uint32_t ans = 0xFFFFFFFFu;
-  if (n_c >= k && !lost) {
-    uint32_t prefix = 0, pmask = 0;
-    int kk = k;
-    const int shifts[3] = {21, 10, 0};
-    const int widths[3] = {11, 11, 10};
-#pragma unroll 1
-    for (int d = 0; d < 3; ++d) {
-      const int sh = shifts[d], nb = 1 << widths[d];
-      for (int i = tid; i < nb; i += kLkThreads) s_hist[i] = 0;
-      __syncthreads();
-      for (int i = tid; i < n_c; i += kLkThreads) {
-        const uint32_t u = lk_ord(a.cand_key[c0 + i]);
-        if ((u & pmask) == prefix) atomicAdd(s_hist + ((u >> sh) & (nb - 1)), 1);
-      }
-      __syncthreads();
-      // the bin holding the kk-th: per-thread sums of nb / kLkThreads consecutive bins, then a scan
-      const int per = nb / kLkThreads;
-      int cs = 0;
-      for (int j = 0; j < per; ++j) cs += s_hist[tid * per + j];
-      int tot;
-      const int ex = lk_block_scan(cs, s_sh, &tot);
-      if (ex < kk && kk <= ex + cs) {
-        int c = ex;
-        for (int j = 0; j < per; ++j) {
-          const int h = s_hist[tid * per + j];
-          if (c + h >= kk) {
-            s_sel[0] = (uint32_t)(tid * per + j);
-            s_sel[1] = (uint32_t)(kk - c);
-            break;
-          }
-          c += h;
-        }
-      }
-      __syncthreads();
-      prefix |= s_sel[0] << sh;
-      pmask |= (uint32_t)(nb - 1) << sh;
-      kk = (int)s_sel[1];
-      __syncthreads();
-    }
-    ans = prefix;
-  }
+  if (n_c >= k && !lost)
+    ans = lk_select(n_c, k, [&](int i) { return lk_ord(a.cand_key[c0 + i]); }, s_hist, s_sh, s_sel);
   const float Ak = ans == 0xFFFFFFFFu ? INFINITY : lk_unord(ans);
   const float T = Ak < INFINITY ? pf_window(Ak, delta) : INFINITY;
   // 2. the proof: every row whose pinned key can reach the top-k has approximate key <= T; the candidates hold
@@ -257,6 +287,96 @@ __global__ __launch_bounds__(256) void k_lk_recompute(LkArgs a) {
   }
 }
 
+// K16r from the row-major copy: the same keys, the rows gathered by LDS-DMA. A wave's 64 window rows arrive in
+// 64-dim chunks: DMA instruction t writes rows 4t .. 4t + 3 (256 B each, 1 KiB contiguous in LDS); lane L fetches
+// piece (L & 15) ^ (r & 15) of row r = 4t + (L >> 4), so each instruction reads 4 whole 256-B row segments (full
+// cache lines, not 64 scattered 16-B pieces) and piece p of row r sits at slot p ^ (r & 15): lane r's reads of
+// its own row (piece p for every lane at once) fall on 16 different slots -- conflict-free ds_read_b128. The
+// query (zero past d) is staged once per run of items of the same query. No barriers: every wave owns its LDS.
+constexpr int kLkRmWaves = 4;
+__device__ __forceinline__ void lk_glds16(const float* src, float* lds) {
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src), (lds_ptr_t)(lds), 16, 0, 0);
+}
+
+template <int METRIC>
+__global__ __launch_bounds__(64 * kLkRmWaves) void k_lk_recompute_rm(LkArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lk_smem[];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int dp = a.dp;
+  float* const rbuf = lk_smem + (size_t)wv * (64 * 64 + dp);  // [64 rows][64 dims], swizzled 16-B pieces
+  float* const qbuf = rbuf + 64 * 64;                           // the query, dp floats
+  const int64_t n_items = a.chunk_off[a.nq];
+  const int64_t n_waves = (int64_t)gridDim.x * kLkRmWaves;
+  const int nch = dp >> 6;
+  int64_t q_staged = -1;
+  for (int64_t w = (int64_t)blockIdx.x * kLkRmWaves + wv; w < n_items; w += n_waves) {
+    int64_t lo = 0, hi = a.nq - 1;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (a.chunk_off[mid] <= w) lo = mid; else hi = mid - 1;
+    }
+    const int64_t q = __builtin_amdgcn_readfirstlane((int)lo);
+    const int j = (int)(w - a.chunk_off[q]);
+    const int i = 64 * j + lane;
+    const int n_w = a.win_n[q];
+    const bool live = i < n_w;
+    const int pos = live ? a.win_pos[q * a.cap + i] : 0;
+    if (q != q_staged) {  // the query into LDS, zero past d (16-B pieces, register-staged: d may not be 4-aligned)
+      const float* qv = a.queries + q * a.d;
+      for (int c = 4 * lane; c < dp; c += 256) {
+        float4 v;
+        v.x = c + 0 < a.d ? qv[c + 0] : 0.0f;
+        v.y = c + 1 < a.d ? qv[c + 1] : 0.0f;
+        v.z = c + 2 < a.d ? qv[c + 2] : 0.0f;
+        v.w = c + 3 < a.d ? qv[c + 3] : 0.0f;
+        *reinterpret_cast<float4*>(qbuf + c) = v;
+      }
+      q_staged = q;
+    }
+    // the source of DMA instruction t for this lane: row 4 t + (lane >> 4), piece (lane & 15) ^ (row & 15)
+    const float* rowp = a.rows_rm + (int64_t)pos * dp;
+    const float* src[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int r = 4 * t + (lane >> 4);
+      const uint64_t b = (uint64_t)__shfl((long long)(uintptr_t)rowp, r);
+      src[t] = reinterpret_cast<const float*>(b) + 4 * ((lane & 15) ^ (r & 15));
+    }
+    float acc = 0.0f;
+    for (int c = 0; c < nch; ++c) {
+#pragma unroll
+      for (int t = 0; t < 16; ++t) lk_glds16(src[t] + 64 * c, rbuf + t * 256);
+      __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): this chunk landed (and the query's writes)
+      const float* myrow = rbuf + lane * 64;
+      const float* qc = qbuf + 64 * c;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const float4 x0 = *reinterpret_cast<const float4*>(myrow + 4 * ((2 * b) ^ (lane & 15)));
+        const float4 x1 = *reinterpret_cast<const float4*>(myrow + 4 * ((2 * b + 1) ^ (lane & 15)));
+        const float4 y0 = *reinterpret_cast<const float4*>(qc + 8 * b);
+        const float4 y1 = *reinterpret_cast<const float4*>(qc + 8 * b + 4);
+        acc = fmaf(x0.x, y0.x, acc); acc = fmaf(x1.x, y1.x, acc);
+        acc = fmaf(x0.y, y0.y, acc); acc = fmaf(x1.y, y1.y, acc);
+        acc = fmaf(x0.z, y0.z, acc); acc = fmaf(x1.z, y1.z, acc);
+        acc = fmaf(x0.w, y0.w, acc); acc = fmaf(x1.w, y1.w, acc);
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the chunk's reads done before the next DMA overwrites it
+    }
+    if (live) {
+      float P;
+      if (METRIC == kL2) {
+        const float v = fmaf(-2.0f, acc, a.row_norms[pos] + a.qnorms[q]);
+        P = v > 0.0f ? v : 0.0f;
+      } else {
+        P = -acc;
+      }
+      a.win_key[q * a.cap + i] = P;
+    }
+  }
+}
+
 // (key, id) order with the id looked up only for equal keys (rare: duplicate rows)
 __device__ __forceinline__ bool lk_less(float ka, int pa, float kb, int pb, const int64_t* __restrict__ row_ids) {
   if (ka != kb) return ka < kb;
@@ -338,11 +458,12 @@ hipError_t launch_lk_sample_probes(const int64_t* probes, int64_t n, int64_t* ou
   return hipGetLastError();
 }
 
-hipError_t launch_lk_rank(const int64_t* probes, int64_t nq, int np, const int64_t* list_off, const int64_t* goff2,
-                          int k, float z, const float* sel, int r_max, int ip, float* kth, hipStream_t s) {
+hipError_t launch_lk_sample_kth(const int64_t* probes, int64_t nq, int np, const int64_t* list_off, const int64_t* goff2,
+                                int k, float z, const float* keys, const int64_t* slot_info, const int64_t* slot_begin,
+                                int slot_rows, float* kth, hipStream_t s) {
   if (nq <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_lk_rank, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, s, probes, nq, np, list_off, goff2, k,
-                     z, sel, r_max, ip, kth);
+  hipLaunchKernelGGL(k_lk_sample_kth, dim3((unsigned)nq), dim3(kLkThreads), 0, s, probes, np, list_off, goff2, k, z,
+                     keys, slot_info, slot_begin, slot_rows, kth);
   return hipGetLastError();
 }
 
@@ -359,10 +480,26 @@ hipError_t launch_lk_chunks(const int* win_n, int64_t nq, int64_t* chunks, hipSt
   return hipGetLastError();
 }
 
-hipError_t launch_lk_recompute(const LkArgs& a, int grid, hipStream_t s) {
+hipError_t launch_lk_recompute(const LkArgs& a, int cus, hipStream_t s) {
   if (a.nq <= 0) return hipSuccess;
-  if (a.metric == kIP) hipLaunchKernelGGL(k_lk_recompute<kIP>, dim3((unsigned)grid), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(k_lk_recompute<kL2>, dim3((unsigned)grid), dim3(256), 0, s, a);
+  const char* e = getenv("MIVS_LK_GATHER");
+  if (a.rows_rm && a.dp % 64 == 0 && a.dp <= 1024 && !(e && e[0] == '0')) {
+    // two workgroups of 4 waves per CU: 8 waves x 16 KiB of rows in flight
+    const size_t lds = sizeof(float) * (size_t)kLkRmWaves * (64 * 64 + a.dp);
+    static const hipError_t a0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lk_recompute_rm<kL2>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    static const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lk_recompute_rm<kIP>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    if (a0 != hipSuccess) return a0;
+    if (a1 != hipSuccess) return a1;
+    const dim3 g((unsigned)(2 * cus));  // persistent: every workgroup resident
+    if (a.metric == kIP) hipLaunchKernelGGL(k_lk_recompute_rm<kIP>, g, dim3(64 * kLkRmWaves), lds, s, a);
+    else hipLaunchKernelGGL(k_lk_recompute_rm<kL2>, g, dim3(64 * kLkRmWaves), lds, s, a);
+    return hipGetLastError();
+  }
+  const dim3 g((unsigned)(8 * cus));
+  if (a.metric == kIP) hipLaunchKernelGGL(k_lk_recompute<kIP>, g, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(k_lk_recompute<kL2>, g, dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

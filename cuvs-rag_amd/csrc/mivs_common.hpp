@@ -297,11 +297,14 @@ struct LkArgs {
 };
 int lk_cap(int k);
 hipError_t launch_lk_sample_probes(const int64_t* probes, int64_t n, int64_t* out, hipStream_t s);
-hipError_t launch_lk_rank(const int64_t* probes, int64_t nq, int np, const int64_t* list_off, const int64_t* goff2,
-                          int k, float z, const float* sel, int r_max, int ip, float* kth, hipStream_t s);
+constexpr int kLkMaxSampleSlots = 1024;  // K3 DUMP slots of one query's sample (more: T_q = +inf)
+// T_q's key per query: the r_q-th smallest key of the sample's DUMP slots (r_q from the binomial margin)
+hipError_t launch_lk_sample_kth(const int64_t* probes, int64_t nq, int np, const int64_t* list_off, const int64_t* goff2,
+                                int k, float z, const float* keys, const int64_t* slot_info, const int64_t* slot_begin,
+                                int slot_rows, float* kth, hipStream_t s);
 hipError_t launch_lk_window(const LkArgs& a, hipStream_t s);
 hipError_t launch_lk_chunks(const int* win_n, int64_t nq, int64_t* chunks, hipStream_t s);
-hipError_t launch_lk_recompute(const LkArgs& a, int grid, hipStream_t s);
+hipError_t launch_lk_recompute(const LkArgs& a, int cus, hipStream_t s);  // cus: the device's CUs
 hipError_t launch_lk_sort(const LkArgs& a, hipStream_t s);
 
 // K13a k-means assign on the row-stationary loop (assign.hip)
