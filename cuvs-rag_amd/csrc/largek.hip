@@ -69,10 +69,10 @@ __device__ __forceinline__ int lk_block_scan(int v, int* sh, int* tot) {
   return base + x - v;
 }
 
-// the kk-th smallest orderable key among n values produced by key_at(i) (i < n), kk in [1, n], by three LDS histogram
-// digits of 11 / 11 / 10 bits (one workgroup of kLkThreads; every thread calls it)
-template <typename F>
-__device__ __forceinline__ uint32_t lk_select(int n, int kk, F&& key_at, int* s_hist, int* s_sh, uint32_t* s_sel) {
+// the kk-th smallest orderable key among the values visit(f) hands to f (each thread its share), kk in [1, count],
+// by three LDS histogram digits of 11 / 11 / 10 bits (one workgroup of kLkThreads; every thread calls it)
+template <typename V>
+__device__ __forceinline__ uint32_t lk_select(int kk, V&& visit, int* s_hist, int* s_sh, uint32_t* s_sel) {
   const int tid = threadIdx.x;
   uint32_t prefix = 0, pmask = 0;
   const int shifts[3] = {21, 10, 0};
@@ -82,10 +82,9 @@ __device__ __forceinline__ uint32_t lk_select(int n, int kk, F&& key_at, int* s_
     const int sh = shifts[d], nb = 1 << widths[d];
     for (int i = tid; i < nb; i += kLkThreads) s_hist[i] = 0;
     __syncthreads();
-    for (int i = tid; i < n; i += kLkThreads) {
-      const uint32_t u = key_at(i);
+    visit([&](uint32_t u) {
       if ((u & pmask) == prefix) atomicAdd(s_hist + ((u >> sh) & (nb - 1)), 1);
-    }
+    });
     __syncthreads();
     // the bin holding the kk-th: per-thread sums of nb / kLkThreads consecutive bins, then a scan
     const int per = nb / kLkThreads;
@@ -155,12 +154,14 @@ __global__ __launch_bounds__(kLkThreads) void k_lk_sample_kth(const int64_t* __r
       }
       __syncthreads();
       const int n = s_cum[ns_slots];
-      auto key_at = [&](int i) {
-        int t = 0;
-        while (s_cum[t + 1] <= i) ++t;  // (a few slots per query: a short LDS scan)
-        return lk_ord(keys[(s0 + t) * (int64_t)slot_rows + (i - s_cum[t])]);
+      auto visit = [&](auto&& f) {
+        for (int64_t t = 0; t < ns_slots; ++t) {
+          const float* kb = keys + (s0 + t) * (int64_t)slot_rows;
+          const int nr = s_cum[t + 1] - s_cum[t];
+          for (int i = tid; i < nr; i += kLkThreads) f(lk_ord(kb[i]));
+        }
       };
-      if ((int)r <= n) out = lk_unord(lk_select(n, (int)r, key_at, s_hist, s_sh, s_sel));
+      if ((int)r <= n) out = lk_unord(lk_select((int)r, visit, s_hist, s_sh, s_sel));
       if (!(out < INFINITY) || out != out) out = INFINITY;
     }
   }
@@ -185,7 +186,8 @@ __global__ __launch_bounds__(kLkThreads) void k_lk_window(LkArgs a) {
   // 1. Ak = the k-th smallest approximate key (orderable bits); +inf with fewer than k candidates
   uint32_t ans = 0xFFFFFFFFu;
   if (n_c >= k && !lost)
-    ans = lk_select(n_c, k, [&](int i) { return lk_ord(a.cand_key[c0 + i]); }, s_hist, s_sh, s_sel);
+    ans = lk_select(k, [&](auto&& f) { for (int i = tid; i < n_c; i += kLkThreads) f(lk_ord(a.cand_key[c0 + i])); },
+                    s_hist, s_sh, s_sel);
   const float Ak = ans == 0xFFFFFFFFu ? INFINITY : lk_unord(ans);
   const float T = Ak < INFINITY ? pf_window(Ak, delta) : INFINITY;
   // 2. the proof: every row whose pinned key can reach the top-k has approximate key <= T; the candidates hold
@@ -377,19 +379,12 @@ __global__ __launch_bounds__(64 * kLkRmWaves) void k_lk_recompute_rm(LkArgs a) {
   }
 }
 
-// (key, id) order with the id looked up only for equal keys (rare: duplicate rows)
-__device__ __forceinline__ bool lk_less(float ka, int pa, float kb, int pb, const int64_t* __restrict__ row_ids) {
-  if (ka != kb) return ka < kb;
-  if (pa == pb) return false;
-  if (pa < 0 || pb < 0) return pb < 0 && pa >= 0;
-  return row_ids[pa] < row_ids[pb];
-}
-
-// K16s: one workgroup per query; bitonic sort of the window's (key, position) by (key, id) in LDS, the first k out
+// K16s: one workgroup per query; bitonic sort of the window's (key, id) pairs in LDS (the ids gathered once: exact
+// ties between distinct rows are common at this k, ~1e-7 apart in a dense bulk), the first k out
 template <int METRIC, int CAP>
 __global__ __launch_bounds__(kLkThreads) void k_lk_sort(LkArgs a) {
   __shared__ float s_k[CAP];
-  __shared__ int s_p[CAP];
+  __shared__ int64_t s_i[CAP];
   const int64_t q = blockIdx.x;
   const int n_w = a.win_n[q];
   if (n_w < 0) return;  // (the exact scan's answer is scattered in later)
@@ -398,7 +393,7 @@ __global__ __launch_bounds__(kLkThreads) void k_lk_sort(LkArgs a) {
   for (int i = threadIdx.x; i < N; i += kLkThreads) {
     const bool v = i < n_w;
     s_k[i] = v ? a.win_key[q * a.cap + i] : INFINITY;
-    s_p[i] = v ? a.win_pos[q * a.cap + i] : -1;
+    s_i[i] = v ? a.row_ids[a.win_pos[q * a.cap + i]] : LLONG_MAX;
   }
   __syncthreads();
   for (int size = 2; size <= N; size <<= 1) {
@@ -408,11 +403,12 @@ __global__ __launch_bounds__(kLkThreads) void k_lk_sort(LkArgs a) {
         const int hi = lo + stride;
         const bool up = (lo & size) == 0;
         const float kl = s_k[lo], kh = s_k[hi];
-        const int pl = s_p[lo], ph = s_p[hi];
-        const bool sw = up ? lk_less(kh, ph, kl, pl, a.row_ids) : lk_less(kl, pl, kh, ph, a.row_ids);
-        if (sw) {
+        const int64_t il = s_i[lo], ih = s_i[hi];
+        const bool h_lt = kh < kl || (kh == kl && ih < il);  // (key, id) of hi below lo's
+        const bool l_lt = kl < kh || (kl == kh && il < ih);
+        if (up ? h_lt : l_lt) {
           s_k[lo] = kh; s_k[hi] = kl;
-          s_p[lo] = ph; s_p[hi] = pl;
+          s_i[lo] = ih; s_i[hi] = il;
         }
       }
       __syncthreads();
@@ -422,7 +418,7 @@ __global__ __launch_bounds__(kLkThreads) void k_lk_sort(LkArgs a) {
     const bool v = i < n_w;
     const float P = v ? s_k[i] : INFINITY;
     a.out_d[q * a.k + i] = v ? (METRIC == kIP ? -P : P) : (METRIC == kIP ? -INFINITY : INFINITY);
-    a.out_i[q * a.k + i] = v ? a.row_ids[s_p[i]] : (int64_t)-1;
+    a.out_i[q * a.k + i] = v ? s_i[i] : (int64_t)-1;
   }
 }
 
