@@ -717,6 +717,7 @@ def main():
     _native.set_profiling(False)
     build_phases = idx.build_phases()
     build_vps = n * world / t_build
+    index_mem = idx.memory()  # one fp32 copy (64-B row blocks) + the fp16 and fp8 copies, all built in build()
     sizes = idx.list_sizes.numpy()
     rl(f"[build] {n * world} rows in {t_build:.2f} s -> {build_vps / 1e6:.2f} M vec/s; lists min/med/max "
        f"{sizes.min()}/{int(np.median(sizes))}/{sizes.max()}")
@@ -938,6 +939,8 @@ def main():
         "build_vectors_per_s": round(build_vps, 1),
         "build_s": round(t_build, 3),
         "build_phases_s": build_phases,
+        "index_bytes_per_row": round(index_mem["total_bytes"] / max(index_mem["n_rows"], 1), 1),
+        "index_memory": index_mem,
         "roofline": roof,
         "cpu_baseline": cpu,
         "search_stats": stats,

@@ -316,7 +316,7 @@ __global__ __launch_bounds__(kAsThreads, 1) void k_as_scan(AsScanArgs a) {
 __global__ __launch_bounds__(256) void k_as_ctiles(const float* __restrict__ groups, const float* __restrict__ norms,
                                                    int64_t n_groups, int dp, int hx, char* __restrict__ tiles,
                                                    unsigned* __restrict__ stat) {
-  const int nk = dp / 16, nb = dp / 8;
+  const int nk = dp / 16;
   const int64_t img = (int64_t)(nk + 1) * 1024;
   const int64_t t = blockIdx.x;  // one block per tile (group)
   if (t >= n_groups) return;
@@ -329,7 +329,7 @@ __global__ __launch_bounds__(256) void k_as_ctiles(const float* __restrict__ gro
     const int s = i >> 6, L = i & 63;
     const int cj = 16 * (s & 1) + (L & 15);  // centroid within the tile
     const int b = 4 * (s >> 1) + (L >> 4);   // 8-dim block: dims 32 (s >> 1) + 8 kq
-    const float* src = groups + ((t * nb + b) * kGroupRows + cj) * 8;
+    const float* src = groups + row_elem(t * kGroupRows + cj, 0, dp) + row_blk8(b);
     const float4 v0 = *reinterpret_cast<const float4*>(src), v1 = *reinterpret_cast<const float4*>(src + 4);
     const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
     _Float16 hv[8];

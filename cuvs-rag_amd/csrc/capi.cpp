@@ -135,10 +135,10 @@ struct mivs_index_s {
   Buf pq_codes, pq_books;
   // fp16 copy of the lists for the K10 pre-filter; empty = exact scan only
   Buf groups_h;
-  Buf rows_rm;     // K11: the fp32 lists row-major (built with groups_h when HBM has room; MIVS_PF_ROWMAJOR=0: off)
   Buf group_nmin;  // K13: the smallest row norm of every 32-row group (built with groups_h)
-  Buf groups_f8;   // K13's pre-pass: the lists' fp8 copy at 2^hx8 (built on first use when HBM has room)
+  Buf groups_f8;   // K13's pre-pass: the lists' fp8 copy at 2^hx8 (built with groups_h when the HBM budget allows)
   int hx8 = 0;
+  int copies_skipped = 0;  // kCopySkippedF8: the fp8 copy was not built (HBM budget), K13's pre-pass uses fp16
   int hx_exp = 0;
   float x_norm_max = 0.0f, x_res_max = 0.0f;
   int pf_G = kPfChunkGroups;                  // groups per K10 work item
@@ -702,17 +702,66 @@ void check_common(int device, const void* data, int64_t n, int32_t dim) {
 
 
 // ---- fp16 pre-filter (K10 / K11) ----
+// The optional copies an index may build beside its fp32 rows must leave this much of the device's HBM to the
+// rest of the process (an LLM or tensors sharing the GPU in a RAG pipeline): MIVS_INDEX_HBM_FRAC (default 0.6) is
+// the largest fraction of the device's HBM the index may hold with the copy, and 4 GiB must stay free beside it.
+bool copy_fits(const mivs_index_s* idx, size_t bytes);
 bool pf_default_on() {
   const char* e = getenv("MIVS_PREFILTER");
   return !(e && e[0] == '0');
+}
+
+// K13's pre-pass operand: the lists' fp8 copy at 2^(hx - 7), built with the fp16 copy (in the
+// build, counted in its time) for IVF indexes K13 serves, when the HBM budget allows; otherwise the pre-pass scans
+// the fp16 sample and last_search_stats / mivs_index_memory report the skipped copy
+void pf_build_f8(mivs_index_s* idx, hipStream_t s) {
+  const int nsb = idx->dp / 32;
+  if (idx->kind != 0 || idx->dp % 32 != 0 || (nsb % 6 != 0 && nsb % 4 != 0) || !pf_pair_mode() ||
+      !rs_scan_supported(idx->dp))
+    return;
+  const ListSet& L = idx->lists;
+  const size_t bytes = (size_t)L.n_groups * kGroupRows * idx->dp;
+  if (bytes == 0) return;
+  if (!copy_fits(idx, bytes)) {
+    idx->copies_skipped |= kCopySkippedF8;
+    return;
+  }
+  idx->hx8 = idx->hx_exp - 7;  // |x| max 2^hx_exp in [2^14, 2^15) -> [128, 256) under e4m3's 448
+  idx->groups_f8.reserve(bytes);
+  HIPCHK(launch_groups_to_f8(L.groups.as<float>(), L.n_groups, idx->dp, idx->hx8, idx->groups_f8.as<uint8_t>(), s));
+}
+
+size_t listset_bytes(const ListSet& L) { return L.groups.n + L.norms.n + L.ids.n + L.off.n + L.goff.n; }
+
+mivs_index_memory index_memory(const mivs_index_s* idx) {
+  mivs_index_memory m{};
+  const ListSet& L = idx->lists;
+  m.n_rows = L.n_rows;
+  m.rows_bytes = (int64_t)L.groups.n;
+  m.side_bytes = (int64_t)(L.norms.n + L.ids.n + L.off.n + L.goff.n);
+  m.centroid_bytes = (int64_t)(listset_bytes(idx->cents) + idx->centroids_rm.n);
+  m.fp16_bytes = (int64_t)(idx->groups_h.n + idx->group_nmin.n);
+  m.fp8_bytes = (int64_t)idx->groups_f8.n;
+  m.pq_bytes = (int64_t)(idx->pq_codes.n + idx->pq_books.n);
+  m.total_bytes = m.rows_bytes + m.side_bytes + m.centroid_bytes + m.fp16_bytes + m.fp8_bytes + m.pq_bytes;
+  m.copies_skipped = idx->copies_skipped;
+  return m;
+}
+
+bool copy_fits(const mivs_index_s* idx, size_t bytes) {
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) return false;
+  const char* e = getenv("MIVS_INDEX_HBM_FRAC");
+  const double frac = e ? atof(e) : 0.6;
+  return fr >= bytes + ((size_t)4 << 30) && (double)index_memory(idx).total_bytes + (double)bytes <= frac * (double)tot;
 }
 
 // build the fp16 copy of idx->lists (+ the per-index maxima the refine window needs)
 void pf_enable(mivs_index_s* idx, hipStream_t s) {
   const ListSet& L = idx->lists;
   idx->groups_h.release();
-  idx->rows_rm.release();
   idx->groups_f8.release();
+  idx->copies_skipped = 0;
   if (L.n_groups == 0 || idx->dp % 64 != 0) return;
   const int64_t nslot = L.n_groups * (int64_t)kGroupRows;
   Buf st;
@@ -738,16 +787,7 @@ void pf_enable(mivs_index_s* idx, hipStream_t s) {
   std::memcpy(&resmax, &h[2], 4);
   idx->x_norm_max = sqrtf(normmax) * (1.0f + 0x1p-12f);
   idx->x_res_max = resmax;
-  {  // K11's row-major copy (+ the fp32 lists' size again): only with a quarter of it (>= 4 GiB) to spare beside it
-    const char* rme = getenv("MIVS_PF_ROWMAJOR");
-    const size_t bytes = sizeof(float) * (size_t)nslot * idx->dp;
-    size_t fr = 0, tot = 0;
-    if (!(rme && rme[0] == '0') && hipMemGetInfo(&fr, &tot) == hipSuccess &&
-        fr > bytes + std::max<size_t>(bytes / 4, (size_t)4 << 30)) {
-      idx->rows_rm.reserve(bytes);
-      HIPCHK(launch_groups_to_rows(L.groups.as<float>(), L.n_groups, idx->dp, idx->rows_rm.as<float>(), s));
-    }
-  }
+  pf_build_f8(idx, s);
   std::vector<int64_t> c(L.n_lists);
   const char* ce = getenv("MIVS_PF_CHUNK_ROWS");
   // rows per work item: as many as the LDS holds the norms of beside the query tile (the tile's
@@ -904,7 +944,6 @@ void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_
   r.dp = dp;
   r.metric = idx->metric;
   r.groups = L.groups.as<float>();
-  r.rows_rm = idx->rows_rm.p ? idx->rows_rm.as<float>() : nullptr;
   r.row_norms = L.norms.as<float>();
   r.row_ids = L.ids.as<int64_t>();
   r.queries = q;
@@ -1003,22 +1042,11 @@ bool rs_use(const mivs_index_s* idx, int np) {
   return idx->kind == 0 && np >= 2 && rs_scan_supported(idx->dp) && !(e && e[0] == '0');
 }
 
-// K13's fp8 pre-pass nomination (MIVS_RS_PRE_F8=0: off): the rows' fp8 copy is built on first use if the
-// HBM has room for it beside a 4 GiB margin; dp / 32 must be a multiple of 4 or 6 (K10's rings)
-bool rs_pre_f8(mivs_index_s* idx, hipStream_t s) {
+// K13's fp8 pre-pass nomination (MIVS_RS_PRE_F8=0: off) where the index has the fp8 copy (pf_build_f8)
+bool rs_pre_f8(mivs_index_s* idx, hipStream_t) {
   const char* e = getenv("MIVS_RS_PRE_F8");
   if (e && e[0] == '0') return false;
-  const int nsb = idx->dp / 32;
-  if (idx->dp % 32 != 0 || (nsb % 6 != 0 && nsb % 4 != 0) || !pf_pair_mode()) return false;
-  if (idx->groups_f8.p) return true;
-  const ListSet& L = idx->lists;
-  const size_t bytes = (size_t)L.n_groups * kGroupRows * idx->dp;
-  size_t fr = 0, tot = 0;
-  if (bytes == 0 || hipMemGetInfo(&fr, &tot) != hipSuccess || fr < bytes + ((size_t)4 << 30)) return false;
-  idx->hx8 = idx->hx_exp - 7;  // |x| max 2^hx_exp in [2^14, 2^15) -> [128, 256) under e4m3's 448
-  idx->groups_f8.reserve(bytes);
-  HIPCHK(launch_groups_to_f8(L.groups.as<float>(), L.n_groups, idx->dp, idx->hx8, idx->groups_f8.as<uint8_t>(), s));
-  return true;
+  return idx->groups_f8.p != nullptr;
 }
 
 // records per K13 stream: twice the batch's queries, at most kRsWaveCapMax (MIVS_RS_WAVE_CAP overrides it: the
@@ -1191,7 +1219,6 @@ void lk_finish(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   a.ovf_q = ws.ovf_q.as<int64_t>();
   a.n_window = reinterpret_cast<int64_t*>(ws.pf_stats.as<char>() + 8);
   a.chunk_off = ws.lk_chunk_off.as<int64_t>();
-  a.rows_rm = idx->rows_rm.p ? idx->rows_rm.as<float>() : nullptr;
   a.groups = L.groups.as<float>();
   a.row_norms = L.norms.as<float>();
   a.row_ids = L.ids.as<int64_t>();
@@ -1860,7 +1887,6 @@ int32_t mivs_ivf_flat_extend(mivs_index_t idx, void* stream, const float* d_new,
     HIPCHK(hipStreamSynchronize(s));
     const bool had_pf = idx->groups_h.p != nullptr;
     idx->groups_h.release();
-    idx->rows_rm.release();
     idx->groups_f8.release();  // (copies of the old lists; pf_enable would drop them too)
     pack_lists(L, rows.as<float>(), d, idx->dp, perm.as<int64_t>(), h_off, 0, ids.as<int64_t>(), idx->G, s);
     if (had_pf) pf_enable(idx, s);
@@ -2452,6 +2478,7 @@ int32_t mivs_index_last_search_stats(mivs_index_t idx, mivs_search_stats* out) {
     st.scan_kernel = idx->last_scan;
     st.overflow_queries = idx->last_ovf;
     st.window_candidates = idx->last_window;
+    st.copies_skipped = idx->copies_skipped;
     const ListSet& L = idx->lists;
     if (idx->last_nq > 0 && idx->kind == 0) {
       HIPCHK(hipDeviceSynchronize());
@@ -2491,6 +2518,14 @@ int32_t mivs_index_last_search_stats(mivs_index_t idx, mivs_search_stats* out) {
       st.work_items = ceil_div(idx->last_nq, idx->last_qtile) * std::max<int64_t>(1, ceil_div(L.n_groups, G));
     }
     *out = st;
+  });
+}
+
+int32_t mivs_index_memory_info(mivs_index_t idx, mivs_index_memory* out) {
+  return guarded([&] {
+    require(idx != nullptr && out != nullptr, "NULL argument");
+    std::lock_guard<std::mutex> g(idx->mu);
+    *out = index_memory(idx);
   });
 }
 
@@ -2542,7 +2577,6 @@ int32_t mivs_index_set_prefilter(mivs_index_t idx, void* stream, int32_t enable)
       if (!idx->groups_h.p) pf_enable(idx, s);
     } else {
       idx->groups_h.release();
-      idx->rows_rm.release();
       idx->groups_f8.release();
     }
   });

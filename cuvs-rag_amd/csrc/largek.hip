@@ -248,16 +248,14 @@ __global__ __launch_bounds__(256) void k_lk_recompute(LkArgs a) {
     const int n_w = a.win_n[q];
     const bool live = i < n_w;
     const int pos = live ? a.win_pos[q * a.cap + i] : 0;
-    const float* rowp = a.rows_rm ? a.rows_rm + (int64_t)pos * a.dp
-                                  : a.groups + ((int64_t)(pos >> 5) * nb * kGroupRows + (pos & 31)) * 8;
-    const int64_t bstride = a.rows_rm ? 8 : 256;
+    const float* rowp = a.groups + row_elem(pos, 0, a.dp);
     const float* qv = a.queries + q * a.d;
     float acc = 0.0f;
     const int nbd = a.d >> 3;  // blocks fully inside d (the padded tail is zero: neutral, the accumulator is never -0)
 #pragma unroll 8
     for (int b = 0; b < nbd; ++b) {
-      const float4 x0 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride);
-      const float4 x1 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride + 4);
+      const float4 x0 = *reinterpret_cast<const float4*>(rowp + row_blk8(b));
+      const float4 x1 = *reinterpret_cast<const float4*>(rowp + row_blk8(b) + 4);
       const float* y = qv + 8 * b;
       acc = fmaf(x0.x, y[0], acc); acc = fmaf(x1.x, y[4], acc);
       acc = fmaf(x0.y, y[1], acc); acc = fmaf(x1.y, y[5], acc);
@@ -266,8 +264,8 @@ __global__ __launch_bounds__(256) void k_lk_recompute(LkArgs a) {
     }
     if (nbd < nb) {  // d % 8 != 0: the last block's query dims past d read as zero
       const int b = nbd;
-      const float4 x0 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride);
-      const float4 x1 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride + 4);
+      const float4 x0 = *reinterpret_cast<const float4*>(rowp + row_blk8(b));
+      const float4 x1 = *reinterpret_cast<const float4*>(rowp + row_blk8(b) + 4);
       float y[8];
 #pragma unroll
       for (int t = 0; t < 8; ++t) y[t] = 8 * b + t < a.d ? qv[8 * b + t] : 0.0f;
@@ -289,10 +287,10 @@ __global__ __launch_bounds__(256) void k_lk_recompute(LkArgs a) {
   }
 }
 
-// K16r from the row-major copy: the same keys, the rows gathered by LDS-DMA. A wave's 64 window rows arrive in
-// 64-dim chunks: DMA instruction t writes rows 4t .. 4t + 3 (256 B each, 1 KiB contiguous in LDS); lane L fetches
-// piece (L & 15) ^ (r & 15) of row r = 4t + (L >> 4), so each instruction reads 4 whole 256-B row segments (full
-// cache lines, not 64 scattered 16-B pieces) and piece p of row r sits at slot p ^ (r & 15): lane r's reads of
+// K16r with LDS-DMA: the same keys, the rows gathered by LDS-DMA. A wave's 64 window rows arrive in 64-dim
+// chunks: DMA instruction t writes rows 4t .. 4t + 3 (256 B each, 1 KiB contiguous in LDS); lane L fetches
+// piece (L & 15) ^ (r & 15) of row r = 4t + (L >> 4), so each instruction reads 4 rows x 4 whole 64-B row blocks
+// (not 64 scattered 16-B pieces) and piece p of row r sits at slot p ^ (r & 15): lane r's reads of
 // its own row (piece p for every lane at once) fall on 16 different slots -- conflict-free ds_read_b128. The
 // query (zero past d) is staged once per run of items of the same query. No barriers: every wave owns its LDS.
 constexpr int kLkRmWaves = 4;
@@ -337,19 +335,21 @@ __global__ __launch_bounds__(64 * kLkRmWaves) void k_lk_recompute_rm(LkArgs a) {
       }
       q_staged = q;
     }
-    // the source of DMA instruction t for this lane: row 4 t + (lane >> 4), piece (lane & 15) ^ (row & 15)
-    const float* rowp = a.rows_rm + (int64_t)pos * dp;
+    // the source of DMA instruction t for this lane: row 4 t + (lane >> 4), piece p = (lane & 15) ^ (row & 15) of
+    // the chunk: dims 4p .. 4p + 3 = 16 B of the row's 64-B block p / 4 (row_elem layout)
+    const float* rowp = a.groups + row_elem(pos, 0, dp);
     const float* src[16];
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
       const int r = 4 * t + (lane >> 4);
+      const int p = (lane & 15) ^ (r & 15);
       const uint64_t b = (uint64_t)__shfl((long long)(uintptr_t)rowp, r);
-      src[t] = reinterpret_cast<const float*>(b) + 4 * ((lane & 15) ^ (r & 15));
+      src[t] = reinterpret_cast<const float*>(b) + (p >> 2) * kRowBlkStride + (p & 3) * 4;
     }
     float acc = 0.0f;
     for (int c = 0; c < nch; ++c) {
 #pragma unroll
-      for (int t = 0; t < 16; ++t) lk_glds16(src[t] + 64 * c, rbuf + t * 256);
+      for (int t = 0; t < 16; ++t) lk_glds16(src[t] + 4 * kRowBlkStride * c, rbuf + t * 256);
       __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): this chunk landed (and the query's writes)
       const float* myrow = rbuf + lane * 64;
       const float* qc = qbuf + 64 * c;
@@ -479,7 +479,7 @@ hipError_t launch_lk_chunks(const int* win_n, int64_t nq, int64_t* chunks, hipSt
 hipError_t launch_lk_recompute(const LkArgs& a, int cus, hipStream_t s) {
   if (a.nq <= 0) return hipSuccess;
   const char* e = getenv("MIVS_LK_GATHER");
-  if (a.rows_rm && a.dp % 64 == 0 && a.dp <= 1024 && !(e && e[0] == '0')) {
+  if (a.dp % 64 == 0 && a.dp <= 1024 && !(e && e[0] == '0')) {
     // two workgroups of 4 waves per CU: 8 waves x 16 KiB of rows in flight
     const size_t lds = sizeof(float) * (size_t)kLkRmWaves * (64 * 64 + a.dp);
     static const hipError_t a0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lk_recompute_rm<kL2>),

@@ -39,13 +39,13 @@ __global__ __launch_bounds__(256) void k_pack(const float* __restrict__ src, int
   const int64_t sidx = list_off[l] + r;
   const int64_t srow = valid ? (src_index ? src_index[sidx] : sidx) : 0;
   const float* rowp = src + srow * (int64_t)d;
-  float* dst = groups + g * (int64_t)(kGroupRows * dp) + rr * 8 + 4 * h;
+  float* dst = groups + g * (int64_t)(kGroupRows * dp) + rr * kRowBlk + 4 * h;
   float acc = 0.0f;
   const int S = dp >> 3;
   for (int s = 0; s < S; ++s) {
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (valid) v = ld4(rowp, 8 * s + 4 * h, d);
-    *reinterpret_cast<float4*>(dst + s * 256) = v;
+    *reinterpret_cast<float4*>(dst + row_blk8(s)) = v;
     const float px = __shfl_xor(v.x, 32), py = __shfl_xor(v.y, 32);
     const float pz = __shfl_xor(v.z, 32), pw = __shfl_xor(v.w, 32);
     acc = fmaf(v.x, v.x, acc); acc = fmaf(px, px, acc);
@@ -147,7 +147,7 @@ __global__ void k_unpack(const float* __restrict__ groups, int dp, int d, const 
     const int64_t r = row - list_off[l];
     const int64_t g = list_goff[l] + r / kGroupRows;
     const int rr = (int)(r % kGroupRows);
-    out[t] = groups[g * (int64_t)(kGroupRows * dp) + (c >> 3) * 256 + rr * 8 + (c & 7)];
+    out[t] = groups[row_elem(g * kGroupRows + rr, c, dp)];
   }
 }
 

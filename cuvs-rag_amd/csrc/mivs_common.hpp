@@ -27,6 +27,19 @@ constexpr int kMaxSelectK = 4096;  // largest k / n_probes (K8 select path above
 enum Metric : int { kL2 = 0, kIP = 1 };
 
 __host__ __device__ inline int dim_pad(int d) { return (d + kDimAlign - 1) / kDimAlign * kDimAlign; }
+
+// The fp32 rows of every list: groups of 32 rows, inside a group 64-B row blocks
+// [dp/16][32 rows][16 floats]. One MFMA k-step of the scans (lane (r, h): dims 8s + 4h .. + 3 of row r) reads
+// 32 B of each of the 32 rows, two k-steps per block, 2 KiB of one group per k-step pair; a row gather (the
+// exact recompute of a candidate) reads whole 64-B blocks, nothing of the neighbour rows.
+constexpr int kRowBlk = 16;                          // floats per row block
+constexpr int kRowBlkStride = kGroupRows * kRowBlk;  // floats between a row's consecutive blocks (512)
+// element offset of dim c of row slot `slot` (g * 32 + r)
+__host__ __device__ inline int64_t row_elem(int64_t slot, int c, int dp) {
+  return (slot >> 5) * (int64_t)(kGroupRows * dp) + (int64_t)(c >> 4) * kRowBlkStride + (slot & 31) * kRowBlk + (c & 15);
+}
+// offset of a row's 8-dim block b (dims 8b .. 8b + 7) from its dim 0 (row_elem(slot, 0, dp))
+__host__ __device__ inline int row_blk8(int b) { return (b >> 1) * kRowBlkStride + (b & 1) * 8; }
 __host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -266,6 +279,7 @@ struct RsScanArgs {
 
 // K16 large-k search through the pre-filter (largek.hip): K13's candidates -> per query the refine
 // window (K16w) -> pinned fp32 keys of the window rows (K16r) -> (key, id) sort and the first k (K16s)
+constexpr int kCopySkippedF8 = 1;  // == MIVS_COPY_SKIPPED_F8
 constexpr int kLkMaxCap = 8192;    // window rows per query at most (more: the exact scan)
 constexpr int kLkSampleDiv = 64;   // T_q's sample: the first 1 / kLkSampleDiv of every probed list (MIVS_LK_SAMPLE_DIV)
 constexpr float kLkSampleZ = 4.0f; // sample rank margin in standard deviations (binomial)
@@ -287,8 +301,7 @@ struct LkArgs {
   int64_t* ovf_q;
   int64_t* n_window;        // optional: total window rows (stats)
   const int64_t* chunk_off; // [nq + 1] exclusive prefix of the windows' 64-row chunks (K16r's items)
-  const float* rows_rm;     // fp32 rows row-major (or nullptr: the group layout below)
-  const float* groups;
+  const float* groups;      // fp32 rows (row_elem layout)
   const float* row_norms;
   const int64_t* row_ids;
   const float* queries;     // fp32 [nq][d]
@@ -355,8 +368,7 @@ struct PfRefineArgs {
   int slot_k;
   int64_t nq;
   int k, d, dp, metric;
-  const float* groups;        // fp32 lists (group layout) for the exact recompute
-  const float* rows_rm;       // optional: the same rows row-major ([slot][dp], launch_groups_to_rows)
+  const float* groups;        // fp32 lists (row_elem layout) for the exact recompute
   const float* row_norms;
   const int64_t* row_ids;
   const float* queries;       // fp32 [nq][d]
@@ -459,9 +471,6 @@ hipError_t launch_gather_ids(const int64_t* src, const int64_t* idx, int64_t n, 
 constexpr unsigned kPfOrdInf = 0xFF800000u;  // order mapping of +inf (qtheta's initial value)
 // fp32 groups -> fp16 groups scaled by 2^hx_exp (FTZ below the fp16 normal range), per-index maxima of
 // ||x - x_h|| and max |x| (as float bits, atomicMax) into stats[0..1] (zeroed by the caller)
-// the fp32 lists row-major ([n_groups * 32][dp], group-row order): K11's exact recompute reads a candidate's 3 KiB
-// contiguously instead of 32 B from each of 96 lines shared with three other rows
-hipError_t launch_groups_to_rows(const float* groups, int64_t n_groups, int dp, float* out, hipStream_t s);
 hipError_t launch_groups_to_half(const float* groups, int64_t n_groups, int dp, int hx_exp, uint16_t* out,
                                  unsigned* stats, hipStream_t s);
 hipError_t launch_abs_max(const float* x, int64_t n, unsigned* out, hipStream_t s);

@@ -730,16 +730,14 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
   if (live && !ovf && lane < cnt) {
     const int pos = s_cp[wv][lane];
     const int nb = a.dp >> 3;
-    // the row's block b: 8 floats at rowp + b * bstride (row-major copy: contiguous; group layout: 1 KiB apart)
-    const float* rowp = a.rows_rm ? a.rows_rm + (int64_t)pos * a.dp
-                                  : a.groups + ((int64_t)(pos >> 5) * nb * kGroupRows + (pos & 31)) * 8;
-    const int64_t bstride = a.rows_rm ? 8 : 256;
+    // the row's 8-dim block b at rowp + row_blk8(b) (64-B row blocks: a candidate reads whole blocks)
+    const float* rowp = a.groups + row_elem(pos, 0, a.dp);
     const float* qv = s_qv[wv];
     float acc = 0.0f;
 #pragma unroll 12
     for (int b = 0; b < nb; ++b) {
-      const float4 x0 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride);
-      const float4 x1 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride + 4);
+      const float4 x0 = *reinterpret_cast<const float4*>(rowp + row_blk8(b));
+      const float4 x1 = *reinterpret_cast<const float4*>(rowp + row_blk8(b) + 4);
       const float4 y0 = *reinterpret_cast<const float4*>(qv + 8 * b);
       const float4 y1 = *reinterpret_cast<const float4*>(qv + 8 * b + 4);
       acc = fmaf(x0.x, y0.x, acc); acc = fmaf(x1.x, y1.x, acc);
@@ -856,13 +854,11 @@ __global__ __launch_bounds__(256) void k_pf_verify(PfRefineArgs a) {
     const int nb = a.dp >> 3;
     for (int n = 0; n < nvf; ++n) {
       const int pos = s_cp[wv][n];
-      const float* rowp = a.rows_rm ? a.rows_rm + (int64_t)pos * a.dp
-                                    : a.groups + ((int64_t)(pos >> 5) * nb * kGroupRows + (pos & 31)) * 8;
-      const int64_t bstride = a.rows_rm ? 8 : 256;
+      const float* rowp = a.groups + row_elem(pos, 0, a.dp);
       float acc = 0.0f;
       for (int b = lane; b < nb; b += 64) {
-        const float4 x0 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride);
-        const float4 x1 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * bstride + 4);
+        const float4 x0 = *reinterpret_cast<const float4*>(rowp + row_blk8(b));
+        const float4 x1 = *reinterpret_cast<const float4*>(rowp + row_blk8(b) + 4);
         const float4 y0 = *reinterpret_cast<const float4*>(s_qv[wv] + 8 * b);
         const float4 y1 = *reinterpret_cast<const float4*>(s_qv[wv] + 8 * b + 4);
         acc = fmaf(x0.x, y0.x, acc); acc = fmaf(x0.y, y0.y, acc); acc = fmaf(x0.z, y0.z, acc); acc = fmaf(x0.w, y0.w, acc);
@@ -917,10 +913,11 @@ __global__ void k_groups_to_half(const float* __restrict__ groups, int64_t n_gro
   if (g < n_groups) {
     const int nb = dp >> 3;
     const float sc = ldexpf(1.0f, hx_exp), isc = ldexpf(1.0f, -hx_exp);
+    const float* row = groups + row_elem(g * kGroupRows + r, 0, dp);
     for (int b = 0; b < nb; ++b) {
-      const int64_t o = ((g * nb + b) * kGroupRows + r) * 8;
-      const float4 x0 = *reinterpret_cast<const float4*>(groups + o);
-      const float4 x1 = *reinterpret_cast<const float4*>(groups + o + 4);
+      const int64_t o = ((g * nb + b) * kGroupRows + r) * 8;  // (the fp16 copy: [dp/8][32][8] per group)
+      const float4 x0 = *reinterpret_cast<const float4*>(row + row_blk8(b));
+      const float4 x1 = *reinterpret_cast<const float4*>(row + row_blk8(b) + 4);
       uint4 pk;
       pk.x = pf_to_half(x0.x, sc, isc, res) | ((unsigned)pf_to_half(x0.y, sc, isc, res) << 16);
       pk.y = pf_to_half(x0.z, sc, isc, res) | ((unsigned)pf_to_half(x0.w, sc, isc, res) << 16);
@@ -1461,11 +1458,11 @@ __global__ __launch_bounds__(256) void k_pf_refine1(PfRefineArgs a) {
       if (!(key <= T)) continue;
       if (++cnt > kPfCap) { ovf = true; break; }
       const int pos = a.slot_pos[sl * a.slot_k + t];
-      const float* rowp = a.groups + ((int64_t)(pos >> 5) * nb * kGroupRows + (pos & 31)) * 8;
+      const float* rowp = a.groups + row_elem(pos, 0, a.dp);
       float acc = 0.0f;
       for (int b = 0; b < nb; ++b) {
-        const float4 x0 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * 256);
-        const float4 x1 = *reinterpret_cast<const float4*>(rowp + (int64_t)b * 256 + 4);
+        const float4 x0 = *reinterpret_cast<const float4*>(rowp + row_blk8(b));
+        const float4 x1 = *reinterpret_cast<const float4*>(rowp + row_blk8(b) + 4);
         float y[8];
         if (vec) {
           const float4 y0 = *reinterpret_cast<const float4*>(qv + 8 * b);
@@ -1630,28 +1627,6 @@ hipError_t launch_pf_refine(const PfRefineArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// thread = (row slot, 8-dim block), block fastest: every store is 32 B of one row, consecutive threads contiguous
-__global__ void k_groups_to_rows(const float* __restrict__ groups, int64_t n_groups, int dp, float* __restrict__ out) {
-  const int nb = dp >> 3;
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_groups * kGroupRows * nb) return;
-  const int64_t slot = t / nb;
-  const int b = (int)(t - slot * nb);
-  const int64_t g = slot / kGroupRows;
-  const int r = (int)(slot - g * kGroupRows);
-  const float4* src = reinterpret_cast<const float4*>(groups + ((g * nb + b) * kGroupRows + r) * 8);
-  float4* dst = reinterpret_cast<float4*>(out + slot * dp + 8 * b);
-  dst[0] = src[0];
-  dst[1] = src[1];
-}
-
-hipError_t launch_groups_to_rows(const float* groups, int64_t n_groups, int dp, float* out, hipStream_t s) {
-  const int64_t n = n_groups * kGroupRows * (dp >> 3);
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_groups_to_rows, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, groups, n_groups, dp, out);
-  return hipGetLastError();
-}
-
 hipError_t launch_groups_to_half(const float* groups, int64_t n_groups, int dp, int hx_exp, uint16_t* out,
                                  unsigned* stats, hipStream_t s) {
   if (n_groups <= 0) return hipSuccess;
@@ -1675,7 +1650,7 @@ __device__ __forceinline__ uint4 f8_pack16(const float (&v)[16], float sc) {
 
 __global__ void k_groups_to_f8(const float* __restrict__ groups, int64_t n_groups, int dp, int hx8,
                                uint8_t* __restrict__ out) {
-  const int nsb = dp >> 5, nb = dp >> 3;
+  const int nsb = dp >> 5;
   const int64_t n = n_groups * nsb * 64;
   const float sc = ldexpf(1.0f, hx8);
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
@@ -1685,7 +1660,7 @@ __global__ void k_groups_to_f8(const float* __restrict__ groups, int64_t n_group
     float v[16];
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
-      const float* src = groups + ((g * nb + 4 * S + 2 * e + hh) * kGroupRows + jj) * 8;
+      const float* src = groups + row_elem(g * kGroupRows + jj, 0, dp) + row_blk8(4 * S + 2 * e + hh);
       const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
       v[8 * e + 0] = x0.x; v[8 * e + 1] = x0.y; v[8 * e + 2] = x0.z; v[8 * e + 3] = x0.w;
       v[8 * e + 4] = x1.x; v[8 * e + 5] = x1.y; v[8 * e + 6] = x1.z; v[8 * e + 7] = x1.w;

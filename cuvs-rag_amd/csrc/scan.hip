@@ -50,11 +50,11 @@ __device__ __forceinline__ void lane_insert(float (&lk)[KCAP], int (&lp)[KCAP], 
   }
 }
 
-// Block of BLK k-steps of one row group: BLK dwordx4 loads per lane (one contiguous 1 KiB wave load each)
+// Block of BLK k-steps of one row group (p at an even k-step): BLK dwordx4 loads per lane, 32 rows x 32 B each
 template <int BLK>
 __device__ __forceinline__ void load_block(float4 (&v)[BLK], const float* __restrict__ p) {
 #pragma unroll
-  for (int u = 0; u < BLK; ++u) v[u] = *reinterpret_cast<const float4*>(p + u * 256);
+  for (int u = 0; u < BLK; ++u) v[u] = *reinterpret_cast<const float4*>(p + row_blk8(u));
 }
 
 template <int BLK>
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(W * 64, 1) void k_scan(ScanArgs a, float* __restric
     const int ng = g_end > g0 ? (int)((g_end - g0 + W - 1) / W) : 0;
     const int nb = ng * bpg;
     if (nb > 0) {
-      const float* lane_base = a.groups + g0 * (int64_t)(kGroupRows * dp) + j * 8 + 4 * h;
+      const float* lane_base = a.groups + g0 * (int64_t)(kGroupRows * dp) + j * kRowBlk + 4 * h;
       const int64_t gstride = (int64_t)W * kGroupRows * dp;
       auto bptr = [&](int b) {
         const int bb = b < nb ? b : nb - 1;  // past the end: re-read the last block (never consumed)

@@ -84,7 +84,7 @@ __device__ __forceinline__ void mma8_refill(f32x16& c0, f32x16& c1, float4 (&v)[
     c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v[u].z, b1.z, c1, 0, 0, 0);
     c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v[u].w, b0.w, c0, 0, 0, 0);
     c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v[u].w, b1.w, c1, 0, 0, 0);
-    v[u] = *reinterpret_cast<const float4*>(next + u * 256);
+    v[u] = *reinterpret_cast<const float4*>(next + row_blk8(u));
     __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);  // MFMA
     __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
     __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
@@ -93,7 +93,7 @@ __device__ __forceinline__ void mma8_refill(f32x16& c0, f32x16& c1, float4 (&v)[
 
 __device__ __forceinline__ void load8(float4 (&v)[8], const float* __restrict__ p) {
 #pragma unroll
-  for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(p + u * 256);
+  for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(p + row_blk8(u));
 }
 
 // W waves per workgroup (4: two workgroups per CU interleave their barriers / merges on every
@@ -206,7 +206,7 @@ __global__ __launch_bounds__(W * 64, 1) void k_scan_wide(ScanArgs a) {
     const int nsteps = npass * ns;
     auto grp_ptr = [&](int pass) {
       const int64_t g = g_begin + pass * W + wave;
-      return a.groups + (g < g_end ? g : g_begin) * gstride + j * 8 + 4 * h;
+      return a.groups + (g < g_end ? g : g_begin) * gstride + j * kRowBlk + 4 * h;
     };
     float4 A[8], B[8];
     {

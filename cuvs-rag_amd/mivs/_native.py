@@ -89,6 +89,24 @@ class SearchStats(ctypes.Structure):
         ("candidates", c_int64),
         ("cand_overflow", c_int64),
         ("spun_out_waves", c_int64),
+        ("copies_skipped", c_int32),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+class IndexMemory(ctypes.Structure):
+    _fields_ = [
+        ("n_rows", c_int64),
+        ("rows_bytes", c_int64),
+        ("side_bytes", c_int64),
+        ("centroid_bytes", c_int64),
+        ("fp16_bytes", c_int64),
+        ("fp8_bytes", c_int64),
+        ("pq_bytes", c_int64),
+        ("total_bytes", c_int64),
+        ("copies_skipped", c_int32),
     ]
 
     def as_dict(self) -> dict:
@@ -139,6 +157,7 @@ _SIGS = {
     "mivs_index_info": (c_int32, [c_void_p, POINTER(c_int64), POINTER(c_int32), POINTER(c_int32), POINTER(c_int32),
                                   POINTER(c_int32)]),
     "mivs_index_last_search_stats": (c_int32, [c_void_p, POINTER(SearchStats)]),
+    "mivs_index_memory_info": (c_int32, [c_void_p, POINTER(IndexMemory)]),
     "mivs_index_profile_collect": (c_int32, [c_void_p, POINTER(Profile)]),
     "mivs_index_build_phases": (c_int32, [c_void_p, c_void_p, c_int32, POINTER(c_int32)]),
     "mivs_index_set_prefilter": (c_int32, [c_void_p, c_void_p, c_int32]),

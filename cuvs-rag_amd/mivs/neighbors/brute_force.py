@@ -51,6 +51,14 @@ class Index:
         _native.check(_native.lib().mivs_index_set_prefilter(self.handle, stream_ptr(self.device),
                                                              1 if enable else 0))
 
+    def memory(self) -> dict:
+        """Bytes the index holds in HBM by part (mivs_index_memory_info): the fp32 rows, norms / ids / offsets,
+        centroids, the fp16 and fp8 copies, PQ codes; copies_skipped = 1 when the fp8 copy was left out (HBM
+        budget, MIVS_INDEX_HBM_FRAC)."""
+        m = _native.IndexMemory()
+        _native.check(_native.lib().mivs_index_memory_info(self.handle, ctypes.byref(m)))
+        return m.as_dict()
+
     def last_search_stats(self) -> dict:
         st = _native.SearchStats()
         _native.check(_native.lib().mivs_index_last_search_stats(self.handle, ctypes.byref(st)))

@@ -155,6 +155,14 @@ class Index:
         _native.check(_native.lib().mivs_ivf_pq_get_codes(self.handle, stream_ptr(self.device), ptr(out)))
         return out
 
+    def memory(self) -> dict:
+        """Bytes the index holds in HBM by part (mivs_index_memory_info): the fp32 rows, norms / ids / offsets,
+        centroids, the fp16 and fp8 copies, PQ codes; copies_skipped = 1 when the fp8 copy was left out (HBM
+        budget, MIVS_INDEX_HBM_FRAC)."""
+        m = _native.IndexMemory()
+        _native.check(_native.lib().mivs_index_memory_info(self.handle, ctypes.byref(m)))
+        return m.as_dict()
+
     def build_phases(self) -> dict:
         """Host wall time (s) of this index's build phases (recorded only while profiling was on)."""
         ph = _native.build_phases(self.handle, 2)

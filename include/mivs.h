@@ -89,7 +89,26 @@ typedef struct {
   int64_t cand_overflow;    /* K13: queries sent to the fallback because a record stream overflowed */
   int64_t spun_out_waves;   /* K13: waves that gave up waiting for a tile (~40 ms; never expected): their
                                batch took the fallback search, as for a stream overflow */
+  int32_t copies_skipped;   /* MIVS_COPY_SKIPPED_F8: the index has no fp8 copy (HBM budget): K13's pre-pass ran on
+                               the fp16 sample */
 } mivs_search_stats;
+
+/* what an index holds in HBM (mivs_index_memory_info). The optional copies are built at build / extend /
+ * set_prefilter(1) only while the index stays within MIVS_INDEX_HBM_FRAC (default 0.6) of the device's HBM and 4 GiB
+ * stay free beside it; a skipped copy is reported in copies_skipped (the search then takes the path without it). */
+#define MIVS_COPY_SKIPPED_F8 1
+typedef struct {
+  int64_t n_rows;
+  int64_t rows_bytes;      /* the fp32 rows (64-B row blocks): the only fp32 copy */
+  int64_t side_bytes;      /* row norms, ids, list offsets */
+  int64_t centroid_bytes;  /* the coarse centroids */
+  int64_t fp16_bytes;      /* the pre-filter's fp16 copy of the rows (+ its per-group minima) */
+  int64_t fp8_bytes;       /* K13's pre-pass fp8 copy */
+  int64_t pq_bytes;        /* IVF-PQ codes + codebooks */
+  int64_t total_bytes;
+  int32_t copies_skipped;  /* MIVS_COPY_SKIPPED_* bits */
+} mivs_index_memory;
+int32_t mivs_index_memory_info(mivs_index_t index, mivs_index_memory* out);
 
 /* device time of the searches issued since the last collect while profiling was on
  * (hipEvents recorded on each call's stream; no host sync inside the calls) */

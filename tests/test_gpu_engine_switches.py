@@ -277,3 +277,36 @@ def test_k13_query_batches_same_bits(ivf, flat_data):
         ds, is_ = _search(idx, q[lo:hi])
         np.testing.assert_array_equal(i[lo:hi], is_)
         np.testing.assert_array_equal(_bits(d[lo:hi]), _bits(ds))
+
+
+def test_index_memory_single_fp32_copy_and_fp8_budget(flat_data, mivs_lib, monkeypatch):
+    """the index holds ONE fp32 copy of the rows (64-B row blocks), the fp16 copy and -- within the HBM budget -- the
+    fp8 copy, all built in build(); MIVS_INDEX_HBM_FRAC=0 leaves the fp8 copy out (reported in memory() and the search
+    stats) and the search gives the same bits through the fp16 pre-pass sample"""
+    from mivs.neighbors import ivf_flat
+
+    x, q = flat_data
+    xt = torch.from_numpy(x).cuda()
+    p = ivf_flat.IndexParams(n_lists=48, kmeans_n_iters=4)
+    a = ivf_flat.build(p, xt)
+    m = a.memory()
+    n, d = x.shape
+    dp = (d + 63) // 64 * 64
+    slots = m["rows_bytes"] // (4 * dp)
+    assert slots >= n and m["fp16_bytes"] >= 2 * dp * slots and m["fp8_bytes"] == dp * slots, m
+    assert m["copies_skipped"] == 0
+    assert m["total_bytes"] == sum(m[k] for k in ("rows_bytes", "side_bytes", "centroid_bytes", "fp16_bytes",
+                                                  "fp8_bytes", "pq_bytes"))
+    # fp32 + fp16 + fp8 (+ norms, ids, offsets, centroids): no second fp32 copy
+    assert m["total_bytes"] < (4 + 2 + 1) * dp * slots + 12 * slots + m["centroid_bytes"] + 4 * 48 * 64 + (1 << 20), m
+    d0, i0 = _search(a, q)
+    monkeypatch.setenv("MIVS_INDEX_HBM_FRAC", "0")
+    b = ivf_flat.build(p, xt)
+    mb = b.memory()
+    assert mb["copies_skipped"] == 1 and mb["fp8_bytes"] == 0, mb
+    d1, i1 = _search(b, q)
+    assert b.last_search_stats()["copies_skipped"] == 1
+    np.testing.assert_array_equal(i1, i0)
+    np.testing.assert_array_equal(_bits(d1), _bits(d0))
+    a.close()
+    b.close()
