@@ -1674,6 +1674,7 @@ void ivf_search_impl(mivs_index_s* idx, hipStream_t s, const float* q, int64_t n
   } else if (idx->groups_h.p != nullptr && k <= kPfMaxK && rs_use(idx, np)) {
     qb = std::min<int64_t>(nq, kRsMaxBatch);  // K13: bounded record streams and LDS-histogram bucketing
   }
+  qb = ceil_div(nq, ceil_div(nq, std::max<int64_t>(qb, 1)));  // equal batches (a small last one rescans every list)
   int64_t nb = 0;
   for (int64_t b0 = 0; b0 < nq; b0 += qb) {
     nb = std::min<int64_t>(qb, nq - b0);

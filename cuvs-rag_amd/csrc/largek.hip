@@ -289,7 +289,7 @@ __global__ __launch_bounds__(256) void k_lk_recompute(LkArgs a) {
 
 // K16r with LDS-DMA: the same keys, the rows gathered by LDS-DMA. A wave's 64 window rows arrive in 64-dim
 // chunks: DMA instruction t writes rows 4t .. 4t + 3 (256 B each, 1 KiB contiguous in LDS); lane L fetches
-// piece (L & 15) ^ (r & 15) of row r = 4t + (L >> 4), so each instruction reads 4 rows x 4 whole 64-B row blocks
+// piece (L & 15) ^ (r & 15) of row r = 4t + (L >> 4), so each instruction reads 4 rows x one whole 256-B row block
 // (not 64 scattered 16-B pieces) and piece p of row r sits at slot p ^ (r & 15): lane r's reads of
 // its own row (piece p for every lane at once) fall on 16 different slots -- conflict-free ds_read_b128. The
 // query (zero past d) is staged once per run of items of the same query. No barriers: every wave owns its LDS.
@@ -336,7 +336,7 @@ __global__ __launch_bounds__(64 * kLkRmWaves) void k_lk_recompute_rm(LkArgs a) {
       q_staged = q;
     }
     // the source of DMA instruction t for this lane: row 4 t + (lane >> 4), piece p = (lane & 15) ^ (row & 15) of
-    // the chunk: dims 4p .. 4p + 3 = 16 B of the row's 64-B block p / 4 (row_elem layout)
+    // the chunk: dims 4p .. 4p + 3 (row_elem layout: the chunk is one 256-B row block)
     const float* rowp = a.groups + row_elem(pos, 0, dp);
     const float* src[16];
 #pragma unroll
@@ -344,12 +344,12 @@ __global__ __launch_bounds__(64 * kLkRmWaves) void k_lk_recompute_rm(LkArgs a) {
       const int r = 4 * t + (lane >> 4);
       const int p = (lane & 15) ^ (r & 15);
       const uint64_t b = (uint64_t)__shfl((long long)(uintptr_t)rowp, r);
-      src[t] = reinterpret_cast<const float*>(b) + (p >> 2) * kRowBlkStride + (p & 3) * 4;
+      src[t] = reinterpret_cast<const float*>(b) + row_dim(4 * p);
     }
     float acc = 0.0f;
     for (int c = 0; c < nch; ++c) {
 #pragma unroll
-      for (int t = 0; t < 16; ++t) lk_glds16(src[t] + 4 * kRowBlkStride * c, rbuf + t * 256);
+      for (int t = 0; t < 16; ++t) lk_glds16(src[t] + row_dim(64 * c), rbuf + t * 256);
       __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): this chunk landed (and the query's writes)
       const float* myrow = rbuf + lane * 64;
       const float* qc = qbuf + 64 * c;

@@ -28,18 +28,20 @@ enum Metric : int { kL2 = 0, kIP = 1 };
 
 __host__ __device__ inline int dim_pad(int d) { return (d + kDimAlign - 1) / kDimAlign * kDimAlign; }
 
-// The fp32 rows of every list: groups of 32 rows, inside a group 64-B row blocks
-// [dp/16][32 rows][16 floats]. One MFMA k-step of the scans (lane (r, h): dims 8s + 4h .. + 3 of row r) reads
-// 32 B of each of the 32 rows, two k-steps per block, 2 KiB of one group per k-step pair; a row gather (the
-// exact recompute of a candidate) reads whole 64-B blocks, nothing of the neighbour rows.
-constexpr int kRowBlk = 16;                          // floats per row block
-constexpr int kRowBlkStride = kGroupRows * kRowBlk;  // floats between a row's consecutive blocks (512)
+// The fp32 rows of every list: groups of 32 rows, inside a group 256-B row blocks
+// [dp/64][32 rows][64 floats]. One MFMA k-step of the scans (lane (r, h): dims 8s + 4h .. + 3 of row r) reads
+// 32 B of each of the 32 rows, eight k-steps per block, 8 KiB of one group per eight k-steps; a row gather (the
+// exact recompute of a candidate) reads whole 256-B blocks, nothing of the neighbour rows.
+constexpr int kRowBlk = 64;                          // floats per row block (dp is a multiple of 64)
+constexpr int kRowBlkStride = kGroupRows * kRowBlk;  // floats between a row's consecutive blocks
+// offset of dim c of a row from its dim 0
+__host__ __device__ inline int64_t row_dim(int c) { return (int64_t)(c / kRowBlk) * kRowBlkStride + c % kRowBlk; }
 // element offset of dim c of row slot `slot` (g * 32 + r)
 __host__ __device__ inline int64_t row_elem(int64_t slot, int c, int dp) {
-  return (slot >> 5) * (int64_t)(kGroupRows * dp) + (int64_t)(c >> 4) * kRowBlkStride + (slot & 31) * kRowBlk + (c & 15);
+  return (slot >> 5) * (int64_t)(kGroupRows * dp) + (slot & 31) * kRowBlk + row_dim(c);
 }
 // offset of a row's 8-dim block b (dims 8b .. 8b + 7) from its dim 0 (row_elem(slot, 0, dp))
-__host__ __device__ inline int row_blk8(int b) { return (b >> 1) * kRowBlkStride + (b & 1) * 8; }
+__host__ __device__ inline int row_blk8(int b) { return (int)row_dim(8 * b); }
 __host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));

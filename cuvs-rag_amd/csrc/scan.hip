@@ -234,7 +234,7 @@ __global__ __launch_bounds__(W * 64, 1) void k_scan(ScanArgs a, float* __restric
       auto bptr = [&](int b) {
         const int bb = b < nb ? b : nb - 1;  // past the end: re-read the last block (never consumed)
         const int gi = bb / bpg;
-        return lane_base + gi * gstride + (bb - gi * bpg) * (BLK * 256);
+        return lane_base + gi * gstride + row_blk8((bb - gi * bpg) * BLK);
       };
       float4 A[BLK], B[BLK];
       load_block<BLK>(A, bptr(0));

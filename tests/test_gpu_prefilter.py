@@ -113,9 +113,18 @@ def test_prefilter_toggle_identical(mivs_lib):
     idx.set_prefilter(True)
     d3, i3 = ivf_flat.search(sp, idx, q, 10)
     assert torch.equal(i1, i3) and torch.equal(d1, d3)
-    # k above kPfMaxK uses the fp32 scan
-    ivf_flat.search(sp, idx, q, 20)
-    assert idx.last_search_stats()["prefilter"] == 0
+    # k above kPfMaxK: K13 + K16, the same bits as the fp32 scan (MIVS_LARGE_K_PF=0)
+    d4, i4 = ivf_flat.search(sp, idx, q, 20)
+    assert idx.last_search_stats()["prefilter"] == 1 and idx.last_search_stats()["scan_kernel"] == 13
+    import os
+
+    os.environ["MIVS_LARGE_K_PF"] = "0"
+    try:
+        d5, i5 = ivf_flat.search(sp, idx, q, 20)
+        assert idx.last_search_stats()["prefilter"] == 0
+    finally:
+        del os.environ["MIVS_LARGE_K_PF"]
+    assert torch.equal(i4, i5) and torch.equal(d4, d5)
 
 
 def test_prefilter_matches_fp32_scan_at_scale(mivs_lib):
