@@ -1105,11 +1105,11 @@ LkPlan lk_plan(const mivs_index_s* idx, int k, int np) {
 }
 
 // queries per K16 batch: the record streams, the windows and the sample's DUMP slots within the large-k workspace
-// (MIVS_LK_WORKSPACE_MB, default 8 GiB; K13 reads every probed row once per batch, so fewer batches are better)
+// (MIVS_LK_WORKSPACE_MB, default 12 GiB; K13 reads every probed row once per batch, so fewer batches are better)
 int64_t lk_batch(const mivs_index_s* idx, int64_t nq, int k, int np) {
   const LkPlan p = lk_plan(idx, k, np);
   const char* e = getenv("MIVS_LK_WORKSPACE_MB");
-  const size_t budget = (size_t)std::max<long long>(e ? atoll(e) : 8192, 1) << 20;
+  const size_t budget = (size_t)std::max<long long>(e ? atoll(e) : 12288, 1) << 20;
   const size_t per_q = (size_t)p.est_cand * (2 * kRsRecInt4 * 16 + 8) + (size_t)lk_cap(k) * 12 +
                        (size_t)p.slots_per_q * ((size_t)idx->G * kGroupRows * 4 + 16);
   return std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t)(budget / std::max<size_t>(per_q, 1))));
