@@ -20,7 +20,6 @@ namespace mivs {
 namespace {
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef int v4i __attribute__((ext_vector_type(4)));
 
 constexpr int kAsWaves = 8;

@@ -133,6 +133,7 @@ struct mivs_index_s {
   // IVF-PQ: codes in the interleaved group layout + codebooks (lists.off/goff/ids/h_* describe the lists)
   int pq_dim = 0, pq_bits = 0, pq_len = 0, pq_dim_pad = 0, rot_dim_pad = 0;
   Buf pq_codes, pq_books;
+  Buf pq_book_norms, pq_books_mfma;  // derived from pq_books at build (launch_pq_book_prep)
   // fp16 copy of the lists for the K10 pre-filter; empty = exact scan only
   Buf groups_h;
   Buf group_nmin;  // K13: the smallest row norm of every 32-row group (built with groups_h)
@@ -742,7 +743,7 @@ mivs_index_memory index_memory(const mivs_index_s* idx) {
   m.centroid_bytes = (int64_t)(listset_bytes(idx->cents) + idx->centroids_rm.n);
   m.fp16_bytes = (int64_t)(idx->groups_h.n + idx->group_nmin.n);
   m.fp8_bytes = (int64_t)idx->groups_f8.n;
-  m.pq_bytes = (int64_t)(idx->pq_codes.n + idx->pq_books.n);
+  m.pq_bytes = (int64_t)(idx->pq_codes.n + idx->pq_books.n + idx->pq_book_norms.n + idx->pq_books_mfma.n);
   m.total_bytes = m.rows_bytes + m.side_bytes + m.centroid_bytes + m.fp16_bytes + m.fp8_bytes + m.pq_bytes;
   m.copies_skipped = idx->copies_skipped;
   return m;
@@ -1347,7 +1348,7 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   HIPCHK(launch_probe_map(ws.probes_full.as<int64_t>(), nq, np, L.n_lists, L.goff.as<int64_t>(), kRsBlockGroups,
                           1 << 30, ws.counts.as<int>(), ws.fill.as<int>(), ws.bucket_off.as<int>(),
                           ws.work_off.as<int>(), ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(),
-                          ws.qp_slots.as<int64_t>(), ws.slot_begin.as<int64_t>(), ws.scan_tmp.p, stb, s));
+                          ws.qp_slots.as<int64_t>(), nullptr, ws.scan_tmp.p, stb, s));  // (no output slots)
   {  // (cheap: n_lists ints)
     ws.stat_counts.reserve(sizeof(int) * L.n_lists);
     HIPCHK(hipMemcpyAsync(ws.stat_counts.p, ws.counts.p, sizeof(int) * L.n_lists, hipMemcpyDeviceToDevice, s));
@@ -1607,6 +1608,8 @@ void pq_search_rt(mivs_index_s* idx, hipStream_t s, const float* d_q, int64_t nq
     a.queries = d_q + b0 * (int64_t)idx->d;
     a.cents = idx->centroids_rm.as<float>();
     a.books = idx->pq_books.as<float>();
+    a.book_norms = idx->pq_book_norms.as<float>();
+    a.books_mfma = idx->pq_books_mfma.as<float>();
     a.codes = static_cast<const uint8_t*>(idx->pq_codes.p);
     a.row_ids = L.ids.as<int64_t>();
     a.list_off = L.off.as<int64_t>();
@@ -2065,6 +2068,11 @@ int32_t mivs_ivf_pq_build(int32_t device, void* stream, const float* d_data, int
       kmeans_fit_impl(rj, rnorm.as<float>(), nullptr, n_pq, pl, dim_pad(pl), nc, p->kmeans_n_iters, bj, idx->G,
                       device, idx->ws, s, p->kmeans_balance != 0);
     }
+    // the codes' norms (the L2 LUT's start) and K9r's MFMA operand copy of the codebooks
+    idx->pq_book_norms.reserve(sizeof(float) * (size_t)p->pq_dim * nc);
+    idx->pq_books_mfma.reserve(sizeof(float) * (size_t)p->pq_dim * nc * pl);
+    HIPCHK(launch_pq_book_prep(idx->pq_books.as<float>(), p->pq_dim, pl, idx->metric == MIVS_METRIC_IP ? 1 : 0,
+                               idx->pq_book_norms.as<float>(), idx->pq_books_mfma.as<float>(), s));
     phase();
     // ---- encode + ids into the interleaved layout ----
     const int64_t slots = std::max<int64_t>(L.n_groups, 1) * kGroupRows;
@@ -2156,6 +2164,7 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
         a.queries = d_q + b0 * (int64_t)idx->d;
         a.cents = idx->centroids_rm.as<float>();
         a.books = idx->pq_books.as<float>();
+        a.book_norms = idx->pq_book_norms.as<float>();
         a.codes = static_cast<const uint8_t*>(idx->pq_codes.p);
         a.row_ids = L.ids.as<int64_t>();
         a.list_off = L.off.as<int64_t>();
@@ -2243,6 +2252,7 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
       a.queries = d_q;
       a.cents = idx->centroids_rm.as<float>();
       a.books = idx->pq_books.as<float>();
+      a.book_norms = idx->pq_book_norms.as<float>();
       a.codes = static_cast<const uint8_t*>(idx->pq_codes.p);
       a.row_ids = L.ids.as<int64_t>();
       a.list_off = L.off.as<int64_t>();
@@ -2285,6 +2295,7 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
       a.queries = d_q;
       a.cents = idx->centroids_rm.as<float>();
       a.books = idx->pq_books.as<float>();
+      a.book_norms = idx->pq_book_norms.as<float>();
       a.codes = static_cast<const uint8_t*>(idx->pq_codes.p);
       a.row_ids = L.ids.as<int64_t>();
       a.list_off = L.off.as<int64_t>();

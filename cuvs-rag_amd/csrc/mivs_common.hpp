@@ -45,6 +45,7 @@ __host__ __device__ inline int row_blk8(int b) { return (int)row_dim(8 * b); }
 __host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------
 // Scan job: (lists of interleaved groups) x (buckets of queries probing them).
@@ -115,6 +116,7 @@ struct PqScanArgs {
   const float* queries;        // [nq][d]
   const float* cents;          // [n_lists][d] row-major
   const float* books;          // [pq_dim][256][pq_len]
+  const float* book_norms;     // [pq_dim][256] the fmaf chain of b_i b_i (L2 LUT start, oracle orc_pq_l2_lut)
   const uint8_t* codes;        // interleaved groups [g][pq_dim_pad/16][32][16]
   const int64_t* row_ids;      // [groups*32]
   const int64_t* list_off;     // [n_lists+1] rows
@@ -146,6 +148,10 @@ struct PqTileArgs {
   const float* queries;
   const float* cents;
   const float* books;
+  const float* book_norms;  // [pq_dim][256] (PqScanArgs)
+  // K9r's MFMA LUT operands [pq_dim][256][4][pq_len/4]: entry (j, c) dim 4s + g at g * pq_len/4 + s, scaled
+  // by -2 (L2) or -1 (IP) -- exact (pq_book_prep)
+  const float* books_mfma;
   const uint8_t* codes;
   const int64_t* row_ids;
   const int64_t* list_off;
@@ -176,7 +182,10 @@ constexpr int kRtQ = 16;
 constexpr int kRtRpt = 8;
 constexpr int kRtRows = kRtThreads * kRtRpt;  // 4096
 constexpr int kRtGroups = kRtRows / 32;
-size_t pq_rt_lds_bytes(int rot_dim_pad, int k);
+size_t pq_rt_lds_bytes(int rot_dim_pad, int pq_dim, int k);
+// book_norms and books_mfma from the codebooks (after training; pq.hip)
+hipError_t launch_pq_book_prep(const float* books, int pq_dim, int pq_len, int ip, float* book_norms,
+                               float* books_mfma, hipStream_t s);
 bool pq_rt_supported(int rot_dim_pad, int pq_dim, int pq_len, int k);
 hipError_t launch_pq_scan_rt(const PqTileArgs& a, int grid, hipStream_t s);
 

@@ -132,11 +132,20 @@ __device__ __forceinline__ void pq_insert(float (&lk)[KCAP], int (&lp)[KCAP], fl
   }
 }
 
-// one term of a LUT entry's chain, dims ascending: L2 (r_i - b_i)^2 into acc (r = q - c_l), IP q_i b_i
+// The search LUT (oracle orc_pq_l2_lut / orc_pq_ip). L2: the expanded form ||r||^2 + ||b||^2 - 2 r.b as one
+// chain -- acc = rn + bn, then fmaf(r_i, -2 b_i, acc), dims ascending (r = q - c_l; rn = the fmaf chain of
+// r_i r_i, bn = the codebook entry's, precomputed in book_norms) -- which K9r runs on MFMA. IP: the chain of
+// q_i b_i from 0, negated by pq_lut_entry.
 __device__ __forceinline__ float pq_lut_term(bool ip, float r, float b, float acc) {
-  if (ip) return fmaf(r, b, acc);
-  const float t = r - b;
-  return fmaf(t, t, acc);
+  return ip ? fmaf(r, b, acc) : fmaf(r, -2.0f * b, acc);
+}
+
+// the chain's start for the entry (j, c): L2 rn_j + bn_jc, IP 0
+__device__ __forceinline__ float pq_lut_start(bool ip, const float* __restrict__ r, int pl, float bn) {
+  if (ip) return 0.0f;
+  float rn = 0.0f;
+  for (int i = 0; i < pl; ++i) rn = fmaf(r[i], r[i], rn);
+  return rn + bn;
 }
 
 // the entry: L2 acc; IP -acc, plus the probe's coarse key -(q . c_l) in subspace 0
@@ -245,7 +254,7 @@ __global__ __launch_bounds__(NT) void k_pq_scan(PqScanArgs a) {
         const int e = base + v * NT;
         if (e >= nlut) break;
         const float* r = s_res + (e >> 8) * pl;
-        float acc = 0.0f;
+        float acc = pq_lut_start(a.ip, r, pl, a.book_norms[e]);
 #pragma unroll
         for (int c4 = 0; c4 < 4; ++c4) {
           if (c4 < nv) {
@@ -262,7 +271,7 @@ __global__ __launch_bounds__(NT) void k_pq_scan(PqScanArgs a) {
       const int j = e >> 8;
       const float* b = a.books + (int64_t)e * pl;
       const float* r = s_res + j * pl;
-      float acc = 0.0f;
+      float acc = pq_lut_start(a.ip, r, pl, a.book_norms[e]);
       for (int i = 0; i < pl; ++i) acc = pq_lut_term(a.ip, r[i], b[i], acc);
       lut[e] = pq_lut_entry(a.ip, acc, e < kPqCodes, base0);
     }
@@ -404,8 +413,9 @@ __global__ __launch_bounds__(NT) void k_pq_scan(PqScanArgs a) {
 // thread keeps V = 8 / PL4 entries' codebook rows (32 floats) in flight before the first FMA; the
 // fmaf chain of K9 / the oracle
 template <int PL4, int NT>
-__device__ __forceinline__ void pq_lut_build(const float* __restrict__ books, const float* res, int nlut, int tid,
-                                             float* lut, bool ip, bool with_base, float base0) {
+__device__ __forceinline__ void pq_lut_build(const float* __restrict__ books, const float* __restrict__ bnorms,
+                                             const float* res, int nlut, int tid, float* lut, bool ip, bool with_base,
+                                             float base0) {
   constexpr int pl = 4 * PL4, V = PL4 >= 4 ? 2 : 8 / PL4;
   for (int base = tid; base < nlut; base += V * NT) {
     float4 bv[V][PL4];
@@ -420,7 +430,7 @@ __device__ __forceinline__ void pq_lut_build(const float* __restrict__ books, co
       const int e = base + v * NT;
       if (e >= nlut) break;
       const float* r = res + (e >> 8) * pl;
-      float acc = 0.0f;
+      float acc = pq_lut_start(ip, r, pl, bnorms[e]);
 #pragma unroll
       for (int c4 = 0; c4 < PL4; ++c4) {
         const float b4[4] = {bv[v][c4].x, bv[v][c4].y, bv[v][c4].z, bv[v][c4].w};
@@ -504,12 +514,13 @@ __global__ __launch_bounds__(256) void k_pq_scan_split(PqScanArgs a) {
       // LUT[j - j0][c] = ||res_j - B_j[c]||^2 for j in [j0, j1): the K9 fmaf chain, entries 4 at a time
       const int nlut = (j1 - j0) * kPqCodes;
       const float* books = a.books + (int64_t)j0 * kPqCodes * pl;
+      const float* bnorms = a.book_norms + (int64_t)j0 * kPqCodes;
       const float* res = s_res + j0 * pl;
       switch (pl >> 2) {
-        case 1: pq_lut_build<1, NT>(books, res, nlut, tid, lut, a.ip, h == 0, base0); break;
-        case 2: pq_lut_build<2, NT>(books, res, nlut, tid, lut, a.ip, h == 0, base0); break;
-        case 3: pq_lut_build<3, NT>(books, res, nlut, tid, lut, a.ip, h == 0, base0); break;
-        default: pq_lut_build<4, NT>(books, res, nlut, tid, lut, a.ip, h == 0, base0); break;
+        case 1: pq_lut_build<1, NT>(books, bnorms, res, nlut, tid, lut, a.ip, h == 0, base0); break;
+        case 2: pq_lut_build<2, NT>(books, bnorms, res, nlut, tid, lut, a.ip, h == 0, base0); break;
+        case 3: pq_lut_build<3, NT>(books, bnorms, res, nlut, tid, lut, a.ip, h == 0, base0); break;
+        default: pq_lut_build<4, NT>(books, bnorms, res, nlut, tid, lut, a.ip, h == 0, base0); break;
       }
       __syncthreads();
       // this half's code chunks of each of my rows (<= 4 x 16 codes), the next row's requested first
@@ -696,11 +707,8 @@ __global__ __launch_bounds__(512) void k_pq_scan_tiled(PqTileArgs a) {
         const int t = e >> 8, c = e & 255;
         const float* r = s_rj + buf * TQ * pl + t * pl;
         const float* b = cb + c * pl;
-        float v = 0.0f;
-        for (int i = 0; i < pl; ++i) {
-          const float dd = r[i] - b[i];
-          v = fmaf(dd, dd, v);
-        }
+        float v = pq_lut_start(false, r, pl, a.book_norms[j * 256 + c]);
+        for (int i = 0; i < pl; ++i) v = pq_lut_term(false, r[i], b[i], v);
         lut[e] = v;
       }
       if (j + 1 < a.pq_dim) load_stage(j + 1, buf ^ 1);
@@ -803,6 +811,7 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
   const int rdp = a.rot_dim_pad;
   float* s_res = reinterpret_cast<float*>(smem + 512);    // [TQ][rdp] residuals (IP: the queries)
   float* s_lut = s_res + TQ * rdp;                        // [2][256][LS]
+  float* s_rn = s_lut + 2 * kPqCodes * LS;                // [pq_dim][TQ] L2: ||r_j||^2 of the tile's queries
   // after the subspace loop (aliasing s_res / s_lut)
   uint32_t* s_min = reinterpret_cast<uint32_t*>(smem + 512);   // [TQ][NT]
   float* s_ck = reinterpret_cast<float*>(s_min + TQ * NT);     // [TQ][CQ]
@@ -811,7 +820,13 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
   int* s_wr = reinterpret_cast<int*>(s_wk + NT / 64);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int c_own = tid & 255, qh = tid >> 8;  // LUT build: code, half of the tile's queries
+  // LUT build on v_mfma_f32_16x16x4_f32, whose result is the chain fma(a3,b3, fma(a2,b2, fma(a1,b1, fma(a0,b0,
+  // c)))) (tools/mfma_f32_order.hip: every output of 1M random trials): wave w builds codes 32w..32w+31 of LUT_j
+  // for the tile as two 16-code blocks. Lane (g = lane >> 4, i = lane & 15) feeds A[i][g] = dim 4s + g of
+  // query i's residual and B[g][i] = dim 4s + g of code 32w + 16cb + i (books_mfma: x(-2) for L2, x(-1) for
+  // IP), so the pl / 4 MFMAs of a block run the oracle's chain over the dims in ascending order from C =
+  // rn_j[query] + bn_j[code] (L2) or 0 (IP). D register r = query 4g + r of code 32w + 16cb + i.
+  const int bg = lane >> 4, bi = lane & 15;
   const int total = a.work_off[a.n_lists];
   for (;;) {
     if (tid == 0) s_misc[0] = atomicAdd(a.work_counter, 1);
@@ -857,50 +872,71 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
         }
       }
     }
+    // residuals (IP: the queries) with each subspace's dims in MFMA operand order: dim 4s + g of subspace j
+    // at j * PL + g * PL4 + s (dims >= pq_dim * PL, if any, as they are)
+    const int rd = a.pq_dim * PL;
     for (int i = tid; i < TQ * rdp; i += NT) {
       const int t = i / rdp, c = i - t * rdp;
       const int64_t q = s_q[t];
       float v = 0.0f;
       if (q >= 0 && c < a.d) v = a.ip ? a.queries[q * a.d + c] : a.queries[q * a.d + c] - a.cents[(int64_t)l * a.d + c];
-      s_res[i] = v;
+      const int jj = c / PL, ii = c - jj * PL;
+      s_res[t * rdp + (c < rd ? jj * PL + (ii & 3) * PL4 + (ii >> 2) : c)] = v;
     }
-    // LUT_j (j < pq_dim) into buffer `buf`: thread (c_own, qh) computes the 8 entries (qh * 8 + u, c_own)
-    float bk[2][PL];  // codebook rows of subspaces j + 1 (parity (j + 1) & 1) and j + 2: no register copies
-    auto load_book = [&](int j, float (&b)[PL]) {
-      const float4* src = reinterpret_cast<const float4*>(a.books + ((int64_t)j * kPqCodes + c_own) * PL);
+    // LUT_j (j < pq_dim) into buffer `buf` (see bg / bi above)
+    float bk[2][2][PL4];  // MFMA B operands of the two code blocks, subspaces j + 1 (parity (j + 1) & 1) and j + 2
+    float bnk[2][2];      // and the codes' norms
+    auto load_book = [&](int j, float (&b)[2][PL4], float (&bn)[2]) {
 #pragma unroll
-      for (int c4 = 0; c4 < PL4; ++c4) {
-        const float4 v = src[c4];
-        b[4 * c4] = v.x; b[4 * c4 + 1] = v.y; b[4 * c4 + 2] = v.z; b[4 * c4 + 3] = v.w;
+      for (int cb = 0; cb < 2; ++cb) {
+        const int c = wave * 32 + cb * 16 + bi;
+        const float* src = a.books_mfma + ((int64_t)j * kPqCodes + c) * PL + bg * PL4;
+#pragma unroll
+        for (int u = 0; u < PL4; ++u) b[cb][u] = src[u];
+        bn[cb] = a.book_norms[j * kPqCodes + c];
       }
     };
-    auto build = [&](int j, const float (&b)[PL], int buf) {
-      float e[8];
+    auto build = [&](int j, const float (&b)[2][PL4], const float (&bn)[2], int buf) {
+      float ra[PL4];
+      const float* rsrc = s_res + bi * rdp + j * PL + bg * PL4;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int t = qh * 8 + u;
-        const float4* r4 = reinterpret_cast<const float4*>(s_res + t * rdp + j * PL);
-        float acc = 0.0f;
+      for (int u = 0; u < PL4; ++u) ra[u] = rsrc[u];
+      float4 rn = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      if (!a.ip) rn = *reinterpret_cast<const float4*>(s_rn + j * TQ + 4 * bg);
 #pragma unroll
-        for (int c4 = 0; c4 < PL4; ++c4) {
-          const float4 r = r4[c4];
-          acc = pq_lut_term(a.ip, r.x, b[4 * c4], acc);
-          acc = pq_lut_term(a.ip, r.y, b[4 * c4 + 1], acc);
-          acc = pq_lut_term(a.ip, r.z, b[4 * c4 + 2], acc);
-          acc = pq_lut_term(a.ip, r.w, b[4 * c4 + 3], acc);
+      for (int cb = 0; cb < 2; ++cb) {
+        f32x4 acc;
+        if (!a.ip) {
+          acc[0] = rn.x + bn[cb]; acc[1] = rn.y + bn[cb]; acc[2] = rn.z + bn[cb]; acc[3] = rn.w + bn[cb];
+        } else {
+          acc[0] = 0.0f; acc[1] = 0.0f; acc[2] = 0.0f; acc[3] = 0.0f;
         }
-        e[u] = pq_lut_entry(a.ip, acc, j == 0, s_base[t]);
-        __builtin_amdgcn_sched_barrier(0);  // one entry's residual reads in flight
+#pragma unroll
+        for (int u = 0; u < PL4; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[u], b[cb][u], acc, 0, 0, 0);
+        if (a.ip && j == 0) {  // the probe's coarse key in subspace 0 (pq_lut_entry)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[r] = acc[r] + s_base[4 * bg + r];
+        }
+        *reinterpret_cast<float4*>(s_lut + (buf * kPqCodes + wave * 32 + cb * 16 + bi) * LS + 4 * bg) =
+            make_float4(acc[0], acc[1], acc[2], acc[3]);
       }
-      float4* dst = reinterpret_cast<float4*>(s_lut + (buf * kPqCodes + c_own) * LS + qh * 8);
-      dst[0] = make_float4(e[0], e[1], e[2], e[3]);
-      dst[1] = make_float4(e[4], e[5], e[6], e[7]);
     };
-    load_book(0, bk[0]);
-    if (a.pq_dim > 1) load_book(1, bk[1]);
+    load_book(0, bk[0], bnk[0]);
+    if (a.pq_dim > 1) load_book(1, bk[1], bnk[1]);
     __syncthreads();  // s_res, s_base
-    if (!(a.flags & 1)) build(0, bk[0], 0);
-    if (a.pq_dim > 2) load_book(2, bk[0]);
+    if (!a.ip) {  // rn_j of the tile's queries: the fmaf chain of r_i r_i, dims ascending (pq_lut_start)
+      for (int e = tid; e < a.pq_dim * TQ; e += NT) {
+        const int j = e / TQ, t = e - j * TQ;
+        const float* r = s_res + t * rdp + j * PL;
+        float rn = 0.0f;
+#pragma unroll
+        for (int i = 0; i < PL; ++i) rn = fmaf(r[(i & 3) * PL4 + (i >> 2)], r[(i & 3) * PL4 + (i >> 2)], rn);
+        s_rn[e] = rn;
+      }
+      __syncthreads();
+    }
+    if (!(a.flags & 1)) build(0, bk[0], bnk[0], 0);
+    if (a.pq_dim > 2) load_book(2, bk[0], bnk[0]);
 
     // my rows: i * NT + tid of the chunk; their codes, 16 subspaces (one uint4) per chunk ch
     float acc[RPT][TQ];
@@ -936,8 +972,8 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
         const int j = wq * 4 + b;
         __syncthreads();  // LUT_j complete; LUT_{j-1}'s buffer free
         if (j + 1 < a.pq_dim) {  // (b is static: j's parity is b's)
-          if (!(a.flags & 1)) build(j + 1, bk[(b + 1) & 1], (b + 1) & 1);
-          if (j + 3 < a.pq_dim) load_book(j + 3, bk[(b + 1) & 1]);
+          if (!(a.flags & 1)) build(j + 1, bk[(b + 1) & 1], bnk[(b + 1) & 1], (b + 1) & 1);
+          if (j + 3 < a.pq_dim) load_book(j + 3, bk[(b + 1) & 1], bnk[(b + 1) & 1]);
         }
         const float* lut = s_lut + (j & 1) * (kPqCodes * LS);
 #pragma unroll
@@ -1146,8 +1182,8 @@ hipError_t launch_pq_scan_tiled(const PqTileArgs& a, int kcap, int grid, hipStre
 
 static int pq_rt_cq(int k) { return k > 64 ? 0 : (k <= 16 ? 128 : 512); }
 
-size_t pq_rt_lds_bytes(int rot_dim_pad, int k) {
-  const size_t loop = (size_t)kRtQ * rot_dim_pad * 4 + (size_t)2 * kPqCodes * 20 * 4;
+size_t pq_rt_lds_bytes(int rot_dim_pad, int pq_dim, int k) {
+  const size_t loop = (size_t)kRtQ * rot_dim_pad * 4 + (size_t)2 * kPqCodes * 20 * 4 + (size_t)pq_dim * kRtQ * 4;
   const size_t sel = (size_t)kRtQ * kRtThreads * 4 + (size_t)kRtQ * pq_rt_cq(k) * 8;
   return 512 + (loop > sel ? loop : sel);
 }
@@ -1155,7 +1191,7 @@ size_t pq_rt_lds_bytes(int rot_dim_pad, int k) {
 bool pq_rt_supported(int rot_dim_pad, int pq_dim, int pq_len, int k) {
   return (pq_len & 3) == 0 && pq_len >= 4 && pq_len <= 16 && rot_dim_pad % 4 == 0 && k >= 1 &&
          (pq_dim & 3) == 0 &&
-         k <= kMaxSelectK && pq_rt_lds_bytes(rot_dim_pad, k) <= 160 * 1024;
+         k <= kMaxSelectK && pq_rt_lds_bytes(rot_dim_pad, pq_dim, k) <= 160 * 1024;
 }
 
 template <int PL4, int CQ>
@@ -1176,11 +1212,37 @@ static hipError_t launch_pq_rt_pl(const PqTileArgs& a, int grid, size_t lds, hip
   }
 }
 
+namespace {
+// entry e = (j, c): the fmaf chain of b_i b_i (dims ascending, from 0), and K9r's MFMA operand copy of the
+// row (dim 4s + g at g * pl / 4 + s, times -2 for L2 / -1 for IP: exact)
+__global__ void k_pq_book_prep(const float* __restrict__ books, int n, int pl, float scale, float* __restrict__ norms,
+                               float* __restrict__ mf) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const float* b = books + (int64_t)e * pl;
+  float bn = 0.0f;
+  for (int i = 0; i < pl; ++i) {
+    bn = fmaf(b[i], b[i], bn);
+    mf[(int64_t)e * pl + ((pl & 3) ? i : (i & 3) * (pl / 4) + (i >> 2))] = scale * b[i];  // (pl % 4: no K9r)
+  }
+  norms[e] = bn;
+}
+}  // namespace
+
+hipError_t launch_pq_book_prep(const float* books, int pq_dim, int pq_len, int ip, float* book_norms,
+                               float* books_mfma, hipStream_t s) {
+  const int n = pq_dim * kPqCodes;
+  hipLaunchKernelGGL(k_pq_book_prep, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, books, n, pq_len,
+                     ip ? -1.0f : -2.0f, book_norms, books_mfma);
+  return hipGetLastError();
+}
+
 hipError_t launch_pq_scan_rt(const PqTileArgs& a, int grid, hipStream_t s) {
   if (!pq_rt_supported(a.rot_dim_pad, a.pq_dim, a.pq_len, a.k)) return hipErrorInvalidValue;
+  if (a.books_mfma == nullptr || a.book_norms == nullptr) return hipErrorInvalidValue;
   if (pq_rt_cq(a.k) == 0 && a.slot_info == nullptr) return hipErrorInvalidValue;
   if (a.ip && (a.probes == nullptr || a.probes_d == nullptr)) return hipErrorInvalidValue;
-  const size_t lds = pq_rt_lds_bytes(a.rot_dim_pad, a.k);
+  const size_t lds = pq_rt_lds_bytes(a.rot_dim_pad, a.pq_dim, a.k);
   switch (a.pq_len >> 2) {
     case 1: return launch_pq_rt_pl<1>(a, grid, lds, s);
     case 2: return launch_pq_rt_pl<2>(a, grid, lds, s);

@@ -362,6 +362,7 @@ hipError_t launch_probe_map(const int64_t* probes, int64_t nq, int np, int n_lis
   else
     hipLaunchKernelGGL(k_probe_fill, grid1(n, 256), dim3(256), 0, s, probes, n, np, bucket_off, fill, bucket_q,
                        bucket_slot, list_goff, chunk_groups, qp_slots);
+  if (slot_begin == nullptr) return hipGetLastError();  // (K13: no per-(query, probe) output slots)
   e = launch_exclusive_scan_i64(qp_slots, qp_base, n, stmp, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_bucket_slot, grid1(n, 256), dim3(256), 0, s, bucket_slot, n, qp_base);

@@ -440,6 +440,24 @@ float orc_pq_l2(const float* a, const float* b, int pl) {
   return acc;
 }
 
+/* The search LUT's L2 entry (round 4: the expanded form, so that the GPU builds it on MFMA,
+ * pq.hip k_pq_scan_rt): ||r - b||^2 = ||r||^2 + ||b||^2 - 2 r.b, as
+ *   rn = fmaf chain of r_i r_i, bn = fmaf chain of b_i b_i (i ascending, from 0),
+ *   acc = rn + bn, then acc = fmaf(r_i, -2 b_i, acc) for i ascending.
+ * v_mfma_f32_16x16x4_f32 computes fma(a3,b3, fma(a2,b2, fma(a1,b1, fma(a0,b0, c)))) (measured:
+ * tools/mfma_f32_order.hip), so MFMA s fed dims 4s..4s+3
+ * with c = rn + bn is this chain; -2 b_i is exact. cuVS builds the difference form
+ * (ivf_pq compute_similarity); the two agree to fp32 rounding (tests/test_oracle_pq.py checks the ranking
+ * against fp64 ||q - x_hat||^2). The encoder's argmin keeps the difference form (orc_pq_l2). */
+float orc_pq_l2_lut(const float* r, const float* b, int pl) {
+  float rn = 0.0f, bn = 0.0f;
+  for (int i = 0; i < pl; ++i) rn = fmaf(r[i], r[i], rn);
+  for (int i = 0; i < pl; ++i) bn = fmaf(b[i], b[i], bn);
+  float acc = rn + bn;
+  for (int i = 0; i < pl; ++i) acc = fmaf(r[i], -2.0f * b[i], acc);
+  return acc;
+}
+
 /* residual sub-vector j (pq_len dims) of row x w.r.t. centre c; dims >= d are 0 */
 /* the IP LUT entry's dot, dims ascending (the GPU K9/K9s chain): -(sum_i q_i b_i) */
 float orc_pq_ip(const float* a, const float* b, int pl) {
@@ -533,7 +551,8 @@ void orc_ivfpq_build(const float* x, int64_t n, int d, int n_lists, int iters, d
 }
 
 /* IVF-PQ search (cuvs.neighbors.ivf_pq.search, improved_multi_gpu_rag.py:228-230). metric ORC_L2: a row's key
- * is sum_j LUT_j[code_j] (j ascending, from 0) with LUT_j[c] = ||(q - c_l)_j - B_j[c]||^2. ORC_IP: LUT_j[c] =
+ * is sum_j LUT_j[code_j] (j ascending, from 0) with LUT_j[c] = ||(q - c_l)_j - B_j[c]||^2 in the expanded form
+ * of orc_pq_l2_lut. ORC_IP: LUT_j[c] =
  * -(q_j . B_j[c]) and subspace 0's row also carries the probe's coarse key -(q . c_l) (orc_dot), so the key
  * estimates -(q . x_hat); distances out are the inner products (-key). Probes rank by the metric's key. */
 void orc_ivfpq_search(const float* centroids, int n_lists, int d, const float* codebooks, int pq_dim, int pq_bits,
@@ -577,7 +596,7 @@ void orc_ivfpq_search(const float* centroids, int n_lists, int d, const float* c
         } else {
           pq_residual(qq, centroids + (int64_t)l * d, d, j, pl, r);
           for (int c = 0; c < nc; ++c)
-            lut[j * nc + c] = orc_pq_l2(r, codebooks + ((int64_t)j * nc + c) * pl, pl);
+            lut[j * nc + c] = orc_pq_l2_lut(r, codebooks + ((int64_t)j * nc + c) * pl, pl);
         }
       }
       for (int64_t m = offs[l]; m < offs[l + 1]; ++m) {

@@ -81,6 +81,7 @@ void orc_ivf_search(const float* x, int64_t id_offset, int d, const float* centr
 int orc_pq_len(int d, int pq_dim);
 int64_t orc_pq_train_count(int64_t n, int pq_bits, int64_t max_per_code);
 float orc_pq_l2(const float* a, const float* b, int pl);
+float orc_pq_l2_lut(const float* r, const float* b, int pl);
 float orc_pq_ip(const float* a, const float* b, int pl);
 void orc_ivfpq_train_codebooks(const float* x, int64_t n, int d, const float* centroids, const int32_t* labels,
                                int pq_dim, int pq_bits, int iters, int balance, int64_t max_per_code,
