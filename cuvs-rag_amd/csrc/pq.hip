@@ -913,6 +913,11 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
         }
 #pragma unroll
         for (int u = 0; u < PL4; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[u], b[cb][u], acc, 0, 0, 0);
+        // the result is read next by an LDS store: the wait states of an XDL result read as LDS data, explicit
+        // (the compiler placed the store one instruction after the MFMA: 12 % of the LUT entries were stale)
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
         if (a.ip && j == 0) {  // the probe's coarse key in subspace 0 (pq_lut_entry)
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[r] = acc[r] + s_base[4 * bg + r];

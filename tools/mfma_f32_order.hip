@@ -41,6 +41,20 @@ __global__ void k16(const float* A, const float* B, const float* C, float* D) {
   for (int r = 0; r < 4; ++r) D[t * 256 + (4 * kk + r) * 16 + i] = c[r];
 }
 
+// two chained MFMAs (dims 0..3, then 4..7): A [16][8], B [8][16] per trial
+__global__ void k16x2(const float* A, const float* B, const float* C, float* D) {
+  const int t = blockIdx.x, l = threadIdx.x;
+  const int i = l & 15, kk = l >> 4;
+  f32x4 c;
+  for (int r = 0; r < 4; ++r) c[r] = C[t * 256 + (4 * kk + r) * 16 + i];
+  for (int u = 0; u < 2; ++u) {
+    const float a = A[t * 128 + i * 8 + 4 * u + kk];
+    const float b = B[t * 128 + (4 * u + kk) * 16 + i];
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+  for (int r = 0; r < 4; ++r) D[t * 256 + (4 * kk + r) * 16 + i] = c[r];
+}
+
 // control: A [32][2], B [2][32], C [32][32]
 __global__ void k32(const float* A, const float* B, const float* C, float* D) {
   const int t = blockIdx.x, l = threadIdx.x;
@@ -102,6 +116,35 @@ int main() {
         m_pair += pr == d;
       }
   printf("16x16x4f32: %ld outputs | chain %ld rchain %ld exact %ld pair %ld\n", n, m_chain, m_rchain, m_exact, m_pair);
+  {  // two chained MFMAs against the 8-step chain
+    std::vector<float> A2(T * 128), B2(T * 128);
+    for (auto& v : A2) v = rnd(g);
+    for (auto& v : B2) v = rnd(g);
+    float *dA2, *dB2;
+    CHECK(hipMalloc(&dA2, A2.size() * 4));
+    CHECK(hipMalloc(&dB2, B2.size() * 4));
+    CHECK(hipMemcpy(dA2, A2.data(), A2.size() * 4, hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(dB2, B2.data(), B2.size() * 4, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k16x2, dim3(T), dim3(64), 0, 0, dA2, dB2, dC, dD);
+    CHECK(hipGetLastError());
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipMemcpy(D.data(), dD, D.size() * 4, hipMemcpyDeviceToHost));
+    long n2 = 0, m2 = 0, m2s = 0;
+    for (int t = 0; t < T; ++t)
+      for (int i = 0; i < 16; ++i)
+        for (int j = 0; j < 16; ++j) {
+          const float c = C[t * 256 + i * 16 + j], d = D[t * 256 + i * 16 + j];
+          float ch = c;
+          for (int k = 0; k < 8; ++k) ch = fmaf(A2[t * 128 + i * 8 + k], B2[t * 128 + k * 16 + j], ch);
+          float h0 = c, h1 = 0.0f;  // each MFMA's own chain, the two rounded sums added
+          for (int k = 0; k < 4; ++k) h0 = fmaf(A2[t * 128 + i * 8 + k], B2[t * 128 + k * 16 + j], h0);
+          for (int k = 4; k < 8; ++k) h1 = fmaf(A2[t * 128 + i * 8 + k], B2[t * 128 + k * 16 + j], h1);
+          ++n2;
+          m2 += ch == d;
+          m2s += (h0 + h1) == d;
+        }
+    printf("16x16x4f32 x2 chained: %ld outputs | 8-step chain %ld split-sum %ld\n", n2, m2, m2s);
+  }
   // control 32x32x2
   std::vector<float> C2(T * 1024), D2(T * 1024);
   for (auto& v : C2) v = rnd(g);
