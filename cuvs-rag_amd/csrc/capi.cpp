@@ -88,8 +88,14 @@ struct Workspace {
   // fp16 pre-filter path (K10 / K11) and its exact-scan fallback
   Buf qh, qscale, qres, qtheta, pf_key, pf_pos, pf_bound, pf_stats, ovf_q, ovf_rows, ovf_d, ovf_i;
   Buf q8, qscale8;  // K13's fp8 nomination: the queries' fp8 copy and scales
+  // the batch whose qn / qh / qscale / qres (and, prep_f8, q8 / qscale8) launch_queries_prep wrote at the start of the
+  // search (pf_scan_refine skips its own conversions for it)
+  HostBuf h_stats;  // pinned: the refine's fallback count and window size
+  const float* prep_q = nullptr;
+  int64_t prep_nq = 0;
+  bool prep_f8 = false;
   // K13 row-stationary scan: the full probe list, the pre-pass result, per-query headers and candidates
-  Buf probes_full, pre_kth, pre_goff, qhdr, rs_tq, cand_off, cand_key, cand_pos, rs_bucket_tmp, rs_tiles, rs_wave_buf,
+  Buf pre_probes, pre_kth, pre_goff, qhdr, rs_tq, cand_off, cand_key, cand_pos, rs_bucket_tmp, rs_tiles, rs_wave_buf,
       rs_wave_cnt, rs_bounds;
   // per-list query counts of the last search's own probe map (an exact fallback re-maps its queries)
   Buf stat_counts, rs_ovf_q, rs_ovf_rows, rs_ovf_d, rs_ovf_i, rs_items;
@@ -808,6 +814,8 @@ void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t 
                       int64_t* out_i, int32_t* out_probes, bool allow_pf = true, bool prof = true,
                       bool allow_rs = true);
 bool lk_use(const mivs_index_s* idx, int k, int np);
+bool rs_use(const mivs_index_s* idx, int np);
+bool rs_pre_f8(mivs_index_s* idx, hipStream_t);
 int64_t lk_batch(const mivs_index_s* idx, int64_t nq, int k, int np);
 void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                        int64_t* out_i, bool pf, ProfRec* pr, bool prof, const int64_t* probes = nullptr,
@@ -830,11 +838,13 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   Workspace& ws = idx->ws;
   const ListSet& L = idx->lists;
   const int dp = idx->dp;
+  const bool prepped = ws.prep_q == q && ws.prep_nq == nq;  // (launch_queries_prep wrote them for this batch)
   ws.qh.reserve(sizeof(uint16_t) * (size_t)nq * dp);
   ws.qscale.reserve(sizeof(float) * nq);
   ws.qres.reserve(sizeof(float) * nq);
-  HIPCHK(launch_queries_to_half(q, nq, idx->d, dp, idx->hx_exp, ws.qh.as<uint16_t>(), ws.qscale.as<float>(),
-                                ws.qres.as<float>(), s));
+  if (!prepped)
+    HIPCHK(launch_queries_to_half(q, nq, idx->d, dp, idx->hx_exp, ws.qh.as<uint16_t>(), ws.qscale.as<float>(),
+                                  ws.qres.as<float>(), s));
   const std::vector<int64_t>& tcp = idx->pf_top_chunks_prefix;
   const int64_t max_slots = std::max<int64_t>(1, nq * tcp[std::min<int64_t>(np, L.n_lists)]);
   // per-slot candidates: room above k so that a neighbourhood packed into one chunk does not overflow
@@ -859,7 +869,8 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   if (f8) {  // K13's fp8 nomination: the fp8 queries beside the fp16 ones (the headers and tiles use those)
     ws.q8.reserve((size_t)nq * dp);
     ws.qscale8.reserve(sizeof(float) * nq);
-    HIPCHK(launch_queries_to_f8(q, nq, idx->d, dp, idx->hx8, ws.q8.as<uint8_t>(), ws.qscale8.as<float>(), s));
+    if (!(prepped && ws.prep_f8))
+      HIPCHK(launch_queries_to_f8(q, nq, idx->d, dp, idx->hx8, ws.q8.as<uint8_t>(), ws.qscale8.as<float>(), s));
     a.groups_f8 = idx->groups_f8.as<uint8_t>();
     a.q8 = ws.q8.as<uint8_t>();
     a.qscale8 = ws.qscale8.as<float>();
@@ -927,7 +938,7 @@ void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_
   const ListSet& L = idx->lists;
   const int dp = idx->dp;
   ws.pf_stats.reserve(32);
-  HIPCHK(hipMemsetAsync(ws.pf_stats.p, 0, 32, s));
+  if (!kth_out) HIPCHK(hipMemsetAsync(ws.pf_stats.p, 0, 32, s));  // (the k-th-only modes leave the stats alone)
   ws.ovf_q.reserve(sizeof(int64_t) * nq);
   PfRefineArgs r{};
   r.slot_key = slot_key;
@@ -959,9 +970,10 @@ void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_
   r.n_window = reinterpret_cast<int64_t*>(ws.pf_stats.as<char>() + 8);
   HIPCHK(launch_pf_refine(r, s));
   if (kth_out) return;
-  int64_t h[2] = {0, 0};
+  ws.h_stats.reserve(16);
+  int64_t* h = ws.h_stats.as<int64_t>();
   HIPCHK(hipMemcpyAsync(h, ws.pf_stats.p, 16, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));  // the only host sync of the search: the fallback size
+  spin_wait(s);  // the only host sync of the search: the fallback size
   const int64_t novf = (int64_t)(int32_t)(h[0] & 0xFFFFFFFF);
   idx->last_ovf += novf;
   idx->last_window += h[1];
@@ -1023,7 +1035,26 @@ void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t 
   ProfRec* pr = prof && g_profiling.load() ? idx->prof.begin(s) : nullptr;
   const bool pf = allow_pf && idx->groups_h.p != nullptr && (k <= kPfMaxK || (allow_rs && lk_use(idx, k, np)));
   ws.qn.reserve(sizeof(float) * nq);
-  HIPCHK(launch_row_norms(q, nq, idx->d, ws.qn.as<float>(), s));
+  // the pre-filter search's query conversions in the same pass as the norms (one read of the batch)
+  ws.prep_q = nullptr;
+  if (pf && idx->d % 4 == 0 && (reinterpret_cast<uintptr_t>(q) & 15) == 0 && idx->dp <= 1024) {
+    const bool f8 = rs_use(idx, np) && k <= kPfMaxK && rs_pre_f8(idx, s);
+    ws.qh.reserve(sizeof(uint16_t) * (size_t)nq * idx->dp);
+    ws.qscale.reserve(sizeof(float) * nq);
+    ws.qres.reserve(sizeof(float) * nq);
+    if (f8) {
+      ws.q8.reserve((size_t)nq * idx->dp);
+      ws.qscale8.reserve(sizeof(float) * nq);
+    }
+    HIPCHK(launch_queries_prep(q, nq, idx->d, idx->dp, idx->hx_exp, idx->hx8, ws.qn.as<float>(), ws.qh.as<uint16_t>(),
+                               ws.qscale.as<float>(), ws.qres.as<float>(), f8 ? ws.q8.as<uint8_t>() : nullptr,
+                               f8 ? ws.qscale8.as<float>() : nullptr, s));
+    ws.prep_q = q;
+    ws.prep_nq = nq;
+    ws.prep_f8 = f8;
+  } else {
+    HIPCHK(launch_row_norms(q, nq, idx->d, ws.qn.as<float>(), s));
+  }
   // coarse: top-n_probes centroids per query
   ws.probes_d.reserve(sizeof(float) * nq * np);
   ws.probes_i.reserve(sizeof(int64_t) * nq * np);
@@ -1127,7 +1158,7 @@ void lk_prepass(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, in
   HIPCHK(launch_rs_pre_lists(L.goff.as<int64_t>(), L.n_lists, p.div, 1, nullptr, 0, np, ws.pre_goff.as<int64_t>(),
                              nullptr, s));
   ws.lk_probes.reserve(sizeof(int64_t) * ne);
-  HIPCHK(launch_lk_sample_probes(ws.probes_full.as<int64_t>(), ne, ws.lk_probes.as<int64_t>(), s));
+  HIPCHK(launch_lk_sample_probes(ws.probes_i.as<int64_t>(), ne, ws.lk_probes.as<int64_t>(), s));
   ws.counts.reserve(sizeof(int) * nl2);
   ws.fill.reserve(sizeof(int) * nl2);
   ws.bucket_off.reserve(sizeof(int) * (nl2 + 1));
@@ -1154,7 +1185,7 @@ void lk_prepass(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, in
   j.n_lists = nl2;
   run_scan(j, idx->device, ws, s);
   ws.pre_kth.reserve(sizeof(float) * nq);
-  HIPCHK(launch_lk_sample_kth(ws.probes_full.as<int64_t>(), nq, np, L.off.as<int64_t>(), ws.pre_goff.as<int64_t>(), k,
+  HIPCHK(launch_lk_sample_kth(ws.probes_i.as<int64_t>(), nq, np, L.off.as<int64_t>(), ws.pre_goff.as<int64_t>(), k,
                               kLkSampleZ, ws.part_d.as<float>(), ws.part_i.as<int64_t>(), ws.slot_begin.as<int64_t>(),
                               (int)slot_rows, ws.pre_kth.as<float>(), s));
   // the fp16 queries, their scales and residuals for the headers and tiles
@@ -1234,7 +1265,7 @@ void lk_finish(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   HIPCHK(launch_lk_sort(a, s));
   int64_t h[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(h, ws.pf_stats.p, 16, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));  // the fallback size
+  spin_wait(s);  // the fallback size
   const int64_t novf = (int64_t)(int32_t)(h[0] & 0xFFFFFFFF);
   idx->last_ovf += novf;
   idx->last_window += h[1];
@@ -1266,8 +1297,8 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   const int dp = idx->dp;
   const int64_t ne = nq * np;
   const bool large = k > kPfMaxK;
-  ws.probes_full.reserve(sizeof(int64_t) * ne);
-  HIPCHK(hipMemcpyAsync(ws.probes_full.p, ws.probes_i.p, sizeof(int64_t) * ne, hipMemcpyDeviceToDevice, s));
+  // ws.probes_i keeps every query's probes; the pre-pass's one split list per query goes to ws.pre_probes
+  ws.pre_probes.reserve(sizeof(int64_t) * nq);
   LkPlan plan;
   bool pre_f8 = false;
   int pre_div = 0, pre_sel = 0;
@@ -1286,8 +1317,8 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
     const char* pde = getenv("MIVS_RS_PRE_DIV");
     pre_div = std::max(1, pde ? atoi(pde) : (pre_f8 ? kRsPreDivF8 : kRsPreDiv));
     HIPCHK(launch_rs_pre_lists(L.goff.as<int64_t>(), L.n_lists, pre_div, ceil_div(k, kGroupRows),
-                               ws.probes_full.as<int64_t>(), nq, np, ws.pre_goff.as<int64_t>(),
-                               ws.probes_i.as<int64_t>(), s));
+                               ws.probes_i.as<int64_t>(), nq, np, ws.pre_goff.as<int64_t>(),
+                               ws.pre_probes.as<int64_t>(), s));
     const int nl2 = 2 * L.n_lists;
     ws.counts.reserve(sizeof(int) * nl2);
     ws.fill.reserve(sizeof(int) * nl2);
@@ -1299,7 +1330,7 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
     ws.slot_begin.reserve(sizeof(int64_t) * (nq + 1));
     const size_t stb = scan_tmp_bytes(nq) + sizeof(int64_t) * (size_t)nq;
     ws.scan_tmp.reserve(stb);
-    HIPCHK(launch_probe_map(ws.probes_i.as<int64_t>(), nq, 1, nl2, ws.pre_goff.as<int64_t>(), idx->pf_G, kPfQTile,
+    HIPCHK(launch_probe_map(ws.pre_probes.as<int64_t>(), nq, 1, nl2, ws.pre_goff.as<int64_t>(), idx->pf_G, kPfQTile,
                             ws.counts.as<int>(), ws.fill.as<int>(), ws.bucket_off.as<int>(), ws.work_off.as<int>(),
                             ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(), ws.qp_slots.as<int64_t>(),
                             ws.slot_begin.as<int64_t>(), ws.scan_tmp.p, stb, s));
@@ -1345,7 +1376,7 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   ws.slot_begin.reserve(sizeof(int64_t) * (nq + 1));
   const size_t stb = scan_tmp_bytes(ne) + sizeof(int64_t) * (size_t)ne;
   ws.scan_tmp.reserve(stb);
-  HIPCHK(launch_probe_map(ws.probes_full.as<int64_t>(), nq, np, L.n_lists, L.goff.as<int64_t>(), kRsBlockGroups,
+  HIPCHK(launch_probe_map(ws.probes_i.as<int64_t>(), nq, np, L.n_lists, L.goff.as<int64_t>(), kRsBlockGroups,
                           1 << 30, ws.counts.as<int>(), ws.fill.as<int>(), ws.bucket_off.as<int>(),
                           ws.work_off.as<int>(), ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(),
                           ws.qp_slots.as<int64_t>(), nullptr, ws.scan_tmp.p, stb, s));  // (no output slots)
@@ -1365,8 +1396,14 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   ws.rs_items.reserve(sizeof(int4) * (size_t)std::max<int64_t>(max_items, 1));
   // items dealt from 8 queues of equal tile work, dynamically inside a queue
   ws.rs_bounds.reserve(sizeof(int) * 9);
+  const int grid = std::max(8, cu_count(idx->device) / 8 * 8);
+  const int n_waves = grid * kRsWaves;
+  // the wave stream counts + the lost flag, the 8 item-queue counters, the spun-out wave count (the last 10 are
+  // zeroed by k_rs_items)
+  ws.rs_wave_cnt.reserve(sizeof(int) * (n_waves + 1 + 8 + 1));
   HIPCHK(launch_rs_items(ws.work_off.as<int>(), ws.bucket_off.as<int>(), L.goff.as<int64_t>(), L.n_lists,
-                         (int)max_items, ws.rs_items.as<int4>(), ws.rs_bounds.as<int>(), s));
+                         (int)max_items, ws.rs_items.as<int4>(), ws.rs_bounds.as<int>(), s,
+                         ws.rs_wave_cnt.as<int>() + n_waves, 10));
   RsScanArgs a{};
   a.groups_h = idx->groups_h.as<uint16_t>();
   a.row_norms = L.norms.as<float>();
@@ -1381,19 +1418,14 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   a.group_nmin = idx->group_nmin.as<float>();
   a.nq = (int)nq;
   a.metric = idx->metric;
-  const int grid = std::max(8, cu_count(idx->device) / 8 * 8);
-  const int n_waves = grid * kRsWaves;
   idx->last_rs_waves = n_waves;
   idx->last_rs_nq = nq;
   a.wave_cap = rs_wave_cap(nq, k, plan.est_cand, n_waves);
   ws.rs_wave_buf.reserve(sizeof(int4) * kRsRecInt4 * (size_t)n_waves * a.wave_cap);
-  // + the lost flag, the 8 item-queue counters, the spun-out wave count
-  ws.rs_wave_cnt.reserve(sizeof(int) * (n_waves + 1 + 8 + 1));
   a.wave_buf = ws.rs_wave_buf.as<int4>();
   a.wave_cnt = ws.rs_wave_cnt.as<int>();
   a.queue = a.wave_cnt + n_waves + 1;
   a.bounds = ws.rs_bounds.as<int>();
-  HIPCHK(hipMemsetAsync(a.wave_cnt + n_waves, 0, sizeof(int) * 10, s));  // lost flag, queue counters, spun-out
   a.flags = getenv("MIVS_RS_FLAGS") ? atoi(getenv("MIVS_RS_FLAGS")) : 0;
   if (a.flags & 2) a.flags |= 1;  // stale LDS tiles: never run an epilogue on them
   Buf pbuf;
@@ -1459,7 +1491,7 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
                                 ws.cand_off.as<int64_t>(), ws.rs_bucket_tmp.p, a.wave_cnt + n_waves, s));
   int64_t total = 0;
   HIPCHK(hipMemcpyAsync(&total, ws.cand_off.as<int64_t>() + nq, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
+  spin_wait(s);
   ws.cand_key.reserve(sizeof(float) * (size_t)std::max<int64_t>(total, 1));
   ws.cand_pos.reserve(sizeof(int) * (size_t)std::max<int64_t>(total, 1));
   HIPCHK(launch_rs_bucket_scatter(a.wave_buf, a.wave_cap, a.wave_cnt, n_waves, (int)nq, qhdr, a.row_norms, idx->metric,

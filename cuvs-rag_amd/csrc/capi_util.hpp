@@ -76,6 +76,41 @@ struct Buf {
   T* as() const { return static_cast<T*>(p); }
 };
 
+// pinned host memory for the search's small device-to-host reads (hipHostMalloc: the copy is a DMA the host
+// can poll for, not a staged pageable copy)
+struct HostBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  HostBuf() = default;
+  HostBuf(const HostBuf&) = delete;
+  HostBuf& operator=(const HostBuf&) = delete;
+  ~HostBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  void reserve(size_t bytes) {
+    if (bytes <= n && p) return;
+    if (p) {
+      HIPCHK(hipDeviceSynchronize());
+      (void)hipHostFree(p);
+    }
+    p = nullptr;
+    HIPCHK(hipHostMalloc(&p, bytes > 0 ? bytes : 16, hipHostMallocDefault));
+    n = bytes;
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+// Wait for the stream by polling it: the search's one host sync (the fallback size) sits on the step's critical
+// path, and a blocking wait's wake-up adds tens of microseconds to every batch
+inline void spin_wait(hipStream_t s) {
+  for (;;) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) HIPCHK(e);
+  }
+}
+
 inline int cu_count(int device) {
   static std::mutex mu;
   static std::vector<int> cache;

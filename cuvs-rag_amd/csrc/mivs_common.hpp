@@ -471,7 +471,8 @@ hipError_t launch_group_nmin(const float* norms, int64_t n_groups, float* out, h
 hipError_t launch_rs_pre_lists(const int64_t* goff, int n_lists, int div, int min_groups, const int64_t* probes,
                                int64_t nq, int np, int64_t* goff2, int64_t* probes2, hipStream_t s);
 hipError_t launch_rs_items(const int* work_off, const int* bucket_off, const int64_t* list_goff, int n_lists,
-                           int max_items, int4* items, int* bounds, hipStream_t s);
+                           int max_items, int4* items, int* bounds, hipStream_t s,
+                           int* zero = nullptr, int nzero = 0);
 hipError_t launch_rs_tiles(const int64_t* bucket_q, const int* bucket_off, int n_lists, const uint16_t* qh,
                            const float4* qhdr, int nq, int dp, char* tiles, hipStream_t s);
 // tq (optional): T_q per query, the bound K11 checks its final window against
@@ -519,6 +520,10 @@ hipError_t launch_pack_groups(const float* src, int64_t src_rows_total, int d, i
                               int64_t n_groups, float* groups, float* norms, int64_t* ids_out,
                               const int64_t* id_map, int64_t id_offset, hipStream_t s);
 hipError_t launch_row_norms(const float* x, int64_t n, int d, float* out, hipStream_t s);
+// one pass over the query batch: norms (launch_row_norms), fp16 copy (launch_queries_to_half) and, q8 != nullptr,
+// fp8 copy (launch_queries_to_f8); d % 4 == 0 and 16-B aligned rows
+hipError_t launch_queries_prep(const float* q, int64_t nq, int d, int dp, int hx_exp, int hx8, float* qn, uint16_t* qh,
+                               float* qscale, float* qres, uint8_t* q8, float* qscale8, hipStream_t s);
 // cosine: out = x / sqrt(pinned ‖x‖²) per row (zero rows stay zero); n2: [n] scratch (the squared norms)
 hipError_t launch_normalize_rows(const float* x, int64_t n, int d, float* n2, float* out, hipStream_t s);
 hipError_t launch_iota_i64(int64_t* out, int64_t n, int64_t start, int64_t step, hipStream_t s);

@@ -1695,6 +1695,93 @@ __global__ __launch_bounds__(256) void k_queries_to_f8(const float* __restrict__
   if (lane == 0) qscale8[qi] = ldexpf(1.0f, -(hx8 + e));
 }
 
+// The query batch's prep in one pass, each row read once: ||q||^2 (k_row_norms_w's chain), the fp16 copy, scale and
+// residual bound (k_queries_to_half_v) and, with q8, the fp8 copy and scale (k_queries_to_f8). One wave per query;
+// the row is staged in LDS for the norm chain and the fp8 pieces. (Three kernels had read the batch three times:
+// 30 + 10 + 24 us per 10k x 768 batch.)
+template <int NV>
+__global__ __launch_bounds__(256) void k_queries_prep(const float* __restrict__ q, int64_t nq, int d, int dp, int hx_exp,
+                                                      int hx8, float* __restrict__ qn, uint16_t* __restrict__ qh,
+                                                      float* __restrict__ qscale, float* __restrict__ qres,
+                                                      uint8_t* __restrict__ q8, float* __restrict__ qscale8) {
+  extern __shared__ __attribute__((aligned(16))) float qp_t[];  // [4][dp]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t qi = (int64_t)blockIdx.x * 4 + w;
+  const bool live = qi < nq;
+  float* my = qp_t + w * dp;
+  const float4* row = reinterpret_cast<const float4*>(q + (live ? qi : 0) * d);
+  float4 v[NV];
+  float m = 0.0f;
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    const int c4 = lane + 64 * u;
+    v[u] = live && 4 * c4 < d ? row[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
+    if (4 * c4 < dp) *reinterpret_cast<float4*>(my + 4 * c4) = v[u];
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+  // fp16 (k_queries_to_half_v)
+  const int e = pf_exp_for(m);
+  const float sc = ldexpf(1.0f, e), isc = ldexpf(1.0f, -e);
+  float res = 0.0f;
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    const int c4 = lane + 64 * u;
+    if (4 * c4 < dp) {
+      uint2 pk;
+      pk.x = pf_to_half(v[u].x, sc, isc, res) | ((unsigned)pf_to_half(v[u].y, sc, isc, res) << 16);
+      pk.y = pf_to_half(v[u].z, sc, isc, res) | ((unsigned)pf_to_half(v[u].w, sc, isc, res) << 16);
+      if (live) *reinterpret_cast<uint2*>(qh + qi * dp + 4 * c4) = pk;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) res += __shfl_xor(res, off);
+  if (live && lane == 0) {
+    qscale[qi] = ldexpf(1.0f, -(hx_exp + e));
+    qres[qi] = sqrtf(res) * (1.0f + 0x1p-12f);
+  }
+  __syncthreads();  // the staged rows
+  if (live && lane == 0) {  // ||q||^2: k_row_norms_w's chain
+    float acc = 0.0f;
+    for (int s8 = 0; s8 < dp; s8 += 8) {
+      const float4 a = *reinterpret_cast<const float4*>(my + s8), b = *reinterpret_cast<const float4*>(my + s8 + 4);
+      acc = fmaf(a.x, a.x, acc); acc = fmaf(b.x, b.x, acc);
+      acc = fmaf(a.y, a.y, acc); acc = fmaf(b.y, b.y, acc);
+      acc = fmaf(a.z, a.z, acc); acc = fmaf(b.z, b.z, acc);
+      acc = fmaf(a.w, a.w, acc); acc = fmaf(b.w, b.w, acc);
+    }
+    qn[qi] = acc;
+  }
+  if (live && q8) {  // fp8 (k_queries_to_f8): piece pc = (S, h) = dims 32 S + 16 (i >> 3) + 8 h + (i & 7)
+    const int e8 = (m > 0.0f && m < INFINITY) ? 7 - ilogbf(m) : 0;
+    const float sc8 = ldexpf(1.0f, e8);
+    for (int pc = lane; pc < (dp >> 4); pc += 64) {
+      const int S = pc >> 1, hh = pc & 1;
+      float f[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) f[i] = my[32 * S + 16 * (i >> 3) + 8 * hh + (i & 7)];
+      *reinterpret_cast<uint4*>(q8 + qi * dp + pc * 16) = f8_pack16(f, sc8);
+    }
+    if (lane == 0) qscale8[qi] = ldexpf(1.0f, -(hx8 + e8));
+  }
+}
+
+hipError_t launch_queries_prep(const float* q, int64_t nq, int d, int dp, int hx_exp, int hx8, float* qn, uint16_t* qh,
+                               float* qscale, float* qres, uint8_t* q8, float* qscale8, hipStream_t s) {
+  if (nq <= 0) return hipSuccess;
+  if ((d & 3) != 0 || (reinterpret_cast<uintptr_t>(q) & 15) != 0 || dp > 1024 || dp % 32 != 0 || d > dp)
+    return hipErrorInvalidValue;
+  const size_t lds = (size_t)4 * dp * sizeof(float);
+  switch ((dp + 255) / 256) {
+    case 1: hipLaunchKernelGGL(k_queries_prep<1>, pf_grid(nq, 4), dim3(256), lds, s, q, nq, d, dp, hx_exp, hx8, qn, qh, qscale, qres, q8, qscale8); break;
+    case 2: hipLaunchKernelGGL(k_queries_prep<2>, pf_grid(nq, 4), dim3(256), lds, s, q, nq, d, dp, hx_exp, hx8, qn, qh, qscale, qres, q8, qscale8); break;
+    case 3: hipLaunchKernelGGL(k_queries_prep<3>, pf_grid(nq, 4), dim3(256), lds, s, q, nq, d, dp, hx_exp, hx8, qn, qh, qscale, qres, q8, qscale8); break;
+    default: hipLaunchKernelGGL(k_queries_prep<4>, pf_grid(nq, 4), dim3(256), lds, s, q, nq, d, dp, hx_exp, hx8, qn, qh, qscale, qres, q8, qscale8); break;
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_groups_to_f8(const float* groups, int64_t n_groups, int dp, int hx8, uint8_t* out, hipStream_t s) {
   if (n_groups <= 0) return hipSuccess;
   if (dp % 32 != 0) return hipErrorInvalidValue;

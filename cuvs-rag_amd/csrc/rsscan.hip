@@ -504,8 +504,10 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
 // Work items of K13 from the probe map (chunk = kRsBlockGroups groups, one tile column per list):
 // item w -> {first group, end group, first tile slot of its list, tiles of its list}
 __global__ void k_rs_items(const int* __restrict__ work_off, const int* __restrict__ bucket_off,
-                           const int64_t* __restrict__ list_goff, int n_lists, int max_items, int4* __restrict__ items) {
+                           const int64_t* __restrict__ list_goff, int n_lists, int max_items, int4* __restrict__ items,
+                           int* __restrict__ zero, int nzero) {
   const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w < nzero) zero[w] = 0;  // K13's counters (a memset launch less)
   if (w >= max_items || w >= work_off[n_lists]) return;
   int lo = 0, hi = n_lists - 1;
   while (lo < hi) {
@@ -708,10 +710,11 @@ hipError_t launch_rs_tiles(const int64_t* bucket_q, const int* bucket_off, int n
 }
 
 hipError_t launch_rs_items(const int* work_off, const int* bucket_off, const int64_t* list_goff, int n_lists,
-                           int max_items, int4* items, int* bounds, hipStream_t s) {
-  if (max_items <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_rs_items, dim3((unsigned)ceil_div(max_items, 256)), dim3(256), 0, s, work_off, bucket_off,
-                     list_goff, n_lists, max_items, items);
+                           int max_items, int4* items, int* bounds, hipStream_t s, int* zero, int nzero) {
+  if (nzero > 256) return hipErrorInvalidValue;
+  if (max_items <= 0 && nzero <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rs_items, dim3((unsigned)ceil_div(max_items > 0 ? max_items : 1, 256)), dim3(256), 0, s,
+                     work_off, bucket_off, list_goff, n_lists, max_items, items, zero, nzero);
   if (bounds) hipLaunchKernelGGL(k_rs_bounds, dim3(1), dim3(1024), 0, s, work_off, bucket_off, n_lists, bounds);
   return hipGetLastError();
 }
