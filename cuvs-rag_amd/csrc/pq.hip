@@ -810,8 +810,8 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
   float* s_base = reinterpret_cast<float*>(s_bound + TQ);       // [TQ] IP: the probe's coarse key
   const int rdp = a.rot_dim_pad;
   float* s_res = reinterpret_cast<float*>(smem + 512);    // [TQ][rdp] residuals (IP: the queries)
-  float* s_lut = s_res + TQ * rdp;                        // [2][256][LS]
-  float* s_rn = s_lut + 2 * kPqCodes * LS;                // [pq_dim][TQ] L2: ||r_j||^2 of the tile's queries
+  float* s_lut = s_res + TQ * rdp;                        // [4][256][LS]: two subspace pairs
+  float* s_rn = s_lut + 4 * kPqCodes * LS;                // [pq_dim][TQ] L2: ||r_j||^2 of the tile's queries
   // after the subspace loop (aliasing s_res / s_lut)
   uint32_t* s_min = reinterpret_cast<uint32_t*>(smem + 512);   // [TQ][NT]
   float* s_ck = reinterpret_cast<float*>(s_min + TQ * NT);     // [TQ][CQ]
@@ -884,7 +884,7 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
       s_res[t * rdp + (c < rd ? jj * PL + (ii & 3) * PL4 + (ii >> 2) : c)] = v;
     }
     // LUT_j (j < pq_dim) into buffer `buf` (see bg / bi above)
-    float bk[2][2][PL4];  // MFMA B operands of the two code blocks, subspaces j + 1 (parity (j + 1) & 1) and j + 2
+    float bk[2][2][PL4];  // MFMA B operands of the two code blocks of the two subspaces of the next pair
     float bnk[2][2];      // and the codes' norms
     auto load_book = [&](int j, float (&b)[2][PL4], float (&bn)[2]) {
 #pragma unroll
@@ -896,38 +896,53 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
         bn[cb] = a.book_norms[j * kPqCodes + c];
       }
     };
-    auto build = [&](int j, const float (&b)[2][PL4], const float (&bn)[2], int buf) {
-      float ra[PL4];
-      const float* rsrc = s_res + bi * rdp + j * PL + bg * PL4;
+    // LUT_j0 and LUT_j0+1 into slots j0 & 3, (j0 + 1) & 3: the four MFMA chains, then one wait for their results
+    auto build2 = [&](int j0, const float (&b)[2][2][PL4], const float (&bn)[2][2]) {
+      f32x4 acc[2][2];
 #pragma unroll
-      for (int u = 0; u < PL4; ++u) ra[u] = rsrc[u];
-      float4 rn = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      if (!a.ip) rn = *reinterpret_cast<const float4*>(s_rn + j * TQ + 4 * bg);
+      for (int sb = 0; sb < 2; ++sb) {
+        const int j = j0 + sb;
+        float ra[PL4];
+        const float* rsrc = s_res + bi * rdp + j * PL + bg * PL4;
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        f32x4 acc;
-        if (!a.ip) {
-          acc[0] = rn.x + bn[cb]; acc[1] = rn.y + bn[cb]; acc[2] = rn.z + bn[cb]; acc[3] = rn.w + bn[cb];
-        } else {
-          acc[0] = 0.0f; acc[1] = 0.0f; acc[2] = 0.0f; acc[3] = 0.0f;
+        for (int u = 0; u < PL4; ++u) ra[u] = rsrc[u];
+        float4 rn = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (!a.ip) rn = *reinterpret_cast<const float4*>(s_rn + j * TQ + 4 * bg);
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          if (!a.ip) {
+            acc[sb][cb][0] = rn.x + bn[sb][cb]; acc[sb][cb][1] = rn.y + bn[sb][cb];
+            acc[sb][cb][2] = rn.z + bn[sb][cb]; acc[sb][cb][3] = rn.w + bn[sb][cb];
+          } else {
+            acc[sb][cb][0] = 0.0f; acc[sb][cb][1] = 0.0f; acc[sb][cb][2] = 0.0f; acc[sb][cb][3] = 0.0f;
+          }
+#pragma unroll
+          for (int u = 0; u < PL4; ++u)
+            acc[sb][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[u], b[sb][cb][u], acc[sb][cb], 0, 0, 0);
         }
+      }
+      // the results are read next by LDS stores: the wait states of an XDL result read as LDS data, explicit
+      // (the compiler placed a store one instruction after its MFMA: 12 % of the LUT entries were stale)
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int u = 0; u < PL4; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[u], b[cb][u], acc, 0, 0, 0);
-        // the result is read next by an LDS store: the wait states of an XDL result read as LDS data, explicit
-        // (the compiler placed the store one instruction after the MFMA: 12 % of the LUT entries were stale)
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        if (a.ip && j == 0) {  // the probe's coarse key in subspace 0 (pq_lut_entry)
+      for (int sb = 0; sb < 2; ++sb) {
+        const int j = j0 + sb;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[r] = acc[r] + s_base[4 * bg + r];
+        for (int cb = 0; cb < 2; ++cb) {
+          f32x4 v = acc[sb][cb];
+          if (a.ip && j == 0) {  // the probe's coarse key in subspace 0 (pq_lut_entry)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = v[r] + s_base[4 * bg + r];
+          }
+          *reinterpret_cast<float4*>(s_lut + ((j & 3) * kPqCodes + wave * 32 + cb * 16 + bi) * LS + 4 * bg) =
+              make_float4(v[0], v[1], v[2], v[3]);
         }
-        *reinterpret_cast<float4*>(s_lut + (buf * kPqCodes + wave * 32 + cb * 16 + bi) * LS + 4 * bg) =
-            make_float4(acc[0], acc[1], acc[2], acc[3]);
       }
     };
     load_book(0, bk[0], bnk[0]);
-    if (a.pq_dim > 1) load_book(1, bk[1], bnk[1]);
+    load_book(1, bk[1], bnk[1]);
     __syncthreads();  // s_res, s_base
     if (!a.ip) {  // rn_j of the tile's queries: the fmaf chain of r_i r_i, dims ascending (pq_lut_start)
       for (int e = tid; e < a.pq_dim * TQ; e += NT) {
@@ -940,8 +955,7 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
       }
       __syncthreads();
     }
-    if (!(a.flags & 1)) build(0, bk[0], bnk[0], 0);
-    if (a.pq_dim > 2) load_book(2, bk[0], bnk[0]);
+    if (!(a.flags & 1)) build2(0, bk, bnk);
 
     // my rows: i * NT + tid of the chunk; their codes, 16 subspaces (one uint4) per chunk ch
     float acc[RPT][TQ];
@@ -970,17 +984,22 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
     const bool skip_scan = a.flags & 2;
     // row iterations of this wave inside the chunk (wave-uniform)
     const int nvi = nr > wave * 64 ? (nr - wave * 64 + NT - 1) / NT : 0;
+    // subspaces in pairs, one barrier per pair: at pair (j, j + 1) the next pair's codebook rows are requested, the
+    // pair is scanned, then the next pair's LUTs are built into the other two of four slots (the pair before
+    // this one used them, and every wave has passed this pair's barrier, so is done with it)
     for (int wq = 0; wq < nwd; ++wq) {
       if (wq + 1 < nwd) load_word(wq + 1, nw);
 #pragma unroll
       for (int b = 0; b < 4; ++b) {  // (pq_dim % 4 == 0: pq_rt_supported)
         const int j = wq * 4 + b;
-        __syncthreads();  // LUT_j complete; LUT_{j-1}'s buffer free
-        if (j + 1 < a.pq_dim) {  // (b is static: j's parity is b's)
-          if (!(a.flags & 1)) build(j + 1, bk[(b + 1) & 1], bnk[(b + 1) & 1], (b + 1) & 1);
-          if (j + 3 < a.pq_dim) load_book(j + 3, bk[(b + 1) & 1], bnk[(b + 1) & 1]);
+        if ((b & 1) == 0) {
+          __syncthreads();  // LUT_j, LUT_j+1 complete; the slots of LUT_j-2, LUT_j-1 free
+          if (j + 2 < a.pq_dim) {
+            load_book(j + 2, bk[0], bnk[0]);
+            load_book(j + 3, bk[1], bnk[1]);
+          }
         }
-        const float* lut = s_lut + (j & 1) * (kPqCodes * LS);
+        const float* lut = s_lut + (j & 3) * (kPqCodes * LS);
 #pragma unroll
         for (int i = 0; i < RPT; ++i) {
           if (i < nvi && !skip_scan) {
@@ -994,6 +1013,7 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
           }
           __builtin_amdgcn_sched_barrier(0);  // one row's 16 LUT floats in flight: bounds the VGPRs
         }
+        if ((b & 1) == 1 && j + 1 < a.pq_dim && !(a.flags & 1)) build2(j + 1, bk, bnk);
       }
 #pragma unroll
       for (int i = 0; i < RPT; ++i) cw[i] = nw[i];
@@ -1188,7 +1208,7 @@ hipError_t launch_pq_scan_tiled(const PqTileArgs& a, int kcap, int grid, hipStre
 static int pq_rt_cq(int k) { return k > 64 ? 0 : (k <= 16 ? 128 : 512); }
 
 size_t pq_rt_lds_bytes(int rot_dim_pad, int pq_dim, int k) {
-  const size_t loop = (size_t)kRtQ * rot_dim_pad * 4 + (size_t)2 * kPqCodes * 20 * 4 + (size_t)pq_dim * kRtQ * 4;
+  const size_t loop = (size_t)kRtQ * rot_dim_pad * 4 + (size_t)4 * kPqCodes * 20 * 4 + (size_t)pq_dim * kRtQ * 4;
   const size_t sel = (size_t)kRtQ * kRtThreads * 4 + (size_t)kRtQ * pq_rt_cq(k) * 8;
   return 512 + (loop > sel ? loop : sel);
 }
