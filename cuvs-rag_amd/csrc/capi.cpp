@@ -1388,7 +1388,7 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   // straight from the fp16 query matrix was measured 0.45 ms slower per launch: 16 separate 64-B segments per
   // DMA instruction)
   ws.rs_tiles.reserve((size_t)rs_tiles_bytes(ne, L.n_lists, dp));
-  HIPCHK(launch_rs_tiles(ws.bucket_q.as<int64_t>(), ws.bucket_off.as<int>(), L.n_lists, ws.qh.as<uint16_t>(), qhdr,
+  HIPCHK(launch_rs_tiles(ws.bucket_q.as<int64_t>(), ws.bucket_off.as<int>(), L.n_lists, ne, ws.qh.as<uint16_t>(), qhdr,
                          (int)nq, dp, ws.rs_tiles.as<char>(), s));
   // 4. K13
   int64_t max_items = 0;  // every list probed: the item table's bound (the probe map decides the count)

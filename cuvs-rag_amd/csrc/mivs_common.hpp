@@ -473,7 +473,7 @@ hipError_t launch_rs_pre_lists(const int64_t* goff, int n_lists, int div, int mi
 hipError_t launch_rs_items(const int* work_off, const int* bucket_off, const int64_t* list_goff, int n_lists,
                            int max_items, int4* items, int* bounds, hipStream_t s,
                            int* zero = nullptr, int nzero = 0);
-hipError_t launch_rs_tiles(const int64_t* bucket_q, const int* bucket_off, int n_lists, const uint16_t* qh,
+hipError_t launch_rs_tiles(const int64_t* bucket_q, const int* bucket_off, int n_lists, int64_t ne, const uint16_t* qh,
                            const float4* qhdr, int nq, int dp, char* tiles, hipStream_t s);
 // tq (optional): T_q per query, the bound K11 checks its final window against
 hipError_t launch_rs_headers(const float* pre_kth, int64_t nq, const float* qscale, const float* qnorms,

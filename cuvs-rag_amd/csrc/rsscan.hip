@@ -612,32 +612,47 @@ __global__ void k_rs_headers(const float* __restrict__ pre_kth, int64_t nq, cons
 // Piece s = 2 t + qb, lane (c, kq) = (L & 15, L >> 4): dims 32 t + 8 kq .. + 8 of query 16 qb + c (the B
 // operand of v_mfma_f32_16x16x32_f16).
 template <int NK>
-__global__ __launch_bounds__(1024) void k_rs_tiles(const int64_t* __restrict__ bucket_q, const int* __restrict__ bucket_off,
-                                                  const uint16_t* __restrict__ qh, const float4* __restrict__ qhdr,
-                                                  int nq, char* __restrict__ tiles) {
-  const int l = blockIdx.x;
-  const int e0 = bucket_off[l], m = bucket_off[l + 1] - e0;
-  if (m <= 0) return;
-  const int ntiles = (m + kRsQTile - 1) / kRsQTile;
+// one workgroup per tile slot (rs_tile_slot: list l's tiles start at bucket_off[l] / 32 + l): the tile's 32
+// query ids staged in LDS, then its NK pieces in image order (lane L of piece s fastest: every wave-instruction
+// stores 1 KiB contiguous; lanes L and L + 32 read the two adjacent 16-B halves of one query's 32 B of k-step s)
+// and its header piece. (A workgroup per list had ~10 tiles' worth of dependent id -> row loads per thread.)
+__global__ __launch_bounds__(256) void k_rs_tiles(const int64_t* __restrict__ bucket_q, const int* __restrict__ bucket_off,
+                                                 int n_lists, const uint16_t* __restrict__ qh,
+                                                 const float4* __restrict__ qhdr, int nq, char* __restrict__ tiles) {
   constexpr int64_t IMG = (int64_t)(NK + 1) * 1024;
-  char* base = tiles + rs_tile_slot(bucket_off, l, 0) * IMG;
-  // image order (lane L of piece s of tile t fastest): every wave-instruction stores 1 KiB contiguous;
-  // lanes L and L + 32 read the two adjacent 16-B halves of one query's 32 B of k-step s
-  for (int i = threadIdx.x; i < ntiles * NK * 64; i += blockDim.x) {
-    const int t = i / (NK * 64), r = i - t * (NK * 64);
-    const int s = r >> 6, L = r & 63;
-    const int jq = 16 * (s & 1) + (L & 15);
+  __shared__ int s_l;
+  __shared__ int s_q[kRsQTile];
+  const int b = blockIdx.x;
+  if (threadIdx.x == 0) {
+    int lo = 0, hi = n_lists - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (bucket_off[mid] / kRsQTile + mid <= b) lo = mid; else hi = mid - 1;
+    }
+    s_l = lo;
+  }
+  __syncthreads();
+  const int l = s_l;
+  const int e0 = bucket_off[l], m = bucket_off[l + 1] - e0;
+  const int t = b - (int)rs_tile_slot(bucket_off, l, 0);
+  if (t < 0 || t * kRsQTile >= m) return;  // a padding slot between two lists' tiles (never read)
+  if (threadIdx.x < kRsQTile) {
+    const int e = t * kRsQTile + threadIdx.x;
+    s_q[threadIdx.x] = e < m ? (int)bucket_q[e0 + e] : -1;
+  }
+  __syncthreads();
+  char* img = tiles + (int64_t)b * IMG;
+  for (int i = threadIdx.x; i < NK * 64; i += 256) {
+    const int s = i >> 6, L = i & 63;
+    const int q = s_q[16 * (s & 1) + (L & 15)];
     const int dim0 = 32 * (s >> 1) + 8 * (L >> 4);
-    const int e = t * kRsQTile + jq;
-    const int q = e < m ? (int)bucket_q[e0 + e] : -1;
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
     if (q >= 0) v = *reinterpret_cast<const uint4*>(qh + (int64_t)q * (NK * 16) + dim0);
-    *reinterpret_cast<uint4*>(base + t * IMG + s * 1024 + L * 16) = v;
+    *reinterpret_cast<uint4*>(img + s * 1024 + L * 16) = v;
   }
-  for (int i = threadIdx.x; i < ntiles * 64; i += blockDim.x) {
-    const int t = i >> 6, L = i & 63, e = t * kRsQTile + (L & 31);
-    const int q = e < m ? (int)bucket_q[e0 + e] : -1;
-    *reinterpret_cast<float4*>(base + t * IMG + NK * 1024 + L * 16) = qhdr[q >= 0 ? q : nq];
+  if (threadIdx.x < 64) {
+    const int q = s_q[threadIdx.x & 31];
+    *reinterpret_cast<float4*>(img + NK * 1024 + threadIdx.x * 16) = qhdr[q >= 0 ? q : nq];
   }
 }
 
@@ -692,16 +707,18 @@ int64_t rs_tiles_bytes(int64_t ne, int n_lists, int dp) {
 }
 
 template <int NK>
-static void launch_rs_tiles_k(const int64_t* bucket_q, const int* bucket_off, int n_lists, const uint16_t* qh,
-                              const float4* qhdr, int nq, char* tiles, hipStream_t s) {
-  hipLaunchKernelGGL(k_rs_tiles<NK>, dim3((unsigned)n_lists), dim3(1024), 0, s, bucket_q, bucket_off, qh, qhdr, nq,
-                     tiles);
+static void launch_rs_tiles_k(const int64_t* bucket_q, const int* bucket_off, int n_lists, int64_t n_slots,
+                              const uint16_t* qh, const float4* qhdr, int nq, char* tiles, hipStream_t s) {
+  hipLaunchKernelGGL(k_rs_tiles<NK>, dim3((unsigned)n_slots), dim3(256), 0, s, bucket_q, bucket_off, n_lists, qh, qhdr,
+                     nq, tiles);
 }
 
-hipError_t launch_rs_tiles(const int64_t* bucket_q, const int* bucket_off, int n_lists, const uint16_t* qh,
+hipError_t launch_rs_tiles(const int64_t* bucket_q, const int* bucket_off, int n_lists, int64_t ne, const uint16_t* qh,
                            const float4* qhdr, int nq, int dp, char* tiles, hipStream_t s) {
+  const int64_t n_slots = ne / kRsQTile + n_lists + 1;  // (rs_tiles_bytes' slot bound)
+  if (n_lists <= 0 || ne <= 0) return hipSuccess;
   switch (dp / 16) {
-#define RS_T(NK) case NK: launch_rs_tiles_k<NK>(bucket_q, bucket_off, n_lists, qh, qhdr, nq, tiles, s); break;
+#define RS_T(NK) case NK: launch_rs_tiles_k<NK>(bucket_q, bucket_off, n_lists, n_slots, qh, qhdr, nq, tiles, s); break;
     RS_T(4) RS_T(8) RS_T(12) RS_T(16) RS_T(20) RS_T(24) RS_T(28) RS_T(32) RS_T(36) RS_T(40) RS_T(44) RS_T(48)
 #undef RS_T
     default: return hipErrorInvalidValue;
