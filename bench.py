@@ -561,8 +561,8 @@ PEAK_LDS_B128_LOOKUPS = 256 * 2.4e9 * 64  # ds_read_b128: 256 B/clk/CU = 64 fp32
 def pq_side_line(a, rl, rank=0, world=1, dev=None):
     """BASELINE configs[4]: IVF-PQ over 12.5M x 768 fp16 rows PER RANK (100M over 8 GPUs), n_lists 4096,
     pq_dim 96, pq_bits 8 (improved_multi_gpu_rag.py:131-137), the same query batch shape; plain PQ at
-    n_probes 16 and PQ + exact re-ranking of 10 k candidates (cuvs.neighbors.refine) -- the configuration
-    that reaches recall@10 >= 0.95 on this mixture. With N ranks every rank builds its own shard (rows
+    n_probes 10 and PQ + exact re-ranking of 12 k candidates (cuvs.neighbors.refine) -- the fastest point of the
+    n_probes x candidates sweep that reaches recall@10 >= 0.95 on this mixture with a margin. With N ranks every rank builds its own shard (rows
     rank*n..), and one step = each rank's search (+ refine) and the RCCL all-gather + K7 merge of the
     per-shard top-k (mivs.distributed.merge_across_ranks), timed between barriers, max over ranks. The
     scan's roofline: one fp32 LUT entry read from LDS per (probed row, subspace, query), against the
@@ -572,7 +572,10 @@ def pq_side_line(a, rl, rank=0, world=1, dev=None):
     from mivs.neighbors import brute_force, ivf_pq, refine
 
     dev = torch.cuda.current_device() if dev is None else dev
-    n, d, Q, k, pq_dim, n_lists, n_probes, ratio = a.pq_rows, a.dim, a.queries, a.k, 96, 4096, 16, 10
+    # operating point (round 4, profiles/r04_ivf_pq_sweep.log): the refined recall is set by the candidate count, not by
+    # n_probes in 10..16 (the coarse recall is >= 0.99 there), so the fastest sweep point with a margin over recall 0.95:
+    # n_probes 10, 12 x k = 120 candidates (recall 0.976; 100 candidates give 0.952)
+    n, d, Q, k, pq_dim, n_lists, n_probes, ratio = a.pq_rows, a.dim, a.queries, a.k, 96, 4096, 10, 12
     start = rank * n
     x = ops.synth_mixture(n, d, SEED + 11, n_centers=a.centers, sigma=a.sigma, row_begin=start, device=dev).half()
     torch.cuda.empty_cache()
