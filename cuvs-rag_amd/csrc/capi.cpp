@@ -182,6 +182,7 @@ struct ScanJob {
   int64_t* out_i;
   int qtile;  // 32: K3, 64: K3w (must match the work decomposition of the probe map / single job)
   bool dump = false;  // DUMP mode (raw keys per slot for K8) whatever k: set by every caller that runs K8
+  bool counter_zeroed = false;  // ws.counter[0] was zeroed on the stream already (k_single_job)
   const int64_t* goff = nullptr;  // another split of ls's groups into lists (K16's sample), else ls->goff
   int n_lists = 0;
 };
@@ -203,7 +204,7 @@ void run_scan(const ScanJob& j, int device, Workspace& ws, hipStream_t s) {
           MIVS_ERR_UNSUPPORTED);
   require(j.dp <= 1024, "dim > 1024 is not supported by this build", MIVS_ERR_UNSUPPORTED);
   ws.counter.reserve(16);
-  HIPCHK(hipMemsetAsync(ws.counter.p, 0, sizeof(int), s));
+  if (!j.counter_zeroed) HIPCHK(hipMemsetAsync(ws.counter.p, 0, sizeof(int), s));
   ScanArgs a{};
   a.groups = j.ls->groups.as<float>();
   a.row_norms = j.ls->norms.as<float>();
@@ -275,8 +276,9 @@ void single_list_topk(const ListSet& ls, int G, const float* queries, const floa
       ws.work_off.reserve(sizeof(int) * 2);
       ws.part_d.reserve(sizeof(float) * (size_t)(nb * chunks * slot_rows));
       ws.part_i.reserve(sizeof(int64_t) * (size_t)(nb * chunks * 2));
+      ws.counter.reserve(16);
       HIPCHK(launch_single_list_job(nb, chunks, kQTile, ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(),
-                                    ws.bucket_off.as<int>(), ws.work_off.as<int>(), nullptr, s));
+                                    ws.bucket_off.as<int>(), ws.work_off.as<int>(), nullptr, s, ws.counter.as<int>()));
       const float* qb_ptr = queries;
       const float* qn_ptr = qnorms;
       if (rows) HIPCHK(hipMemcpyAsync(ws.bucket_q.p, rows + b0, sizeof(int64_t) * nb, hipMemcpyDeviceToDevice, s));
@@ -285,6 +287,7 @@ void single_list_topk(const ListSet& ls, int G, const float* queries, const floa
                 ws.bucket_off.as<int>(), ws.work_off.as<int>(), ws.part_d.as<float>(), ws.part_i.as<int64_t>(),
                 kQTile};
       j.dump = true;
+      j.counter_zeroed = true;
       run_scan(j, device, ws, s);
       SelectArgs sa{};
       sa.keys = ws.part_d.as<float>();
@@ -824,7 +827,8 @@ void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t
 void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                         int64_t* out_i, const float* slot_key, const int* slot_pos, const float* slot_bound,
                         const int* force_ovf, const int64_t* slot_begin, int slot_k, bool fallback_pf = false,
-                        float* kth_out = nullptr, const float* window_cap = nullptr, int verify_sel = 0);
+                        float* kth_out = nullptr, const float* window_cap = nullptr, int verify_sel = 0,
+                        bool stats_zeroed = false);
 
 // K10 scan + K11 refine for a probe map built with (kPfChunkGroups, kPfQTile); queries the refine
 // could not prove are re-run through the exact scan and scattered back.
@@ -857,8 +861,7 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   const char* cve = getenv("MIVS_PF_CONVOY");
   const bool convoy = !(cve && cve[0] == '0');
   const int64_t n_cpos = convoy ? (int64_t)n_lists * tcp[1] : 0;
-  ws.counter.reserve(sizeof(int) * (8 * 16 + n_cpos));
-  HIPCHK(hipMemsetAsync(ws.counter.p, 0, sizeof(int) * (8 * 16 + n_cpos), s));
+  ws.counter.reserve(sizeof(int) * (8 * 16 + n_cpos));  // (zeroed below, in the qtheta fill's launch)
   PfScanArgs a{};
   if (convoy) {
     a.chunk_pos = ws.counter.as<int>() + 8 * 16;
@@ -896,9 +899,12 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   a.x_norm_max = idx->x_norm_max;
   a.x_res_max = idx->x_res_max;
   ws.qtheta.reserve(sizeof(unsigned) * nq);
-  HIPCHK(launch_fill_i32(ws.qtheta.as<int>(), nq, (int)kPfOrdInf, s));
+  HIPCHK(launch_fill2_i32(ws.qtheta.as<int>(), nq, (int)kPfOrdInf, ws.counter.as<int>(), 8 * 16 + n_cpos, 0, s));
   a.qtheta = ws.qtheta.as<unsigned>();
   a.k = verify_sel > 0 ? std::min(verify_sel, kPfMaxK) : k;  // (nomination: the slots keep the verify_sel best)
+  // (nomination: K11v reads only each slot's verify_sel best keys and their ties; MIVS_PF_SLOT_OUT=0: merge whole slots)
+  const char* soe = getenv("MIVS_PF_SLOT_OUT");
+  a.slot_out = verify_sel > 0 && !(soe && soe[0] == '0') ? a.k : 0;
   // K13's pre-pass (kth_out): each list sample is scanned by one tile -- its rows are read once
   // (MIVS_PF_PRE_NT=0: the default policy, A/B runs)
   const char* pne = getenv("MIVS_PF_PRE_NT");
@@ -933,12 +939,13 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
 void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                         int64_t* out_i, const float* slot_key, const int* slot_pos, const float* slot_bound,
                         const int* force_ovf, const int64_t* slot_begin, int slot_k, bool fallback_pf,
-                        float* kth_out, const float* window_cap, int verify_sel) {
+                        float* kth_out, const float* window_cap, int verify_sel, bool stats_zeroed) {
   Workspace& ws = idx->ws;
   const ListSet& L = idx->lists;
   const int dp = idx->dp;
   ws.pf_stats.reserve(32);
-  if (!kth_out) HIPCHK(hipMemsetAsync(ws.pf_stats.p, 0, 32, s));  // (the k-th-only modes leave the stats alone)
+  // (the k-th-only modes leave the stats alone; stats_zeroed: an earlier kernel of the search zeroed them)
+  if (!kth_out && !stats_zeroed) HIPCHK(hipMemsetAsync(ws.pf_stats.p, 0, 32, s));
   ws.ovf_q.reserve(sizeof(int64_t) * nq);
   PfRefineArgs r{};
   r.slot_key = slot_key;
@@ -1376,14 +1383,12 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   ws.slot_begin.reserve(sizeof(int64_t) * (nq + 1));
   const size_t stb = scan_tmp_bytes(ne) + sizeof(int64_t) * (size_t)ne;
   ws.scan_tmp.reserve(stb);
+  // (the per-list query counts go to their own buffer, which the search stats read: a nested search reuses ws.counts)
+  ws.stat_counts.reserve(sizeof(int) * L.n_lists);
   HIPCHK(launch_probe_map(ws.probes_i.as<int64_t>(), nq, np, L.n_lists, L.goff.as<int64_t>(), kRsBlockGroups,
-                          1 << 30, ws.counts.as<int>(), ws.fill.as<int>(), ws.bucket_off.as<int>(),
+                          1 << 30, ws.stat_counts.as<int>(), ws.fill.as<int>(), ws.bucket_off.as<int>(),
                           ws.work_off.as<int>(), ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(),
                           ws.qp_slots.as<int64_t>(), nullptr, ws.scan_tmp.p, stb, s));  // (no output slots)
-  {  // (cheap: n_lists ints)
-    ws.stat_counts.reserve(sizeof(int) * L.n_lists);
-    HIPCHK(hipMemcpyAsync(ws.stat_counts.p, ws.counts.p, sizeof(int) * L.n_lists, hipMemcpyDeviceToDevice, s));
-  }
   // the query tiles in the LDS image layout (one contiguous 1 KiB per DMA wave-instruction; a per-lane gather
   // straight from the fp16 query matrix was measured 0.45 ms slower per launch: 16 separate 64-B segments per
   // DMA instruction)
@@ -1473,16 +1478,20 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   // the streams into per-query CSR runs (a record expands to at most 8 candidates)
   ws.cand_off.reserve(sizeof(int64_t) * (nq + 1));
   ws.rs_bucket_tmp.reserve(rs_bucket_tmp_bytes((int)nq, n_waves));
+  ws.pf_stats.reserve(32);
   if (!large) {
     const size_t max_cand = (size_t)n_waves * a.wave_cap * 8;
     ws.cand_key.reserve(sizeof(float) * max_cand);
     ws.cand_pos.reserve(sizeof(int) * max_cand);
     HIPCHK(launch_rs_bucket(a.wave_buf, a.wave_cap, a.wave_cnt, n_waves, (int)nq, qhdr, a.row_norms,
                             idx->metric, ws.cand_off.as<int64_t>(), ws.cand_key.as<float>(), ws.cand_pos.as<int>(),
-                            ws.rs_bucket_tmp.p, a.wave_cnt + n_waves, 4 * cu_count(idx->device), s));
-    // 5. exact ranking of every query's run (slot = one entry); a window above T_q is not proven
+                            ws.rs_bucket_tmp.p, a.wave_cnt + n_waves, 4 * cu_count(idx->device), s, ws.pf_stats.p,
+                            32));
+    // 5. exact ranking of every query's run (slot = one entry); a window above T_q is not proven (its stats were
+    // zeroed by the bucketing's first kernel)
     pf_refine_fallback(idx, s, q, nq, k, np, out_d, out_i, ws.cand_key.as<float>(), ws.cand_pos.as<int>(), nullptr,
-                       a.wave_cnt + n_waves, ws.cand_off.as<int64_t>(), 1, true, nullptr, ws.rs_tq.as<float>());
+                       a.wave_cnt + n_waves, ws.cand_off.as<int64_t>(), 1, true, nullptr, ws.rs_tq.as<float>(), 0,
+                       true);
     return;
   }
   // large k: the candidate arrays sized by the count (one host sync: up to 8 candidates per record would be

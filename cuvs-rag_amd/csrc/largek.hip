@@ -38,7 +38,7 @@ __device__ __forceinline__ float lk_unord(uint32_t o) {
   return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
 }
 
-// every probe p of query q -> sample list 2 p (the first part of the split list set, k_rs_pre_goff)
+// every probe p of query q -> sample list 2 p (the first part of the split list set, k_rs_pre_lists)
 __global__ void k_lk_sample_probes(const int64_t* __restrict__ probes, int64_t n, int64_t* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;

@@ -227,6 +227,8 @@ struct PfScanArgs {
   int* slot_pos;              // [slots][slot_k] row positions
   float* slot_bound;          // [slots] every dropped candidate's approximate key is >= this
   int slot_k;
+  int slot_out;               // > 0: a slot's merge stops after this many keys (and their ties) -- the pre-pass's
+                              // nomination, whose verify reads only the best verify_sel of a slot; 0: slot_k
   int dp, metric;
   const float* qres;          // [nq] ||q - q_h|| (the window bound theta of the scan)
   float x_norm_max, x_res_max;
@@ -452,12 +454,13 @@ __device__ inline int64_t block_excl_scan(int64_t v, int64_t* sh, int64_t* tot) 
 size_t rs_bucket_tmp_bytes(int nq, int n_waves);
 hipError_t launch_rs_bucket(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
                             const float4* qhdr, const float* row_norms, int metric, int64_t* cand_off,
-                            float* cand_key, int* cand_pos, void* tmp, int* lost, int grid, hipStream_t s);
+                            float* cand_key, int* cand_pos, void* tmp, int* lost, int grid, hipStream_t s,
+                            void* zero2 = nullptr, int zero2_bytes = 0);  // (zero2: also zeroed, 16-B words)
 // the same in two halves (large k sizes the candidate arrays from cand_off[nq] between them): count -> cand_off,
 // then the scatter
 hipError_t launch_rs_bucket_count(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
                                   const float4* qhdr, const float* row_norms, int metric, int64_t* cand_off, void* tmp,
-                                  int* lost, hipStream_t s);
+                                  int* lost, hipStream_t s, void* zero2 = nullptr, int zero2_bytes = 0);
 hipError_t launch_rs_bucket_scatter(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
                                     const float4* qhdr, const float* row_norms, int metric, const int64_t* cand_off,
                                     float* cand_key, int* cand_pos, void* tmp, hipStream_t s);
@@ -528,10 +531,11 @@ hipError_t launch_queries_prep(const float* q, int64_t nq, int d, int dp, int hx
 hipError_t launch_normalize_rows(const float* x, int64_t n, int d, float* n2, float* out, hipStream_t s);
 hipError_t launch_iota_i64(int64_t* out, int64_t n, int64_t start, int64_t step, hipStream_t s);
 hipError_t launch_fill_i32(int* out, int64_t n, int v, hipStream_t s);
+hipError_t launch_fill2_i32(int* o1, int64_t n1, int v1, int* o2, int64_t n2, int v2, hipStream_t s);
 
 // single-list job prep: bucket = identity over nq queries, slot base = q * chunks
 hipError_t launch_single_list_job(int64_t nq, int64_t chunks, int qtile, int64_t* bucket_q, int64_t* bucket_slot,
-                                  int* bucket_off, int* work_off, int64_t* slot_begin, hipStream_t s);
+                                  int* bucket_off, int* work_off, int64_t* slot_begin, hipStream_t s, int* zero = nullptr);
 // IVF probe map: probes [nq][np] (int64 list ids) -> buckets, work offsets, slot bases
 hipError_t launch_probe_map(const int64_t* probes, int64_t nq, int np, int n_lists, const int64_t* list_goff,
                             int chunk_groups, int qtile, int* counts, int* fill, int* bucket_off, int* work_off,

@@ -570,6 +570,7 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
       int head = 0;
       float hk = myk[0];
       int hp = myp[0];
+      float lastk = -INFINITY;
       for (int r = 0; r <= a.slot_k; ++r) {  // slot_k outputs, then the smallest key left behind
         float bk = hk;
         int bp = hp;
@@ -579,6 +580,15 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
             for (int t = r; t < a.slot_k; ++t) { a.slot_key[slot * a.slot_k + t] = INFINITY; a.slot_pos[slot * a.slot_k + t] = INT_MAX; }
           break;
         }
+        // nomination (slot_out): past slot_out keys and their ties, the slot's reader takes nothing more; the rest
+        // is empty and bk is the smallest key left behind (uniform within the 16-lane group, like bk)
+        if (a.slot_out > 0 && r >= a.slot_out && r < a.slot_k && bk != lastk) {
+          if (slot >= 0)
+            for (int t = r + src; t < a.slot_k; t += 16) { a.slot_key[slot * a.slot_k + t] = INFINITY; a.slot_pos[slot * a.slot_k + t] = INT_MAX; }
+          bnd = fminf(bnd, bk);
+          break;
+        }
+        lastk = bk;
         if (r < a.slot_k) {
           if (src == 0 && slot >= 0) {
             a.slot_key[slot * a.slot_k + r] = bk;

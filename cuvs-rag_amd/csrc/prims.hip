@@ -57,6 +57,29 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_down(const int64_t* __restr
   }
 }
 
+// one block for small n (the per-query offsets of a batch): the three launches above cost ~5 us each at any size
+constexpr int64_t kScanSmallMax = 4 * kScanTile;
+__global__ __launch_bounds__(kScanBlock) void k_scan_small(const int64_t* __restrict__ in, int64_t n,
+                                                           int64_t* __restrict__ out) {
+  __shared__ int64_t sh[16];
+  int64_t carry = 0;
+  for (int64_t b0 = 0; b0 < n; b0 += kScanTile) {
+    const int64_t base = b0 + (int64_t)threadIdx.x * kScanPerThread;
+    int64_t vals[kScanPerThread];
+    int64_t v = 0;
+#pragma unroll
+    for (int i = 0; i < kScanPerThread; ++i) { vals[i] = base + i < n ? in[base + i] : 0; v += vals[i]; }
+    int64_t tot;
+    int64_t run = carry + block_excl_scan(v, sh, &tot);
+#pragma unroll
+    for (int i = 0; i < kScanPerThread; ++i) {
+      if (base + i < n) out[base + i] = run;
+      run += vals[i];
+    }
+    carry += tot;
+  }
+}
+
 // ---------------- stable counting sort by label ----------------
 constexpr int kSortBlock = 1024;  // rows per histogram block (16 waves)
 
@@ -202,22 +225,22 @@ __global__ __launch_bounds__(1024) void k_probe_fill_lds(const int64_t* __restri
   }
 }
 
-__global__ void k_bucket_slot(int64_t* __restrict__ bucket_slot, int64_t n, const int64_t* __restrict__ qp_base) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < n) bucket_slot[e] = qp_base[bucket_slot[e]];
-}
-
-__global__ void k_slot_begin(const int64_t* __restrict__ qp_base, const int64_t* __restrict__ qp_slots, int64_t nq,
-                             int np, int64_t* __restrict__ slot_begin) {
-  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q < nq) slot_begin[q] = qp_base[q * np];
-  if (q == nq) slot_begin[nq] = qp_base[nq * np - 1] + qp_slots[nq * np - 1];
+// the output slot of every bucket entry (its (query, probe)'s first slot) and each query's first slot, one launch
+// (thread t: bucket entry t and query t)
+__global__ void k_bucket_slot_begin(int64_t* __restrict__ bucket_slot, int64_t n, const int64_t* __restrict__ qp_base,
+                                    const int64_t* __restrict__ qp_slots, int64_t nq, int np,
+                                    int64_t* __restrict__ slot_begin) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) bucket_slot[t] = qp_base[bucket_slot[t]];
+  if (t < nq) slot_begin[t] = qp_base[t * np];
+  if (t == nq) slot_begin[nq] = qp_base[nq * np - 1] + qp_slots[nq * np - 1];
 }
 
 __global__ void k_single_job(int64_t nq, int64_t chunks, int qtile, int64_t* __restrict__ bucket_q,
                              int64_t* __restrict__ bucket_slot, int* __restrict__ bucket_off,
-                             int* __restrict__ work_off, int64_t* __restrict__ slot_begin) {
+                             int* __restrict__ work_off, int64_t* __restrict__ slot_begin, int* __restrict__ zero) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (zero && q == 0) *zero = 0;  // (the scan's work counter: no memset launch of its own)
   if (q < nq) {
     bucket_q[q] = q;
     bucket_slot[q] = q * chunks;
@@ -240,6 +263,13 @@ __global__ void k_iota(int64_t* __restrict__ out, int64_t n, int64_t start, int6
 __global__ void k_fill_i32(int* __restrict__ out, int64_t n, int v) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = v;
+}
+
+// two fills in one launch (thread i: element i of each)
+__global__ void k_fill2_i32(int* __restrict__ o1, int64_t n1, int v1, int* __restrict__ o2, int64_t n2, int v2) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n1) o1[i] = v1;
+  if (i < n2) o2[i] = v2;
 }
 
 __global__ void k_group_list(const int64_t* __restrict__ list_goff, int n_lists, int64_t n_groups,
@@ -285,6 +315,10 @@ size_t scan_tmp_bytes(int64_t n) { return (size_t)(ceil_div(n > 0 ? n : 1, kScan
 
 hipError_t launch_exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, void* tmp, hipStream_t s) {
   if (n <= 0) return hipSuccess;
+  if (n <= kScanSmallMax) {
+    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(kScanBlock), 0, s, in, n, out);
+    return hipGetLastError();
+  }
   const int64_t nb = ceil_div(n, kScanTile);
   int64_t* sums = static_cast<int64_t*>(tmp);
   hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(kScanBlock), 0, s, in, n, sums);
@@ -365,15 +399,15 @@ hipError_t launch_probe_map(const int64_t* probes, int64_t nq, int np, int n_lis
   if (slot_begin == nullptr) return hipGetLastError();  // (K13: no per-(query, probe) output slots)
   e = launch_exclusive_scan_i64(qp_slots, qp_base, n, stmp, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_bucket_slot, grid1(n, 256), dim3(256), 0, s, bucket_slot, n, qp_base);
-  hipLaunchKernelGGL(k_slot_begin, grid1(nq + 1, 256), dim3(256), 0, s, qp_base, qp_slots, nq, np, slot_begin);
+  hipLaunchKernelGGL(k_bucket_slot_begin, grid1(n > nq ? n : nq + 1, 256), dim3(256), 0, s, bucket_slot, n, qp_base,
+                     qp_slots, nq, np, slot_begin);
   return hipGetLastError();
 }
 
 hipError_t launch_single_list_job(int64_t nq, int64_t chunks, int qtile, int64_t* bucket_q, int64_t* bucket_slot,
-                                  int* bucket_off, int* work_off, int64_t* slot_begin, hipStream_t s) {
+                                  int* bucket_off, int* work_off, int64_t* slot_begin, hipStream_t s, int* zero) {
   hipLaunchKernelGGL(k_single_job, grid1(nq, 256), dim3(256), 0, s, nq, chunks, qtile, bucket_q, bucket_slot,
-                     bucket_off, work_off, slot_begin);
+                     bucket_off, work_off, slot_begin, zero);
   return hipGetLastError();
 }
 
@@ -386,6 +420,13 @@ hipError_t launch_iota_i64(int64_t* out, int64_t n, int64_t start, int64_t step,
 hipError_t launch_fill_i32(int* out, int64_t n, int v, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_fill_i32, grid1(n, 256), dim3(256), 0, s, out, n, v);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill2_i32(int* o1, int64_t n1, int v1, int* o2, int64_t n2, int v2, hipStream_t s) {
+  const int64_t n = n1 > n2 ? n1 : n2;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fill2_i32, grid1(n, 256), dim3(256), 0, s, o1, n1, v1, o2, n2, v2);
   return hipGetLastError();
 }
 

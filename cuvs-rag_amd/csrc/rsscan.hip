@@ -612,24 +612,34 @@ __global__ void k_rs_headers(const float* __restrict__ pre_kth, int64_t nq, cons
 // Piece s = 2 t + qb, lane (c, kq) = (L & 15, L >> 4): dims 32 t + 8 kq .. + 8 of query 16 qb + c (the B
 // operand of v_mfma_f32_16x16x32_f16).
 template <int NK>
-// one workgroup per tile slot (rs_tile_slot: list l's tiles start at bucket_off[l] / 32 + l): the tile's 32
-// query ids staged in LDS, then its NK pieces in image order (lane L of piece s fastest: every wave-instruction
-// stores 1 KiB contiguous; lanes L and L + 32 read the two adjacent 16-B halves of one query's 32 B of k-step s)
-// and its header piece. (A workgroup per list had ~10 tiles' worth of dependent id -> row loads per thread.)
+// one workgroup per tile slot (rs_tile_slot: list l's tiles start at bucket_off[l] / 32 + l): wave 0 finds the slot's
+// list (64 probes per round: two dependent rounds of loads up to 4,096 lists, where a one-thread binary search took
+// log2(n_lists)), the tile's 32 query ids are staged in LDS, then its NK pieces in image order (lane L of piece s
+// fastest: every wave-instruction stores 1 KiB contiguous; lanes L and L + 32 read the two adjacent 16-B halves of
+// one query's 32 B of k-step s), all of a thread's loads issued before its stores, and the header piece.
+// (A workgroup per list had ~10 tiles' worth of dependent id -> row loads per thread.)
 __global__ __launch_bounds__(256) void k_rs_tiles(const int64_t* __restrict__ bucket_q, const int* __restrict__ bucket_off,
                                                  int n_lists, const uint16_t* __restrict__ qh,
                                                  const float4* __restrict__ qhdr, int nq, char* __restrict__ tiles) {
   constexpr int64_t IMG = (int64_t)(NK + 1) * 1024;
+  static_assert(NK % 4 == 0, "NK * 64 pieces over 256 threads");
+  constexpr int PER = NK / 4;
   __shared__ int s_l;
   __shared__ int s_q[kRsQTile];
   const int b = blockIdx.x;
-  if (threadIdx.x == 0) {
-    int lo = 0, hi = n_lists - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (bucket_off[mid] / kRsQTile + mid <= b) lo = mid; else hi = mid - 1;
+  if (threadIdx.x < 64) {
+    // the largest l with bucket_off[l] / 32 + l <= b (the slot function is increasing in l; l = 0 gives 0 <= b)
+    const int lane = threadIdx.x;
+    int lo = 0, n = n_lists;  // the answer lies in [lo, lo + n)
+    while (n > 1) {
+      const int step = (n + 63) / 64;
+      const int l = lo + lane * step;
+      const bool ok = lane * step < n && (bucket_off[l] / kRsQTile + l <= b);
+      const int c = __popcll(__ballot(ok));  // probes 0 .. c - 1 pass (c >= 1: probe 0 is lo, which passes)
+      lo += (c - 1) * step;
+      n = min(step, n - (c - 1) * step);
     }
-    s_l = lo;
+    if (lane == 0) s_l = lo;
   }
   __syncthreads();
   const int l = s_l;
@@ -642,18 +652,24 @@ __global__ __launch_bounds__(256) void k_rs_tiles(const int64_t* __restrict__ bu
   }
   __syncthreads();
   char* img = tiles + (int64_t)b * IMG;
-  for (int i = threadIdx.x; i < NK * 64; i += 256) {
+  uint4 v[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int i = threadIdx.x + u * 256;
     const int s = i >> 6, L = i & 63;
     const int q = s_q[16 * (s & 1) + (L & 15)];
     const int dim0 = 32 * (s >> 1) + 8 * (L >> 4);
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (q >= 0) v = *reinterpret_cast<const uint4*>(qh + (int64_t)q * (NK * 16) + dim0);
-    *reinterpret_cast<uint4*>(img + s * 1024 + L * 16) = v;
+    v[u] = make_uint4(0u, 0u, 0u, 0u);
+    if (q >= 0) v[u] = *reinterpret_cast<const uint4*>(qh + (int64_t)q * (NK * 16) + dim0);
   }
+  float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
   if (threadIdx.x < 64) {
     const int q = s_q[threadIdx.x & 31];
-    *reinterpret_cast<float4*>(img + NK * 1024 + threadIdx.x * 16) = qhdr[q >= 0 ? q : nq];
+    h = qhdr[q >= 0 ? q : nq];
   }
+#pragma unroll
+  for (int u = 0; u < PER; ++u) *reinterpret_cast<uint4*>(img + (int64_t)(threadIdx.x + u * 256) * 16) = v[u];
+  if (threadIdx.x < 64) *reinterpret_cast<float4*>(img + NK * 1024 + threadIdx.x * 16) = h;
 }
 
 }  // namespace
@@ -741,9 +757,14 @@ hipError_t launch_rs_items(const int* work_off, const int* bucket_off, const int
 // exact filter value fma(acc, mm, xn) passes uf -- the same test, on the same values, as a per-row test in
 // K13's epilogue would make -- each with its approximate key. A stream longer than its capacity lost
 // records of unknown queries: `lost` is then set and K11 proves no query (every query goes to the fallback).
+// (it also zeroes the count kernel's per-query counters and the scatter's fills: zero[0 .. nzero) in 16-B words)
 __global__ __launch_bounds__(1024) void k_rs_stream_off(const int* __restrict__ wave_cnt, int n_waves, int wave_cap,
-                                                        int64_t* __restrict__ woff, int* __restrict__ lost) {
+                                                        int64_t* __restrict__ woff, int* __restrict__ lost,
+                                                        int4* __restrict__ zero, int64_t nzero,
+                                                        int4* __restrict__ zero2, int nzero2) {
   __shared__ int64_t sh[16];
+  for (int64_t i = threadIdx.x; i < nzero; i += 1024) zero[i] = make_int4(0, 0, 0, 0);
+  if (threadIdx.x < nzero2) zero2[threadIdx.x] = make_int4(0, 0, 0, 0);  // (the final refine's stats)
   int64_t base = 0;
   for (int w0 = 0; w0 < n_waves; w0 += 1024) {
     const int w = w0 + threadIdx.x;
@@ -977,12 +998,21 @@ static RsBucketTmp rs_bucket_tmp(void* tmp, int nq, int n_waves) {
 
 hipError_t launch_rs_bucket_count(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
                                   const float4* qhdr, const float* row_norms, int metric, int64_t* cand_off, void* tmp,
-                                  int* lost, hipStream_t s) {
+                                  int* lost, hipStream_t s, void* zero2, int zero2_bytes) {
   const RsBucketTmp t = rs_bucket_tmp(tmp, nq, n_waves);
-  hipError_t e = hipMemsetAsync(t.qcnt, 0, sizeof(int64_t) * ((size_t)nq + 1) + sizeof(int) * (size_t)nq, s);
-  if (e != hipSuccess) return e;
-  if (n_waves <= 0) return launch_exclusive_scan_i64(t.qcnt, cand_off, nq + 1, t.stmp, s);
-  hipLaunchKernelGGL(k_rs_stream_off, dim3(1), dim3(1024), 0, s, wave_cnt, n_waves, wave_cap, t.woff, lost);
+  if (zero2_bytes % 16 != 0 || zero2_bytes > 16 * 1024 || (reinterpret_cast<uintptr_t>(zero2) & 15) != 0)
+    return hipErrorInvalidValue;
+  // qcnt [nq + 1] and fill [nq], rounded up to the 16-B boundary where woff starts (rs_bucket_tmp)
+  const size_t zbytes = reinterpret_cast<char*>(t.woff) - reinterpret_cast<char*>(t.qcnt);
+  if (n_waves <= 0) {
+    hipError_t e = hipMemsetAsync(t.qcnt, 0, zbytes, s);
+    if (e == hipSuccess && zero2_bytes > 0) e = hipMemsetAsync(zero2, 0, zero2_bytes, s);
+    if (e != hipSuccess) return e;
+    return launch_exclusive_scan_i64(t.qcnt, cand_off, nq + 1, t.stmp, s);
+  }
+  if ((reinterpret_cast<uintptr_t>(t.qcnt) & 15) != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_rs_stream_off, dim3(1), dim3(1024), 0, s, wave_cnt, n_waves, wave_cap, t.woff, lost,
+                     reinterpret_cast<int4*>(t.qcnt), (int64_t)(zbytes / 16), static_cast<int4*>(zero2), zero2_bytes / 16);
   return metric == kIP ? rs_bucket_count_m<kIP>(wave_buf, wave_cap, wave_cnt, n_waves, nq, qhdr, row_norms, cand_off,
                                                 t.qcnt, t.stmp, s)
                        : rs_bucket_count_m<kL2>(wave_buf, wave_cap, wave_cnt, n_waves, nq, qhdr, row_norms, cand_off,
@@ -1002,10 +1032,11 @@ hipError_t launch_rs_bucket_scatter(const int4* wave_buf, int wave_cap, const in
 
 hipError_t launch_rs_bucket(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
                             const float4* qhdr, const float* row_norms, int metric, int64_t* cand_off,
-                            float* cand_key, int* cand_pos, void* tmp, int* lost, int grid, hipStream_t s) {
+                            float* cand_key, int* cand_pos, void* tmp, int* lost, int grid, hipStream_t s,
+                            void* zero2, int zero2_bytes) {
   (void)grid;
   hipError_t e = launch_rs_bucket_count(wave_buf, wave_cap, wave_cnt, n_waves, nq, qhdr, row_norms, metric, cand_off,
-                                        tmp, lost, s);
+                                        tmp, lost, s, zero2, zero2_bytes);
   if (e != hipSuccess) return e;
   return launch_rs_bucket_scatter(wave_buf, wave_cap, wave_cnt, n_waves, nq, qhdr, row_norms, metric, cand_off,
                                   cand_key, cand_pos, tmp, s);
@@ -1031,33 +1062,32 @@ hipError_t launch_group_nmin(const float* norms, int64_t n_groups, float* out, h
 // at most all) and 2l + 1 = the rest, so the n_probes = 1 search of probe 2 p0 scans a sample of the
 // nearest list p0 with the unchanged K10 / probe map (the sample's rows are still rows of the probed
 // lists, so its k-th exact key bounds the final k-th from above)
-__global__ void k_rs_pre_goff(const int64_t* __restrict__ goff, int n_lists, int div, int min_groups,
-                              int64_t* __restrict__ goff2) {
-  const int l = blockIdx.x * blockDim.x + threadIdx.x;
-  if (l > n_lists) return;
+__global__ void k_rs_pre_lists(const int64_t* __restrict__ goff, int n_lists, int div, int min_groups,
+                               int64_t* __restrict__ goff2, const int64_t* __restrict__ probes, int64_t nq, int np,
+                               int64_t* __restrict__ probes2) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // every probe of the batch's queries -> the sample list of its nearest probe (2 p0); -1 (no probe) stays -1
+  if (t < nq) {
+    const int64_t p = probes[t * np];
+    probes2[t] = p < 0 ? p : 2 * p;
+  }
+  if (t > n_lists) return;
+  const int l = (int)t;
   const int64_t b = goff[l];
   goff2[2 * l] = b;
   if (l == n_lists) return;
   const int64_t ng = goff[l + 1] - b;
-  int64_t t = (ng + div - 1) / div;
-  t = t < min_groups ? min_groups : t;
-  goff2[2 * l + 1] = b + (t < ng ? t : ng);
-}
-
-__global__ void k_rs_pre_probes(const int64_t* __restrict__ probes, int64_t nq, int np, int64_t* __restrict__ out) {
-  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= nq) return;
-  const int64_t p = probes[q * np];
-  out[q] = p < 0 ? p : 2 * p;
+  int64_t m = (ng + div - 1) / div;
+  m = m < min_groups ? min_groups : m;
+  goff2[2 * l + 1] = b + (m < ng ? m : ng);
 }
 
 hipError_t launch_rs_pre_lists(const int64_t* goff, int n_lists, int div, int min_groups, const int64_t* probes,
                                int64_t nq, int np, int64_t* goff2, int64_t* probes2, hipStream_t s) {
   if (div < 1 || min_groups < 1) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_rs_pre_goff, dim3((unsigned)ceil_div(n_lists + 1, 256)), dim3(256), 0, s, goff, n_lists, div,
-                     min_groups, goff2);
-  if (nq > 0)
-    hipLaunchKernelGGL(k_rs_pre_probes, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, s, probes, nq, np, probes2);
+  const int64_t n = nq > n_lists + 1 ? nq : n_lists + 1;  // (one launch for the split offsets and the probes)
+  hipLaunchKernelGGL(k_rs_pre_lists, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, goff, n_lists, div, min_groups,
+                     goff2, probes, nq, np, probes2);
   return hipGetLastError();
 }
 

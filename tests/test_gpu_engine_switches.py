@@ -68,6 +68,7 @@ SEARCH_SWITCHES = [
     {"MIVS_RS_FLAGS": "24"},                                          # K13 clocks (stderr only)
     {"MIVS_RS_WAVE_CAP": "2"},                                        # K13 streams overflow: the fallback
     {"MIVS_PF_ROWSTAT": "0", "MIVS_PF_FLAGS": "32"},                  # K10 phase clocks (stderr only)
+    {"MIVS_PF_SLOT_OUT": "0"},                                        # pre-pass merges whole slots
 ]
 
 
@@ -81,6 +82,22 @@ def test_ivf_search_switch_same_bits(ivf, flat_data, monkeypatch, env):
     d1, i1 = _search(idx, q)
     np.testing.assert_array_equal(i1, i0)
     np.testing.assert_array_equal(_bits(d1), _bits(d0))
+
+
+def test_ivf_prepass_slot_out_same_candidates(ivf, flat_data, monkeypatch):
+    """the pre-pass merge stops after the nominees (MIVS_PF_SLOT_OUT): K11v takes the same rows, so T_q and with
+    it K13's candidate count are unchanged, not only the answer"""
+    idx, _ = ivf
+    _, q = flat_data
+    d0, i0 = _search(idx, q)
+    st0 = idx.last_search_stats()
+    monkeypatch.setenv("MIVS_PF_SLOT_OUT", "0")
+    d1, i1 = _search(idx, q)
+    st1 = idx.last_search_stats()
+    np.testing.assert_array_equal(i1, i0)
+    np.testing.assert_array_equal(_bits(d1), _bits(d0))
+    assert st0["scan_kernel"] == st1["scan_kernel"] == 13
+    assert st0["candidates"] == st1["candidates"]
 
 
 def test_ivf_default_matches_oracle(ivf, flat_data):
