@@ -98,6 +98,7 @@ struct Workspace {
   Buf pre_probes, pre_kth, pre_goff, qhdr, rs_tq, cand_off, cand_key, cand_pos, rs_bucket_tmp, rs_tiles, rs_wave_buf,
       rs_wave_cnt, rs_bounds;
   // per-list query counts of the last search's own probe map (an exact fallback re-maps its queries)
+  Buf rs_qcnt;  // K13's one-pass bucketing: candidates per query
   Buf stat_counts, rs_ovf_q, rs_ovf_rows, rs_ovf_d, rs_ovf_i, rs_items;
   // K16 large-k: T_q's sample probes and selection, the per-query windows and K16r's work items
   Buf lk_probes, lk_win_pos, lk_win_key, lk_win_n, lk_chunks, lk_chunk_off;
@@ -160,6 +161,7 @@ struct mivs_index_s {
   int last_scan = 0;  // fine-scan kernel of the last search: 3 K3, 31 K3w, 10 K10, 12 K12, 13 K13
   int last_rs_waves = 0;  // K13: candidate streams of the last search (the lost flag follows their counts)
   int64_t last_rs_nq = 0; // K13: queries of the last search batch (its cand_off holds last_rs_nq + 1 offsets)
+  bool last_rs_one_pass = false;  // K13: the last batch's candidates are in fixed-capacity runs (ws.rs_qcnt)
   int64_t last_ovf = 0, last_window = 0;
   // host wall time of the build's phases (mivs_index_build_phases; recorded while profiling is on)
   std::vector<double> build_phase_s;
@@ -828,7 +830,7 @@ void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_
                         int64_t* out_i, const float* slot_key, const int* slot_pos, const float* slot_bound,
                         const int* force_ovf, const int64_t* slot_begin, int slot_k, bool fallback_pf = false,
                         float* kth_out = nullptr, const float* window_cap = nullptr, int verify_sel = 0,
-                        bool stats_zeroed = false);
+                        bool stats_zeroed = false, const int* slot_cnt = nullptr, int slot_cap = 0);
 
 // K10 scan + K11 refine for a probe map built with (kPfChunkGroups, kPfQTile); queries the refine
 // could not prove are re-run through the exact scan and scattered back.
@@ -939,7 +941,8 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
 void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                         int64_t* out_i, const float* slot_key, const int* slot_pos, const float* slot_bound,
                         const int* force_ovf, const int64_t* slot_begin, int slot_k, bool fallback_pf,
-                        float* kth_out, const float* window_cap, int verify_sel, bool stats_zeroed) {
+                        float* kth_out, const float* window_cap, int verify_sel, bool stats_zeroed,
+                        const int* slot_cnt, int slot_cap) {
   Workspace& ws = idx->ws;
   const ListSet& L = idx->lists;
   const int dp = idx->dp;
@@ -956,6 +959,8 @@ void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_
   r.kth_out = kth_out;
   r.verify_sel = verify_sel;
   r.slot_begin = slot_begin;
+  r.slot_cnt = slot_cnt;
+  r.slot_cap = slot_cap;
   r.slot_k = slot_k;
   r.nq = nq;
   r.k = k;
@@ -1031,6 +1036,8 @@ bool coarse_dump(int np) {
 // batch over 1024 centroids is only 313 query tiles -- with K7 merging the chunks' top-n_probes
 int coarse_groups(const mivs_index_s* idx, int64_t nq) {
   const int64_t ng = std::max<int64_t>(1, idx->cents.n_groups);
+  const char* ge = getenv("MIVS_COARSE_G");  // (A/B runs: groups per coarse work item)
+  if (ge && atoi(ge) > 0) return (int)std::max<int64_t>(1, std::min<int64_t>(idx->G, atoi(ge)));
   const int64_t tiles = std::max<int64_t>(1, ceil_div(nq, kQTile));
   const int64_t chunks = std::min<int64_t>(ng, std::max<int64_t>(1, ceil_div(4LL * cu_count(idx->device), tiles)));
   return (int)std::max<int64_t>(1, std::min<int64_t>(idx->G, ceil_div(ng, chunks)));
@@ -1056,6 +1063,7 @@ void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t 
     HIPCHK(launch_queries_prep(q, nq, idx->d, idx->dp, idx->hx_exp, idx->hx8, ws.qn.as<float>(), ws.qh.as<uint16_t>(),
                                ws.qscale.as<float>(), ws.qres.as<float>(), f8 ? ws.q8.as<uint8_t>() : nullptr,
                                f8 ? ws.qscale8.as<float>() : nullptr, s));
+    if (host_trace().on) host_trace().t_first = std::chrono::steady_clock::now();
     ws.prep_q = q;
     ws.prep_nq = nq;
     ws.prep_f8 = f8;
@@ -1086,6 +1094,20 @@ bool rs_pre_f8(mivs_index_s* idx, hipStream_t) {
   const char* e = getenv("MIVS_RS_PRE_F8");
   if (e && e[0] == '0') return false;
   return idx->groups_f8.p != nullptr;
+}
+
+// K13's bucketing in one pass into fixed-capacity per-query runs (MIVS_RS_BUCKET_1P=0: the two-pass CSR form);
+// MIVS_RS_QCAP: the run capacity (a query with more candidates is not proven and takes the fallback)
+bool rs_bucket_one_pass() {
+  const char* e = getenv("MIVS_RS_BUCKET_1P");
+  return !(e && e[0] == '0');
+}
+// (default: the batch's share of kRsCandBudget entries, at least kRsQCap, at most the rows a query can probe)
+int rs_qcap(int64_t nq, int64_t max_probed) {
+  const char* e = getenv("MIVS_RS_QCAP");
+  if (e && atoi(e) > 0) return atoi(e);
+  const int64_t c = std::max<int64_t>(kRsQCap, kRsCandBudget / std::max<int64_t>(nq, 1));
+  return (int)std::max<int64_t>(1, std::min<int64_t>({c, max_probed, INT32_MAX / 2}));
 }
 
 // records per K13 stream: twice the batch's queries, at most kRsWaveCapMax (MIVS_RS_WAVE_CAP overrides it: the
@@ -1349,8 +1371,16 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   ws.qhdr.reserve(sizeof(float4) * (nq + 1));
   float4* qhdr = ws.qhdr.as<float4>();
   ws.rs_tq.reserve(sizeof(float) * nq);
+  const bool one_pass = !large && rs_bucket_one_pass();
+  idx->last_rs_one_pass = one_pass;
+  if (one_pass) {  // (the headers' launch zeroes the one-pass bucketing's counts and the final refine's stats)
+    ws.rs_qcnt.reserve(sizeof(int) * (size_t)nq);
+    ws.pf_stats.reserve(32);
+  }
   HIPCHK(launch_rs_headers(ws.pre_kth.as<float>(), nq, ws.qscale.as<float>(), ws.qn.as<float>(), ws.qres.as<float>(),
-                           idx->x_norm_max, idx->x_res_max, dp, idx->metric, qhdr, ws.rs_tq.as<float>(), s));
+                           idx->x_norm_max, idx->x_res_max, dp, idx->metric, qhdr, ws.rs_tq.as<float>(), s,
+                           one_pass ? ws.rs_qcnt.as<int>() : nullptr, one_pass ? nq : 0,
+                           one_pass ? ws.pf_stats.as<int>() : nullptr, one_pass ? 8 : 0));
   if (getenv("MIVS_RS_PRE_STATS")) {  // diagnostic: the pre-pass's k-th keys and T_q (stderr)
     std::vector<float> hk(nq), ht(nq);
     HIPCHK(hipMemcpyAsync(hk.data(), ws.pre_kth.p, sizeof(float) * nq, hipMemcpyDeviceToHost, s));
@@ -1397,7 +1427,11 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
                          (int)nq, dp, ws.rs_tiles.as<char>(), s));
   // 4. K13
   int64_t max_items = 0;  // every list probed: the item table's bound (the probe map decides the count)
-  for (int l = 0; l < L.n_lists; ++l) max_items += ceil_div(L.h_goff[l + 1] - L.h_goff[l], kRsBlockGroups);
+  int64_t max_groups = 1;  // the largest list's groups (a query's candidates are at most np of its lists' rows)
+  for (int l = 0; l < L.n_lists; ++l) {
+    max_items += ceil_div(L.h_goff[l + 1] - L.h_goff[l], kRsBlockGroups);
+    max_groups = std::max<int64_t>(max_groups, L.h_goff[l + 1] - L.h_goff[l]);
+  }
   ws.rs_items.reserve(sizeof(int4) * (size_t)std::max<int64_t>(max_items, 1));
   // items dealt from 8 queues of equal tile work, dynamically inside a queue
   ws.rs_bounds.reserve(sizeof(int) * 9);
@@ -1479,6 +1513,18 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   ws.cand_off.reserve(sizeof(int64_t) * (nq + 1));
   ws.rs_bucket_tmp.reserve(rs_bucket_tmp_bytes((int)nq, n_waves));
   ws.pf_stats.reserve(32);
+  if (one_pass) {
+    const int cap = rs_qcap(nq, (int64_t)np * max_groups * kGroupRows);
+    ws.cand_key.reserve(sizeof(float) * (size_t)nq * cap);
+    ws.cand_pos.reserve(sizeof(int) * (size_t)nq * cap);
+    HIPCHK(launch_rs_bucket_fused(a.wave_buf, a.wave_cap, a.wave_cnt, n_waves, (int)nq, qhdr, a.row_norms, idx->metric,
+                                  cap, ws.rs_qcnt.as<int>(), ws.cand_key.as<float>(), ws.cand_pos.as<int>(), s));
+    // 5. exact ranking of every query's run; a window above T_q, or a run that dropped candidates, is not proven
+    pf_refine_fallback(idx, s, q, nq, k, np, out_d, out_i, ws.cand_key.as<float>(), ws.cand_pos.as<int>(), nullptr,
+                       a.wave_cnt + n_waves, nullptr, 1, true, nullptr, ws.rs_tq.as<float>(), 0, true,
+                       ws.rs_qcnt.as<int>(), cap);
+    return;
+  }
   if (!large) {
     const size_t max_cand = (size_t)n_waves * a.wave_cap * 8;
     ws.cand_key.reserve(sizeof(float) * max_cand);
@@ -1954,7 +2000,21 @@ int32_t mivs_ivf_flat_search(mivs_index_t idx, void* stream, const float* d_q, i
     const int np = std::min<int>(n_probes, idx->lists.n_lists);
     require(np <= kMaxSelectK, "n_probes must be <= " + std::to_string(kMaxSelectK), MIVS_ERR_UNSUPPORTED);
     require(np == n_probes || d_probes == nullptr, "n_probes > n_lists with a probes output");
+    HostTrace& ht = host_trace();
+    static const bool trace = getenv("MIVS_HOST_TRACE") && getenv("MIVS_HOST_TRACE")[0] == '1';
+    ht.on = trace;
+    if (trace) {
+      ht.n_wait = 0;
+      ht.t0 = std::chrono::steady_clock::now();
+    }
     ivf_search_impl(idx, static_cast<hipStream_t>(stream), d_q, nq, k, np, d_dist, d_ids, d_probes);
+    if (trace) {
+      const auto t1 = std::chrono::steady_clock::now();
+      auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+      fprintf(stderr, "[host] entry->first launch %.1f us, ->wait %.1f us, wait %.1f us (%d), wait->exit %.1f us\n",
+              us(ht.t0, ht.t_first), us(ht.t_first, ht.t_wait0), us(ht.t_wait0, ht.t_wait1), ht.n_wait,
+              us(ht.t_wait1, t1));
+    }
   });
 }
 
@@ -2555,8 +2615,14 @@ int32_t mivs_index_last_search_stats(mivs_index_t idx, mivs_search_stats* out) {
         // the candidates K13 appended; a lost stream entry sends every query to the fallback
         int64_t total = 0;
         int lost[10] = {};
-        HIPCHK(hipMemcpy(&total, idx->ws.cand_off.as<int64_t>() + idx->last_rs_nq, sizeof(int64_t),
-                         hipMemcpyDeviceToHost));
+        if (idx->last_rs_one_pass) {  // (per-query counts of the fixed-capacity runs, dropped entries included)
+          std::vector<int> qc((size_t)idx->last_rs_nq);
+          HIPCHK(hipMemcpy(qc.data(), idx->ws.rs_qcnt.p, sizeof(int) * qc.size(), hipMemcpyDeviceToHost));
+          for (int c : qc) total += c;
+        } else {
+          HIPCHK(hipMemcpy(&total, idx->ws.cand_off.as<int64_t>() + idx->last_rs_nq, sizeof(int64_t),
+                           hipMemcpyDeviceToHost));
+        }
         HIPCHK(hipMemcpy(lost, idx->ws.rs_wave_cnt.as<int>() + idx->last_rs_waves, sizeof(lost), hipMemcpyDeviceToHost));
         st.candidates = total;
         st.spun_out_waves = lost[9];

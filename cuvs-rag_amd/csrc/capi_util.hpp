@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <chrono>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -103,12 +104,26 @@ struct HostBuf {
 
 // Wait for the stream by polling it: the search's one host sync (the fallback size) sits on the step's critical
 // path, and a blocking wait's wake-up adds tens of microseconds to every batch
+// host-side timeline of a search (MIVS_HOST_TRACE=1: stderr per call; diagnostics only)
+struct HostTrace {
+  bool on = false;
+  std::chrono::steady_clock::time_point t0, t_first, t_wait0, t_wait1;
+  int n_wait = 0;
+};
+inline HostTrace& host_trace() {
+  static thread_local HostTrace t;
+  return t;
+}
+
 inline void spin_wait(hipStream_t s) {
+  HostTrace& ht = host_trace();
+  if (ht.on && ht.n_wait++ == 0) ht.t_wait0 = std::chrono::steady_clock::now();
   for (;;) {
     const hipError_t e = hipStreamQuery(s);
-    if (e == hipSuccess) return;
+    if (e == hipSuccess) break;
     if (e != hipErrorNotReady) HIPCHK(e);
   }
+  if (ht.on) ht.t_wait1 = std::chrono::steady_clock::now();
 }
 
 inline int cu_count(int device) {

@@ -261,6 +261,8 @@ constexpr int kRsBlockGroups = kRsWaves;
 constexpr int kRsPreDiv = 4;
 constexpr int kRsPreDivF8 = 4;
 constexpr int kRsPreSel = 10;
+constexpr int kRsQCap = 4096;  // K13 one-pass bucketing: least candidates per query run (MIVS_RS_QCAP)
+constexpr int64_t kRsCandBudget = int64_t(1) << 27;  // ... and the batch's runs: 128M entries (1 GiB of key + position)
 constexpr int kRsWaveCapMax = 16384;  // records of a K13 wave's candidate stream (more: all queries fall back)
 constexpr int kRsWaveCapMaxLk = 1 << 18;  // the same for large k (K16: thousands of candidates per query)
 constexpr int kRsRecInt4 = 3;         // a record: 8 dots of one lane and query half + {first row position, query}
@@ -403,6 +405,8 @@ struct PfRefineArgs {
   int verify_sel;             // with kth_out: > 0 -> the candidates with the verify_sel smallest keys (nomination
                               // scores) get fp32 keys (within delta of their pinned keys), and kth_out is the k-th
                               // smallest of THOSE
+  const int* slot_cnt;        // optional (K13's one-pass bucketing): query q's run is [q * slot_cap, + min(cnt, cap))
+  int slot_cap;               // instead of slot_begin; cnt > cap: candidates were dropped, the query is not proven
 };
 
 hipError_t launch_pf_scan(const PfScanArgs& a, int grid, size_t lds, hipStream_t s);
@@ -461,6 +465,11 @@ hipError_t launch_rs_bucket(const int4* wave_buf, int wave_cap, const int* wave_
 hipError_t launch_rs_bucket_count(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
                                   const float4* qhdr, const float* row_norms, int metric, int64_t* cand_off, void* tmp,
                                   int* lost, hipStream_t s, void* zero2 = nullptr, int zero2_bytes = 0);
+// one pass (the k <= 16 path): each query's candidates go to a fixed-capacity run [q * cap, q * cap + qcnt[q]) (entries
+// past cap are dropped and counted: K11 then proves nothing for that query); qcnt [nq] must be zero on entry
+hipError_t launch_rs_bucket_fused(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
+                                  const float4* qhdr, const float* row_norms, int metric, int cap, int* qcnt,
+                                  float* cand_key, int* cand_pos, hipStream_t s);
 hipError_t launch_rs_bucket_scatter(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
                                     const float4* qhdr, const float* row_norms, int metric, const int64_t* cand_off,
                                     float* cand_key, int* cand_pos, void* tmp, hipStream_t s);
@@ -481,7 +490,8 @@ hipError_t launch_rs_tiles(const int64_t* bucket_q, const int* bucket_off, int n
 // tq (optional): T_q per query, the bound K11 checks its final window against
 hipError_t launch_rs_headers(const float* pre_kth, int64_t nq, const float* qscale, const float* qnorms,
                              const float* qres, float x_norm_max, float x_res_max, int dp, int metric, float4* hdr,
-                             float* tq, hipStream_t s);
+                             float* tq, hipStream_t s, int* zero = nullptr, int64_t nzero = 0,
+                             int* zero2 = nullptr, int nzero2 = 0);
 hipError_t launch_gather_ids(const int64_t* src, const int64_t* idx, int64_t n, int64_t* out, hipStream_t s);
 constexpr unsigned kPfOrdInf = 0xFF800000u;  // order mapping of +inf (qtheta's initial value)
 // fp32 groups -> fp16 groups scaled by 2^hx_exp (FTZ below the fp16 normal range), per-index maxima of

@@ -638,10 +638,21 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
   const bool live = q < a.nq;
   const int k = a.k;
   int64_t sb = 0, se = 0;
-  if (live) { sb = a.slot_begin[q]; se = a.slot_begin[q + 1]; }
+  bool cap_ovf = false;  // (slot_cnt: the query's fixed-capacity run dropped candidates)
+  if (live) {
+    if (a.slot_cnt) {
+      const int c = a.slot_cnt[q];
+      sb = q * (int64_t)a.slot_cap;
+      se = sb + (c < a.slot_cap ? c : a.slot_cap);
+      cap_ovf = c > a.slot_cap;
+    } else {
+      sb = a.slot_begin[q];
+      se = a.slot_begin[q + 1];
+    }
+  }
   const int64_t c1 = se * a.slot_k;
-  // (K13: slot_k = 1 and slot_begin the per-query CSR runs of unsorted candidates)
-  const bool cnt_ovf = a.force_ovf && *a.force_ovf;
+  // (K13: slot_k = 1 and slot_begin the per-query CSR runs of unsorted candidates, or slot_cnt the fixed-capacity runs)
+  const bool cnt_ovf = (a.force_ovf && *a.force_ovf) || cap_ovf;
 
   // phase 1: Ak = k-th smallest approximate key. Up to kPfSelRegs * 64 candidates (K13's runs: ~200 per query at the
   // benchmark shape): held in registers, a 32-step radix select over their orderable bits -- the largest u with

@@ -577,8 +577,12 @@ __global__ __launch_bounds__(1024) void k_rs_bounds(const int* __restrict__ work
 template <int METRIC>
 __global__ void k_rs_headers(const float* __restrict__ pre_kth, int64_t nq, const float* __restrict__ qscale,
                              const float* __restrict__ qnorms, const float* __restrict__ qres, float x_norm_max,
-                             float x_res_max, int dp, float4* __restrict__ hdr, float* __restrict__ tq) {
+                             float x_res_max, int dp, float4* __restrict__ hdr, float* __restrict__ tq,
+                             int* __restrict__ zero, int64_t nzero, int* __restrict__ zero2, int nzero2) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // (zero[0 .. nzero): the one-pass bucketing's per-query counts (nzero <= nq + 1), zero2: the final refine's stats)
+  if (q < nzero) zero[q] = 0;
+  if (q < nzero2) zero2[q] = 0;
   if (q > nq) return;
   if (q == nq) {  // the null header
     hdr[q] = make_float4(0.0f, -INFINITY, -INFINITY, __int_as_float(-1));
@@ -930,6 +934,45 @@ __global__ __launch_bounds__(1024) void k_rs_scatter_lds(const int4* __restrict_
   }
 }
 
+// The one-pass bucketing (k <= 16): the group's LDS histogram, then ONE global atomic per (group, query) that reserves
+// the group's range inside the query's fixed-capacity run, then the scatter -- the count kernel, the scan over the
+// queries and the second pass over the records of the two-pass form are gone (K11 reads the runs by count).
+template <int METRIC>
+__global__ __launch_bounds__(1024) void k_rs_bucket_fused(const int4* __restrict__ wave_buf, int wave_cap,
+                                                          const int* __restrict__ wave_cnt, int J, int nq,
+                                                          const float4* __restrict__ qhdr,
+                                                          const float* __restrict__ row_norms, int cap,
+                                                          int* __restrict__ qcnt, float* __restrict__ key,
+                                                          int* __restrict__ pos) {
+  extern __shared__ int bins[];
+  __shared__ int pre[kRsMaxGroupStreams + 1];
+  const int n = rs_group_hist<METRIC>(wave_buf, wave_cap, wave_cnt, J, nq, qhdr, row_norms, bins, pre);
+  for (int i = threadIdx.x; i < nq; i += blockDim.x) {
+    const int c = bins[i];
+    if (c) bins[i] = atomicAdd(qcnt + i, c);  // the group's first entry in query i's run
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < n; e += blockDim.x) {
+    const RsRec r = rs_rec_load(rs_group_rec(wave_buf, wave_cap, J, pre, e));
+    const float4 h = qhdr[r.q];
+    float xn[8];
+    const unsigned m = rs_rec_hits<METRIC>(r, h, row_norms, xn);
+    if (!m) continue;
+    int at = atomicAdd(bins + r.q, __popc(m));
+    const int64_t base = (int64_t)r.q * cap;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (m & (1u << i)) {
+        if (at < cap) {
+          const float c = i < 4 ? r.c0[i] : r.c1[i - 4];
+          key[base + at] = pf_key<METRIC>(c, h.x, xn[i], h.z);
+          pos[base + at] = rs_rec_row(r.pos0, i);
+        }
+        ++at;
+      }
+  }
+}
+
 size_t rs_bucket_tmp_bytes(int nq, int n_waves) {
   return sizeof(int64_t) * ((size_t)nq + 1) + sizeof(int) * (size_t)nq + sizeof(int64_t) * ((size_t)n_waves + 1) +
          scan_tmp_bytes(nq + 1) + 64;
@@ -994,6 +1037,33 @@ static RsBucketTmp rs_bucket_tmp(void* tmp, int nq, int n_waves) {
       reinterpret_cast<char*>(tmp) + ((sizeof(int64_t) * ((size_t)nq + 1) + sizeof(int) * (size_t)nq + 15) & ~(size_t)15));
   t.stmp = reinterpret_cast<char*>(t.woff) + ((sizeof(int64_t) * ((size_t)n_waves + 1) + 15) & ~(size_t)15);
   return t;
+}
+
+hipError_t launch_rs_bucket_fused(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
+                                  const float4* qhdr, const float* row_norms, int metric, int cap, int* qcnt,
+                                  float* cand_key, int* cand_pos, hipStream_t s) {
+  if (n_waves <= 0 || nq <= 0) return hipSuccess;
+  if (cap < 1 || (int64_t)cap * nq > INT64_C(1) << 40) return hipErrorInvalidValue;
+  int J = 1;
+  const int nb = rs_bucket_groups(n_waves, nq, &J);
+  if (nb == 0) return hipErrorInvalidValue;
+  const size_t lds = sizeof(int) * (size_t)nq;
+  if (metric == kIP) {
+    static const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rs_bucket_fused<kIP>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)(sizeof(int) * kRsLdsMaxQ));
+    if (a1 != hipSuccess) return a1;
+    hipLaunchKernelGGL(k_rs_bucket_fused<kIP>, dim3((unsigned)nb), dim3(1024), lds, s, wave_buf, wave_cap, wave_cnt, J,
+                       nq, qhdr, row_norms, cap, qcnt, cand_key, cand_pos);
+  } else {
+    static const hipError_t a2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rs_bucket_fused<kL2>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)(sizeof(int) * kRsLdsMaxQ));
+    if (a2 != hipSuccess) return a2;
+    hipLaunchKernelGGL(k_rs_bucket_fused<kL2>, dim3((unsigned)nb), dim3(1024), lds, s, wave_buf, wave_cap, wave_cnt, J,
+                       nq, qhdr, row_norms, cap, qcnt, cand_key, cand_pos);
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_rs_bucket_count(const int4* wave_buf, int wave_cap, const int* wave_cnt, int n_waves, int nq,
@@ -1093,14 +1163,15 @@ hipError_t launch_rs_pre_lists(const int64_t* goff, int n_lists, int div, int mi
 
 hipError_t launch_rs_headers(const float* pre_kth, int64_t nq, const float* qscale, const float* qnorms,
                              const float* qres, float x_norm_max, float x_res_max, int dp, int metric, float4* hdr,
-                             float* tq, hipStream_t s) {
+                             float* tq, hipStream_t s, int* zero, int64_t nzero, int* zero2, int nzero2) {
+  if (nzero > nq + 1 || nzero2 > 256) return hipErrorInvalidValue;  // (the grid has >= max(nq + 1, 256) threads)
   const dim3 grid((unsigned)ceil_div(nq + 1, 256));
   if (metric == kIP)
     hipLaunchKernelGGL(k_rs_headers<kIP>, grid, dim3(256), 0, s, pre_kth, nq, qscale, qnorms, qres, x_norm_max,
-                       x_res_max, dp, hdr, tq);
+                       x_res_max, dp, hdr, tq, zero, nzero, zero2, nzero2);
   else
     hipLaunchKernelGGL(k_rs_headers<kL2>, grid, dim3(256), 0, s, pre_kth, nq, qscale, qnorms, qres, x_norm_max,
-                       x_res_max, dp, hdr, tq);
+                       x_res_max, dp, hdr, tq, zero, nzero, zero2, nzero2);
   return hipGetLastError();
 }
 

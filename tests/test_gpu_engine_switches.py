@@ -69,6 +69,8 @@ SEARCH_SWITCHES = [
     {"MIVS_RS_WAVE_CAP": "2"},                                        # K13 streams overflow: the fallback
     {"MIVS_PF_ROWSTAT": "0", "MIVS_PF_FLAGS": "32"},                  # K10 phase clocks (stderr only)
     {"MIVS_PF_SLOT_OUT": "0"},                                        # pre-pass merges whole slots
+    {"MIVS_RS_BUCKET_1P": "0"},                                       # K13 bucketing: two-pass CSR runs
+    {"MIVS_RS_QCAP": "4"},                                            # one-pass runs overflow: the fallback
 ]
 
 
@@ -98,6 +100,21 @@ def test_ivf_prepass_slot_out_same_candidates(ivf, flat_data, monkeypatch):
     np.testing.assert_array_equal(_bits(d1), _bits(d0))
     assert st0["scan_kernel"] == st1["scan_kernel"] == 13
     assert st0["candidates"] == st1["candidates"]
+
+
+def test_ivf_one_pass_bucketing_same_candidates(ivf, flat_data, monkeypatch):
+    """K13's one-pass bucketing (fixed-capacity runs per query) and the two-pass CSR form hold the same candidates"""
+    idx, _ = ivf
+    _, q = flat_data
+    d0, i0 = _search(idx, q)
+    st0 = idx.last_search_stats()
+    monkeypatch.setenv("MIVS_RS_BUCKET_1P", "0")
+    d1, i1 = _search(idx, q)
+    st1 = idx.last_search_stats()
+    np.testing.assert_array_equal(i1, i0)
+    np.testing.assert_array_equal(_bits(d1), _bits(d0))
+    assert st0["candidates"] == st1["candidates"] > 0
+    assert st0["overflow_queries"] == st1["overflow_queries"]  # (this small shape has unproven windows either way)
 
 
 def test_ivf_default_matches_oracle(ivf, flat_data):
