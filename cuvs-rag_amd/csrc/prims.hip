@@ -225,6 +225,95 @@ __global__ __launch_bounds__(1024) void k_probe_fill_lds(const int64_t* __restri
   }
 }
 
+// The whole probe map in ONE workgroup for a small batch (n entries <= kPmSmallMax, n_lists <= kPmSmallLists: K13's
+// pre-pass map, one probe per query): LDS count, prefix, fill, and with slot_begin the scan of the per-(query, probe)
+// slot counts, the entries' slots and the queries' first slots -- the six launches of the general path (memset,
+// count, prefix, fill, scan, slots) cost ~5 us each however small the batch.
+constexpr int kPmSmallPer = 32;  // entries per thread: a thread keeps its contiguous run of entries in registers
+constexpr int64_t kPmSmallMax = 1024 * kPmSmallPer;
+constexpr int kPmSmallLists = 8192;
+__global__ __launch_bounds__(1024) void k_probe_map_small(const int64_t* __restrict__ probes, int64_t nq, int np,
+                                                          int n_lists, const int64_t* __restrict__ list_goff, int G,
+                                                          int qtile, int* __restrict__ counts,
+                                                          int* __restrict__ bucket_off, int* __restrict__ work_off,
+                                                          int64_t* __restrict__ bucket_q, int64_t* __restrict__ bucket_slot,
+                                                          int64_t* __restrict__ qp_slots, int64_t* __restrict__ slot_begin) {
+  __shared__ int bins[kPmSmallLists];
+  __shared__ int chunks[kPmSmallLists];
+  __shared__ int64_t sh[16];
+  const int64_t n = nq * np;
+  const int per = (int)((n + 1023) / 1024);
+  const int64_t i0 = (int64_t)threadIdx.x * per;
+  for (int l = threadIdx.x; l < n_lists; l += 1024) bins[l] = 0;
+  int li[kPmSmallPer];
+#pragma unroll
+  for (int j = 0; j < kPmSmallPer; ++j) li[j] = j < per && i0 + j < n ? (int)probes[i0 + j] : -1;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kPmSmallPer; ++j)
+    if (li[j] >= 0) atomicAdd(bins + li[j], 1);
+  __syncthreads();
+  // bucket and work offsets (k_probe_prefix); bins become each list's next free bucket entry
+  int64_t cb = 0, cw = 0;
+  for (int l0 = 0; l0 < n_lists; l0 += 1024) {
+    const int l = l0 + threadIdx.x;
+    int64_t c = 0, wk = 0;
+    if (l < n_lists) {
+      c = bins[l];
+      const int ch = (int)ceil_div(list_goff[l + 1] - list_goff[l], G);
+      chunks[l] = ch;
+      wk = ceil_div(c, qtile) * ch;
+      counts[l] = (int)c;
+    }
+    int64_t tb, tw;
+    const int64_t eb = block_excl_scan(c, sh, &tb);
+    const int64_t ew = block_excl_scan(wk, sh, &tw);
+    if (l < n_lists) {
+      bucket_off[l] = (int)(cb + eb);
+      work_off[l] = (int)(cw + ew);
+      bins[l] = (int)(cb + eb);
+    }
+    cb += tb;
+    cw += tw;
+  }
+  if (threadIdx.x == 0) { bucket_off[n_lists] = (int)cb; work_off[n_lists] = (int)cw; }
+  __syncthreads();
+  // fill (k_probe_fill) from the registers: the entry's bucket position and its (query, probe)'s slot count
+  int ei[kPmSmallPer];
+  int64_t tsum = 0;
+#pragma unroll
+  for (int j = 0; j < kPmSmallPer; ++j) {
+    ei[j] = -1;
+    if (li[j] >= 0) {
+      ei[j] = atomicAdd(bins + li[j], 1);
+      bucket_q[ei[j]] = (i0 + j) / np;
+      tsum += chunks[li[j]];
+    }
+    if (j < per && i0 + j < n) qp_slots[i0 + j] = li[j] >= 0 ? chunks[li[j]] : 0;
+  }
+  if (slot_begin == nullptr) {
+#pragma unroll
+    for (int j = 0; j < kPmSmallPer; ++j)
+      if (ei[j] >= 0) bucket_slot[ei[j]] = i0 + j;
+    return;
+  }
+  // the slots: an exclusive scan of the slot counts in entry order (a thread's entries are contiguous)
+  int64_t tot;
+  int64_t run = block_excl_scan(tsum, sh, &tot);
+#pragma unroll
+  for (int j = 0; j < kPmSmallPer; ++j) {
+    const int64_t i = i0 + j;
+    if (j < per && i < n) {
+      if (i % np == 0) slot_begin[i / np] = run;
+      if (ei[j] >= 0) {
+        bucket_slot[ei[j]] = run;
+        run += chunks[li[j]];
+      }
+    }
+  }
+  if (threadIdx.x == 0) slot_begin[nq] = tot;
+}
+
 // the output slot of every bucket entry (its (query, probe)'s first slot) and each query's first slot, one launch
 // (thread t: bucket entry t and query t)
 __global__ void k_bucket_slot_begin(int64_t* __restrict__ bucket_slot, int64_t n, const int64_t* __restrict__ qp_base,
@@ -370,6 +459,12 @@ hipError_t launch_probe_map(const int64_t* probes, int64_t nq, int np, int n_lis
   if (scan_tmp_bytes_ < scan_tmp_bytes(n) + sizeof(int64_t) * (size_t)n) return hipErrorInvalidValue;
   int64_t* qp_base = static_cast<int64_t*>(scan_tmp);
   void* stmp = qp_base + n;
+  if (n > 0 && n <= kPmSmallMax && n_lists <= kPmSmallLists) {
+    hipLaunchKernelGGL(k_probe_map_small, dim3(1), dim3(1024), 0, s, probes, nq, np, n_lists, list_goff, chunk_groups,
+                       qtile, counts, bucket_off, work_off, bucket_q, bucket_slot, qp_slots, slot_begin);
+    (void)fill;
+    return hipGetLastError();
+  }
   hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * n_lists, s);
   if (e != hipSuccess) return e;
   // LDS-histogram form once the entries outnumber the lists (a chunk then repeats lists)

@@ -501,31 +501,12 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   block_prof();
 }
 
-// Work items of K13 from the probe map (chunk = kRsBlockGroups groups, one tile column per list):
-// item w -> {first group, end group, first tile slot of its list, tiles of its list}
-__global__ void k_rs_items(const int* __restrict__ work_off, const int* __restrict__ bucket_off,
-                           const int64_t* __restrict__ list_goff, int n_lists, int max_items, int4* __restrict__ items,
-                           int* __restrict__ zero, int nzero) {
-  const int w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w < nzero) zero[w] = 0;  // K13's counters (a memset launch less)
-  if (w >= max_items || w >= work_off[n_lists]) return;
-  int lo = 0, hi = n_lists - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (work_off[mid] <= w) lo = mid; else hi = mid - 1;
-  }
-  const int64_t g0 = list_goff[lo] + (int64_t)(w - work_off[lo]) * kRsBlockGroups;
-  const int64_t ge = list_goff[lo + 1] < g0 + kRsBlockGroups ? list_goff[lo + 1] : g0 + kRsBlockGroups;
-  const int m = bucket_off[lo + 1] - bucket_off[lo];
-  items[w] = make_int4((int)g0, (int)ge, (int)rs_tile_slot(bucket_off, lo, 0), (m + kRsQTile - 1) / kRsQTile);
-}
-
 // The 8 item queues of K13 as ranges of equal TILE work (bounds [9]): an item costs its list's tile count,
 // and lists differ in queries, so equal item counts left one queue ~3 % heavier than the mean. Item
 // weights are uniform inside a list: queue x starts at the first item whose work prefix reaches
 // W x / 8 (W = all items' tiles).
-__global__ __launch_bounds__(1024) void k_rs_bounds(const int* __restrict__ work_off, const int* __restrict__ bucket_off,
-                                                    int n_lists, int* __restrict__ bounds) {
+__device__ void rs_bounds_block(const int* __restrict__ work_off, const int* __restrict__ bucket_off, int n_lists,
+                                int* __restrict__ bounds) {
   __shared__ int64_t sh[16];
   __shared__ int64_t s_total;
   // pass 1: W
@@ -570,6 +551,31 @@ __global__ __launch_bounds__(1024) void k_rs_bounds(const int* __restrict__ work
     }
     cum += t;
   }
+}
+
+// Work items of K13 from the probe map (chunk = kRsBlockGroups groups, one tile column per list):
+// item w -> {first group, end group, first tile slot of its list, tiles of its list}
+// (one launch: blocks of 1024 items, and with bounds the last block computes the queue bounds)
+__global__ __launch_bounds__(1024) void k_rs_items(const int* __restrict__ work_off, const int* __restrict__ bucket_off,
+                                                   const int64_t* __restrict__ list_goff, int n_lists, int max_items,
+                                                   int4* __restrict__ items, int* __restrict__ zero, int nzero,
+                                                   int* __restrict__ bounds) {
+  if (bounds && blockIdx.x == gridDim.x - 1) {
+    rs_bounds_block(work_off, bucket_off, n_lists, bounds);
+    return;
+  }
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w < nzero) zero[w] = 0;  // K13's counters (a memset launch less)
+  if (w >= max_items || w >= work_off[n_lists]) return;
+  int lo = 0, hi = n_lists - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (work_off[mid] <= w) lo = mid; else hi = mid - 1;
+  }
+  const int64_t g0 = list_goff[lo] + (int64_t)(w - work_off[lo]) * kRsBlockGroups;
+  const int64_t ge = list_goff[lo + 1] < g0 + kRsBlockGroups ? list_goff[lo + 1] : g0 + kRsBlockGroups;
+  const int m = bucket_off[lo + 1] - bucket_off[lo];
+  items[w] = make_int4((int)g0, (int)ge, (int)rs_tile_slot(bucket_off, lo, 0), (m + kRsQTile - 1) / kRsQTile);
 }
 
 // per query: {qs, uf, qn, q} for K13 (uf carries T_q: the one-fma filter bound for the exact k-th key over the
@@ -750,9 +756,9 @@ hipError_t launch_rs_items(const int* work_off, const int* bucket_off, const int
                            int max_items, int4* items, int* bounds, hipStream_t s, int* zero, int nzero) {
   if (nzero > 256) return hipErrorInvalidValue;
   if (max_items <= 0 && nzero <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_rs_items, dim3((unsigned)ceil_div(max_items > 0 ? max_items : 1, 256)), dim3(256), 0, s,
-                     work_off, bucket_off, list_goff, n_lists, max_items, items, zero, nzero);
-  if (bounds) hipLaunchKernelGGL(k_rs_bounds, dim3(1), dim3(1024), 0, s, work_off, bucket_off, n_lists, bounds);
+  const unsigned nb = (unsigned)ceil_div(max_items > 0 ? max_items : 1, 1024) + (bounds ? 1 : 0);
+  hipLaunchKernelGGL(k_rs_items, dim3(nb), dim3(1024), 0, s, work_off, bucket_off, list_goff, n_lists, max_items, items,
+                     zero, nzero, bounds);
   return hipGetLastError();
 }
 
