@@ -201,7 +201,8 @@ int pick_qtile(int k, int d, int G) {
 void run_scan(const ScanJob& j, int device, Workspace& ws, hipStream_t s) {
   // 0 = DUMP mode (k > kMaxK, or asked for): raw keys per slot + (first row, rows) slot info for K8
   const int kcap = j.dump ? 0 : scan_kcap(j.k);
-  require(!(j.dump && j.qtile == 64), "internal: DUMP runs the 32-query K3", MIVS_ERR_UNSUPPORTED);
+  require(!(j.dump && j.qtile == 64 && !scan_wide_supported(0, j.d, j.dp, j.G)), "internal: DUMP on K3w not applicable",
+          MIVS_ERR_UNSUPPORTED);
   require(j.k >= 1 && j.k <= kMaxSelectK, "k must be in [1, " + std::to_string(kMaxSelectK) + "]",
           MIVS_ERR_UNSUPPORTED);
   require(j.dp <= 1024, "dim > 1024 is not supported by this build", MIVS_ERR_UNSUPPORTED);
@@ -229,7 +230,7 @@ void run_scan(const ScanJob& j, int device, Workspace& ws, hipStream_t s) {
   a.metric = j.metric;
   a.qtile = j.qtile;
   if (j.qtile == 64) {
-    require(kcap > 0 && scan_wide_supported(kcap, j.d, j.dp, j.G), "internal: wide scan not applicable");
+    require(kcap >= 0 && scan_wide_supported(kcap, j.d, j.dp, j.G), "internal: wide scan not applicable");
     const size_t lds = scan_wide_lds_bytes(kcap, j.G);
     const int grid = cu_count(device) * std::min(2, scan_wide_occupancy(kcap, j.metric, lds));
     HIPCHK(launch_scan_wide(a, kcap, grid, lds, s));
@@ -268,6 +269,9 @@ void single_list_topk(const ListSet& ls, int G, const float* queries, const floa
   const int64_t chunks = std::max<int64_t>(1, ceil_div(ls.n_groups, G));
   require(ceil_div(nq, kQTile) * chunks < (int64_t)INT32_MAX, "too many work items", MIVS_ERR_UNSUPPORTED);
   if (k > kMaxK || dump) {  // DUMP scan + K8 select, in query batches
+    // K3w's 64-query tiles where they apply (two accumulator chains per wave; MIVS_DUMP_WIDE=0: K3's 32)
+    const char* dwe = getenv("MIVS_DUMP_WIDE");
+    const int dq = !(dwe && dwe[0] == '0') && scan_wide_supported(0, d, dp, G) ? 64 : kQTile;
     const int64_t slot_rows = (int64_t)G * kGroupRows;
     const int64_t qb = select_batch(nq, (size_t)(chunks * (slot_rows * 4 + 16)));
     for (int64_t b0 = 0; b0 < nq; b0 += qb) {
@@ -279,15 +283,14 @@ void single_list_topk(const ListSet& ls, int G, const float* queries, const floa
       ws.part_d.reserve(sizeof(float) * (size_t)(nb * chunks * slot_rows));
       ws.part_i.reserve(sizeof(int64_t) * (size_t)(nb * chunks * 2));
       ws.counter.reserve(16);
-      HIPCHK(launch_single_list_job(nb, chunks, kQTile, ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(),
+      HIPCHK(launch_single_list_job(nb, chunks, dq, ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(),
                                     ws.bucket_off.as<int>(), ws.work_off.as<int>(), nullptr, s, ws.counter.as<int>()));
       const float* qb_ptr = queries;
       const float* qn_ptr = qnorms;
       if (rows) HIPCHK(hipMemcpyAsync(ws.bucket_q.p, rows + b0, sizeof(int64_t) * nb, hipMemcpyDeviceToDevice, s));
       else { qb_ptr = queries + b0 * (int64_t)d; qn_ptr = qnorms + b0; }
       ScanJob j{&ls, G, qb_ptr, qn_ptr, d, dp, k, metric, ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(),
-                ws.bucket_off.as<int>(), ws.work_off.as<int>(), ws.part_d.as<float>(), ws.part_i.as<int64_t>(),
-                kQTile};
+                ws.bucket_off.as<int>(), ws.work_off.as<int>(), ws.part_d.as<float>(), ws.part_i.as<int64_t>(), dq};
       j.dump = true;
       j.counter_zeroed = true;
       run_scan(j, device, ws, s);
@@ -1034,10 +1037,19 @@ bool coarse_dump(int np) {
 
 // Centroid chunk of the coarse probe: enough (query tile, chunk) work items for >= 4 per CU -- a 10k-query
 // batch over 1024 centroids is only 313 query tiles -- with K7 merging the chunks' top-n_probes
-int coarse_groups(const mivs_index_s* idx, int64_t nq) {
+// K3w's DUMP (n_probes > 16, 64-query tiles, two workgroups of 4 waves per CU): >= 8 items per CU in chunks of a
+// multiple of 4 groups (a pass is one group per wave): 194 us against 212 us at 8 groups (configs[2], 1024 lists)
+int coarse_groups(const mivs_index_s* idx, int64_t nq, int np) {
   const int64_t ng = std::max<int64_t>(1, idx->cents.n_groups);
   const char* ge = getenv("MIVS_COARSE_G");  // (A/B runs: groups per coarse work item)
   if (ge && atoi(ge) > 0) return (int)std::max<int64_t>(1, std::min<int64_t>(idx->G, atoi(ge)));
+  const char* dwe = getenv("MIVS_DUMP_WIDE");
+  if (coarse_dump(np) && !(dwe && dwe[0] == '0') && scan_wide_supported(0, idx->d, idx->dp, 4)) {
+    const int64_t tiles = std::max<int64_t>(1, ceil_div(nq, 64));
+    const int64_t chunks = std::min<int64_t>(ng, std::max<int64_t>(1, ceil_div(8LL * cu_count(idx->device), tiles)));
+    const int64_t g4 = ceil_div(ceil_div(ng, chunks), 4) * 4;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(idx->G, g4));
+  }
   const int64_t tiles = std::max<int64_t>(1, ceil_div(nq, kQTile));
   const int64_t chunks = std::min<int64_t>(ng, std::max<int64_t>(1, ceil_div(4LL * cu_count(idx->device), tiles)));
   return (int)std::max<int64_t>(1, std::min<int64_t>(idx->G, ceil_div(ng, chunks)));
@@ -1073,7 +1085,7 @@ void ivf_search_batch(mivs_index_s* idx, hipStream_t s, const float* q, int64_t 
   // coarse: top-n_probes centroids per query
   ws.probes_d.reserve(sizeof(float) * nq * np);
   ws.probes_i.reserve(sizeof(int64_t) * nq * np);
-  single_list_topk(idx->cents, coarse_groups(idx, nq), q, ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, np,
+  single_list_topk(idx->cents, coarse_groups(idx, nq, np), q, ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, np,
                    idx->metric, ws.probes_d.as<float>(), ws.probes_i.as<int64_t>(), idx->device, ws, s,
                    coarse_dump(np));
   if (out_probes) HIPCHK(launch_i64_to_i32(ws.probes_i.as<int64_t>(), nq * np, out_probes, s));
@@ -2230,7 +2242,7 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
     HIPCHK(launch_row_norms(d_q, nq, idx->d, ws.qn.as<float>(), s));
     ws.probes_d.reserve(sizeof(float) * nq * np);
     ws.probes_i.reserve(sizeof(int64_t) * nq * np);
-    single_list_topk(idx->cents, coarse_groups(idx, nq), d_q, ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, np,
+    single_list_topk(idx->cents, coarse_groups(idx, nq, np), d_q, ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, np,
                      idx->metric, ws.probes_d.as<float>(), ws.probes_i.as<int64_t>(), idx->device, ws, s,
                      coarse_dump(np));
     if (d_probes) HIPCHK(launch_i64_to_i32(ws.probes_i.as<int64_t>(), nq * np, d_probes, s));

@@ -91,6 +91,30 @@ __device__ __forceinline__ void mma8_refill(f32x16& c0, f32x16& c1, float4 (&v)[
   }
 }
 
+// DUMP mode (KCAP == 0): the group's keys of one query tile straight to the query's slot (K3's epilogue_dump; rows
+// 8 r4 + 4 h + 0..3 of this lane are contiguous: 4 dwordx4 stores)
+template <int METRIC>
+__device__ __forceinline__ void wepilogue_dump(const f32x16& acc, const float* __restrict__ gnorm, int h, float qn,
+                                               float* __restrict__ dst) {
+  if (dst == nullptr) return;
+#pragma unroll
+  for (int r4 = 0; r4 < 4; ++r4) {
+    const float4 xn = *reinterpret_cast<const float4*>(gnorm + 8 * r4 + 4 * h);
+    const float xs[4] = {xn.x, xn.y, xn.z, xn.w};
+    float kv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (METRIC == kL2) {
+        const float v = fmaf(-2.0f, acc[4 * r4 + i], xs[i] + qn);
+        kv[i] = v > 0.0f ? v : 0.0f;
+      } else {
+        kv[i] = xs[i] < INFINITY ? -acc[4 * r4 + i] : INFINITY;
+      }
+    }
+    *reinterpret_cast<float4*>(dst + 8 * r4 + 4 * h) = make_float4(kv[0], kv[1], kv[2], kv[3]);
+  }
+}
+
 __device__ __forceinline__ void load8(float4 (&v)[8], const float* __restrict__ p) {
 #pragma unroll
   for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(p + row_blk8(u));
@@ -100,6 +124,8 @@ __device__ __forceinline__ void load8(float4 (&v)[8], const float* __restrict__ 
 // SIMD; 8: one workgroup per CU). A pass covers W row groups, one per wave.
 template <int KCAP, int METRIC, int W>
 __global__ __launch_bounds__(W * 64, 1) void k_scan_wide(ScanArgs a) {
+  constexpr bool DUMP = KCAP == 0;     // every key to the query's slot (the coarse probe: K8 selects)
+  constexpr int KR = DUMP ? 1 : KCAP;  // register list length
   constexpr int NT = W * 64;
   constexpr int NS = 2 * W;          // lane lists per query (W waves x 2 halves)
   constexpr int SPT = 2048 / NT;     // staged float4s per thread per slab (64 queries x 128 dims)
@@ -112,7 +138,7 @@ __global__ __launch_bounds__(W * 64, 1) void k_scan_wide(ScanArgs a) {
   float* s_norm = reinterpret_cast<float*>(smem + kWSmall);  // [G*32]
   float* qs = s_norm + a.chunk_groups * kGroupRows;       // [2][64][kSld]; merge area after the scan
   float* mkey = qs;
-  int* mpos = reinterpret_cast<int*>(mkey + 32 * NS * KCAP);
+  int* mpos = reinterpret_cast<int*>(mkey + 32 * NS * KR);
 
   const int dp = a.dp;
   const int tid = threadIdx.x;
@@ -164,15 +190,23 @@ __global__ __launch_bounds__(W * 64, 1) void k_scan_wide(ScanArgs a) {
     {
       const int nn = (int)(g_end - g_begin) * kGroupRows;
       for (int i = tid; i < nn; i += NT) s_norm[i] = a.row_norms[g_begin * kGroupRows + i];
+      if (DUMP && tid < nqt) {  // slot header: first row position + rows of this chunk
+        const int64_t slot = a.bucket_slot[e0 + tid] + chunk;
+        a.out_i[2 * slot] = g_begin * kGroupRows;
+        a.out_i[2 * slot + 1] = nn;
+      }
     }
     __syncthreads();
 
-    float lk0[KCAP], lk1[KCAP];
-    int lp0[KCAP], lp1[KCAP];
+    float lk0[KR], lk1[KR];
+    int lp0[KR], lp1[KR];
 #pragma unroll
-    for (int t = 0; t < KCAP; ++t) { lk0[t] = INFINITY; lp0[t] = INT_MAX; lk1[t] = INFINITY; lp1[t] = INT_MAX; }
+    for (int t = 0; t < KR; ++t) { lk0[t] = INFINITY; lp0[t] = INT_MAX; lk1[t] = INFINITY; lp1[t] = INT_MAX; }
     const float qn0 = s_qn[j], qn1 = s_qn[32 + j];
     const bool qv0 = s_q[j] >= 0, qv1 = s_q[32 + j] >= 0;
+    const int slot_rows = a.chunk_groups * kGroupRows;
+    float* const dump0 = DUMP && qv0 ? a.out_d + s_slot[j] * (int64_t)slot_rows : nullptr;
+    float* const dump1 = DUMP && qv1 ? a.out_d + s_slot[32 + j] * (int64_t)slot_rows : nullptr;
 
     // query-slab staging: staged float4 i of this thread = query row sr + RS i (int32 row id kept,
     // -1: empty lane), dims slab * 128 + sc .. + 3. An invalid float4 reads query row 0 (always
@@ -258,8 +292,14 @@ __global__ __launch_bounds__(W * 64, 1) void k_scan_wide(ScanArgs a) {
         const int64_t g = g_begin + p * W + wave;
         if (g < g_end) {
           const float* gn = s_norm + (g - g_begin) * kGroupRows;
-          wepilogue<KCAP, METRIC>(c0, gn, g * kGroupRows, h, qn0, qv0, lk0, lp0);
-          wepilogue<KCAP, METRIC>(c1, gn, g * kGroupRows, h, qn1, qv1, lk1, lp1);
+          if constexpr (DUMP) {
+            const int64_t ro = (g - g_begin) * kGroupRows;
+            wepilogue_dump<METRIC>(c0, gn, h, qn0, dump0 ? dump0 + ro : nullptr);
+            wepilogue_dump<METRIC>(c1, gn, h, qn1, dump1 ? dump1 + ro : nullptr);
+          } else {
+            wepilogue<KCAP, METRIC>(c0, gn, g * kGroupRows, h, qn0, qv0, lk0, lp0);
+            wepilogue<KCAP, METRIC>(c1, gn, g * kGroupRows, h, qn1, qv1, lk1, lp1);
+          }
         }
         c0 = zero;
         c1 = zero;
@@ -270,6 +310,10 @@ __global__ __launch_bounds__(W * 64, 1) void k_scan_wide(ScanArgs a) {
       }
     }
 
+    if constexpr (DUMP) {
+      __syncthreads();  // LDS (s_*, slabs) reused by the next work item
+      continue;
+    } else {
     // ---- merge: two rounds of 32 queries, NS lane lists (W waves x 2 halves) per query ----
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -313,6 +357,7 @@ __global__ __launch_bounds__(W * 64, 1) void k_scan_wide(ScanArgs a) {
       }
     }
     __syncthreads();
+    }
   }
 }
 
@@ -347,7 +392,8 @@ size_t scan_wide_lds_bytes(int kcap, int chunk_groups) {
 }
 
 bool scan_wide_supported(int kcap, int d, int dp, int chunk_groups) {
-  return (kcap == 1 || kcap == 4 || kcap == 8 || kcap == 12 || kcap == 16) && d % 4 == 0 && dp % kSlab == 0 &&
+  return (kcap == 0 || kcap == 1 || kcap == 4 || kcap == 8 || kcap == 12 || kcap == 16) && d % 4 == 0 &&
+         dp % kSlab == 0 &&
          scan_wide_lds_bytes(kcap, chunk_groups) <= 160 * 1024;
 }
 
@@ -370,6 +416,7 @@ static int wocc_k(int metric, size_t lds) {
 
 int scan_wide_occupancy(int kcap, int metric, size_t lds) {
   switch (kcap) {
+    case 0: return wocc_k<0>(metric, lds);
     case 1: return wocc_k<1>(metric, lds);
     case 4: return wocc_k<4>(metric, lds);
     case 8: return wocc_k<8>(metric, lds);
@@ -381,6 +428,7 @@ int scan_wide_occupancy(int kcap, int metric, size_t lds) {
 
 hipError_t launch_scan_wide(const ScanArgs& a, int kcap, int grid, size_t lds, hipStream_t s) {
   switch (kcap) {
+    case 0: return launch_w<0>(a, grid, lds, s);
     case 1: return launch_w<1>(a, grid, lds, s);
     case 4: return launch_w<4>(a, grid, lds, s);
     case 8: return launch_w<8>(a, grid, lds, s);
