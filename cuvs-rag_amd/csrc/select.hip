@@ -343,7 +343,7 @@ constexpr int kSmallWaves = 4;
 // V2 (default; MIVS_SELECT_SMALL_V2=0 keeps the bit search only): T0 = the need-th smallest of the 64 lanes' minima bounds the need-th
 // smallest key from above (need <= 64 lanes, each minimum a distinct key at or below it); when at most 64 keys lie
 // at or below T0 they are the candidates -- one per lane, bitonic-sorted by (key, id) -- without the bit search
-template <int METRIC, bool V2>
+template <int METRIC, bool V2, bool FAST>
 __global__ __launch_bounds__(64 * kSmallWaves) void k_select_small(SelectArgs a) {
   __shared__ uint32_t s_u[kSmallWaves][64];
   __shared__ int64_t s_i[kSmallWaves][64];
@@ -355,6 +355,34 @@ __global__ __launch_bounds__(64 * kSmallWaves) void k_select_small(SelectArgs a)
   const int n_total = (int)(a.slots_per_q * a.slot_rows);
   uint32_t u[kSmallPer];
   int nv = 0;
+  // Slots of whole 64-row multiples (the coarse probe's DUMP: 128): key i of every lane lies in slot i / (slot_rows /
+  // 64), uniform over the wave, so the slot headers are read once (lane s holds slot s's) and each key is one load at
+  // a scalar base -- cand_key's per-key header load and 64-bit address kept ~118 VGPRs live (4 waves per SIMD)
+  constexpr bool fast = FAST;  // (launched where slot_rows % 64 == 0 and slots_per_q <= 64)
+  const int spr = a.slot_rows >> 6;  // (fast) 64-key rows per slot
+  int nr_v = 0;
+  int64_t f_v = 0;
+  if (fast && lane < a.slots_per_q) {
+    nr_v = (int)a.slot_info[2 * (base + lane) + 1];
+    f_v = a.slot_info[2 * (base + lane)];
+  }
+  if constexpr (fast) {
+    int sq = 0, ri = 0;  // (uniform) slot of key i and its 64-row block in the slot
+#pragma unroll
+    for (int i = 0; i < kSmallPer; ++i) {
+      u[i] = 0xFFFFFFFFu;
+      if (64 * i < n_total) {
+        const int rr = 64 * ri + lane;
+        const int nr = __builtin_amdgcn_readlane(nr_v, sq);
+        if (rr < nr) {
+          const uint32_t o = ord_bits(a.keys[(base + sq) * a.slot_rows + rr]);
+          if (o < kOrdInf) u[i] = o;  // pad rows carry +inf
+        }
+      }
+      nv += __popcll(__ballot(u[i] != 0xFFFFFFFFu));
+      if (++ri == spr) { ri = 0; ++sq; }
+    }
+  } else {
 #pragma unroll
   for (int i = 0; i < kSmallPer; ++i) {
     const int t = lane + 64 * i;
@@ -368,6 +396,7 @@ __global__ __launch_bounds__(64 * kSmallWaves) void k_select_small(SelectArgs a)
       }
     }
     nv += __popcll(__ballot(ok));
+  }
   }
   const int need = nv < k ? nv : k;
   // the valid keys' range bounds the search (a few of the 32 bits once the keys share an exponent)
@@ -443,15 +472,21 @@ __global__ __launch_bounds__(64 * kSmallWaves) void k_select_small(SelectArgs a)
   }
   // the chosen pairs, one per lane
   int nsel = 0;
+  int sq = 0, ri = 0;  // (fast) as in the key loads
 #pragma unroll
   for (int i = 0; i < kSmallPer; ++i) {
     const int t = lane + 64 * i;
     bool take = need > 0 && u[i] <= T && u[i] != 0xFFFFFFFFu;
     int64_t id = 0;
-    if (take) {
+    if constexpr (fast) {
+      const uint64_t f = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)((uint64_t)f_v >> 32), sq) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)f_v, sq);
+      if (take) id = a.row_ids[(int64_t)f + 64 * ri + lane];
+      if (++ri == spr) { ri = 0; ++sq; }
+    } else if (take) {
       id = cand_id<false>(a, base, t);
-      if (u[i] == T && id > I) take = false;
     }
+    if (take && u[i] == T && id > I) take = false;
     const uint64_t bm = __ballot(take);
     if (take) {
       const int at = nsel + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
@@ -517,12 +552,18 @@ hipError_t launch_select(const SelectArgs& a, hipStream_t s) {
     const dim3 grid((unsigned)ceil_div(a.nq, (int64_t)kSmallWaves)), block(64 * kSmallWaves);
     const char* v2e = getenv("MIVS_SELECT_SMALL_V2");
     const bool v2 = !(v2e && v2e[0] == '0');  // 122 -> 72 us for the coarse probe's 10k x 1024 keys
-    if (v2) {
-      if (a.metric == kIP) hipLaunchKernelGGL((k_select_small<kIP, true>), grid, block, 0, s, a);
-      else hipLaunchKernelGGL((k_select_small<kL2, true>), grid, block, 0, s, a);
+    // (MIVS_SELECT_SMALL_FAST=0: the per-key slot decode everywhere)
+    const char* fe = getenv("MIVS_SELECT_SMALL_FAST");
+    const bool fast = (a.slot_rows & 63) == 0 && a.slots_per_q <= 64 && !(fe && fe[0] == '0');
+    if (v2 && fast) {
+      if (a.metric == kIP) hipLaunchKernelGGL((k_select_small<kIP, true, true>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((k_select_small<kL2, true, true>), grid, block, 0, s, a);
+    } else if (v2) {
+      if (a.metric == kIP) hipLaunchKernelGGL((k_select_small<kIP, true, false>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((k_select_small<kL2, true, false>), grid, block, 0, s, a);
     } else {
-      if (a.metric == kIP) hipLaunchKernelGGL((k_select_small<kIP, false>), grid, block, 0, s, a);
-      else hipLaunchKernelGGL((k_select_small<kL2, false>), grid, block, 0, s, a);
+      if (a.metric == kIP) hipLaunchKernelGGL((k_select_small<kIP, false, false>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((k_select_small<kL2, false, false>), grid, block, 0, s, a);
     }
     return hipGetLastError();
   }

@@ -260,7 +260,8 @@ def test_ivf_pq_switch_same_bits(mivs_lib, monkeypatch, k, env):
                                            (32, {"MIVS_SELECT_SMALL_V2": "0"}),
                                            (48, {"MIVS_COARSE_DUMP": "0"}),
                                            (32, {"MIVS_DUMP_WIDE": "0"}),           # coarse DUMP on K3, not K3w
-                                           (48, {"MIVS_DUMP_WIDE": "0"})])
+                                           (48, {"MIVS_DUMP_WIDE": "0"}),
+                                           (32, {"MIVS_SELECT_SMALL_FAST": "0"})])
 def test_coarse_probe_switches_same_bits(ivf, flat_data, monkeypatch, n_probes, env):
     """the coarse probe through K3 DUMP + K8s (the default above 16 probes) and through K3's register top-k
     (MIVS_COARSE_DUMP=0), K8s with the bit search alone: the same probes (order and ids) and the same search
