@@ -964,8 +964,6 @@ void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_
   r.slot_begin = slot_begin;
   r.slot_cnt = slot_cnt;
   r.slot_cap = slot_cap;
-  const char* rpe = getenv("MIVS_PF_REFINE_PREFETCH");  // (opt-in until measured: 1 on)
-  r.prefetch_rows = !kth_out && rpe && rpe[0] == '1';
   r.slot_k = slot_k;
   r.nq = nq;
   r.k = k;

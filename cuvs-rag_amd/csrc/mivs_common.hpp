@@ -407,7 +407,6 @@ struct PfRefineArgs {
                               // smallest of THOSE
   const int* slot_cnt;        // optional (K13's one-pass bucketing): query q's run is [q * slot_cap, + min(cnt, cap))
   int slot_cap;               // instead of slot_begin; cnt > cap: candidates were dropped, the query is not proven
-  int prefetch_rows;          // K11: phase 2 pulls each window row's lines toward L2 (LDS-DMA into a scratch slot)
 };
 
 hipError_t launch_pf_scan(const PfScanArgs& a, int grid, size_t lds, hipStream_t s);

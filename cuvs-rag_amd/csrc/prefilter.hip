@@ -629,7 +629,6 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
 // K11. One wave per query (4 per workgroup; every wave reaches every barrier).
 template <int METRIC>
 __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
-  __shared__ float s_pf[4][64];  // (the row prefetch's DMA target)
   __shared__ float s_ck[4][kPfCap];
   __shared__ int s_cp[4][kPfCap];
   __shared__ __attribute__((aligned(16))) float s_qv[4][1024];
@@ -729,17 +728,6 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
       if (at < kPfCap) { s_ck[wv][at] = ck; s_cp[wv][at] = a.slot_pos[cc]; }
     }
     cnt += __popcll(msk);
-  }
-  if (a.prefetch_rows && live && lane < cnt && lane < kPfCap) {
-    // the window row's 128-B lines on their way now, one dword each by LDS-DMA into a scratch slot (never read): the
-    // barrier below waits for them with the query's staging loads, and phase 3's lane-per-row reads then find them
-    // on-die instead of waiting on HBM batch after batch (issued here, not in the loop above: the compiler waits for
-    // every LDS-DMA before the next LDS write)
-    typedef __attribute__((address_space(3))) void* lds_ptr_t;
-    const float* rowp = a.groups + row_elem(s_cp[wv][lane], 0, a.dp);
-    for (int b = 0; b < (a.dp >> 5); ++b)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(rowp + row_dim(32 * b)), (lds_ptr_t)(s_pf[wv]), 4,
-                                       0, 0);
   }
   ovf = ovf || cnt > kPfCap;
   if (live && ovf && lane == 0) {

@@ -180,12 +180,11 @@ __global__ void k_probe_fill(const int64_t* __restrict__ probes, int64_t n, int 
 constexpr int kPmChunk = 8192;
 constexpr int kPmMaxLists = 32768;  // 128 KiB of int bins
 
-__device__ __forceinline__ void pm_chunk_hist(const int64_t* __restrict__ probes, int64_t n, int n_lists, int* bins,
-                                              int chunk) {
+__device__ __forceinline__ void pm_chunk_hist(const int64_t* __restrict__ probes, int64_t n, int n_lists, int* bins) {
   for (int l = threadIdx.x; l < n_lists; l += blockDim.x) bins[l] = 0;
   __syncthreads();
-  const int64_t i0 = (int64_t)blockIdx.x * chunk;
-  const int64_t i1 = i0 + chunk < n ? i0 + chunk : n;
+  const int64_t i0 = (int64_t)blockIdx.x * kPmChunk;
+  const int64_t i1 = i0 + kPmChunk < n ? i0 + kPmChunk : n;
   for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     const int64_t l = probes[i];
     if (l >= 0) atomicAdd(bins + l, 1);
@@ -194,9 +193,9 @@ __device__ __forceinline__ void pm_chunk_hist(const int64_t* __restrict__ probes
 }
 
 __global__ __launch_bounds__(1024) void k_probe_count_lds(const int64_t* __restrict__ probes, int64_t n, int n_lists,
-                                                          int* __restrict__ counts, int chunk) {
+                                                          int* __restrict__ counts) {
   extern __shared__ int bins[];
-  pm_chunk_hist(probes, n, n_lists, bins, chunk);
+  pm_chunk_hist(probes, n, n_lists, bins);
   for (int l = threadIdx.x; l < n_lists; l += blockDim.x)
     if (bins[l]) atomicAdd(counts + l, bins[l]);
 }
@@ -206,16 +205,16 @@ __global__ __launch_bounds__(1024) void k_probe_fill_lds(const int64_t* __restri
                                                          int* __restrict__ fill, int64_t* __restrict__ bucket_q,
                                                          int64_t* __restrict__ bucket_qp,
                                                          const int64_t* __restrict__ list_goff, int G,
-                                                         int64_t* __restrict__ qp_slots, int chunk) {
+                                                         int64_t* __restrict__ qp_slots) {
   extern __shared__ int bins[];
-  pm_chunk_hist(probes, n, n_lists, bins, chunk);
+  pm_chunk_hist(probes, n, n_lists, bins);
   for (int l = threadIdx.x; l < n_lists; l += blockDim.x) {
     const int c = bins[l];
     if (c) bins[l] = bucket_off[l] + atomicAdd(fill + l, c);  // this chunk's range of list l's bucket
   }
   __syncthreads();
-  const int64_t i0 = (int64_t)blockIdx.x * chunk;
-  const int64_t i1 = i0 + chunk < n ? i0 + chunk : n;
+  const int64_t i0 = (int64_t)blockIdx.x * kPmChunk;
+  const int64_t i1 = i0 + kPmChunk < n ? i0 + kPmChunk : n;
   for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     const int l = (int)probes[i];
     if (l < 0) { qp_slots[i] = 0; continue; }
@@ -460,8 +459,7 @@ hipError_t launch_probe_map(const int64_t* probes, int64_t nq, int np, int n_lis
   if (scan_tmp_bytes_ < scan_tmp_bytes(n) + sizeof(int64_t) * (size_t)n) return hipErrorInvalidValue;
   int64_t* qp_base = static_cast<int64_t*>(scan_tmp);
   void* stmp = qp_base + n;
-  const char* pse = getenv("MIVS_PM_SMALL");  // (0: the general multi-launch path at every size, A/B tests)
-  if (n > 0 && n <= kPmSmallMax && n_lists <= kPmSmallLists && !(pse && pse[0] == '0')) {
+  if (n > 0 && n <= kPmSmallMax && n_lists <= kPmSmallLists) {
     hipLaunchKernelGGL(k_probe_map_small, dim3(1), dim3(1024), 0, s, probes, nq, np, n_lists, list_goff, chunk_groups,
                        qtile, counts, bucket_off, work_off, bucket_q, bucket_slot, qp_slots, slot_begin);
     (void)fill;
@@ -471,8 +469,6 @@ hipError_t launch_probe_map(const int64_t* probes, int64_t nq, int np, int n_lis
   if (e != hipSuccess) return e;
   // LDS-histogram form once the entries outnumber the lists (a chunk then repeats lists)
   const bool lds = n_lists <= kPmMaxLists && n >= 2 * (int64_t)n_lists;
-  const char* pce = getenv("MIVS_PM_CHUNK");  // entries per LDS-histogram workgroup (A/B runs)
-  const int pm_chunk = pce && atoi(pce) >= 1024 ? atoi(pce) : kPmChunk;
   const size_t lds_bytes = sizeof(int) * (size_t)n_lists;
   if (lds) {
     static const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_probe_count_lds),
@@ -483,16 +479,15 @@ hipError_t launch_probe_map(const int64_t* probes, int64_t nq, int np, int n_lis
                                                      (int)(sizeof(int) * kPmMaxLists));
     if (a1 != hipSuccess) return a1;
     if (a2 != hipSuccess) return a2;
-    hipLaunchKernelGGL(k_probe_count_lds, grid1(n, pm_chunk), dim3(1024), lds_bytes, s, probes, n, n_lists, counts,
-                       pm_chunk);
+    hipLaunchKernelGGL(k_probe_count_lds, grid1(n, kPmChunk), dim3(1024), lds_bytes, s, probes, n, n_lists, counts);
   } else {
     hipLaunchKernelGGL(k_probe_count, grid1(n, 256), dim3(256), 0, s, probes, n, counts);
   }
   hipLaunchKernelGGL(k_probe_prefix, dim3(1), dim3(1024), 0, s, counts, n_lists, list_goff, chunk_groups, qtile,
                      bucket_off, work_off, fill);
   if (lds)
-    hipLaunchKernelGGL(k_probe_fill_lds, grid1(n, pm_chunk), dim3(1024), lds_bytes, s, probes, n, np, n_lists,
-                       bucket_off, fill, bucket_q, bucket_slot, list_goff, chunk_groups, qp_slots, pm_chunk);
+    hipLaunchKernelGGL(k_probe_fill_lds, grid1(n, kPmChunk), dim3(1024), lds_bytes, s, probes, n, np, n_lists,
+                       bucket_off, fill, bucket_q, bucket_slot, list_goff, chunk_groups, qp_slots);
   else
     hipLaunchKernelGGL(k_probe_fill, grid1(n, 256), dim3(256), 0, s, probes, n, np, bucket_off, fill, bucket_q,
                        bucket_slot, list_goff, chunk_groups, qp_slots);

@@ -852,17 +852,13 @@ __device__ __forceinline__ void rs_rec_emit(const RsRec& r, unsigned m, const fl
 // its stream t, found in an LDS prefix of the kRsWaves * J stream lengths.
 constexpr int kRsLdsMaxQ = 32768;  // 128 KiB of int bins
 constexpr int kRsMaxGroupStreams = 64;
-// (J < 0: a K13 workgroup's streams split over -J groups -- group b holds streams (b % -J) * kRsWaves / -J .. of
-// workgroup b / -J: more, shorter groups; one-pass bucketing only)
 __device__ __forceinline__ int rs_group_stream(int b, int t, int J) {
-  if (J < 0) return (b / -J) * kRsWaves + (b % -J) * (kRsWaves / -J) + t;
   return ((b & 7) + 8 * (J * (b >> 3) + t / kRsWaves)) * kRsWaves + t % kRsWaves;
 }
-__device__ __forceinline__ int rs_group_streams(int J) { return J < 0 ? kRsWaves / -J : kRsWaves * J; }
 
-// the group's stream prefix in LDS (pre[0..S], S = rs_group_streams(J)); returns the group's record count
+// the group's stream prefix in LDS (pre[0..S], S = kRsWaves * J); returns the group's record count
 __device__ __forceinline__ int rs_group_prefix(const int* __restrict__ wave_cnt, int wave_cap, int J, int* pre) {
-  const int S = rs_group_streams(J);
+  const int S = kRsWaves * J;
   if (threadIdx.x < 64) {
     const int t = threadIdx.x;
     int n = t < S ? min(wave_cnt[rs_group_stream(blockIdx.x, t, J)], wave_cap) : 0;
@@ -881,7 +877,7 @@ __device__ __forceinline__ int rs_group_prefix(const int* __restrict__ wave_cnt,
 // record e of the group: its stream's base pointer
 __device__ __forceinline__ const int4* rs_group_rec(const int4* __restrict__ wave_buf, int wave_cap, int J,
                                                     const int* pre, int e) {
-  const int S = rs_group_streams(J);
+  const int S = kRsWaves * J;
   int t = 0;
   while (t + 1 < S && pre[t + 1] <= e) ++t;  // (S <= 64: a short scan of LDS-resident prefixes)
   const int w = rs_group_stream(blockIdx.x, t, J);
@@ -1055,14 +1051,8 @@ hipError_t launch_rs_bucket_fused(const int4* wave_buf, int wave_cap, const int*
   if (n_waves <= 0 || nq <= 0) return hipSuccess;
   if (cap < 1 || (int64_t)cap * nq > INT64_C(1) << 40) return hipErrorInvalidValue;
   int J = 1;
-  int nb = rs_bucket_groups(n_waves, nq, &J);
+  const int nb = rs_bucket_groups(n_waves, nq, &J);
   if (nb == 0) return hipErrorInvalidValue;
-  const char* se = getenv("MIVS_RS_BUCKET_SPLIT");  // K13 workgroup's streams per group split 2 or 4 ways (A/B)
-  const int split = se ? atoi(se) : 1;
-  if (J == 1 && (split == 2 || split == 4)) {
-    J = -split;
-    nb *= split;
-  }
   const size_t lds = sizeof(int) * (size_t)nq;
   if (metric == kIP) {
     static const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rs_bucket_fused<kIP>),

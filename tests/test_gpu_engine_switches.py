@@ -71,11 +71,6 @@ SEARCH_SWITCHES = [
     {"MIVS_PF_SLOT_OUT": "0"},                                        # pre-pass merges whole slots
     {"MIVS_RS_BUCKET_1P": "0"},                                       # K13 bucketing: two-pass CSR runs
     {"MIVS_RS_QCAP": "4"},                                            # one-pass runs overflow: the fallback
-    {"MIVS_PM_SMALL": "0"},                                           # probe maps: the general multi-launch path
-    {"MIVS_PM_SMALL": "0", "MIVS_PM_CHUNK": "1024"},                  # ... with small LDS-histogram chunks
-    {"MIVS_RS_BUCKET_SPLIT": "2"},                                    # one-pass bucketing over half-workgroup groups
-    {"MIVS_RS_BUCKET_SPLIT": "4"},
-    {"MIVS_PF_REFINE_PREFETCH": "1"},                                 # K11 with the window-row prefetch
 ]
 
 
