@@ -1041,8 +1041,6 @@ bool coarse_dump(int np) {
 // multiple of 4 groups (a pass is one group per wave): 194 us against 212 us at 8 groups (configs[2], 1024 lists)
 int coarse_groups(const mivs_index_s* idx, int64_t nq, int np) {
   const int64_t ng = std::max<int64_t>(1, idx->cents.n_groups);
-  const char* ge = getenv("MIVS_COARSE_G");  // (A/B runs: groups per coarse work item)
-  if (ge && atoi(ge) > 0) return (int)std::max<int64_t>(1, std::min<int64_t>(idx->G, atoi(ge)));
   const char* dwe = getenv("MIVS_DUMP_WIDE");
   if (coarse_dump(np) && !(dwe && dwe[0] == '0') && scan_wide_supported(0, idx->d, idx->dp, 4)) {
     const int64_t tiles = std::max<int64_t>(1, ceil_div(nq, 64));
