@@ -49,6 +49,11 @@ __device__ __forceinline__ void dma_b128(v4i desc, const void* lds, int voff, in
                :: "s"(m0), "v"(voff), "s"(desc), "s"(soff) : "memory");
 }
 
+template <bool B>
+struct BoolC {
+  static constexpr bool value = B;
+};
+
 template <int VAR, int PD, int WAVES>
 __global__ __launch_bounds__(WAVES * 64, 1) void probe(const h8* __restrict__ rows, const char* __restrict__ src,
                                                        int src_tiles, int ntiles, float* out,
@@ -74,7 +79,14 @@ __global__ __launch_bounds__(WAVES * 64, 1) void probe(const h8* __restrict__ ro
   if (VAR & 1) {
     if (lane == 0) __hip_atomic_fetch_add(s_ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
-  for (int t = 0; t < ntiles; ++t) {
+  // VAR & 32: staggered item transitions -- wave w reloads in the tiles t with (t + o_w) % 10 == 9, o_w spread over
+  // the 10 tiles of an item (SIMD partners w, w + 4 five tiles apart; VAR & 64: two phases only, waves 4-7 at 5).
+  // The reload tile and the tile after it are one straight-line pair, so the compiler's counted vmcnt before each
+  // MFMA of the second waits only for the registers it reads.
+  const int o_w = (VAR & 64) ? (wave >= 4 ? 5 : 0) : (wave < 4 ? wave : wave + 1);
+  auto tile = [&](int t, auto rl_c, auto after_c) __attribute__((always_inline)) {
+    constexpr bool RL = decltype(rl_c)::value;
+    constexpr bool AFTER = decltype(after_c)::value;
     if (VAR & 1) {
       for (int i = 0; i < (1 << 20); ++i) {
         if (__hip_atomic_load(s_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= WAVES * (t + 1)) break;
@@ -87,9 +99,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void probe(const h8* __restrict__ ro
     char* sbuf = smem + nxt * BUF;
     const int tsrc = (VAR & 16) ? (int)(((blockIdx.x & 7) * 1375 + t + 1) % src_tiles) : (int)((blockIdx.x + t) % src_tiles);
     const v4i sdesc = uniform_desc(src + (size_t)tsrc * (NK + 1) * 1024, (NK + 1) * 1024);
-    const bool reload = (VAR & 8) && (t % 10 == 9);
     const h8* nr = big_rows + ((size_t)(((long long)blockIdx.x * 7919 + t * 131) % big_items) * WAVES + wave) * NK * 64 + lane;
-    if ((VAR & 8) && t % 10 == 0) __builtin_amdgcn_s_waitcnt(0x0070);
+    if (!(VAR & 32) && (VAR & 8) && t % 10 == 0) __builtin_amdgcn_s_waitcnt(0x0070);
     f32x4 acc[4] = {z, z, z, z};
     h8 b[PD + 1];
 #pragma unroll
@@ -100,9 +111,17 @@ __global__ __launch_bounds__(WAVES * 64, 1) void probe(const h8* __restrict__ ro
       const int t2 = 2 * (s >> 1), qb = s & 1;
       acc[2 * qb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[t2], b[s % (PD + 1)], acc[2 * qb], 0, 0, 0);
       acc[2 * qb + 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[t2 + 1], b[s % (PD + 1)], acc[2 * qb + 1], 0, 0, 0);
-      if ((VAR & 8) && reload && (s & 1)) {
-        ra[s - 1] = nr[(s - 1) * 64];
-        ra[s] = nr[s * 64];
+      if (RL && (s & 1)) {
+        if (VAR & 128) {  // (timing only) loads the compiler does not see: no waits for them anywhere
+          asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(ra[s - 1]) : "v"(nr + (s - 1) * 64) : "memory");
+          asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(ra[s]) : "v"(nr + s * 64) : "memory");
+        } else if (VAR & 256) {  // non-temporal policy (K13's rows: aux = 2)
+          ra[s - 1] = __builtin_nontemporal_load(nr + (s - 1) * 64);
+          ra[s] = __builtin_nontemporal_load(nr + s * 64);
+        } else {
+          ra[s - 1] = nr[(s - 1) * 64];
+          ra[s] = nr[s * 64];
+        }
       }
       if (VAR & 2) {
         if (s >= 1 && (s - 1) * WAVES <= NK) {
@@ -112,8 +131,15 @@ __global__ __launch_bounds__(WAVES * 64, 1) void probe(const h8* __restrict__ ro
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    if ((VAR & 2) && !((VAR & 8) && reload)) __builtin_amdgcn_s_waitcnt(0x0070);
-    if ((VAR & 2) && (VAR & 8) && reload) __builtin_amdgcn_s_waitcnt(0x0070);  // (conservative: rows too)
+    if (VAR & 32) {
+      // the reload tile: wait for the DMA pieces only (38 row loads issued after the last piece may stay in flight)
+      if (RL) __builtin_amdgcn_s_waitcnt((38 & 15) | (0x7 << 4) | ((38 >> 4) << 14));
+      else if (VAR & 2) __builtin_amdgcn_s_waitcnt(0x0070);
+    } else {
+      if ((VAR & 2) && !RL) __builtin_amdgcn_s_waitcnt(0x0070);
+      if ((VAR & 2) && RL) __builtin_amdgcn_s_waitcnt(0x0070);  // (conservative: rows too)
+    }
+    (void)AFTER;
     if (VAR & 1) {
       asm volatile("" ::: "memory");
       if (lane == 0) __hip_atomic_fetch_add(s_ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -131,7 +157,28 @@ __global__ __launch_bounds__(WAVES * 64, 1) void probe(const h8* __restrict__ ro
       sink += acc[0][0] + acc[1][1] + acc[2][2] + acc[3][3];
     }
     cur = nxt;
+  };
+  for (int t = 0; t < ntiles;) {
+    if ((VAR & 32) && (VAR & 512)) {  // stagger, one loop: the reload tile is NOT paired with the next
+      if ((VAR & 8) && (t + o_w) % 10 == 9) tile(t, BoolC<true>{}, BoolC<false>{});
+      else tile(t, BoolC<false>{}, BoolC<false>{});
+      t += 1;
+    } else if (VAR & 32) {
+      if ((VAR & 8) && (t + o_w) % 10 == 9 && t + 1 < ntiles) {
+        tile(t, BoolC<true>{}, BoolC<false>{});
+        tile(t + 1, BoolC<false>{}, BoolC<true>{});
+        t += 2;
+      } else {
+        tile(t, BoolC<false>{}, BoolC<false>{});
+        t += 1;
+      }
+    } else {
+      if ((VAR & 8) && t % 10 == 9) tile(t, BoolC<true>{}, BoolC<false>{});
+      else tile(t, BoolC<false>{}, BoolC<false>{});
+      t += 1;
+    }
   }
+  __builtin_amdgcn_s_waitcnt(0x0070);
   const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
   if (lane == 0 && wave == 0) {
     clk[2 * blockIdx.x] = t1 - t0;
@@ -217,6 +264,12 @@ int main(int argc, char** argv) {
   run<15, 2, 8>("+sync +dma +epi +items", rows, src, src_tiles, out, clk, grid, ntiles);
   run<23, 2, 8>("+sync +dma +epi +hbm tiles", rows, src, big_tiles, out, clk, grid, ntiles);
   run<31, 2, 8>("+sync +dma +epi +items +hbm tiles", rows, src, big_tiles, out, clk, grid, ntiles);
+  run<47, 2, 8>("+sync +dma +epi +items staggered 8", rows, src, src_tiles, out, clk, grid, ntiles);
+  run<111, 2, 8>("+sync +dma +epi +items staggered 2", rows, src, src_tiles, out, clk, grid, ntiles);
+  run<63, 2, 8>("+sync +dma +epi +items stag8 +hbm tiles", rows, src, big_tiles, out, clk, grid, ntiles);
+  run<175, 2, 8>("+items stag8, loads never waited", rows, src, src_tiles, out, clk, grid, ntiles);
+  run<303, 2, 8>("+items stag8, nt loads", rows, src, src_tiles, out, clk, grid, ntiles);
+  run<815, 2, 8>("+items stag8 nt, one loop (unpaired)", rows, src, src_tiles, out, clk, grid, ntiles);
   run<10, 2, 8>("+dma +items (no sync)", rows, src, src_tiles, out, clk, grid, ntiles);
   run<26, 2, 8>("+dma +items +hbm tiles (no sync)", rows, src, big_tiles, out, clk, grid, ntiles);
   return 0;
