@@ -96,7 +96,7 @@ struct Workspace {
   bool prep_f8 = false;
   // K13 row-stationary scan: the full probe list, the pre-pass result, per-query headers and candidates
   Buf pre_probes, pre_kth, pre_goff, qhdr, rs_tq, cand_off, cand_key, cand_pos, rs_bucket_tmp, rs_tiles, rs_wave_buf,
-      rs_wave_cnt, rs_bounds, rs_ranges;
+      rs_wave_cnt, rs_bounds;
   // per-list query counts of the last search's own probe map (an exact fallback re-maps its queries)
   Buf rs_qcnt;  // K13's one-pass bucketing: candidates per query
   Buf stat_counts, rs_ovf_q, rs_ovf_rows, rs_ovf_d, rs_ovf_i, rs_items;
@@ -1106,15 +1106,6 @@ bool rs_pre_f8(mivs_index_s* idx, hipStream_t) {
   return idx->groups_f8.p != nullptr;
 }
 
-// K13's work plan: the share of each item queue's tile work dealt as static per-workgroup ranges (in 1/1024; the
-// rest is dealt item by item), where the staggered kernel runs; MIVS_RS_STAGGER=0: the round-4 kernel (-1)
-int rs_static_frac_q10() {
-  const char* e = getenv("MIVS_RS_STAGGER");
-  if (e && e[0] == '0' && e[1] == 0) return -1;
-  if (e && atoi(e) > 1) return std::min(1024, atoi(e));
-  return kRsStaticFracQ10;
-}
-
 // K13's bucketing in one pass into fixed-capacity per-query runs (MIVS_RS_BUCKET_1P=0: the two-pass CSR form);
 // MIVS_RS_QCAP: the run capacity (a query with more candidates is not proven and takes the fallback)
 bool rs_bucket_one_pass() {
@@ -1453,19 +1444,15 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   }
   ws.rs_items.reserve(sizeof(int4) * (size_t)std::max<int64_t>(max_items, 1));
   // items dealt from 8 queues of equal tile work, dynamically inside a queue
-  ws.rs_bounds.reserve(sizeof(int) * 17);
+  ws.rs_bounds.reserve(sizeof(int) * 9);
   const int grid = std::max(8, cu_count(idx->device) / 8 * 8);
   const int n_waves = grid * kRsWaves;
   // the wave stream counts + the lost flag, the 8 item-queue counters, the spun-out wave count (the last 10 are
   // zeroed by k_rs_items)
   ws.rs_wave_cnt.reserve(sizeof(int) * (n_waves + 1 + 8 + 1));
-  // the work plan of the staggered K13 (§6d-5): each workgroup's static range of items, then dynamic single items
-  const int frac_q10 = rs_static_frac_q10();
-  const bool v2 = frac_q10 >= 0;
-  ws.rs_ranges.reserve(sizeof(int) * 2 * (size_t)grid);
   HIPCHK(launch_rs_items(ws.work_off.as<int>(), ws.bucket_off.as<int>(), L.goff.as<int64_t>(), L.n_lists,
                          (int)max_items, ws.rs_items.as<int4>(), ws.rs_bounds.as<int>(), s,
-                         ws.rs_wave_cnt.as<int>() + n_waves, 10, ws.rs_ranges.as<int>(), grid, v2 ? frac_q10 : 0));
+                         ws.rs_wave_cnt.as<int>() + n_waves, 10));
   RsScanArgs a{};
   a.groups_h = idx->groups_h.as<uint16_t>();
   a.row_norms = L.norms.as<float>();
@@ -1488,8 +1475,6 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   a.wave_cnt = ws.rs_wave_cnt.as<int>();
   a.queue = a.wave_cnt + n_waves + 1;
   a.bounds = ws.rs_bounds.as<int>();
-  a.ranges = v2 ? ws.rs_ranges.as<int>() : nullptr;
-  a.stagger = v2 ? 1 : 0;
   a.flags = getenv("MIVS_RS_FLAGS") ? atoi(getenv("MIVS_RS_FLAGS")) : 0;
   if (a.flags & 2) a.flags |= 1;  // stale LDS tiles: never run an epilogue on them
   Buf pbuf;
@@ -1524,17 +1509,11 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
               "cycles/tile/wave %.0f\n", wc, h[3 * grid] / wc, h[3 * grid + 1] / wc, h[3 * grid + 3] / wc,
               h[3 * grid + 2] / wc,
               tiles_sum ? wc / ((double)tiles_sum * kRsWaves) : 0.0);
-    if (wc > 0 && v2)  // (k_rs_scan: [4] idle tiles' cycles, [5] reload tiles' k-loop cycles, [6] reloads)
-      fprintf(stderr, "[k13 phases] idle-tiles %.3f | reload tiles: %llu, k-loop %.0f cycles each (all tiles' k-loop "
-              "%.0f) | wave lifetime %.4g cycles (tile phases %.3f of it)\n", h[3 * grid + 4] / wc, h[3 * grid + 6],
-              h[3 * grid + 6] ? (double)h[3 * grid + 5] / h[3 * grid + 6] : 0.0,
-              tiles_sum ? (double)h[3 * grid + 1] / ((double)tiles_sum * kRsWaves) : 0.0, (double)h[3 * grid + 10],
-              h[3 * grid + 10] ? wc / (double)h[3 * grid + 10] : 0.0);
-    if (wc > 0 && !v2)
+    if (wc > 0)
       fprintf(stderr, "[k13 phases] mfma-result-wait %.3f (in epilogue: hit path %.3f) | wave-tiles taking the hit path "
               "%.4f of %llu\n", h[3 * grid + 4] / wc, h[3 * grid + 5] / wc,
               h[3 * grid + 7] ? (double)h[3 * grid + 6] / (double)h[3 * grid + 7] : 0.0, h[3 * grid + 7]);
-    if (wc > 0 && !v2 && h[3 * grid + 9] && h[3 * grid + 7] > h[3 * grid + 9])
+    if (wc > 0 && h[3 * grid + 9] && h[3 * grid + 7] > h[3 * grid + 9])
       fprintf(stderr, "[k13 phases] k-loop cycles: items' first tile %.0f, other tiles %.0f | wave lifetime %.4g cycles "
               "(tile phases %.3f of it)\n", (double)h[3 * grid + 8] / h[3 * grid + 9],
               (double)(h[3 * grid + 1] - h[3 * grid + 8]) / (double)(h[3 * grid + 7] - h[3 * grid + 9]),

@@ -266,8 +266,7 @@ constexpr int64_t kRsCandBudget = int64_t(1) << 27;  // ... and the batch's runs
 constexpr int kRsWaveCapMax = 16384;  // records of a K13 wave's candidate stream (more: all queries fall back)
 constexpr int kRsWaveCapMaxLk = 1 << 18;  // the same for large k (K16: thousands of candidates per query)
 constexpr int kRsRecInt4 = 3;         // a record: 8 dots of one lane and query half + {first row position, query}
-constexpr int kRsMaxBatch = 32768;
-constexpr int kRsStaticFracQ10 = 922;  // K13 work plan: ~90 % of each queue's tile work in static ranges (MIVS_RS_STAGGER)    // queries per K13 search batch (the LDS-histogram bucketing's bins)
+constexpr int kRsMaxBatch = 32768;    // queries per K13 search batch (the LDS-histogram bucketing's bins)
 
 struct RsScanArgs {
   const uint16_t* groups_h;  // fp16 lists, group layout [g][dp/8][32][8]
@@ -287,9 +286,7 @@ struct RsScanArgs {
   int wave_cap;              // records per stream
   int* wave_cnt;             // [grid * kRsWaves] stream lengths (may exceed wave_cap: records lost)
   int* queue;                // [8] per-queue item counters, zero at launch (dynamic dealing)
-  const int* bounds;         // [17] the queues' item ranges by tile work, then each queue's dynamic part's start
-  const int* ranges;         // [grid][2] each workgroup's static item range (k_rs_items' plan); nullptr: k_rs_scan_v1
-  int stagger;               // 1: staggered group transitions inside a segment (k_rs_scan)
+  const int* bounds;         // [9] the queues' item ranges by tile work (k_rs_bounds)
   int flags;                 // timing experiments only (MIVS_RS_FLAGS): 1 skip epilogue, 2 skip staging,
                              // 4 keep the rows at item transitions, 8 per-block clocks into prof, 16 phase clocks
   unsigned long long* prof;  // flags & 8: [grid][3] {start, end, tiles}
@@ -487,7 +484,7 @@ hipError_t launch_rs_pre_lists(const int64_t* goff, int n_lists, int div, int mi
                                int64_t nq, int np, int64_t* goff2, int64_t* probes2, hipStream_t s);
 hipError_t launch_rs_items(const int* work_off, const int* bucket_off, const int64_t* list_goff, int n_lists,
                            int max_items, int4* items, int* bounds, hipStream_t s,
-                           int* zero = nullptr, int nzero = 0, int* ranges = nullptr, int n_wg = 0, int frac_q10 = 0);
+                           int* zero = nullptr, int nzero = 0);
 hipError_t launch_rs_tiles(const int64_t* bucket_q, const int* bucket_off, int n_lists, int64_t ne, const uint16_t* qh,
                            const float4* qhdr, int nq, int dp, char* tiles, hipStream_t s);
 // tq (optional): T_q per query, the bound K11 checks its final window against

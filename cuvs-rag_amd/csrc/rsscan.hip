@@ -48,12 +48,10 @@ struct RsItem {
   int g0, gend, slot, ntiles;
 };
 
-// (the item table holds the list id in .z: the tile slot is bucket_off[l] / 32 + l)
 __device__ __forceinline__ RsItem rs_item(const RsScanArgs& a, int w) {
   const int4 v = a.items[w];
-  const int l = __builtin_amdgcn_readfirstlane(v.z);
   return RsItem{__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
-                __builtin_amdgcn_readfirstlane(a.bucket_off[l] / kRsQTile + l), __builtin_amdgcn_readfirstlane(v.w)};
+                __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w)};
 }
 
 // Stage one 32-query tile into an LDS buffer: the tile's image ([NK + 1] pieces x 1 KiB, built by
@@ -139,18 +137,10 @@ __device__ __forceinline__ void rs_signal(int* ctr) {
 }
 
 constexpr int kRsBPrefetch = 3;  // k-steps between a B operand's LDS read and its MFMA
-#ifndef RS_PD2
-#define RS_PD2 2
-#endif
-constexpr int kRsBPrefetchV2 = RS_PD2;  // the same for k_rs_scan
 
 template <bool B>
 struct BoolC {
   static constexpr bool value = B;
-};
-template <int V>
-struct IntC {
-  static constexpr int value = V;
 };
 
 
@@ -168,7 +158,7 @@ struct IntC {
 // behind so that each epilogue would run under the SIMD partner's MFMAs -- was correct but slower,
 // 5.41 vs 5.20 ms: the LDS-DMA issue cost, ~100+ cycles a piece, then sits on four waves.)
 template <int METRIC, int NK>
-__global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan_v1(RsScanArgs a) {
+__global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int BUF = NK * 1024 + 1024;
   constexpr int NBUF = 2;
@@ -286,10 +276,7 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan_v1(RsScanArgs a) {
     *s_ready = 0;
     s_next[1] = grab(1);
     s_next[2] = grab(2);
-    if (s_next[1] >= 0) {
-      const int4 v = a.items[s_next[1]];
-      s_desc[1] = make_int4(v.x, v.y, a.bucket_off[v.z] / kRsQTile + v.z, v.w);
-    }
+    if (s_next[1] >= 0) s_desc[1] = a.items[s_next[1]];
   }
   __syncthreads();  // (the only workgroup barrier: the counter is zero before any wave signals)
   {  // tile 0's pieces
@@ -393,10 +380,7 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan_v1(RsScanArgs a) {
       if (grabber) {
         grabbed = grab(ii + 3);  // (its result is waited for at the signal below)
         const int w2 = s_next[(ii + 2) & 3];  // (grabbed during the previous item's first tile)
-        if (w2 >= 0) {
-          const int4 v = a.items[w2];
-          desc2 = make_int4(v.x, v.y, a.bucket_off[v.z] / kRsQTile + v.z, v.w);
-        }
+        if (w2 >= 0) desc2 = a.items[w2];
       }
       const uint64_t ph1 = (a.flags & 16) ? __builtin_amdgcn_s_memtime() : 0;
       const bool last = LAST;
@@ -517,356 +501,6 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan_v1(RsScanArgs a) {
   block_prof();
 }
 
-// K13 with staggered group transitions. A wave holds one 32-row group in registers for every tile
-// of its list (T = the list's query tiles), then loads its next group during the group's last tile. When all eight
-// waves of a workgroup change groups in the same tile (one 256-row item at a time), the CU pulls 384 KiB of rows at
-// once and the issue of those loads stalls every wave: a quarter of the launch (§6d-3). Here a workgroup works
-// through a SEGMENT of one list -- a run of consecutive items, [g0, g0 + groups) -- and wave w changes groups at
-// tiles o_w + j T, o_w = w T / 8 (SIMD partners w, w + 4 half a list apart), so about one wave per tile reloads 48 KiB
-// while the others compute. Wave w's groups are g0 + w + 8 j; with o_w > 0 its first group is split: tiles [0, o_w)
-// first, the remaining [o_w, T) after its last full group (each (group, tile) pair is scanned once, in any order).
-// A reload tile and the tile after it run as one straight-line pair, so the compiler's counted vmcnt before each
-// MFMA of the second waits only for the registers that MFMA reads.
-// Work: per workgroup a static range of items (k_rs_items' plan: queue x = blockIdx % 8's first share of tile work
-// cut into equal ranges, split into segments at list ends), then single items dealt dynamically from the queues'
-// remaining items (and, once its queue is dry, the others'), as before.
-template <int METRIC, int NK>
-__global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int BUF = NK * 1024 + 1024;
-  constexpr int NBUF = 2;
-  constexpr int NB = 2 * NK;  // 8-dim blocks of a group row
-  constexpr int64_t IMG = (int64_t)(NK + 1) * 1024;
-  constexpr int STAGERS = kRsWaves;
-  static_assert((NK + STAGERS) / STAGERS < NK, "the image's pieces are issued over k-steps 1..");
-  // rows of the next group loaded (two per odd k-step) after this wave's last DMA piece (k-step NK / STAGERS + 1),
-  // less two: the order of a k-step's row load and DMA piece is the compiler's
-  constexpr int ROWS_AFTER = [] {
-    int c = 0;
-    for (int s = NK / STAGERS + 2; s < NK; ++s) c += (s & 1) ? 2 : 0;
-    return c - 2 > 0 ? c - 2 : 0;
-  }();
-  int* s_ready = reinterpret_cast<int*>(smem + NBUF * BUF);
-  // [4] ring of segment descriptors {first group, groups, tile slot of the list's tile 0, tiles}; tiles 0: none.
-  // Segment j + 2's is computed by the grabber (lane 0 of wave 0) during segment j's first tile and published with
-  // that tile's signal; every wave reads segment j + 1's after segment j's first ready wait.
-  int4* const s_seg = reinterpret_cast<int4*>(s_ready + 4);
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int kq = lane >> 4;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int x = blockIdx.x & 7;
-  // the grabber's cursor over its static range (in LDS: no registers held for it through the k-loops)
-  int* const s_range = s_ready + 20;
-  auto grab_seg = [&]() -> int4 {
-    const int si = s_range[0], se = s_range[1];
-    if (si < se) {  // the static range: the run of its items in one list
-      const int4 it = a.items[si];  // {first group, end group, list, tiles}
-      const int e = min(se, a.work_off[it.z + 1]);
-      const int gend = a.items[e - 1].y;
-      s_range[0] = e;
-      return make_int4(it.x, gend - it.x, (int)rs_tile_slot(a.bucket_off, it.z, 0), it.w);
-    }
-    int v = a.bounds[9 + x] + atomicAdd(a.queue + x, 1);
-    if (v >= a.bounds[x + 1]) {  // the queue is dry: the others' remaining items in turn
-      v = -1;
-      for (int k = 1; k < 8; ++k) {
-        const int xq = (x + k) & 7;
-        const int u = a.bounds[9 + xq] + atomicAdd(a.queue + xq, 1);
-        if (u < a.bounds[xq + 1]) {
-          v = u;
-          break;
-        }
-      }
-    }
-    if (v < 0) return make_int4(0, 0, 0, 0);
-    const int4 it = a.items[v];
-    return make_int4(it.x, it.y - it.x, (int)rs_tile_slot(a.bucket_off, it.z, 0), it.w);
-  };
-  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-  int n_tiles_done = 0;
-  int tt = 0;             // tiles this wave has started
-  bool spun_out = false;  // a wait gave up (never expected): the results are then not trusted
-  // flags & 16: this wave's cycles per tile phase, summed in LDS (no registers held for them through the k-loops):
-  // [0] ready wait, [1] k-loop, [2] epilogue, [3] own DMA wait, [4] idle tiles, [5] reload tiles' k-loop, [6] reloads
-  unsigned long long* const s_pw = reinterpret_cast<unsigned long long*>(smem + NBUF * BUF + 128) + 8 * wave;
-  if ((a.flags & 16) && lane < 8) s_pw[lane] = 0;
-  const uint64_t pw_t0 = __builtin_amdgcn_s_memtime();
-  const int widx = blockIdx.x * kRsWaves + wave;
-  int4* const wstream = a.wave_buf + (int64_t)widx * a.wave_cap * kRsRecInt4;
-  int wcnt = 0;  // records of this wave's candidate stream
-  auto block_prof = [&]() {
-    // (as k_rs_scan_v1: the stream length, the lost flag, the spun-out count, the timing records)
-    if (lane == 0) {
-      a.wave_cnt[widx] = spun_out ? 0 : min(wcnt, a.wave_cap);
-      if (spun_out || wcnt > a.wave_cap) atomicOr(a.wave_cnt + gridDim.x * kRsWaves, 1);
-      if (spun_out) atomicAdd(a.wave_cnt + gridDim.x * kRsWaves + 9, 1);
-    }
-    if ((a.flags & 8) && a.prof && tid == 0) {
-      a.prof[3 * blockIdx.x] = t_start;
-      a.prof[3 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-      a.prof[3 * blockIdx.x + 2] = (unsigned long long)n_tiles_done;
-    }
-    if ((a.flags & 16) && a.prof && lane == 0) {
-      unsigned long long* p = a.prof + 3 * gridDim.x;
-      for (int i = 0; i < 7; ++i) atomicAdd(p + i, s_pw[i]);
-      atomicAdd(p + 7, (unsigned long long)n_tiles_done);
-      atomicAdd(p + 10, (unsigned long long)(__builtin_amdgcn_s_memtime() - pw_t0));
-    }
-  };
-  if (tid == 0) {
-    s_range[0] = a.ranges[2 * blockIdx.x];
-    s_range[1] = a.ranges[2 * blockIdx.x + 1];
-    *s_ready = 0;
-    s_seg[0] = grab_seg();
-    s_seg[1] = grab_seg();
-  }
-  __syncthreads();  // (the only workgroup barrier: the counter is zero before any wave signals)
-  int4 sg;
-  {
-    const int4 v = s_seg[0];
-    sg = make_int4(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
-                   __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
-  }
-  if (sg.w == 0) {
-    block_prof();
-    return;
-  }
-  // Buffer loads of a group: a descriptor in SGPRs (uniform base, NB * 512 bytes), this lane's 32-bit offset in one
-  // VGPR and the register's offset in soffset; the non-temporal policy (aux = 2: the rows are read once per search)
-  const int lane_off = kq * 512 + (lane & 15) * 16;
-  auto group_rsrc = [&](int grp) {
-    return uniform_rsrc(reinterpret_cast<const char*>(a.groups_h) + (int64_t)grp * (NB * 512), NB * 512);
-  };
-  // register i = 2 t + rb at byte (i >> 1) * 2048 + (i & 1) * 256: the multiple of 4 KiB in soffset, the rest in the
-  // instruction's offset field (12 distinct SGPR constants for the 48 registers instead of 48)
-  auto ld_rows = [&](__amdgpu_buffer_rsrc_t r, int i) {
-    constexpr int dummy = 0;
-    (void)dummy;
-    const int off = (i >> 1) * 2048 + (i & 1) * 256;
-    return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(r, lane_off + (off & 4095), off & ~4095, 2));
-  };
-  {  // tile 0's pieces
-    const v4i d0 = uniform_desc(a.tiles + (int64_t)sg.z * IMG, (int)IMG);
-#pragma unroll
-    for (int p0 = 0; p0 <= NK; p0 += STAGERS)
-      if (p0 + wave <= NK) dma_b128(d0, smem + (p0 + wave) * 1024, lane * 16, (p0 + wave) * 1024);
-  }
-  int g = sg.x + wave;  // the group in this wave's registers (valid: gv)
-  bool gv = sg.y > wave;
-  // the smallest row norm of the wave's group (the filter's lower bound; pad rows: +inf, so a real row's)
-  float xnmin = METRIC == kL2 ? a.group_nmin[gv ? g : sg.x] : 0.0f;
-  float xn_next = 0.0f;
-  h8 ra[NK];
-  {
-    const __amdgpu_buffer_rsrc_t r0 = group_rsrc(gv ? g : sg.x);
-#pragma unroll
-    for (int s = 0; s < NK; ++s) ra[s] = ld_rows(r0, s);
-  }
-  __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): tile 0's pieces (signalled below) and the rows
-  rs_signal(s_ready);
-  int cur = 0;  // LDS buffer of the current tile
-  int sj = 0;   // segment ordinal
-  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
-  for (;;) {
-    const int sg0 = sg.x, sng = sg.y, sslot = sg.z, snt = sg.w;
-    const int n_max = (sng + kRsWaves - 1) / kRsWaves;
-    const int L = n_max * snt;  // the segment's tiles
-    const int n_w = sng > wave ? (sng - wave + kRsWaves - 1) / kRsWaves : 0;  // this wave's groups
-    // this wave's phase o (0: no split group); both parts of a split group are >= 2 tiles, so a reload tile is never
-    // the second of a pair
-    const int o0 = (wave * snt) / kRsWaves;
-    const int o = a.stagger && snt >= 4 && n_w >= 2 && o0 > 0 ? min(max(o0, 2), snt - 2) : 0;
-    const int n_steps = n_w + (o > 0 ? 1 : 0);
-    const int ga = sg0 + wave;
-    // step k: group, end tile (steps cover [0, n_w T) back to back)
-    auto step_g = [&](int k) { return (o > 0 && k == n_w) ? ga : ga + kRsWaves * k; };
-    auto step_e = [&](int k) { return o > 0 ? (k == 0 ? o : (k == n_w ? n_w * snt : o + k * snt)) : (k + 1) * snt; };
-    int4 nsg = make_int4(0, 0, 0, 0);  // the next segment (read in the first tile, after its ready wait)
-
-    // the filter over one tile's dots (as k_rs_scan_v1)
-    auto epilogue = [&](const f32x4 (&acc4)[4], const float4& h0, const float4& h1) __attribute__((always_inline)) {
-      const float mm0 = METRIC == kL2 ? -2.0f * h0.x : -h0.x;
-      const float mm1 = METRIC == kL2 ? -2.0f * h1.x : -h1.x;
-      float am0 = fmaxf(acc4[0][0], acc4[1][0]), am1 = fmaxf(acc4[2][0], acc4[3][0]);
-#pragma unroll
-      for (int i = 1; i < 4; ++i) {
-        am0 = fmaxf(am0, fmaxf(acc4[0][i], acc4[1][i]));
-        am1 = fmaxf(am1, fmaxf(acc4[2][i], acc4[3][i]));
-      }
-      const float xb = METRIC == kL2 ? xnmin : 0.0f;
-      const bool p0 = fmaf(am0, mm0, xb) < h0.y, p1 = fmaf(am1, mm1, xb) < h1.y;
-      const uint64_t m0 = __ballot(p0), m1 = __ballot(p1);
-      if ((m0 | m1) == 0) return;
-      const int pos0 = g * kGroupRows + 4 * kq;
-      const int n0 = __popcll(m0);
-      if (p0) {
-        const int at = wcnt + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u));
-        if (at < a.wave_cap) {
-          int4* r = wstream + (int64_t)at * kRsRecInt4;
-          r[0] = __builtin_bit_cast(int4, acc4[0]);
-          r[1] = __builtin_bit_cast(int4, acc4[1]);
-          r[2] = make_int4(pos0, __float_as_int(h0.w), 0, 0);
-        }
-      }
-      if (p1) {
-        const int at = wcnt + n0 + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
-        if (at < a.wave_cap) {
-          int4* r = wstream + (int64_t)at * kRsRecInt4;
-          r[0] = __builtin_bit_cast(int4, acc4[2]);
-          r[1] = __builtin_bit_cast(int4, acc4[3]);
-          r[2] = make_int4(pos0, __float_as_int(h1.w), 0, 0);
-        }
-      }
-      wcnt += n0 + __popcll(m1);
-    };
-
-    // One tile t of the segment. MODE 0: the k-loop on the wave's group (act: the tile is one of the wave's steps; an idle
-    // tile -- the wave has no group left in this segment -- skips the k-loop and the epilogue); 1: the same, loading
-    // group g_in (or, g_in < 0, the wave's first group of the next segment) into each register right after its last
-    // MFMA (a wave without a group in this segment does so in its first tile: MFMAs on stale rows, no epilogue).
-    auto tile = [&](int t, auto mode_c, int g_in, bool act) __attribute__((always_inline)) {
-      constexpr int MODE = decltype(mode_c)::value;
-      const uint64_t ph0 = (a.flags & 16) ? __builtin_amdgcn_s_memtime() : 0;
-      // every wave's pieces of this tile have landed and every wave is done with the previous tile
-      if (!spun_out && !rs_spin(s_ready, kRsWaves * (tt + 1))) spun_out = true;
-      ++tt;
-      if (t == 0) {
-        const int4 v = s_seg[(sj + 1) & 3];
-        nsg = make_int4(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
-                        __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
-      }
-      const bool grabber = t == 0 && wave == 0 && lane == 0;
-      int4 gdesc = make_int4(0, 0, 0, 0);
-      if (grabber) gdesc = grab_seg();  // (its result is waited for at the signal below)
-      const uint64_t ph1 = (a.flags & 16) ? __builtin_amdgcn_s_memtime() : 0;
-      int gnx = 0;
-      bool gvn = false;
-      if (MODE == 1) {
-        if (g_in >= 0) {
-          gnx = g_in;
-          gvn = true;
-        } else {
-          gnx = nsg.x + wave;
-          gvn = nsg.w > 0 && nsg.y > wave;
-        }
-      }
-      // the next tile (of this segment, or the next segment's first) goes into the next buffer (nothing to stage:
-      // a descriptor of size 0, whose loads write zeros to a buffer no tile reads again)
-      const bool in_seg = t + 1 < L;
-      const char* simg = a.tiles + (in_seg ? (int64_t)(sslot + (t + 1) % snt) : (int64_t)nsg.z) * IMG;
-      const bool stage = (in_seg || nsg.w > 0) && !(a.flags & 2);
-      const v4i sdesc = uniform_desc(simg, stage ? (int)IMG : 0);
-      const int nxt = cur + 1 == NBUF ? 0 : cur + 1;
-      char* sbuf = smem + nxt * BUF;
-      // (a reload tile always loads, so that it has one k-loop: without a next group, the segment's first group again)
-      const bool reload = MODE == 1;
-      const __amdgpu_buffer_rsrc_t nrs = group_rsrc(gvn ? gnx : sg0);
-      f32x4 acc4[4] = {zero4, zero4, zero4, zero4};
-      auto kloop = [&](auto reload_c) __attribute__((always_inline)) {
-        constexpr bool RL = decltype(reload_c)::value;
-        const char* bb = smem + cur * BUF + lane * 16;
-        constexpr int PD = kRsBPrefetchV2;  // B operands PD pieces ahead (ring of PD + 1)
-        h8 b[PD + 1];
-#pragma unroll
-        for (int u = 0; u < PD; ++u) b[u] = *reinterpret_cast<const h8*>(bb + (u < NK ? u : 0) * 1024);
-#pragma unroll
-        for (int s = 0; s < NK; ++s) {
-          if (s + PD < NK) b[(s + PD) % (PD + 1)] = *reinterpret_cast<const h8*>(bb + (s + PD) * 1024);
-          const int t2 = 2 * (s >> 1), qb = s & 1;
-          acc4[2 * qb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[t2], b[s % (PD + 1)], acc4[2 * qb], 0, 0, 0);
-          acc4[2 * qb + 1] =
-              __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[t2 + 1], b[s % (PD + 1)], acc4[2 * qb + 1], 0, 0, 0);
-          if constexpr (RL) {
-            // the next group's rows, right after the last use of the registers (registers 2 t, 2 t + 1 after piece
-            // 2 t + 1), its smallest row norm first, with the first k-step
-            if (s == 0 && METRIC == kL2) xn_next = a.group_nmin[gvn ? gnx : sg0];
-            if (s & 1) {
-              ra[s - 1] = ld_rows(nrs, s - 1);
-              ra[s] = ld_rows(nrs, s);
-            }
-          }
-          if (s >= 1 && (s - 1) * STAGERS <= NK) {
-            // (past the last piece a wave loads the last one again: the same bytes to the same place)
-            const int p = min((s - 1) * STAGERS + wave, NK);
-            dma_b128(sdesc, sbuf + p * 1024, lane * 16, p * 1024);
-          }
-          // keep each k-step's operations in their k-step (the scheduler otherwise sinks the B reads next to their
-          // MFMAs: one exposed LDS latency per k-step)
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      };
-      float4 hq0 = make_float4(0.f, 0.f, 0.f, 0.f), hq1 = hq0;
-      if (MODE == 1 || act) {
-        kloop(BoolC<MODE == 1>{});
-        // (the header piece holds query j's header at lanes j and j + 32; one conflict-free ds_read_b128 each)
-        hq0 = *reinterpret_cast<const float4*>(smem + cur * BUF + NK * 1024 + (lane & 15) * 16);
-        hq1 = *reinterpret_cast<const float4*>(smem + cur * BUF + NK * 1024 + (16 + (lane & 15)) * 16);
-        asm volatile("" ::"v"(hq0.z), "v"(hq1.z));
-      } else {
-        // idle: this wave's pieces of the next tile
-#pragma unroll
-        for (int p0 = 0; p0 <= NK; p0 += STAGERS)
-          if (p0 + wave <= NK) dma_b128(sdesc, sbuf + (p0 + wave) * 1024, lane * 16, (p0 + wave) * 1024);
-      }
-      const uint64_t ph2 = (a.flags & 16) ? __builtin_amdgcn_s_memtime() : 0;
-      // signal the next tile: this wave's reads of this one are done (lgkmcnt(0)) and its DMA pieces of the next have
-      // landed -- vmcnt counts, in issue order, only the rows issued after its last piece beyond them
-      if (MODE == 1 && reload) rs_wait_vm(ROWS_AFTER);
-      else rs_wait_vm(0);
-      if (grabber) s_seg[(sj + 2) & 3] = gdesc;
-      rs_signal(s_ready);
-      const uint64_t ph2b = (a.flags & 16) ? __builtin_amdgcn_s_memtime() : 0;
-      if (act && !(a.flags & 1)) epilogue(acc4, hq0, hq1);
-      if (MODE == 1) {  // the wave's registers now hold (or are loading) group gnx
-        g = gnx;
-        gv = gvn;
-        if (METRIC == kL2 && gvn) xnmin = xn_next;
-      }
-      if ((a.flags & 16) && lane == 0) {
-        const uint64_t ph3 = __builtin_amdgcn_s_memtime();
-        s_pw[0] += ph1 - ph0;
-        s_pw[MODE == 1 || act ? 1 : 4] += ph2 - ph1;
-        if (MODE == 1) {
-          s_pw[5] += ph2 - ph1;
-          s_pw[6] += 1;
-        }
-        s_pw[3] += ph2b - ph2;
-        s_pw[2] += ph3 - ph2b;
-      }
-      cur = nxt;
-    };
-
-    // this wave's steps: the first tile of each runs as its own copy (the compiler's counted vmcnt before each MFMA
-    // then waits only for the register it reads, loaded in the previous step's last tile), the middle tiles as one,
-    // the last tile (the reload) as one
-    int t = 0;
-    for (int k = 0; k < n_steps; ++k) {
-      const int e = step_e(k);
-      if (e - t >= 2) {
-        tile(t, IntC<0>{}, 0, true);
-        for (++t; t < e - 1; ++t) tile(t, IntC<0>{}, 0, true);
-      }
-      tile(t, IntC<1>{}, k + 1 < n_steps ? step_g(k + 1) : -1, true);
-      ++t;
-    }
-    // the idle tail (fewer groups than the segment's rounds): a wave with no group at all loads the next segment's rows
-    // in its first tile (its MFMAs on stale rows)
-    if (t < L && n_w == 0) {
-      tile(t, IntC<1>{}, -1, false);
-      ++t;
-    }
-    for (; t < L; ++t) tile(t, IntC<0>{}, 0, false);
-    n_tiles_done += L;
-    ++sj;
-    sg = nsg;
-    if (sg.w == 0) break;
-  }
-  block_prof();
-}
-
 // The 8 item queues of K13 as ranges of equal TILE work (bounds [9]): an item costs its list's tile count,
 // and lists differ in queries, so equal item counts left one queue ~3 % heavier than the mean. Item
 // weights are uniform inside a list: queue x starts at the first item whose work prefix reaches
@@ -919,84 +553,15 @@ __device__ void rs_bounds_block(const int* __restrict__ work_off, const int* __r
   }
 }
 
-// K13's work plan, in LDS for up to kRsPlanLists lists: the 8 queues as ranges of equal tile work
-// (bounds[0..8]), the start of each queue's dynamically dealt part (bounds[9 + x]: the part past the first
-// frac_q10 / 1024 of its work) and per workgroup b of the K13 grid (n_wg, a multiple of 8) its static range
-// [ranges[2 b], ranges[2 b + 1]): queue b % 8's static part cut into n_wg / 8 ranges of equal work, in list order.
-// An item of list l costs T_l tiles; item_at(W') is the first item whose work prefix reaches W'.
-constexpr int kRsPlanLists = 4096;
-__device__ void rs_plan_block(const int* __restrict__ work_off, const int* __restrict__ bucket_off, int n_lists,
-                              int* __restrict__ bounds, int* __restrict__ ranges, int n_wg, int frac_q10) {
-  __shared__ int64_t s_wp[kRsPlanLists + 1];
-  __shared__ int s_nt[kRsPlanLists];
-  __shared__ int s_wo[kRsPlanLists + 1];
-  __shared__ int64_t sh[16];
-  int64_t base = 0;
-  for (int l0 = 0; l0 < n_lists; l0 += 1024) {
-    const int l = l0 + threadIdx.x;
-    int64_t wl = 0;
-    if (l < n_lists) {
-      const int nt = (bucket_off[l + 1] - bucket_off[l] + kRsQTile - 1) / kRsQTile;
-      wl = (int64_t)(work_off[l + 1] - work_off[l]) * nt;
-      s_nt[l] = nt;
-      s_wo[l] = work_off[l];
-    }
-    int64_t t;
-    const int64_t ex = block_excl_scan(wl, sh, &t);
-    if (l < n_lists) s_wp[l] = base + ex;
-    base += t;
-  }
-  if (threadIdx.x == 0) {
-    s_wp[n_lists] = base;
-    s_wo[n_lists] = work_off[n_lists];
-  }
-  __syncthreads();
-  const int64_t W = base;
-  const int n_items = s_wo[n_lists];
-  auto item_at = [&](int64_t wt) {
-    if (wt >= W) return n_items;
-    int lo = 0, hi = n_lists - 1;  // the largest l with s_wp[l] <= wt: then s_wp[l + 1] > wt, list l has work
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (s_wp[mid] <= wt) lo = mid;
-      else hi = mid - 1;
-    }
-    const int64_t r = (wt - s_wp[lo] + s_nt[lo] - 1) / s_nt[lo];
-    return (int)min((int64_t)s_wo[lo + 1], (int64_t)s_wo[lo] + r);
-  };
-  const int P = n_wg >> 3;
-  if (threadIdx.x <= 8) bounds[threadIdx.x] = item_at(W * threadIdx.x / 8);
-  if (threadIdx.x < 8) {
-    const int64_t q0 = W * threadIdx.x / 8, q1 = W * (threadIdx.x + 1) / 8;
-    bounds[9 + threadIdx.x] = item_at(q0 + (q1 - q0) * frac_q10 / 1024);
-  }
-  for (int b = threadIdx.x; b < n_wg; b += blockDim.x) {
-    const int x = b & 7, pp = b >> 3;
-    const int64_t q0 = W * x / 8, q1 = W * (x + 1) / 8;
-    const int64_t ws = (q1 - q0) * frac_q10 / 1024;
-    ranges[2 * b] = item_at(q0 + ws * pp / P);
-    ranges[2 * b + 1] = item_at(q0 + ws * (pp + 1) / P);
-  }
-}
-
 // Work items of K13 from the probe map (chunk = kRsBlockGroups groups, one tile column per list):
-// item w -> {first group, end group, its list, tiles of its list}
+// item w -> {first group, end group, first tile slot of its list, tiles of its list}
 // (one launch: blocks of 1024 items, and with bounds the last block computes the queue bounds)
 __global__ __launch_bounds__(1024) void k_rs_items(const int* __restrict__ work_off, const int* __restrict__ bucket_off,
                                                    const int64_t* __restrict__ list_goff, int n_lists, int max_items,
                                                    int4* __restrict__ items, int* __restrict__ zero, int nzero,
-                                                   int* __restrict__ bounds, int* __restrict__ ranges, int n_wg,
-                                                   int frac_q10) {
+                                                   int* __restrict__ bounds) {
   if (bounds && blockIdx.x == gridDim.x - 1) {
-    if (ranges && n_lists <= kRsPlanLists) {
-      rs_plan_block(work_off, bucket_off, n_lists, bounds, ranges, n_wg, frac_q10);
-      return;
-    }
-    // (more lists than the plan's LDS holds: no static ranges, every item dealt dynamically)
     rs_bounds_block(work_off, bucket_off, n_lists, bounds);
-    __syncthreads();
-    if (threadIdx.x < 8) bounds[9 + threadIdx.x] = bounds[threadIdx.x];
-    for (int b = threadIdx.x; ranges && b < 2 * n_wg; b += blockDim.x) ranges[b] = 0;
     return;
   }
   const int w = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1010,7 +575,7 @@ __global__ __launch_bounds__(1024) void k_rs_items(const int* __restrict__ work_
   const int64_t g0 = list_goff[lo] + (int64_t)(w - work_off[lo]) * kRsBlockGroups;
   const int64_t ge = list_goff[lo + 1] < g0 + kRsBlockGroups ? list_goff[lo + 1] : g0 + kRsBlockGroups;
   const int m = bucket_off[lo + 1] - bucket_off[lo];
-  items[w] = make_int4((int)g0, (int)ge, lo, (m + kRsQTile - 1) / kRsQTile);
+  items[w] = make_int4((int)g0, (int)ge, (int)rs_tile_slot(bucket_off, lo, 0), (m + kRsQTile - 1) / kRsQTile);
 }
 
 // per query: {qs, uf, qn, q} for K13 (uf carries T_q: the one-fma filter bound for the exact k-th key over the
@@ -1121,8 +686,8 @@ __global__ __launch_bounds__(256) void k_rs_tiles(const int64_t* __restrict__ bu
 
 size_t rs_scan_lds_bytes(int dp) {
   const int nk = dp / 16;
-  // two tile buffers + the tiles-ready counter, the item / segment ring and its descriptors, the phase clocks
-  return (size_t)2 * (nk * 1024 + 1024) + 128 + 8 * 8 * kRsWaves;
+  // two tile buffers + the tiles-ready counter, the item ring and its descriptors
+  return (size_t)2 * (nk * 1024 + 1024) + 128;
 }
 
 bool rs_scan_supported(int dp) {
@@ -1132,11 +697,10 @@ bool rs_scan_supported(int dp) {
 template <int METRIC, int NK>
 static hipError_t launch_rs_mk(const RsScanArgs& a, int grid, hipStream_t s) {
   const size_t lds = rs_scan_lds_bytes(NK * 16);
-  const void* f = a.ranges ? (const void*)k_rs_scan<METRIC, NK> : (const void*)k_rs_scan_v1<METRIC, NK>;
-  hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipError_t e = hipFuncSetAttribute((const void*)k_rs_scan<METRIC, NK>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
   if (e != hipSuccess) return e;
-  if (a.ranges) hipLaunchKernelGGL((k_rs_scan<METRIC, NK>), dim3(grid), dim3(kRsThreads), lds, s, a);
-  else hipLaunchKernelGGL((k_rs_scan_v1<METRIC, NK>), dim3(grid), dim3(kRsThreads), lds, s, a);
+  hipLaunchKernelGGL((k_rs_scan<METRIC, NK>), dim3(grid), dim3(kRsThreads), lds, s, a);
   return hipGetLastError();
 }
 
@@ -1189,14 +753,12 @@ hipError_t launch_rs_tiles(const int64_t* bucket_q, const int* bucket_off, int n
 }
 
 hipError_t launch_rs_items(const int* work_off, const int* bucket_off, const int64_t* list_goff, int n_lists,
-                           int max_items, int4* items, int* bounds, hipStream_t s, int* zero, int nzero, int* ranges,
-                           int n_wg, int frac_q10) {
+                           int max_items, int4* items, int* bounds, hipStream_t s, int* zero, int nzero) {
   if (nzero > 256) return hipErrorInvalidValue;
   if (max_items <= 0 && nzero <= 0) return hipSuccess;
-  if (ranges && (n_wg <= 0 || n_wg % 8 != 0 || frac_q10 < 0 || frac_q10 > 1024)) return hipErrorInvalidValue;
   const unsigned nb = (unsigned)ceil_div(max_items > 0 ? max_items : 1, 1024) + (bounds ? 1 : 0);
   hipLaunchKernelGGL(k_rs_items, dim3(nb), dim3(1024), 0, s, work_off, bucket_off, list_goff, n_lists, max_items, items,
-                     zero, nzero, bounds, ranges, n_wg, frac_q10);
+                     zero, nzero, bounds);
   return hipGetLastError();
 }
 
