@@ -8,9 +8,14 @@ fraction), batch of Q=10,000 held-out queries, n_probes=32, k=10.
 
 One step = one batched ivf_flat.search of the Q queries on every rank (+ for N>1 the
 RCCL all-gather of the per-shard top-k and the device merge). N GPUs = one process
-per GPU (torch.distributed.run), each rank owns shard `rank` of an N x 10M corpus
-(weak scaling, BASELINE configs[3] at N=8). `value` counts (query, 10M-row shard)
-searches per second = plain QPS at N=1; `qps_full_corpus` is Q / step time.
+per GPU (torch.distributed.run). Two corpus modes:
+  * default (weak scaling, "scaling": "weak"): each rank owns a 10M-row shard of an N x 10M corpus
+    (BASELINE configs[3] at N=8);
+  * --rows-total R (strong scaling, "scaling": "strong"): one R-row corpus split over the N ranks with the
+    reference's 'even' split (gpu_resource_manager.distribute_workload), R = 10M for configs[2] at every N.
+`value` is the full-corpus QPS in both: Q queries answered over the whole corpus (every shard searched and
+the per-shard top-k merged) per second = Q / step time. `shard_searches_per_s` (Q * N / step time) is reported
+beside it.
 
 Also reported: build vectors/s (wall clock, data resident in HBM), recall@10 against
 exact brute-force ground truth (same engine), the fine-scan kernel's roofline
@@ -48,7 +53,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", type=int, default=10_000_000, help="corpus rows per GPU")
+    ap.add_argument("--rows", type=int, default=10_000_000, help="corpus rows per GPU (weak scaling)")
+    ap.add_argument("--rows-total", type=int, default=0,
+                    help="fixed corpus of this many rows split over the ranks (strong scaling; 0: --rows per GPU)")
     ap.add_argument("--dim", type=int, default=768)
     ap.add_argument("--queries", type=int, default=10_000)
     ap.add_argument("--n-lists", type=int, default=1024)
@@ -63,7 +70,12 @@ def parse():
     ap.add_argument("--gt-queries", type=int, default=2000, help="queries with exact ground truth for recall")
     ap.add_argument("--sweep", default="8,16,32,64", help="comma list of n_probes to sweep (QPS + recall each); "
                                                            "'' to skip")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0,
+                    help="target duration of each CPU-baseline sample (the node's cores, then the job's share)")
+    ap.add_argument("--latency", default="1,10,100",
+                    help="side line: per-call latency of searches of this many queries (the reference searches one "
+                         "query per call); '' to skip")
+    ap.add_argument("--latency-probes", default="32,20", help="n_probes of the latency side line (20: cuVS default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--flat-rows", type=int, default=1_000_000,
                     help="BASELINE configs[1] side line: brute force over this many rows (0: skip)")
@@ -161,46 +173,64 @@ def host_cpu_info() -> dict:
     return info
 
 
-def cpu_threads() -> int:
-    """Every core this process may use, within the job's share (OMP_NUM_THREADS when the harness sets it)."""
+def node_threads() -> int:
+    """Every hardware thread this process may run on (sched_getaffinity): north_star's 'the node's own host cores'."""
     try:
-        n = len(os.sched_getaffinity(0))
+        return max(1, len(os.sched_getaffinity(0)))
     except AttributeError:
-        n = os.cpu_count() or 1
+        return os.cpu_count() or 1
+
+
+def cpu_threads() -> int:
+    """The job's CPU share: the node's threads capped by OMP_NUM_THREADS when the harness sets it (16 per GPU)."""
+    n = node_threads()
     omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     return max(1, min(n, omp) if omp else n)
 
 
 def cpu_baseline(idx, q_host, gt, n_probes, k, target_s, rank_log):
-    """FAISS-algorithm IVF-Flat search (oracle/cpu_baseline.c, OpenMP over queries) on this host."""
+    """FAISS-algorithm IVF-Flat search (oracle/cpu_baseline.c, OpenMP over queries) on this host: `value` on every
+    thread of the node (the affinity set), `value_job_share` on the job's share (OMP_NUM_THREADS); each on a query
+    sample sized for ~target_s seconds."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # bench.py's cpu_baseline leg is one of the oracle's allowed users
 
-    threads = cpu_threads()
-    O.fast_set_threads(threads)
     rank_log(f"[cpu] copying index to host ({idx.size} rows) ...")
     rows = idx.list_rows().cpu().numpy()
     ids = idx.list_ids().cpu().numpy()
     sizes = idx.list_sizes.numpy()
     off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
     cents = idx.centers.cpu().numpy()
-    O.fast_ivf_search(rows, ids, off, cents, q_host[:4], n_probes, k)  # warm caches / pages
-    t0 = time.perf_counter()
-    O.fast_ivf_search(rows, ids, off, cents, q_host[:16], n_probes, k)
-    per_q = (time.perf_counter() - t0) / 16
-    ns = int(max(16, min(q_host.shape[0], target_s / max(per_q, 1e-9))))
-    t0 = time.perf_counter()
-    _, ci = O.fast_ivf_search(rows, ids, off, cents, q_host[:ns], n_probes, k)
-    dt = time.perf_counter() - t0
+
+    def timed(threads, q0):
+        O.fast_set_threads(threads)
+        O.fast_ivf_search(rows, ids, off, cents, q_host[q0:q0 + 4], n_probes, k)  # warm caches / pages / threads
+        n16 = max(16, threads)
+        t0 = time.perf_counter()
+        O.fast_ivf_search(rows, ids, off, cents, q_host[q0:q0 + n16], n_probes, k)
+        per_q = (time.perf_counter() - t0) / n16
+        ns = int(max(n16, min(q_host.shape[0] - q0, target_s / max(per_q, 1e-9))))
+        t0 = time.perf_counter()
+        _, ci = O.fast_ivf_search(rows, ids, off, cents, q_host[q0:q0 + ns], n_probes, k)
+        return ns, time.perf_counter() - t0, ci
+
+    node, job = node_threads(), cpu_threads()
+    ns, dt, ci = timed(node, 0)
     nr = min(ns, gt.shape[0])
     rec = recall_at_k(ci[:nr], gt[:nr]) if nr > 0 else None
+    share = None
+    if job != node:
+        ns_j, dt_j, _ = timed(job, 0)
+        share = {"value": ns_j / dt_j, "cores": job, "sample": f"{ns_j} queries, {dt_j:.1f} s"}
     del rows
     host = host_cpu_info()
-    return {"value": ns / dt, "unit": "QPS", "cores": threads, "kind": "port", "host": host,
-            "cores_note": f"{threads} threads = this job's CPU share (the harness's OMP_NUM_THREADS: one GPU's share of "
-                          f"a {host.get('physical_cores')}-core / {host.get('logical_cpus')}-thread node); the "
-                          f"search is OpenMP over queries, so the whole node's cores would scale it by at most "
-                          f"{host.get('logical_cpus') or 0} / {threads}",
+    return {"value": ns / dt, "unit": "QPS", "cores": node, "kind": "port", "host": host,
+            "value_job_share": share["value"] if share else ns / dt,
+            "job_share": share or {"cores": node, "note": "the job's share is the whole affinity set"},
+            "cores_note": f"value: all {node} hardware threads this process may run on (sched_getaffinity; the node "
+                          f"has {host.get('physical_cores')} cores / {host.get('logical_cpus')} threads); "
+                          f"value_job_share: the {job} threads the harness gives one GPU's job (OMP_NUM_THREADS); "
+                          "the search is OpenMP over queries",
             "sample": f"{ns} of the {q_host.shape[0]} benchmark queries, same index (copied to host), n_probes="
                       f"{n_probes}, k={k}; FAISS IndexIVFFlat search algorithm restated in oracle/cpu_baseline.c "
                       f"(faiss not installed); {dt:.1f} s",
@@ -373,6 +403,53 @@ def large_k_side_line(a, idx, q, rl, scanned_rows):
     return out
 
 
+def latency_side_line(a, idx, q, rl):
+    """The reference's own search shape (improved_multi_gpu_rag.py:209-237 search_on_gpu, :279-303 batch_search: one
+    query per call; cuvs-2gpu-main.ipynb:1789-1836): per-call wall time of ivf_flat.search at small batches, each call
+    on the next queries of the benchmark batch, synchronized before and after (what a caller waits for, host
+    enqueue included), and the GPU time of the same calls (hipEvents on the search stream). The pre-filter path is
+    the same as the main line's; recall and bits are the main search's (tests/test_gpu_baseline_configs.py checks
+    Q = 1 and Q = 7 against the oracle)."""
+    from mivs.neighbors import ivf_flat
+
+    out = []
+    for np_ in [int(v) for v in a.latency_probes.split(",") if v.strip()]:
+        sp = ivf_flat.SearchParams(n_probes=np_)
+        for nq in [int(v) for v in a.latency.split(",") if v.strip()]:
+            calls = 400 if nq <= 10 else 200
+            for i in range(5):  # warm (workspace sizes for this batch shape)
+                ivf_flat.search(sp, idx, q[i * nq:(i + 1) * nq], a.k)
+            torch.cuda.synchronize()
+            wall = []
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(calls)]
+            for c in range(calls):
+                o = (c * nq) % (q.shape[0] - nq)
+                qq = q[o:o + nq]
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                ev[c][0].record()
+                ivf_flat.search(sp, idx, qq, a.k)
+                ev[c][1].record()
+                torch.cuda.synchronize()
+                wall.append(time.perf_counter() - t0)
+            gpu = [e0.elapsed_time(e1) for e0, e1 in ev]
+            w = np.array(wall) * 1e3
+            st = idx.last_search_stats()
+            line = {"queries_per_call": nq, "n_probes": np_, "k": a.k, "calls": calls,
+                    "p50_ms": round(float(np.percentile(w, 50)), 4), "p99_ms": round(float(np.percentile(w, 99)), 4),
+                    "mean_ms": round(float(w.mean()), 4), "gpu_p50_ms": round(float(np.percentile(gpu, 50)), 4),
+                    "qps_at_this_batch": round(nq / (w.mean() * 1e-3), 1), "path": {13: "K13", 10: "K10", 31: "K3w",
+                                                                                    3: "K3"}.get(st.get("scan_kernel"),
+                                                                                                 str(st.get("scan_kernel")))}
+            out.append(line)
+            rl(f"[latency] Q={nq} n_probes={np_}: p50 {line['p50_ms']:.3f} ms p99 {line['p99_ms']:.3f} ms "
+               f"(GPU p50 {line['gpu_p50_ms']:.3f} ms) via {line['path']}")
+    return {"calls": out, "reference_published": {"search_time_ms": 2.013, "hardware": "A100 (cuVS IVF-Flat)",
+                                                  "corpus": "2M rows (its scaling test)",
+                                                  "source": "Attempt_1/cuvs_2gpu.ipynb:1258"},
+            "note": "context only: the reference's published per-query time is from other hardware and another corpus"}
+
+
 def single_process_side_line(a, q, ref_ids, rl, devices, indexes=None):
     """The reference's own multi-GPU shape (improved_multi_gpu_rag.py:105,206,239-277; merge contract
     Attempt_1/test_search_result_aggregator.py:405-457): ONE process drives `devices` -- a rows-per-GPU
@@ -389,7 +466,7 @@ def single_process_side_line(a, q, ref_ids, rl, devices, indexes=None):
 
     devices = list(devices)
     G = len(devices)
-    n = a.rows
+    shards = corpus_shards(a, G)
     indexes = dict(indexes or {})
     extra = {}
     t_build = 0.0
@@ -400,10 +477,11 @@ def single_process_side_line(a, q, ref_ids, rl, devices, indexes=None):
                   "kmeans_trainset_fraction": a.trainset_fraction}
 
         def one(g):
+            b0, b1 = shards[devices.index(g)]
             with torch.cuda.device(g):
-                xg = ops.synth_mixture(n, a.dim, SEED, n_centers=a.centers, sigma=a.sigma, row_begin=g * n, device=g)
+                xg = ops.synth_mixture(b1 - b0, a.dim, SEED, n_centers=a.centers, sigma=a.sigma, row_begin=b0, device=g)
                 torch.cuda.synchronize(g)
-                ix, tb = b.build_index_on_gpu(GPUConfig(g), xg, IndexType.IVF_FLAT, params, ids_offset=g * n)
+                ix, tb = b.build_index_on_gpu(GPUConfig(g), xg, IndexType.IVF_FLAT, params, ids_offset=b0)
                 del xg
                 torch.cuda.empty_cache()
                 return g, ix, tb
@@ -422,7 +500,8 @@ def single_process_side_line(a, q, ref_ids, rl, devices, indexes=None):
     for _ in range(reps):
         r = agg.perform_distributed_search(q, indexes, cfg)
     t = (time.perf_counter() - t0) / reps
-    line = {"devices": G, "rows_per_gpu": n, "rows_total": n * G, "queries": q.shape[0], "k": a.k,
+    line = {"devices": G, "rows_per_gpu": [e - b for b, e in shards], "rows_total": shards[-1][1], "queries": q.shape[0],
+            "k": a.k,
             "n_probes": a.n_probes, "qps_full_corpus": round(q.shape[0] / t, 1),
             "shard_searches_per_s": round(q.shape[0] * G / t, 1), "ms_per_batch": round(t * 1e3, 3),
             "shards_built_here": len(todo), "shards_build_s": round(t_build, 3),
@@ -430,13 +509,23 @@ def single_process_side_line(a, q, ref_ids, rl, devices, indexes=None):
                     "results copied to host as the reference's contract returns them"}
     if ref_ids is not None:
         line["final_ids_equal_main_search"] = bool(np.array_equal(r.final_indices, np.asarray(ref_ids)))
-    rl(f"[single-process] {G} GPU(s), {n * G} rows: {q.shape[0] / t:,.0f} QPS through the aggregator + RCCL merge"
+    rl(f"[single-process] {G} GPU(s), {shards[-1][1]} rows: {q.shape[0] / t:,.0f} QPS through the aggregator + RCCL merge"
        + (f"; ids equal to the per-rank run: {line['final_ids_equal_main_search']}" if ref_ids is not None
           else ""))
     for ix in extra.values():
         ix.close()
     torch.cuda.empty_cache()
     return line
+
+
+def corpus_shards(a, world):
+    """[(start, end)] row range of each rank's shard: --rows per rank (weak scaling), or --rows-total split with the
+    reference's 'even' rule (strong scaling)."""
+    if a.rows_total > 0:
+        from gpu_resource_manager import even_split
+
+        return even_split(a.rows_total, world)
+    return [(r * a.rows, (r + 1) * a.rows) for r in range(world)]
 
 
 def run_with_watchdog(fn, timeout_s):
@@ -469,6 +558,39 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
+def run_child(cmd, env, timeout_s, is_result=lambda s: s.startswith("{") and '"metric"' in s):
+    """Start `cmd` in its own session, forward its stdout lines to stderr except the result line, and return
+    (exit status, result line or None). The deadline runs from the start: stdout is read on a helper thread, so a
+    child that hangs with stdout open (a rank stuck in a collective keeps torch.distributed.run alive) is killed --
+    its whole process group -- when the deadline passes, and the status is then 124."""
+    import subprocess
+
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, start_new_session=True)
+    box = {"line": None}
+
+    def _read():
+        for ln in p.stdout:
+            s = ln.strip()
+            if is_result(s):
+                box["line"] = s
+            elif s:
+                print(s, file=sys.stderr, flush=True)
+
+    th = threading.Thread(target=_read, daemon=True)
+    th.start()
+    try:
+        rc = p.wait(timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        try:
+            os.killpg(p.pid, 9)
+        except ProcessLookupError:
+            pass
+        p.wait()
+        rc = 124
+    th.join(timeout=10)
+    return rc, box["line"]
+
+
 def launcher_argv(a, argv, port, ids_out):
     """The child command for `bench.py --gpus N` (N > 1) started without WORLD_SIZE: N ranks, one per GPU,
     under torch.distributed.run on this node (the same command the driver may use itself); rank 0 writes the
@@ -486,7 +608,6 @@ def self_launch(a, argv):
     (single_process_aggregator: every shard on its own device in this process, aggregator threads + the RCCL
     merge of mivs.comm.LocalComm) over the same N devices and check its final ids against the ranks' merged
     ids. Prints one JSON line and exits with the ranks' status (EXIT_HUNG if the one-process line hung)."""
-    import subprocess
     import tempfile
 
     tmpd = tempfile.mkdtemp(prefix="mivs_bench_")
@@ -500,19 +621,7 @@ def self_launch(a, argv):
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     t0 = time.perf_counter()
-    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, start_new_session=True)
-    line = None
-    try:
-        for ln in p.stdout:
-            s = ln.strip()
-            if s.startswith("{") and '"metric"' in s:
-                line = s
-            elif s:
-                print(s, file=sys.stderr, flush=True)
-        rc = p.wait(timeout=a.launch_timeout)
-    except subprocess.TimeoutExpired:
-        os.killpg(p.pid, 9)
-        rc = 124
+    rc, line = run_child(cmd, env, a.launch_timeout)
     if line is None:
         print(f"[launcher] the ranks exited with {rc} and no result line", file=sys.stderr, flush=True)
         return rc or 1
@@ -695,8 +804,11 @@ def main():
 
     mivs.load()
     rl = lambda *m: log(rank, *m)  # noqa: E731
-    n, d, Q, k = a.rows, a.dim, a.queries, a.k
-    start = rank * n
+    shards = corpus_shards(a, world)
+    start, end = shards[rank]
+    n, d, Q, k = end - start, a.dim, a.queries, a.k
+    rows_total = shards[-1][1]
+    strong = a.rows_total > 0
 
     # ---- data: generated on the device (no PCIe in any timed region) ----
     x = ops.synth_mixture(n, d, SEED, n_centers=a.centers, sigma=a.sigma, row_begin=start, device=local)
@@ -719,10 +831,10 @@ def main():
     t_build = max_over_ranks(time.perf_counter() - t0, world, dev)
     _native.set_profiling(False)
     build_phases = idx.build_phases()
-    build_vps = n * world / t_build
+    build_vps = rows_total / t_build
     index_mem = idx.memory()  # one fp32 copy (64-B row blocks) + the fp16 and fp8 copies, all built in build()
     sizes = idx.list_sizes.numpy()
-    rl(f"[build] {n * world} rows in {t_build:.2f} s -> {build_vps / 1e6:.2f} M vec/s; lists min/med/max "
+    rl(f"[build] {rows_total} rows in {t_build:.2f} s -> {build_vps / 1e6:.2f} M vec/s; lists min/med/max "
        f"{sizes.min()}/{int(np.median(sizes))}/{sizes.max()}")
 
     sp = ivf_flat.SearchParams(n_probes=a.n_probes)
@@ -751,7 +863,7 @@ def main():
     stats = idx.last_search_stats()
     ms_per_step = t_steps / a.steps * 1e3
     qps_full = Q * a.steps / t_steps
-    value = qps_full * world  # (query, 10M-row shard) searches per second; = QPS at N=1
+    value = qps_full  # full-corpus QPS: Q queries answered over every shard (searched + merged) per second
     rl(f"[search] {a.steps} steps x {Q} queries: {ms_per_step:.3f} ms/step -> {qps_full:,.0f} QPS (full corpus)")
 
     # ---- PCIe-inclusive rate (not `value`): queries start in pinned host memory, results return to host ----
@@ -882,6 +994,13 @@ def main():
         except Exception as e:  # the IVF line stands without it
             rl(f"[large-k] side line failed: {e!r}")
 
+    latency = None
+    if rank == 0 and world == 1 and a.latency.strip():
+        try:
+            latency = latency_side_line(a, idx, q, rl)
+        except Exception as e:  # the IVF line stands without it
+            rl(f"[latency] side line failed: {e!r}")
+
     if a.ids_out and rank == 0:  # (the launcher's one-process check compares against these)
         np.save(a.ids_out, res_i.cpu().numpy())
 
@@ -924,17 +1043,24 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f32",  # results are the exact fp32 answer (the fp16 pre-filter only selects candidates)
         "data": f"synthetic: on-device Gaussian mixture ({a.centers} centres, sigma={a.sigma}, L2-normalised), "
                 f"seed {SEED}; queries = held-out rows of the same mixture",
-        "config": {"workload": f"IVF-Flat {n // 1_000_000}M x {d} fp32 per GPU, n_lists={a.n_lists}, "
+        "config": {"workload": (f"IVF-Flat {rows_total / 1e6:g}M x {d} fp32 split over {world} GPU(s)" if strong else
+                                f"IVF-Flat {n / 1e6:g}M x {d} fp32 per GPU ({rows_total / 1e6:g}M total)")
+                               + f", n_lists={a.n_lists}, "
                                f"n_probes={a.n_probes}, k={k}, batch of {Q} queries",
-                   "rows_per_gpu": n, "rows_total": n * world, "dim": d, "queries": Q, "n_lists": a.n_lists,
+                   "rows_per_gpu": [e - b for b, e in shards] if strong else n, "rows_total": rows_total, "dim": d,
+                   "queries": Q, "n_lists": a.n_lists,
                    "n_probes": a.n_probes, "k": k, "kmeans_n_iters": a.kmeans_iters,
                    "kmeans_trainset_fraction": a.trainset_fraction, "parallelism": f"corpus-shard{world}",
-                   "value_definition": "(query, 10M-row shard) searches per second; equals QPS at n_gpus=1"},
+                   "value_definition": "full-corpus QPS: queries answered over the whole corpus (every shard searched "
+                                       "and the per-shard top-k merged) per second = queries / step time",
+                   "corpus_mode": "fixed corpus split over the ranks (strong scaling)" if strong else
+                                  "one shard of --rows per rank (weak scaling)"},
+        "shard_searches_per_s": round(qps_full * world, 2),
         "qps_full_corpus": round(qps_full, 2),
         "qps_host_io": round(qps_host_io, 2),
         "qps_host_io_streamed": round(qps_host_io_streamed, 2),
@@ -950,6 +1076,7 @@ def main():
         "n_probes_sweep": sweep,
         "flat_bruteforce_1m": flat,
         "large_k": large_k,
+        "latency": latency,
         "single_process_aggregator": single,
         "ivf_pq_12m5": pq,
         "distributed": dist_info,

@@ -269,9 +269,8 @@ void single_list_topk(const ListSet& ls, int G, const float* queries, const floa
   const int64_t chunks = std::max<int64_t>(1, ceil_div(ls.n_groups, G));
   require(ceil_div(nq, kQTile) * chunks < (int64_t)INT32_MAX, "too many work items", MIVS_ERR_UNSUPPORTED);
   if (k > kMaxK || dump) {  // DUMP scan + K8 select, in query batches
-    // K3w's 64-query tiles where they apply (two accumulator chains per wave; MIVS_DUMP_WIDE=0: K3's 32)
-    const char* dwe = getenv("MIVS_DUMP_WIDE");
-    const int dq = !(dwe && dwe[0] == '0') && scan_wide_supported(0, d, dp, G) ? 64 : kQTile;
+    // K3w's 64-query tiles where they apply (two accumulator chains per wave; K3's 32 otherwise)
+    const int dq = scan_wide_supported(0, d, dp, G) ? 64 : kQTile;
     const int64_t slot_rows = (int64_t)G * kGroupRows;
     const int64_t qb = select_batch(nq, (size_t)(chunks * (slot_rows * 4 + 16)));
     for (int64_t b0 = 0; b0 < nq; b0 += qb) {
@@ -447,7 +446,7 @@ void as_assign_rows(const PfAssign& P, const float* data, const float* data_norm
   a.ovf_count = cnt.as<int>();
   a.ovf_rows = ws.ovf_q.as<int64_t>();
   a.queue = cnt.as<int>() + 2;
-  a.flags = getenv("MIVS_AS_FLAGS") ? atoi(getenv("MIVS_AS_FLAGS")) : 0;
+  a.flags = env_int("MIVS_AS_FLAGS", 0);
   HIPCHK(launch_as_scan(a, cu_count(device), s));
   int h[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(h, cnt.p, 8, hipMemcpyDeviceToHost, s));
@@ -502,9 +501,8 @@ void pf_assign_k12(const PfAssign& P, const float* data, const float* data_norms
   unsigned h[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(h, st.p, 8, hipMemcpyDeviceToHost, s));
   // probe map: one list (the centroids), every query in its bucket. K12 (128 register-resident queries per
-  // CU, the centroids streamed from L2) unless MIVS_PF_ASSIGN_REG=0 or dp is outside its instantiations
-  const char* are = getenv("MIVS_PF_ASSIGN_REG");
-  const bool use_r = !(are && are[0] == '0') && pr_scan_supported(dp);
+  // CU, the centroids streamed from L2) where dp is within its instantiations, else K10
+  const bool use_r = pr_scan_supported(dp);
   const int cg = use_r ? std::max<int>(1, (int)std::min<int64_t>(cents.n_groups, 1 << 20))
                        : std::max(1, std::min<int>(std::min(kPfChunkGroups, pf_max_chunk_groups(dp)),
                                                    (int)cents.n_groups));
@@ -560,7 +558,7 @@ void pf_assign_k12(const PfAssign& P, const float* data, const float* data_norms
   a.no_theta = chunks == 1 ? 1 : 0;  // every row's one work item: no bound to share
   const int grid = std::max(8, cu_count(device) / 8 * 8);
   Buf pbuf;
-  const bool pprof = getenv("MIVS_PF_FLAGS") && (atoi(getenv("MIVS_PF_FLAGS")) & 32) && use_r;
+  const bool pprof = (env_int("MIVS_PF_FLAGS", 0) & 32) && use_r;
   if (pprof) {  // diagnostic: K12 phase clocks of the assign to stderr
     pbuf.reserve(16 * sizeof(unsigned long long));
     HIPCHK(hipMemsetAsync(pbuf.p, 0, 16 * sizeof(unsigned long long), s));
@@ -804,11 +802,10 @@ void pf_enable(mivs_index_s* idx, hipStream_t s) {
   idx->x_res_max = resmax;
   pf_build_f8(idx, s);
   std::vector<int64_t> c(L.n_lists);
-  const char* ce = getenv("MIVS_PF_CHUNK_ROWS");
-  // rows per work item: as many as the LDS holds the norms of beside the query tile (the tile's
-  // staging is paid once per item), unless MIVS_PF_CHUNK_ROWS asks for fewer
+  // rows per work item: kPfChunkGroups groups, or as many as the LDS holds the norms of beside the query tile (the
+  // tile's staging is paid once per item)
   const int gmax = pf_max_chunk_groups(idx->dp);
-  idx->pf_G = std::max(1, std::min(gmax, ce ? atoi(ce) / kGroupRows : kPfChunkGroups));
+  idx->pf_G = std::max(1, std::min(gmax, kPfChunkGroups));
   auto top_prefix = [&](int G, std::vector<int64_t>& out) {
     for (int l = 0; l < L.n_lists; ++l) c[l] = L.chunks_of(l, G);
     std::sort(c.begin(), c.end(), std::greater<int64_t>());
@@ -857,21 +854,16 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   const std::vector<int64_t>& tcp = idx->pf_top_chunks_prefix;
   const int64_t max_slots = std::max<int64_t>(1, nq * tcp[std::min<int64_t>(np, L.n_lists)]);
   // per-slot candidates: room above k so that a neighbourhood packed into one chunk does not overflow
-  const char* ske = getenv("MIVS_PF_SLOT_K");  // K10 slot size override (16 or 32)
-  const int slot_k = (ske && atoi(ske) <= 16 && k <= 16) ? 16 : kPfSlotKMax;  // (k > 16: the coarse probe)
+  const int slot_k = kPfSlotKMax;
   ws.pf_key.reserve(sizeof(float) * (size_t)max_slots * slot_k);
   ws.pf_pos.reserve(sizeof(int) * (size_t)max_slots * slot_k);
   ws.pf_bound.reserve(sizeof(float) * (size_t)max_slots);
   // the 8 queue counters, then (K10) one convoy position per (list, chunk)
-  const char* cve = getenv("MIVS_PF_CONVOY");
-  const bool convoy = !(cve && cve[0] == '0');
-  const int64_t n_cpos = convoy ? (int64_t)n_lists * tcp[1] : 0;
+  const int64_t n_cpos = (int64_t)n_lists * tcp[1];
   ws.counter.reserve(sizeof(int) * (8 * 16 + n_cpos));  // (zeroed below, in the qtheta fill's launch)
   PfScanArgs a{};
-  if (convoy) {
-    a.chunk_pos = ws.counter.as<int>() + 8 * 16;
-    a.chunk_stride = (int)tcp[1];
-  }
+  a.chunk_pos = ws.counter.as<int>() + 8 * 16;
+  a.chunk_stride = (int)tcp[1];
   a.groups_h = idx->groups_h.as<uint16_t>();
   a.row_norms = L.norms.as<float>();
   if (f8) {  // K13's fp8 nomination: the fp8 queries beside the fp16 ones (the headers and tiles use those)
@@ -907,14 +899,11 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   HIPCHK(launch_fill2_i32(ws.qtheta.as<int>(), nq, (int)kPfOrdInf, ws.counter.as<int>(), 8 * 16 + n_cpos, 0, s));
   a.qtheta = ws.qtheta.as<unsigned>();
   a.k = verify_sel > 0 ? std::min(verify_sel, kPfMaxK) : k;  // (nomination: the slots keep the verify_sel best)
-  // (nomination: K11v reads only each slot's verify_sel best keys and their ties; MIVS_PF_SLOT_OUT=0: merge whole slots)
-  const char* soe = getenv("MIVS_PF_SLOT_OUT");
-  a.slot_out = verify_sel > 0 && !(soe && soe[0] == '0') ? a.k : 0;
-  // K13's pre-pass (kth_out): each list sample is scanned by one tile -- its rows are read once
-  // (MIVS_PF_PRE_NT=0: the default policy, A/B runs)
-  const char* pne = getenv("MIVS_PF_PRE_NT");
-  a.rows_nt = kth_out != nullptr && !(pne && pne[0] == '0');
-  a.flags = getenv("MIVS_PF_FLAGS") ? atoi(getenv("MIVS_PF_FLAGS")) : 0;
+  // (nomination: K11v reads only each slot's verify_sel best keys and their ties, so the slot merge stops there)
+  a.slot_out = verify_sel > 0 ? a.k : 0;
+  // K13's pre-pass (kth_out): each list sample is scanned by one tile -- its rows are read once (non-temporal)
+  a.rows_nt = kth_out != nullptr;
+  a.flags = env_int("MIVS_PF_FLAGS", 0);
   Buf pbuf;
   if (a.flags & 32) {  // diagnostic: K10 phase clocks to stderr
     pbuf.reserve(16 * sizeof(unsigned long long));
@@ -1028,12 +1017,8 @@ void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_
 
 // The coarse probe for n_probes > 16 (beyond K3w's register top-k): K3 in DUMP mode (every key of the
 // centroid list, written as computed) + K8 per query, instead of K3's 32- or 64-entry register top-k per
-// lane + K7 over the chunks (same keys, same (key, id) order: bit-identical probes). MIVS_COARSE_DUMP=0
-// keeps the register top-k.
-bool coarse_dump(int np) {
-  const char* e = getenv("MIVS_COARSE_DUMP");
-  return np > 16 && !(e && e[0] == '0');
-}
+// lane + K7 over the chunks (same keys, same (key, id) order: bit-identical probes).
+bool coarse_dump(int np) { return np > 16; }
 
 // Centroid chunk of the coarse probe: enough (query tile, chunk) work items for >= 4 per CU -- a 10k-query
 // batch over 1024 centroids is only 313 query tiles -- with K7 merging the chunks' top-n_probes
@@ -1041,8 +1026,7 @@ bool coarse_dump(int np) {
 // multiple of 4 groups (a pass is one group per wave): 194 us against 212 us at 8 groups (configs[2], 1024 lists)
 int coarse_groups(const mivs_index_s* idx, int64_t nq, int np) {
   const int64_t ng = std::max<int64_t>(1, idx->cents.n_groups);
-  const char* dwe = getenv("MIVS_DUMP_WIDE");
-  if (coarse_dump(np) && !(dwe && dwe[0] == '0') && scan_wide_supported(0, idx->d, idx->dp, 4)) {
+  if (coarse_dump(np) && scan_wide_supported(0, idx->d, idx->dp, 4)) {
     const int64_t tiles = std::max<int64_t>(1, ceil_div(nq, 64));
     const int64_t chunks = std::min<int64_t>(ng, std::max<int64_t>(1, ceil_div(8LL * cu_count(idx->device), tiles)));
     const int64_t g4 = ceil_div(ceil_div(ng, chunks), 4) * 4;
@@ -1302,7 +1286,10 @@ void lk_finish(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   HIPCHK(launch_exclusive_scan_i64(ws.lk_chunks.as<int64_t>(), ws.lk_chunk_off.as<int64_t>(), nq + 1, ws.scan_tmp.p, s));
   HIPCHK(launch_lk_recompute(a, cu_count(idx->device), s));
   HIPCHK(launch_lk_sort(a, s));
-  int64_t h[2] = {0, 0};
+  // (the fallback size and window count through the pinned stats: a pageable destination would make the copy
+  // host-synchronous and the polling pointless)
+  ws.h_stats.reserve(16);
+  int64_t* h = ws.h_stats.as<int64_t>();
   HIPCHK(hipMemcpyAsync(h, ws.pf_stats.p, 16, hipMemcpyDeviceToHost, s));
   spin_wait(s);  // the fallback size
   const int64_t novf = (int64_t)(int32_t)(h[0] & 0xFFFFFFFF);
@@ -1391,27 +1378,6 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
                            idx->x_norm_max, idx->x_res_max, dp, idx->metric, qhdr, ws.rs_tq.as<float>(), s,
                            one_pass ? ws.rs_qcnt.as<int>() : nullptr, one_pass ? nq : 0,
                            one_pass ? ws.pf_stats.as<int>() : nullptr, one_pass ? 8 : 0));
-  if (getenv("MIVS_RS_PRE_STATS")) {  // diagnostic: the pre-pass's k-th keys and T_q (stderr)
-    std::vector<float> hk(nq), ht(nq);
-    HIPCHK(hipMemcpyAsync(hk.data(), ws.pre_kth.p, sizeof(float) * nq, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(ht.data(), ws.rs_tq.p, sizeof(float) * nq, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    double sk = 0, st = 0;
-    int64_t ninf = 0;
-    for (int64_t i = 0; i < nq; ++i) {
-      if (!(hk[i] < INFINITY)) { ++ninf; continue; }
-      sk += hk[i];
-      st += ht[i];
-    }
-    const double nf = std::max<double>(1.0, (double)(nq - ninf));
-    std::vector<float> sorted = ht;
-    std::sort(sorted.begin(), sorted.end());
-    auto pc = [&](double f) { return sorted[std::min<int64_t>(nq - 1, (int64_t)(f * nq))]; };
-    fprintf(stderr, "[rs pre] k %d f8 %d div %d sel %d r_max %d | mean kth %.6f mean T_q %.6f | inf %lld of %lld | "
-            "T_q p10 %.4f p50 %.4f p90 %.4f p99 %.4f max %.4f\n", k, (int)pre_f8, large ? plan.div : pre_div, pre_sel,
-            large ? plan.r_max : 0, sk / nf, st / nf, (long long)ninf, (long long)nq, pc(0.1), pc(0.5), pc(0.9),
-            pc(0.99), sorted[nq - 1]);
-  }
   // 3. probe map: items = (list, block of kRsBlockGroups groups); every query of a list in one tile column
   ws.counts.reserve(sizeof(int) * L.n_lists);
   ws.fill.reserve(sizeof(int) * L.n_lists);
@@ -1475,7 +1441,7 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   a.wave_cnt = ws.rs_wave_cnt.as<int>();
   a.queue = a.wave_cnt + n_waves + 1;
   a.bounds = ws.rs_bounds.as<int>();
-  a.flags = getenv("MIVS_RS_FLAGS") ? atoi(getenv("MIVS_RS_FLAGS")) : 0;
+  a.flags = env_int("MIVS_RS_FLAGS", 0);
   if (a.flags & 2) a.flags |= 1;  // stale LDS tiles: never run an epilogue on them
   Buf pbuf;
   if (a.flags & 24) {  // diagnostic: per-block clocks (8) / per-phase wave-cycles (16) to stderr
@@ -1554,9 +1520,10 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   // several GB at this k)
   HIPCHK(launch_rs_bucket_count(a.wave_buf, a.wave_cap, a.wave_cnt, n_waves, (int)nq, qhdr, a.row_norms, idx->metric,
                                 ws.cand_off.as<int64_t>(), ws.rs_bucket_tmp.p, a.wave_cnt + n_waves, s));
-  int64_t total = 0;
-  HIPCHK(hipMemcpyAsync(&total, ws.cand_off.as<int64_t>() + nq, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  ws.h_stats.reserve(16);
+  HIPCHK(hipMemcpyAsync(ws.h_stats.p, ws.cand_off.as<int64_t>() + nq, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   spin_wait(s);
+  const int64_t total = *ws.h_stats.as<int64_t>();
   ws.cand_key.reserve(sizeof(float) * (size_t)std::max<int64_t>(total, 1));
   ws.cand_pos.reserve(sizeof(int) * (size_t)std::max<int64_t>(total, 1));
   HIPCHK(launch_rs_bucket_scatter(a.wave_buf, a.wave_cap, a.wave_cnt, n_waves, (int)nq, qhdr, a.row_norms, idx->metric,
@@ -1676,7 +1643,7 @@ void pq_search_rt(mivs_index_s* idx, hipStream_t s, const float* d_q, int64_t nq
   }
   max_chunks = std::max<int64_t>(max_chunks, 1);
   const int64_t qb = dump ? select_batch(nq, (size_t)max_chunks * ((size_t)kRtRows * 4 + 16)) : nq;
-  const int flags = getenv("MIVS_PQ_FLAGS") ? atoi(getenv("MIVS_PQ_FLAGS")) : 0;
+  const int flags = env_int("MIVS_PQ_FLAGS", 0);
   if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
   for (int64_t b0 = 0; b0 < nq; b0 += qb) {
     const int64_t nb = std::min<int64_t>(qb, nq - b0);
@@ -2011,7 +1978,7 @@ int32_t mivs_ivf_flat_search(mivs_index_t idx, void* stream, const float* d_q, i
     require(np <= kMaxSelectK, "n_probes must be <= " + std::to_string(kMaxSelectK), MIVS_ERR_UNSUPPORTED);
     require(np == n_probes || d_probes == nullptr, "n_probes > n_lists with a probes output");
     HostTrace& ht = host_trace();
-    static const bool trace = getenv("MIVS_HOST_TRACE") && getenv("MIVS_HOST_TRACE")[0] == '1';
+    static const bool trace = env_int("MIVS_HOST_TRACE", 0) == 1;
     ht.on = trace;
     if (trace) {
       ht.n_wait = 0;
@@ -2422,12 +2389,10 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
       a.k = k;
       a.out_d = ws.part_d.as<float>();
       a.out_i = ws.part_i.as<int64_t>();
-      a.flags = getenv("MIVS_PQ_FLAGS") ? atoi(getenv("MIVS_PQ_FLAGS")) : 0;
-      // list-sorted, XCD-aware slot order (MIVS_PQ_ORDER=0: slot order q * n_probes + p): the probe map
-      // with one chunk per list gives, per list, the queries probing it and their output slots
-      const char* oe = getenv("MIVS_PQ_ORDER");
-      const bool order = !(oe && oe[0] == '0');
-      if (order) {
+      a.flags = env_int("MIVS_PQ_FLAGS", 0);
+      // list-sorted, XCD-aware slot order: the probe map with one chunk per list gives, per list, the queries
+      // probing it and their output slots
+      {
         const int64_t ne = nq * np;
         ws.counts.reserve(sizeof(int) * L.n_lists);
         ws.fill.reserve(sizeof(int) * L.n_lists);
@@ -2463,7 +2428,7 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
       MergeArgs m{};
       m.in_d = ws.part_d.as<float>();
       m.in_i = ws.part_i.as<int64_t>();
-      m.slot_begin = order ? ws.slot_begin.as<int64_t>() : nullptr;
+      m.slot_begin = ws.slot_begin.as<int64_t>();
       m.slots_per_q = np;
       m.nq = nq;
       m.k_in = k;

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cstdlib>
 #include <chrono>
 #include <mutex>
 #include <stdexcept>
@@ -79,6 +80,12 @@ struct Buf {
 
 // pinned host memory for the search's small device-to-host reads (hipHostMalloc: the copy is a DMA the host
 // can poll for, not a staged pageable copy)
+// an integer engine setting from the environment (timing / diagnostic flags, workspace sizes), read at the call
+inline int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && e[0] ? atoi(e) : dflt;
+}
+
 struct HostBuf {
   void* p = nullptr;
   size_t n = 0;

@@ -23,6 +23,14 @@
 #include "mivs_common.hpp"
 #include "pf_math.hpp"
 
+// LDS: k_lk_sort<kLkMaxCap> keeps kLkMaxCap (key, id) pairs in static LDS (96 KiB at 8192) and k_lk_recompute_rm asks
+// for kLkRmWaves x (64 x 64 + dp) floats of dynamic LDS (~82 KiB at dp = 1024): both fit gfx950's 160 KiB per
+// workgroup, not the 64 KiB of earlier CDNA parts. The build is for gfx950 only (Makefile ARCH); another target fails
+// here rather than at launch.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "largek.hip sizes its LDS for gfx950 (160 KiB per workgroup)"
+#endif
+
 namespace mivs {
 
 namespace {
@@ -478,8 +486,7 @@ hipError_t launch_lk_chunks(const int* win_n, int64_t nq, int64_t* chunks, hipSt
 
 hipError_t launch_lk_recompute(const LkArgs& a, int cus, hipStream_t s) {
   if (a.nq <= 0) return hipSuccess;
-  const char* e = getenv("MIVS_LK_GATHER");
-  if (a.dp % 64 == 0 && a.dp <= 1024 && !(e && e[0] == '0')) {
+  if (a.dp % 64 == 0 && a.dp <= 1024) {
     // two workgroups of 4 waves per CU: 8 waves x 16 KiB of rows in flight
     const size_t lds = sizeof(float) * (size_t)kLkRmWaves * (64 * 64 + a.dp);
     static const hipError_t a0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lk_recompute_rm<kL2>),

@@ -922,7 +922,14 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
         }
       }
       // the results are read next by LDS stores: the wait states of an XDL result read as LDS data, explicit
-      // (the compiler placed a store one instruction after its MFMA: 12 % of the LUT entries were stale)
+      // (the compiler placed a store one instruction after its MFMA: 12 % of the LUT entries were stale). gfx950,
+      // v_mfma_f32_16x16x4_f32 (8 passes): 18 wait states between the last MFMA writing a register and an LDS store
+      // (ds_write) reading it as data -- s_nop N idles N + 1 cycles, so 8 + 8 + 5 = 21 >= 18 with a margin. Another
+      // target or MFMA shape needs its own count: the guard below stops the build, and the K9r-vs-K9s / oracle
+      // parity tests (every pq_len K9r serves, tests/test_gpu_parity.py::test_ivf_pq_k9r_mfma_lut_every_pq_len) catch a schedule that moves a store closer.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "K9r's MFMA -> LDS-store wait states are counted for gfx950"
+#endif
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);

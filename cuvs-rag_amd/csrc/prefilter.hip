@@ -1542,10 +1542,7 @@ int pf_hx_exp(float abs_max) {
   return e < -60 ? -60 : (e > 60 ? 60 : e);
 }
 
-bool pf_pair_mode() {
-  const char* pe = getenv("MIVS_PF_PAIR");
-  return !(pe && pe[0] == '0');
-}
+bool pf_pair_mode() { return true; }
 
 size_t pf_scan_lds_bytes(int dp, int chunk_groups) {
   const size_t b = (size_t)dp * kPfQTile * 2;
@@ -1565,8 +1562,8 @@ static hipError_t launch_pf_scan_md(const PfScanArgs& a, int grid, size_t lds, h
 
 template <int METRIC>
 static hipError_t launch_pf_scan_m(const PfScanArgs& a, int grid, size_t lds, hipStream_t s) {
-  // default: two groups per pass with 6-deep rings (half the LDS operand traffic per flop: the kernel is
-  // power-bound); MIVS_PF_PAIR=0: one group per pass with MIVS_PF_DEPTH (16) k-steps in flight
+  // two groups per pass with 6-deep rings (half the LDS operand traffic per flop: the kernel is power-bound,
+  // DESIGN.md §6b; one group per pass with a 16-deep ring measured slower and was retired in round 5)
   if (a.groups_f8) {  // fp8 nomination (pair mode): superblocks of 32 dims, a ring of 6 or 4
     const int nsb = a.dp / 32;
     if (a.q8 == nullptr || a.qscale8 == nullptr) return hipErrorInvalidValue;
@@ -1575,14 +1572,8 @@ static hipError_t launch_pf_scan_m(const PfScanArgs& a, int grid, size_t lds, hi
     return hipErrorInvalidValue;
   }
   const int nk = a.dp / 16;
-  if (pf_pair_mode()) {
-    if (a.rows_nt && nk % 6 == 0) return launch_pf_scan_md<METRIC, 6, 2, true>(a, grid, lds, s);
-    return nk % 6 == 0 ? launch_pf_scan_md<METRIC, 6, 2>(a, grid, lds, s) : launch_pf_scan_md<METRIC, 4, 2>(a, grid, lds, s);
-  }
-  const int dsel = getenv("MIVS_PF_DEPTH") ? atoi(getenv("MIVS_PF_DEPTH")) : 16;
-  if (dsel >= 16 && nk % 16 == 0) return launch_pf_scan_md<METRIC, 16, 1>(a, grid, lds, s);
-  if (dsel >= 8 && nk % 8 == 0) return launch_pf_scan_md<METRIC, 8, 1>(a, grid, lds, s);
-  return launch_pf_scan_md<METRIC, 4, 1>(a, grid, lds, s);
+  if (a.rows_nt && nk % 6 == 0) return launch_pf_scan_md<METRIC, 6, 2, true>(a, grid, lds, s);
+  return nk % 6 == 0 ? launch_pf_scan_md<METRIC, 6, 2>(a, grid, lds, s) : launch_pf_scan_md<METRIC, 4, 2>(a, grid, lds, s);
 }
 
 // grid: a multiple of 8 (one queue per XCD group); the work counters (8 x 16 ints) are zeroed by the caller

@@ -984,16 +984,14 @@ size_t rs_bucket_tmp_bytes(int nq, int n_waves) {
          scan_tmp_bytes(nq + 1) + 64;
 }
 
-// J: K13 workgroups per bucketing group (MIVS_RS_BUCKET_J, A/B runs: fewer means more groups and more global atomics
-// per query, more means fewer, longer groups); the streams come from K13's 8 item queues (n_waves = 8 queues x P
-// workgroups x kRsWaves) and a batch's bins fit LDS (K13 batches are at most kRsMaxBatch = kRsLdsMaxQ queries)
+// J: K13 workgroups per bucketing group (1: one K13 workgroup's 8 streams per LDS histogram; 2 and 4 measured slower
+// and were retired in round 5); the streams come from K13's 8 item queues (n_waves = 8 queues x P workgroups x
+// kRsWaves) and a batch's bins fit LDS (K13 batches are at most kRsMaxBatch = kRsLdsMaxQ queries)
 static int rs_bucket_groups(int n_waves, int nq, int* J_out) {
   const int P = n_waves / (8 * kRsWaves);
   if (!(nq <= kRsLdsMaxQ && n_waves == 8 * kRsWaves * P && P > 0)) return 0;
-  const char* je = getenv("MIVS_RS_BUCKET_J");
-  const int jw = je ? atoi(je) : 1;
-  *J_out = (jw >= 4 && P % 4 == 0) ? 4 : (jw >= 2 && P % 2 == 0) ? 2 : 1;
-  return 8 * (P / *J_out);
+  *J_out = 1;
+  return 8 * P;
 }
 
 template <int METRIC>

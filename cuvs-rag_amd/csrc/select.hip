@@ -550,20 +550,15 @@ hipError_t launch_select(const SelectArgs& a, hipStream_t s) {
   const bool expl = a.slot_info == nullptr;
   if (!expl && a.k <= 64 && a.slots_per_q * a.slot_rows <= 64 * kSmallPer) {  // K8s
     const dim3 grid((unsigned)ceil_div(a.nq, (int64_t)kSmallWaves)), block(64 * kSmallWaves);
-    const char* v2e = getenv("MIVS_SELECT_SMALL_V2");
-    const bool v2 = !(v2e && v2e[0] == '0');  // 122 -> 72 us for the coarse probe's 10k x 1024 keys
-    // (MIVS_SELECT_SMALL_FAST=0: the per-key slot decode everywhere)
-    const char* fe = getenv("MIVS_SELECT_SMALL_FAST");
-    const bool fast = (a.slot_rows & 63) == 0 && a.slots_per_q <= 64 && !(fe && fe[0] == '0');
-    if (v2 && fast) {
+    // (the threshold from the 64 lanes' minima: 122 -> 72 us for the coarse probe's 10k x 1024 keys; the bit search
+    // alone was retired in round 5)
+    const bool fast = (a.slot_rows & 63) == 0 && a.slots_per_q <= 64;  // slot-uniform key loads
+    if (fast) {
       if (a.metric == kIP) hipLaunchKernelGGL((k_select_small<kIP, true, true>), grid, block, 0, s, a);
       else hipLaunchKernelGGL((k_select_small<kL2, true, true>), grid, block, 0, s, a);
-    } else if (v2) {
+    } else {
       if (a.metric == kIP) hipLaunchKernelGGL((k_select_small<kIP, true, false>), grid, block, 0, s, a);
       else hipLaunchKernelGGL((k_select_small<kL2, true, false>), grid, block, 0, s, a);
-    } else {
-      if (a.metric == kIP) hipLaunchKernelGGL((k_select_small<kIP, false, false>), grid, block, 0, s, a);
-      else hipLaunchKernelGGL((k_select_small<kL2, false, false>), grid, block, 0, s, a);
     }
     return hipGetLastError();
   }

@@ -22,6 +22,19 @@ import torch
 logger = logging.getLogger(__name__)
 
 
+
+def even_split(total_items: int, parts: int) -> List[Tuple[int, int]]:
+    """The 'even' strategy's contiguous ranges [(start, end)] of [0, total_items) over `parts` shards: floor(N/P)
+    rows each, the first N mod P shards one more (reference gpu_resource_manager.py:190-202). bench.py's fixed-corpus
+    mode splits its corpus with it."""
+    base, extra = divmod(int(total_items), int(parts))
+    out, start = [], 0
+    for i in range(int(parts)):
+        end = start + base + (1 if i < extra else 0)
+        out.append((start, end))
+        start = end
+    return out
+
 @dataclass
 class GPUConfig:
     """One device as seen at discovery time (reference :21-28)."""
@@ -126,8 +139,7 @@ class GPUResourceManager:
             raise ValueError(f"Invalid total_items: {total_items}")
         gpus = self.available_gpus
         if strategy == "even":
-            base, extra = divmod(total_items, len(gpus))
-            sizes = [base + (1 if i < extra else 0) for i in range(len(gpus))]
+            sizes = [e - b for b, e in even_split(total_items, len(gpus))]
         elif strategy == "memory_based":
             mem = [self.gpu_memory_info[g]["available"] for g in gpus]
             total_mem = sum(mem)

@@ -107,10 +107,11 @@ class SearchConfig:
     timeout_seconds: Optional[float] = None
     validate_results: bool = True
     id_offsets: Optional[Dict[int, int]] = field(default=None)
-    # mivs extension: how per-shard tiles meet for the merge. "auto": RCCL all-gather across the GPUs
-    # of this process when there are several, the K7 merge alone for one; "rccl": always the RCCL
-    # exchange (also for one GPU); "peer": peer copies to the first GPU, then K7
-    exchange: str = "auto"
+    # mivs extension: how per-shard tiles meet for the merge. "peer" (default): device-to-device copies to the
+    # first GPU, then K7 -- the path the multi-GPU tests have run; "rccl": the RCCL all-gather across the GPUs of
+    # this process (ncclCommInitAll) + K7, opt-in until it has run on a multi-GPU node; "auto": "rccl" with several
+    # GPUs, the K7 merge alone for one
+    exchange: str = "peer"
     # mivs extension: also merge across torch.distributed ranks (a collective: every rank must search the
     # same query batch with the same k at the same point; see the module docstring). Default off.
     merge_across_ranks: bool = False

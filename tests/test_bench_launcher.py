@@ -67,3 +67,54 @@ def test_watchdog_reports_a_hang_and_an_error():
     r, e, hung = bench.run_with_watchdog(lambda: 7, 5)
     assert (r, e, hung) == (7, None, False)
     assert bench.EXIT_HUNG != 0
+
+
+def _bench_module(name):
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location(name, os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    return bench
+
+
+def test_launcher_deadline_kills_a_child_that_hangs_with_stdout_open():
+    """the deadline runs from the launch, stdout is read on a helper thread, and the whole process group
+    goes when it passes (a rank stuck in a collective keeps torch.distributed.run and its stdout alive)"""
+    bench = _bench_module("bench_mod3")
+    code = ("import subprocess, sys, time; print('rank output', flush=True); "
+            "subprocess.Popen([sys.executable, '-c', 'import time; time.sleep(60)']); time.sleep(60)")
+    t0 = time.perf_counter()
+    rc, line = bench.run_child([sys.executable, "-c", code], dict(os.environ), 2.0)
+    assert rc == 124 and line is None
+    assert time.perf_counter() - t0 < 20
+    # a child that finishes: its result line comes back, its status too
+    code = "import json; print('log'); print(json.dumps({'metric': 'm', 'value': 1}))"
+    rc, line = bench.run_child([sys.executable, "-c", code], dict(os.environ), 30.0)
+    assert rc == 0 and json.loads(line)["value"] == 1
+
+
+def test_corpus_modes_weak_and_strong():
+    """weak scaling: --rows per rank (configs[3] at N = 8); strong scaling: --rows-total split with the reference's
+    'even' rule (gpu_resource_manager.distribute_workload); `value` is full-corpus QPS in both (bench.py docstring)"""
+    bench = _bench_module("bench_mod4")
+
+    class A:
+        rows, rows_total = 10_000_000, 0
+    assert bench.corpus_shards(A, 8) == [(r * 10_000_000, (r + 1) * 10_000_000) for r in range(8)]
+    A.rows_total = 10_000_003
+    sh = bench.corpus_shards(A, 4)
+    assert sh[0] == (0, 2_500_001) and sh[-1][1] == 10_000_003
+    assert all(b == a_ for (_, a_), (b, _) in zip(sh[:-1], sh[1:]))
+    assert [e - b for b, e in sh] == [2_500_001, 2_500_001, 2_500_001, 2_500_000]
+    from gpu_resource_manager import GPUResourceManager, even_split
+
+    assert even_split(10, 3) == [(0, 4), (4, 7), (7, 10)]
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert "value = qps_full  # full-corpus QPS" in src and '"shard_searches_per_s"' in src
+
+
+def test_launcher_forwards_strong_scaling_flags():
+    j = _dry_run("--gpus", "4", "--rows-total", "10000000", "--steps", "3")
+    child = j["argv"][j["argv"].index(os.path.join(ROOT, "bench.py")) + 1:]
+    assert child[:6] == ["--gpus", "4", "--rows-total", "10000000", "--steps", "3"]

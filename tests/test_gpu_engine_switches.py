@@ -55,20 +55,13 @@ def _search(idx, q, k=10, n_probes=8):
 
 SEARCH_SWITCHES = [
     {"MIVS_PF_ROWSTAT": "0"},                                         # K10 instead of K13
-    {"MIVS_PF_ROWSTAT": "0", "MIVS_PF_PAIR": "0"},                    # K10 one group per pass (R = 1)
-    {"MIVS_PF_ROWSTAT": "0", "MIVS_PF_PAIR": "0", "MIVS_PF_DEPTH": "8"},
-    {"MIVS_PF_ROWSTAT": "0", "MIVS_PF_CONVOY": "0"},
-    {"MIVS_PF_ROWSTAT": "0", "MIVS_PF_SLOT_K": "16"},
     {"MIVS_RS_PRE_DIV": "1"},
     {"MIVS_RS_PRE_DIV": "16"},
     {"MIVS_RS_PRE_F8": "0"},                                          # pre-pass: the fp16 sample (round 2)
-    {"MIVS_SELECT_SMALL_V2": "0"},                                    # K8s by the bit search alone
     {"MIVS_RS_PRE_DIV": "1"},                                         # fp8 nomination over the whole list
-    {"MIVS_RS_PRE_STATS": "1"},                                       # pre-pass T_q stats (stderr only)
     {"MIVS_RS_FLAGS": "24"},                                          # K13 clocks (stderr only)
     {"MIVS_RS_WAVE_CAP": "2"},                                        # K13 streams overflow: the fallback
     {"MIVS_PF_ROWSTAT": "0", "MIVS_PF_FLAGS": "32"},                  # K10 phase clocks (stderr only)
-    {"MIVS_PF_SLOT_OUT": "0"},                                        # pre-pass merges whole slots
     {"MIVS_RS_BUCKET_1P": "0"},                                       # K13 bucketing: two-pass CSR runs
     {"MIVS_RS_QCAP": "4"},                                            # one-pass runs overflow: the fallback
 ]
@@ -84,22 +77,6 @@ def test_ivf_search_switch_same_bits(ivf, flat_data, monkeypatch, env):
     d1, i1 = _search(idx, q)
     np.testing.assert_array_equal(i1, i0)
     np.testing.assert_array_equal(_bits(d1), _bits(d0))
-
-
-def test_ivf_prepass_slot_out_same_candidates(ivf, flat_data, monkeypatch):
-    """the pre-pass merge stops after the nominees (MIVS_PF_SLOT_OUT): K11v takes the same rows, so T_q and with
-    it K13's candidate count are unchanged, not only the answer"""
-    idx, _ = ivf
-    _, q = flat_data
-    d0, i0 = _search(idx, q)
-    st0 = idx.last_search_stats()
-    monkeypatch.setenv("MIVS_PF_SLOT_OUT", "0")
-    d1, i1 = _search(idx, q)
-    st1 = idx.last_search_stats()
-    np.testing.assert_array_equal(i1, i0)
-    np.testing.assert_array_equal(_bits(d1), _bits(d0))
-    assert st0["scan_kernel"] == st1["scan_kernel"] == 13
-    assert st0["candidates"] == st1["candidates"]
 
 
 def test_ivf_one_pass_bucketing_same_candidates(ivf, flat_data, monkeypatch):
@@ -127,27 +104,6 @@ def test_ivf_default_matches_oracle(ivf, flat_data):
     np.testing.assert_array_equal(_bits(d), _bits(od))
 
 
-@pytest.mark.parametrize("env", [{"MIVS_PF_CHUNK_ROWS": "2048"}])
-def test_ivf_chunk_rows_switch_same_bits(ivf, flat_data, monkeypatch, env):
-    """work-item sizes are fixed when the fp16 copy is made (build / set_prefilter(True))"""
-    idx, _ = ivf
-    _, q = flat_data
-    d0, i0 = _search(idx, q)
-    for kk, v in env.items():
-        monkeypatch.setenv(kk, v)
-    idx.set_prefilter(False)
-    idx.set_prefilter(True)
-    try:
-        d1, i1 = _search(idx, q)
-    finally:
-        for kk in env:
-            monkeypatch.delenv(kk)
-        idx.set_prefilter(False)
-        idx.set_prefilter(True)
-    np.testing.assert_array_equal(i1, i0)
-    np.testing.assert_array_equal(_bits(d1), _bits(d0))
-
-
 @pytest.mark.parametrize("k,env", [(10, {"MIVS_SCAN_WIDE": "0"}), (10, {"MIVS_SCAN_WIDE_WAVES": "8"}),
                                    (100, {"MIVS_SCAN_WAVES": "8"})])
 def test_exact_scan_switch_same_bits(ivf, flat_data, monkeypatch, k, env):
@@ -167,17 +123,15 @@ def test_exact_scan_switch_same_bits(ivf, flat_data, monkeypatch, k, env):
 
 
 def test_build_assign_switches_same_index(flat_data, mivs_lib, monkeypatch):
-    """the build's assign through K13a (default), through K12 (MIVS_PF_ASSIGN_RS=0), through K10
-    (MIVS_PF_ASSIGN_RS=0 MIVS_PF_ASSIGN_REG=0) and in fp32 (MIVS_PF_ASSIGN=0): the same centroids, list sizes
-    and list order"""
+    """the build's assign through K13a (default), through K12 (MIVS_PF_ASSIGN_RS=0) and in fp32 (MIVS_PF_ASSIGN=0):
+    the same centroids, list sizes and list order"""
     from mivs.neighbors import ivf_flat
 
     x, _ = flat_data
     xt = torch.from_numpy(x).cuda()
     p = ivf_flat.IndexParams(n_lists=48, kmeans_n_iters=4)
     ref = ivf_flat.build(p, xt)
-    for env in ({"MIVS_PF_ASSIGN_RS": "0"}, {"MIVS_PF_ASSIGN_RS": "0", "MIVS_PF_ASSIGN_REG": "0"},
-                {"MIVS_PF_ASSIGN": "0"}):
+    for env in ({"MIVS_PF_ASSIGN_RS": "0"}, {"MIVS_PF_ASSIGN": "0"}):
         for kk, v in env.items():
             monkeypatch.setenv(kk, v)
         other = ivf_flat.build(p, xt)
@@ -231,10 +185,10 @@ def test_prefilter_default_switch(flat_data, mivs_lib, monkeypatch):
 
 
 @pytest.mark.parametrize("k", [10, 40])
-@pytest.mark.parametrize("env", [{"MIVS_PQ_RT": "0"}, {"MIVS_PQ_RT": "0", "MIVS_PQ_ORDER": "0"},
-                                 {"MIVS_PQ_RT": "0", "MIVS_PQ_SPLIT": "0"}, {"MIVS_PQ_RT": "0", "MIVS_PQ_TILED": "1"}])
+@pytest.mark.parametrize("env", [{"MIVS_PQ_RT": "0"}, {"MIVS_PQ_RT": "0", "MIVS_PQ_SPLIT": "0"},
+                                 {"MIVS_PQ_RT": "0", "MIVS_PQ_TILED": "1"}])
 def test_ivf_pq_switch_same_bits(mivs_lib, monkeypatch, k, env):
-    """IVF-PQ: K9r (default) vs K9s, its slot order, K9 vs K9s, K9b (tiled; k <= 32 there): the same bits"""
+    """IVF-PQ: K9r (default) vs K9s, K9 vs K9s, K9b (tiled; k <= 32 there): the same bits"""
     from mivs.neighbors import ivf_pq
 
     if env.get("MIVS_PQ_TILED") == "1" and k > 32:
@@ -255,32 +209,22 @@ def test_ivf_pq_switch_same_bits(mivs_lib, monkeypatch, k, env):
     idx.close()
 
 
-@pytest.mark.parametrize("n_probes,env", [(17, {"MIVS_COARSE_DUMP": "0"}),
-                                           (32, {"MIVS_COARSE_DUMP": "0"}),
-                                           (32, {"MIVS_SELECT_SMALL_V2": "0"}),
-                                           (48, {"MIVS_COARSE_DUMP": "0"}),
-                                           (32, {"MIVS_DUMP_WIDE": "0"}),           # coarse DUMP on K3, not K3w
-                                           (48, {"MIVS_DUMP_WIDE": "0"}),
-                                           (32, {"MIVS_SELECT_SMALL_FAST": "0"})])
-def test_coarse_probe_switches_same_bits(ivf, flat_data, monkeypatch, n_probes, env):
-    """the coarse probe through K3 DUMP + K8s (the default above 16 probes) and through K3's register top-k
-    (MIVS_COARSE_DUMP=0), K8s with the bit search alone: the same probes (order and ids) and the same search
-    result"""
+@pytest.mark.parametrize("n_probes", [16, 17, 32, 48])
+def test_coarse_probe_equals_oracle(ivf, flat_data, n_probes):
+    """the coarse probe -- K3's register top-k up to 16 probes, K3w DUMP + K8s above (slot-uniform key loads, the
+    threshold from the lanes' minima) -- gives the oracle's probes in order, and the search its answer"""
     from mivs.neighbors import ivf_flat
 
-    idx, _ = ivf
-    _, q = flat_data
+    idx, metric = ivf
+    x, q = flat_data
     qd = torch.from_numpy(q).cuda()
-    sp = ivf_flat.SearchParams(n_probes=n_probes)
     p0 = torch.empty((q.shape[0], n_probes), dtype=torch.int32, device="cuda")
-    d0, i0 = ivf_flat.search(sp, idx, qd, 10, probes_out=p0)
-    for kk, v in env.items():
-        monkeypatch.setenv(kk, v)
-    p1 = torch.empty_like(p0)
-    d1, i1 = ivf_flat.search(sp, idx, qd, 10, probes_out=p1)
-    np.testing.assert_array_equal(p1.cpu().numpy(), p0.cpu().numpy())
-    np.testing.assert_array_equal(i1.cpu().numpy(), i0.cpu().numpy())
-    np.testing.assert_array_equal(_bits(d1.cpu().numpy()), _bits(d0.cpu().numpy()))
+    d0, i0 = ivf_flat.search(ivf_flat.SearchParams(n_probes=n_probes), idx, qd, 10, probes_out=p0)
+    od, oi, op = O.ivf_search(x, idx.centers.cpu().numpy(), idx.list_sizes.numpy(), idx.list_ids().cpu().numpy(), q,
+                              n_probes, 10, metric=metric)
+    np.testing.assert_array_equal(p0.cpu().numpy(), op)
+    np.testing.assert_array_equal(i0.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(d0.cpu().numpy()), _bits(od))
 
 
 def test_k13_lost_stream_fallback_is_exact_and_reported(ivf, flat_data, monkeypatch):

@@ -95,7 +95,7 @@ def test_large_k_prefilter_bitexact_vs_oracle_and_exact(mivs_lib, built, monkeyp
 
 @pytest.mark.parametrize("env", [{"MIVS_LK_SAMPLE_DIV": "1"}, {"MIVS_LK_SAMPLE_DIV": "7"},
                                  {"MIVS_LK_SAMPLE_DIV": "100000"}, {"MIVS_RS_WAVE_CAP": "2"},
-                                 {"MIVS_LK_WORKSPACE_MB": "1"}, {"MIVS_RS_PRE_STATS": "1"}],
+                                 {"MIVS_LK_WORKSPACE_MB": "1"}],
                          ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_large_k_switches_same_bits(mivs_lib, built, monkeypatch, env):
     """the whole list as the sample (T_q from the exact k-th: every query provable), a 1/7 sample, a one-group

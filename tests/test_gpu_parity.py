@@ -420,6 +420,17 @@ def test_ivf_pq_register_lists_bitexact(mivs_lib, monkeypatch, case):
     _pq_case(*case)
 
 
+@pytest.mark.parametrize("pq_len", [4, 8, 12, 16])
+def test_ivf_pq_k9r_mfma_lut_every_pq_len(mivs_lib, monkeypatch, pq_len):
+    """K9r builds each LUT on v_mfma_f32_16x16x4_f32 and stores the results to LDS after hand-counted wait states
+    (pq.hip): for every pq_len it serves (pq_rt_supported: 4, 8, 12, 16) its search equals the oracle and
+    K9s (MIVS_PQ_RT=0) bit for bit, so a toolchain that schedules a store closer to its MFMA fails here"""
+    pq_dim = 8
+    _pq_case(3000, pq_dim * pq_len, 8, pq_dim, 2, 24, 4, 10)
+    monkeypatch.setenv("MIVS_PQ_RT", "0")
+    _pq_case(3000, pq_dim * pq_len, 8, pq_dim, 2, 24, 4, 10)
+
+
 def _pq_case(n, d, n_lists, pq_dim, iters, nq, n_probes, k):
     from mivs.neighbors import ivf_pq
 

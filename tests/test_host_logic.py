@@ -97,7 +97,9 @@ def test_merge_search_results_inner_product_without_engine(monkeypatch):
 
 
 def test_search_config_exchange_switch():
-    assert sra.SearchConfig(k=5).exchange == "auto"
+    # (peer copies + K7 by default: the RCCL exchange stays opt-in until ncclCommInitAll has run on a multi-GPU node)
+    assert sra.SearchConfig(k=5).exchange == "peer"
+    assert sra.SearchConfig(k=5, exchange="auto").exchange == "auto"
     assert sra.SearchConfig(k=5, exchange="rccl").exchange == "rccl"
     with pytest.raises(ValueError, match="exchange"):
         sra.SearchConfig(k=5, exchange="nccl2")
