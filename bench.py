@@ -403,6 +403,34 @@ def large_k_side_line(a, idx, q, rl, scanned_rows):
     return out
 
 
+def build_roofline(kern, t_build):
+    """The build's hot kernels against their peaks (device time by hipEvents during the timed build, algorithmic work
+    per launch from the engine: mivs_index_build_kernels): k_as_scan (the k-means assign, per iteration, and the final
+    assign of every row) in TFLOP/s against the fp16 MFMA peak -- the assign runs through the fp16 pre-filter, the
+    labels are the fp32 ones -- and the byte-moving kernels (K5's centroid update, K6's pack, the fp16
+    and fp8 copies) in GB/s against HBM."""
+    out = {}
+    for name, v in kern.items():
+        if v["calls"] == 0 or v["ms"] <= 0:
+            continue
+        rate = v["work"] / (v["ms"] * 1e-3)
+        line = {"launches": v["calls"], "ms_total": round(v["ms"], 3), "ms_per_launch": round(v["ms"] / v["calls"], 4)}
+        if v["unit"] == "flop":
+            line.update({"bound": "mfma", "achieved": round(rate / 1e12, 2), "peak": PEAK_F16_MFMA_TFS,
+                         "unit": "TFLOP/s", "frac": round(rate / 1e12 / PEAK_F16_MFMA_TFS, 4),
+                         "flops_per_launch": v["work"] / v["calls"]})
+        else:
+            line.update({"bound": "hbm", "achieved": round(rate / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(rate / 1e9 / PEAK_HBM_GBS, 4), "bytes_per_launch": v["work"] / v["calls"]})
+        out[name] = line
+    if out:
+        tot = sum(v["ms_total"] for v in out.values())
+        out["kernels_ms_total"] = round(tot, 3)
+        out["kernels_share_of_build"] = round(tot / (t_build * 1e3), 4)
+        out["timing"] = "hipEvents around each launch on the build stream (profiling on during the timed build)"
+    return out
+
+
 def latency_side_line(a, idx, q, rl):
     """The reference's own search shape (improved_multi_gpu_rag.py:209-237 search_on_gpu, :279-303 batch_search: one
     query per call; cuvs-2gpu-main.ipynb:1789-1836): per-call wall time of ivf_flat.search at small batches, each call
@@ -831,6 +859,7 @@ def main():
     t_build = max_over_ranks(time.perf_counter() - t0, world, dev)
     _native.set_profiling(False)
     build_phases = idx.build_phases()
+    build_roof = build_roofline(idx.build_kernels(), t_build)
     build_vps = rows_total / t_build
     index_mem = idx.memory()  # one fp32 copy (64-B row blocks) + the fp16 and fp8 copies, all built in build()
     sizes = idx.list_sizes.numpy()
@@ -1068,6 +1097,7 @@ def main():
         "build_vectors_per_s": round(build_vps, 1),
         "build_s": round(t_build, 3),
         "build_phases_s": build_phases,
+        "build_roofline": build_roof,
         "index_bytes_per_row": round(index_mem["total_bytes"] / max(index_mem["n_rows"], 1), 1),
         "index_memory": index_mem,
         "roofline": roof,

@@ -32,6 +32,58 @@ using namespace mivs_capi;
 
 namespace {
 
+// hipEvent pairs around the build's hot kernels while profiling is on (the build's phase clock syncs the stream
+// anyway): k_as_scan per k-means iteration and for the final assign (flops), K5's update, K6's pack and the fp16 / fp8
+// copies (bytes). Set per build on the building thread (ParallelIndexBuilder builds one index per thread).
+struct BuildProf {
+  struct Rec {
+    int kind;
+    double work;
+    hipEvent_t e0, e1;
+  };
+  std::vector<Rec> recs;
+  int assign_kind = MIVS_BUILD_KMEANS_ASSIGN;  // the assign the build is in: k-means iterations, then the final
+  ~BuildProf() {
+    for (auto& r : recs) {
+      (void)hipEventDestroy(r.e0);
+      (void)hipEventDestroy(r.e1);
+    }
+  }
+  size_t begin(int kind, double work, hipStream_t s) {
+    Rec r{kind, work, nullptr, nullptr};
+    HIPCHK(hipEventCreate(&r.e0));
+    HIPCHK(hipEventCreate(&r.e1));
+    HIPCHK(hipEventRecord(r.e0, s));
+    recs.push_back(r);
+    return recs.size() - 1;
+  }
+  void end(size_t i, hipStream_t s) { HIPCHK(hipEventRecord(recs[i].e1, s)); }
+  // (the stream synchronized) -> per kind {calls, ms, work}
+  void collect(mivs_build_kernel* out) {
+    for (int k = 0; k < MIVS_BUILD_KERNEL_KINDS; ++k) out[k] = mivs_build_kernel{k, 0, 0.0, 0.0};
+    for (auto& r : recs) {
+      float ms = 0.0f;
+      HIPCHK(hipEventElapsedTime(&ms, r.e0, r.e1));
+      out[r.kind].calls += 1;
+      out[r.kind].ms += ms;
+      out[r.kind].work += r.work;
+    }
+  }
+};
+thread_local BuildProf* g_bprof = nullptr;
+
+// one timed build kernel (no-op unless a profiled build is running on this thread)
+struct BuildTimer {
+  size_t i = 0;
+  hipStream_t s;
+  BuildTimer(int kind, double work, hipStream_t s_) : s(s_) {
+    if (g_bprof) i = g_bprof->begin(kind, work, s);
+  }
+  ~BuildTimer() {
+    if (g_bprof) g_bprof->end(i, s);
+  }
+};
+
 // A set of inverted lists in the interleaved group layout.
 struct ListSet {
   int n_lists = 0;
@@ -75,9 +127,13 @@ void pack_lists(ListSet& ls, const float* src, int d, int dp, const int64_t* per
     group_list.reserve(sizeof(int) * (size_t)std::max<int64_t>(ls.n_groups, 1));
     HIPCHK(launch_group_list(ls.goff.as<int64_t>(), ls.n_lists, ls.n_groups, group_list.as<int>(), s));
   }
-  HIPCHK(launch_pack_groups(src, 0, d, dp, perm_d, ls.off.as<int64_t>(), ls.goff.as<int64_t>(),
-                            ls.n_lists > 1 ? group_list.as<int>() : nullptr, ls.n_groups, ls.groups.as<float>(),
-                            ls.norms.as<float>(), ls.ids.as<int64_t>(), id_map, id_offset, s));
+  {
+    // (each row read once, written once in its list's group layout, plus its norm and id)
+    BuildTimer bt(MIVS_BUILD_PACK, (double)ls.n_rows * ((double)d * 4 + (double)dp * 4 + 12), s);
+    HIPCHK(launch_pack_groups(src, 0, d, dp, perm_d, ls.off.as<int64_t>(), ls.goff.as<int64_t>(),
+                              ls.n_lists > 1 ? group_list.as<int>() : nullptr, ls.n_groups, ls.groups.as<float>(),
+                              ls.norms.as<float>(), ls.ids.as<int64_t>(), id_map, id_offset, s));
+  }
   ls.finalize_host(G);
   HIPCHK(hipStreamSynchronize(s));  // host vectors above are referenced by the async copies
 }
@@ -165,6 +221,8 @@ struct mivs_index_s {
   int64_t last_ovf = 0, last_window = 0;
   // host wall time of the build's phases (mivs_index_build_phases; recorded while profiling is on)
   std::vector<double> build_phase_s;
+  // device time and algorithmic work of the build's hot kernels (mivs_index_build_kernels; profiling on)
+  mivs_build_kernel build_kern[MIVS_BUILD_KERNEL_KINDS] = {};
 };
 
 namespace {
@@ -447,7 +505,10 @@ void as_assign_rows(const PfAssign& P, const float* data, const float* data_norm
   a.ovf_rows = ws.ovf_q.as<int64_t>();
   a.queue = cnt.as<int>() + 2;
   a.flags = env_int("MIVS_AS_FLAGS", 0);
-  HIPCHK(launch_as_scan(a, cu_count(device), s));
+  {
+    BuildTimer bt(g_bprof ? g_bprof->assign_kind : 0, 2.0 * (double)nr * (double)cents.n_rows * d, s);
+    HIPCHK(launch_as_scan(a, cu_count(device), s));
+  }
   int h[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(h, cnt.p, 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
@@ -669,8 +730,11 @@ void kmeans_fit_impl(const float* data, const float* data_norms, const int64_t* 
       HIPCHK(hipMemcpyAsync(labels_out, labels.p, sizeof(int64_t) * n_train, hipMemcpyDeviceToDevice, s));
     HIPCHK(launch_counting_sort(labels.as<int64_t>(), n_train, nc, perm.as<int64_t>(), off.as<int64_t>(), ctmp.p,
                                 cb, s));
-    HIPCHK(launch_km_update(data, d, rows, perm.as<int64_t>(), off.as<int64_t>(), nc, n_train,
-                            partial.as<double>(), chunk_off.as<int64_t>(), tmp.p, centroids_rm, s));
+    {
+      BuildTimer bt(MIVS_BUILD_KMEANS_UPDATE, (double)n_train * d * 4.0, s);  // (each member row read once)
+      HIPCHK(launch_km_update(data, d, rows, perm.as<int64_t>(), off.as<int64_t>(), nc, n_train,
+                              partial.as<double>(), chunk_off.as<int64_t>(), tmp.p, centroids_rm, s));
+    }
     if (balance && it < it_total - kBalanceKeepLast)
       HIPCHK(launch_km_rebalance(data, d, rows, labels.as<int64_t>(), off.as<int64_t>(), nc, n_train, it,
                                  centroids_rm, s));
@@ -741,6 +805,7 @@ void pf_build_f8(mivs_index_s* idx, hipStream_t s) {
   }
   idx->hx8 = idx->hx_exp - 7;  // |x| max 2^hx_exp in [2^14, 2^15) -> [128, 256) under e4m3's 448
   idx->groups_f8.reserve(bytes);
+  BuildTimer bt(MIVS_BUILD_FP8_COPY, (double)bytes * 5.0, s);  // (fp32 read, fp8 written)
   HIPCHK(launch_groups_to_f8(L.groups.as<float>(), L.n_groups, idx->dp, idx->hx8, idx->groups_f8.as<uint8_t>(), s));
 }
 
@@ -792,8 +857,11 @@ void pf_enable(mivs_index_s* idx, hipStream_t s) {
   idx->groups_h.reserve(sizeof(uint16_t) * (size_t)nslot * idx->dp);
   idx->group_nmin.reserve(sizeof(float) * (size_t)L.n_groups);
   HIPCHK(launch_group_nmin(L.norms.as<float>(), L.n_groups, idx->group_nmin.as<float>(), s));
-  HIPCHK(launch_groups_to_half(L.groups.as<float>(), L.n_groups, idx->dp, idx->hx_exp, idx->groups_h.as<uint16_t>(),
-                               st.as<unsigned>() + 2, s));
+  {
+    BuildTimer bt(MIVS_BUILD_FP16_COPY, (double)nslot * idx->dp * 6.0, s);  // (fp32 read, fp16 written)
+    HIPCHK(launch_groups_to_half(L.groups.as<float>(), L.n_groups, idx->dp, idx->hx_exp,
+                                 idx->groups_h.as<uint16_t>(), st.as<unsigned>() + 2, s));
+  }
   HIPCHK(hipMemcpyAsync(&h[2], st.as<unsigned>() + 2, sizeof(unsigned), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   float resmax;
@@ -1814,6 +1882,12 @@ int32_t mivs_ivf_flat_build(int32_t device, void* stream, const float* d_data, i
       idx->build_phase_s.push_back(std::chrono::duration<double>(t1 - t_ph).count());
       t_ph = t1;
     };
+    // (profiling: the hot kernels' hipEvents, collected after the last phase)
+    std::unique_ptr<BuildProf> bprof(clk ? new BuildProf() : nullptr);
+    struct ProfScope {
+      ProfScope(BuildProf* p) { g_bprof = p; }
+      ~ProfScope() { g_bprof = nullptr; }
+    } prof_scope(bprof.get());
     PfAssign pfa;  // the data's fp16 copy: k-means assign + list fill through the pre-filter
     pf_assign_prepare(pfa, d_data, n, dim, idx->dp, s);
     phase();
@@ -1821,6 +1895,7 @@ int32_t mivs_ivf_flat_build(int32_t device, void* stream, const float* d_data, i
                     idx->centroids_rm.as<float>(), idx->G, device, idx->ws, s, p->kmeans_balance != 0, &pfa);
     make_single_list(idx->cents, idx->centroids_rm.as<float>(), nl, dim, idx->dp, 0, idx->G, s);
     phase();
+    if (bprof) bprof->assign_kind = MIVS_BUILD_FINAL_ASSIGN;
     if (p->add_data_on_build) {
       build_lists(idx.get(), d_data, norms.as<float>(), n, s, &pfa);
     } else {
@@ -1830,6 +1905,7 @@ int32_t mivs_ivf_flat_build(int32_t device, void* stream, const float* d_data, i
     if (p->prefilter && pf_default_on()) pf_enable(idx.get(), s);
     phase();
     HIPCHK(hipStreamSynchronize(s));
+    if (bprof) bprof->collect(idx->build_kern);
     *out = idx.release();
   });
 }
@@ -2620,6 +2696,18 @@ int32_t mivs_index_memory_info(mivs_index_t idx, mivs_index_memory* out) {
     require(idx != nullptr && out != nullptr, "NULL argument");
     std::lock_guard<std::mutex> g(idx->mu);
     *out = index_memory(idx);
+  });
+}
+
+int32_t mivs_index_build_kernels(mivs_index_t idx, mivs_build_kernel* out, int32_t n_max, int32_t* n_out) {
+  return guarded([&] {
+    require(idx != nullptr, "index is NULL");
+    int n = 0;
+    for (int k = 0; k < MIVS_BUILD_KERNEL_KINDS && k < n_max; ++k) {
+      if (out) out[k] = idx->build_kern[k];
+      ++n;
+    }
+    if (n_out) *n_out = n;
   });
 }
 

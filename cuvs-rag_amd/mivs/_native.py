@@ -127,6 +127,16 @@ class Profile(ctypes.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class BuildKernel(ctypes.Structure):
+    """mivs_build_kernel (include/mivs.h): one hot kernel kind of an ivf_flat build, profiled"""
+    _fields_ = [("kind", c_int32), ("calls", c_int32), ("ms", ctypes.c_double), ("work", ctypes.c_double)]
+
+
+# kinds of mivs_index_build_kernels: (name, unit of `work`)
+BUILD_KERNELS = (("kmeans_assign", "flop"), ("final_assign", "flop"), ("kmeans_update", "byte"), ("pack", "byte"),
+                 ("fp16_copy", "byte"), ("fp8_copy", "byte"))
+
+
 _SIGS = {
     "mivs_last_error": (ctypes.c_char_p, []),
     "mivs_version": (c_int32, []),
@@ -160,6 +170,7 @@ _SIGS = {
     "mivs_index_memory_info": (c_int32, [c_void_p, POINTER(IndexMemory)]),
     "mivs_index_profile_collect": (c_int32, [c_void_p, POINTER(Profile)]),
     "mivs_index_build_phases": (c_int32, [c_void_p, c_void_p, c_int32, POINTER(c_int32)]),
+    "mivs_index_build_kernels": (c_int32, [c_void_p, POINTER(BuildKernel), c_int32, POINTER(c_int32)]),
     "mivs_index_set_prefilter": (c_int32, [c_void_p, c_void_p, c_int32]),
     "mivs_index_get_prefilter": (c_int32, [c_void_p, POINTER(c_int32)]),
     "mivs_index_free": (None, [c_void_p]),
@@ -255,6 +266,17 @@ def profiling() -> bool:
 
 BUILD_PHASES = {0: ("prepare", "coarse_kmeans", "assign_pack", "fp16_copy"),
                 2: ("prepare", "coarse_kmeans", "assign_sort", "codebooks", "encode")}
+
+
+def build_kernels(handle) -> dict:
+    """{kind: {calls, ms, work, unit}} of an ivf_flat build's hot kernels (device time by hipEvents; recorded only while
+    profiling was on during the build)"""
+    n_max = len(BUILD_KERNELS)
+    buf = (BuildKernel * n_max)()
+    n = c_int32(0)
+    check(lib().mivs_index_build_kernels(handle, buf, n_max, ctypes.byref(n)))
+    return {BUILD_KERNELS[i][0]: {"calls": int(buf[i].calls), "ms": float(buf[i].ms), "work": float(buf[i].work),
+                                  "unit": BUILD_KERNELS[i][1]} for i in range(min(n.value, n_max))}
 
 
 def build_phases(handle, kind: int) -> dict:

@@ -171,6 +171,10 @@ class Index:
             ph = {"to_fp32": round(self._to_f32_s, 4), **ph}
         return ph
 
+    def build_kernels(self) -> dict:
+        """Device time and algorithmic work of this index's build kernels (recorded only while profiling was on)."""
+        return _native.build_kernels(self.handle)
+
     def profile_collect(self) -> dict:
         """Device time of the searches since the last collect (needs mivs._native.set_profiling(True))."""
         pr = _native.Profile()

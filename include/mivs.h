@@ -177,6 +177,26 @@ int32_t mivs_index_profile_collect(mivs_index_t index, mivs_profile* out);
  * between phases): ivf_flat {prepare, coarse k-means, assign + pack, fp16 copy}; ivf_pq {prepare, coarse
  * k-means, assign + sort, codebooks, encode}. *n_out = phases recorded (0: profiling was off). */
 int32_t mivs_index_build_phases(mivs_index_t index, double* out_s, int32_t n_max, int32_t* n_out);
+/* device time (hipEvents) and algorithmic work of an ivf_flat build's hot kernels, recorded when profiling was on
+ * during the build (the build's roofline): per kind its launches, summed ms and work -- flops for the
+ * assign scans (2 x rows x centroids x dim per launch), bytes for the rest. Replaces no reference call: it reports on
+ * ivf_flat.build (index_building_coordinator.py:392-396). out[k] for k < min(n_max, MIVS_BUILD_KERNEL_KINDS). */
+enum {
+  MIVS_BUILD_KMEANS_ASSIGN = 0, /* k_as_scan (K13a) in the k-means iterations: flops */
+  MIVS_BUILD_FINAL_ASSIGN = 1,  /* k_as_scan for the final assign of every row: flops */
+  MIVS_BUILD_KMEANS_UPDATE = 2, /* K5 k_km_partial + k_km_final: bytes (member rows read once) */
+  MIVS_BUILD_PACK = 3,          /* K6 k_pack: bytes (rows read, written in the group layout, norms, ids) */
+  MIVS_BUILD_FP16_COPY = 4,     /* k_groups_to_half: bytes */
+  MIVS_BUILD_FP8_COPY = 5,      /* k_groups_to_f8: bytes */
+  MIVS_BUILD_KERNEL_KINDS = 6
+};
+typedef struct {
+  int32_t kind;
+  int32_t calls;
+  double ms;
+  double work;
+} mivs_build_kernel;
+int32_t mivs_index_build_kernels(mivs_index_t index, mivs_build_kernel* out, int32_t n_max, int32_t* n_out);
 /* keep (1) or drop (0) the fp16 copy of the lists that the pre-filter search uses (ivf_flat, brute force).
  * Results are identical either way (the refine recomputes every candidate that can reach the top-k in
  * the pinned fp32 order); the copy costs 2 bytes per padded dimension per row of HBM. */

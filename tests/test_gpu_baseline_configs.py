@@ -105,6 +105,14 @@ def ivf_10m():
     torch.cuda.empty_cache()
 
 
+@pytest.fixture(scope="module")
+def x10m_host(ivf_10m):
+    """the 10M corpus on the host, copied once for every oracle comparison of the module (30.7 GB)"""
+    xh = ivf_10m[0].cpu().numpy()
+    yield xh
+    del xh
+
+
 def test_config2_ivf_10m_prefilter_equals_exact_all_queries(ivf_10m):
     from mivs.neighbors import ivf_flat
 
@@ -128,7 +136,7 @@ def test_config2_ivf_10m_prefilter_equals_exact_all_queries(ivf_10m):
     assert (np.diff(dd, axis=1) >= 0).all()
 
 
-def test_config2_ivf_10m_oracle_on_query_sample(ivf_10m):
+def test_config2_ivf_10m_oracle_on_query_sample(ivf_10m, x10m_host):
     from mivs.neighbors import ivf_flat
 
     x, q, idx = ivf_10m
@@ -136,15 +144,38 @@ def test_config2_ivf_10m_oracle_on_query_sample(ivf_10m):
     qs = q[torch.from_numpy(s).to("cuda:0")]
     probes = torch.empty((len(s), 32), dtype=torch.int32, device="cuda:0")
     d, i = ivf_flat.search(ivf_flat.SearchParams(n_probes=32), idx, qs, 10, probes_out=probes)
-    xh = x.cpu().numpy()
-    od, oi, op = O.ivf_search(xh, idx.centers.cpu().numpy(), idx.list_sizes.numpy(), idx.list_ids().cpu().numpy(),
+    od, oi, op = O.ivf_search(x10m_host, idx.centers.cpu().numpy(), idx.list_sizes.numpy(), idx.list_ids().cpu().numpy(),
                               qs.cpu().numpy(), 32, 10)
     np.testing.assert_array_equal(probes.cpu().numpy(), op)
     np.testing.assert_array_equal(i.cpu().numpy(), oi)
     np.testing.assert_array_equal(_bits(d.cpu().numpy()), _bits(od))
 
 
-def test_config2_ivf_10m_large_k_equals_exact_all_queries_and_oracle_sample(ivf_10m):
+@pytest.mark.parametrize("nq", [1, 7])
+def test_config2_ivf_10m_small_batches_equal_oracle(ivf_10m, x10m_host, nq):
+    """the reference's own search shape (one query per call: improved_multi_gpu_rag.py:209-237,279-303;
+    cuvs-2gpu-main.ipynb:1789-1836) and a ragged small batch at configs[2]: probes, ids and distance bits equal the
+    oracle, and the rows of the full 10k batch's answer"""
+    from mivs.neighbors import ivf_flat
+
+    x, q, idx = ivf_10m
+    s = _sample(q.shape[0], nq, 11 + nq)
+    qs = q[torch.from_numpy(s).to("cuda:0")]
+    sp = ivf_flat.SearchParams(n_probes=32)
+    probes = torch.empty((nq, 32), dtype=torch.int32, device="cuda:0")
+    d, i = ivf_flat.search(sp, idx, qs, 10, probes_out=probes)
+    assert idx.last_search_stats()["n_queries"] == nq
+    od, oi, op = O.ivf_search(x10m_host, idx.centers.cpu().numpy(), idx.list_sizes.numpy(),
+                              idx.list_ids().cpu().numpy(), qs.cpu().numpy(), 32, 10)
+    np.testing.assert_array_equal(probes.cpu().numpy(), op)
+    np.testing.assert_array_equal(i.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(d.cpu().numpy()), _bits(od))
+    df, i_full = ivf_flat.search(sp, idx, q, 10)
+    np.testing.assert_array_equal(i.cpu().numpy(), i_full.cpu().numpy()[s])
+    np.testing.assert_array_equal(_bits(d.cpu().numpy()), _bits(df.cpu().numpy()[s]))
+
+
+def test_config2_ivf_10m_large_k_equals_exact_all_queries_and_oracle_sample(ivf_10m, x10m_host):
     """the reference's top_k = 2000 (improved_multi_gpu_rag.py:40,247) at configs[2]: K13 + K16 on
     all 10k queries bit-equal to the exact fp32 path (K3 DUMP + K8), and a query sample bit-equal to the oracle"""
     from mivs.neighbors import ivf_flat
@@ -165,8 +196,7 @@ def test_config2_ivf_10m_large_k_equals_exact_all_queries_and_oracle_sample(ivf_
     np.testing.assert_array_equal(i_pf.cpu().numpy(), i_ex.cpu().numpy())
     np.testing.assert_array_equal(_bits(d_pf.cpu().numpy()), _bits(d_ex.cpu().numpy()))
     s = _sample(q.shape[0], 12, 5)
-    xh = x.cpu().numpy()
-    od, oi, _ = O.ivf_search(xh, idx.centers.cpu().numpy(), idx.list_sizes.numpy(), idx.list_ids().cpu().numpy(),
+    od, oi, _ = O.ivf_search(x10m_host, idx.centers.cpu().numpy(), idx.list_sizes.numpy(), idx.list_ids().cpu().numpy(),
                              q.cpu().numpy()[s], 32, k)
     np.testing.assert_array_equal(i_pf.cpu().numpy()[s], oi)
     np.testing.assert_array_equal(_bits(d_pf.cpu().numpy()[s]), _bits(od))
