@@ -76,6 +76,8 @@ def parse():
                     help="side line: per-call latency of searches of this many queries (the reference searches one "
                          "query per call); '' to skip")
     ap.add_argument("--latency-probes", default="32,20", help="n_probes of the latency side line (20: cuVS default)")
+    ap.add_argument("--batch-sweep", default="1000,5000,20000,32768",
+                    help="side line: QPS at these query batch sizes (the headline's batch is --queries); '' to skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--flat-rows", type=int, default=1_000_000,
                     help="BASELINE configs[1] side line: brute force over this many rows (0: skip)")
@@ -397,6 +399,9 @@ def large_k_side_line(a, idx, q, rl, scanned_rows):
                     "rest_ms_per_search": round(t * 1e3 - scan_ms, 3),
                     "candidates": st["candidates"], "window_rows": st["window_candidates"],
                     "window_gather_gb": round(win_bytes / 1e9, 2), "unproven_queries": st["overflow_queries"],
+                    # last_search_stats() describes the last query batch of a search (ivf_search_impl splits the
+                    # batch when the K16 workspace cannot hold every query's window)
+                    "stats_scope": "whole search" if batches == 1 else f"last of {batches} query batches",
                     "exact_path_qps": round(q.shape[0] / t_ex, 1), "equal_to_exact_path": same, "well_formed": ok})
         rl(f"[large-k] k={kk}: {q.shape[0] / t:,.0f} QPS ({t * 1e3:.1f} ms per {q.shape[0]} queries; K13 {scan_ms:.2f} ms, "
            f"{st['candidates']} candidates, {st['window_candidates']} window rows, {st['overflow_queries']} unproven); "
@@ -431,6 +436,45 @@ def build_roofline(kern, t_build):
         out["kernels_ms_total"] = round(tot, 3)
         out["kernels_share_of_build"] = round(tot / (t_build * 1e3), 4)
         out["timing"] = "hipEvents around each launch on the build stream (profiling on during the timed build)"
+    return out
+
+
+def batch_sweep_side_line(a, idx, rl, gt, dev):
+    """QPS against the query batch size at the main line's index and n_probes (the headline keeps the 10k batch of
+    BASELINE.md's plan). K13 streams every probed row once per batch, so its row traffic and its item transitions
+    are spread over more queries as the batch grows; batches above kRsMaxBatch (32,768) are split. Queries: the same
+    mixture rows as the main batch (its first rows), recall over the main line's ground-truth queries."""
+    from mivs import _native, ops
+    from mivs.neighbors import ivf_flat
+
+    sp = ivf_flat.SearchParams(n_probes=a.n_probes)
+    out = []
+    for nq in [int(v) for v in a.batch_sweep.split(",") if v.strip()]:
+        qq = ops.synth_mixture(nq, a.dim, SEED, n_centers=a.centers, sigma=a.sigma, row_begin=QUERY_ROW_BASE,
+                               device=dev)
+        for _ in range(2):
+            ivf_flat.search(sp, idx, qq, a.k)
+        _native.set_profiling(True)
+        idx.profile_collect()
+        reps = max(3, a.steps // 4)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dd, ii = ivf_flat.search(sp, idx, qq, a.k)
+        torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) / reps
+        pr = idx.profile_collect()
+        _native.set_profiling(False)
+        st = idx.last_search_stats()
+        ng = min(nq, gt.shape[0])
+        rec = recall_at_k(ii[:ng].cpu().numpy(), gt[:ng])
+        out.append({"queries": nq, "qps": round(nq / t, 1), "ms_per_batch": round(t * 1e3, 3),
+                    "k13_ms_per_batch": round(pr["scan_ms"] / reps, 3), "recall_at_10": round(rec, 4),
+                    "recall_queries": ng, "unproven_queries_last_batch": st["overflow_queries"]})
+        rl(f"[batch] Q={nq}: {nq / t:,.0f} QPS ({t * 1e3:.2f} ms per batch, K13 {pr['scan_ms'] / reps:.2f} ms), "
+           f"recall {rec:.4f}")
+        del qq, dd, ii
+        torch.cuda.empty_cache()
     return out
 
 
@@ -1026,6 +1070,13 @@ def main():
         except Exception as e:  # the IVF line stands without it
             rl(f"[large-k] side line failed: {e!r}")
 
+    batch_sweep = None
+    if rank == 0 and world == 1 and a.batch_sweep.strip():
+        try:
+            batch_sweep = batch_sweep_side_line(a, idx, rl, gt, local)
+        except Exception as e:  # the IVF line stands without it
+            rl(f"[batch] side line failed: {e!r}")
+
     latency = None
     if rank == 0 and world == 1 and a.latency.strip():
         try:
@@ -1110,6 +1161,7 @@ def main():
         "flat_bruteforce_1m": flat,
         "large_k": large_k,
         "latency": latency,
+        "batch_sweep": batch_sweep,
         "single_process_aggregator": single,
         "ivf_pq_12m5": pq,
         "distributed": dist_info,

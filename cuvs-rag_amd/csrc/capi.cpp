@@ -219,6 +219,9 @@ struct mivs_index_s {
   int64_t last_rs_nq = 0; // K13: queries of the last search batch (its cand_off holds last_rs_nq + 1 offsets)
   bool last_rs_one_pass = false;  // K13: the last batch's candidates are in fixed-capacity runs (ws.rs_qcnt)
   int64_t last_ovf = 0, last_window = 0;
+  // the last batch's fallback count and window size are still on the device (ws.pf_stats): the device-sized
+  // fallback did not read them; last_search_stats does
+  bool last_stats_dev = false;
   // host wall time of the build's phases (mivs_index_build_phases; recorded while profiling is on)
   std::vector<double> build_phase_s;
   // device time and algorithmic work of the build's hot kernels (mivs_index_build_kernels; profiling on)
@@ -996,6 +999,58 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
                      verify_sel);
 }
 
+// The exact fallback of K13's unproven queries sized on the device: K11 leaves their count in
+// ws.pf_stats[0] and their rows in ws.ovf_q; the probe map over their probes (ws.probes_i, from the search's coarse
+// probe), K3 over those (query, list) pairs, and K7 writing each query's top-k straight into its row of out_d / out_i
+// all take their size from that count on the device, so the search enqueues and returns without a host round trip.
+// An empty fallback is three launches that leave at once (~10 us of GPU time, against the ~55-90 us turnaround of
+// reading the count on the host). MIVS_FALLBACK_SYNC=1 keeps the host-sized path (A/B runs).
+bool device_fallback_ok(const mivs_index_s* idx, int k) {
+  return env_int("MIVS_FALLBACK_SYNC", 0) == 0 && idx->kind == 0 && k <= kMaxK && idx->lists.n_lists <= probe_map_dev_max_lists();
+}
+
+void exact_fallback_on_device(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np,
+                              float* out_d, int64_t* out_i) {
+  Workspace& ws = idx->ws;
+  const ListSet& L = idx->lists;
+  const int64_t ne = nq * np;
+  const int qtile = pick_qtile(k, idx->d, idx->G);
+  ws.counts.reserve(sizeof(int) * L.n_lists);
+  ws.bucket_off.reserve(sizeof(int) * (L.n_lists + 1));
+  ws.work_off.reserve(sizeof(int) * (L.n_lists + 1));
+  ws.bucket_q.reserve(sizeof(int64_t) * ne);
+  ws.bucket_slot.reserve(sizeof(int64_t) * ne);
+  ws.slot_begin.reserve(sizeof(int64_t) * (nq + 1));
+  ws.counter.reserve(16);
+  const int* n_dev = ws.pf_stats.as<int>();
+  HIPCHK(launch_probe_map_dev(n_dev, nq, ws.ovf_q.as<int64_t>(), ws.probes_i.as<int64_t>(), np, L.n_lists,
+                              L.goff.as<int64_t>(), idx->G, qtile, ws.counts.as<int>(), ws.bucket_off.as<int>(),
+                              ws.work_off.as<int>(), ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(),
+                              ws.slot_begin.as<int64_t>(), ws.counter.as<int>(), s));
+  // the partials of every query the batch could send here (the count is not known on the host)
+  const int64_t max_slots = nq * L.top_chunks_prefix[std::min<int64_t>(np, L.n_lists)];
+  ws.part_d.reserve(sizeof(float) * (size_t)std::max<int64_t>(max_slots * k, 1));
+  ws.part_i.reserve(sizeof(int64_t) * (size_t)std::max<int64_t>(max_slots * k, 1));
+  ScanJob j{&L, idx->G, q, ws.qn.as<float>(), idx->d, idx->dp, k, idx->metric, ws.bucket_q.as<int64_t>(),
+            ws.bucket_slot.as<int64_t>(), ws.bucket_off.as<int>(), ws.work_off.as<int>(), ws.part_d.as<float>(),
+            ws.part_i.as<int64_t>(), qtile};
+  j.counter_zeroed = true;
+  run_scan(j, idx->device, ws, s);
+  MergeArgs m{};
+  m.in_d = ws.part_d.as<float>();
+  m.in_i = ws.part_i.as<int64_t>();
+  m.slot_begin = ws.slot_begin.as<int64_t>();
+  m.nq = nq;
+  m.k_in = k;
+  m.k = k;
+  m.metric = idx->metric;
+  m.out_d = out_d;
+  m.out_i = out_i;
+  m.nq_dev = n_dev;
+  m.out_rows = ws.ovf_q.as<int64_t>();
+  HIPCHK(launch_merge(m, s));
+}
+
 // K11 over the scan's candidate slots, then the exact scan for the queries the refine could not prove
 // (scattered back into out_d / out_i). force_ovf (K13): device flag, nonzero -> every query falls back.
 void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
@@ -1042,6 +1097,11 @@ void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_
   r.n_window = reinterpret_cast<int64_t*>(ws.pf_stats.as<char>() + 8);
   HIPCHK(launch_pf_refine(r, s));
   if (kth_out) return;
+  if (fallback_pf && device_fallback_ok(idx, k)) {  // K13's unproven queries: no host round trip
+    exact_fallback_on_device(idx, s, q, nq, k, np, out_d, out_i);
+    idx->last_stats_dev = true;
+    return;
+  }
   ws.h_stats.reserve(16);
   int64_t* h = ws.h_stats.as<int64_t>();
   HIPCHK(hipMemcpyAsync(h, ws.pf_stats.p, 16, hipMemcpyDeviceToHost, s));
@@ -1815,6 +1875,7 @@ void ivf_search_impl(mivs_index_s* idx, hipStream_t s, const float* q, int64_t n
     nb = std::min<int64_t>(qb, nq - b0);
     idx->last_ovf = 0;  // (every stat describes the last batch, as n_queries does)
     idx->last_window = 0;
+    idx->last_stats_dev = false;
     ivf_search_batch(idx, s, q + b0 * (int64_t)idx->d, nb, k, np, out_d + b0 * k, out_i + b0 * k,
                      out_probes ? out_probes + b0 * np : nullptr);
   }
@@ -2591,6 +2652,7 @@ int32_t mivs_brute_force_search(mivs_index_t idx, void* stream, const float* d_q
       HIPCHK(hipMemsetAsync(idx->ws.probes_i.p, 0, sizeof(int64_t) * nq, s));
       idx->last_ovf = 0;
       idx->last_window = 0;
+      idx->last_stats_dev = false;
       ivf_search_probed(idx, s, d_q, nq, k, 1, d_dist, d_ids, true, pr, true);
       idx->last_nq = nq;
       idx->last_np = 1;
@@ -2601,6 +2663,7 @@ int32_t mivs_brute_force_search(mivs_index_t idx, void* stream, const float* d_q
     idx->last_pf = 0;
     idx->last_ovf = 0;
     idx->last_window = 0;
+    idx->last_stats_dev = false;
     if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
     single_list_topk(idx->lists, idx->G, d_q, idx->ws.qn.as<float>(), nullptr, nq, idx->d, idx->dp, k, idx->metric,
                      d_dist, d_ids, idx->device, idx->ws, s);
@@ -2642,6 +2705,13 @@ int32_t mivs_index_last_search_stats(mivs_index_t idx, mivs_search_stats* out) {
     st.scan_kernel = idx->last_scan;
     st.overflow_queries = idx->last_ovf;
     st.window_candidates = idx->last_window;
+    if (idx->last_stats_dev) {  // (the device-sized fallback left them in ws.pf_stats: {count, pad, window})
+      int64_t h[2] = {0, 0};
+      HIPCHK(hipDeviceSynchronize());
+      HIPCHK(hipMemcpy(h, idx->ws.pf_stats.p, sizeof(h), hipMemcpyDeviceToHost));
+      st.overflow_queries = (int64_t)(int32_t)(h[0] & 0xFFFFFFFF);
+      st.window_candidates = h[1];
+    }
     st.copies_skipped = idx->copies_skipped;
     const ListSet& L = idx->lists;
     if (idx->last_nq > 0 && idx->kind == 0) {

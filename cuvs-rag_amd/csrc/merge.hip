@@ -9,6 +9,7 @@
 // after the RCCL all-gather — the merge the reference does on the host with
 // numpy (improved_multi_gpu_rag.py:266-275, cuvs-2gpu-main.ipynb:1820-1834,
 // contract test_search_result_aggregator.py:308-358).
+#include <algorithm>
 #include <climits>
 
 #include "mivs_common.hpp"
@@ -22,10 +23,7 @@ __device__ __forceinline__ bool kv_lt(float ak, int64_t ai, float bk, int64_t bi
 }
 
 template <int METRIC>
-__global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (q >= a.nq) return;
+__device__ __forceinline__ void merge_query(const MergeArgs& a, int64_t q, int lane) {
   int64_t sb, se;
   if (a.slot_begin) { sb = a.slot_begin[q]; se = a.slot_begin[q + 1]; }
   else if (a.part_stride > 0) { sb = 0; se = a.slots_per_q; }
@@ -74,9 +72,24 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
   }
   if (lane < k) {
     const bool valid = mi != LLONG_MAX;
-    a.out_d[q * k + lane] = valid ? (METRIC == kIP ? -mk : mk) : (METRIC == kIP ? -INFINITY : INFINITY);
-    a.out_i[q * k + lane] = valid ? mi : (int64_t)-1;
+    const int64_t o = a.out_rows ? a.out_rows[q] : q;
+    a.out_d[o * k + lane] = valid ? (METRIC == kIP ? -mk : mk) : (METRIC == kIP ? -INFINITY : INFINITY);
+    a.out_i[o * k + lane] = valid ? mi : (int64_t)-1;
   }
+}
+
+// one wave per query; with nq_dev (the device-sized fallback) a fixed grid strides over the *nq_dev queries, so
+// an empty fallback costs one launch of workgroups that leave at once
+template <int METRIC>
+__global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q0 = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (!a.nq_dev) {
+    if (q0 < a.nq) merge_query<METRIC>(a, q0, lane);
+    return;
+  }
+  const int64_t n = *a.nq_dev < a.nq ? (int64_t)*a.nq_dev : a.nq;
+  for (int64_t q = q0; q < n; q += (int64_t)gridDim.x * 4) merge_query<METRIC>(a, q, lane);
 }
 
 }  // namespace
@@ -84,7 +97,7 @@ __global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
 hipError_t launch_merge(const MergeArgs& a, hipStream_t s) {
   if (a.k < 1 || a.k > kMaxK) return hipErrorInvalidValue;
   if (a.nq <= 0) return hipSuccess;
-  const dim3 grid((unsigned)ceil_div(a.nq, 4));
+  const dim3 grid((unsigned)(a.nq_dev ? std::min<int64_t>(ceil_div(a.nq, 4), 1024) : ceil_div(a.nq, 4)));
   if (a.metric == kIP) hipLaunchKernelGGL(k_merge<kIP>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(k_merge<kL2>, grid, dim3(256), 0, s, a);
   return hipGetLastError();

@@ -109,6 +109,10 @@ struct MergeArgs {
   // > 0: gathered layout [slots_per_q parts][nq][k_in] with parts part_stride elements apart (the
   // all-gather receive buffer, rank-major); 0: [nq][slots][k_in] / slot_begin as above
   int64_t part_stride;
+  // the device-sized exact fallback: only queries q < *nq_dev (<= nq) are merged, and query q's top-k goes to
+  // output row out_rows[q] (the unproven query's row in the batch) instead of row q
+  const int* nq_dev = nullptr;
+  const int64_t* out_rows = nullptr;
 };
 
 // IVF-PQ scan job (K9, pq.hip): one workgroup per (query, probe) slot = q * n_probes + p.
@@ -261,8 +265,11 @@ constexpr int kRsBlockGroups = kRsWaves;
 constexpr int kRsPreDiv = 4;
 constexpr int kRsPreDivF8 = 4;
 constexpr int kRsPreSel = 10;
-constexpr int kRsQCap = 4096;  // K13 one-pass bucketing: least candidates per query run (MIVS_RS_QCAP)
-constexpr int64_t kRsCandBudget = int64_t(1) << 27;  // ... and the batch's runs: 128M entries (1 GiB of key + position)
+// K13 one-pass bucketing: least candidates per query run (MIVS_RS_QCAP), and the batch's runs: 256M entries (2 GiB of
+// key + position). A query past its run's capacity is unproven and takes the exact fallback (~0.2 ms each at configs[2]):
+// at 1 GiB / 4,096 a 32,768-query batch had 13 of them (profiles/r05_qsweep.txt)
+constexpr int kRsQCap = 8192;
+constexpr int64_t kRsCandBudget = int64_t(1) << 28;
 constexpr int kRsWaveCapMax = 16384;  // records of a K13 wave's candidate stream (more: all queries fall back)
 constexpr int kRsWaveCapMaxLk = 1 << 18;  // the same for large k (K16: thousands of candidates per query)
 constexpr int kRsRecInt4 = 3;         // a record: 8 dots of one lane and query half + {first row position, query}
@@ -546,6 +553,14 @@ hipError_t launch_fill2_i32(int* o1, int64_t n1, int v1, int* o2, int64_t n2, in
 // single-list job prep: bucket = identity over nq queries, slot base = q * chunks
 hipError_t launch_single_list_job(int64_t nq, int64_t chunks, int qtile, int64_t* bucket_q, int64_t* bucket_slot,
                                   int* bucket_off, int* work_off, int64_t* slot_begin, hipStream_t s, int* zero = nullptr);
+// The exact fallback's probe map sized on the device: entries (i, p) for i < min(*n_dev, cap) are probe p of query
+// ovf_q[i] in probes [.][np]; bucket_q holds the query's own row, bucket_slot / slot_begin number the slots by i.
+// One workgroup (n_lists <= probe_map_dev_max_lists()); zero: the scan's work counter, zeroed here.
+int probe_map_dev_max_lists();
+hipError_t launch_probe_map_dev(const int* n_dev, int64_t cap, const int64_t* ovf_q, const int64_t* probes, int np,
+                                int n_lists, const int64_t* list_goff, int chunk_groups, int qtile, int* counts,
+                                int* bucket_off, int* work_off, int64_t* bucket_q, int64_t* bucket_slot,
+                                int64_t* slot_begin, int* zero, hipStream_t s);
 // IVF probe map: probes [nq][np] (int64 list ids) -> buckets, work offsets, slot bases
 hipError_t launch_probe_map(const int64_t* probes, int64_t nq, int np, int n_lists, const int64_t* list_goff,
                             int chunk_groups, int qtile, int* counts, int* fill, int* bucket_off, int* work_off,

@@ -314,6 +314,81 @@ __global__ __launch_bounds__(1024) void k_probe_map_small(const int64_t* __restr
   if (threadIdx.x == 0) slot_begin[nq] = tot;
 }
 
+// The exact fallback's probe map, sized on the device: the unproven queries of a pre-filter search
+// are ovf_q[0 .. *n_dev) (K11 appends them); entry e = i * np + p is probe p of query ovf_q[i]. One workgroup, as
+// k_probe_map_small, but over a count it reads on the device: LDS count, prefix, then the fill in entry order in
+// rounds of 1024 entries, each round's slots numbered by a block scan. bucket_q = the query's own row (K3 reads the
+// batch's rows and norms), bucket_slot / slot_begin number the slots by i (K7 merges query i into row ovf_q[i]).
+// With nothing to fall back on it writes empty offsets: one launch, no host round trip.
+__global__ __launch_bounds__(1024) void k_probe_map_dev(const int* __restrict__ n_dev, int64_t cap,
+                                                        const int64_t* __restrict__ ovf_q,
+                                                        const int64_t* __restrict__ probes, int np, int n_lists,
+                                                        const int64_t* __restrict__ list_goff, int G, int qtile,
+                                                        int* __restrict__ counts, int* __restrict__ bucket_off,
+                                                        int* __restrict__ work_off, int64_t* __restrict__ bucket_q,
+                                                        int64_t* __restrict__ bucket_slot,
+                                                        int64_t* __restrict__ slot_begin, int* __restrict__ zero) {
+  __shared__ int bins[kPmSmallLists];
+  __shared__ int chunks[kPmSmallLists];
+  __shared__ int64_t sh[16];
+  const int nr = *n_dev;
+  const int64_t nf = nr <= 0 ? 0 : (nr < cap ? nr : cap);
+  const int64_t n = nf * np;
+  if (threadIdx.x == 0 && zero) *zero = 0;
+  for (int l = threadIdx.x; l < n_lists; l += 1024) bins[l] = 0;
+  __syncthreads();
+  auto list_of = [&](int64_t e) {
+    const int64_t i = e / np;
+    return (int)probes[ovf_q[i] * np + (e - i * np)];
+  };
+  for (int64_t e = threadIdx.x; e < n; e += 1024) {
+    const int l = list_of(e);
+    if (l >= 0) atomicAdd(bins + l, 1);
+  }
+  __syncthreads();
+  int64_t cb = 0, cw = 0;
+  for (int l0 = 0; l0 < n_lists; l0 += 1024) {
+    const int l = l0 + threadIdx.x;
+    int64_t c = 0, wk = 0;
+    if (l < n_lists) {
+      c = bins[l];
+      const int ch = (int)ceil_div(list_goff[l + 1] - list_goff[l], G);
+      chunks[l] = ch;
+      wk = ceil_div(c, qtile) * ch;
+      counts[l] = (int)c;
+    }
+    int64_t tb, tw;
+    const int64_t eb = block_excl_scan(c, sh, &tb);
+    const int64_t ew = block_excl_scan(wk, sh, &tw);
+    if (l < n_lists) {
+      bucket_off[l] = (int)(cb + eb);
+      work_off[l] = (int)(cw + ew);
+      bins[l] = (int)(cb + eb);
+    }
+    cb += tb;
+    cw += tw;
+  }
+  if (threadIdx.x == 0) { bucket_off[n_lists] = (int)cb; work_off[n_lists] = (int)cw; }
+  __syncthreads();
+  int64_t carry = 0;
+  for (int64_t e0 = 0; e0 < n; e0 += 1024) {  // (a uniform trip count: every thread reaches every scan)
+    const int64_t e = e0 + threadIdx.x;
+    const int l = e < n ? list_of(e) : -1;
+    int64_t tot;
+    const int64_t run = carry + block_excl_scan(l >= 0 ? (int64_t)chunks[l] : 0, sh, &tot);
+    if (e < n) {
+      if (e % np == 0) slot_begin[e / np] = run;
+      if (l >= 0) {
+        const int at = atomicAdd(bins + l, 1);
+        bucket_q[at] = ovf_q[e / np];
+        bucket_slot[at] = run;
+      }
+    }
+    carry += tot;
+  }
+  if (threadIdx.x == 0) slot_begin[nf] = carry;
+}
+
 // the output slot of every bucket entry (its (query, probe)'s first slot) and each query's first slot, one launch
 // (thread t: bucket entry t and query t)
 __global__ void k_bucket_slot_begin(int64_t* __restrict__ bucket_slot, int64_t n, const int64_t* __restrict__ qp_base,
@@ -496,6 +571,18 @@ hipError_t launch_probe_map(const int64_t* probes, int64_t nq, int np, int n_lis
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_bucket_slot_begin, grid1(n > nq ? n : nq + 1, 256), dim3(256), 0, s, bucket_slot, n, qp_base,
                      qp_slots, nq, np, slot_begin);
+  return hipGetLastError();
+}
+
+int probe_map_dev_max_lists() { return kPmSmallLists; }
+
+hipError_t launch_probe_map_dev(const int* n_dev, int64_t cap, const int64_t* ovf_q, const int64_t* probes, int np,
+                                int n_lists, const int64_t* list_goff, int chunk_groups, int qtile, int* counts,
+                                int* bucket_off, int* work_off, int64_t* bucket_q, int64_t* bucket_slot,
+                                int64_t* slot_begin, int* zero, hipStream_t s) {
+  if (n_lists <= 0 || n_lists > kPmSmallLists || np <= 0 || cap < 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_probe_map_dev, dim3(1), dim3(1024), 0, s, n_dev, cap, ovf_q, probes, np, n_lists, list_goff,
+                     chunk_groups, qtile, counts, bucket_off, work_off, bucket_q, bucket_slot, slot_begin, zero);
   return hipGetLastError();
 }
 

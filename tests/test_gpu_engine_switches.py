@@ -64,6 +64,9 @@ SEARCH_SWITCHES = [
     {"MIVS_PF_ROWSTAT": "0", "MIVS_PF_FLAGS": "32"},                  # K10 phase clocks (stderr only)
     {"MIVS_RS_BUCKET_1P": "0"},                                       # K13 bucketing: two-pass CSR runs
     {"MIVS_RS_QCAP": "4"},                                            # one-pass runs overflow: the fallback
+    {"MIVS_FALLBACK_SYNC": "1"},                                      # fallback sized on the host (round 4)
+    {"MIVS_FALLBACK_SYNC": "1", "MIVS_RS_QCAP": "4"},
+    {"MIVS_FALLBACK_SYNC": "1", "MIVS_RS_WAVE_CAP": "2"},
 ]
 
 
@@ -92,6 +95,29 @@ def test_ivf_one_pass_bucketing_same_candidates(ivf, flat_data, monkeypatch):
     np.testing.assert_array_equal(_bits(d1), _bits(d0))
     assert st0["candidates"] == st1["candidates"] > 0
     assert st0["overflow_queries"] == st1["overflow_queries"]  # (this small shape has unproven windows either way)
+
+
+@pytest.mark.parametrize("env", [{}, {"MIVS_RS_QCAP": "4"}, {"MIVS_RS_WAVE_CAP": "2"}],
+                         ids=["default", "qcap4", "lost"])
+def test_device_fallback_stats_and_bits(ivf, flat_data, monkeypatch, env):
+    """the exact fallback of K13's unproven queries sized on the device (no host round trip) against the host-sized
+    one: the same bits; few, most and all queries unproven. The device path's stats (read back by last_search_stats)
+    count K13's unproven queries and windows; the host path sends those queries through K10 first and adds its
+    unproven queries and windows, so its counts are at least as large"""
+    idx, _ = ivf
+    _, q = flat_data
+    for kk, v in env.items():
+        monkeypatch.setenv(kk, v)
+    d0, i0 = _search(idx, q)
+    st0 = idx.last_search_stats()
+    monkeypatch.setenv("MIVS_FALLBACK_SYNC", "1")
+    d1, i1 = _search(idx, q)
+    st1 = idx.last_search_stats()
+    np.testing.assert_array_equal(i0, i1)
+    np.testing.assert_array_equal(_bits(d0), _bits(d1))
+    assert st0["overflow_queries"] <= st1["overflow_queries"] and st0["window_candidates"] <= st1["window_candidates"]
+    if env:
+        assert st0["overflow_queries"] > q.shape[0] // 2, st0
 
 
 def test_ivf_default_matches_oracle(ivf, flat_data):

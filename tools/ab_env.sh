@@ -6,7 +6,7 @@ TAG=$1; REPS=$2; shift 2
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-QB="--steps 10 --warmup 2 --no-cpu-baseline --sweep '' --flat-rows 0 --pq-rows 0 --large-k '' --single-process 0 --gt-queries 200 --latency ''"
+QB="--steps 10 --warmup 2 --no-cpu-baseline --sweep '' --flat-rows 0 --pq-rows 0 --large-k '' --single-process 0 --gt-queries 200 --latency '' --batch-sweep ''"
 for r in $(seq 1 $REPS); do
   i=0
   for e in "$@"; do

@@ -9,6 +9,13 @@
 //      item's last tile, waited for at the next item's start (K13's item transition)
 //   16 tile images from a 540 MB pool (11k tiles, HBM/MALL): the 32 blocks of one XCD walk one range of it
 //      together, as the items of one list do (otherwise 64 L2-resident tiles)
+//   2048 three tile buffers and two counters instead of one: a wave signals 'my pieces of tile t + 1 landed' at
+//      k-step LANDED_AT of tile t (after a vmcnt wait) and 'done reading tile t' after its k-loop; it starts tile t + 1
+//      once every wave's pieces landed, and issues its pieces of tile t + 2 (into the buffer of tile t - 1) once every
+//      wave is done with tile t - 1 -- waves may drift up to about a tile apart instead of meeting at every tile
+//   1024 the query pieces gathered straight from a [10k][768] fp16 query array (lane (c, kq) of piece 2 t + qb reads
+//      16 B of query id(16 qb + c) at dims 32 t + 8 kq; ids spread pseudo-randomly over the 15 MB array) instead of
+//      copied from a prebuilt tile image; the header piece still from the image
 // Reports TF/s, the in-kernel clock (s_memtime / s_memrealtime) and the MFMA pipe's busy fraction.
 // Build: hipcc -O3 --offload-arch=gfx950 -ffp-contract=off tools/k13_probe.hip -o tools/k13_probe
 #include <hip/hip_runtime.h>
@@ -32,6 +39,7 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 
 constexpr int NK = 48;
 constexpr int BUF = NK * 1024 + 1024;
+constexpr int kQ = 10000;  // queries in the VAR & 1024 query array
 
 __device__ __forceinline__ v4i uniform_desc(const void* p, int bytes) {
   const uint64_t v = reinterpret_cast<uint64_t>(p);
@@ -58,15 +66,19 @@ template <int VAR, int PD, int WAVES>
 __global__ __launch_bounds__(WAVES * 64, 1) void probe(const h8* __restrict__ rows, const char* __restrict__ src,
                                                        int src_tiles, int ntiles, float* out,
                                                        unsigned long long* clk, const h8* __restrict__ big_rows,
-                                                       long long big_items) {
+                                                       long long big_items, const char* __restrict__ qarr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  int* s_ready = reinterpret_cast<int*>(smem + 2 * BUF);
+  constexpr int NBUF = (VAR & 2048) ? 3 : 2;
+  constexpr int LANDED_AT = 40;
+  int* s_ready = reinterpret_cast<int*>(smem + NBUF * BUF);
+  int* s_done = s_ready + 1;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  for (int i = tid; i < 2 * BUF / 16; i += WAVES * 64) {
+  const v4i qdesc = uniform_desc(qarr, kQ * NK * 32);
+  for (int i = tid; i < NBUF * BUF / 16; i += WAVES * 64) {
     const int v = (i * 2654435761u) >> 7;
     reinterpret_cast<uint4*>(smem)[i] = make_uint4(v & 0x3BFF3BFF, (v >> 3) & 0x3BFF3BFF, v & 0x37FF37FF, 0x3C003C00 ^ (v & 0x03FF03FF));
   }
-  if (tid == 0) *s_ready = 0;
+  if (tid == 0) { *s_ready = 0; *s_done = 0; }
   __syncthreads();
   h8 ra[NK];
   const h8* rp = rows + ((size_t)(blockIdx.x * WAVES + wave) * NK) * 64 + lane;
@@ -95,10 +107,14 @@ __global__ __launch_bounds__(WAVES * 64, 1) void probe(const h8* __restrict__ ro
       asm volatile("" ::: "memory");
     }
     const char* bb = smem + cur * BUF + lane * 16;
-    const int nxt = cur ^ 1;
+    const int nxt = cur + 1 == NBUF ? 0 : cur + 1;
     char* sbuf = smem + nxt * BUF;
     const int tsrc = (VAR & 16) ? (int)(((blockIdx.x & 7) * 1375 + t + 1) % src_tiles) : (int)((blockIdx.x + t) % src_tiles);
     const v4i sdesc = uniform_desc(src + (size_t)tsrc * (NK + 1) * 1024, (NK + 1) * 1024);
+    // VAR & 1024: the tile's query ids -> per-lane byte offsets into the query array (qb = 0, 1)
+    const int c = lane & 15;
+    const int gq0 = (int)(((long long)(tsrc * 32 + c) * 7919) % kQ), gq1 = (int)(((long long)(tsrc * 32 + 16 + c) * 7919) % kQ);
+    const int qo0 = gq0 * (NK * 32) + (lane >> 4) * 16, qo1 = gq1 * (NK * 32) + (lane >> 4) * 16;
     const h8* nr = big_rows + ((size_t)(((long long)blockIdx.x * 7919 + t * 131) % big_items) * WAVES + wave) * NK * 64 + lane;
     if (!(VAR & 32) && (VAR & 8) && t % 10 == 0) __builtin_amdgcn_s_waitcnt(0x0070);
     f32x4 acc[4] = {z, z, z, z};
@@ -123,10 +139,23 @@ __global__ __launch_bounds__(WAVES * 64, 1) void probe(const h8* __restrict__ ro
           ra[s] = nr[s * 64];
         }
       }
+      if ((VAR & 2048) && s == 1 && t >= 2) {  // the buffer of tile t - 1 is free once every wave is done with it
+        for (int i = 0; i < (1 << 20); ++i) {
+          if (__hip_atomic_load(s_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= WAVES * (t - 1)) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        asm volatile("" ::: "memory");
+      }
+      if ((VAR & 2048) && s == LANDED_AT) {  // this wave's pieces of tile t + 1 have landed
+        __builtin_amdgcn_s_waitcnt(0x0070);
+        asm volatile("" ::: "memory");
+        if (lane == 0) __hip_atomic_fetch_add(s_ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
       if (VAR & 2) {
         if (s >= 1 && (s - 1) * WAVES <= NK) {
           const int p = min((s - 1) * WAVES + wave, NK);
-          dma_b128(sdesc, sbuf + p * 1024, lane * 16, p * 1024);
+          if ((VAR & 1024) && p < NK) dma_b128(qdesc, sbuf + p * 1024, (p & 1) ? qo1 : qo0, 64 * (p >> 1));
+          else dma_b128(sdesc, sbuf + p * 1024, lane * 16, p * 1024);
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -140,7 +169,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void probe(const h8* __restrict__ ro
       if ((VAR & 2) && RL) __builtin_amdgcn_s_waitcnt(0x0070);  // (conservative: rows too)
     }
     (void)AFTER;
-    if (VAR & 1) {
+    if (VAR & 2048) {  // done reading tile t (the k-loop's B reads are in: lgkmcnt(0))
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      asm volatile("" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(s_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else if (VAR & 1) {
       asm volatile("" ::: "memory");
       if (lane == 0) __hip_atomic_fetch_add(s_ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
@@ -188,20 +221,21 @@ __global__ __launch_bounds__(WAVES * 64, 1) void probe(const h8* __restrict__ ro
 }
 
 const h8* g_big = nullptr;
+const char* g_q = nullptr;
 long long g_big_items = 1;
 
 template <int VAR, int PD, int WAVES>
 int run(const char* name, const h8* rows, const char* src, int src_tiles, float* out, unsigned long long* clk,
         int grid, int ntiles) {
-  const size_t lds = 2 * BUF + 64;
+  const size_t lds = ((VAR & 2048) ? 3 : 2) * BUF + 64;
   CHECK(hipFuncSetAttribute((const void*)probe<VAR, PD, WAVES>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
   for (int rep = 0; rep < 3; ++rep)  // warm: >= 2 s of back-to-back launches before the timed one
-    hipLaunchKernelGGL((probe<VAR, PD, WAVES>), dim3(grid), dim3(WAVES * 64), lds, 0, rows, src, src_tiles, ntiles, out, clk, g_big, g_big_items);
+    hipLaunchKernelGGL((probe<VAR, PD, WAVES>), dim3(grid), dim3(WAVES * 64), lds, 0, rows, src, src_tiles, ntiles, out, clk, g_big, g_big_items, g_q);
   CHECK(hipEventRecord(e0));
-  hipLaunchKernelGGL((probe<VAR, PD, WAVES>), dim3(grid), dim3(WAVES * 64), lds, 0, rows, src, src_tiles, ntiles, out, clk, g_big, g_big_items);
+  hipLaunchKernelGGL((probe<VAR, PD, WAVES>), dim3(grid), dim3(WAVES * 64), lds, 0, rows, src, src_tiles, ntiles, out, clk, g_big, g_big_items, g_q);
   CHECK(hipEventRecord(e1));
   CHECK(hipEventSynchronize(e1));
   float ms = 0;
@@ -241,6 +275,12 @@ int main(int argc, char** argv) {
     g_big = big;
     g_big_items = (long long)(big_bytes / ((size_t)8 * NK * 1024));
   }
+  {
+    char* qa;
+    CHECK(hipMalloc(&qa, (size_t)kQ * NK * 32));
+    CHECK(hipMemset(qa, 0x31, (size_t)kQ * NK * 32));
+    g_q = qa;
+  }
   CHECK(hipMalloc(&out, (size_t)grid * 8 * 64 * sizeof(float)));
   CHECK(hipMalloc(&clk, sizeof(unsigned long long) * 2 * grid));
   {
@@ -261,16 +301,10 @@ int main(int argc, char** argv) {
   printf("grid %d, %d tiles per wave, 16x16x32 f16, 32 rows x 768 dims per wave in registers\n", grid, ntiles);
   run<0, 2, 8>("loop only, PD 2, 8 waves", rows, src, src_tiles, out, clk, grid, ntiles);
   run<7, 2, 8>("+sync +dma +epi", rows, src, src_tiles, out, clk, grid, ntiles);
-  run<15, 2, 8>("+sync +dma +epi +items", rows, src, src_tiles, out, clk, grid, ntiles);
+  run<7 + 2048, 2, 8>("+split sync (3 bufs) +dma +epi", rows, src, src_tiles, out, clk, grid, ntiles);
   run<23, 2, 8>("+sync +dma +epi +hbm tiles", rows, src, big_tiles, out, clk, grid, ntiles);
-  run<31, 2, 8>("+sync +dma +epi +items +hbm tiles", rows, src, big_tiles, out, clk, grid, ntiles);
-  run<47, 2, 8>("+sync +dma +epi +items staggered 8", rows, src, src_tiles, out, clk, grid, ntiles);
-  run<111, 2, 8>("+sync +dma +epi +items staggered 2", rows, src, src_tiles, out, clk, grid, ntiles);
-  run<63, 2, 8>("+sync +dma +epi +items stag8 +hbm tiles", rows, src, big_tiles, out, clk, grid, ntiles);
-  run<175, 2, 8>("+items stag8, loads never waited", rows, src, src_tiles, out, clk, grid, ntiles);
-  run<303, 2, 8>("+items stag8, nt loads", rows, src, src_tiles, out, clk, grid, ntiles);
-  run<815, 2, 8>("+items stag8 nt, one loop (unpaired)", rows, src, src_tiles, out, clk, grid, ntiles);
-  run<10, 2, 8>("+dma +items (no sync)", rows, src, src_tiles, out, clk, grid, ntiles);
-  run<26, 2, 8>("+dma +items +hbm tiles (no sync)", rows, src, big_tiles, out, clk, grid, ntiles);
+  run<23 + 2048, 2, 8>("+split sync +dma +epi +hbm tiles", rows, src, big_tiles, out, clk, grid, ntiles);
+  run<7, 2, 8>("+sync +dma +epi (again)", rows, src, src_tiles, out, clk, grid, ntiles);
+  run<7 + 2048, 2, 8>("+split sync +dma +epi (again)", rows, src, src_tiles, out, clk, grid, ntiles);
   return 0;
 }

@@ -8,7 +8,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 run_pmc() {  # name, counters...
   local nm=$1; shift
-  timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-include-regex "$KRE" -f csv -d $OUT/$nm -o pmc -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --gt-queries 16 --sweep "" --flat-rows 0 --pq-rows 0 --large-k "" --single-process 0 --latency "" > $OUT/$nm.log 2>&1
+  timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-include-regex "$KRE" -f csv -d $OUT/$nm -o pmc -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --gt-queries 16 --sweep "" --flat-rows 0 --pq-rows 0 --large-k "" --single-process 0 --latency "" --batch-sweep "" > $OUT/$nm.log 2>&1
 }
 run_pmc fetch FETCH_SIZE || exit 11
 run_pmc write WRITE_SIZE || exit 12
