@@ -61,6 +61,10 @@ template <bool B>
 struct BoolC {
   static constexpr bool value = B;
 };
+template <int I>
+struct IntC {
+  static constexpr int value = I;
+};
 
 template <int VAR, int PD, int WAVES>
 __global__ __launch_bounds__(WAVES * 64, 1) void probe(const h8* __restrict__ rows, const char* __restrict__ src,
@@ -220,6 +224,108 @@ __global__ __launch_bounds__(WAVES * 64, 1) void probe(const h8* __restrict__ ro
   out[(size_t)(blockIdx.x * WAVES + wave) * 64 + lane] = sink;
 }
 
+// 16-row waves with a double-buffered row set (VERDICT r04 item 1's candidate): each wave keeps 16 rows (24 A registers,
+// 96 VGPRs) and loads the next item's 16 rows into another 24 registers three per tile over the item's first eight
+// tiles (loads the compiler does not see, waited for once at the item boundary); a 32-query tile is then two B pieces
+// per 32 dims, one MFMA each. The 8 waves of a workgroup hold 128 rows. VAR bits as probe's: 1 sync, 2 dma, 4 epi,
+// 8 items of 10 tiles, 16 hbm tiles.
+template <int VAR>
+__global__ __launch_bounds__(512, 1) void probe16(const h8* __restrict__ rows, const char* __restrict__ src,
+                                                  int src_tiles, int ntiles, float* out, unsigned long long* clk,
+                                                  const h8* __restrict__ big_rows, long long big_items) {
+  constexpr int WAVES = 8, PD = 2, NR = NK / 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* s_ready = reinterpret_cast<int*>(smem + 2 * BUF);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int i = tid; i < 2 * BUF / 16; i += WAVES * 64) {
+    const int v = (i * 2654435761u) >> 7;
+    reinterpret_cast<uint4*>(smem)[i] = make_uint4(v & 0x3BFF3BFF, (v >> 3) & 0x3BFF3BFF, v & 0x37FF37FF, 0x3C003C00 ^ (v & 0x03FF03FF));
+  }
+  if (tid == 0) *s_ready = 0;
+  __syncthreads();
+  h8 ra[NR], rn[NR];
+  const h8* rp = rows + ((size_t)(blockIdx.x * WAVES + wave) * NR) * 64 + lane;
+#pragma unroll
+  for (int r = 0; r < NR; ++r) { ra[r] = rp[r * 64]; rn[r] = rp[r * 64]; }
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  float sink = 0.f;
+  int cur = 0;
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  if (VAR & 1) {
+    if (lane == 0) __hip_atomic_fetch_add(s_ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  auto tile = [&](int t, h8 (&A)[NR], h8 (&N)[NR], auto j_c) __attribute__((always_inline)) {
+    constexpr int j = decltype(j_c)::value;  // tile of the item: registers 3j .. 3j + 2 of the next item at j < 8
+    if (VAR & 1) {
+      for (int i = 0; i < (1 << 20); ++i) {
+        if (__hip_atomic_load(s_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= WAVES * (t + 1)) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      asm volatile("" ::: "memory");
+    }
+    if ((VAR & 8) && t % 10 == 0) __builtin_amdgcn_s_waitcnt(0x0070);  // (the item's rows, loaded over its first 8 tiles)
+    const char* bb = smem + cur * BUF + lane * 16;
+    const int nxt = cur ^ 1;
+    char* sbuf = smem + nxt * BUF;
+    const int tsrc = (VAR & 16) ? (int)(((blockIdx.x & 7) * 1375 + t + 1) % src_tiles) : (int)((blockIdx.x + t) % src_tiles);
+    const v4i sdesc = uniform_desc(src + (size_t)tsrc * (NK + 1) * 1024, (NK + 1) * 1024);
+    const h8* nr = big_rows + ((size_t)(((long long)blockIdx.x * 7919 + (t / 10) * 131) % big_items) * WAVES + wave) * NR * 64 + lane;
+    f32x4 acc[2] = {z, z};
+    h8 b[PD + 1];
+#pragma unroll
+    for (int u = 0; u < PD; ++u) b[u] = *reinterpret_cast<const h8*>(bb + u * 1024);
+#pragma unroll
+    for (int s = 0; s < NK; ++s) {
+      if (s + PD < NK) b[(s + PD) % (PD + 1)] = *reinterpret_cast<const h8*>(bb + (s + PD) * 1024);
+      acc[s & 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[s >> 1], b[s % (PD + 1)], acc[s & 1], 0, 0, 0);
+      if constexpr ((VAR & 8) && j < 8) {
+        if (s == 12 || s == 24 || s == 36) {
+          const int r = 3 * j + s / 12 - 1;
+          asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(N[r]) : "v"(nr + r * 64) : "memory");
+        }
+      }
+      if (VAR & 2) {
+        if (s >= 1 && (s - 1) * WAVES <= NK) {
+          const int p = min((s - 1) * WAVES + wave, NK);
+          dma_b128(sdesc, sbuf + p * 1024, lane * 16, p * 1024);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (VAR & 2) __builtin_amdgcn_s_waitcnt(0x0070);
+    if (VAR & 1) {
+      asm volatile("" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(s_ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (VAR & 4) {
+      float am = fmaxf(fmaxf(acc[0][0], acc[0][1]), fmaxf(acc[0][2], acc[0][3]));
+      float am1 = fmaxf(fmaxf(acc[1][0], acc[1][1]), fmaxf(acc[1][2], acc[1][3]));
+      if (__ballot(fmaf(am, -2.f, 0.5f) < -1e30f || fmaf(am1, -2.f, 0.5f) < -1e30f)) sink += 1.f;
+      sink += am * 1e-30f;
+    } else {
+      sink += acc[0][0] + acc[1][1];
+    }
+    cur = nxt;
+  };
+  auto item = [&](int t, h8 (&A)[NR], h8 (&N)[NR]) __attribute__((always_inline)) {
+    tile(t + 0, A, N, IntC<0>{}); tile(t + 1, A, N, IntC<1>{}); tile(t + 2, A, N, IntC<2>{});
+    tile(t + 3, A, N, IntC<3>{}); tile(t + 4, A, N, IntC<4>{}); tile(t + 5, A, N, IntC<5>{});
+    tile(t + 6, A, N, IntC<6>{}); tile(t + 7, A, N, IntC<7>{}); tile(t + 8, A, N, IntC<8>{});
+    tile(t + 9, A, N, IntC<9>{});
+  };
+  for (int t = 0; t + 20 <= ntiles; t += 20) {
+    item(t, ra, rn);
+    item(t + 10, rn, ra);
+  }
+  __builtin_amdgcn_s_waitcnt(0x0070);
+  const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0 && wave == 0) {
+    clk[2 * blockIdx.x] = t1 - t0;
+    clk[2 * blockIdx.x + 1] = r1 - r0;
+  }
+  out[(size_t)(blockIdx.x * WAVES + wave) * 64 + lane] = sink;
+}
+
 const h8* g_big = nullptr;
 const char* g_q = nullptr;
 long long g_big_items = 1;
@@ -246,6 +352,37 @@ int run(const char* name, const h8* rows, const char* src, int src_tiles, float*
   for (int b = 0; b < grid; ++b) ghz += (double)h[2 * b] / (double)h[2 * b + 1] * 0.1;
   ghz /= grid;
   const double n_mfma = (double)grid * WAVES * ntiles * 2 * NK;
+  const double tf = n_mfma * 16 * 16 * 32 * 2 / (ms * 1e-3) / 1e12;
+  const double pipe = n_mfma / (grid * 4.0) * 16 / (ms * 1e-3 * ghz * 1e9);
+  printf("%-34s %8.3f ms  %7.1f TF/s  clock %.3f GHz  pipe busy %.3f  frac-of-2.5PF %.3f\n", name, ms, tf, ghz, pipe,
+         tf / 2500.0);
+  CHECK(hipEventDestroy(e0));
+  CHECK(hipEventDestroy(e1));
+  return 0;
+}
+
+template <int VAR>
+int run16(const char* name, const h8* rows, const char* src, int src_tiles, float* out, unsigned long long* clk,
+          int grid, int ntiles) {
+  const size_t lds = 2 * BUF + 64;
+  CHECK(hipFuncSetAttribute((const void*)probe16<VAR>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  for (int rep = 0; rep < 3; ++rep)
+    hipLaunchKernelGGL((probe16<VAR>), dim3(grid), dim3(512), lds, 0, rows, src, src_tiles, ntiles, out, clk, g_big, g_big_items);
+  CHECK(hipEventRecord(e0));
+  hipLaunchKernelGGL((probe16<VAR>), dim3(grid), dim3(512), lds, 0, rows, src, src_tiles, ntiles, out, clk, g_big, g_big_items);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  float ms = 0;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  std::vector<unsigned long long> h(2 * grid);
+  CHECK(hipMemcpy(h.data(), clk, sizeof(unsigned long long) * 2 * grid, hipMemcpyDeviceToHost));
+  double ghz = 0;
+  for (int b = 0; b < grid; ++b) ghz += (double)h[2 * b] / (double)h[2 * b + 1] * 0.1;
+  ghz /= grid;
+  const double n_mfma = (double)grid * 8 * ntiles * NK;  // one MFMA per piece per wave
   const double tf = n_mfma * 16 * 16 * 32 * 2 / (ms * 1e-3) / 1e12;
   const double pipe = n_mfma / (grid * 4.0) * 16 / (ms * 1e-3 * ghz * 1e9);
   printf("%-34s %8.3f ms  %7.1f TF/s  clock %.3f GHz  pipe busy %.3f  frac-of-2.5PF %.3f\n", name, ms, tf, ghz, pipe,
@@ -299,12 +436,12 @@ int main(int argc, char** argv) {
     CHECK(hipMemcpy(src, hs.data(), hs.size() * 2, hipMemcpyHostToDevice));
   }
   printf("grid %d, %d tiles per wave, 16x16x32 f16, 32 rows x 768 dims per wave in registers\n", grid, ntiles);
-  run<0, 2, 8>("loop only, PD 2, 8 waves", rows, src, src_tiles, out, clk, grid, ntiles);
-  run<7, 2, 8>("+sync +dma +epi", rows, src, src_tiles, out, clk, grid, ntiles);
-  run<7 + 2048, 2, 8>("+split sync (3 bufs) +dma +epi", rows, src, src_tiles, out, clk, grid, ntiles);
-  run<23, 2, 8>("+sync +dma +epi +hbm tiles", rows, src, big_tiles, out, clk, grid, ntiles);
-  run<23 + 2048, 2, 8>("+split sync +dma +epi +hbm tiles", rows, src, big_tiles, out, clk, grid, ntiles);
-  run<7, 2, 8>("+sync +dma +epi (again)", rows, src, src_tiles, out, clk, grid, ntiles);
-  run<7 + 2048, 2, 8>("+split sync +dma +epi (again)", rows, src, src_tiles, out, clk, grid, ntiles);
+  run<7, 2, 8>("32 rows: +sync +dma +epi", rows, src, src_tiles, out, clk, grid, ntiles);
+  run<15, 2, 8>("32 rows: +sync +dma +epi +items", rows, src, src_tiles, out, clk, grid, ntiles);
+  run<31 + 256, 2, 8>("32 rows: +items +hbm tiles (nt)", rows, src, big_tiles, out, clk, grid, ntiles);
+  run16<0>("16 rows: loop only", rows, src, src_tiles, out, clk, grid, ntiles);
+  run16<7>("16 rows: +sync +dma +epi", rows, src, src_tiles, out, clk, grid, ntiles);
+  run16<15>("16 rows: +sync +dma +epi +items (2-buf)", rows, src, src_tiles, out, clk, grid, ntiles);
+  run16<31>("16 rows: +items (2-buf) +hbm tiles", rows, src, big_tiles, out, clk, grid, ntiles);
   return 0;
 }
