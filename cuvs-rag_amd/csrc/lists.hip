@@ -16,10 +16,14 @@ __device__ __forceinline__ float4 ld4(const float* __restrict__ row, int c, int 
   return v;
 }
 
-// One wave per destination group: gathers its 32 source rows (sorted list
-// order), writes the interleaved [dp/8][32][8] image (one contiguous 1 KiB wave
-// store per k-step) and the row norms in the mivs k-order
-// (k = 8s+j then 8s+4+j, i.e. this lane's dim then its lane^32 partner's).
+// One wave per destination group: gathers its 32 source rows (sorted list order) into the group image (a row's
+// dims in 256-B blocks of 64, the 32 rows' blocks side by side: [dp/64][32][64]) and writes the row norms in the
+// mivs k-order (k = 8s+j then 8s+4+j). Per 64-dim block the copy moves whole 256-B row pieces -- lane (i, c) =
+// (lane >> 4, lane & 15) carries dims 4c .. 4c + 3 of rows 4 rb + i -- so each wave-instruction reads four 256-B
+// source segments and writes 1 KiB contiguous (the round-4 kernel moved 32-B pieces both ways: 2.2 TB/s,
+// build_roofline "pack"); the next block's loads are in flight while this one is stored. The norm chain runs over
+// a padded LDS copy of the block (row stride 68 floats: conflict-free ds_read_b128), lane (rr, h) = (lane & 31,
+// lane >> 5) holding dims 8t + 4h .. + 3 of row rr and taking its lane^32 partner's by shuffle, as before.
 __global__ __launch_bounds__(256) void k_pack(const float* __restrict__ src, int d, int dp,
                                               const int64_t* __restrict__ src_index,
                                               const int64_t* __restrict__ list_off,
@@ -28,42 +32,65 @@ __global__ __launch_bounds__(256) void k_pack(const float* __restrict__ src, int
                                               float* __restrict__ groups, float* __restrict__ norms,
                                               int64_t* __restrict__ ids_out, const int64_t* __restrict__ id_map,
                                               int64_t id_offset) {
-  const int lane = threadIdx.x & 63;
-  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (g >= n_groups) return;
-  const int rr = lane & 31, h = lane >> 5;
+  constexpr int LDSR = kRowBlk + 4;  // padded row stride of the staged block (floats)
+  __shared__ __attribute__((aligned(16))) float s_blk[4][kGroupRows * LDSR];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t g = (int64_t)blockIdx.x * 4 + w;
+  if (g >= n_groups) return;  // (no workgroup barrier below: each wave stages in its own LDS slice)
   const int l = group_list ? group_list[g] : 0;
-  const int64_t r = (g - list_goff[l]) * kGroupRows + rr;
+  const int64_t r0 = (g - list_goff[l]) * kGroupRows;
   const int64_t size = list_off[l + 1] - list_off[l];
-  const bool valid = r < size;
-  const int64_t sidx = list_off[l] + r;
-  const int64_t srow = valid ? (src_index ? src_index[sidx] : sidx) : 0;
-  const float* rowp = src + srow * (int64_t)d;
-  float* dst = groups + g * (int64_t)(kGroupRows * dp) + rr * kRowBlk + 4 * h;
+  const int i4 = lane >> 4, c = lane & 15;
+  const float* rp[8];
+  bool rv[8];
+#pragma unroll
+  for (int rb = 0; rb < 8; ++rb) {
+    const int64_t r = r0 + 4 * rb + i4;
+    rv[rb] = r < size;
+    const int64_t sidx = list_off[l] + r;
+    rp[rb] = src + (rv[rb] ? (src_index ? src_index[sidx] : sidx) : 0) * (int64_t)d;
+  }
+  float* gb = groups + g * (int64_t)(kGroupRows * dp) + (int64_t)i4 * kRowBlk + 4 * c;
+  float* sb = s_blk[w];
+  const int rr = lane & 31, h = lane >> 5;
   float acc = 0.0f;
-  const int S = dp >> 3;  // (a multiple of 8: dp % 64 == 0)
-  // eight k-steps' loads in flight before their stores: one at a time, each wave waited out a gather of 32 rows'
-  // 32-B pieces per k-step (2.2 TB/s, build_roofline "pack")
-  constexpr int U = 8;
-  for (int s0 = 0; s0 < S; s0 += U) {
-    float4 v[U];
+  const int NB = dp / kRowBlk;
+  float4 v[8];
+  auto load = [&](int blk, float4 (&o)[8]) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (valid) v[u] = ld4(rowp, 8 * (s0 + u) + 4 * h, d);
+    for (int rb = 0; rb < 8; ++rb) {
+      o[rb] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (rv[rb]) o[rb] = ld4(rp[rb], kRowBlk * blk + 4 * c, d);
+    }
+  };
+  load(0, v);
+  for (int blk = 0; blk < NB; ++blk) {
+    float4 nv[8];
+    if (blk + 1 < NB) load(blk + 1, nv);
+#pragma unroll
+    for (int rb = 0; rb < 8; ++rb) {
+      *reinterpret_cast<float4*>(gb + (int64_t)blk * kRowBlkStride + 4 * rb * kRowBlk) = v[rb];
+      *reinterpret_cast<float4*>(sb + (4 * rb + i4) * LDSR + 4 * c) = v[rb];
+    }
+    // (one wave's LDS operations complete in order: its reads below see its stores above)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const float4 u = *reinterpret_cast<const float4*>(sb + rr * LDSR + 8 * t + 4 * h);
+      const float px = __shfl_xor(u.x, 32), py = __shfl_xor(u.y, 32);
+      const float pz = __shfl_xor(u.z, 32), pw = __shfl_xor(u.w, 32);
+      acc = fmaf(u.x, u.x, acc); acc = fmaf(px, px, acc);
+      acc = fmaf(u.y, u.y, acc); acc = fmaf(py, py, acc);
+      acc = fmaf(u.z, u.z, acc); acc = fmaf(pz, pz, acc);
+      acc = fmaf(u.w, u.w, acc); acc = fmaf(pw, pw, acc);
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      *reinterpret_cast<float4*>(dst + row_blk8(s0 + u)) = v[u];
-      const float px = __shfl_xor(v[u].x, 32), py = __shfl_xor(v[u].y, 32);
-      const float pz = __shfl_xor(v[u].z, 32), pw = __shfl_xor(v[u].w, 32);
-      acc = fmaf(v[u].x, v[u].x, acc); acc = fmaf(px, px, acc);
-      acc = fmaf(v[u].y, v[u].y, acc); acc = fmaf(py, py, acc);
-      acc = fmaf(v[u].z, v[u].z, acc); acc = fmaf(pz, pz, acc);
-      acc = fmaf(v[u].w, v[u].w, acc); acc = fmaf(pw, pw, acc);
-    }
+    for (int rb = 0; rb < 8; ++rb) v[rb] = nv[rb];
   }
   if (h == 0) {
+    const int64_t r = r0 + rr;
+    const bool valid = r < size;
+    const int64_t sidx = list_off[l] + r;
+    const int64_t srow = valid ? (src_index ? src_index[sidx] : sidx) : 0;
     const int64_t pos = g * kGroupRows + rr;
     norms[pos] = valid ? acc : INFINITY;
     if (ids_out) ids_out[pos] = valid ? (id_map ? id_map[srow] : srow + id_offset) : (int64_t)-1;
