@@ -628,7 +628,7 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
 
 // K11. One wave per query (4 per workgroup; every wave reaches every barrier).
 template <int METRIC>
-__global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_pf_refine(PfRefineArgs a) {
   __shared__ float s_ck[4][kPfCap];
   __shared__ int s_cp[4][kPfCap];
   __shared__ __attribute__((aligned(16))) float s_qv[4][1024];
@@ -745,27 +745,57 @@ __global__ __launch_bounds__(256) void k_pf_refine(PfRefineArgs a) {
     if (w) atomicAdd(reinterpret_cast<unsigned long long*>(a.n_window), (unsigned long long)w);
   }
 
-  // phase 3: exact keys in the pinned order (oracle orc_dot), then a bitonic sort by (key, id)
+  // phase 3: exact keys in the pinned order (oracle orc_dot), then a bitonic sort by (key, id).
+  // Eight lanes per window row, eight rows per pass: lane (j, p) = (lane >> 3, lane & 7) loads the 8-dim blocks
+  // b = 8 B + p of row j (32 B each, the group of eight reading a whole 256-B row block), every block of the pass in
+  // flight at once, and the row's one fmaf chain runs over the blocks in order b = 0, 1, 2, ... by handing the
+  // accumulator to the next lane of the group with a DPP move (row_shr:1; part 7 -> part 0 of the next 64-dim
+  // block by row_shl:7): lane (j, h) extends it at hop h, the other lanes' results are discarded. One lane per row
+  // issued 192 16-B loads per row (12 lanes active), ~8 dependent memory rounds a query.
   float P = INFINITY;
   int64_t id = LLONG_MAX;
+  if (live && !ovf) {  // (wave-uniform)
+    const int j8 = lane >> 3, p8 = lane & 7;
+    const int nB = a.dp >> 6;
+    const float* qv = s_qv[wv];
+    float* s_dot = s_ck[wv];  // (the window's approximate keys are dead: their slots take the dots)
+    constexpr int CH = 12;    // 64-dim blocks of a pass in flight (d = 768: the whole row)
+    for (int r0 = 0; r0 < cnt; r0 += 8) {
+      const int rj = r0 + j8;
+      const float* rowp = a.groups + row_elem(s_cp[wv][rj < cnt ? rj : r0], 0, a.dp) + 8 * p8;
+      float acc = 0.0f;
+      for (int B0 = 0; B0 < nB; B0 += CH) {
+        float4 x[CH][2];
+#pragma unroll
+        for (int u = 0; u < CH; ++u)
+          if (B0 + u < nB) {
+            x[u][0] = *reinterpret_cast<const float4*>(rowp + (int64_t)(B0 + u) * kRowBlkStride);
+            x[u][1] = *reinterpret_cast<const float4*>(rowp + (int64_t)(B0 + u) * kRowBlkStride + 4);
+          }
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          if (B0 + u >= nB) break;
+          const int b = 8 * (B0 + u) + p8;
+          const float4 y0 = *reinterpret_cast<const float4*>(qv + 8 * b);
+          const float4 y1 = *reinterpret_cast<const float4*>(qv + 8 * b + 4);
+          const float4 x0 = x[u][0], x1 = x[u][1];
+#pragma unroll
+          for (int h = 0; h < 8; ++h) {
+            if (h > 0) acc = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, acc), 0x111, 0xF, 0xF, false));
+            else if (B0 + u > 0) acc = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, acc), 0x107, 0xF, 0xF, false));
+            acc = fmaf(x0.x, y0.x, acc); acc = fmaf(x1.x, y1.x, acc);
+            acc = fmaf(x0.y, y0.y, acc); acc = fmaf(x1.y, y1.y, acc);
+            acc = fmaf(x0.z, y0.z, acc); acc = fmaf(x1.z, y1.z, acc);
+            acc = fmaf(x0.w, y0.w, acc); acc = fmaf(x1.w, y1.w, acc);
+          }
+        }
+      }
+      if (p8 == 7 && rj < cnt) s_dot[rj] = acc;  // (part 7 ends the row's chain)
+    }
+  }
   if (live && !ovf && lane < cnt) {
     const int pos = s_cp[wv][lane];
-    const int nb = a.dp >> 3;
-    // the row's 8-dim block b at rowp + row_blk8(b) (64-B row blocks: a candidate reads whole blocks)
-    const float* rowp = a.groups + row_elem(pos, 0, a.dp);
-    const float* qv = s_qv[wv];
-    float acc = 0.0f;
-#pragma unroll 12
-    for (int b = 0; b < nb; ++b) {
-      const float4 x0 = *reinterpret_cast<const float4*>(rowp + row_blk8(b));
-      const float4 x1 = *reinterpret_cast<const float4*>(rowp + row_blk8(b) + 4);
-      const float4 y0 = *reinterpret_cast<const float4*>(qv + 8 * b);
-      const float4 y1 = *reinterpret_cast<const float4*>(qv + 8 * b + 4);
-      acc = fmaf(x0.x, y0.x, acc); acc = fmaf(x1.x, y1.x, acc);
-      acc = fmaf(x0.y, y0.y, acc); acc = fmaf(x1.y, y1.y, acc);
-      acc = fmaf(x0.z, y0.z, acc); acc = fmaf(x1.z, y1.z, acc);
-      acc = fmaf(x0.w, y0.w, acc); acc = fmaf(x1.w, y1.w, acc);
-    }
+    const float acc = s_ck[wv][lane];
     if (METRIC == kL2) {
       const float v = fmaf(-2.0f, acc, a.row_norms[pos] + qn);
       P = v > 0.0f ? v : 0.0f;
@@ -873,6 +903,7 @@ __global__ __launch_bounds__(256) void k_pf_verify(PfRefineArgs a) {
     float P = INFINITY;
     const int nvf = live ? (cnt < 64 ? cnt : 64) : 0;
     const int nb = a.dp >> 3;
+    // (one nominee's row at a time, at 8 waves / SIMD: four rows in flight at 4 waves / SIMD measured 87 -> 93 us)
     for (int n = 0; n < nvf; ++n) {
       const int pos = s_cp[wv][n];
       const float* rowp = a.groups + row_elem(pos, 0, a.dp);
@@ -935,16 +966,23 @@ __global__ void k_groups_to_half(const float* __restrict__ groups, int64_t n_gro
     const int nb = dp >> 3;
     const float sc = ldexpf(1.0f, hx_exp), isc = ldexpf(1.0f, -hx_exp);
     const float* row = groups + row_elem(g * kGroupRows + r, 0, dp);
-    for (int b = 0; b < nb; ++b) {
-      const int64_t o = ((g * nb + b) * kGroupRows + r) * 8;  // (the fp16 copy: [dp/8][32][8] per group)
-      const float4 x0 = *reinterpret_cast<const float4*>(row + row_blk8(b));
-      const float4 x1 = *reinterpret_cast<const float4*>(row + row_blk8(b) + 4);
-      uint4 pk;
-      pk.x = pf_to_half(x0.x, sc, isc, res) | ((unsigned)pf_to_half(x0.y, sc, isc, res) << 16);
-      pk.y = pf_to_half(x0.z, sc, isc, res) | ((unsigned)pf_to_half(x0.w, sc, isc, res) << 16);
-      pk.z = pf_to_half(x1.x, sc, isc, res) | ((unsigned)pf_to_half(x1.y, sc, isc, res) << 16);
-      pk.w = pf_to_half(x1.z, sc, isc, res) | ((unsigned)pf_to_half(x1.w, sc, isc, res) << 16);
-      *reinterpret_cast<uint4*>(out + o) = pk;
+    // a 64-dim block of the row (256 B, 16 loads) in flight at a time (dp % 64 == 0): one 32-B step at a time the
+    // copy ran at 3.7 TB/s (build_roofline "fp16_copy")
+    for (int b0 = 0; b0 < nb; b0 += 8) {
+      float4 x[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) x[u] = *reinterpret_cast<const float4*>(row + row_blk8(b0 + (u >> 1)) + 4 * (u & 1));
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int64_t o = ((g * nb + b0 + u) * kGroupRows + r) * 8;  // (the fp16 copy: [dp/8][32][8] per group)
+        const float4 x0 = x[2 * u], x1 = x[2 * u + 1];
+        uint4 pk;
+        pk.x = pf_to_half(x0.x, sc, isc, res) | ((unsigned)pf_to_half(x0.y, sc, isc, res) << 16);
+        pk.y = pf_to_half(x0.z, sc, isc, res) | ((unsigned)pf_to_half(x0.w, sc, isc, res) << 16);
+        pk.z = pf_to_half(x1.x, sc, isc, res) | ((unsigned)pf_to_half(x1.y, sc, isc, res) << 16);
+        pk.w = pf_to_half(x1.z, sc, isc, res) | ((unsigned)pf_to_half(x1.w, sc, isc, res) << 16);
+        *reinterpret_cast<uint4*>(out + o) = pk;
+      }
     }
   }
   float rn = sqrtf(res) * (1.0f + 0x1p-12f);
