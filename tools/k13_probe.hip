@@ -73,7 +73,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void probe(const h8* __restrict__ ro
                                                        long long big_items, const char* __restrict__ qarr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NBUF = (VAR & 2048) ? 3 : 2;
-  constexpr int LANDED_AT = 40;
+  constexpr int LANDED_AT = (VAR & 4096) ? 16 : 40;  // (4096: the landed signal early, so waves may lag ~2/3 tile)
   int* s_ready = reinterpret_cast<int*>(smem + NBUF * BUF);
   int* s_done = s_ready + 1;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -94,6 +94,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void probe(const h8* __restrict__ ro
   const f32x4 z = {0.f, 0.f, 0.f, 0.f};
   if (VAR & 1) {
     if (lane == 0) __hip_atomic_fetch_add(s_ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  // VAR & 4096 (with 2048): waves 4..7 start about half a k-loop late, so each SIMD's two waves run their epilogues
+  // and waits under each other's MFMAs
+  if ((VAR & 4096) && wave >= 4) {
+    for (int i = 0; i < 24; ++i) __builtin_amdgcn_s_sleep(1);
   }
   // VAR & 32: staggered item transitions -- wave w reloads in the tiles t with (t + o_w) % 10 == 9, o_w spread over
   // the 10 tiles of an item (SIMD partners w, w + 4 five tiles apart; VAR & 64: two phases only, waves 4-7 at 5).
@@ -436,12 +441,12 @@ int main(int argc, char** argv) {
     CHECK(hipMemcpy(src, hs.data(), hs.size() * 2, hipMemcpyHostToDevice));
   }
   printf("grid %d, %d tiles per wave, 16x16x32 f16, 32 rows x 768 dims per wave in registers\n", grid, ntiles);
-  run<7, 2, 8>("32 rows: +sync +dma +epi", rows, src, src_tiles, out, clk, grid, ntiles);
-  run<15, 2, 8>("32 rows: +sync +dma +epi +items", rows, src, src_tiles, out, clk, grid, ntiles);
-  run<31 + 256, 2, 8>("32 rows: +items +hbm tiles (nt)", rows, src, big_tiles, out, clk, grid, ntiles);
-  run16<0>("16 rows: loop only", rows, src, src_tiles, out, clk, grid, ntiles);
-  run16<7>("16 rows: +sync +dma +epi", rows, src, src_tiles, out, clk, grid, ntiles);
-  run16<15>("16 rows: +sync +dma +epi +items (2-buf)", rows, src, src_tiles, out, clk, grid, ntiles);
-  run16<31>("16 rows: +items (2-buf) +hbm tiles", rows, src, big_tiles, out, clk, grid, ntiles);
+  run<7, 2, 8>("+sync +dma +epi", rows, src, src_tiles, out, clk, grid, ntiles);
+  run<7 + 2048, 2, 8>("+split sync (3 bufs) +dma +epi", rows, src, src_tiles, out, clk, grid, ntiles);
+  run<7 + 2048 + 4096, 2, 8>("+split sync, waves 4-7 offset", rows, src, src_tiles, out, clk, grid, ntiles);
+  run<23, 2, 8>("+sync +dma +epi +hbm tiles", rows, src, big_tiles, out, clk, grid, ntiles);
+  run<23 + 2048 + 4096, 2, 8>("+split sync offset +hbm tiles", rows, src, big_tiles, out, clk, grid, ntiles);
+  run<7, 2, 8>("+sync +dma +epi (again)", rows, src, src_tiles, out, clk, grid, ntiles);
+  run<7 + 2048 + 4096, 2, 8>("+split sync offset (again)", rows, src, src_tiles, out, clk, grid, ntiles);
   return 0;
 }
