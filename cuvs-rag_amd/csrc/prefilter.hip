@@ -903,27 +903,51 @@ __global__ __launch_bounds__(256) void k_pf_verify(PfRefineArgs a) {
     float P = INFINITY;
     const int nvf = live ? (cnt < 64 ? cnt : 64) : 0;
     const int nb = a.dp >> 3;
-    // (one nominee's row at a time, at 8 waves / SIMD: four rows in flight at 4 waves / SIMD measured 87 -> 93 us)
-    for (int n = 0; n < nvf; ++n) {
-      const int pos = s_cp[wv][n];
-      const float* rowp = a.groups + row_elem(pos, 0, a.dp);
-      float acc = 0.0f;
-      for (int b = lane; b < nb; b += 64) {
-        const float4 x0 = *reinterpret_cast<const float4*>(rowp + row_blk8(b));
-        const float4 x1 = *reinterpret_cast<const float4*>(rowp + row_blk8(b) + 4);
-        const float4 y0 = *reinterpret_cast<const float4*>(s_qv[wv] + 8 * b);
-        const float4 y1 = *reinterpret_cast<const float4*>(s_qv[wv] + 8 * b + 4);
-        acc = fmaf(x0.x, y0.x, acc); acc = fmaf(x0.y, y0.y, acc); acc = fmaf(x0.z, y0.z, acc); acc = fmaf(x0.w, y0.w, acc);
-        acc = fmaf(x1.x, y1.x, acc); acc = fmaf(x1.y, y1.y, acc); acc = fmaf(x1.z, y1.z, acc); acc = fmaf(x1.w, y1.w, acc);
+    // two nominees' rows in flight at a time (lane: 8-dim blocks lane, lane + 64; dp <= 1024), at 8 waves / SIMD:
+    // one row at a time, each nominee was a dependent memory round of its own (~10 per query); four rows at a time
+    // took 112 VGPRs (4 waves / SIMD) and measured 87 -> 93 us
+    constexpr int RW = 2;
+    for (int n0 = 0; n0 < nvf; n0 += RW) {
+      float4 xs[RW][2][2];
+      int pos[RW];
+#pragma unroll
+      for (int r = 0; r < RW; ++r) {
+        pos[r] = s_cp[wv][n0 + r < nvf ? n0 + r : n0];
+        const float* rowp = a.groups + row_elem(pos[r], 0, a.dp);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int b = lane + 64 * i;
+          xs[r][i][0] = xs[r][i][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (n0 + r < nvf && b < nb) {
+            xs[r][i][0] = *reinterpret_cast<const float4*>(rowp + row_blk8(b));
+            xs[r][i][1] = *reinterpret_cast<const float4*>(rowp + row_blk8(b) + 4);
+          }
+        }
       }
 #pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
-      if (lane == n) {
-        if (METRIC == kL2) {
-          const float v = fmaf(-2.0f, acc, a.row_norms[pos] + qn);
-          P = v > 0.0f ? v : 0.0f;
-        } else {
-          P = -acc;
+      for (int r = 0; r < RW; ++r) {
+        if (n0 + r >= nvf) break;
+        float acc = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int b = lane + 64 * i;
+          if (b < nb) {
+            const float4 x0 = xs[r][i][0], x1 = xs[r][i][1];
+            const float4 y0 = *reinterpret_cast<const float4*>(s_qv[wv] + 8 * b);
+            const float4 y1 = *reinterpret_cast<const float4*>(s_qv[wv] + 8 * b + 4);
+            acc = fmaf(x0.x, y0.x, acc); acc = fmaf(x0.y, y0.y, acc); acc = fmaf(x0.z, y0.z, acc); acc = fmaf(x0.w, y0.w, acc);
+            acc = fmaf(x1.x, y1.x, acc); acc = fmaf(x1.y, y1.y, acc); acc = fmaf(x1.z, y1.z, acc); acc = fmaf(x1.w, y1.w, acc);
+          }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+        if (lane == n0 + r) {
+          if (METRIC == kL2) {
+            const float v = fmaf(-2.0f, acc, a.row_norms[pos[r]] + qn);
+            P = v > 0.0f ? v : 0.0f;
+          } else {
+            P = -acc;
+          }
         }
       }
     }
