@@ -153,7 +153,9 @@ int32_t mivs_ivf_flat_extend(mivs_index_t index, void* stream, const float* d_ne
                              int64_t n_new);
 /* ---- replaces cuvs.neighbors.ivf_flat.search(SearchParams(n_probes), index, q, k)
  *      (improved_multi_gpu_rag.py:225-227, cuvs-2gpu-main.ipynb:1801) ----
- *  d_probes (optional, may be NULL): [nq][n_probes] int32 probed list ids in probe order */
+ *  d_probes (optional, may be NULL): [nq][n_probes] int32 probed list ids in probe order.
+ *  Enqueued on `stream`; for k <= 16 on an index with the pre-filter copies the call returns without waiting
+ *  for the device. */
 int32_t mivs_ivf_flat_search(mivs_index_t index, void* stream, const float* d_queries, int64_t nq, int32_t k,
                              int32_t n_probes, float* d_distances, int64_t* d_neighbors, int32_t* d_probes);
 int32_t mivs_ivf_flat_get_centroids(mivs_index_t index, void* stream, float* d_out /* [n_lists][dim] */);
