@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void k_pack(const float* __restrict__ src, int
     if (blk + 1 < NB) load(blk + 1, nv);
 #pragma unroll
     for (int rb = 0; rb < 8; ++rb) {
-      *reinterpret_cast<float4*>(gb + (int64_t)blk * kRowBlkStride + 4 * rb * kRowBlk) = v[rb];
+      __builtin_nontemporal_store(__builtin_bit_cast(f32x4, v[rb]), reinterpret_cast<f32x4*>(gb + (int64_t)blk * kRowBlkStride + 4 * rb * kRowBlk));
       *reinterpret_cast<float4*>(sb + (4 * rb + i4) * LDSR + 4 * c) = v[rb];
     }
     // (one wave's LDS operations complete in order: its reads below see its stores above)

@@ -966,6 +966,8 @@ __global__ __launch_bounds__(256) void k_pf_verify(PfRefineArgs a) {
   }
 }
 
+typedef unsigned int pf_u32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ int pf_exp_for(float m) {
   if (!(m > 0.0f) || !(m < INFINITY)) return 0;
   int e = 14 - ilogbf(m);  // m * 2^e in [2^14, 2^15)
@@ -1005,7 +1007,7 @@ __global__ void k_groups_to_half(const float* __restrict__ groups, int64_t n_gro
         pk.y = pf_to_half(x0.z, sc, isc, res) | ((unsigned)pf_to_half(x0.w, sc, isc, res) << 16);
         pk.z = pf_to_half(x1.x, sc, isc, res) | ((unsigned)pf_to_half(x1.y, sc, isc, res) << 16);
         pk.w = pf_to_half(x1.z, sc, isc, res) | ((unsigned)pf_to_half(x1.w, sc, isc, res) << 16);
-        *reinterpret_cast<uint4*>(out + o) = pk;
+        __builtin_nontemporal_store(__builtin_bit_cast(pf_u32x4, pk), reinterpret_cast<pf_u32x4*>(out + o));
       }
     }
   }
@@ -1739,7 +1741,7 @@ __global__ void k_groups_to_f8(const float* __restrict__ groups, int64_t n_group
       v[8 * e + 0] = x0.x; v[8 * e + 1] = x0.y; v[8 * e + 2] = x0.z; v[8 * e + 3] = x0.w;
       v[8 * e + 4] = x1.x; v[8 * e + 5] = x1.y; v[8 * e + 6] = x1.z; v[8 * e + 7] = x1.w;
     }
-    *reinterpret_cast<uint4*>(out + t * 16) = f8_pack16(v, sc);
+    __builtin_nontemporal_store(__builtin_bit_cast(pf_u32x4, f8_pack16(v, sc)), reinterpret_cast<pf_u32x4*>(out + t * 16));
   }
 }
 
