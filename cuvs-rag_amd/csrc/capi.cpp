@@ -832,6 +832,8 @@ mivs_index_memory index_memory(const mivs_index_s* idx) {
 bool copy_fits(const mivs_index_s* idx, size_t bytes) {
   size_t fr = 0, tot = 0;
   if (hipMemGetInfo(&fr, &tot) != hipSuccess) return false;
+  int dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess) fr += BlockCache::get().cached(dev);  // (blocks this process holds for reuse)
   const char* e = getenv("MIVS_INDEX_HBM_FRAC");
   const double frac = e ? atof(e) : 0.6;
   return fr >= bytes + ((size_t)4 << 30) && (double)index_memory(idx).total_bytes + (double)bytes <= frac * (double)tot;

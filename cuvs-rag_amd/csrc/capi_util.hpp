@@ -54,25 +54,120 @@ int32_t guarded(F&& f) {
   }
 }
 
+// Large device blocks released by Bufs, kept for reuse by later Bufs of the process. A fresh
+// hipMalloc of tens of GB can stall for seconds while the pages are cleared -- a timed 10M build after an untimed
+// one spent 5.4 s in its first allocations once in four runs (profiles/r05_variants_build.txt) -- whereas a block
+// this process freed is handed out again as it is. Blocks of at least kCacheMin bytes are cached, up to a quarter of
+// the device's memory (the rest is freed: other allocators in the process, torch's among them, do not see this
+// cache); a request takes the smallest cached block of its device within 1/8 above its size; an allocation that
+// fails for memory frees the device's cached blocks and tries again.
+struct BlockCache {
+  static constexpr size_t kCacheMin = (size_t)64 << 20;
+  struct Blk {
+    void* p;
+    size_t n;
+    int dev;
+  };
+  std::mutex mu;
+  std::vector<Blk> blocks;
+  static BlockCache& get() {
+    static BlockCache* c = new BlockCache;  // (never destroyed: Bufs may be released during process exit)
+    return *c;
+  }
+  void* take(size_t want, int dev, size_t* got) {
+    std::lock_guard<std::mutex> g(mu);
+    int best = -1;
+    for (int i = 0; i < (int)blocks.size(); ++i)
+      if (blocks[i].dev == dev && blocks[i].n >= want && blocks[i].n - want <= want / 8 &&
+          (best < 0 || blocks[i].n < blocks[best].n))
+        best = i;
+    if (best < 0) return nullptr;
+    const Blk b = blocks[best];
+    blocks.erase(blocks.begin() + best);
+    *got = b.n;
+    return b.p;
+  }
+  void put(void* p, size_t n, int dev) {
+    std::lock_guard<std::mutex> g(mu);
+    blocks.push_back(Blk{p, n, dev});
+  }
+  void flush(int dev) {
+    std::lock_guard<std::mutex> g(mu);
+    for (size_t i = 0; i < blocks.size();) {
+      if (blocks[i].dev == dev) {
+        (void)hipFree(blocks[i].p);
+        blocks.erase(blocks.begin() + i);
+      } else {
+        ++i;
+      }
+    }
+  }
+  size_t cached(int dev) {
+    std::lock_guard<std::mutex> g(mu);
+    size_t t = 0;
+    for (const Blk& b : blocks)
+      if (b.dev == dev) t += b.n;
+    return t;
+  }
+};
+
 // owning device buffer (grow-only when reused as workspace)
 struct Buf {
   void* p = nullptr;
-  size_t n = 0;
+  size_t n = 0;    // bytes asked for (what the index footprint reports)
+  size_t cap = 0;  // bytes of the block (a cached block may be up to 1/8 larger)
+  int dev = -1;
   Buf() = default;
   Buf(const Buf&) = delete;
   Buf& operator=(const Buf&) = delete;
   ~Buf() { release(); }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) {
+      if (cap >= BlockCache::kCacheMin) {
+        // (hipFree waited for the device's work; a cached block may be handed out at once, so wait here)
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (cur != dev) (void)hipSetDevice(dev);
+        (void)hipDeviceSynchronize();
+        size_t fr = 0, tot = 0;
+        const bool keep = hipMemGetInfo(&fr, &tot) == hipSuccess && BlockCache::get().cached(dev) + cap <= tot / 4;
+        if (keep) BlockCache::get().put(p, cap, dev);
+        else (void)hipFree(p);
+        if (cur != dev) (void)hipSetDevice(cur);
+      } else {
+        (void)hipFree(p);
+      }
+    }
     p = nullptr;
     n = 0;
+    cap = 0;
   }
   void reserve(size_t bytes) {
-    if (bytes <= n && p) return;
+    if (p && bytes <= cap) {
+      if (bytes > n) n = bytes;
+      return;
+    }
     if (p) HIPCHK(hipDeviceSynchronize());  // in-flight work may still use the old workspace
     release();
-    HIPCHK(hipMalloc(&p, bytes > 0 ? bytes : 16));
-    n = bytes;
+    int d = 0;
+    HIPCHK(hipGetDevice(&d));
+    const size_t want = bytes > 0 ? bytes : 16;
+    size_t got = 0;
+    if (want >= BlockCache::kCacheMin) p = BlockCache::get().take(want, d, &got);
+    if (!p) {
+      hipError_t e = hipMalloc(&p, want);
+      if (e == hipErrorOutOfMemory) {
+        (void)hipGetLastError();
+        BlockCache::get().flush(d);
+        e = hipMalloc(&p, want);
+      }
+      if (e != hipSuccess) p = nullptr;
+      HIPCHK(e);
+      got = want;
+    }
+    n = want;
+    cap = got;
+    dev = d;
   }
   template <class T>
   T* as() const { return static_cast<T*>(p); }

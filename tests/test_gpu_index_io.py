@@ -118,3 +118,28 @@ def test_extend_with_explicit_ids(mivs_lib):
     # a new row finds itself at distance 0 under its explicit id
     d, i = ivf_flat.search(ivf_flat.SearchParams(n_probes=6), idx, _gpu(x[2500:2501]), 1)
     assert int(i[0, 0]) == 10_001_500 and float(d[0, 0]) <= 1e-5
+
+
+def test_rebuild_reuses_cached_blocks_same_index(mivs_lib):
+    """Buf's block cache (capi_util.hpp): an index built after another was closed gets the closed one's device
+    blocks back (the sizes match) and must come out identical -- lists, rows, footprint and search bits -- as must
+    a third build while the second is alive (fresh allocations)."""
+    from mivs.neighbors import ivf_flat
+
+    x, q = _data(120000, 768, 5), _data(64, 768, 6)  # (rows 370 MB: above the cache's 64 MB block floor)
+    p = ivf_flat.IndexParams(n_lists=64, kmeans_n_iters=3)
+    a = ivf_flat.build(p, _gpu(x))
+    da, ia = ivf_flat.search(ivf_flat.SearchParams(n_probes=8), a, _gpu(q), 10)
+    ref = (a.list_sizes.numpy().copy(), a.list_ids().cpu().numpy(), a.memory())
+    a.close()
+    b = ivf_flat.build(p, _gpu(x))  # (takes a's cached blocks)
+    c = ivf_flat.build(p, _gpu(x))  # (b is alive: new blocks)
+    for idx in (b, c):
+        d, i = ivf_flat.search(ivf_flat.SearchParams(n_probes=8), idx, _gpu(q), 10)
+        np.testing.assert_array_equal(i.cpu().numpy(), ia.cpu().numpy())
+        np.testing.assert_array_equal(_bits(d.cpu().numpy()), _bits(da.cpu().numpy()))
+        np.testing.assert_array_equal(idx.list_sizes.numpy(), ref[0])
+        np.testing.assert_array_equal(idx.list_ids().cpu().numpy(), ref[1])
+        assert idx.memory() == ref[2]
+    b.close()
+    c.close()
