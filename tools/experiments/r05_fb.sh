@@ -21,4 +21,4 @@ for ln in open('$O/b$m-$r.log'):
   done
 done
 cat $O/probe.log
-bash tools/r05_qsweep.sh ${1:-r05fb}_q
+bash tools/experiments/r05_qsweep.sh ${1:-r05fb}_q
