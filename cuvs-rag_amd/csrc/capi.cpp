@@ -1007,8 +1007,10 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
 // all take their size from that count on the device, so the search enqueues and returns without a host round trip.
 // An empty fallback is three launches that leave at once (~10 us of GPU time, against the ~55-90 us turnaround of
 // reading the count on the host). MIVS_FALLBACK_SYNC=1 keeps the host-sized path (A/B runs).
-bool device_fallback_ok(const mivs_index_s* idx, int k) {
-  return env_int("MIVS_FALLBACK_SYNC", 0) == 0 && idx->kind == 0 && k <= kMaxK && idx->lists.n_lists <= probe_map_dev_max_lists();
+// (the device-sized probe map is one workgroup: up to 2M (query, probe) entries, ~1 ms when every query of such a batch
+// falls back; beyond that the host-sized path keeps the multi-workgroup map)
+bool device_fallback_ok(const mivs_index_s* idx, int k, int64_t nq, int np) {
+  return env_int("MIVS_FALLBACK_SYNC", 0) == 0 && nq * (int64_t)np <= ((int64_t)1 << 21) && idx->kind == 0 && k <= kMaxK && idx->lists.n_lists <= probe_map_dev_max_lists();
 }
 
 void exact_fallback_on_device(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np,
@@ -1099,7 +1101,7 @@ void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_
   r.n_window = reinterpret_cast<int64_t*>(ws.pf_stats.as<char>() + 8);
   HIPCHK(launch_pf_refine(r, s));
   if (kth_out) return;
-  if (fallback_pf && device_fallback_ok(idx, k)) {  // K13's unproven queries: no host round trip
+  if (fallback_pf && device_fallback_ok(idx, k, nq, np)) {  // K13's unproven queries: no host round trip
     exact_fallback_on_device(idx, s, q, nq, k, np, out_d, out_i);
     idx->last_stats_dev = true;
     return;

@@ -317,3 +317,26 @@ def test_index_memory_single_fp32_copy_and_fp8_budget(flat_data, mivs_lib, monke
     np.testing.assert_array_equal(_bits(d1), _bits(d0))
     a.close()
     b.close()
+
+
+def test_back_to_back_searches_without_sync(ivf, flat_data):
+    """the k <= 16 search is stream-ordered (no host round trip since round 5): several searches enqueued back to back
+    on one stream, of different batch sizes (one grows the workspaces), each equal to the same search run alone"""
+    from mivs.neighbors import ivf_flat
+
+    idx, _ = ivf
+    _, q = flat_data
+    sp = ivf_flat.SearchParams(n_probes=8)
+    qt = torch.from_numpy(q).cuda()
+    # (batch, k): k = 40 takes the large-k path (K16, host-sized) between stream-ordered ones
+    parts = [(qt[:50], 10), (qt[50:], 10), (qt[:7], 16), (qt, 40), (qt, 5), (qt[:1], 10)]
+    alone = []
+    for p, k in parts:
+        d, i = ivf_flat.search(sp, idx, p, k)
+        torch.cuda.synchronize()
+        alone.append((d.cpu().numpy(), i.cpu().numpy()))
+    outs = [ivf_flat.search(sp, idx, p, k) for p, k in parts]  # (no synchronisation in between)
+    torch.cuda.synchronize()
+    for (d, i), (d0, i0) in zip(outs, alone):
+        np.testing.assert_array_equal(i.cpu().numpy(), i0)
+        np.testing.assert_array_equal(_bits(d.cpu().numpy()), _bits(d0))
