@@ -130,6 +130,25 @@ def _descending(metric: str) -> bool:
     return str(metric).lower() in ("inner_product", "innerproduct", "ip", "dot")
 
 
+def _to_host(ts: List[torch.Tensor]) -> List[np.ndarray]:
+    """numpy copies of tensors on any devices (or the host): device tensors are copied into pinned host buffers
+    asynchronously on their device's current stream, then every device involved is synchronised once."""
+    outs, devs = [], set()
+    for t in ts:
+        t = t.detach()
+        if t.is_cuda:
+            with torch.cuda.device(t.device):
+                h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+                h.copy_(t, non_blocking=True)
+            devs.add(t.device.index)
+            outs.append(h)
+        else:
+            outs.append(t)
+    for d in devs:
+        torch.cuda.current_stream(d).synchronize()
+    return [o.numpy() for o in outs]
+
+
 def _host_merge(dist: np.ndarray, ids: np.ndarray, k: int, metric: str = "sqeuclidean"
                 ) -> Tuple[np.ndarray, np.ndarray]:
     """Row-wise merge of [nq, m] candidates by (distance, id) -- distance descending for inner
@@ -351,12 +370,14 @@ class SearchResultAggregator:
         metric = str(getattr(indices[order[0]], "metric", "sqeuclidean"))
         kk = min(config.k, sum(int(raw[g][0].shape[1]) for g in order))
         final_dev = None
+        nan_flags = {}
         if CUVS_AVAILABLE and kk <= _MAX_K:
-            # device merge first: the tiles never round-trip through the host on the way to it
+            # device merge first: the tiles never round-trip through the host on the way to it (the NaN check's
+            # flags are computed on the devices and read with the results, below)
             if config.validate_results:
                 for g in order:
-                    if bool(torch.isnan(raw[g][0]).any()):
-                        raise ValueError(f"GPU {g} results contains NaN distances")
+                    with torch.cuda.device(raw[g][0].device):
+                        nan_flags[g] = torch.isnan(raw[g][0]).any().reshape(1)
             use_rccl = config.exchange == "rccl" or (config.exchange == "auto" and len(order) > 1)
             if use_rccl:
                 fd, fi = _rccl_merge({g: (raw[g][0], raw[g][1]) for g in order}, kk, metric)
@@ -365,14 +386,24 @@ class SearchResultAggregator:
                     fd, fi = _device_merge([raw[g][0] for g in order], [raw[g][1] for g in order], kk, metric,
                                            torch.device(f"cuda:{order[0]}"))
             final_dev = _rank_merge(fd, fi, kk, metric) if config.merge_across_ranks else (fd, fi)
-        gpu_results = [SearchResult(distances=raw[g][0].detach().cpu().numpy().astype(np.float32, copy=False),
-                                    indices=raw[g][1].detach().cpu().numpy().astype(np.int64, copy=False),
+        # everything the caller gets back crosses to the host in one round trip per device: the per-shard tiles,
+        # the merged result and the NaN flags are copied into pinned memory on each device's stream, then each
+        # device is synchronised once (one blocking copy per tensor cost a host round trip each)
+        host = _to_host([raw[g][0] for g in order] + [raw[g][1] for g in order] +
+                        ([final_dev[0], final_dev[1]] if final_dev is not None else []) +
+                        [nan_flags[g] for g in order if g in nan_flags])
+        no = len(order)
+        for j, g in enumerate([g for g in order if g in nan_flags]):
+            if bool(host[2 * no + (2 if final_dev is not None else 0) + j][0]):
+                raise ValueError(f"GPU {g} results contains NaN distances")
+        gpu_results = [SearchResult(distances=host[x].astype(np.float32, copy=False),
+                                    indices=host[no + x].astype(np.int64, copy=False),
                                     gpu_id=g, query_time=raw[g][2], k_requested=config.k,
-                                    k_returned=min(config.k, int(raw[g][0].shape[1]))) for g in order]
+                                    k_returned=min(config.k, int(raw[g][0].shape[1]))) for x, g in enumerate(order)]
         if config.validate_results:
             self.validate_search_results(gpu_results, nq, config.k)
         if final_dev is not None:
-            final_d, final_i = final_dev[0].cpu().numpy(), final_dev[1].cpu().numpy()
+            final_d, final_i = host[2 * no], host[2 * no + 1]
         else:
             final_d, final_i = self.merge_search_results(gpu_results, config.k, metric)
             if config.merge_across_ranks:
