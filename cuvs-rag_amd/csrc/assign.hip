@@ -287,10 +287,11 @@ __global__ __launch_bounds__(kAsThreads, 1) void k_as_scan(AsScanArgs a) {
         for (int j = 0; j < 8; ++j) {
           const float t = fmaf(acc4[2 * qb + (j >> 2)][j & 3], -2.0f * qsv[j], h.x + qnv[j]);
           const float key = t > 0.0f ? t : 0.0f;
-          const bool lt = key < run.m1[j];
-          run.m2[j] = lt ? run.m1[j] : fminf(run.m2[j], key);
-          run.id1[j] = lt ? cid : run.id1[j];
-          run.m1[j] = lt ? key : run.m1[j];
+          // (m1 <= m2: the new second smallest is the median of {m1, key, m2} -- one v_med3 for the select and
+          // the min of the two-way form)
+          run.m2[j] = __builtin_amdgcn_fmed3f(run.m1[j], key, run.m2[j]);
+          run.id1[j] = key < run.m1[j] ? cid : run.id1[j];
+          run.m1[j] = fminf(run.m1[j], key);
         }
       }
       cur = nxt;
