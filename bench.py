@@ -84,6 +84,9 @@ def parse():
     ap.add_argument("--pq-rows", type=int, default=12_500_000,
                     help="BASELINE configs[4] line: IVF-PQ over this many fp16 rows PER RANK (the per-GPU share of "
                          "100M x 768 on 8 GPUs), refined top-k merged across ranks over RCCL (0: skip)")
+    ap.add_argument("--pq-lut16", type=int, default=1,
+                    help="add the same PQ searches with the opt-in fp16 LUT (SearchParams lut_dtype float16) to the "
+                         "configs[4] line as 'lut_fp16' (0: skip)")
     ap.add_argument("--large-k", default="2000,4000",
                     help="side line (rank 0, N=1): the reference's large-k requests at configs[2] "
                          "(top_k 2000, k*2 per shard: improved_multi_gpu_rag.py:40,247); '' to skip")
@@ -742,6 +745,53 @@ def self_launch(a, argv):
 PEAK_LDS_B128_LOOKUPS = 256 * 2.4e9 * 64  # ds_read_b128: 256 B/clk/CU = 64 fp32 LUT entries / clk / CU
 
 
+def pq_lut16_leg(idx, x, q, gt, ng, k, kc, n_probes, start, world, dev):
+    """The same plain and refined PQ searches with SearchParams(lut_dtype=float16) (cuVS's half-precision LUT,
+    opt-in: the headline PQ numbers above stay fp32). A ds_read_b128 carries 8 fp16 entries, so its LDS peak
+    is twice the fp32 one."""
+    from mivs import _native
+    from mivs.distributed import merge_across_ranks
+    from mivs.neighbors import ivf_pq, refine
+
+    sp = ivf_pq.SearchParams(n_probes=n_probes, lut_dtype=np.float16)
+    reps = 5
+
+    def plain():
+        dd, ii = ivf_pq.search(sp, idx, q, k)
+        ii = ii + start if start else ii
+        return merge_across_ranks(dd, ii, k) if world > 1 else (dd, ii)
+
+    def refined():
+        _, cand = ivf_pq.search(sp, idx, q, kc)
+        dd, ii = refine(x, q, cand, k)
+        ii = ii + start if start else ii
+        return merge_across_ranks(dd, ii, k) if world > 1 else (dd, ii)
+
+    Q = q.shape[0]
+    plain()
+    _native.set_profiling(True)
+    idx.profile_collect()
+    sync_all(world)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        _, ids = plain()
+    torch.cuda.synchronize()
+    t_plain = max_over_ranks(time.perf_counter() - t0, world, dev) / reps
+    pr = idx.profile_collect()
+    _native.set_profiling(False)
+    refined()
+    sync_all(world)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        _, rids = refined()
+    torch.cuda.synchronize()
+    t_ref = max_over_ranks(time.perf_counter() - t0, world, dev) / reps
+    return {"qps_pq": round(Q / t_plain, 1), "recall_at_10_pq": round(recall_at_k(ids[:ng].cpu().numpy(), gt), 4),
+            "qps_pq_refined": round(Q / t_ref, 1),
+            "recall_at_10_pq_refined": round(recall_at_k(rids[:ng].cpu().numpy(), gt), 4),
+            "scan_ms": pr["scan_ms"] / max(pr["n_calls"], 1)}
+
+
 def pq_side_line(a, rl, rank=0, world=1, dev=None):
     """BASELINE configs[4]: IVF-PQ over 12.5M x 768 fp16 rows PER RANK (100M over 8 GPUs), n_lists 4096,
     pq_dim 96, pq_bits 8 (improved_multi_gpu_rag.py:131-137), the same query batch shape; plain PQ at
@@ -823,6 +873,7 @@ def pq_side_line(a, rl, rank=0, world=1, dev=None):
     torch.cuda.synchronize()
     t_ref = max_over_ranks(time.perf_counter() - t0, world, dev) / reps
     rec_ref = recall_at_k(rids[:ng].cpu().numpy(), gt)
+    lut16 = pq_lut16_leg(idx, x, q, gt, ng, k, kc, n_probes, start, world, dev) if a.pq_lut16 else None
     probes = torch.empty((Q, n_probes), dtype=torch.int32, device=dev)
     ivf_pq.search(sp, idx, q, k, probes_out=probes)
     rows = int(idx.list_sizes.cpu()[probes.long().cpu()].sum())
@@ -843,6 +894,16 @@ def pq_side_line(a, rl, rank=0, world=1, dev=None):
             "roofline": {"bound": "lds", "achieved": round(ach / 1e9, 1), "peak": round(PEAK_LDS_B128_LOOKUPS / 1e9, 1),
                          "unit": "G LUT entries/s", "frac": round(ach / PEAK_LDS_B128_LOOKUPS, 4),
                          "launch_ms": round(scan_ms, 4), "lut_entries_per_launch": lookups, "rows_scanned": rows}}
+    if lut16 is not None:
+        ms16 = lut16.pop("scan_ms")
+        a16 = lookups / (ms16 * 1e-3)
+        lut16["roofline"] = {"bound": "lds", "achieved": round(a16 / 1e9, 1),
+                             "peak": round(2 * PEAK_LDS_B128_LOOKUPS / 1e9, 1), "unit": "G LUT entries/s",
+                             "frac": round(a16 / (2 * PEAK_LDS_B128_LOOKUPS), 4), "launch_ms": round(ms16, 4)}
+        line["lut_fp16"] = lut16
+        rl(f"[pq] lut_dtype float16 (opt-in): {lut16['qps_pq']:,.0f} QPS recall {lut16['recall_at_10_pq']:.3f}; "
+           f"refined {lut16['qps_pq_refined']:,.0f} QPS recall {lut16['recall_at_10_pq_refined']:.3f}; "
+           f"K9r {ms16:.3f} ms")
     rl(f"[pq] {n * world} x {d} fp16 on {world} GPU(s), build {n * world / t_build / 1e6:.2f} M vec/s {phases}; "
        f"n_probes {n_probes}: {Q / t_plain:,.0f} QPS recall {rec_plain:.3f}; refined x{ratio}: {Q / t_ref:,.0f} QPS "
        f"recall {rec_ref:.3f}")

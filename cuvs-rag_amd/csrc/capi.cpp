@@ -1762,7 +1762,7 @@ bool pq_rt_use(const mivs_index_s* idx, int k) {
 }
 
 void pq_search_rt(mivs_index_s* idx, hipStream_t s, const float* d_q, int64_t nq, int k, int np, float* d_dist,
-                  int64_t* d_ids, ProfRec* pr) {
+                  int64_t* d_ids, ProfRec* pr, bool lut16 = false) {
   Workspace& ws = idx->ws;
   const ListSet& L = idx->lists;
   const bool dump = k > kMaxK;
@@ -1801,6 +1801,7 @@ void pq_search_rt(mivs_index_s* idx, hipStream_t s, const float* d_q, int64_t nq
     ws.counter.reserve(16);
     HIPCHK(hipMemsetAsync(ws.counter.p, 0, sizeof(int), s));
     PqTileArgs a{};
+    a.lut16 = lut16 ? 1 : 0;
     a.queries = d_q + b0 * (int64_t)idx->d;
     a.cents = idx->centroids_rm.as<float>();
     a.books = idx->pq_books.as<float>();
@@ -2322,8 +2323,18 @@ int32_t mivs_ivf_pq_build(int32_t device, void* stream, const float* d_data, int
 
 int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int64_t nq, int32_t k,
                            int32_t n_probes, float* d_dist, int64_t* d_ids, int32_t* d_probes) {
+  return mivs_ivf_pq_search_ex(idx, stream, d_q, nq, k, n_probes, MIVS_LUT_FP32, d_dist, d_ids, d_probes);
+}
+
+int32_t mivs_ivf_pq_search_ex(mivs_index_t idx, void* stream, const float* d_q, int64_t nq, int32_t k,
+                              int32_t n_probes, int32_t lut_dtype, float* d_dist, int64_t* d_ids, int32_t* d_probes) {
   return guarded([&] {
     require(idx != nullptr && idx->kind == 2, "not an ivf_pq index");
+    require(lut_dtype == MIVS_LUT_FP32 || lut_dtype == MIVS_LUT_FP16, "lut_dtype must be MIVS_LUT_FP32 or MIVS_LUT_FP16");
+    const bool lut16 = lut_dtype == MIVS_LUT_FP16;
+    require(!lut16 || (idx->metric == kL2 && pq_rt_use(idx, k)),
+            "ivf_pq: the fp16 LUT is served by the K9r scan, for the L2 metric with pq_len % 4 == 0 (4..16)",
+            MIVS_ERR_UNSUPPORTED);
     require(nq >= 0, "nq must be >= 0");
     require(k >= 1 && k <= kMaxSelectK, "ivf_pq: k must be in [1, " + std::to_string(kMaxSelectK) + "]",
             MIVS_ERR_UNSUPPORTED);
@@ -2358,7 +2369,7 @@ int32_t mivs_ivf_pq_search(mivs_index_t idx, void* stream, const float* d_q, int
     // the 32/64-entry register lists at 40 candidates (profiles/r02_ivf_pq_refine_bench.log);
     // MIVS_PQ_DUMP_K raises the threshold (up to 64) for the register path
     if (pq_rt_use(idx, k)) {
-      pq_search_rt(idx, s, d_q, nq, k, np, d_dist, d_ids, pr);
+      pq_search_rt(idx, s, d_q, nq, k, np, d_dist, d_ids, pr, lut16);
       if (pr) HIPCHK(hipEventRecord(pr->e[3], s));
       idx->last_nq = nq;
       idx->last_np = np;

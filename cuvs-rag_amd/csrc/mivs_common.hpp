@@ -176,6 +176,7 @@ struct PqTileArgs {
   int n_probes;
   int64_t* slot_info;       // DUMP: [slots][2] = (first row position, rows); out_d is [slots][kRtRows]
   int flags;                // timing experiments only (MIVS_PQ_FLAGS): 1 skip LUT build, 2 skip row scan
+  int lut16 = 0;            // K9r: LUT entries stored as fp16 (cuvs SearchParams.lut_dtype = float16; L2 only)
 };
 
 // K9r (k_pq_scan_rt, pq.hip): work item = (list, <= 16 queries probing it, chunk of kRtRows rows); the
@@ -186,7 +187,7 @@ constexpr int kRtQ = 16;
 constexpr int kRtRpt = 8;
 constexpr int kRtRows = kRtThreads * kRtRpt;  // 4096
 constexpr int kRtGroups = kRtRows / 32;
-size_t pq_rt_lds_bytes(int rot_dim_pad, int pq_dim, int k);
+size_t pq_rt_lds_bytes(int rot_dim_pad, int pq_dim, int k, bool lut16 = false);
 // book_norms and books_mfma from the codebooks (after training; pq.hip)
 hipError_t launch_pq_book_prep(const float* books, int pq_dim, int pq_len, int ip, float* book_norms,
                                float* books_mfma, hipStream_t s);

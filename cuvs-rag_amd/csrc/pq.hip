@@ -797,9 +797,26 @@ __device__ __forceinline__ bool rt_less(float ka, int ra, float kb, int rb) {
   return ka < kb || (ka == kb && ra < rb);
 }
 
-template <int PL4, int CQ>
+typedef uint32_t pq_u32x4 __attribute__((ext_vector_type(4)));
+
+// acc + (float)(half `hi` of w) in one VALU op: v_fma_mix_f32 with the f16 operand times 1.0 is exact, so its one
+// rounding is the fp32 add's (the compiler folds fmaf(h, 1, acc) to a cvt + add, two ops per entry)
+__device__ __forceinline__ float rt_add_f16(float acc, uint32_t w, int hi) {
+  if (hi)
+    asm("v_fma_mix_f32 %0, %1, 1.0, %0 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(acc) : "v"(w));
+  else
+    asm("v_fma_mix_f32 %0, %1, 1.0, %0 op_sel_hi:[1,0,0]" : "+v"(acc) : "v"(w));
+  return acc;
+}
+
+// H16 (cuvs SearchParams.lut_dtype = float16, L2): each LUT entry is rounded to fp16 when it is stored (RNE, as
+// oracle orc_round_f16) and a code row is 16 halves padded to 48 B (its 16-lane groups start at quad 3c mod 16: a
+// permutation over c mod 16, like the 80-B fp32 rows' 5c), so a (row, subspace) takes two ds_read_b128 instead of
+// four; the row sums stay fp32 in the same order.
+template <int PL4, int CQ, bool H16 = false>
 __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
-  constexpr int NT = kRtThreads, TQ = kRtQ, RPT = kRtRpt, R = kRtRows, LS = 20, PL = 4 * PL4;
+  constexpr int NT = kRtThreads, TQ = kRtQ, RPT = kRtRpt, R = kRtRows, PL = 4 * PL4;
+  constexpr int LS = H16 ? 12 : 20;  // code row stride in 4-B words (fp16: 24 halves = 48 B; fp32: 20 floats)
   constexpr bool DUMP = CQ == 0;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int64_t* s_q = reinterpret_cast<int64_t*>(smem);        // [TQ] query (-1: no query)
@@ -943,8 +960,15 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = v[r] + s_base[4 * bg + r];
           }
-          *reinterpret_cast<float4*>(s_lut + ((j & 3) * kPqCodes + wave * 32 + cb * 16 + bi) * LS + 4 * bg) =
-              make_float4(v[0], v[1], v[2], v[3]);
+          if constexpr (H16) {
+            typedef _Float16 hx4 __attribute__((ext_vector_type(4)));
+            const hx4 hv = {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+            *reinterpret_cast<hx4*>(reinterpret_cast<char*>(s_lut + ((j & 3) * kPqCodes + wave * 32 + cb * 16 + bi) * LS) +
+                                     8 * bg) = hv;
+          } else {
+            *reinterpret_cast<float4*>(s_lut + ((j & 3) * kPqCodes + wave * 32 + cb * 16 + bi) * LS + 4 * bg) =
+                make_float4(v[0], v[1], v[2], v[3]);
+          }
         }
       }
     };
@@ -1007,16 +1031,45 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
           }
         }
         const float* lut = s_lut + (j & 3) * (kPqCodes * LS);
+        if constexpr (H16) {  // RH rows' halves in flight (2: 7.97 ms, 4: 7.84 ms at configs[4])
+          constexpr int RH = 4;
 #pragma unroll
-        for (int i = 0; i < RPT; ++i) {
+          for (int i0 = 0; i0 < RPT; i0 += RH) {
+            if (i0 < nvi && !skip_scan) {
+              pq_u32x4 v[RH][2];
+#pragma unroll
+              for (int r = 0; r < RH; ++r) {
+                const pq_u32x4* p = reinterpret_cast<const pq_u32x4*>(lut + ((cw[i0 + r] >> (8 * b)) & 0xFF) * LS);
+                v[r][0] = p[0];
+                v[r][1] = p[1];
+              }
+              __builtin_amdgcn_sched_group_barrier(0x100, 2 * RH, 0);  // the LDS reads issue first
+#pragma unroll
+              for (int r = 0; r < RH; ++r) {
+                if (r == 0 || i0 + r < nvi) {
+#pragma unroll
+                  for (int t = 0; t < 8; ++t) {
+                    acc[i0 + r][t] = rt_add_f16(acc[i0 + r][t], v[r][0][t >> 1], t & 1);
+                    acc[i0 + r][8 + t] = rt_add_f16(acc[i0 + r][8 + t], v[r][1][t >> 1], t & 1);
+                  }
+                }
+              }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < (H16 ? 0 : RPT); ++i) {
           if (i < nvi && !skip_scan) {
             const int code = (cw[i] >> (8 * b)) & 0xFF;
-            const float4* p = reinterpret_cast<const float4*>(lut + code * LS);
-            const float4 v0 = p[0], v1 = p[1], v2 = p[2], v3 = p[3];
-            acc[i][0] += v0.x; acc[i][1] += v0.y; acc[i][2] += v0.z; acc[i][3] += v0.w;
-            acc[i][4] += v1.x; acc[i][5] += v1.y; acc[i][6] += v1.z; acc[i][7] += v1.w;
-            acc[i][8] += v2.x; acc[i][9] += v2.y; acc[i][10] += v2.z; acc[i][11] += v2.w;
-            acc[i][12] += v3.x; acc[i][13] += v3.y; acc[i][14] += v3.z; acc[i][15] += v3.w;
+            {
+              const float4* p = reinterpret_cast<const float4*>(lut + code * LS);
+              const float4 v0 = p[0], v1 = p[1], v2 = p[2], v3 = p[3];
+              acc[i][0] += v0.x; acc[i][1] += v0.y; acc[i][2] += v0.z; acc[i][3] += v0.w;
+              acc[i][4] += v1.x; acc[i][5] += v1.y; acc[i][6] += v1.z; acc[i][7] += v1.w;
+              acc[i][8] += v2.x; acc[i][9] += v2.y; acc[i][10] += v2.z; acc[i][11] += v2.w;
+              acc[i][12] += v3.x; acc[i][13] += v3.y; acc[i][14] += v3.z; acc[i][15] += v3.w;
+            }
           }
           __builtin_amdgcn_sched_barrier(0);  // one row's 16 LUT floats in flight: bounds the VGPRs
         }
@@ -1214,8 +1267,9 @@ hipError_t launch_pq_scan_tiled(const PqTileArgs& a, int kcap, int grid, hipStre
 
 static int pq_rt_cq(int k) { return k > 64 ? 0 : (k <= 16 ? 128 : 512); }
 
-size_t pq_rt_lds_bytes(int rot_dim_pad, int pq_dim, int k) {
-  const size_t loop = (size_t)kRtQ * rot_dim_pad * 4 + (size_t)4 * kPqCodes * 20 * 4 + (size_t)pq_dim * kRtQ * 4;
+size_t pq_rt_lds_bytes(int rot_dim_pad, int pq_dim, int k, bool lut16) {
+  const size_t loop = (size_t)kRtQ * rot_dim_pad * 4 + (size_t)4 * kPqCodes * (lut16 ? 12 : 20) * 4 +
+                      (size_t)pq_dim * kRtQ * 4;
   const size_t sel = (size_t)kRtQ * kRtThreads * 4 + (size_t)kRtQ * pq_rt_cq(k) * 8;
   return 512 + (loop > sel ? loop : sel);
 }
@@ -1226,13 +1280,18 @@ bool pq_rt_supported(int rot_dim_pad, int pq_dim, int pq_len, int k) {
          k <= kMaxSelectK && pq_rt_lds_bytes(rot_dim_pad, pq_dim, k) <= 160 * 1024;
 }
 
-template <int PL4, int CQ>
-static hipError_t launch_pq_rt_k(const PqTileArgs& a, int grid, size_t lds, hipStream_t s) {
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pq_scan_rt<PL4, CQ>),
+template <int PL4, int CQ, bool H16>
+static hipError_t launch_pq_rt_kh(const PqTileArgs& a, int grid, size_t lds, hipStream_t s) {
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pq_scan_rt<PL4, CQ, H16>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL((k_pq_scan_rt<PL4, CQ>), dim3((unsigned)grid), dim3(kRtThreads), lds, s, a);
+  hipLaunchKernelGGL((k_pq_scan_rt<PL4, CQ, H16>), dim3((unsigned)grid), dim3(kRtThreads), lds, s, a);
   return hipGetLastError();
+}
+
+template <int PL4, int CQ>
+static hipError_t launch_pq_rt_k(const PqTileArgs& a, int grid, size_t lds, hipStream_t s) {
+  return a.lut16 ? launch_pq_rt_kh<PL4, CQ, true>(a, grid, lds, s) : launch_pq_rt_kh<PL4, CQ, false>(a, grid, lds, s);
 }
 
 template <int PL4>
@@ -1274,7 +1333,8 @@ hipError_t launch_pq_scan_rt(const PqTileArgs& a, int grid, hipStream_t s) {
   if (a.books_mfma == nullptr || a.book_norms == nullptr) return hipErrorInvalidValue;
   if (pq_rt_cq(a.k) == 0 && a.slot_info == nullptr) return hipErrorInvalidValue;
   if (a.ip && (a.probes == nullptr || a.probes_d == nullptr)) return hipErrorInvalidValue;
-  const size_t lds = pq_rt_lds_bytes(a.rot_dim_pad, a.pq_dim, a.k);
+  if (a.lut16 && a.ip) return hipErrorInvalidValue;  // (fp16 LUT: L2 only)
+  const size_t lds = pq_rt_lds_bytes(a.rot_dim_pad, a.pq_dim, a.k, a.lut16 != 0);
   switch (a.pq_len >> 2) {
     case 1: return launch_pq_rt_pl<1>(a, grid, lds, s);
     case 2: return launch_pq_rt_pl<2>(a, grid, lds, s);

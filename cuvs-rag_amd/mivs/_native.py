@@ -158,6 +158,8 @@ _SIGS = {
                                     POINTER(c_void_p)]),
     "mivs_ivf_pq_search": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p,
                                      c_void_p]),
+    "mivs_ivf_pq_search_ex": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_void_p,
+                                        c_void_p, c_void_p]),
     "mivs_ivf_pq_info": (c_int32, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
     "mivs_ivf_pq_get_codebooks": (c_int32, [c_void_p, c_void_p, c_void_p]),
     "mivs_ivf_pq_get_codes": (c_int32, [c_void_p, c_void_p, c_void_p]),

@@ -80,19 +80,27 @@ class IndexParams:
 
 
 class SearchParams:
-    """cuvs.neighbors.ivf_pq.SearchParams (cuVS defaults: n_probes 20, fp32 LUT and distances)."""
+    """cuvs.neighbors.ivf_pq.SearchParams (cuVS defaults: n_probes 20, fp32 LUT and distances).
+
+    ``lut_dtype=np.float16`` stores every LUT entry as fp16 (rounded to nearest even when the LUT is built) and
+    keeps the row sums in fp32, as cuVS's half-precision LUT does; the K9r scan then reads half the LDS bytes
+    (DESIGN.md §6a). It is served for the L2 metric with pq_len a multiple of 4 in 4..16; other indexes raise
+    NotImplementedError at search. ``internal_distance_dtype`` is fp32 only."""
 
     def __init__(self, n_probes: int = 20, lut_dtype=np.float32, internal_distance_dtype=np.float32):
         if int(n_probes) < 1:
             raise ValueError(f"n_probes must be >= 1, got {n_probes}")
-        if np.dtype(lut_dtype) != np.float32 or np.dtype(internal_distance_dtype) != np.float32:
-            raise NotImplementedError("ivf_pq: this build computes the LUT and distances in fp32")
+        if np.dtype(lut_dtype) not in (np.float32, np.float16):
+            raise NotImplementedError(f"ivf_pq: lut_dtype {np.dtype(lut_dtype)} (this build: float32 or float16)")
+        if np.dtype(internal_distance_dtype) != np.float32:
+            raise NotImplementedError("ivf_pq: this build accumulates distances in fp32")
         self.n_probes = int(n_probes)
-        self.lut_dtype = np.float32
+        self.lut_dtype = np.dtype(lut_dtype).type
         self.internal_distance_dtype = np.float32
 
     def __repr__(self):
-        return f"SearchParams(n_probes={self.n_probes})"
+        lut = "" if self.lut_dtype == np.float32 else ", lut_dtype=float16"
+        return f"SearchParams(n_probes={self.n_probes}{lut})"
 
 
 class Index:
@@ -232,9 +240,13 @@ def _search(search_params, index, queries, k: int, neighbors=None, distances=Non
     nq = q.shape[0]
     dist = out_tensor(distances, (nq, k), torch.float32, dev, "distances")
     nbrs = out_tensor(neighbors, (nq, k), torch.int64, dev, "neighbors")
+    lut = 1 if getattr(sp, "lut_dtype", np.float32) == np.float16 else 0  # (MIVS_LUT_FP16 / MIVS_LUT_FP32)
     with torch.cuda.device(dev):
-        _native.check(_native.lib().mivs_ivf_pq_search(index.handle, stream_ptr(dev), ptr(q), nq, k, sp.n_probes,
-                                                       ptr(dist), ptr(nbrs), ptr(probes_out)))
+        rc = _native.lib().mivs_ivf_pq_search_ex(index.handle, stream_ptr(dev), ptr(q), nq, k, sp.n_probes, lut,
+                                                 ptr(dist), ptr(nbrs), ptr(probes_out))
+    if rc == _native.MIVS_ERR_UNSUPPORTED and lut:  # the fp16 LUT is not served for this index
+        raise NotImplementedError(_native.lib().mivs_last_error().decode(errors="replace"))
+    _native.check(rc)
     return dist, nbrs
 
 

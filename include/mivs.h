@@ -214,6 +214,13 @@ int32_t mivs_ivf_pq_build(int32_t device, void* stream, const float* d_data, int
 int32_t mivs_ivf_pq_search(mivs_index_t index, void* stream, const float* d_queries, int64_t n_queries, int32_t k,
                            int32_t n_probes, float* d_distances, int64_t* d_neighbors, int32_t* d_probes);
 /* pq_dim, pq_bits, pq_len of an IVF-PQ index */
+/* The same with cuvs.neighbors.ivf_pq.SearchParams.lut_dtype: MIVS_LUT_FP32 (cuVS's default) or MIVS_LUT_FP16 --
+ * every LUT entry rounded to fp16 when stored, row sums in fp32 (L2 metric, pq_len a multiple of 4 in 4..16; else
+ * MIVS_ERR_UNSUPPORTED). */
+enum { MIVS_LUT_FP32 = 0, MIVS_LUT_FP16 = 1 };
+int32_t mivs_ivf_pq_search_ex(mivs_index_t index, void* stream, const float* d_queries, int64_t n_queries, int32_t k,
+                              int32_t n_probes, int32_t lut_dtype, float* d_distances, int64_t* d_neighbors,
+                              int32_t* d_probes);
 int32_t mivs_ivf_pq_info(mivs_index_t index, int32_t* pq_dim, int32_t* pq_bits, int32_t* pq_len);
 /* d_out: [pq_dim][2^pq_bits][pq_len] fp32 codebooks */
 int32_t mivs_ivf_pq_get_codebooks(mivs_index_t index, void* stream, float* d_out);

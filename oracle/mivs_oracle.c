@@ -550,15 +550,32 @@ void orc_ivfpq_build(const float* x, int64_t n, int d, int n_lists, int iters, d
   free(which);
 }
 
+/* fp32 -> the nearest fp16 (ties to even, fp16 subnormals kept, |v| >= 65520 -> inf) -> fp32: what a LUT entry
+ * stored as fp16 (v_cvt_f16_f32, round to nearest even) and read back (v_cvt_f32_f16) holds. gcc 11 has no
+ * _Float16 on x86, so the rounding is done in double: spacing 2^(e - 10) at binary exponent e >= -14, 2^-24 below. */
+float orc_round_f16(float v) {
+  if (!(fabsf(v) < INFINITY)) return v;
+  int e = 0;
+  (void)frexp((double)v, &e); /* |v| in [2^(e-1), 2^e) */
+  int ex = e - 1;
+  if (ex < -14) ex = -14;
+  const double sp = ldexp(1.0, ex - 10);
+  const double r = rint((double)v / sp) * sp;
+  if (fabs(r) >= 65536.0) return v < 0.0f ? -INFINITY : INFINITY;
+  return (float)r;
+}
+
 /* IVF-PQ search (cuvs.neighbors.ivf_pq.search, improved_multi_gpu_rag.py:228-230). metric ORC_L2: a row's key
  * is sum_j LUT_j[code_j] (j ascending, from 0) with LUT_j[c] = ||(q - c_l)_j - B_j[c]||^2 in the expanded form
  * of orc_pq_l2_lut. ORC_IP: LUT_j[c] =
  * -(q_j . B_j[c]) and subspace 0's row also carries the probe's coarse key -(q . c_l) (orc_dot), so the key
  * estimates -(q . x_hat); distances out are the inner products (-key). Probes rank by the metric's key. */
-void orc_ivfpq_search(const float* centroids, int n_lists, int d, const float* codebooks, int pq_dim, int pq_bits,
-                      const int64_t* list_sizes, const int64_t* list_ids, const uint8_t* codes, const float* q,
-                      int64_t nq, int n_probes, int k, int metric, float* out_d, int64_t* out_i,
-                      int32_t* out_probes) {
+/* lut_fp16 (cuvs SearchParams.lut_dtype = float16; ORC_L2 only): every LUT entry is rounded to fp16 (orc_round_f16)
+ * when the LUT is built, the row sums stay fp32 in the same order */
+void orc_ivfpq_search_ex(const float* centroids, int n_lists, int d, const float* codebooks, int pq_dim, int pq_bits,
+                         const int64_t* list_sizes, const int64_t* list_ids, const uint8_t* codes, const float* q,
+                         int64_t nq, int n_probes, int k, int metric, float* out_d, int64_t* out_i,
+                         int32_t* out_probes, int lut_fp16) {
   if (n_probes > n_lists) n_probes = n_lists;
   const int pl = orc_pq_len(d, pq_dim);
   const int nc = 1 << pq_bits;
@@ -595,8 +612,10 @@ void orc_ivfpq_search(const float* centroids, int n_lists, int d, const float* c
           }
         } else {
           pq_residual(qq, centroids + (int64_t)l * d, d, j, pl, r);
-          for (int c = 0; c < nc; ++c)
-            lut[j * nc + c] = orc_pq_l2_lut(r, codebooks + ((int64_t)j * nc + c) * pl, pl);
+          for (int c = 0; c < nc; ++c) {
+            const float v = orc_pq_l2_lut(r, codebooks + ((int64_t)j * nc + c) * pl, pl);
+            lut[j * nc + c] = lut_fp16 ? orc_round_f16(v) : v;
+          }
         }
       }
       for (int64_t m = offs[l]; m < offs[l + 1]; ++m) {
@@ -615,4 +634,12 @@ void orc_ivfpq_search(const float* centroids, int n_lists, int d, const float* c
   }
   free(offs);
   free(cn);
+}
+
+void orc_ivfpq_search(const float* centroids, int n_lists, int d, const float* codebooks, int pq_dim, int pq_bits,
+                      const int64_t* list_sizes, const int64_t* list_ids, const uint8_t* codes, const float* q,
+                      int64_t nq, int n_probes, int k, int metric, float* out_d, int64_t* out_i,
+                      int32_t* out_probes) {
+  orc_ivfpq_search_ex(centroids, n_lists, d, codebooks, pq_dim, pq_bits, list_sizes, list_ids, codes, q, nq, n_probes,
+                      k, metric, out_d, out_i, out_probes, 0);
 }

@@ -91,6 +91,11 @@ void orc_ivfpq_encode(const float* x, const int64_t* rows, int64_t nr, int d, co
 void orc_ivfpq_build(const float* x, int64_t n, int d, int n_lists, int iters, double fraction, int pq_dim,
                      int pq_bits, int64_t max_per_code, int balance, int64_t id_offset, float* centroids,
                      float* codebooks, int64_t* list_sizes, int64_t* list_ids, uint8_t* codes);
+float orc_round_f16(float v);
+void orc_ivfpq_search_ex(const float* centroids, int n_lists, int d, const float* codebooks, int pq_dim, int pq_bits,
+                         const int64_t* list_sizes, const int64_t* list_ids, const uint8_t* codes, const float* q,
+                         int64_t nq, int n_probes, int k, int metric, float* out_d, int64_t* out_i,
+                         int32_t* out_probes, int lut_fp16);
 void orc_ivfpq_search(const float* centroids, int n_lists, int d, const float* codebooks, int pq_dim, int pq_bits,
                       const int64_t* list_sizes, const int64_t* list_ids, const uint8_t* codes, const float* q,
                       int64_t nq, int n_probes, int k, int metric, float* out_d, int64_t* out_i,

@@ -55,6 +55,8 @@ def lib():
             "orc_pq_train_count": (i64, [i64, i32, i64]),
             "orc_ivfpq_build": (None, [P, i64, i32, i32, i32, f64, i32, i32, i64, i32, i64, P, P, P, P, P]),
             "orc_ivfpq_search": (None, [P, i32, i32, P, i32, i32, P, P, P, P, i64, i32, i32, i32, P, P, P]),
+            "orc_ivfpq_search_ex": (None, [P, i32, i32, P, i32, i32, P, P, P, P, i64, i32, i32, i32, P, P, P, i32]),
+            "orc_round_f16": (ctypes.c_float, [ctypes.c_float]),
             "orc_fast_threads": (i32, []),
             "orc_fast_set_threads": (None, [i32]),
             "orc_fast_knn": (None, [P, i64, P, i64, i32, i32, P, P]),
@@ -258,8 +260,14 @@ def ivfpq_build(x, n_lists, pq_dim, pq_bits=8, iters=20, fraction=0.5, max_per_c
     return cents, cbs, sizes, ids, codes
 
 
-def ivfpq_search(centroids, codebooks, sizes, ids, codes, q, n_probes, k, metric="sqeuclidean"):
-    """-> (dist [nq,k], ids [nq,k], probes [nq, n_probes]); metric sqeuclidean or inner_product."""
+def round_f16(v) -> float:
+    """orc_round_f16: fp32 -> nearest fp16 (ties to even) -> fp32."""
+    return float(lib().orc_round_f16(float(v)))
+
+
+def ivfpq_search(centroids, codebooks, sizes, ids, codes, q, n_probes, k, metric="sqeuclidean", lut_fp16=False):
+    """-> (dist [nq,k], ids [nq,k], probes [nq, n_probes]); metric sqeuclidean or inner_product. lut_fp16: LUT entries
+    rounded to fp16 (cuvs SearchParams.lut_dtype = float16; sqeuclidean only)."""
     c, cb, q = _f32(centroids), _f32(codebooks), _f32(q)
     sizes, ids = _i64(sizes), _i64(ids)
     codes = np.ascontiguousarray(codes, dtype=np.uint8)
@@ -269,8 +277,9 @@ def ivfpq_search(centroids, codebooks, sizes, ids, codes, q, n_probes, k, metric
     od = np.empty((nq, k), np.float32)
     oi = np.empty((nq, k), np.int64)
     op = np.empty((nq, np_), np.int32)
-    lib().orc_ivfpq_search(_p(c), c.shape[0], c.shape[1], _p(cb), pq_dim, int(ncodes).bit_length() - 1, _p(sizes),
-                           _p(ids), _p(codes), _p(q), nq, np_, k, metric_code(metric), _p(od), _p(oi), _p(op))
+    lib().orc_ivfpq_search_ex(_p(c), c.shape[0], c.shape[1], _p(cb), pq_dim, int(ncodes).bit_length() - 1, _p(sizes),
+                              _p(ids), _p(codes), _p(q), nq, np_, k, metric_code(metric), _p(od), _p(oi), _p(op),
+                              1 if lut_fp16 else 0)
     return od, oi, op
 
 

@@ -431,7 +431,63 @@ def test_ivf_pq_k9r_mfma_lut_every_pq_len(mivs_lib, monkeypatch, pq_len):
     _pq_case(3000, pq_dim * pq_len, 8, pq_dim, 2, 24, 4, 10)
 
 
-def _pq_case(n, d, n_lists, pq_dim, iters, nq, n_probes, k):
+PQ_LUT16_CASES = [
+    # n, d, n_lists, pq_dim, iters, nq, n_probes, k
+    (6000, 64, 16, 16, 4, 40, 4, 10),     # pq_len 4
+    (9000, 128, 24, 16, 3, 33, 8, 16),    # pq_len 8
+    (4000, 96, 8, 8, 3, 17, 8, 5),        # pq_len 12
+    (5000, 128, 12, 8, 2, 29, 5, 1),      # pq_len 16, k = 1
+    (7000, 64, 16, 16, 3, 19, 5, 40),     # k in (16, 64]
+    (6000, 64, 16, 16, 4, 40, 8, 200),    # k > 64: DUMP + K8 select
+    (12000, 768, 32, 192, 2, 20, 6, 10),  # d = 768, pq_len 4
+]
+
+
+@pytest.mark.parametrize("n,d,n_lists,pq_dim,iters,nq,n_probes,k", PQ_LUT16_CASES)
+def test_ivf_pq_fp16_lut_bitexact(mivs_lib, n, d, n_lists, pq_dim, iters, nq, n_probes, k):
+    """SearchParams(lut_dtype=float16): K9r stores each LUT entry rounded to fp16 (nearest even) and sums them in
+    fp32 -- probes, ids and distance bits equal to oracle orc_ivfpq_search_ex(lut_fp16=1)"""
+    _pq_case(n, d, n_lists, pq_dim, iters, nq, n_probes, k, lut16=True)
+
+
+def test_ivf_pq_fp16_lut_unsupported_and_recall(mivs_lib, monkeypatch):
+    """the fp16 LUT is served by K9r for L2 only: inner product, pq_len 3 and MIVS_PQ_RT=0 raise
+    NotImplementedError; on clustered data its recall stays within 0.02 of the fp32 LUT's"""
+    from mivs import ops
+    from mivs.neighbors import brute_force, ivf_pq
+
+    sp16 = ivf_pq.SearchParams(n_probes=4, lut_dtype=np.float16)
+    x = _data(3000, 64, seed=5, normalize=True)
+    q = _gpu(_data(8, 64, seed=6, normalize=True))
+    ip = ivf_pq.build(ivf_pq.IndexParams(n_lists=8, metric="inner_product", pq_dim=16, kmeans_n_iters=2), _gpu(x))
+    with pytest.raises(NotImplementedError):
+        ivf_pq.search(sp16, ip, q, 10)
+    x96 = _data(3000, 96, seed=7, normalize=True)
+    l3 = ivf_pq.build(ivf_pq.IndexParams(n_lists=8, pq_dim=32, kmeans_n_iters=2), _gpu(x96))
+    with pytest.raises(NotImplementedError):
+        ivf_pq.search(sp16, l3, _gpu(_data(8, 96, seed=8, normalize=True)), 10)
+    l2 = ivf_pq.build(ivf_pq.IndexParams(n_lists=8, pq_dim=16, kmeans_n_iters=2), _gpu(x))
+    ivf_pq.search(sp16, l2, q, 10)
+    monkeypatch.setenv("MIVS_PQ_RT", "0")
+    with pytest.raises(NotImplementedError):
+        ivf_pq.search(sp16, l2, q, 10)
+    monkeypatch.delenv("MIVS_PQ_RT")
+    with pytest.raises(NotImplementedError):
+        ivf_pq.SearchParams(lut_dtype=np.float64)
+
+    xs = ops.synth_mixture(50000, 128, 4, n_centers=256, sigma=0.35)
+    qs = ops.synth_mixture(300, 128, 4, n_centers=256, sigma=0.35, row_begin=1 << 40)
+    idx = ivf_pq.build(ivf_pq.IndexParams(n_lists=64, pq_dim=32, kmeans_n_iters=5), xs)
+    _, gt = brute_force.search(brute_force.build(xs), qs, 10)
+    gt = gt.cpu().numpy()
+    rec = {}
+    for lut in (np.float32, np.float16):
+        _, ids = ivf_pq.search(ivf_pq.SearchParams(n_probes=16, lut_dtype=lut), idx, qs, 10)
+        rec[lut] = np.mean([len(set(a) & set(b)) / 10 for a, b in zip(ids.cpu().numpy(), gt)])
+    assert rec[np.float16] > rec[np.float32] - 0.02, rec
+
+
+def _pq_case(n, d, n_lists, pq_dim, iters, nq, n_probes, k, lut16=False):
     from mivs.neighbors import ivf_pq
 
     x = _data(n, d, seed=n + pq_dim, normalize=True)
@@ -445,8 +501,9 @@ def _pq_case(n, d, n_lists, pq_dim, iters, nq, n_probes, k):
     np.testing.assert_array_equal(idx.list_ids().cpu().numpy(), oids)
     np.testing.assert_array_equal(idx.codes().cpu().numpy(), ocodes)
     probes = torch.empty((nq, n_probes), dtype=torch.int32, device="cuda")
-    dist, ids = ivf_pq.search(ivf_pq.SearchParams(n_probes=n_probes), idx, _gpu(q), k, probes_out=probes)
-    od, oi, op = O.ivfpq_search(oc, ocb, osz, oids, ocodes, q, n_probes, k)
+    sp = ivf_pq.SearchParams(n_probes=n_probes, lut_dtype=np.float16 if lut16 else np.float32)
+    dist, ids = ivf_pq.search(sp, idx, _gpu(q), k, probes_out=probes)
+    od, oi, op = O.ivfpq_search(oc, ocb, osz, oids, ocodes, q, n_probes, k, lut_fp16=lut16)
     np.testing.assert_array_equal(probes.cpu().numpy(), op)
     np.testing.assert_array_equal(ids.cpu().numpy(), oi)
     np.testing.assert_array_equal(_bits(dist.cpu().numpy()), _bits(od))

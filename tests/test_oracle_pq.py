@@ -62,3 +62,41 @@ def test_full_probe_inner_product_ranks_by_q_dot_reconstruction():
     # probes rank the centroids by inner product
     cp = np.argsort(-(q.astype(np.float64) @ cents.astype(np.float64).T), axis=1, kind="stable")
     np.testing.assert_array_equal(p, cp[:, :5])
+
+
+def test_round_f16_matches_numpy_half():
+    """orc_round_f16 (the fp16 LUT rounding of orc_ivfpq_search_ex): round to nearest even, subnormals, overflow to
+    inf -- equal to numpy's float32 -> float16 -> float32 on every sampled value"""
+    rng = np.random.default_rng(11)
+    v = np.concatenate([
+        rng.standard_normal(50000).astype(np.float32) * np.float32(10.0) ** rng.integers(-8, 6, 50000),
+        np.float32([0.0, -0.0, 65504.0, 65519.99, 65520.0, -65520.0, 6.1e-5, 5.96e-8, 2.98e-8, 1e-9, 1e30]),
+        # halfway cases: odd and even mantissas at several exponents
+        ((np.arange(1, 2000, dtype=np.float32) + 0.5) * np.float32(2.0 ** -10)).astype(np.float32),
+    ]).astype(np.float32)
+    got = np.array([O.round_f16(t) for t in v.tolist()], dtype=np.float32)
+    with np.errstate(over="ignore"):
+        ref = v.astype(np.float16).astype(np.float32)
+    np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def test_fp16_lut_search_sums_rounded_entries():
+    """lut_fp16: each distance = sum over subspaces of the fp16-rounded LUT entry, accumulated in fp32; the
+    ranking stays close to the fp32 LUT's"""
+    x = _data(2500, 32, 6)
+    q = _data(15, 32, 7)
+    cents, cbs, sizes, ids, codes = O.ivfpq_build(x, 5, pq_dim=8, iters=3, max_per_code=8)
+    d32, i32, _ = O.ivfpq_search(cents, cbs, sizes, ids, codes, q, 5, 10)
+    d16, i16, _ = O.ivfpq_search(cents, cbs, sizes, ids, codes, q, 5, 10, lut_fp16=True)
+    pl = O.pq_len(32, 8)
+    lab = np.repeat(np.arange(5), sizes)
+    pos = {int(r): j for j, r in enumerate(ids)}
+    for qi in range(15):
+        for c in range(10):
+            row = pos[int(i16[qi, c])]
+            r = (q[qi] - cents[lab[row]]).reshape(8, pl)
+            lut = ((r - cbs[np.arange(8), codes[row]]) ** 2).sum(-1).astype(np.float32)
+            ref = np.float64(lut.astype(np.float16).astype(np.float32)).sum()
+            assert abs(d16[qi, c] - ref) <= 2e-3 * max(1.0, abs(ref)), (qi, c, d16[qi, c], ref)
+    assert (i16 == i32).mean() > 0.8
+    assert np.abs(d16 - d32).max() < 0.05 * np.abs(d32).max()
