@@ -140,7 +140,7 @@ def test_config2_ivf_10m_oracle_on_query_sample(ivf_10m, x10m_host):
     from mivs.neighbors import ivf_flat
 
     x, q, idx = ivf_10m
-    s = _sample(q.shape[0], 200, 2)
+    s = _sample(q.shape[0], 1000, 2)
     qs = q[torch.from_numpy(s).to("cuda:0")]
     probes = torch.empty((len(s), 32), dtype=torch.int32, device="cuda:0")
     d, i = ivf_flat.search(ivf_flat.SearchParams(n_probes=32), idx, qs, 10, probes_out=probes)
@@ -195,7 +195,7 @@ def test_config2_ivf_10m_large_k_equals_exact_all_queries_and_oracle_sample(ivf_
         idx.set_prefilter(True)
     np.testing.assert_array_equal(i_pf.cpu().numpy(), i_ex.cpu().numpy())
     np.testing.assert_array_equal(_bits(d_pf.cpu().numpy()), _bits(d_ex.cpu().numpy()))
-    s = _sample(q.shape[0], 12, 5)
+    s = _sample(q.shape[0], 500, 5)
     od, oi, _ = O.ivf_search(x10m_host, idx.centers.cpu().numpy(), idx.list_sizes.numpy(), idx.list_ids().cpu().numpy(),
                              q.cpu().numpy()[s], 32, k)
     np.testing.assert_array_equal(i_pf.cpu().numpy()[s], oi)
