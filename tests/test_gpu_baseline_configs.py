@@ -301,4 +301,10 @@ def test_config4_share_ivf_pq_12m5_fp16_oracle_on_query_sample(mivs_lib):
     od, oi, _ = O.ivfpq_search(cents, books, sizes, ids, codes, q.cpu().numpy(), 32, 10)
     np.testing.assert_array_equal(i.cpu().numpy(), oi)
     np.testing.assert_array_equal(_bits(d.cpu().numpy()), _bits(od))
+    # the opt-in fp16 LUT (cuVS lut_dtype) at the same scale, k = 10 and the refined line's 120 candidates
+    for k in (10, 120):
+        d, i = ivf_pq.search(ivf_pq.SearchParams(n_probes=32, lut_dtype=np.float16), idx, q, k)
+        od, oi, _ = O.ivfpq_search(cents, books, sizes, ids, codes, q.cpu().numpy(), 32, k, lut_fp16=True)
+        np.testing.assert_array_equal(i.cpu().numpy(), oi)
+        np.testing.assert_array_equal(_bits(d.cpu().numpy()), _bits(od))
     idx.close()
