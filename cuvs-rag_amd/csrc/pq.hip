@@ -1057,21 +1057,19 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
             }
             __builtin_amdgcn_sched_barrier(0);
           }
-        }
+        } else {
 #pragma unroll
-        for (int i = 0; i < (H16 ? 0 : RPT); ++i) {
-          if (i < nvi && !skip_scan) {
-            const int code = (cw[i] >> (8 * b)) & 0xFF;
-            {
-              const float4* p = reinterpret_cast<const float4*>(lut + code * LS);
+          for (int i = 0; i < RPT; ++i) {
+            if (i < nvi && !skip_scan) {
+              const float4* p = reinterpret_cast<const float4*>(lut + ((cw[i] >> (8 * b)) & 0xFF) * LS);
               const float4 v0 = p[0], v1 = p[1], v2 = p[2], v3 = p[3];
               acc[i][0] += v0.x; acc[i][1] += v0.y; acc[i][2] += v0.z; acc[i][3] += v0.w;
               acc[i][4] += v1.x; acc[i][5] += v1.y; acc[i][6] += v1.z; acc[i][7] += v1.w;
               acc[i][8] += v2.x; acc[i][9] += v2.y; acc[i][10] += v2.z; acc[i][11] += v2.w;
               acc[i][12] += v3.x; acc[i][13] += v3.y; acc[i][14] += v3.z; acc[i][15] += v3.w;
             }
+            __builtin_amdgcn_sched_barrier(0);  // one row's 16 LUT floats in flight: bounds the VGPRs
           }
-          __builtin_amdgcn_sched_barrier(0);  // one row's 16 LUT floats in flight: bounds the VGPRs
         }
         if ((b & 1) == 1 && j + 1 < a.pq_dim && !(a.flags & 1)) build2(j + 1, bk, bnk);
       }
