@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--gt-queries", type=int, default=1000)
     ap.add_argument("--centers", type=int, default=65536)
     ap.add_argument("--sigma", type=float, default=0.75)
+    ap.add_argument("--lut-dtype", default="float32", choices=["float32", "float16"],
+                    help="SearchParams.lut_dtype (float16: the opt-in fp16 LUT)")
     ap.add_argument("--refine-ratios", default="4,10,20,40",
                     help="cuVS-style refinement: ivf_pq.search for ratio*k candidates, then exact re-ranking "
                          "against the fp16 rows (mivs.neighbors.refine)")
@@ -60,7 +62,7 @@ def main():
     sweep = []
     sizes = idx.list_sizes.cpu()
     for npb in [int(s) for s in a.sweep.split(",") if s.strip()]:
-        sp = ivf_pq.SearchParams(n_probes=npb)
+        sp = ivf_pq.SearchParams(n_probes=npb, lut_dtype=np.dtype(a.lut_dtype).type)
         ivf_pq.search(sp, idx, q, k)
         _native.set_profiling(True)
         idx.profile_collect()
