@@ -68,8 +68,15 @@ def parse():
     ap.add_argument("--centers", type=int, default=65536, help="mixture centres of the synthetic corpus")
     ap.add_argument("--sigma", type=float, default=0.75)
     ap.add_argument("--gt-queries", type=int, default=2000, help="queries with exact ground truth for recall")
-    ap.add_argument("--sweep", default="8,16,32,64", help="comma list of n_probes to sweep (QPS + recall each); "
-                                                           "'' to skip")
+    ap.add_argument("--sweep", default="8,16,20,24,32,64", help="comma list of n_probes to sweep (QPS + recall each); "
+                                                                "'' to skip")
+    ap.add_argument("--cpu-sweep", default="16,20,24,32",
+                    help="n_probes of the CPU baseline's sweep (matched-recall point); '' to skip")
+    ap.add_argument("--cpu-build-rows", type=int, default=2_000_000,
+                    help="corpus rows the CPU build baseline's add is timed on (scaled to the corpus; 0: skip)")
+    ap.add_argument("--block-cache-gb", type=float, default=96.0,
+                    help="engine block cache (opt-in, DESIGN.md §5) enabled for the warm builds after the cold one; "
+                         "0 keeps it off")
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="target duration of each CPU-baseline sample (the node's cores, then the job's share)")
     ap.add_argument("--latency", default="1,10,100",
@@ -94,7 +101,8 @@ def parse():
                     help="side line (N=1 launch): the reference's one-process shape -- every visible GPU holds a "
                          "rows-per-GPU shard, ParallelIndexBuilder threads build them, SearchResultAggregator "
                          "searches them and merges over RCCL (LocalComm); 0 to skip")
-    ap.add_argument("--build-warmup", type=int, default=1, help="untimed builds before the timed one (allocator warm-up)")
+    ap.add_argument("--build-warmup", type=int, default=1,
+                    help="untimed warm builds between the cold (first) build and the timed warm one")
     ap.add_argument("--single-process-timeout", type=float, default=240.0,
                     help="seconds the one-process multi-GPU side line may take before it is abandoned")
     ap.add_argument("--json-out", default="")
@@ -146,6 +154,23 @@ def load_traffic(cfg_key: str):
     return None, None
 
 
+MAX_SCLK_MHZ = 2400.0  # MI355X max engine clock (MI355X_MICROARCH.md): the dense MFMA peaks are quoted at it
+
+
+def load_clock(cfg_key: str):
+    """The clock the fine-scan kernel held (GRBM_GUI_ACTIVE / 8 XCDs / kernel time, MI355X_MICROARCH.md 'DVFS
+    give-back') from the committed rocprofv3 --pmc pass of this configuration, if one matches."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*clock*.json")), reverse=True):
+        try:
+            with open(path) as f:
+                j = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if j.get("config_key") == cfg_key and j.get("clock_mhz_held"):
+            return j, os.path.relpath(path, ROOT)
+    return None, None
+
+
 def host_cpu_info() -> dict:
     """What the CPU baseline ran on: model, logical / physical cores and NUMA nodes of the node (lscpu),
     the cores this process may run on (sched_getaffinity) and the share the job is given (OMP_NUM_THREADS,
@@ -179,70 +204,237 @@ def host_cpu_info() -> dict:
 
 
 def node_threads() -> int:
-    """Every hardware thread this process may run on (sched_getaffinity): north_star's 'the node's own host cores'."""
+    """Every hardware thread this process may run on (sched_getaffinity)."""
     try:
         return max(1, len(os.sched_getaffinity(0)))
     except AttributeError:
         return os.cpu_count() or 1
 
 
-def cpu_threads() -> int:
-    """The job's CPU share: the node's threads capped by OMP_NUM_THREADS when the harness sets it (16 per GPU)."""
-    n = node_threads()
+def cgroup_cpu_quota():
+    """CPUs' worth of time the process's cgroup may use per period (cgroup v2 cpu.max, v1 cfs_quota_us / period), or
+    None when unlimited or unreadable, and the file it came from."""
+    try:
+        with open("/proc/self/cgroup") as f:
+            rel = [ln.strip().split(":", 2)[2] for ln in f if ln.startswith("0::")]
+    except (OSError, IndexError):
+        rel = []
+    cands = [os.path.join("/sys/fs/cgroup", r.lstrip("/"), "cpu.max") for r in rel] + ["/sys/fs/cgroup/cpu.max"]
+    for path in cands:
+        try:
+            with open(path) as f:
+                q, per = f.read().split()[:2]
+            return (None if q == "max" else float(q) / float(per)), path
+        except (OSError, ValueError):
+            continue
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return (None if q <= 0 else q / per), "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"
+    except (OSError, ValueError):
+        return None, None
+
+
+def effective_cpus() -> dict:
+    """The host cores the CPU baseline can actually use: the affinity set capped by the cgroup's CPU quota (a
+    quota of 16 CPUs on a 256-thread affinity set throttles 256 threads to 16 CPUs' worth of time, with every
+    thread descheduled for most of each period -- why the round-5 line ran slower on 256 threads than on 16)."""
+    import math
+
+    aff = node_threads()
+    quota, src = cgroup_cpu_quota()
+    eff = aff if quota is None else max(1, min(aff, int(math.floor(quota + 1e-6))))
     omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    return max(1, min(n, omp) if omp else n)
+    return {"effective": eff, "affinity": aff, "cgroup_quota_cpus": quota, "cgroup_file": src,
+            "omp_num_threads": omp or None,
+            "limited_by": "cgroup cpu quota" if quota is not None and eff < aff else "affinity set"}
 
 
-def cpu_baseline(idx, q_host, gt, n_probes, k, target_s, rank_log):
-    """FAISS-algorithm IVF-Flat search (oracle/cpu_baseline.c, OpenMP over queries) on this host: `value` on every
-    thread of the node (the affinity set), `value_job_share` on the job's share (OMP_NUM_THREADS); each on a query
-    sample sized for ~target_s seconds."""
+def cpu_threads() -> int:
+    """Threads for the CPU legs: the effective cores (affinity set capped by the cgroup quota)."""
+    return effective_cpus()["effective"]
+
+
+def host_copy_rows(t_dev, threads, chunk_rows=1 << 20):
+    """A host numpy copy of a device [n, d] fp32 tensor, first-touched by `threads` OpenMP threads (orc_parallel_copy:
+    the pages spread over the NUMA nodes of the threads that will scan them), staged through ~3 GB pageable chunks."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # (the cpu_baseline leg: an allowed oracle user)
+
+    O.fast_set_threads(threads)
+    n = t_dev.shape[0]
+    out = np.empty(tuple(t_dev.shape), dtype=np.float32)
+    for a0 in range(0, n, chunk_rows):
+        h = t_dev[a0:a0 + chunk_rows].cpu().numpy()
+        O.parallel_copy(out[a0:a0 + h.shape[0]], np.ascontiguousarray(h))
+        del h
+    return out
+
+
+def cpu_baseline(idx, q_host, gt, n_probes, k, target_s, rank_log, sweep=(), gpu_sweep=None):
+    """FAISS-algorithm IVF-Flat search (oracle/cpu_baseline.c: IndexIVFFlat's per-query scan, OpenMP over queries,
+    AVX-512 / AVX2 workers picked for this host) on the effective cores (the affinity set capped by the cgroup CPU
+    quota), on the same index copied to host memory first-touched in parallel. Each point on a query sample of >= 8
+    queries per thread sized for ~target_s seconds; `value` at n_probes (the headline's), `n_probes_sweep` at the
+    points of `sweep`, and the matched-recall point: the smallest swept n_probes reaching recall@10 >= 0.95."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # bench.py's cpu_baseline leg is one of the oracle's allowed users
 
-    rank_log(f"[cpu] copying index to host ({idx.size} rows) ...")
-    rows = idx.list_rows().cpu().numpy()
+    cpus = effective_cpus()
+    threads = cpus["effective"]
+    rank_log(f"[cpu] host cores: {cpus}; copying the index to host ({idx.size} rows, parallel first touch) ...")
+    t0 = time.perf_counter()
+    rows_dev = idx.list_rows()
+    rows = host_copy_rows(rows_dev, threads)
+    del rows_dev
+    torch.cuda.empty_cache()
+    t_copy = time.perf_counter() - t0
     ids = idx.list_ids().cpu().numpy()
     sizes = idx.list_sizes.numpy()
     off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
     cents = idx.centers.cpu().numpy()
 
-    def timed(threads, q0):
-        O.fast_set_threads(threads)
-        O.fast_ivf_search(rows, ids, off, cents, q_host[q0:q0 + 4], n_probes, k)  # warm caches / pages / threads
-        n16 = max(16, threads)
+    def timed(nthreads, npr, tgt, q0=0, min_per_thread=8):
+        O.fast_set_threads(nthreads)
+        O.fast_ivf_search(rows, ids, off, cents, q_host[q0:q0 + nthreads], npr, k)  # warm threads / pages
+        n0 = nthreads
         t0 = time.perf_counter()
-        O.fast_ivf_search(rows, ids, off, cents, q_host[q0:q0 + n16], n_probes, k)
-        per_q = (time.perf_counter() - t0) / n16
-        ns = int(max(n16, min(q_host.shape[0] - q0, target_s / max(per_q, 1e-9))))
+        O.fast_ivf_search(rows, ids, off, cents, q_host[q0:q0 + n0], npr, k)
+        per_q = (time.perf_counter() - t0) / n0
+        ns = int(max(min_per_thread * nthreads, min(q_host.shape[0] - q0, tgt / max(per_q, 1e-9))))
+        ns = min(ns, q_host.shape[0] - q0)
         t0 = time.perf_counter()
-        _, ci = O.fast_ivf_search(rows, ids, off, cents, q_host[q0:q0 + ns], n_probes, k)
+        _, ci = O.fast_ivf_search(rows, ids, off, cents, q_host[q0:q0 + ns], npr, k)
         return ns, time.perf_counter() - t0, ci
 
-    node, job = node_threads(), cpu_threads()
-    ns, dt, ci = timed(node, 0)
-    nr = min(ns, gt.shape[0])
-    rec = recall_at_k(ci[:nr], gt[:nr]) if nr > 0 else None
-    share = None
-    if job != node:
-        ns_j, dt_j, _ = timed(job, 0)
-        share = {"value": ns_j / dt_j, "cores": job, "sample": f"{ns_j} queries, {dt_j:.1f} s"}
+    def rec_of(ci, ns):
+        nr = min(ns, gt.shape[0])
+        return recall_at_k(ci[:nr], gt[:nr]) if nr > 0 else None
+
+    ns, dt, ci = timed(threads, n_probes, target_s)
+    rec = rec_of(ci, ns)
+    out = {"value": ns / dt, "unit": "QPS", "cores": threads, "kind": "port", "isa": O.fast_isa(),
+           "host": host_cpu_info(), "cpus": cpus, "host_copy_s": round(t_copy, 2),
+           "sample": f"{ns} of the {q_host.shape[0]} benchmark queries ({ns / threads:.0f} per thread), same index "
+                     f"(copied to host, pages first-touched by the {threads} threads), n_probes={n_probes}, k={k}; "
+                     f"FAISS IndexIVFFlat search algorithm restated in oracle/cpu_baseline.c (faiss not installed), "
+                     f"OpenMP over queries; {dt:.1f} s",
+           "recall_at_10": rec,
+           "cores_note": f"cores = the {threads} CPUs this process can use: its affinity set ({cpus['affinity']} "
+                         f"threads) capped by the cgroup CPU quota ({cpus['cgroup_quota_cpus']} CPUs, "
+                         f"{cpus['cgroup_file']})"}
+    if cpus["affinity"] > threads:
+        # the diagnostic behind the cap: every affinity thread against the quota (one short sample)
+        ns_a, dt_a, _ = timed(cpus["affinity"], n_probes, 0.0, min_per_thread=1)
+        out["all_affinity_threads"] = {"value": ns_a / dt_a, "threads": cpus["affinity"],
+                                       "sample": f"{ns_a} queries, {dt_a:.1f} s",
+                                       "note": "oversubscribed: more threads than the cgroup quota's CPUs"}
+    pts = []
+    for npr in sweep:
+        if npr == n_probes:
+            pts.append({"n_probes": npr, "qps": ns / dt, "recall_at_10": rec, "queries": ns})
+            continue
+        ns_s, dt_s, ci_s = timed(threads, npr, target_s / 2)
+        pts.append({"n_probes": npr, "qps": ns_s / dt_s, "recall_at_10": rec_of(ci_s, ns_s), "queries": ns_s})
+        rank_log(f"[cpu] n_probes={npr}: {ns_s / dt_s:.1f} QPS recall {pts[-1]['recall_at_10']}")
+    out["n_probes_sweep"] = pts
+    if pts and gpu_sweep:
+        out["matched_recall"] = matched_recall(gpu_sweep, pts)
     del rows
-    host = host_cpu_info()
-    return {"value": ns / dt, "unit": "QPS", "cores": node, "kind": "port", "host": host,
-            "value_job_share": share["value"] if share else ns / dt,
-            "value_best": max(ns / dt, share["value"] if share else 0.0),
-            "job_share": share or {"cores": node, "note": "the job's share is the whole affinity set"},
-            "cores_note": f"value: all {node} hardware threads this process may run on (sched_getaffinity; the node "
-                          f"has {host.get('physical_cores')} cores / {host.get('logical_cpus')} threads); "
-                          f"value_job_share: the {job} threads the harness gives one GPU's job (OMP_NUM_THREADS); "
-                          "the search is OpenMP over queries. On a node shared by 8 GPU jobs the other jobs hold most "
-                          "of the node's threads, so the whole node can run slower than the job's share: value_best "
-                          "is the faster of the two",
-            "sample": f"{ns} of the {q_host.shape[0]} benchmark queries, same index (copied to host), n_probes="
-                      f"{n_probes}, k={k}; FAISS IndexIVFFlat search algorithm restated in oracle/cpu_baseline.c "
-                      f"(faiss not installed); {dt:.1f} s",
-            "recall_at_10": rec}
+    return out
+
+
+def matched_recall(gpu_sweep, cpu_sweep, target=0.95):
+    """each side's QPS at its smallest swept n_probes with recall@10 >= target."""
+    def pick(pts, qkey):
+        ok = [p for p in pts if p.get("recall_at_10") is not None and p["recall_at_10"] >= target]
+        if not ok:
+            return None
+        b = min(ok, key=lambda p: p["n_probes"])
+        return {"n_probes": b["n_probes"], "qps": round(b[qkey], 2), "recall_at_10": round(b["recall_at_10"], 4)}
+
+    g, c = pick(gpu_sweep, "qps_full_corpus"), pick(cpu_sweep, "qps")
+    out = {"target_recall_at_10": target, "gpu": g, "cpu": c}
+    if g and c:
+        out["gpu_over_cpu"] = round(g["qps"] / c["qps"], 1)
+    return out
+
+
+def faiss_kmeans_train(xt, n_lists, niter=10, seed=1234):
+    """FAISS Clustering::train as IndexIVFFlat.train runs it (Level1Quantizer sets cp.niter = 10;
+    max_points_per_centroid 256): the training set subsampled to 256 x n_lists rows (a random permutation, FAISS's
+    rand_perm), the first n_lists of the permutation as the initial centroids, then per iteration the assign through
+    IndexFlatL2 (BLAS: ||c||^2 - 2 x.c, argmin, per 16k-row block), the centroid means (compute_centroids) and the
+    empty-cluster split (split_clusters: an empty centroid takes a copy of a large cluster's, both nudged by
+    +-1/1024). Torch-CPU (MKL) tensors on the caller's threads."""
+    g = torch.Generator().manual_seed(seed)
+    n = xt.shape[0]
+    if n > 256 * n_lists:
+        xt = xt[torch.randperm(n, generator=g)[:256 * n_lists]].contiguous()
+        n = xt.shape[0]
+    c = xt[torch.randperm(n, generator=g)[:n_lists]].clone()
+    for _ in range(niter):
+        lab = faiss_assign(xt, c)
+        cnt = torch.bincount(lab, minlength=n_lists)
+        s = torch.zeros_like(c).index_add_(0, lab, xt)
+        nz = cnt > 0
+        c[nz] = s[nz] / cnt[nz].unsqueeze(1).to(c.dtype)
+        for j in torch.nonzero(~nz).flatten().tolist():  # split_clusters
+            big = int(torch.multinomial(cnt.double().clamp_min(0) ** 1.0, 1, generator=g))
+            c[j] = c[big] * (1 + 1 / 1024.0)
+            c[big] = c[big] * (1 - 1 / 1024.0)
+            cnt[j] = cnt[big] // 2
+            cnt[big] -= cnt[j]
+    return c, n
+
+
+def faiss_assign(x, c, bs=16384):
+    """IndexFlatL2 k=1 over the centroids (FAISS's BLAS form for nq >= 20): argmin of ||c||^2 - 2 x.c per block"""
+    cn = (c * c).sum(1)
+    out = torch.empty(x.shape[0], dtype=torch.int64)
+    for b0 in range(0, x.shape[0], bs):
+        xb = x[b0:b0 + bs]
+        out[b0:b0 + xb.shape[0]] = torch.addmm(cn[None, :], xb, c.t(), beta=1.0, alpha=-2.0).argmin(1)
+    return out
+
+
+def cpu_build_baseline(x_dev, n_lists, rows_total, threads, add_rows, rank_log):
+    """FAISS-algorithm IndexIVFFlat build (train + add) on this host's effective cores, torch-CPU (MKL sgemm) for the
+    BLAS steps as FAISS uses BLAS: train = faiss_kmeans_train on a 256 x n_lists subsample of the corpus, add = the
+    quantizer assign of every row (IndexFlatL2 BLAS form) + the list fill (rows appended to their list: a stable
+    gather in list order). The add is timed on `add_rows` rows of the corpus and scaled to rows_total:
+    build vec/s = rows_total / (train_s + add_s * rows_total / add_rows). Reference: Latest/faiss.ipynb:554-570,
+    Latest/cuVS-2-gpu/old/colab_a100_test.ipynb:472-483 (index_ivf.train + add)."""
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        xh = torch.from_numpy(host_copy_rows(x_dev[:add_rows], threads))
+        faiss_assign(xh[:20000], xh[:n_lists].clone())  # warm MKL / pages
+        t0 = time.perf_counter()
+        c, n_train = faiss_kmeans_train(xh, n_lists)
+        t_train = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        lab = faiss_assign(xh, c)
+        order = torch.sort(lab, stable=True).indices
+        lists = xh.index_select(0, order)
+        sizes = torch.bincount(lab, minlength=n_lists)
+        t_add = time.perf_counter() - t0
+        del lists, xh
+    finally:
+        torch.set_num_threads(prev)
+    add_vps = add_rows / t_add
+    total = t_train + rows_total / add_vps
+    rank_log(f"[cpu-build] train {t_train:.2f} s on {n_train} rows, add {add_vps / 1e6:.2f} M vec/s -> "
+             f"{rows_total / total / 1e6:.3f} M vec/s for {rows_total} rows on {threads} threads")
+    return {"build_vectors_per_s": round(rows_total / total, 1), "unit": "vectors/s", "cores": threads,
+            "kind": "port", "train_s": round(t_train, 3), "train_rows": n_train, "kmeans_iters": 10,
+            "add_vectors_per_s": round(add_vps, 1), "add_sample_rows": add_rows, "build_s_scaled": round(total, 2),
+            "list_sizes_min_max": [int(sizes.min()), int(sizes.max())],
+            "sample": f"FAISS IndexIVFFlat.train (Clustering: niter 10, 256 x {n_lists} = {n_train} training rows) "
+                      f"+ add (IndexFlatL2 BLAS assign + list fill) restated on torch-CPU (MKL sgemm, faiss not "
+                      f"installed); add timed on {add_rows} corpus rows and scaled to {rows_total}"}
 
 
 def faiss_blas_knn(x, qb, k, bs_x=65536):
@@ -954,13 +1146,30 @@ def main():
     # ---- build (wall clock, data resident) ----
     params = ivf_flat.IndexParams(n_lists=a.n_lists, kmeans_n_iters=a.kmeans_iters,
                                   kmeans_trainset_fraction=a.trainset_fraction)
+    # 1. the cold build: the first in the process, as each of the reference's builds is (one per GPU thread,
+    # index_building_coordinator.py:370-420): its ~54 GB of fresh device allocations are part of its time
+    _native.set_block_cache_limit(0)
     sync_all(world)
-    if a.build_warmup:  # an untimed first build: a process's first ~100 GB of device allocations can stall for
-        # seconds (once seen: 2.96 s in the copies' phase against 0.03 s), as the search's warmup steps do for it
+    _native.set_profiling(True)  # (the build's phase clocks: one stream sync per phase)
+    t0 = time.perf_counter()
+    idx_cold = ivf_flat.build(params, x, ids_offset=start)
+    torch.cuda.synchronize()
+    t_build_cold = max_over_ranks(time.perf_counter() - t0, world, dev)
+    _native.set_profiling(False)
+    build_cold_phases = idx_cold.build_phases()
+    idx_cold.close()
+    del idx_cold
+    rl(f"[build] cold (first in the process): {rows_total} rows in {t_build_cold:.2f} s -> "
+       f"{rows_total / t_build_cold / 1e6:.2f} M vec/s {build_cold_phases}")
+    # 2. warm: the engine's block cache (opt-in) keeps the released blocks, so a process that rebuilds reuses them
+    if a.block_cache_gb > 0:
+        _native.set_block_cache_limit(int(a.block_cache_gb * (1 << 30)), local)
+    sync_all(world)
+    for _ in range(a.build_warmup):
         ivf_flat.build(params, x, ids_offset=start).close()
         torch.cuda.synchronize()
         sync_all(world)
-    _native.set_profiling(True)  # (the build's phase clocks: one stream sync per phase)
+    _native.set_profiling(True)
     t0 = time.perf_counter()
     idx = ivf_flat.build(params, x, ids_offset=start)
     torch.cuda.synchronize()
@@ -1002,6 +1211,28 @@ def main():
     qps_full = Q * a.steps / t_steps
     value = qps_full  # full-corpus QPS: Q queries answered over every shard (searched + merged) per second
     rl(f"[search] {a.steps} steps x {Q} queries: {ms_per_step:.3f} ms/step -> {qps_full:,.0f} QPS (full corpus)")
+    ranks_diag = None
+    if world > 1:  # what a flat 1 -> 8 curve would need to be read: every rank's own step time and the step's parts
+        from mivs.distributed import per_rank_values, timed_sharded_step
+
+        per_rank = per_rank_values(t_local / a.steps * 1e3, dev)
+        parts = []
+        for _ in range(max(3, a.steps // 4)):
+            sync_all(world)
+            _, t_parts = timed_sharded_step(lambda: ivf_flat.search(sp, idx, q, k), k)
+            parts.append(t_parts)
+        mean = {key: sum(p_[key] for p_ in parts) / len(parts) for key in parts[0]}
+        ranks_diag = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
+                      "rccl_version": ".".join(str(v) for v in torch.cuda.nccl.version()),
+                      "per_rank_ms": [round(v, 4) for v in per_rank],
+                      "per_rank_search_ms": [round(v, 4) for v in per_rank_values(mean["search_ms"], dev)],
+                      "allgather_ms": [round(v, 4) for v in per_rank_values(mean["allgather_ms"], dev)],
+                      "merge_ms": [round(v, 4) for v in per_rank_values(mean["merge_ms"], dev)],
+                      "allgather_bytes_per_rank": Q * k * 12,
+                      "timing": f"per_rank_ms: each rank's own clock over the {a.steps} timed steps; the parts: "
+                                f"hipEvents on the search stream over {len(parts)} extra steps (search | RCCL "
+                                "all-gather of the [Q, k] (distance, id) tiles | K7 merge), mean per rank"}
+        rl(f"[ranks] {ranks_diag}")
 
     # ---- PCIe-inclusive rate (not `value`): queries start in pinned host memory, results return to host ----
     q_host = q.cpu().pin_memory()
@@ -1098,6 +1329,12 @@ def main():
         roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(gbs / PEAK_HBM_GBS, 4)}
     roof["traffic"] = traffic
+    clk, clk_src = load_clock(cfg_key)
+    if clk is not None and roof["bound"] == "mfma":
+        held = float(clk["clock_mhz_held"])
+        roof["clock_mhz_held"] = round(held, 1)
+        roof["frac_at_held_clock"] = round(roof["frac"] * MAX_SCLK_MHZ / held, 4)
+        roof["clock_source"] = clk_src
     roof.update({"kernel": f"{kname} (fine list scan, {stats['query_tile']}-query tiles)",
                  "launch_ms": round(scan_ms, 4),
                  "algorithmic_flops_per_launch": flops, "algorithmic_bytes_per_launch": bytes_alg,
@@ -1112,10 +1349,19 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(idx, q.cpu().numpy(), gt, a.n_probes, k, a.cpu_seconds, rl)
-            rl(f"[cpu] {cpu['value']:.2f} QPS on {cpu['cores']} threads (recall {cpu['recall_at_10']})")
+            cpu = cpu_baseline(idx, q.cpu().numpy(), gt, a.n_probes, k, a.cpu_seconds, rl,
+                               sweep=[int(v) for v in a.cpu_sweep.split(",") if v.strip()], gpu_sweep=sweep)
+            rl(f"[cpu] {cpu['value']:.2f} QPS on {cpu['cores']} cores (recall {cpu['recall_at_10']}); matched recall: "
+               f"{cpu.get('matched_recall')}")
         except Exception as e:  # the GPU result stands without the CPU column
             rl(f"[cpu] baseline failed: {e!r}")
+        if cpu is not None and a.cpu_build_rows > 0:
+            try:
+                cb = cpu_build_baseline(x, a.n_lists, rows_total, cpu["cores"], min(a.cpu_build_rows, n), rl)
+                cpu["build_vectors_per_s"] = cb["build_vectors_per_s"]
+                cpu["build"] = cb
+            except Exception as e:  # the search column stands without the build column
+                rl(f"[cpu-build] baseline failed: {e!r}")
 
     flat = None
     if rank == 0 and world == 1 and a.flat_rows > 0:
@@ -1212,6 +1458,14 @@ def main():
         "build_vectors_per_s": round(build_vps, 1),
         "build_s": round(t_build, 3),
         "build_phases_s": build_phases,
+        "build_cold_s": round(t_build_cold, 3),
+        "build_cold_vectors_per_s": round(rows_total / t_build_cold, 1),
+        "build_cold_phases_s": build_cold_phases,
+        "build_note": "build_s: a warm rebuild (after the cold one and --build-warmup untimed builds) with the engine's "
+                      f"opt-in block cache at {a.block_cache_gb:g} GB (mivs.set_block_cache_limit; released blocks "
+                      "reused instead of fresh page-cleared allocations); build_cold_s: the first build in the "
+                      "process, cache off, as each of the reference's builds is",
+        "matched_recall": cpu.get("matched_recall") if cpu else matched_recall(sweep, []),
         "build_roofline": build_roof,
         "index_bytes_per_row": round(index_mem["total_bytes"] / max(index_mem["n_rows"], 1), 1),
         "index_memory": index_mem,
@@ -1226,6 +1480,7 @@ def main():
         "single_process_aggregator": single,
         "ivf_pq_12m5": pq,
         "distributed": dist_info,
+        "ranks": ranks_diag,
     }
     if rank == 0:
         line = json.dumps(out)

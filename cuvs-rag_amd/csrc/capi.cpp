@@ -226,9 +226,55 @@ struct mivs_index_s {
   std::vector<double> build_phase_s;
   // device time and algorithmic work of the build's hot kernels (mivs_index_build_kernels; profiling on)
   mivs_build_kernel build_kern[MIVS_BUILD_KERNEL_KINDS] = {};
+  // an event per stream the index's calls were enqueued on, recorded at the end of each call: mivs_index_free waits
+  // for these (not for the whole device) before its buffers go back to the driver or the block cache
+  struct StreamDone {
+    hipStream_t s;
+    hipEvent_t ev;
+  };
+  std::vector<StreamDone> stream_done;
+  ~mivs_index_s() {
+    for (auto& e : stream_done) (void)hipEventDestroy(e.ev);
+  }
 };
 
 namespace {
+
+// record the index's done-event for stream s (the index's device is current)
+void note_stream(mivs_index_s* idx, hipStream_t s) {
+  for (auto& e : idx->stream_done)
+    if (e.s == s) {
+      (void)hipEventRecord(e.ev, s);
+      return;
+    }
+  if (idx->stream_done.size() >= 8) {  // (a caller cycling through many streams: retire the oldest)
+    (void)hipEventSynchronize(idx->stream_done.front().ev);
+    (void)hipEventDestroy(idx->stream_done.front().ev);
+    idx->stream_done.erase(idx->stream_done.begin());
+  }
+  hipEvent_t ev = nullptr;
+  if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  (void)hipEventRecord(ev, s);
+  idx->stream_done.push_back({s, ev});
+}
+
+// wait for every call enqueued on the index so far (its done-events; the index's device is current)
+void wait_index(mivs_index_s* idx) {
+  for (auto& e : idx->stream_done) HIPCHK(hipEventSynchronize(e.ev));
+}
+
+// one C-ABI call on an index: its stream is the thread's release stream while it runs (Buf::release orders a cached
+// block's reuse after it), and the index's done-event for that stream is recorded when it ends
+struct IndexCall {
+  mivs_index_s* idx;
+  hipStream_t s;
+  StreamScope ss;
+  IndexCall(mivs_index_s* i, hipStream_t s_) : idx(i), s(s_), ss(s_) {}
+  ~IndexCall() { note_stream(idx, s); }
+};
 
 // ---- one scan job: lists x buckets -> partial slots ----
 struct ScanJob {
@@ -1009,9 +1055,20 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
 // reading the count on the host). MIVS_FALLBACK_SYNC=1 keeps the host-sized path (A/B runs).
 // (the device-sized probe map is one workgroup: up to 2M (query, probe) entries, ~1 ms when every query of such a batch
 // falls back; beyond that the host-sized path keeps the multi-workgroup map)
+// (MIVS_FALLBACK_SYNC is read once, at the first search after load or mivs_reload_settings)
+std::atomic<int> g_fallback_sync{-1};
+
 bool device_fallback_ok(const mivs_index_s* idx, int k, int64_t nq, int np) {
-  return env_int("MIVS_FALLBACK_SYNC", 0) == 0 && nq * (int64_t)np <= ((int64_t)1 << 21) && idx->kind == 0 && k <= kMaxK && idx->lists.n_lists <= probe_map_dev_max_lists();
+  int fs = g_fallback_sync.load(std::memory_order_relaxed);
+  if (fs < 0) {
+    fs = env_int("MIVS_FALLBACK_SYNC", 0) != 0 ? 1 : 0;
+    g_fallback_sync.store(fs, std::memory_order_relaxed);
+  }
+  return fs == 0 && nq * (int64_t)np <= ((int64_t)1 << 21) && idx->kind == 0 && k <= kMaxK &&
+         idx->lists.n_lists <= probe_map_dev_max_lists();
 }
+
+void reload_settings() { g_fallback_sync.store(-1, std::memory_order_relaxed); }
 
 void exact_fallback_on_device(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np,
                               float* out_d, int64_t* out_i) {
@@ -1912,6 +1969,7 @@ int32_t mivs_ivf_flat_build(int32_t device, void* stream, const float* d_data, i
     DeviceGuard dg(device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     auto idx = std::make_unique<mivs_index_s>();
+    IndexCall ic(idx.get(), s);
     idx->kind = 0;
     idx->device = device;
     idx->d = dim;
@@ -1988,6 +2046,7 @@ int32_t mivs_ivf_flat_build_from_centroids(int32_t device, void* stream, const f
     DeviceGuard dg(device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     auto idx = std::make_unique<mivs_index_s>();
+    IndexCall ic(idx.get(), s);
     idx->kind = 0;
     idx->device = device;
     idx->d = dim;
@@ -2028,6 +2087,7 @@ int32_t mivs_ivf_flat_build_from_lists(int32_t device, void* stream, const float
     DeviceGuard dg(device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     auto idx = std::make_unique<mivs_index_s>();
+    IndexCall ic(idx.get(), s);
     idx->kind = 0;
     idx->device = device;
     idx->d = dim;
@@ -2055,6 +2115,7 @@ int32_t mivs_ivf_flat_extend(mivs_index_t idx, void* stream, const float* d_new,
     std::lock_guard<std::mutex> g(idx->mu);
     DeviceGuard dg(idx->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
+    IndexCall ic(idx, s);
     ListSet& L = idx->lists;
     const int d = idx->d;
     const int nl = idx->cents.n_lists == 1 ? (int)idx->cents.n_rows : idx->cents.n_lists;
@@ -2126,6 +2187,7 @@ int32_t mivs_ivf_flat_search(mivs_index_t idx, void* stream, const float* d_q, i
       ht.n_wait = 0;
       ht.t0 = std::chrono::steady_clock::now();
     }
+    IndexCall ic(idx, static_cast<hipStream_t>(stream));
     ivf_search_impl(idx, static_cast<hipStream_t>(stream), d_q, nq, k, np, d_dist, d_ids, d_probes);
     if (trace) {
       const auto t1 = std::chrono::steady_clock::now();
@@ -2141,6 +2203,7 @@ int32_t mivs_ivf_flat_get_centroids(mivs_index_t idx, void* stream, float* d_out
   return guarded([&] {
     require(idx != nullptr && (idx->kind == 0 || idx->kind == 2), "not an IVF index");
     DeviceGuard dg(idx->device);
+    IndexCall ic(idx, static_cast<hipStream_t>(stream));
     HIPCHK(hipMemcpyAsync(d_out, idx->centroids_rm.p, sizeof(float) * (size_t)idx->lists.n_lists * idx->d,
                           hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
   });
@@ -2157,6 +2220,7 @@ int32_t mivs_ivf_flat_get_list_ids(mivs_index_t idx, void* stream, int64_t* d_ou
   return guarded([&] {
     require(idx != nullptr, "index is NULL");
     DeviceGuard dg(idx->device);
+    IndexCall ic(idx, static_cast<hipStream_t>(stream));
     const ListSet& L = idx->lists;
     HIPCHK(launch_compact_ids(L.ids.as<int64_t>(), L.off.as<int64_t>(), L.goff.as<int64_t>(), L.n_lists, L.n_rows,
                               d_out, static_cast<hipStream_t>(stream)));
@@ -2167,6 +2231,7 @@ int32_t mivs_ivf_flat_get_list_rows(mivs_index_t idx, void* stream, float* d_out
   return guarded([&] {
     require(idx != nullptr, "index is NULL");
     DeviceGuard dg(idx->device);
+    IndexCall ic(idx, static_cast<hipStream_t>(stream));
     const ListSet& L = idx->lists;
     HIPCHK(launch_unpack_rows(L.groups.as<float>(), idx->dp, idx->d, L.off.as<int64_t>(), L.goff.as<int64_t>(),
                               L.n_lists, L.n_rows, d_out, static_cast<hipStream_t>(stream)));
@@ -2194,6 +2259,7 @@ int32_t mivs_ivf_pq_build(int32_t device, void* stream, const float* d_data, int
     DeviceGuard dg(device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     auto idx = std::make_unique<mivs_index_s>();
+    IndexCall ic(idx.get(), s);
     idx->kind = 2;
     idx->device = device;
     idx->d = dim;
@@ -2344,6 +2410,7 @@ int32_t mivs_ivf_pq_search_ex(mivs_index_t idx, void* stream, const float* d_q, 
     std::lock_guard<std::mutex> g(idx->mu);
     DeviceGuard dg(idx->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
+    IndexCall ic(idx, s);
     const int np = std::min<int>(n_probes, idx->lists.n_lists);
     require(np <= kMaxSelectK, "n_probes must be <= " + std::to_string(kMaxSelectK), MIVS_ERR_UNSUPPORTED);
     require(np == n_probes || d_probes == nullptr, "n_probes > n_lists with a probes output");
@@ -2610,6 +2677,7 @@ int32_t mivs_ivf_pq_get_codebooks(mivs_index_t idx, void* stream, float* d_out) 
   return guarded([&] {
     require(idx != nullptr && idx->kind == 2, "not an ivf_pq index");
     DeviceGuard dg(idx->device);
+    IndexCall ic(idx, static_cast<hipStream_t>(stream));
     HIPCHK(hipMemcpyAsync(d_out, idx->pq_books.p, sizeof(float) * (size_t)idx->pq_dim * (1 << idx->pq_bits) * idx->pq_len,
                           hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
   });
@@ -2619,6 +2687,7 @@ int32_t mivs_ivf_pq_get_codes(mivs_index_t idx, void* stream, uint8_t* d_out) {
   return guarded([&] {
     require(idx != nullptr && idx->kind == 2, "not an ivf_pq index");
     DeviceGuard dg(idx->device);
+    IndexCall ic(idx, static_cast<hipStream_t>(stream));
     const ListSet& L = idx->lists;
     HIPCHK(launch_pq_unpack(static_cast<const uint8_t*>(idx->pq_codes.p), L.n_rows, L.off.as<int64_t>(),
                             L.goff.as<int64_t>(), L.n_lists, idx->pq_dim, idx->pq_dim_pad, d_out,
@@ -2635,6 +2704,7 @@ int32_t mivs_brute_force_build(int32_t device, void* stream, const float* d_data
     DeviceGuard dg(device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     auto idx = std::make_unique<mivs_index_s>();
+    IndexCall ic(idx.get(), s);
     idx->kind = 1;
     idx->device = device;
     idx->d = dim;
@@ -2658,6 +2728,7 @@ int32_t mivs_brute_force_search(mivs_index_t idx, void* stream, const float* d_q
     std::lock_guard<std::mutex> g(idx->mu);
     DeviceGuard dg(idx->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
+    IndexCall ic(idx, s);
     ProfRec* pr = g_profiling.load() ? idx->prof.begin(s) : nullptr;
     idx->ws.qn.reserve(sizeof(float) * nq);
     HIPCHK(launch_row_norms(d_q, nq, idx->d, idx->ws.qn.as<float>(), s));
@@ -2720,9 +2791,9 @@ int32_t mivs_index_last_search_stats(mivs_index_t idx, mivs_search_stats* out) {
     st.scan_kernel = idx->last_scan;
     st.overflow_queries = idx->last_ovf;
     st.window_candidates = idx->last_window;
+    wait_index(idx);  // (the last search may still run on its stream: its stats are written by the device)
     if (idx->last_stats_dev) {  // (the device-sized fallback left them in ws.pf_stats: {count, pad, window})
       int64_t h[2] = {0, 0};
-      HIPCHK(hipDeviceSynchronize());
       HIPCHK(hipMemcpy(h, idx->ws.pf_stats.p, sizeof(h), hipMemcpyDeviceToHost));
       st.overflow_queries = (int64_t)(int32_t)(h[0] & 0xFFFFFFFF);
       st.window_candidates = h[1];
@@ -2730,7 +2801,6 @@ int32_t mivs_index_last_search_stats(mivs_index_t idx, mivs_search_stats* out) {
     st.copies_skipped = idx->copies_skipped;
     const ListSet& L = idx->lists;
     if (idx->last_nq > 0 && idx->kind == 0) {
-      HIPCHK(hipDeviceSynchronize());
       std::vector<int> counts(L.n_lists), woff(L.n_lists + 1);
       // K13: its own probe map's counts (the exact fallback of unproven queries maps only those)
       const Buf& cb = idx->last_scan == 13 ? idx->ws.stat_counts : idx->ws.counts;
@@ -2839,6 +2909,7 @@ int32_t mivs_index_set_prefilter(mivs_index_t idx, void* stream, int32_t enable)
     std::lock_guard<std::mutex> g(idx->mu);
     DeviceGuard dg(idx->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
+    IndexCall ic(idx, s);
     HIPCHK(hipStreamSynchronize(s));
     if (enable) {
       if (!idx->groups_h.p) pf_enable(idx, s);
@@ -2861,9 +2932,42 @@ void mivs_index_free(mivs_index_t idx) {
   int prev = -1;
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(idx->device);
+  // wait for the index's own calls (their done-events), not for the device: a concurrent search on another index of
+  // this GPU keeps running; the buffers then go back without further waiting
+  bool synced = true;
+  for (auto& e : idx->stream_done) synced = hipEventSynchronize(e.ev) == hipSuccess && synced;
+  (void)hipGetLastError();
+  tl_release_synced = synced && !idx->stream_done.empty();
   delete idx;
+  tl_release_synced = false;
   if (prev >= 0) (void)hipSetDevice(prev);
 }
+
+int32_t mivs_set_block_cache_limit(int32_t device, int64_t bytes) {
+  return guarded([&] {
+    require(bytes >= 0, "bytes must be >= 0");
+    require(device >= -1 && device < BlockCache::kMaxDev, "device out of range");
+    BlockCache::get().set_limit(device, (size_t)bytes);
+  });
+}
+
+int32_t mivs_release_cached_memory(int32_t device, int64_t* freed_bytes) {
+  return guarded([&] {
+    require(device >= -1 && device < BlockCache::kMaxDev, "device out of range");
+    const size_t f = BlockCache::get().flush(device);
+    if (freed_bytes) *freed_bytes = (int64_t)f;
+  });
+}
+
+int32_t mivs_cached_memory(int32_t device, int64_t* bytes, int64_t* limit) {
+  return guarded([&] {
+    require(device >= -1 && device < BlockCache::kMaxDev, "device out of range");
+    if (bytes) *bytes = (int64_t)BlockCache::get().cached(device);
+    if (limit) *limit = device >= 0 ? (int64_t)BlockCache::get().limit_of(device) : -1;
+  });
+}
+
+void mivs_reload_settings(void) { reload_settings(); }
 
 int32_t mivs_kmeans_fit(int32_t device, void* stream, const float* d_data, int64_t n, int32_t dim,
                         const int64_t* d_rows, int64_t n_train, int32_t n_clusters, int32_t n_iters,
@@ -2874,6 +2978,7 @@ int32_t mivs_kmeans_fit(int32_t device, void* stream, const float* d_data, int64
     require(n_train >= 1 && (d_rows != nullptr || n_train <= n), "bad trainset");
     DeviceGuard dg(device);
     hipStream_t s = static_cast<hipStream_t>(stream);
+    StreamScope ss(s);
     Workspace ws;
     Buf norms;
     norms.reserve(sizeof(float) * std::max<int64_t>(n, 1));
@@ -2894,6 +2999,7 @@ int32_t mivs_kmeans_steps(int32_t device, void* stream, const float* d_data, int
     if (n_steps == 0) return;
     DeviceGuard dg(device);
     hipStream_t s = static_cast<hipStream_t>(stream);
+    StreamScope ss(s);
     Workspace ws;
     Buf norms;
     norms.reserve(sizeof(float) * std::max<int64_t>(n, 1));
@@ -2914,6 +3020,7 @@ int32_t mivs_kmeans_predict(int32_t device, void* stream, const float* d_data, i
     if (n == 0) return;
     DeviceGuard dg(device);
     hipStream_t s = static_cast<hipStream_t>(stream);
+    StreamScope ss(s);
     Workspace ws;
     ListSet cents;
     make_single_list(cents, d_centroids, n_clusters, dim, dim_pad(dim), 0, kDefaultChunkGroups, s);

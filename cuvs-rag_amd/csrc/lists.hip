@@ -72,7 +72,9 @@ __global__ __launch_bounds__(256) void k_pack(const float* __restrict__ src, int
       __builtin_nontemporal_store(__builtin_bit_cast(f32x4, v[rb]), reinterpret_cast<f32x4*>(gb + (int64_t)blk * kRowBlkStride + 4 * rb * kRowBlk));
       *reinterpret_cast<float4*>(sb + (4 * rb + i4) * LDSR + 4 * c) = v[rb];
     }
-    // (one wave's LDS operations complete in order: its reads below see its stores above)
+    // the reads below take other lanes' stores above (and the next block's stores must not pass this block's reads):
+    // order them explicitly at wave scope rather than relying on in-order LDS within a wave
+    wave_lds_sync();
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       const float4 u = *reinterpret_cast<const float4*>(sb + rr * LDSR + 8 * t + 4 * h);
@@ -85,6 +87,7 @@ __global__ __launch_bounds__(256) void k_pack(const float* __restrict__ src, int
     }
 #pragma unroll
     for (int rb = 0; rb < 8; ++rb) v[rb] = nv[rb];
+    wave_lds_sync();
   }
   if (h == 0) {
     const int64_t r = r0 + rr;

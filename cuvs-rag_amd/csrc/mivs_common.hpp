@@ -434,6 +434,15 @@ size_t rs_scan_lds_bytes(int dp);
 bool rs_scan_supported(int dp);
 hipError_t launch_rs_scan(const RsScanArgs& a, int dp, int grid, hipStream_t s);
 int64_t rs_tiles_bytes(int64_t ne, int n_lists, int dp);
+// order one wave's LDS stores before its later LDS loads (and the loads before later stores) across its lanes: a
+// wave-scope release/acquire pair around a wave barrier, so an LDS hand-off between lanes of one wave does not depend
+// on the compiler keeping the accesses in program order
+__device__ inline void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // block-wide exclusive scan of one value per thread (returns exclusive prefix, total via *tot)
 __device__ inline int64_t block_excl_scan(int64_t v, int64_t* sh, int64_t* tot) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;

@@ -793,6 +793,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
       if (p8 == 7 && rj < cnt) s_dot[rj] = acc;  // (part 7 ends the row's chain)
     }
   }
+  // s_dot (= s_ck[wv]) is written by lanes p8 == 7 and read below by other lanes of the same wave: order the LDS
+  // stores before the loads explicitly instead of relying on in-order LDS within a wave
+  wave_lds_sync();
   if (live && !ovf && lane < cnt) {
     const int pos = s_cp[wv][lane];
     const float acc = s_ck[wv][lane];

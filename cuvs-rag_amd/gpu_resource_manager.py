@@ -63,6 +63,17 @@ def _probe_device(gpu_id: int) -> Tuple[GPUConfig, Dict[str, int]]:
     return GPUConfig(gpu_id, props.name, total, total - allocated, True), info
 
 
+def release_engine_cache(gpu_id: int) -> int:
+    """Hand the blocks the mivs engine keeps for reuse on `gpu_id` back to the driver (bytes freed), so that the
+    reference's torch-only cleanup (empty_cache after it) and torch.cuda.mem_get_info see that memory free. A process
+    that never loaded the engine holds nothing."""
+    try:
+        from mivs import _native
+    except ImportError:
+        return 0
+    return _native.release_cached_memory(gpu_id)
+
+
 class GPUResourceManager:
     """Owns the list of usable devices and the row-range split of a corpus over them."""
 
@@ -161,6 +172,7 @@ class GPUResourceManager:
             if not self.validate_gpu_index(gpu_id):
                 continue
             try:
+                release_engine_cache(gpu_id)
                 with torch.cuda.device(gpu_id):
                     torch.cuda.empty_cache()
                     torch.cuda.synchronize()

@@ -36,6 +36,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from gpu_resource_manager import release_engine_cache  # noqa: E402
 from mivs import config as mivs_config  # noqa: E402
 
 logger = logging.getLogger(__name__)
@@ -96,6 +97,7 @@ class CUDAMemoryManager:
             yield
         except (torch.cuda.OutOfMemoryError, MemoryError) as e:
             logger.error("[GPU %d] OOM during %s: %s", gpu_config.device_id, operation, e)
+            release_engine_cache(gpu_config.device_id)  # (the engine's cached blocks first: torch cannot see them)
             torch.cuda.empty_cache()
             gc.collect()
             raise

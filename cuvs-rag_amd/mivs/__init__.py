@@ -6,6 +6,7 @@ runs in the in-tree ``libmivs.so`` through the C-ABI of include/mivs.h.
 """
 from . import _native, config  # noqa: F401
 from ._native import MAX_K, MivsError, MivsOutOfMemoryError, NativeLibraryMissing, available, load  # noqa: F401
+from ._native import cached_memory, release_cached_memory, set_block_cache_limit  # noqa: F401
 
 __version__ = "0.1.0"
 

@@ -176,6 +176,10 @@ _SIGS = {
     "mivs_index_set_prefilter": (c_int32, [c_void_p, c_void_p, c_int32]),
     "mivs_index_get_prefilter": (c_int32, [c_void_p, POINTER(c_int32)]),
     "mivs_index_free": (None, [c_void_p]),
+    "mivs_set_block_cache_limit": (c_int32, [c_int32, c_int64]),
+    "mivs_release_cached_memory": (c_int32, [c_int32, POINTER(c_int64)]),
+    "mivs_cached_memory": (c_int32, [c_int32, POINTER(c_int64), POINTER(c_int64)]),
+    "mivs_reload_settings": (None, []),
     "mivs_kmeans_fit": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32, c_int32,
                                   c_void_p]),
     "mivs_kmeans_predict": (c_int32, [c_int32, c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_int32, c_int32,
@@ -290,3 +294,32 @@ def build_phases(handle, kind: int) -> dict:
     check(lib().mivs_index_build_phases(handle, buf, 16, ctypes.byref(n)))
     names = BUILD_PHASES.get(kind, ())
     return {(names[i] if i < len(names) else f"phase{i}"): round(buf[i], 4) for i in range(min(n.value, 16))}
+
+
+def set_block_cache_limit(bytes_: int, device: int = -1) -> None:
+    """Let the engine keep up to `bytes_` of released large device blocks per device for reuse (0: off, the default;
+    device -1: every device). Lowering it frees the blocks above the new limit."""
+    check(lib().mivs_set_block_cache_limit(int(device), int(bytes_)))
+
+
+def release_cached_memory(device: int = -1) -> int:
+    """Return every block the engine's block cache holds on `device` (-1: all devices) to the driver; bytes freed.
+    Called by the drop-ins' cleanup and OOM paths before torch.cuda.empty_cache()."""
+    if _lib is None:  # nothing loaded: nothing cached
+        return 0
+    freed = c_int64(0)
+    check(_lib.mivs_release_cached_memory(int(device), ctypes.byref(freed)))
+    return int(freed.value)
+
+
+def cached_memory(device: int = -1) -> dict:
+    """{"bytes": cached, "limit": per-device limit (-1 for device -1)}"""
+    b, lim = c_int64(0), c_int64(0)
+    check(lib().mivs_cached_memory(int(device), ctypes.byref(b), ctypes.byref(lim)))
+    return {"bytes": int(b.value), "limit": int(lim.value)}
+
+
+def reload_settings() -> None:
+    """Re-read the engine settings the library caches from the environment (MIVS_FALLBACK_SYNC)."""
+    if _lib is not None:
+        _lib.mivs_reload_settings()

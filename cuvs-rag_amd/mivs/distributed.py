@@ -60,3 +60,58 @@ def allreduce_max(value: float, device: torch.device | None = None, group=None) 
     t = torch.tensor([float(value)], dtype=torch.float64, device=device or "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())
+
+
+def per_rank_values(value: float, device: torch.device | str | None = None, group=None) -> list:
+    """[value of rank 0, rank 1, ...]: a host scalar gathered from every rank (diagnostics of the N > 1 line)."""
+    if not dist.is_available() or not dist.is_initialized():
+        return [float(value)]
+    world = dist.get_world_size(group)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device or "cpu")
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t, group=group)
+    return [float(v.item()) for v in out]
+
+
+def timed_sharded_step(search_fn: Callable, k: int, metric: str = "sqeuclidean", group=None,
+                       merge_fn: Optional[Callable] = None):
+    """One sharded step -- this rank's search, the all-gather of the per-shard top-k, the merge -- with each part
+    timed: hipEvents on the current stream when the results are on a GPU (the all-gather's RCCL work is ordered
+    before the event that follows it), the host clock otherwise. -> ((dist, ids), {"search_ms", "allgather_ms",
+    "merge_ms"}). The merge is K7 over the rank-major receive buffer (``merge_fn(gd, gi, k, metric)`` replaces it,
+    taking the same [world, Q, k] buffers)."""
+    import time
+
+    marks = []
+
+    def mark(on_gpu):
+        if on_gpu:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            marks.append(e)
+        else:
+            marks.append(time.perf_counter())
+
+    gpu = torch.cuda.is_available() and torch.cuda.is_initialized()
+    mark(gpu)
+    d, i = search_fn()
+    gpu = d.is_cuda
+    if gpu and not isinstance(marks[0], torch.cuda.Event):  # (the search initialised the GPU: restart the clock)
+        marks[0] = torch.cuda.Event(enable_timing=True)
+        marks[0].record()
+    mark(gpu)
+    gd, gi = all_gather_raw(d, i, group)
+    mark(gpu)
+    if merge_fn is None:
+        from .ops import merge_topk_gathered
+
+        out = merge_topk_gathered(gd, gi, k, metric)
+    else:
+        out = merge_fn(gd, gi, k, metric)
+    mark(gpu)
+    if gpu:
+        marks[-1].synchronize()
+        ms = [marks[j].elapsed_time(marks[j + 1]) for j in range(3)]
+    else:
+        ms = [(marks[j + 1] - marks[j]) * 1e3 for j in range(3)]
+    return out, {"search_ms": ms[0], "allgather_ms": ms[1], "merge_ms": ms[2]}

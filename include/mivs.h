@@ -154,8 +154,10 @@ int32_t mivs_ivf_flat_extend(mivs_index_t index, void* stream, const float* d_ne
 /* ---- replaces cuvs.neighbors.ivf_flat.search(SearchParams(n_probes), index, q, k)
  *      (improved_multi_gpu_rag.py:225-227, cuvs-2gpu-main.ipynb:1801) ----
  *  d_probes (optional, may be NULL): [nq][n_probes] int32 probed list ids in probe order.
- *  Enqueued on `stream`; for k <= 16 on an index with the pre-filter copies the call returns without waiting
- *  for the device. */
+ *  Stream-ordered: the call enqueues on `stream` and may return before the device has finished,
+ *  so synchronise `stream` before reading d_distances / d_neighbors on the host. (Some shapes still wait on the host
+ *  inside the call -- k > 16, very large batches, an index without the pre-filter copies -- but callers must not
+ *  rely on either behaviour.) */
 int32_t mivs_ivf_flat_search(mivs_index_t index, void* stream, const float* d_queries, int64_t nq, int32_t k,
                              int32_t n_probes, float* d_distances, int64_t* d_neighbors, int32_t* d_probes);
 int32_t mivs_ivf_flat_get_centroids(mivs_index_t index, void* stream, float* d_out /* [n_lists][dim] */);
@@ -204,7 +206,27 @@ int32_t mivs_index_build_kernels(mivs_index_t index, mivs_build_kernel* out, int
  * the pinned fp32 order); the copy costs 2 bytes per padded dimension per row of HBM. */
 int32_t mivs_index_set_prefilter(mivs_index_t index, void* stream, int32_t enable);
 int32_t mivs_index_get_prefilter(mivs_index_t index, int32_t* enabled);
+/* Waits for the calls enqueued on the index (an event per stream they used, not the whole device), then frees its
+ * device memory: back to the driver, or into the block cache when its limit allows (mivs_set_block_cache_limit). */
 void mivs_index_free(mivs_index_t index);
+
+/* ---- device block cache ----
+ * Large engine allocations (>= 64 MB) released by an index or a call may be kept for reuse by later allocations of
+ * the process (a fresh hipMalloc of tens of GB can stall for seconds while the driver clears pages). OFF by default:
+ * the per-device limit is 0 (MIVS_BLOCK_CACHE_MB at load sets another default). Cached blocks are invisible to
+ * torch's allocator and count as used in hipMemGetInfo / torch.cuda.mem_get_info until released.
+ * Replaces no reference call: the drop-ins call mivs_release_cached_memory from the reference's cleanup and OOM
+ * paths -- cleanup_gpu_resources (Attempt_1/gpu_resource_manager.py:235-255), CUDAMemoryManager's OOM handler
+ * (Latest/cuVS-2-gpu/improved_multi_gpu_rag.py:74-97), cleanup_failed_builds / cleanup_all_indices
+ * (Attempt_1/index_building_coordinator.py:472-497,583-603) -- before torch.cuda.empty_cache(). */
+/* device -1: every device. Lowering the limit frees the blocks above it. */
+int32_t mivs_set_block_cache_limit(int32_t device, int64_t bytes);
+/* free every cached block of `device` (-1: of every device); *freed_bytes (may be NULL) = bytes returned */
+int32_t mivs_release_cached_memory(int32_t device, int64_t* freed_bytes);
+/* bytes cached on `device` (-1: all devices) and its limit (-1 for device -1); either pointer may be NULL */
+int32_t mivs_cached_memory(int32_t device, int64_t* bytes, int64_t* limit);
+/* re-read the engine settings the library caches from the environment (MIVS_FALLBACK_SYNC) */
+void mivs_reload_settings(void);
 
 /* ---- IVF-PQ: replaces ivf_pq.build (index_building_coordinator.py:404, improved_multi_gpu_rag.py:137)
  * and ivf_pq.search (improved_multi_gpu_rag.py:228-230). L2, pq_bits 8, k <= 64. Codes live on the

@@ -110,6 +110,10 @@ void orc_fast_knn(const float* x, int64_t n, const float* q, int64_t nq, int d, 
 void orc_fast_ivf_search(const float* list_rows, const int64_t* list_ids, const int64_t* offsets,
                          const float* centroids, int n_lists, int d, const float* q, int64_t nq,
                          int n_probes, int k, float* out_d, int64_t* out_i);
+/* dst <- src, first-touched in 2 MiB chunks by every OpenMP thread (NUMA spread of a host copy) */
+void orc_parallel_copy(void* dst, const void* src, int64_t nbytes);
+/* the ISA the workers run with on this host: "avx512", "avx2+fma" or "x86-64" */
+const char* orc_fast_isa(void);
 
 #ifdef __cplusplus
 }

@@ -61,6 +61,8 @@ def lib():
             "orc_fast_set_threads": (None, [i32]),
             "orc_fast_knn": (None, [P, i64, P, i64, i32, i32, P, P]),
             "orc_fast_ivf_search": (None, [P, P, P, P, i32, i32, P, i64, i32, i32, P, P]),
+            "orc_parallel_copy": (None, [P, P, i64]),
+            "orc_fast_isa": (ctypes.c_char_p, []),
         }
         for name, (res, args) in sig.items():
             fn = getattr(_lib, name)
@@ -290,6 +292,17 @@ def fast_threads() -> int:
 
 def fast_set_threads(t: int) -> None:
     lib().orc_fast_set_threads(int(t))
+
+
+def fast_isa() -> str:
+    """the ISA the baseline's workers run with on this host (target_clones dispatch)"""
+    return lib().orc_fast_isa().decode()
+
+
+def parallel_copy(dst: np.ndarray, src: np.ndarray) -> None:
+    """dst[...] = src, first-touched by every OpenMP thread (NUMA spread); both C-contiguous, same nbytes"""
+    assert dst.flags.c_contiguous and src.flags.c_contiguous and dst.nbytes == src.nbytes
+    lib().orc_parallel_copy(_p(dst), _p(src), dst.nbytes)
 
 
 def fast_knn(x, q, k):

@@ -16,6 +16,24 @@ import oracle as O
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _fresh_settings():
+    """the library caches MIVS_FALLBACK_SYNC (read once): re-read it at the start of every test, after the previous
+    test's monkeypatch has restored the environment"""
+    from mivs import _native
+
+    _native.load()
+    _native.reload_settings()
+    yield
+
+
+def _setenv(monkeypatch, k, v):
+    from mivs import _native
+
+    monkeypatch.setenv(k, v)
+    _native.reload_settings()
+
+
 def _bits(a):
     return np.ascontiguousarray(a, dtype=np.float32).view(np.int32)
 
@@ -76,7 +94,7 @@ def test_ivf_search_switch_same_bits(ivf, flat_data, monkeypatch, env):
     _, q = flat_data
     d0, i0 = _search(idx, q)
     for kk, v in env.items():
-        monkeypatch.setenv(kk, v)
+        _setenv(monkeypatch, kk, v)
     d1, i1 = _search(idx, q)
     np.testing.assert_array_equal(i1, i0)
     np.testing.assert_array_equal(_bits(d1), _bits(d0))
@@ -107,10 +125,10 @@ def test_device_fallback_stats_and_bits(ivf, flat_data, monkeypatch, env):
     idx, _ = ivf
     _, q = flat_data
     for kk, v in env.items():
-        monkeypatch.setenv(kk, v)
+        _setenv(monkeypatch, kk, v)
     d0, i0 = _search(idx, q)
     st0 = idx.last_search_stats()
-    monkeypatch.setenv("MIVS_FALLBACK_SYNC", "1")
+    _setenv(monkeypatch, "MIVS_FALLBACK_SYNC", "1")
     d1, i1 = _search(idx, q)
     st1 = idx.last_search_stats()
     np.testing.assert_array_equal(i0, i1)
@@ -140,7 +158,7 @@ def test_exact_scan_switch_same_bits(ivf, flat_data, monkeypatch, k, env):
     try:
         d0, i0 = _search(idx, q, k=k)
         for kk, v in env.items():
-            monkeypatch.setenv(kk, v)
+            _setenv(monkeypatch, kk, v)
         d1, i1 = _search(idx, q, k=k)
     finally:
         idx.set_prefilter(True)
@@ -159,7 +177,7 @@ def test_build_assign_switches_same_index(flat_data, mivs_lib, monkeypatch):
     ref = ivf_flat.build(p, xt)
     for env in ({"MIVS_PF_ASSIGN_RS": "0"}, {"MIVS_PF_ASSIGN": "0"}):
         for kk, v in env.items():
-            monkeypatch.setenv(kk, v)
+            _setenv(monkeypatch, kk, v)
         other = ivf_flat.build(p, xt)
         for kk in env:
             monkeypatch.delenv(kk)
@@ -228,7 +246,7 @@ def test_ivf_pq_switch_same_bits(mivs_lib, monkeypatch, k, env):
     if k > 16:
         monkeypatch.setenv("MIVS_PQ_DUMP_K", "64")  # K9s: the register lists, where the switches apply
     for kk, v in env.items():
-        monkeypatch.setenv(kk, v)
+        _setenv(monkeypatch, kk, v)
     d1, i1 = ivf_pq.search(sp, idx, qt, k)
     np.testing.assert_array_equal(i1.cpu().numpy(), i0.cpu().numpy())
     np.testing.assert_array_equal(_bits(d1.cpu().numpy()), _bits(d0.cpu().numpy()))

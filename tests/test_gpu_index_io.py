@@ -121,13 +121,15 @@ def test_extend_with_explicit_ids(mivs_lib):
 
 
 def test_rebuild_reuses_cached_blocks_same_index(mivs_lib):
-    """Buf's block cache (capi_util.hpp): an index built after another was closed gets the closed one's device
+    """Buf's block cache (capi_util.hpp; opt-in, enabled here): an index built after another was closed gets the closed one's device
     blocks back (the sizes match) and must come out identical -- lists, rows, footprint and search bits -- as must
     a third build while the second is alive (fresh allocations)."""
+    from mivs import _native
     from mivs.neighbors import ivf_flat
 
     x, q = _data(120000, 768, 5), _data(64, 768, 6)  # (rows 370 MB: above the cache's 64 MB block floor)
     p = ivf_flat.IndexParams(n_lists=64, kmeans_n_iters=3)
+    _native.set_block_cache_limit(8 << 30, 0)  # (the cache is opt-in)
     a = ivf_flat.build(p, _gpu(x))
     da, ia = ivf_flat.search(ivf_flat.SearchParams(n_probes=8), a, _gpu(q), 10)
     ref = (a.list_sizes.numpy().copy(), a.list_ids().cpu().numpy(), a.memory())
@@ -143,3 +145,6 @@ def test_rebuild_reuses_cached_blocks_same_index(mivs_lib):
         assert idx.memory() == ref[2]
     b.close()
     c.close()
+    assert _native.cached_memory(0)["bytes"] > 0
+    _native.set_block_cache_limit(0, 0)  # (lowering the limit frees what it held)
+    assert _native.cached_memory(0)["bytes"] == 0

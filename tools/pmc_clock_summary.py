@@ -4,7 +4,9 @@ the effective clock (GRBM_GUI_ACTIVE / 8 XCDs / launch time, MI355X_MICROARCH.md
 MFMA pipe's busy fraction (SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 * SIMDs)) and the wave-cycle
 split (WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY = WAVE_CYCLES, all in quad-cycles).
 
-Usage: pmc_clock_summary.py PASS_DIR OUT_JSON [kernel-substring]
+Usage: pmc_clock_summary.py PASS_DIR OUT_JSON [kernel-substring] [config_key]
+With a config_key (bench.py's cfg_key of the profiled run) the summary also carries it and clock_mhz_held at the top
+level: bench.py's roofline reads them (load_clock) for clock_mhz_held / frac_at_held_clock.
 """
 import csv
 import json
@@ -33,6 +35,8 @@ def main():
     d, out = sys.argv[1], sys.argv[2]
     kernel = sys.argv[3] if len(sys.argv) > 3 else "k_rs_scan"
     res = {"kernel": kernel, "passes": {}}
+    if len(sys.argv) > 4:
+        res["config_key"] = sys.argv[4]
     for name in sorted(os.listdir(d)):
         p = os.path.join(d, name, "pmc_counter_collection.csv")
         if not os.path.exists(p):
@@ -63,6 +67,9 @@ def main():
                 if c in mean:
                     pas[c + "_per_mfma"] = mean[c] / mean["SQ_INSTS_MFMA"]
         res["passes"][name] = pas
+        if "effective_clock_ghz" in pas and "clock_mhz_held" not in res:
+            res["clock_mhz_held"] = pas["effective_clock_ghz"] * 1e3
+            res["clock_source"] = f"pass {name}: GRBM_GUI_ACTIVE / 8 XCDs / mean launch time under PMC"
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))
