@@ -1013,6 +1013,8 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
     };
     load_word(0, cw);
     const bool skip_scan = a.flags & 2;
+    const int np4 = (nqt + 3) >> 2;  // fp32 LUT: 16-B pieces (4 queries each) of a code row the tile uses
+    const bool nh2 = nqt > 8;        // fp16 LUT: the second piece (queries 8..15) is used
     // row iterations of this wave inside the chunk (wave-uniform)
     const int nvi = nr > wave * 64 ? (nr - wave * 64 + NT - 1) / NT : 0;
     // subspaces in pairs, one barrier per pair: at pair (j, j + 1) the next pair's codebook rows are requested, the
@@ -1031,6 +1033,8 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
           }
         }
         const float* lut = s_lut + (j & 3) * (kPqCodes * LS);
+        // only the 16-B pieces of a code row that hold the tile's queries are read (np4 / nh2 are item-uniform: the
+        // branches are scalar): a tile of 12 queries reads 3 of 4 fp32 pieces, of <= 8 one of two fp16 pieces
         if constexpr (H16) {  // RH rows' halves in flight (2: 7.97 ms, 4: 7.84 ms at configs[4])
           constexpr int RH = 4;
 #pragma unroll
@@ -1041,16 +1045,19 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
               for (int r = 0; r < RH; ++r) {
                 const pq_u32x4* p = reinterpret_cast<const pq_u32x4*>(lut + ((cw[i0 + r] >> (8 * b)) & 0xFF) * LS);
                 v[r][0] = p[0];
-                v[r][1] = p[1];
+                v[r][1] = pq_u32x4{0u, 0u, 0u, 0u};
+                if (nh2) v[r][1] = p[1];
               }
               __builtin_amdgcn_sched_group_barrier(0x100, 2 * RH, 0);  // the LDS reads issue first
 #pragma unroll
               for (int r = 0; r < RH; ++r) {
                 if (r == 0 || i0 + r < nvi) {
 #pragma unroll
-                  for (int t = 0; t < 8; ++t) {
-                    acc[i0 + r][t] = rt_add_f16(acc[i0 + r][t], v[r][0][t >> 1], t & 1);
-                    acc[i0 + r][8 + t] = rt_add_f16(acc[i0 + r][8 + t], v[r][1][t >> 1], t & 1);
+                  for (int t = 0; t < 8; ++t) acc[i0 + r][t] = rt_add_f16(acc[i0 + r][t], v[r][0][t >> 1], t & 1);
+                  if (nh2) {
+#pragma unroll
+                    for (int t = 0; t < 8; ++t)
+                      acc[i0 + r][8 + t] = rt_add_f16(acc[i0 + r][8 + t], v[r][1][t >> 1], t & 1);
                   }
                 }
               }
@@ -1061,12 +1068,16 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
 #pragma unroll
           for (int i = 0; i < RPT; ++i) {
             if (i < nvi && !skip_scan) {
-              const float4* p = reinterpret_cast<const float4*>(lut + ((cw[i] >> (8 * b)) & 0xFF) * LS);
-              const float4 v0 = p[0], v1 = p[1], v2 = p[2], v3 = p[3];
-              acc[i][0] += v0.x; acc[i][1] += v0.y; acc[i][2] += v0.z; acc[i][3] += v0.w;
-              acc[i][4] += v1.x; acc[i][5] += v1.y; acc[i][6] += v1.z; acc[i][7] += v1.w;
-              acc[i][8] += v2.x; acc[i][9] += v2.y; acc[i][10] += v2.z; acc[i][11] += v2.w;
-              acc[i][12] += v3.x; acc[i][13] += v3.y; acc[i][14] += v3.z; acc[i][15] += v3.w;
+              const f32x4* p = reinterpret_cast<const f32x4*>(lut + ((cw[i] >> (8 * b)) & 0xFF) * LS);
+              f32x4 v[4] = {p[0], {0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+              if (np4 > 1) v[1] = p[1];  // (one ds_read_b128 each, under a scalar branch)
+              if (np4 > 2) v[2] = p[2];
+              if (np4 > 3) v[3] = p[3];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                acc[i][4 * u] += v[u][0]; acc[i][4 * u + 1] += v[u][1];
+                acc[i][4 * u + 2] += v[u][2]; acc[i][4 * u + 3] += v[u][3];
+              }
             }
             __builtin_amdgcn_sched_barrier(0);  // one row's 16 LUT floats in flight: bounds the VGPRs
           }

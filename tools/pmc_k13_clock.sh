@@ -5,7 +5,7 @@
 set -u
 OUT=gpurun_out/${1:-pmc13c}
 KRE=${KRE:-k_rs_scan}
-BENCH_ARGS=${BENCH_ARGS:-"--steps 3 --warmup 1 --no-cpu-baseline --gt-queries 16 --sweep '' --flat-rows 0 --pq-rows 0 --large-k '' --single-process 0"}
+BENCH_ARGS=${BENCH_ARGS:-"--steps 3 --warmup 1 --no-cpu-baseline --gt-queries 16 --sweep '' --flat-rows 0 --pq-rows 0 --large-k '' --single-process 0 --batch-sweep '' --latency ''"}
 mkdir -p $OUT
 export TMPDIR=/tmp
 run_pmc() {  # name, counters...
