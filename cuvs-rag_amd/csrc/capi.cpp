@@ -1068,7 +1068,23 @@ bool device_fallback_ok(const mivs_index_s* idx, int k, int64_t nq, int np) {
          idx->lists.n_lists <= probe_map_dev_max_lists();
 }
 
-void reload_settings() { g_fallback_sync.store(-1, std::memory_order_relaxed); }
+// K9r's candidate-superset slots for 64 < k <= kRtCandMax (MIVS_PQ_CANDS=0: the DUMP path, A/B runs); read once
+// like MIVS_FALLBACK_SYNC
+std::atomic<int> g_pq_cands{-1};
+
+bool pq_cand_slots() {
+  int v = g_pq_cands.load(std::memory_order_relaxed);
+  if (v < 0) {
+    v = env_int("MIVS_PQ_CANDS", 1) != 0 ? 1 : 0;
+    g_pq_cands.store(v, std::memory_order_relaxed);
+  }
+  return v == 1;
+}
+
+void reload_settings() {
+  g_fallback_sync.store(-1, std::memory_order_relaxed);
+  g_pq_cands.store(-1, std::memory_order_relaxed);
+}
 
 void exact_fallback_on_device(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np,
                               float* out_d, int64_t* out_i) {
@@ -1822,7 +1838,10 @@ void pq_search_rt(mivs_index_s* idx, hipStream_t s, const float* d_q, int64_t nq
                   int64_t* d_ids, ProfRec* pr, bool lut16 = false) {
   Workspace& ws = idx->ws;
   const ListSet& L = idx->lists;
-  const bool dump = k > kMaxK;
+  // K8 over per-slot candidate supersets of kRtSlotCap entries (64 < k <= kRtCandMax), or over every row's key
+  const bool cands = k > kMaxK && k <= kRtCandMax && pq_cand_slots();
+  const bool dump = k > kMaxK && !cands;
+  const int per_slot = dump ? kRtRows : (cands ? kRtSlotCap : k);
   int64_t max_chunks = 0;  // slots per query at most: the np longest lists' chunk counts
   {
     std::vector<int64_t> c(L.n_lists);
@@ -1831,7 +1850,9 @@ void pq_search_rt(mivs_index_s* idx, hipStream_t s, const float* d_q, int64_t nq
     for (int l = 0; l < std::min<int>(np, L.n_lists); ++l) max_chunks += c[l];
   }
   max_chunks = std::max<int64_t>(max_chunks, 1);
-  const int64_t qb = dump ? select_batch(nq, (size_t)max_chunks * ((size_t)kRtRows * 4 + 16)) : nq;
+  const int64_t qb = dump    ? select_batch(nq, (size_t)max_chunks * ((size_t)kRtRows * 4 + 16))
+                     : cands ? select_batch(nq, (size_t)max_chunks * kRtSlotCap * 12)
+                             : nq;
   const int flags = env_int("MIVS_PQ_FLAGS", 0);
   if (pr) HIPCHK(hipEventRecord(pr->e[1], s));
   for (int64_t b0 = 0; b0 < nq; b0 += qb) {
@@ -1853,8 +1874,8 @@ void pq_search_rt(mivs_index_s* idx, hipStream_t s, const float* d_q, int64_t nq
                             ws.bucket_q.as<int64_t>(), ws.bucket_slot.as<int64_t>(), ws.qp_slots.as<int64_t>(),
                             ws.slot_begin.as<int64_t>(), ws.scan_tmp.p, stb, s));
     const int64_t slots = nb * max_chunks;
-    ws.part_d.reserve(sizeof(float) * (size_t)slots * (dump ? kRtRows : k));
-    ws.part_i.reserve(sizeof(int64_t) * (size_t)slots * (dump ? 2 : k));
+    ws.part_d.reserve(sizeof(float) * (size_t)slots * per_slot);
+    ws.part_i.reserve(sizeof(int64_t) * (size_t)slots * (dump ? 2 : per_slot));
     ws.counter.reserve(16);
     HIPCHK(hipMemsetAsync(ws.counter.p, 0, sizeof(int), s));
     PqTileArgs a{};
@@ -1888,8 +1909,21 @@ void pq_search_rt(mivs_index_s* idx, hipStream_t s, const float* d_q, int64_t nq
     a.probes_d = ws.probes_d.as<float>() + b0 * np;
     a.n_probes = np;
     a.flags = flags;
+    a.slot_cap = cands ? kRtSlotCap : 0;
     HIPCHK(launch_pq_scan_rt(a, cu_count(idx->device), s));
-    if (dump) {
+    if (cands) {  // K8 over each query's slots of candidates (EXPLICIT, slot ranges)
+      SelectArgs sa{};
+      sa.keys = ws.part_d.as<float>();
+      sa.ids = ws.part_i.as<int64_t>();
+      sa.slot_begin = ws.slot_begin.as<int64_t>();
+      sa.n_in = kRtSlotCap;
+      sa.nq = nb;
+      sa.k = k;
+      sa.metric = idx->metric;
+      sa.out_d = d_dist + b0 * k;
+      sa.out_i = d_ids + b0 * k;
+      HIPCHK(launch_select(sa, s));
+    } else if (dump) {
       SelectArgs sa{};
       sa.keys = ws.part_d.as<float>();
       sa.row_ids = L.ids.as<int64_t>();

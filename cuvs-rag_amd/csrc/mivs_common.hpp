@@ -177,6 +177,9 @@ struct PqTileArgs {
   int64_t* slot_info;       // DUMP: [slots][2] = (first row position, rows); out_d is [slots][kRtRows]
   int flags;                // timing experiments only (MIVS_PQ_FLAGS): 1 skip LUT build, 2 skip row scan
   int lut16 = 0;            // K9r: LUT entries stored as fp16 (cuvs SearchParams.lut_dtype = float16; L2 only)
+  // K9r, kMaxK < k <= kRtCandMax: each (query, chunk) slot receives a SUPERSET of its top-k by (key, id), unsorted,
+  // slot_cap entries (id -1 past its end), which K8 ranks over the query's slots (EXPLICIT with slot_begin)
+  int slot_cap = 0;
 };
 
 // K9r (k_pq_scan_rt, pq.hip): work item = (list, <= 16 queries probing it, chunk of kRtRows rows); the
@@ -187,6 +190,8 @@ constexpr int kRtQ = 16;
 constexpr int kRtRpt = 8;
 constexpr int kRtRows = kRtThreads * kRtRpt;  // 4096
 constexpr int kRtGroups = kRtRows / 32;
+constexpr int kRtCandMax = 256;  // K9r candidate-superset slots up to this k (the refine's 12 x k candidates); DUMP above
+constexpr int kRtSlotCap = 256;  // entries per candidate-superset slot (>= kRtCandMax)
 size_t pq_rt_lds_bytes(int rot_dim_pad, int pq_dim, int k, bool lut16 = false);
 // book_norms and books_mfma from the codebooks (after training; pq.hip)
 hipError_t launch_pq_book_prep(const float* books, int pq_dim, int pq_len, int ip, float* book_norms,

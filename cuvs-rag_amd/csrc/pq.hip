@@ -786,8 +786,11 @@ __global__ __launch_bounds__(512) void k_pq_scan_tiled(PqTileArgs a) {
 // the k-th smallest of the 512 per-thread minima (>= k distinct rows lie at or below it, so every row
 // of the slot's top-k does too); rows <= bound_q -> LDS (at most 8 (k - 1) below it plus ties), and a
 // wave picks k by rounds of 64-lane minima. A slot whose list overflows CQ (many tied keys) is finished
-// by block-wide rounds over the registers instead. CQ == 0 (DUMP, k > 64): every row's key ->
-// out_d[slot][kRtRows] and (first row position, rows) -> slot_info for K8.
+// by block-wide rounds over the registers instead. 64 < k <= kRtCandMax (slot_cap > 0): the slot takes the rows
+// at or below bound_q as they are (a superset of its top-k), or
+// its exact top-k when they exceed slot_cap, and K8 ranks a query's slots -- the refine's 12 x k candidates had
+// taken the DUMP path, 1.9 GB of keys written and read back per 10k queries. CQ == 0 (DUMP, k > kRtCandMax):
+// every row's key -> out_d[slot][kRtRows] and (first row position, rows) -> slot_info for K8.
 __device__ __forceinline__ uint32_t rt_ord(float f) {  // orderable bits, -0 and +0 equal
   const uint32_t u = __float_as_uint(f == 0.0f ? 0.0f : f);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -818,6 +821,8 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
   constexpr int NT = kRtThreads, TQ = kRtQ, RPT = kRtRpt, R = kRtRows, PL = 4 * PL4;
   constexpr int LS = H16 ? 12 : 20;  // code row stride in 4-B words (fp16: 24 halves = 48 B; fp32: 20 floats)
   constexpr bool DUMP = CQ == 0;
+  const int SC = a.slot_cap;         // > 0: candidate-superset slots of SC entries (k > kMaxK)
+  const int ST = SC > 0 ? SC : a.k;  // entries per output slot
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int64_t* s_q = reinterpret_cast<int64_t*>(smem);        // [TQ] query (-1: no query)
   int64_t* s_slot = s_q + TQ;                             // [TQ] output slot
@@ -1152,11 +1157,26 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
         }
       }
       __syncthreads();
-      // 4. per query (wave w: 2w, 2w + 1) k rounds of the 64-lane (key, row) minimum
+      // 4. per query (wave w: 2w, 2w + 1) k rounds of the 64-lane (key, row) minimum; candidate-superset slots
+      // (slot_cap > 0) take the n <= slot_cap rows at or below the bound as they are, unsorted (K8 ranks them)
       for (int t = wave; t < TQ; t += NT / 64) {
         const int64_t slot = s_slot[t];
         const int n = s_cnt[t];
         if (slot < 0 || n > CQ) continue;
+        if (SC > 0 && n <= SC) {
+          for (int e = lane; e < SC; e += 64) {
+            float o = a.ip ? -INFINITY : INFINITY;
+            int64_t id = -1;
+            if (e < n) {
+              const float x = s_ck[t * CQ + e];
+              o = a.ip ? -x : x;
+              id = a.row_ids[g0 * kGroupRows + r0 + s_cr[t * CQ + e]];
+            }
+            a.out_d[slot * SC + e] = o;
+            a.out_i[slot * SC + e] = id;
+          }
+          continue;
+        }
         constexpr int PER = CQ / 64;
         float ck[PER];
         int cr[PER];
@@ -1180,12 +1200,16 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
           }
           const bool valid = br != INT_MAX;
           if (lane == 0) {
-            a.out_d[slot * a.k + rk] = valid ? (a.ip ? -bk : bk) : (a.ip ? -INFINITY : INFINITY);
-            a.out_i[slot * a.k + rk] = valid ? a.row_ids[g0 * kGroupRows + r0 + br] : (int64_t)-1;
+            a.out_d[slot * ST + rk] = valid ? (a.ip ? -bk : bk) : (a.ip ? -INFINITY : INFINITY);
+            a.out_i[slot * ST + rk] = valid ? a.row_ids[g0 * kGroupRows + r0 + br] : (int64_t)-1;
           }
 #pragma unroll
           for (int u = 0; u < PER; ++u)
             if (ck[u] == bk && cr[u] == br) { ck[u] = INFINITY; cr[u] = INT_MAX; }
+        }
+        for (int e = a.k + lane; e < SC; e += 64) {  // (superset slot holding its exact top-k: the rest is empty)
+          a.out_d[slot * SC + e] = a.ip ? -INFINITY : INFINITY;
+          a.out_i[slot * SC + e] = -1;
         }
       }
       // 5. (rare) slots whose candidate list overflowed: block-wide rounds over the registers
@@ -1225,11 +1249,15 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
             if (rt_less(s_wk[u], s_wr[u], bk, br)) { bk = s_wk[u]; br = s_wr[u]; }
           const bool valid = br != INT_MAX;
           if (tid == 0) {
-            a.out_d[slot * a.k + rk] = valid ? (a.ip ? -bk : bk) : (a.ip ? -INFINITY : INFINITY);
-            a.out_i[slot * a.k + rk] = valid ? a.row_ids[g0 * kGroupRows + r0 + br] : (int64_t)-1;
+            a.out_d[slot * ST + rk] = valid ? (a.ip ? -bk : bk) : (a.ip ? -INFINITY : INFINITY);
+            a.out_i[slot * ST + rk] = valid ? a.row_ids[g0 * kGroupRows + r0 + br] : (int64_t)-1;
           }
           lk = bk;
           lr = br;
+        }
+        for (int e = a.k + tid; e < SC; e += NT) {
+          a.out_d[slot * SC + e] = a.ip ? -INFINITY : INFINITY;
+          a.out_i[slot * SC + e] = -1;
         }
       }
     }
@@ -1274,12 +1302,13 @@ hipError_t launch_pq_scan_tiled(const PqTileArgs& a, int kcap, int grid, hipStre
   }
 }
 
-static int pq_rt_cq(int k) { return k > 64 ? 0 : (k <= 16 ? 128 : 512); }
+// LDS candidate capacity per query: 0 = DUMP (k > kMaxK without candidate-superset slots, or k > kRtCandMax)
+static int pq_rt_cq(int k, bool cands) { return k > kMaxK && !(cands && k <= kRtCandMax) ? 0 : (k <= 16 ? 128 : 512); }
 
 size_t pq_rt_lds_bytes(int rot_dim_pad, int pq_dim, int k, bool lut16) {
   const size_t loop = (size_t)kRtQ * rot_dim_pad * 4 + (size_t)4 * kPqCodes * (lut16 ? 12 : 20) * 4 +
                       (size_t)pq_dim * kRtQ * 4;
-  const size_t sel = (size_t)kRtQ * kRtThreads * 4 + (size_t)kRtQ * pq_rt_cq(k) * 8;
+  const size_t sel = (size_t)kRtQ * kRtThreads * 4 + (size_t)kRtQ * pq_rt_cq(k, true) * 8;  // (the larger)
   return 512 + (loop > sel ? loop : sel);
 }
 
@@ -1305,7 +1334,7 @@ static hipError_t launch_pq_rt_k(const PqTileArgs& a, int grid, size_t lds, hipS
 
 template <int PL4>
 static hipError_t launch_pq_rt_pl(const PqTileArgs& a, int grid, size_t lds, hipStream_t s) {
-  switch (pq_rt_cq(a.k)) {
+  switch (pq_rt_cq(a.k, a.slot_cap > 0)) {
     case 0: return launch_pq_rt_k<PL4, 0>(a, grid, lds, s);
     case 128: return launch_pq_rt_k<PL4, 128>(a, grid, lds, s);
     default: return launch_pq_rt_k<PL4, 512>(a, grid, lds, s);
@@ -1340,7 +1369,11 @@ hipError_t launch_pq_book_prep(const float* books, int pq_dim, int pq_len, int i
 hipError_t launch_pq_scan_rt(const PqTileArgs& a, int grid, hipStream_t s) {
   if (!pq_rt_supported(a.rot_dim_pad, a.pq_dim, a.pq_len, a.k)) return hipErrorInvalidValue;
   if (a.books_mfma == nullptr || a.book_norms == nullptr) return hipErrorInvalidValue;
-  if (pq_rt_cq(a.k) == 0 && a.slot_info == nullptr) return hipErrorInvalidValue;
+  const int cq = pq_rt_cq(a.k, a.slot_cap > 0);
+  if (cq == 0 && a.slot_info == nullptr) return hipErrorInvalidValue;
+  // (k > kMaxK without DUMP: candidate-superset slots of slot_cap >= k entries)
+  if (cq > 0 && a.k > kMaxK && (a.slot_cap < a.k || a.slot_cap % 64 != 0)) return hipErrorInvalidValue;
+  if ((a.k <= kMaxK || cq == 0) && a.slot_cap != 0) return hipErrorInvalidValue;
   if (a.ip && (a.probes == nullptr || a.probes_d == nullptr)) return hipErrorInvalidValue;
   if (a.lut16 && a.ip) return hipErrorInvalidValue;  // (fp16 LUT: L2 only)
   const size_t lds = pq_rt_lds_bytes(a.rot_dim_pad, a.pq_dim, a.k, a.lut16 != 0);

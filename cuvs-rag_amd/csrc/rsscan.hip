@@ -389,7 +389,9 @@ __global__ __launch_bounds__(kRsThreads, 1) void k_rs_scan(RsScanArgs a) {
       // rows there (vmcnt(0): it cannot order them across the loop) would wait for this DMA too
       // (a buffer descriptor over the image: no branch per piece; with nothing to stage -- the block's
       // last tile -- its size is 0 and the loads write zeros to a buffer no tile reads again)
-      const char* simg = !last ? a.tiles + (it.slot + t + 1) * IMG : a.tiles + nx.slot * IMG;
+      // (flags & 32, timing only: every tile of an item re-reads the item's first image, so the tile DMA only ever
+      // reads L2-resident bytes -- separates the tiles' L2 / fabric latency from the rest of the ready wait)
+      const char* simg = !last ? a.tiles + (it.slot + ((a.flags & 32) ? 0 : t + 1)) * IMG : a.tiles + nx.slot * IMG;
       const bool stage = (!last || has_next) && !(a.flags & 2);
       const v4i sdesc = uniform_desc(simg, stage ? (int)IMG : 0);
       const int nxt = cur + 1 == NBUF ? 0 : cur + 1;

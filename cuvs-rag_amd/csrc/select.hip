@@ -21,7 +21,8 @@
 //
 // Candidate sources: DUMP slots (keys [slot][slot_rows], slot_info = (first row
 // position, rows) per slot, ids = row_ids[position]) or an EXPLICIT [nq][n_in]
-// (dist, id) array (cross-shard merge of large k; id < 0 = missing).
+// (dist, id) array (cross-shard merge of large k; id < 0 = missing), or EXPLICIT
+// slots of n_in entries with slot_begin (K9r's per-chunk candidate supersets).
 // Replaces the large-k select_k inside cuVS ivf_flat::search / brute_force (reference
 // top_k = 2000, improved_multi_gpu_rag.py:65,247; 2*k per shard cuvs-2gpu-main.ipynb:1801).
 #include <climits>
@@ -199,7 +200,10 @@ __global__ __launch_bounds__(kSelThreads) void k_select(SelectArgs a) {
   const int64_t q = blockIdx.x;
   const int tid = threadIdx.x;
   int64_t base, ncand, nslots = 0;
-  if (EXPLICIT) {
+  if (EXPLICIT && a.slot_begin) {  // slots of n_in (dist, id) entries each, query q's in [slot_begin[q], [q + 1]) (K9r)
+    base = a.slot_begin[q] * a.n_in;
+    ncand = (a.slot_begin[q + 1] - a.slot_begin[q]) * a.n_in;
+  } else if (EXPLICIT) {
     base = q * a.n_in;
     ncand = a.n_in;
   } else {

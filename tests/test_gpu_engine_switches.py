@@ -253,6 +253,26 @@ def test_ivf_pq_switch_same_bits(mivs_lib, monkeypatch, k, env):
     idx.close()
 
 
+@pytest.mark.parametrize("k,metric", [(120, "sqeuclidean"), (256, "sqeuclidean"), (100, "inner_product")])
+def test_ivf_pq_candidate_slots_same_bits_as_dump(mivs_lib, monkeypatch, k, metric):
+    """64 < k <= 256: K9r's per-chunk candidate supersets + K8 over a query's slots (default) give the bits of
+    the DUMP path (every row's key + K8, MIVS_PQ_CANDS=0), with ragged lists and chunks past 4096 rows"""
+    from mivs.neighbors import ivf_pq
+
+    x = _data(30_000, 64, 5)
+    q = _data(41, 64, 6)
+    idx = ivf_pq.build(ivf_pq.IndexParams(n_lists=6, pq_dim=16, kmeans_n_iters=3, metric=metric),
+                       torch.from_numpy(x).cuda())
+    sp = ivf_pq.SearchParams(n_probes=3)
+    qt = torch.from_numpy(q).cuda()
+    d0, i0 = ivf_pq.search(sp, idx, qt, k)
+    _setenv(monkeypatch, "MIVS_PQ_CANDS", "0")
+    d1, i1 = ivf_pq.search(sp, idx, qt, k)
+    np.testing.assert_array_equal(i1.cpu().numpy(), i0.cpu().numpy())
+    np.testing.assert_array_equal(_bits(d1.cpu().numpy()), _bits(d0.cpu().numpy()))
+    idx.close()
+
+
 @pytest.mark.parametrize("n_probes", [16, 17, 32, 48])
 def test_coarse_probe_equals_oracle(ivf, flat_data, n_probes):
     """the coarse probe -- K3's register top-k up to 16 probes, K3w DUMP + K8s above (slot-uniform key loads, the

@@ -401,8 +401,10 @@ PQ_CASES = [
     (9000, 32, 2, 8, 3, 15, 2, 10),       # lists > 4096 rows (K9s row blocks), one LUT half only
     (8000, 768, 16, 96, 2, 21, 6, 64),    # k = 64: the candidate pool of IVF-PQ + refine
     (7000, 64, 16, 16, 3, 19, 5, 40),
-    (6000, 64, 16, 16, 4, 40, 8, 200),    # k > 64: K9 DUMP + K8 select (IVF-PQ + refine pools)
-    (12000, 768, 32, 96, 2, 20, 6, 300),
+    (6000, 64, 16, 16, 4, 40, 8, 200),    # 64 < k <= 256: K9r candidate-superset slots + K8 (IVF-PQ + refine pools)
+    (12000, 768, 32, 96, 2, 20, 6, 120),  # the bench's refine pool (12 x k = 120) at the reference's pq_dim
+    (9000, 32, 2, 8, 3, 15, 2, 100),      # lists > 4096 rows: two chunks, two candidate slots per probe
+    (12000, 768, 32, 96, 2, 20, 6, 300),  # k > 256: K9r DUMP + K8
 ]
 
 

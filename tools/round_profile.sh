@@ -9,7 +9,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 MAIN="--steps 20 --warmup 3 --no-cpu-baseline --flat-rows 0 --pq-rows 0 --large-k '' --single-process 0 --sweep '' --batch-sweep '' --latency '' --gt-queries 200"
-eval timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o main -- python3 bench.py $MAIN \
+eval timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o main -- python3 bench.py $MAIN \
   --json-out $OUT/main_bench.json > $OUT/trace.log 2>&1 || { echo "trace run failed"; tail -5 $OUT/trace.log; exit 2; }
 find $OUT/trace -name "*kernel_stats.csv" -exec cp {} $OUT/main_kernel_stats.csv \;
 head -6 $OUT/main_kernel_stats.csv
