@@ -14,6 +14,8 @@ namespace mivs {
 
 namespace {
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 template <typename T>
 __device__ __forceinline__ float rf_ld(const T* p) { return (float)p[0]; }
 
@@ -127,9 +129,48 @@ __global__ __launch_bounds__(256) void k_refine(RefineArgs a) {
 // b = 0, 1, 2, ... by handing the accumulators to the next lane of the group with a DPP move (row_shr:1; part 7 ->
 // part 0 of the next 64-dim block by row_shl:7): lane (j, h) extends them at hop h, the other lanes' values are
 // discarded. Needs d % 8 == 0 (a block is all in the row or all padding) and 16-B aligned rows.
-template <int METRIC, typename T>
+// A pass = 8 candidates (rows c0 .. c0 + 7 of the query's list). PF (fp16 rows, dp <= 768): the next pass's loads
+// are issued before this pass's chains run, two passes' raw blocks in registers (12 x 16 B each), so a wave has a row
+// set in flight while it computes -- one pass at a time left every pass waiting a full HBM round trip.
+template <typename T>
+struct RfRaw {  // one lane's 8-dim block of a row, as loaded
+  typedef uint4 type;
+};
+template <>
+struct RfRaw<float> {
+  struct type {
+    float4 a, b;
+  };
+};
+
+template <typename T>
+__device__ __forceinline__ typename RfRaw<T>::type rf_raw_ld(const T* p) {
+  typename RfRaw<T>::type r;
+  if constexpr (sizeof(T) == 4) {
+    r.a = *reinterpret_cast<const float4*>(p);
+    r.b = *reinterpret_cast<const float4*>(p + 4);
+  } else {
+    r = *reinterpret_cast<const uint4*>(p);
+  }
+  return r;
+}
+
+template <typename T>
+__device__ __forceinline__ void rf_raw_cvt(const typename RfRaw<T>::type& r, float (&v)[8]) {
+  if constexpr (sizeof(T) == 4) {
+    v[0] = r.a.x; v[1] = r.a.y; v[2] = r.a.z; v[3] = r.a.w; v[4] = r.b.x; v[5] = r.b.y; v[6] = r.b.z; v[7] = r.b.w;
+  } else {
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    const h8 h = __builtin_bit_cast(h8, r);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)h[i];
+  }
+}
+
+template <int METRIC, typename T, bool PF>
 __global__ __launch_bounds__(256) void k_refine_g(RefineArgs a) {
   constexpr int CH = 12;  // 64-dim blocks of a row in flight per pass (d = 768: the whole row)
+  typedef typename RfRaw<T>::type Raw;
   __shared__ __attribute__((aligned(16))) float s_q[4][1024];
   __shared__ float s_key[4][64];
   __shared__ int64_t s_id[4][64];
@@ -150,80 +191,85 @@ __global__ __launch_bounds__(256) void k_refine_g(RefineArgs a) {
     }
   const int k = a.k;
   const int j8 = lane >> 3, p8 = lane & 7;
-  const int nB = dp >> 6;
+  const int nB = dp >> 6;  // (PF: nB <= CH)
+  const int npass = (a.n_cand + 7) >> 3;
   float mk = INFINITY, tk = INFINITY;  // rank `lane` of the running top-k, and rank k-1
   int64_t mi = LLONG_MAX, ti = LLONG_MAX;
-  for (int c0 = 0; c0 < a.n_cand; c0 += 64) {
-    // 8 passes of 8 rows: each row's key lands in s_key[wv][row - c0] (lane p == 7 ends its chains)
-    for (int r0 = 0; r0 < 64; r0 += 8) {
-      const int c = c0 + r0 + j8;
-      const int64_t cid = c < a.n_cand ? a.cand[q * a.n_cand + c] : -1;
-      const bool ok = cid >= 0 && cid < a.n;
-      if (__ballot(ok) == 0) {  // (a pass with no row: nothing to read)
-        if (p8 == 7) { s_key[wv][r0 + j8] = INFINITY; s_id[wv][r0 + j8] = LLONG_MAX; }
-        continue;
-      }
-      const T* rowp = data + (ok ? cid : 0) * (int64_t)d + 8 * p8;
-      float dot = 0.0f, xn = 0.0f;
-      for (int B0 = 0; B0 < nB; B0 += CH) {
-        float v[CH][8];
+  // candidate row of pass p for this lane's group (-1: none)
+  auto cand_of = [&](int p) {
+    const int c = 8 * p + j8;
+    const int64_t cid = c < a.n_cand ? a.cand[q * a.n_cand + c] : -1;
+    return cid >= 0 && cid < a.n ? cid : (int64_t)-1;
+  };
+  auto load_blocks = [&](int64_t cid, int B0, Raw (&r)[CH]) {
+    const T* rowp = data + (cid >= 0 ? cid : 0) * (int64_t)d + 8 * p8;
 #pragma unroll
-        for (int u = 0; u < CH; ++u) {
-          const int dim = 64 * (B0 + u) + 8 * p8;
-          if (B0 + u < nB && dim < d) {
-            rf_ld8<T>(rowp + 64 * (B0 + u), v[u]);
-          } else {
+    for (int u = 0; u < CH; ++u) {
+      const int dim = 64 * (B0 + u) + 8 * p8;
+      if (B0 + u < nB && dim < d) r[u] = rf_raw_ld<T>(rowp + 64 * (B0 + u));
+      else r[u] = Raw{};
+    }
+  };
+  // the two chains over blocks B0 .. B0 + CH - 1 (see above), from (dot, xn)
+  auto chains = [&](const Raw (&r)[CH], int B0, float& dot, float& xn) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) v[u][i] = 0.0f;
-          }
+    for (int u = 0; u < CH; ++u) {
+      if (B0 + u >= nB) break;
+      float v[8];
+      rf_raw_cvt<T>(r[u], v);
+      const float* y = qv + 64 * (B0 + u) + 8 * p8;
+      const float4 y0 = *reinterpret_cast<const float4*>(y);
+      const float4 y1 = *reinterpret_cast<const float4*>(y + 4);
+      const float yy[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+#pragma unroll
+      for (int h = 0; h < 8; ++h) {
+        if (h > 0) {
+          dot = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, dot), 0x111, 0xF, 0xF, false));
+          xn = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, xn), 0x111, 0xF, 0xF, false));
+        } else if (B0 + u > 0) {
+          dot = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, dot), 0x107, 0xF, 0xF, false));
+          xn = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, xn), 0x107, 0xF, 0xF, false));
         }
+        // the two chains side by side in one v_pk_fma_f32 per dim ((dot, xn) += (x, x) * (y, x): each half of the
+        // pair is an fmaf, so the bits are the two separate chains')
+        f32x2 acc2 = {dot, xn};
 #pragma unroll
-        for (int u = 0; u < CH; ++u) {
-          if (B0 + u >= nB) break;
-          const float* y = qv + 64 * (B0 + u) + 8 * p8;
-          const float4 y0 = *reinterpret_cast<const float4*>(y);
-          const float4 y1 = *reinterpret_cast<const float4*>(y + 4);
-          const float yy[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
-#pragma unroll
-          for (int h = 0; h < 8; ++h) {
-            if (h > 0) {
-              dot = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, dot), 0x111, 0xF, 0xF, false));
-              xn = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, xn), 0x111, 0xF, 0xF, false));
-            } else if (B0 + u > 0) {
-              dot = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, dot), 0x107, 0xF, 0xF, false));
-              xn = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, xn), 0x107, 0xF, 0xF, false));
-            }
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-              dot = fmaf(v[u][jj], yy[jj], dot);
-              dot = fmaf(v[u][4 + jj], yy[4 + jj], dot);
-              xn = fmaf(v[u][jj], v[u][jj], xn);
-              xn = fmaf(v[u][4 + jj], v[u][4 + jj], xn);
-            }
-          }
+        for (int jj = 0; jj < 4; ++jj) {
+          const f32x2 x0 = {v[jj], v[jj]}, w0 = {yy[jj], v[jj]};
+          acc2 = __builtin_elementwise_fma(x0, w0, acc2);
+          const f32x2 x1 = {v[4 + jj], v[4 + jj]}, w1 = {yy[4 + jj], v[4 + jj]};
+          acc2 = __builtin_elementwise_fma(x1, w1, acc2);
         }
-      }
-      if (p8 == 7) {
-        float key = INFINITY;
-        int64_t id = LLONG_MAX;
-        if (ok) {
-          if (METRIC == kL2) {
-            const float t = fmaf(-2.0f, dot, xn + qn);
-            key = t > 0.0f ? t : 0.0f;
-          } else {
-            key = -dot;
-          }
-          id = a.id_map ? a.id_map[cid] : cid;
-        }
-        s_key[wv][r0 + j8] = key;
-        s_id[wv][r0 + j8] = id;
+        dot = acc2[0];
+        xn = acc2[1];
       }
     }
+  };
+  // pass p's key -> s_key[(p & 7) * 8 + j8] (lane p8 == 7 ends its group's chains); every 8 passes, or at the end, the
+  // 64 keys go through the running top-k by (key, id): K7's ballot insertion, as k_refine
+  auto finish_pass = [&](int p, int64_t cid, float dot, float xn) {
+    const int slot = (p & 7) * 8 + j8;
+    if (p8 == 7) {
+      float key = INFINITY;
+      int64_t id = LLONG_MAX;
+      if (cid >= 0) {
+        if (METRIC == kL2) {
+          const float t = fmaf(-2.0f, dot, xn + qn);
+          key = t > 0.0f ? t : 0.0f;
+        } else {
+          key = -dot;
+        }
+        id = a.id_map ? a.id_map[cid] : cid;
+      }
+      s_key[wv][slot] = key;
+      s_id[wv][slot] = id;
+    }
+    if ((p & 7) != 7 && p + 1 < npass) return;
     wave_lds_sync();
-    const float key = s_key[wv][lane];
-    const int64_t id = s_id[wv][lane];
+    const int nk_ = ((p & 7) + 1) * 8;  // keys written this round
+    const float key = lane < nk_ ? s_key[wv][lane] : INFINITY;
+    const int64_t id = lane < nk_ ? s_id[wv][lane] : LLONG_MAX;
     wave_lds_sync();  // (the next round's stores come after every lane's reads)
-    // the running top-k by (key, id): K7's ballot insertion, as k_refine
     uint64_t mask = __ballot(rf_lt(key, id, tk, ti));
     while (mask) {
       const int b = __ffsll((unsigned long long)mask) - 1;
@@ -238,6 +284,43 @@ __global__ __launch_bounds__(256) void k_refine_g(RefineArgs a) {
       ti = __shfl(mi, k - 1);
       mask &= ~(1ull << b);
       mask &= __ballot(rf_lt(key, id, tk, ti));
+    }
+  };
+  if constexpr (PF) {
+    // two named buffers, passes in pairs: A holds pass p, B pass p + 1 (loaded while A's chains run)
+    Raw ra[CH], rb[CH];
+    int64_t ca = cand_of(0), cb = -1;
+    load_blocks(ca, 0, ra);
+    for (int p = 0; p < npass; p += 2) {
+      if (p + 1 < npass) {
+        cb = cand_of(p + 1);
+        load_blocks(cb, 0, rb);
+      }
+      float dot = 0.0f, xn = 0.0f;
+      chains(ra, 0, dot, xn);
+      finish_pass(p, ca, dot, xn);
+      if (p + 1 >= npass) break;
+      if (p + 2 < npass) {
+        ca = cand_of(p + 2);
+        load_blocks(ca, 0, ra);
+      }
+      dot = 0.0f;
+      xn = 0.0f;
+      chains(rb, 0, dot, xn);
+      finish_pass(p + 1, cb, dot, xn);
+    }
+  } else {
+    for (int p = 0; p < npass; ++p) {
+      const int64_t cid = cand_of(p);
+      float dot = 0.0f, xn = 0.0f;
+      if (__ballot(cid >= 0) != 0) {  // (a pass with no row: nothing to read)
+        for (int B0 = 0; B0 < nB; B0 += CH) {
+          Raw r[CH];
+          load_blocks(cid, B0, r);
+          chains(r, B0, dot, xn);
+        }
+      }
+      finish_pass(p, cid, dot, xn);
     }
   }
   if (lane < k) {
@@ -260,12 +343,16 @@ hipError_t launch_refine(const RefineArgs& a, hipStream_t s) {
   const bool gather = !lane_per_row && (a.d & 7) == 0 && (a.dp & 63) == 0 &&
                       (reinterpret_cast<uintptr_t>(a.data) & 15) == 0;
   if (gather) {
-    if (a.half) {
-      if (a.metric == kIP) hipLaunchKernelGGL((k_refine_g<kIP, _Float16>), grid, dim3(256), 0, s, a);
-      else hipLaunchKernelGGL((k_refine_g<kL2, _Float16>), grid, dim3(256), 0, s, a);
+    const bool pf = a.dp <= 768;  // (fp16 rows: the next pass's 12 blocks fit beside the current pass's)
+    if (a.half && pf) {
+      if (a.metric == kIP) hipLaunchKernelGGL((k_refine_g<kIP, _Float16, true>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((k_refine_g<kL2, _Float16, true>), grid, dim3(256), 0, s, a);
+    } else if (a.half) {
+      if (a.metric == kIP) hipLaunchKernelGGL((k_refine_g<kIP, _Float16, false>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((k_refine_g<kL2, _Float16, false>), grid, dim3(256), 0, s, a);
     } else {
-      if (a.metric == kIP) hipLaunchKernelGGL((k_refine_g<kIP, float>), grid, dim3(256), 0, s, a);
-      else hipLaunchKernelGGL((k_refine_g<kL2, float>), grid, dim3(256), 0, s, a);
+      if (a.metric == kIP) hipLaunchKernelGGL((k_refine_g<kIP, float, false>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((k_refine_g<kL2, float, false>), grid, dim3(256), 0, s, a);
     }
     return hipGetLastError();
   }

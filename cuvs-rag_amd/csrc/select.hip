@@ -56,11 +56,11 @@ __device__ __forceinline__ Cand cand_key(const SelectArgs& a, int64_t base, int6
   Cand r;
   if (EXPLICIT) {
     const int64_t c = base + t;
-    const int64_t id = a.ids[c];
     const float dd = a.keys[c];
     const float key = METRIC == kIP ? -dd : dd;
     r.u = ord_bits(key);
-    r.valid = id >= 0 && r.u < kOrdInf;
+    // (K9r's candidate slots pad with +inf keys: the key alone decides, the 8-B ids are read only when collected)
+    r.valid = r.u < kOrdInf && (a.slot_begin != nullptr || a.ids[c] >= 0);
   } else {
     // (t < a query's slots x slot_rows < 2^31: a 32-bit division, not the 64-bit one)
     const uint32_t sq = (uint32_t)t / (uint32_t)a.slot_rows;
