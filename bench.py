@@ -549,7 +549,7 @@ def flat_side_line(a, q, k, rl):
 
 def large_k_side_line(a, idx, q, rl, scanned_rows):
     """The reference's large-k default at configs[2]: its driver asks for top_k = 2000 and each shard for
-    k * 2 (improved_multi_gpu_rag.py:40,247,416). Every k > 16 runs through the fp16 pre-filter (DESIGN.md §6e):
+    k * 2 (improved_multi_gpu_rag.py:40,247,416). Every k > 16 runs through the fp16 pre-filter (DESIGN.md §6.6):
     T_q from an exact scan of a 1/64 sample of the probed rows, K13 streams the rows under it, K16 proves each
     query's window and recomputes it in the pinned fp32 order (the exact fp32 scan, K3 DUMP + K8, answers the
     queries it cannot prove). QPS over the full 10k-query batch; the same search through the exact path
@@ -613,7 +613,7 @@ def build_roofline(kern, t_build):
     """The build's hot kernels against their peaks (device time by hipEvents during the timed build, algorithmic work
     per launch from the engine: mivs_index_build_kernels): k_as_scan (the k-means assign, per iteration, and the final
     assign of every row) in TFLOP/s against the fp16 MFMA peak -- the assign runs through the fp16 pre-filter, the
-    labels are the fp32 ones (DESIGN.md §6c) -- and the byte-moving kernels (K5's centroid update, K6's pack, the fp16
+    labels are the fp32 ones (DESIGN.md §7) -- and the byte-moving kernels (K5's centroid update, K6's pack, the fp16
     and fp8 copies) in GB/s against HBM."""
     out = {}
     for name, v in kern.items():

@@ -1,5 +1,5 @@
 // K13a — the k-means assign (nearest centroid of every train / data row) on K13's row-stationary loop
-// (DESIGN.md §6c).
+// (DESIGN.md §7).
 //
 // K12 keeps the rows' fp16 vectors as MFMA B operands and streams the centroids through LDS, one ds_read_b128
 // per MFMA: at 4 SIMDs x 1 KiB per 16-cycle MFMA that is the LDS's own 256 B/clk, so the assign runs at ~0.2-0.3
@@ -10,7 +10,7 @@
 //
 // The result is the pinned fp32 argmin: per row the lanes keep the smallest approximate key, its centroid and
 // the second smallest; a row whose second smallest is above the refine window of its smallest has exactly one
-// candidate (the true argmin's approximate key is inside that window, DESIGN.md §6b), any other row (a near
+// candidate (the true argmin's approximate key is inside that window, DESIGN.md §6.2), any other row (a near
 // tie) goes to the exact fp32 K4 scan (the caller's fallback).
 #include "mivs_common.hpp"
 #include "pf_math.hpp"

@@ -197,7 +197,7 @@ struct mivs_index_s {
   int pq_dim = 0, pq_bits = 0, pq_len = 0, pq_dim_pad = 0, rot_dim_pad = 0;
   Buf pq_codes, pq_books;
   Buf pq_book_norms, pq_books_mfma;  // derived from pq_books at build (launch_pq_book_prep)
-  // fp16 copy of the lists for the K10 pre-filter (DESIGN.md §6b); empty = exact scan only
+  // fp16 copy of the lists for the K10 pre-filter (DESIGN.md §6.2); empty = exact scan only
   Buf groups_h;
   Buf group_nmin;  // K13: the smallest row norm of every 32-row group (built with groups_h)
   Buf groups_f8;   // K13's pre-pass: the lists' fp8 copy at 2^hx8 (built with groups_h when the HBM budget allows)
@@ -469,7 +469,7 @@ void repack_single_list(ListSet& ls, const float* src, int64_t n, int d, int dp,
                             ls.groups.as<float>(), ls.norms.as<float>(), ls.ids.as<int64_t>(), nullptr, 0, s));
 }
 
-// ---- fp16 pre-filter assign (DESIGN.md §6c): k-means assign and list fill as a one-list K10 scan
+// ---- fp16 pre-filter assign (DESIGN.md §7): k-means assign and list fill as a one-list K10 scan
 // (queries = data rows, rows = centroids, k = 1) + the K11 exact refine; labels equal the fp32 K4's ----
 struct PfAssign {
   Buf qh, qscale, qres;  // fp16 copy of every data row: 2^hx x a per-row power of two (k_queries_to_half)
@@ -827,7 +827,7 @@ void check_common(int device, const void* data, int64_t n, int32_t dim) {
 }
 
 
-// ---- fp16 pre-filter (K10 / K11, DESIGN.md §6b) ----
+// ---- fp16 pre-filter (K10 / K11, DESIGN.md §6.2) ----
 // The optional copies an index may build beside its fp32 rows must leave this much of the device's HBM to the
 // rest of the process (an LLM or tensors sharing the GPU in a RAG pipeline): MIVS_INDEX_HBM_FRAC (default 0.6) is
 // the largest fraction of the device's HBM the index may hold with the copy, and 4 GiB must stay free beside it.
@@ -837,7 +837,7 @@ bool pf_default_on() {
   return !(e && e[0] == '0');
 }
 
-// K13's pre-pass operand (DESIGN.md §6d-3): the lists' fp8 copy at 2^(hx - 7), built with the fp16 copy (in the
+// K13's pre-pass operand (DESIGN.md §6.3): the lists' fp8 copy at 2^(hx - 7), built with the fp16 copy (in the
 // build, counted in its time) for IVF indexes K13 serves, when the HBM budget allows; otherwise the pre-pass scans
 // the fp16 sample and last_search_stats / mivs_index_memory report the skipped copy
 void pf_build_f8(mivs_index_s* idx, hipStream_t s) {
@@ -1024,7 +1024,7 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   a.rows_nt = kth_out != nullptr;
   a.flags = env_int("MIVS_PF_FLAGS", 0);
   Buf pbuf;
-  if (a.flags & 32) {  // diagnostic: K10 phase clocks to stderr (DESIGN.md §6b)
+  if (a.flags & 32) {  // diagnostic: K10 phase clocks to stderr (DESIGN.md §6.2)
     pbuf.reserve(16 * sizeof(unsigned long long));
     HIPCHK(hipMemsetAsync(pbuf.p, 0, 16 * sizeof(unsigned long long), s));
     a.prof = pbuf.as<unsigned long long>();
@@ -1047,7 +1047,7 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
                      verify_sel);
 }
 
-// The exact fallback of K13's unproven queries sized on the device (DESIGN.md §6d-6): K11 leaves their count in
+// The exact fallback of K13's unproven queries sized on the device (DESIGN.md §6.5): K11 leaves their count in
 // ws.pf_stats[0] and their rows in ws.ovf_q; the probe map over their probes (ws.probes_i, from the search's coarse
 // probe), K3 over those (query, list) pairs, and K7 writing each query's top-k straight into its row of out_d / out_i
 // all take their size from that count on the device, so the search enqueues and returns without a host round trip.
@@ -1321,7 +1321,7 @@ int rs_wave_cap(int64_t nq, int k = 1, int64_t est_cand = 0, int n_waves = 1) {
   return (int)std::min<int64_t>(kRsWaveCapMax, std::max<int64_t>(1024, 2 * nq));
 }
 
-// K16 (DESIGN.md §6e) serves k in (kPfMaxK, kMaxSelectK] through K13 when the index has the fp16 copy
+// K16 (DESIGN.md §6.6) serves k in (kPfMaxK, kMaxSelectK] through K13 when the index has the fp16 copy
 // (MIVS_LARGE_K_PF=0: the exact K3 DUMP + K8 path, A/B runs)
 bool lk_use(const mivs_index_s* idx, int k, int np) {
   const char* e = getenv("MIVS_LARGE_K_PF");
@@ -1375,7 +1375,7 @@ int64_t lk_batch(const mivs_index_s* idx, int64_t nq, int k, int np) {
   return std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t)(budget / std::max<size_t>(per_q, 1))));
 }
 
-// K16 step 1 (DESIGN.md §6e): T_q per query into ws.pre_kth from an exact scan of the sample (K3 DUMP over the
+// K16 step 1 (DESIGN.md §6.6): T_q per query into ws.pre_kth from an exact scan of the sample (K3 DUMP over the
 // split lists 2l = the sample of list l) and the sample's r_q-th key (k_lk_sample_kth)
 void lk_prepass(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, const LkPlan& p) {
   Workspace& ws = idx->ws;
@@ -1514,7 +1514,7 @@ void lk_finish(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
   }
 }
 
-// The K13 search of queries whose probes are in ws.probes_i and norms in ws.qn (DESIGN.md §6d, §6e):
+// The K13 search of queries whose probes are in ws.probes_i and norms in ws.qn (DESIGN.md §6.3, §6.6):
 //   1. T_q: k <= 16, a pre-pass over a sample of each query's nearest list through K10 + K11 (the k-th key there);
 //      large k, an exact scan of a uniform sample of the probed rows (lk_prepass);
 //   2. per-query header {qs, uf, qn, q}: uf is the filter bound for T_q;
@@ -1826,7 +1826,7 @@ void ivf_search_probed(mivs_index_s* idx, hipStream_t s, const float* q, int64_t
   if (pr) HIPCHK(hipEventRecord(pr->e[3], s));
 }
 
-// K9r IVF-PQ search of queries whose probes are in ws.probes_i / probes_d (DESIGN.md §6a): probe map in
+// K9r IVF-PQ search of queries whose probes are in ws.probes_i / probes_d (DESIGN.md §8): probe map in
 // (list, 16-query tile, kRtRows-row chunk) items, K9r, then K7 over the (query, probe, chunk) slots'
 // top-k (k <= 64) or K8 over their dumped keys (k > 64, in query batches bounded by the dump size)
 bool pq_rt_use(const mivs_index_s* idx, int k) {
@@ -2336,7 +2336,7 @@ int32_t mivs_ivf_pq_build(int32_t device, void* stream, const float* d_data, int
     HIPCHK(launch_row_norms(d_data, n, dim, norms.as<float>(), s));
     HIPCHK(hipStreamSynchronize(s));
     {
-      PfAssign pfa;  // coarse k-means + list assign through the fp16 pre-filter (DESIGN.md §6c)
+      PfAssign pfa;  // coarse k-means + list assign through the fp16 pre-filter (DESIGN.md §7)
       pf_assign_prepare(pfa, d_data, n, dim, idx->dp, s);
       phase();
       kmeans_fit_impl(d_data, norms.as<float>(), rows.as<int64_t>(), nt, dim, idx->dp, nl, p->kmeans_n_iters,

@@ -1,4 +1,4 @@
-// K16 -- large-k IVF search through the fp16 pre-filter (k in (16, 4096]; DESIGN.md §6e).
+// K16 -- large-k IVF search through the fp16 pre-filter (k in (16, 4096]; DESIGN.md §6.6).
 //
 // The reference's driver asks for top_k = 2000 and each shard for k * 2 (Latest/cuVS-2-gpu/
 // improved_multi_gpu_rag.py:40,247). At that k the k-th key lies in the bulk of the distance distribution:

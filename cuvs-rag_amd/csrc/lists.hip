@@ -1,5 +1,5 @@
 // K6 list fill + row norms, K5 deterministic k-means update, and the synthetic
-// corpus generator. All HBM-bound streaming kernels (DESIGN.md §"Kernels").
+// corpus generator. All HBM-bound streaming kernels.
 #include "mivs_common.hpp"
 
 namespace mivs {

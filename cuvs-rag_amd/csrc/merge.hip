@@ -1,4 +1,4 @@
-// K7 — wave-level top-k merge of sorted candidate lists (DESIGN.md §"Kernels").
+// K7 — wave-level top-k merge of sorted candidate lists.
 //
 // One wave per query. The wave holds the running top-k distributed over its
 // lanes (lane r = rank r, k <= 64). Candidates stream in 64 at a time; one

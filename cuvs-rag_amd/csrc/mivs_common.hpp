@@ -1,6 +1,6 @@
 // mivs — MI355X-native IVF-Flat / brute-force k-NN. Shared device/host definitions.
 //
-// Data layout in HBM (DESIGN.md §"Data layout"):
+// Data layout in HBM:
 //   * dims are zero-padded to dp = round_up(d, 32);
 //   * rows are stored in GROUPS of 32 rows; inside a group the row-major
 //     [32][dp] block is re-ordered as [dp/8][32 rows][8 floats] so that the
@@ -200,7 +200,7 @@ bool pq_rt_supported(int rot_dim_pad, int pq_dim, int pq_len, int k);
 hipError_t launch_pq_scan_rt(const PqTileArgs& a, int grid, hipStream_t s);
 
 // ---------------------------------------------------------------------------
-// fp16 pre-filter + exact refine (prefilter.hip, DESIGN.md §6b).
+// fp16 pre-filter + exact refine (prefilter.hip, DESIGN.md §6.2).
 //   K10 scans an fp16 copy of the lists (same group layout, scaled by 2^hx_exp)
 //   against fp16 queries (per-query scale) with v_mfma_f32_32x32x16_f16 and keeps,
 //   per (query, probe, chunk) slot, the slot_k smallest APPROXIMATE keys + a
@@ -259,7 +259,7 @@ struct PfScanArgs {
   const float* qscale8;       //   qh and qscale
 };
 
-// K13 row-stationary pre-filter scan (rsscan.hip, DESIGN.md §6d): work item = (list, block of
+// K13 row-stationary pre-filter scan (rsscan.hip, DESIGN.md §6.3): work item = (list, block of
 // kRsBlockGroups groups), one group per wave held in registers, the list's queries streamed past in
 // kRsQTile-query tiles; every (approximate key <= T_q, row) goes to the query's candidate buffer.
 constexpr int kRsWaves = 8;
@@ -267,7 +267,7 @@ constexpr int kRsQTile = 32;
 constexpr int kRsBlockGroups = kRsWaves;
 // K13's pre-pass scans the first 1 / kRsPreDiv of each query's nearest list (MIVS_RS_PRE_DIV); with the fp8 copies
 // (MIVS_RS_PRE_F8, default) the sample is scored on fp8 rows and queries over every dim and the kRsPreSel best rows
-// of each query are verified with fp32 keys (DESIGN.md §6d-3)
+// of each query are verified with fp32 keys (DESIGN.md §6.3)
 constexpr int kRsPreDiv = 4;
 constexpr int kRsPreDivF8 = 4;
 constexpr int kRsPreSel = 10;
@@ -305,7 +305,7 @@ struct RsScanArgs {
   unsigned long long* prof;  // flags & 8: [grid][3] {start, end, tiles}
 };
 
-// K16 large-k search through the pre-filter (largek.hip, DESIGN.md §6e): K13's candidates -> per query the refine
+// K16 large-k search through the pre-filter (largek.hip, DESIGN.md §6.6): K13's candidates -> per query the refine
 // window (K16w) -> pinned fp32 keys of the window rows (K16r) -> (key, id) sort and the first k (K16s)
 constexpr int kCopySkippedF8 = 1;  // == MIVS_COPY_SKIPPED_F8
 constexpr int kLkMaxCap = 8192;    // window rows per query at most (more: the exact scan)
@@ -348,7 +348,7 @@ hipError_t launch_lk_chunks(const int* win_n, int64_t nq, int64_t* chunks, hipSt
 hipError_t launch_lk_recompute(const LkArgs& a, int cus, hipStream_t s);  // cus: the device's CUs
 hipError_t launch_lk_sort(const LkArgs& a, hipStream_t s);
 
-// K13a k-means assign on the row-stationary loop (assign.hip, DESIGN.md §6c)
+// K13a k-means assign on the row-stationary loop (assign.hip, DESIGN.md §7)
 struct AsScanArgs {
   const uint16_t* qh;        // data rows fp16 [n][dp], row r scaled by its own power of two (k_queries_to_half)
   const float* qscale;       // [n] 2^-(hx + row exp): the fp16 dot -> approximate fp32 dot

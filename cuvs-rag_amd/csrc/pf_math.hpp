@@ -1,6 +1,6 @@
 // Pre-filter arithmetic shared by K10/K11 (prefilter.hip) and K13 (rsscan.hip): the approximate key of
 // an fp16 MFMA dot, the rigorous bound delta of |approximate - pinned fp32 key|, the refine window and
-// the one-fma fast filter (DESIGN.md §6b).
+// the one-fma fast filter (DESIGN.md §6.2).
 #pragma once
 #include "mivs_common.hpp"
 

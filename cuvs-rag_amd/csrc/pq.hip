@@ -1,4 +1,4 @@
-// IVF-PQ kernels (DESIGN.md §"IVF-PQ"): residual extraction for codebook training, encoding
+// IVF-PQ kernels: residual extraction for codebook training, encoding
 // into the interleaved code layout, and the LUT scan with its per-(query, probe) top-k.
 //
 // Code layout in HBM: like the IVF-Flat rows, every list starts on a 32-row group; a group

@@ -1,4 +1,4 @@
-// K10 / K11 — fp16 pre-filter list scan + exact fp32 refine (DESIGN.md §6b).
+// K10 / K11 — fp16 pre-filter list scan + exact fp32 refine (DESIGN.md §6.2).
 //
 // Why: at the benchmark shape every list is probed by ~300 queries, so the exact
 // fp32 scan (K3w) is bound by the fp32 MFMA rate (157 TF). The fp16 MFMA runs 16x
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
   const float xnmax2 = a.x_norm_max * a.x_norm_max;       // >= every row's pinned norm
   const int mth = a.k > 16 ? (a.k + kPfLaneK - 1) / kPfLaneK : 2;  // lane lists theta needs (pf_theta)
   if (tid == 0) s_misc[1] = 0;                            // queues exhausted so far
-  // diagnostic phase clocks (a.prof != nullptr only under MIVS_PF_FLAGS & 32; DESIGN.md §6b)
+  // diagnostic phase clocks (a.prof != nullptr only under MIVS_PF_FLAGS & 32; DESIGN.md §6.2)
   unsigned long long pr_top = 0, pr_item = 0, pr_stage = 0, pr_loop = 0, pr_bar = 0, pr_slow = 0, pr_epi = 0;
   const unsigned long long pr_t0 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
   const unsigned long long pr_r0 = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -351,7 +351,7 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
       // Convoy: the tiles of one chunk start at different times on CUs of one XCD; a late tile joins
       // the pair the earlier ones are scanning (cpos, published after every pair) and wraps round to the
       // pairs it skipped, so the tiles read the chunk together as L2 hits instead of a second time from
-      // HBM once their lag exceeds the L2's reach. The visiting order changes no result (DESIGN.md §6b).
+      // HBM once their lag exceeds the L2's reach. The visiting order changes no result (DESIGN.md §6.2).
       const int npair = (npw + 1) >> 1;
       if (npw > 0) {
         const int rot = s_misc[2] % npair;
@@ -751,7 +751,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   // flight at once, and the row's one fmaf chain runs over the blocks in order b = 0, 1, 2, ... by handing the
   // accumulator to the next lane of the group with a DPP move (row_shr:1; part 7 -> part 0 of the next 64-dim
   // block by row_shl:7): lane (j, h) extends it at hop h, the other lanes' results are discarded. One lane per row
-  // issued 192 16-B loads per row (12 lanes active), ~8 dependent memory rounds a query.
+  // issued 192 16-B loads per row (12 lanes active), ~8 dependent memory rounds a query (profiles/DESIGN_history_r01_r05.md §6d-6).
   float P = INFINITY;
   int64_t id = LLONG_MAX;
   if (live && !ovf) {  // (wave-uniform)
@@ -1116,7 +1116,7 @@ __global__ void k_scatter_results(const float* __restrict__ in_d, const int64_t*
 }
 
 // ---------------------------------------------------------------------------------------------
-// K12 `k_pf_scan_r` — the pre-filter scan with REGISTER-resident query tiles (DESIGN.md §6b).
+// K12 `k_pf_scan_r` — the pre-filter scan with REGISTER-resident query tiles (DESIGN.md §6.2).
 //
 // K10 keeps a 64-query tile in LDS and streams rows into VGPRs, so every row read from HBM/L2 feeds
 // 64 queries and the scan needs 64 B/clk/CU at the MFMA rate. K12 swaps the roles: one workgroup of
@@ -1491,7 +1491,7 @@ __global__ __launch_bounds__(kPrThreads, 1) void k_pf_scan_r(PfScanArgs a) {
   }
 }
 
-// K11 for k = 1 (the pre-filter assign, DESIGN.md §6c): one LANE per query. The window is
+// K11 for k = 1 (the pre-filter assign, DESIGN.md §7): one LANE per query. The window is
 // min approx key + 2 delta; its candidates (1-3 at k-means shapes) get the pinned fp32 key (the same
 // chain as K11 / orc_dot, the query read from global), the smallest (key, id) is the label.
 template <int METRIC>
@@ -1630,7 +1630,7 @@ static hipError_t launch_pf_scan_md(const PfScanArgs& a, int grid, size_t lds, h
 template <int METRIC>
 static hipError_t launch_pf_scan_m(const PfScanArgs& a, int grid, size_t lds, hipStream_t s) {
   // two groups per pass with 6-deep rings (half the LDS operand traffic per flop: the kernel is power-bound,
-  // DESIGN.md §6b; one group per pass with a 16-deep ring measured slower and was retired in round 5)
+  // DESIGN.md §6.2; one group per pass with a 16-deep ring measured slower and was retired in round 5)
   if (a.groups_f8) {  // fp8 nomination (pair mode): superblocks of 32 dims, a ring of 6 or 4
     const int nsb = a.dp / 32;
     if (a.q8 == nullptr || a.qscale8 == nullptr) return hipErrorInvalidValue;

@@ -2,7 +2,7 @@
 // counting sort (list fill order / k-means member order), and the per-batch
 // probe map that turns coarse probes into (list -> query bucket) work items.
 // All HBM-bound integer work: plain coalesced loads/stores, LDS histograms, no
-// MFMA (DESIGN.md §"Kernels", K6).
+// MFMA.
 #include "mivs_common.hpp"
 
 namespace mivs {
@@ -314,7 +314,7 @@ __global__ __launch_bounds__(1024) void k_probe_map_small(const int64_t* __restr
   if (threadIdx.x == 0) slot_begin[nq] = tot;
 }
 
-// The exact fallback's probe map, sized on the device (DESIGN.md §6d-6): the unproven queries of a pre-filter search
+// The exact fallback's probe map, sized on the device (DESIGN.md §6.5): the unproven queries of a pre-filter search
 // are ovf_q[0 .. *n_dev) (K11 appends them); entry e = i * np + p is probe p of query ovf_q[i]. One workgroup, as
 // k_probe_map_small, but over a count it reads on the device: LDS count, prefix, then the fill in entry order in
 // rounds of 1024 entries, each round's slots numbered by a block scan. bucket_q = the query's own row (K3 reads the

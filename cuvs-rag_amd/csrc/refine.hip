@@ -1,5 +1,5 @@
 // K14 — exact re-ranking of candidate neighbours (cuVS cuvs.neighbors.refine, cuvs 25.06, the step
-// that turns IVF-PQ's approximate top-(r*k) into an exact top-k; DESIGN.md §6a).
+// that turns IVF-PQ's approximate top-(r*k) into an exact top-k; DESIGN.md §8).
 //
 // One wave per query: the query sits in LDS (zero-padded to dp), each lane takes one candidate row at
 // a time and forms its dot and its norm in the pinned fp32 order of the arithmetic contract (k-step s:

@@ -1,4 +1,4 @@
-// K13 — row-stationary fp16 pre-filter scan for IVF search (DESIGN.md §6d).
+// K13 — row-stationary fp16 pre-filter scan for IVF search (DESIGN.md §6.3).
 //
 // Why: K10 keeps a 64-query tile in LDS and streams every list chunk once per tile, so a row of
 // a list probed by m queries crosses the L2 -> CU path ceil(m/64) times and, unless the tiles of a
@@ -17,7 +17,7 @@
 //   * the next item's rows are loaded into the A registers during the item's last tile, each
 //     register right after its last MFMA;
 //   * no per-lane top-k: every query carries a bound T_q from a pre-pass (the exact k-th key over
-//     its nearest list, DESIGN.md §6d) with T_q >= the refine window of the final answer. The epilogue
+//     its nearest list, DESIGN.md §6.3) with T_q >= the refine window of the final answer. The epilogue
 //     tests, per lane and query half, ONE filter value bounding the lane's 8 rows from below (largest dot,
 //     smallest row norm of the group); a lane that may hold a row with approximate key <= T_q writes its 8
 //     dots as a 48-B record to the wave's stream (ballot positions, no atomics, no per-hit loop). The

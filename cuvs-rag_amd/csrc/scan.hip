@@ -1,4 +1,4 @@
-// K1/K2/K3/K4 — the fused distance + top-k list-scan kernel (DESIGN.md §"Kernels").
+// K1/K2/K3/K4 — the fused distance + top-k list-scan kernel.
 //
 // One workgroup (8 waves, 512 threads) takes a work item = (list l, one tile of
 // up to 32 queries probing l, one chunk of <= G row groups of l). The query

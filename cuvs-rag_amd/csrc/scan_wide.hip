@@ -1,4 +1,4 @@
-// K3w — the fine list scan with 64-query tiles (DESIGN.md §"Kernels").
+// K3w — the fine list scan with 64-query tiles.
 //
 // Same job, same arithmetic and same output as K3 (scan.hip), but every list
 // row streamed from HBM feeds TWO 32x32 MFMA column tiles (64 queries), which

@@ -1,4 +1,4 @@
-// K8 — large-k selection (k in (64, 4096]; also n_probes > 64) (DESIGN.md §"Kernels").
+// K8 — large-k selection (k in (64, 4096]; also n_probes > 64).
 //
 // The register top-k of the scan (K3) and of the wave merge (K7) stops at 64.
 // For larger k the scan runs in DUMP mode: every (query, chunk) slot receives

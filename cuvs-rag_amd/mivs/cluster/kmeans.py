@@ -4,7 +4,7 @@ The trainer cuVS runs inside ``ivf_flat::build`` (reached from
 index_building_coordinator.py:396) and FAISS runs in ``IndexIVFFlat.train``
 (colab_a100_test.ipynb:478). Assign = the fused MFMA distance scan with k=1
 (ties to the lower centroid id); update = deterministic fp64 member sums in a
-fixed order (DESIGN.md §"Arithmetic contract"), so results are bit-exact with
+fixed order, so results are bit-exact with
 oracle/mivs_oracle.c and reproducible run to run.
 """
 from __future__ import annotations

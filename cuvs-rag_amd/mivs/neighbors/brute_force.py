@@ -41,7 +41,7 @@ class Index:
     @property
     def prefilter(self) -> bool:
         """True when the fp16 copy of the rows is kept: k <= 16 searches then run the fp16 pre-filter
-        scan + exact fp32 refine (DESIGN.md §6b) instead of the fp32 scan; results are identical."""
+        scan + exact fp32 refine (DESIGN.md §6.2) instead of the fp32 scan; results are identical."""
         v = ctypes.c_int32()
         _native.check(_native.lib().mivs_index_get_prefilter(self.handle, ctypes.byref(v)))
         return bool(v.value)

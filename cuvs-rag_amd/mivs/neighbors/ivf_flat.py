@@ -66,7 +66,7 @@ class IndexParams:
         self.kmeans_max_train_per_list = int(kmeans_max_train_per_list)
         self.chunk_rows = int(chunk_rows)
         self.kmeans_balance = bool(kmeans_balance)
-        # fp16 copy of the lists for the exact-result fp16 pre-filter search (DESIGN.md §6b)
+        # fp16 copy of the lists for the exact-result fp16 pre-filter search (DESIGN.md §6.2)
         self.prefilter = bool(prefilter)
 
     def _c(self) -> _native.IvfFlatParams:

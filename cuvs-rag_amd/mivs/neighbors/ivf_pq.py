@@ -84,7 +84,7 @@ class SearchParams:
 
     ``lut_dtype=np.float16`` stores every LUT entry as fp16 (rounded to nearest even when the LUT is built) and
     keeps the row sums in fp32, as cuVS's half-precision LUT does; the K9r scan then reads half the LDS bytes
-    (DESIGN.md §6a). It is served for the L2 metric with pq_len a multiple of 4 in 4..16; other indexes raise
+    (DESIGN.md §8). It is served for the L2 metric with pq_len a multiple of 4 in 4..16; other indexes raise
     NotImplementedError at search. ``internal_distance_dtype`` is fp32 only."""
 
     def __init__(self, n_probes: int = 20, lut_dtype=np.float32, internal_distance_dtype=np.float32):

@@ -65,7 +65,7 @@ def synth_mixture(n: int, d: int, seed: int, n_centers: int = 4096, sigma: float
     """On-device clustered corpus: row i = C[H(seed,i) % n_centers] + sigma*N(0,I), L2-normalised.
 
     Rows are a pure function of (seed, global row index), so shard s of a sharded corpus is generated
-    on GPU s with row_begin = its start_index (DESIGN.md §"Synthetic data")."""
+    on GPU s with row_begin = its start_index."""
     dev = torch.cuda.current_device() if device is None else device
     if out is None:
         out = torch.empty((n, d), dtype=torch.float32, device=f"cuda:{dev}")

@@ -16,7 +16,7 @@
  *  - results are ordered ascending by (distance, id) for L2 and descending by
  *    inner product (ties: ascending id) for IP; missing results are
  *    id = -1, distance = +inf (L2) / -inf (IP) (FAISS convention);
- *  - arithmetic: DESIGN.md §"Arithmetic contract" (bit-exact with oracle/).
+ *  - arithmetic: DESIGN.md §3 (bit-exact with oracle/).
  */
 #ifndef MIVS_H
 #define MIVS_H
@@ -52,7 +52,7 @@ typedef struct {
   int32_t kmeans_balance;           /* 1: re-seed under-filled clusters (balanced lists, the role of cuVS's
                                        balanced k-means); 0: plain Lloyd */
   int32_t prefilter;                /* 1: also keep an fp16 copy of the lists for the exact-result fp16
-                                       pre-filter search (k <= 16; DESIGN.md §6b); 0: fp32 scan only */
+                                       pre-filter search (k <= 16; DESIGN.md §6.2); 0: fp32 scan only */
 } mivs_ivf_flat_params;
 
 /* cuvs.neighbors.ivf_pq.IndexParams (index_building_coordinator.py:398-404: n_lists, pq_bits=8,
@@ -154,7 +154,7 @@ int32_t mivs_ivf_flat_extend(mivs_index_t index, void* stream, const float* d_ne
 /* ---- replaces cuvs.neighbors.ivf_flat.search(SearchParams(n_probes), index, q, k)
  *      (improved_multi_gpu_rag.py:225-227, cuvs-2gpu-main.ipynb:1801) ----
  *  d_probes (optional, may be NULL): [nq][n_probes] int32 probed list ids in probe order.
- *  Stream-ordered: the call enqueues on `stream` and may return before the device has finished (DESIGN.md §6d-6),
+ *  Stream-ordered: the call enqueues on `stream` and may return before the device has finished (DESIGN.md §6.5),
  *  so synchronise `stream` before reading d_distances / d_neighbors on the host. (Some shapes still wait on the host
  *  inside the call -- k > 16, very large batches, an index without the pre-filter copies -- but callers must not
  *  rely on either behaviour.) */
@@ -182,7 +182,7 @@ int32_t mivs_index_profile_collect(mivs_index_t index, mivs_profile* out);
  * k-means, assign + sort, codebooks, encode}. *n_out = phases recorded (0: profiling was off). */
 int32_t mivs_index_build_phases(mivs_index_t index, double* out_s, int32_t n_max, int32_t* n_out);
 /* device time (hipEvents) and algorithmic work of an ivf_flat build's hot kernels, recorded when profiling was on
- * during the build (the build's roofline, DESIGN.md §6c): per kind its launches, summed ms and work -- flops for the
+ * during the build (the build's roofline, DESIGN.md §7): per kind its launches, summed ms and work -- flops for the
  * assign scans (2 x rows x centroids x dim per launch), bytes for the rest. Replaces no reference call: it reports on
  * ivf_flat.build (index_building_coordinator.py:392-396). out[k] for k < min(n_max, MIVS_BUILD_KERNEL_KINDS). */
 enum {

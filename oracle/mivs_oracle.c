@@ -2,7 +2,7 @@
  * mivs CPU oracle — TEST INFRASTRUCTURE ONLY (see mivs_oracle.h header).
  *
  * Bit-exact restatement of the arithmetic the HIP path performs
- * (DESIGN.md §"Arithmetic contract"). Every function cites the reference
+ * (DESIGN.md §3). Every function cites the reference
  * call site whose behaviour it restates. Build: oracle/Makefile
  * (-O2 -mfma -ffp-contract=off: every fused multiply-add below is an explicit
  * fmaf, nothing else may be contracted or reassociated).

@@ -27,7 +27,7 @@ extern "C" {
 #define ORC_IP 1
 
 int orc_dim_pad(int d);
-/* dot in the mivs k-order (MFMA 32x32x2 f32 chain, DESIGN.md §Arithmetic contract) */
+/* dot in the mivs k-order (MFMA 32x32x2 f32 chain) */
 float orc_dot(const float* a, const float* b, int d);
 void orc_norms(const float* x, int64_t n, int d, float* out);
 void orc_normalize_rows(const float* x, int64_t n, int d, float* out);

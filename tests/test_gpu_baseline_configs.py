@@ -176,7 +176,7 @@ def test_config2_ivf_10m_small_batches_equal_oracle(ivf_10m, x10m_host, nq):
 
 
 def test_config2_ivf_10m_large_k_equals_exact_all_queries_and_oracle_sample(ivf_10m, x10m_host):
-    """the reference's top_k = 2000 (improved_multi_gpu_rag.py:40,247) at configs[2]: K13 + K16 (DESIGN.md §6e) on
+    """the reference's top_k = 2000 (improved_multi_gpu_rag.py:40,247) at configs[2]: K13 + K16 (DESIGN.md §6.6) on
     all 10k queries bit-equal to the exact fp32 path (K3 DUMP + K8), and a query sample bit-equal to the oracle"""
     from mivs.neighbors import ivf_flat
 

@@ -1,4 +1,4 @@
-"""Large k through the fp16 pre-filter (K13 + K16, DESIGN.md §6e): the reference's top_k = 2000 and k * 2 per
+"""Large k through the fp16 pre-filter (K13 + K16, DESIGN.md §6.6): the reference's top_k = 2000 and k * 2 per
 shard (Latest/cuVS-2-gpu/improved_multi_gpu_rag.py:40,247).
 
 The answer must be the oracle's (orc_ivf_search) bit for bit and equal the exact fp32 path (K3 DUMP + K8,

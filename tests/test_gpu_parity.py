@@ -1,7 +1,7 @@
 """GPU parity: every kernel of the hot path vs the CPU oracle, BIT-EXACT.
 
 The oracle (oracle/mivs_oracle.c) restates the reference's cuVS/FAISS algorithm
-with the engine's pinned arithmetic order (DESIGN.md §"Arithmetic contract"),
+with the engine's pinned arithmetic order,
 so distances are compared bitwise (np.float32 views as int32) and ids exactly.
 All calls go through libmivs.so (the C-ABI); nothing here has a CPU fallback.
 """

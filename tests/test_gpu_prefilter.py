@@ -1,5 +1,5 @@
 """fp16 pre-filter scan (K10) + exact fp32 refine (K11): results BIT-EXACT with the oracle and with the
-fp32 scan, on shapes, metrics and magnitudes that stress the refine window (DESIGN.md §6b).
+fp32 scan, on shapes, metrics and magnitudes that stress the refine window (DESIGN.md §6.2).
 
 The pre-filter is on by default for ivf_flat indexes and serves k <= 16; these tests check that it
 actually served the search (last_search_stats()['prefilter']), that queries it cannot prove go
@@ -113,7 +113,7 @@ def test_prefilter_toggle_identical(mivs_lib):
     idx.set_prefilter(True)
     d3, i3 = ivf_flat.search(sp, idx, q, 10)
     assert torch.equal(i1, i3) and torch.equal(d1, d3)
-    # k above kPfMaxK: K13 + K16 (DESIGN.md §6e), the same bits as the fp32 scan (MIVS_LARGE_K_PF=0)
+    # k above kPfMaxK: K13 + K16 (DESIGN.md §6.6), the same bits as the fp32 scan (MIVS_LARGE_K_PF=0)
     d4, i4 = ivf_flat.search(sp, idx, q, 20)
     assert idx.last_search_stats()["prefilter"] == 1 and idx.last_search_stats()["scan_kernel"] == 13
     import os

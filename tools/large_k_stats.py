@@ -1,4 +1,4 @@
-"""Distribution of the k-th neighbour key at the benchmark shape (configs[2]) for the large-k design (DESIGN.md §6e):
+"""Distribution of the k-th neighbour key at the benchmark shape (configs[2]) for the large-k design (DESIGN.md §6.6):
 for a sample of queries, the exact L2 keys to every probed row (torch fp32 on the GPU; statistics only, not the
 pinned order) and, for k in KS: the global k-th key over the probed rows, the k-th over candidate pre-pass samples
 and the global rank those reach, and the rows inside the refine window above the k-th key.
