@@ -30,6 +30,30 @@
 using namespace mivs;
 using namespace mivs_capi;
 
+namespace mivs {
+namespace {
+std::atomic<int> g_engine_settings[kSetCount];
+}  // namespace
+
+int engine_setting(EngineSetting id, const char* name, int dflt) {
+  constexpr int kUnset = INT32_MIN;
+  static std::once_flag init;
+  std::call_once(init, [] {
+    for (auto& v : g_engine_settings) v.store(kUnset, std::memory_order_relaxed);
+  });
+  int v = g_engine_settings[id].load(std::memory_order_relaxed);
+  if (v == kUnset) {
+    v = env_int(name, dflt);
+    g_engine_settings[id].store(v, std::memory_order_relaxed);
+  }
+  return v;
+}
+
+void engine_settings_reset() {
+  for (auto& v : g_engine_settings) v.store(INT32_MIN, std::memory_order_relaxed);
+}
+}  // namespace mivs
+
 namespace {
 
 // hipEvent pairs around the build's hot kernels while profiling is on (the build's phase clock syncs the stream
@@ -1084,6 +1108,7 @@ bool pq_cand_slots() {
 void reload_settings() {
   g_fallback_sync.store(-1, std::memory_order_relaxed);
   g_pq_cands.store(-1, std::memory_order_relaxed);
+  engine_settings_reset();
 }
 
 void exact_fallback_on_device(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np,

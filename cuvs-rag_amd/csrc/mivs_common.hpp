@@ -435,6 +435,11 @@ bool pr_scan_supported(int dp);
 hipError_t launch_pr_scan(const PfScanArgs& a, int grid, hipStream_t s);
 hipError_t launch_pf_refine(const PfRefineArgs& a, hipStream_t s);
 hipError_t launch_refine(const RefineArgs& a, hipStream_t s);
+// engine switches the kernel launchers read: the environment variable's integer value, read once and
+// kept until mivs_reload_settings (capi.cpp) -- one getenv per process, not per call
+enum EngineSetting { kSetRefineGather = 0, kSetSelectSlotsWave = 1, kSetCount = 2 };
+int engine_setting(EngineSetting id, const char* name, int dflt);
+void engine_settings_reset();
 size_t rs_scan_lds_bytes(int dp);
 bool rs_scan_supported(int dp);
 hipError_t launch_rs_scan(const RsScanArgs& a, int dp, int grid, hipStream_t s);

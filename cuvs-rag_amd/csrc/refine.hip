@@ -336,10 +336,8 @@ hipError_t launch_refine(const RefineArgs& a, hipStream_t s) {
   if (a.k < 1 || a.k > kMaxK || a.dp > 1024 || a.dp < a.d) return hipErrorInvalidValue;
   if (a.nq <= 0) return hipSuccess;
   const dim3 grid((unsigned)ceil_div(a.nq, 4));
-  static const bool lane_per_row = [] {  // (MIVS_REFINE_GATHER=0: the one-lane-per-row kernel, for A/B runs)
-    const char* e = getenv("MIVS_REFINE_GATHER");
-    return e && e[0] == '0';
-  }();
+  // (MIVS_REFINE_GATHER=0: the one-lane-per-row kernel, for A/B runs)
+  const bool lane_per_row = engine_setting(kSetRefineGather, "MIVS_REFINE_GATHER", 1) == 0;
   const bool gather = !lane_per_row && (a.d & 7) == 0 && (a.dp & 63) == 0 &&
                       (reinterpret_cast<uintptr_t>(a.data) & 15) == 0;
   if (gather) {

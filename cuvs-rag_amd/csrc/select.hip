@@ -26,6 +26,7 @@
 // Replaces the large-k select_k inside cuVS ivf_flat::search / brute_force (reference
 // top_k = 2000, improved_multi_gpu_rag.py:65,247; 2*k per shard cuvs-2gpu-main.ipynb:1801).
 #include <climits>
+#include <cstdlib>
 
 #include "mivs_common.hpp"
 
@@ -532,6 +533,177 @@ __global__ __launch_bounds__(64 * kSmallWaves) void k_select_small(SelectArgs a)
   }
 }
 
+// K8c: the k <= 256 smallest (key, id) over a query's candidate slots (EXPLICIT with slot_begin: K9r's per-chunk
+// supersets for IVF-PQ + refine pools), one WAVE per query instead of K8's 1024-thread block -- a query has a few
+// thousand entries (~10 slots x 256, about half of them +inf padding), where K8's block barriers (a 1024-wide bitonic
+// sort among them) cost ~60 us of latency per query: 0.63 ms per 10k queries.
+//   1. T = the need-th smallest orderable key (need = min(k, valid)): four 8-bit digit passes, MSB first, each a
+//      256-bin LDS histogram of the keys that share the digits found so far and a wave scan to the digit holding
+//      the remaining rank (the keys stream from global each pass; a query's ~10 KB stay in L2);
+//   2. when more keys equal T than are needed, the same digit passes over their 64-bit ids give the largest id I
+//      taken among them (ids are distinct);
+//   3. the chosen (key < T, or key == T with id <= I: exactly need of them) -> LDS, bitonic sort by (key, id) in the
+//      wave, the first k out; missing ranks (id -1, +inf / IP -inf) as in K8.
+constexpr int kScWaves = 4;
+constexpr int kScMaxK = 256;
+
+template <int METRIC>
+__global__ __launch_bounds__(64 * kScWaves) void k_select_slots(SelectArgs a) {
+  __shared__ int s_hist[kScWaves][256];
+  __shared__ uint32_t s_u[kScWaves][kScMaxK];
+  __shared__ int64_t s_i[kScWaves][kScMaxK];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t q = (int64_t)blockIdx.x * kScWaves + wv;
+  if (q >= a.nq) return;  // (wave-uniform; no workgroup barrier below)
+  const int k = a.k;
+  const int64_t base = a.slot_begin[q] * a.n_in;
+  const int64_t n = (a.slot_begin[q + 1] - a.slot_begin[q]) * a.n_in;
+  int* hist = s_hist[wv];
+  auto key_at = [&](int64_t t) {  // orderable key bits; invalid (+inf padding) = 0xFFFFFFFF
+    const float dd = a.keys[base + t];
+    const uint32_t u = ord_bits(METRIC == kIP ? -dd : dd);
+    return u < kOrdInf ? u : 0xFFFFFFFFu;
+  };
+  // every candidate t of this lane with its key: f(t, u), the keys read from global (L2 after the first pass) four
+  // at a time, all four loads issued before any is used (held in registers for the whole selection, 64 per lane,
+  // the kernel ran 2.6x slower: the unrolled passes spilled)
+  auto for_each = [&](auto f) {
+    for (int64_t t0 = lane; t0 < n; t0 += 256) {
+      uint32_t u[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) u[j] = t0 + 64 * j < n ? key_at(t0 + 64 * j) : 0xFFFFFFFFu;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (t0 + 64 * j < n) f(t0 + 64 * j, u[j]);
+    }
+  };
+  int nv = 0;
+  uint32_t umin = 0xFFFFFFFFu, umax = 0u;
+  for_each([&](int64_t, uint32_t u) {
+    if (u == 0xFFFFFFFFu) return;
+    ++nv;
+    umin = u < umin ? u : umin;
+    umax = u > umax ? u : umax;
+  });
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    nv += __shfl_xor(nv, o);
+    const uint32_t a0 = __shfl_xor(umin, o), a1 = __shfl_xor(umax, o);
+    umin = a0 < umin ? a0 : umin;
+    umax = a1 > umax ? a1 : umax;
+  }
+  const int need = nv < k ? nv : k;
+  // digit passes (MSB first) over a 32- or 64-bit value of the members: the rank-th smallest value. The passes start
+  // at the highest byte in which the members can differ (top_shift; prefix = the bytes above it, common to all)
+  auto digit_select = [&](int top_shift, uint64_t prefix, auto value_of, auto member, int rank) {
+    for (int shift = top_shift; shift >= 0; shift -= 8) {
+      for (int b = lane; b < 256; b += 64) hist[b] = 0;
+      wave_lds_sync();
+      for_each([&](int64_t t, uint32_t u) {
+        if (!member(t, u)) return;
+        const uint64_t v = value_of(t, u);
+        if (shift + 8 < 64 && (v >> (shift + 8)) != prefix) return;
+        atomicAdd(&hist[(int)((v >> shift) & 255)], 1);
+      });
+      wave_lds_sync();
+      // the bin holding the rank-th: each lane sums 4 consecutive bins, a wave-inclusive scan over the lanes
+      int h[4], c = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { h[j] = hist[4 * lane + j]; c += h[j]; }
+      int inc = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int x = __shfl_up(inc, o);
+        if (lane >= o) inc += x;
+      }
+      int excl = inc - c, bin = -1, below = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (bin < 0 && excl < rank && rank <= excl + h[j]) { bin = 4 * lane + j; below = excl; }
+        excl += h[j];
+      }
+      const uint64_t found = __ballot(bin >= 0);
+      const int src = found ? __builtin_ctzll(found) : 0;
+      bin = __shfl(bin, src);
+      below = __shfl(below, src);
+      rank -= below;
+      prefix = (prefix << 8) | (uint64_t)bin;
+      wave_lds_sync();  // (the next pass clears the bins after every lane read them)
+    }
+    return prefix;
+  };
+  uint32_t T = 0xFFFFFFFFu;
+  int64_t I = LLONG_MAX;  // among keys == T, ids <= I are chosen
+  if (need > 0) {
+    // (keys of one query share their high bytes: the passes start at the first byte where umin and umax differ)
+    const uint32_t diff = umin ^ umax;
+    const int top = diff == 0 ? 0 : ((31 - __builtin_clz(diff)) / 8) * 8;
+    const uint64_t pre = top + 8 < 32 ? (uint64_t)(umin >> (top + 8)) : 0;
+    T = (uint32_t)digit_select(top, pre, [&](int64_t, uint32_t u) { return (uint64_t)u; },
+                               [&](int64_t, uint32_t u) { return u != 0xFFFFFFFFu; }, need);
+    int lt = 0, eq = 0;
+    for_each([&](int64_t, uint32_t u) {
+      lt += u < T ? 1 : 0;
+      eq += u == T ? 1 : 0;
+    });
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      lt += __shfl_xor(lt, o);
+      eq += __shfl_xor(eq, o);
+    }
+    if (eq > need - lt)  // a tie larger than needed: the (need - lt) smallest ids among keys == T (ids >= 0, distinct)
+      I = (int64_t)digit_select(56, 0, [&](int64_t t, uint32_t) { return (uint64_t)a.ids[base + t]; },
+                                [&](int64_t, uint32_t u) { return u == T; }, need - lt);
+  }
+  // the need chosen pairs -> LDS (ballot prefix positions; exactly need of them, <= kScMaxK)
+  if (need > 0) {
+    int cnt = 0;
+    auto collect = [&](int64_t t, uint32_t u) {  // (every lane calls it: the ballot is wave-wide)
+      bool take = false;
+      int64_t id = LLONG_MAX;
+      if (t < n && u <= T) {
+        id = a.ids[base + t];
+        take = u < T || id <= I;
+      }
+      const uint64_t m = __ballot(take);
+      if (take) {
+        const int at = cnt + __popcll(m & ((1ull << lane) - 1));
+        if (at < kScMaxK) { s_u[wv][at] = u; s_i[wv][at] = id; }
+      }
+      cnt += __popcll(m);
+    };
+    for (int64_t t0 = 0; t0 < n; t0 += 64) collect(t0 + lane, t0 + lane < n ? key_at(t0 + lane) : 0xFFFFFFFFu);
+  }
+  int p2 = 1;
+  while (p2 < need) p2 <<= 1;
+  for (int i = need + lane; i < p2; i += 64) { s_u[wv][i] = 0xFFFFFFFFu; s_i[wv][i] = LLONG_MAX; }
+  wave_lds_sync();
+  // bitonic sort of p2 (<= 256) pairs by (key, id) in the wave's LDS slice
+  for (int size = 2; size <= p2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = lane; i < (p2 >> 1); i += 64) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const uint32_t ka = s_u[wv][lo], kb = s_u[wv][hi];
+        const int64_t ia = s_i[wv][lo], ib = s_i[wv][hi];
+        const bool gt = ka > kb || (ka == kb && ia > ib);
+        if (gt == up) {
+          s_u[wv][lo] = kb; s_u[wv][hi] = ka;
+          s_i[wv][lo] = ib; s_i[wv][hi] = ia;
+        }
+      }
+      wave_lds_sync();
+    }
+  }
+  for (int t = lane; t < k; t += 64) {
+    const bool valid = t < need;
+    const float key = valid ? from_ord(s_u[wv][t]) : INFINITY;
+    a.out_d[q * k + t] = valid ? (METRIC == kIP ? -key : key) : (METRIC == kIP ? -INFINITY : INFINITY);
+    a.out_i[q * k + t] = valid ? s_i[wv][t] : (int64_t)-1;
+  }
+}
+
 template <int CAP>
 hipError_t launch_cap(const SelectArgs& a, bool expl, hipStream_t s) {
   const dim3 grid((unsigned)a.nq), block(kSelThreads);
@@ -564,6 +736,14 @@ hipError_t launch_select(const SelectArgs& a, hipStream_t s) {
       if (a.metric == kIP) hipLaunchKernelGGL((k_select_small<kIP, true, false>), grid, block, 0, s, a);
       else hipLaunchKernelGGL((k_select_small<kL2, true, false>), grid, block, 0, s, a);
     }
+    return hipGetLastError();
+  }
+  // (MIVS_SELECT_SLOTS_WAVE=0: K8's block form for the slots, A/B runs)
+  const bool slots_wave = engine_setting(kSetSelectSlotsWave, "MIVS_SELECT_SLOTS_WAVE", 1) != 0;
+  if (expl && a.slot_begin && a.k <= kScMaxK && slots_wave) {  // K8c
+    const dim3 grid((unsigned)ceil_div(a.nq, (int64_t)kScWaves)), block(64 * kScWaves);
+    if (a.metric == kIP) hipLaunchKernelGGL((k_select_slots<kIP>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_select_slots<kL2>), grid, block, 0, s, a);
     return hipGetLastError();
   }
   if (a.k <= 512) return launch_cap<1024>(a, expl, s);

@@ -273,6 +273,46 @@ def test_ivf_pq_candidate_slots_same_bits_as_dump(mivs_lib, monkeypatch, k, metr
     idx.close()
 
 
+@pytest.mark.parametrize("d,half,metric", [(768, True, "sqeuclidean"), (768, False, "sqeuclidean"),
+                                           (64, False, "inner_product"), (200, True, "sqeuclidean")])
+def test_refine_gather_switch_same_bits(mivs_lib, monkeypatch, d, half, metric):
+    """refine: K14g (eight lanes per candidate row; fp16 rows at dp <= 768 with the next pass prefetched) vs one
+    lane per row (MIVS_REFINE_GATHER=0): the same bits, with missing (-1) candidates and a ragged last pass"""
+    from mivs.neighbors import refine
+
+    rng = np.random.default_rng(d)
+    x = torch.from_numpy(_data(4000, d, 7)).cuda()
+    x = x.half() if half else x
+    q = torch.from_numpy(_data(21, d, 8)).cuda()
+    cand = torch.from_numpy(np.stack([rng.choice(4000, 117, replace=False) for _ in range(21)])).cuda()
+    cand[torch.from_numpy(rng.random(cand.shape) < 0.1).cuda()] = -1
+    d0, i0 = refine(x, q, cand, 10, metric=metric)
+    _setenv(monkeypatch, "MIVS_REFINE_GATHER", "0")
+    d1, i1 = refine(x, q, cand, 10, metric=metric)
+    np.testing.assert_array_equal(i1.cpu().numpy(), i0.cpu().numpy())
+    np.testing.assert_array_equal(_bits(d1.cpu().numpy()), _bits(d0.cpu().numpy()))
+
+
+@pytest.mark.parametrize("k", [65, 120, 256])
+def test_select_slots_wave_switch_same_bits(mivs_lib, monkeypatch, k):
+    """K9r's candidate slots ranked by K8c (one wave per query) vs K8's block form (MIVS_SELECT_SLOTS_WAVE=0), rows
+    duplicated 40 times so the k-th key is tied: the same bits"""
+    from mivs.neighbors import ivf_pq
+
+    base = _data(500, 64, 9)
+    x = np.concatenate([base] * 40)
+    q = _data(37, 64, 10)
+    idx = ivf_pq.build(ivf_pq.IndexParams(n_lists=8, pq_dim=16, kmeans_n_iters=3), torch.from_numpy(x).cuda())
+    sp = ivf_pq.SearchParams(n_probes=4)
+    qt = torch.from_numpy(q).cuda()
+    d0, i0 = ivf_pq.search(sp, idx, qt, k)
+    _setenv(monkeypatch, "MIVS_SELECT_SLOTS_WAVE", "0")
+    d1, i1 = ivf_pq.search(sp, idx, qt, k)
+    np.testing.assert_array_equal(i1.cpu().numpy(), i0.cpu().numpy())
+    np.testing.assert_array_equal(_bits(d1.cpu().numpy()), _bits(d0.cpu().numpy()))
+    idx.close()
+
+
 @pytest.mark.parametrize("n_probes", [16, 17, 32, 48])
 def test_coarse_probe_equals_oracle(ivf, flat_data, n_probes):
     """the coarse probe -- K3's register top-k up to 16 probes, K3w DUMP + K8s above (slot-uniform key loads, the

@@ -404,6 +404,7 @@ PQ_CASES = [
     (6000, 64, 16, 16, 4, 40, 8, 200),    # 64 < k <= 256: K9r candidate-superset slots + K8 (IVF-PQ + refine pools)
     (12000, 768, 32, 96, 2, 20, 6, 120),  # the bench's refine pool (12 x k = 120) at the reference's pq_dim
     (9000, 32, 2, 8, 3, 15, 2, 100),      # lists > 4096 rows: two chunks, two candidate slots per probe
+    (6000, 64, 32, 16, 3, 25, 20, 100),   # 20 slots per query (> 4096 entries): K8c reloads its keys per pass
     (12000, 768, 32, 96, 2, 20, 6, 300),  # k > 256: K9r DUMP + K8
 ]
 
@@ -511,11 +512,12 @@ def _pq_case(n, d, n_lists, pq_dim, iters, nq, n_probes, k, lut16=False):
     np.testing.assert_array_equal(_bits(dist.cpu().numpy()), _bits(od))
 
 
-@pytest.mark.parametrize("k", [10, 40, 100])
+@pytest.mark.parametrize("k", [10, 40, 100, 200])
 def test_ivf_pq_tied_keys_bitexact(mivs_lib, k):
     """every row 250 times: the best key of a list chunk is tied 250 times, more than K9r's 128-entry
-    candidate list at k <= 16 (its block-wide fallback rounds run), within the 512 list at k = 40, and
-    the DUMP + K8 tie order at k = 100 -- ids (ties by id) and bits equal to the oracle"""
+    candidate list at k <= 16 (its block-wide fallback rounds run), within the 512 list at k = 40, and at
+    k = 100 / 200 more than a 256-entry candidate slot holds (the slot's exact top-k) with K8c's id digit passes
+    ordering the ties -- ids (ties by id) and bits equal to the oracle"""
     from mivs.neighbors import ivf_pq
 
     base = _data(40, 64, seed=91, normalize=True)
