@@ -331,6 +331,103 @@ __global__ __launch_bounds__(512, 1) void probe16(const h8* __restrict__ rows, c
   out[(size_t)(blockIdx.x * WAVES + wave) * 64 + lane] = sink;
 }
 
+// W4 (round 6): workgroups of 4 waves (one per SIMD) and TWO per CU, 16-query tiles ([NK/2 + 1] x 1 KiB images,
+// double-buffered: 50 KiB of LDS per workgroup), items of 20 tiles (a list's ~312 queries), each workgroup's item
+// transitions phase-shifted by PHASE tiles against the other's (the real kernel's items differ in length, so the two
+// drift apart). The two waves on a SIMD belong to different workgroups: one's tile wait, epilogue and row reload can
+// run under the other's MFMAs, which K13's per-tile meeting point of all 8 waves prevents. VAR bits as probe's.
+template <int VAR, int PHASE>
+__global__ __launch_bounds__(256, 2) void probe_w4(const h8* __restrict__ rows, const char* __restrict__ src,
+                                                   int src_tiles, int ntiles, float* out, unsigned long long* clk,
+                                                   const h8* __restrict__ big_rows, long long big_items) {
+  constexpr int WAVES = 4, PD = 2, NT = NK / 2, BUF16 = NT * 1024 + 1024, ITEM = 20;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* s_ready = reinterpret_cast<int*>(smem + 2 * BUF16);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int i = tid; i < 2 * BUF16 / 16; i += WAVES * 64) {
+    const int v = (i * 2654435761u) >> 7;
+    reinterpret_cast<uint4*>(smem)[i] = make_uint4(v & 0x3BFF3BFF, (v >> 3) & 0x3BFF3BFF, v & 0x37FF37FF, 0x3C003C00 ^ (v & 0x03FF03FF));
+  }
+  if (tid == 0) *s_ready = 0;
+  __syncthreads();
+  h8 ra[NK];
+  const h8* rp = rows + ((size_t)(blockIdx.x * WAVES + wave) * NK) * 64 + lane;
+#pragma unroll
+  for (int s = 0; s < NK; ++s) ra[s] = rp[s * 64];
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  float sink = 0.f;
+  int cur = 0;
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  if (VAR & 1) {
+    if (lane == 0) __hip_atomic_fetch_add(s_ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  const int phase = (blockIdx.x & 1) ? PHASE : 0;
+  auto tile = [&](int t, auto rl_c) __attribute__((always_inline)) {
+    constexpr bool RL = decltype(rl_c)::value;
+    if (VAR & 1) {
+      for (int i = 0; i < (1 << 20); ++i) {
+        if (__hip_atomic_load(s_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= WAVES * (t + 1)) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      asm volatile("" ::: "memory");
+    }
+    const char* bb = smem + cur * BUF16 + lane * 16;
+    const int nxt = cur ^ 1;
+    char* sbuf = smem + nxt * BUF16;
+    const int tsrc = (VAR & 16) ? (int)(((blockIdx.x & 7) * 1375 + t + 1) % src_tiles) : (int)((blockIdx.x + t) % src_tiles);
+    const v4i sdesc = uniform_desc(src + (size_t)tsrc * (NT + 1) * 1024, (NT + 1) * 1024);
+    const h8* nr = big_rows + ((size_t)(((long long)blockIdx.x * 7919 + t * 131) % big_items) * WAVES + wave) * NK * 64 + lane;
+    if ((VAR & 8) && (t + phase) % ITEM == 0) __builtin_amdgcn_s_waitcnt(0x0070);
+    f32x4 acc[2] = {z, z};
+    h8 b[PD + 1];
+#pragma unroll
+    for (int u = 0; u < PD; ++u) b[u] = *reinterpret_cast<const h8*>(bb + u * 1024);
+#pragma unroll
+    for (int s = 0; s < NT; ++s) {
+      if (s + PD < NT) b[(s + PD) % (PD + 1)] = *reinterpret_cast<const h8*>(bb + (s + PD) * 1024);
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[2 * s], b[s % (PD + 1)], acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[2 * s + 1], b[s % (PD + 1)], acc[1], 0, 0, 0);
+      if (RL) {
+        ra[2 * s] = __builtin_nontemporal_load(nr + (2 * s) * 64);
+        ra[2 * s + 1] = __builtin_nontemporal_load(nr + (2 * s + 1) * 64);
+      }
+      if (VAR & 2) {
+        if (s >= 1 && (s - 1) * WAVES <= NT) {
+          const int p = min((s - 1) * WAVES + wave, NT);
+          dma_b128(sdesc, sbuf + p * 1024, lane * 16, p * 1024);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (VAR & 2) __builtin_amdgcn_s_waitcnt(0x0070);
+    if (VAR & 1) {
+      asm volatile("" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(s_ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (VAR & 4) {
+      float am0 = fmaxf(acc[0][0], acc[1][0]);
+#pragma unroll
+      for (int i = 1; i < 4; ++i) am0 = fmaxf(am0, fmaxf(acc[0][i], acc[1][i]));
+      if (__ballot(fmaf(am0, -2.f, 0.5f) < -1e30f)) sink += 1.f;
+      sink += am0 * 1e-30f;
+    } else {
+      sink += acc[0][0] + acc[1][1];
+    }
+    cur = nxt;
+  };
+  for (int t = 0; t < ntiles; ++t) {
+    if ((VAR & 8) && (t + phase) % ITEM == ITEM - 1) tile(t, BoolC<true>{});
+    else tile(t, BoolC<false>{});
+  }
+  __builtin_amdgcn_s_waitcnt(0x0070);
+  const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0 && wave == 0) {
+    clk[2 * blockIdx.x] = t1 - t0;
+    clk[2 * blockIdx.x + 1] = r1 - r0;
+  }
+  out[(size_t)(blockIdx.x * WAVES + wave) * 64 + lane] = sink;
+}
+
 const h8* g_big = nullptr;
 const char* g_q = nullptr;
 long long g_big_items = 1;
@@ -397,6 +494,37 @@ int run16(const char* name, const h8* rows, const char* src, int src_tiles, floa
   return 0;
 }
 
+template <int VAR, int PHASE>
+int run_w4(const char* name, const h8* rows, const char* src, int src_tiles, float* out, unsigned long long* clk,
+           int grid, int ntiles) {
+  const size_t lds = 2 * (NK / 2 * 1024 + 1024) + 64;
+  CHECK(hipFuncSetAttribute((const void*)probe_w4<VAR, PHASE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  for (int rep = 0; rep < 3; ++rep)
+    hipLaunchKernelGGL((probe_w4<VAR, PHASE>), dim3(grid), dim3(256), lds, 0, rows, src, src_tiles, ntiles, out, clk, g_big, g_big_items);
+  CHECK(hipEventRecord(e0));
+  hipLaunchKernelGGL((probe_w4<VAR, PHASE>), dim3(grid), dim3(256), lds, 0, rows, src, src_tiles, ntiles, out, clk, g_big, g_big_items);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  float ms = 0;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  std::vector<unsigned long long> h(2 * grid);
+  CHECK(hipMemcpy(h.data(), clk, sizeof(unsigned long long) * 2 * grid, hipMemcpyDeviceToHost));
+  double ghz = 0;
+  for (int b = 0; b < grid; ++b) ghz += (double)h[2 * b] / (double)h[2 * b + 1] * 0.1;
+  ghz /= grid;
+  const double n_mfma = (double)grid * 4 * ntiles * NK;  // NK / 2 pieces x 2 MFMAs per wave and tile
+  const double tf = n_mfma * 16 * 16 * 32 * 2 / (ms * 1e-3) / 1e12;
+  const double pipe = n_mfma / (grid / 2 * 4.0) * 16 / (ms * 1e-3 * ghz * 1e9);
+  printf("%-34s %8.3f ms  %7.1f TF/s  clock %.3f GHz  pipe busy %.3f  frac-of-2.5PF %.3f\n", name, ms, tf, ghz, pipe,
+         tf / 2500.0);
+  CHECK(hipEventDestroy(e0));
+  CHECK(hipEventDestroy(e1));
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const int grid = 256;
   const int ntiles = argc > 1 ? atoi(argv[1]) : 4000;
@@ -424,7 +552,7 @@ int main(int argc, char** argv) {
     g_q = qa;
   }
   CHECK(hipMalloc(&out, (size_t)grid * 8 * 64 * sizeof(float)));
-  CHECK(hipMalloc(&clk, sizeof(unsigned long long) * 2 * grid));
+  CHECK(hipMalloc(&clk, sizeof(unsigned long long) * 4 * grid));  // (W4 runs 2 x grid workgroups)
   {
     std::vector<uint16_t> hr(nrows * 8);
     uint32_t x = 12345;
@@ -441,6 +569,19 @@ int main(int argc, char** argv) {
     CHECK(hipMemcpy(src, hs.data(), hs.size() * 2, hipMemcpyHostToDevice));
   }
   printf("grid %d, %d tiles per wave, 16x16x32 f16, 32 rows x 768 dims per wave in registers\n", grid, ntiles);
+  const int mode = argc > 2 ? atoi(argv[2]) : 0;
+  if (mode == 1) {  // round 6: K13's shape (8 waves, 32-query tiles, items of 10) vs W4 (2 x 4 waves, 16-query tiles, items of 20)
+    // (the same MFMAs: W4 runs twice the tiles of half the size on twice the workgroups)
+    const int tiles = ntiles - ntiles % 20;
+    for (int rep = 0; rep < 2; ++rep) {
+      run<7 + 8 + 16 + 256, 2, 8>("K13 8w: sync dma epi items hbm", rows, src, big_tiles, out, clk, grid, tiles);
+      run_w4<7 + 8 + 16, 10>("W4 2x4w: sync dma epi items hbm", rows, src, big_tiles, out, clk, 2 * grid, 2 * tiles);
+      run_w4<7 + 8 + 16, 0>("W4 in phase", rows, src, big_tiles, out, clk, 2 * grid, 2 * tiles);
+      run<7 + 16, 2, 8>("K13 8w: no items (reload-free)", rows, src, big_tiles, out, clk, grid, tiles);
+      run_w4<7 + 16, 0>("W4: no items (reload-free)", rows, src, big_tiles, out, clk, 2 * grid, 2 * tiles);
+    }
+    return 0;
+  }
   run<7, 2, 8>("+sync +dma +epi", rows, src, src_tiles, out, clk, grid, ntiles);
   run<7 + 2048, 2, 8>("+split sync (3 bufs) +dma +epi", rows, src, src_tiles, out, clk, grid, ntiles);
   run<7 + 2048 + 4096, 2, 8>("+split sync, waves 4-7 offset", rows, src, src_tiles, out, clk, grid, ntiles);
