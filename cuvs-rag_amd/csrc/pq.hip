@@ -1110,20 +1110,23 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
         a.slot_info[2 * s_slot[tid] + 1] = nr;
       }
     } else {
-      // 1. per query the minimum of my rows
+      // 1. per query the minimum of my rows (query slots past the tile's nqt queries are skipped in 1-3: their sums
+      // are not formed, see the scan's piece reads)
 #pragma unroll
       for (int t = 0; t < TQ; ++t) {
-        float mn = INFINITY;
-        bool any = false;
+        if (t < nqt) {  // (item-uniform)
+          float mn = INFINITY;
+          bool any = false;
 #pragma unroll
-        for (int i = 0; i < RPT; ++i) {
-          if (i * NT + tid < nr) { mn = fminf(mn, acc[i][t]); any = true; }
+          for (int i = 0; i < RPT; ++i) {
+            if (i * NT + tid < nr) { mn = fminf(mn, acc[i][t]); any = true; }
+          }
+          s_min[t * NT + tid] = any ? rt_ord(mn) : 0xFFFFFFFFu;
         }
-        s_min[t * NT + tid] = any ? rt_ord(mn) : 0xFFFFFFFFu;
       }
       __syncthreads();
       // 2. bound_q = the k-th smallest of the NT minima (wave w: queries 2w, 2w + 1), bit by bit
-      for (int t = wave; t < TQ; t += NT / 64) {
+      for (int t = wave; t < nqt; t += NT / 64) {
         uint32_t v[NT / 64];
 #pragma unroll
         for (int u = 0; u < NT / 64; ++u) v[u] = s_min[t * NT + u * 64 + lane];
@@ -1143,6 +1146,7 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
       // 3. rows at or below the bound -> the query's candidate list
 #pragma unroll
       for (int t = 0; t < TQ; ++t) {
+        if (t >= nqt) continue;  // (item-uniform; unrolled, so a predicated body)
         // rt_ord(x) <= bound  <=>  x <= the bound's float (-0 == +0 both ways); all ones: every row
         const uint32_t bnd = s_bound[t];
         const float fb = bnd == 0xFFFFFFFFu ? INFINITY
