@@ -1019,7 +1019,6 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
     load_word(0, cw);
     const bool skip_scan = a.flags & 2;
     const int np4 = (nqt + 3) >> 2;  // fp32 LUT: 16-B pieces (4 queries each) of a code row the tile uses
-    const bool nh2 = nqt > 8;        // fp16 LUT: the second piece (queries 8..15) is used
     // row iterations of this wave inside the chunk (wave-uniform)
     const int nvi = nr > wave * 64 ? (nr - wave * 64 + NT - 1) / NT : 0;
     // subspaces in pairs, one barrier per pair: at pair (j, j + 1) the next pair's codebook rows are requested, the
@@ -1038,8 +1037,9 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
           }
         }
         const float* lut = s_lut + (j & 3) * (kPqCodes * LS);
-        // only the 16-B pieces of a code row that hold the tile's queries are read (np4 / nh2 are item-uniform: the
-        // branches are scalar): a tile of 12 queries reads 3 of 4 fp32 pieces, of <= 8 one of two fp16 pieces
+        // fp32: only the 16-B pieces of a code row that hold the tile's queries are read (np4 is item-uniform: the
+        // branches are scalar; a tile of 12 queries reads 3 of 4). fp16: both pieces always -- skipping the second for
+        // tiles of <= 8 queries broke the grouped issue of the RH rows' reads (K9r 7.92 vs 8.14 ms, profiles/r06p_pq_lut16_ab/)
         if constexpr (H16) {  // RH rows' halves in flight (2: 7.97 ms, 4: 7.84 ms at configs[4])
           constexpr int RH = 4;
 #pragma unroll
@@ -1050,19 +1050,16 @@ __global__ __launch_bounds__(kRtThreads) void k_pq_scan_rt(PqTileArgs a) {
               for (int r = 0; r < RH; ++r) {
                 const pq_u32x4* p = reinterpret_cast<const pq_u32x4*>(lut + ((cw[i0 + r] >> (8 * b)) & 0xFF) * LS);
                 v[r][0] = p[0];
-                v[r][1] = pq_u32x4{0u, 0u, 0u, 0u};
-                if (nh2) v[r][1] = p[1];
+                v[r][1] = p[1];
               }
               __builtin_amdgcn_sched_group_barrier(0x100, 2 * RH, 0);  // the LDS reads issue first
 #pragma unroll
               for (int r = 0; r < RH; ++r) {
                 if (r == 0 || i0 + r < nvi) {
 #pragma unroll
-                  for (int t = 0; t < 8; ++t) acc[i0 + r][t] = rt_add_f16(acc[i0 + r][t], v[r][0][t >> 1], t & 1);
-                  if (nh2) {
-#pragma unroll
-                    for (int t = 0; t < 8; ++t)
-                      acc[i0 + r][8 + t] = rt_add_f16(acc[i0 + r][8 + t], v[r][1][t >> 1], t & 1);
+                  for (int t = 0; t < 8; ++t) {
+                    acc[i0 + r][t] = rt_add_f16(acc[i0 + r][t], v[r][0][t >> 1], t & 1);
+                    acc[i0 + r][8 + t] = rt_add_f16(acc[i0 + r][8 + t], v[r][1][t >> 1], t & 1);
                   }
                 }
               }
