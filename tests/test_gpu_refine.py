@@ -24,6 +24,8 @@ def _bits(a):
     (4000, 768, 25, 120, 10, "sqeuclidean", True),     # fp16 dataset (BASELINE config 5)
     (2000, 32, 9, 8, 8, "sqeuclidean", False),         # k = n_candidates
     (6000, 128, 11, 200, 64, "inner_product", True),
+    (3000, 1024, 9, 70, 10, "sqeuclidean", True),      # fp16 rows past dp 768: K14g without the next-pass prefetch
+    (2500, 1000, 7, 45, 12, "inner_product", False),   # fp32, dp 1024 > d: two 64-dim block rounds, padding blocks
 ])
 def test_refine_bitexact_vs_oracle(mivs_lib, n, d, nq, nc, k, metric, half):
     from mivs.neighbors import refine
