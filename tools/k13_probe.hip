@@ -428,6 +428,123 @@ __global__ __launch_bounds__(256, 2) void probe_w4(const h8* __restrict__ rows, 
   out[(size_t)(blockIdx.x * WAVES + wave) * 64 + lane] = sink;
 }
 
+// W4H (round 6): as W4 (two 4-wave workgroups per CU, item transitions phase-shifted) but with K13's 32-query tiles:
+// the LDS holds a ring of three HALF tiles per workgroup (pieces 0..23 = dims 0..383, pieces 24..47 + the header =
+// dims 384..767; 3 x 25 KiB), so both workgroups fit; the wave signals after each half (its pieces of the half two
+// ahead are issued during a half, into the buffer of the half before it). Per-tile work, epilogue and reloads as K13.
+template <int VAR, int PHASE>
+__global__ __launch_bounds__(256, 2) void probe_w4h(const h8* __restrict__ rows, const char* __restrict__ src,
+                                                    int src_tiles, int ntiles, float* out, unsigned long long* clk,
+                                                    const h8* __restrict__ big_rows, long long big_items) {
+  constexpr int WAVES = 4, PD = 2, NH = NK / 2, HBUF = NH * 1024 + 1024, ITEM = 10;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* s_ready = reinterpret_cast<int*>(smem + 3 * HBUF);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int i = tid; i < 3 * HBUF / 16; i += WAVES * 64) {
+    const int v = (i * 2654435761u) >> 7;
+    reinterpret_cast<uint4*>(smem)[i] = make_uint4(v & 0x3BFF3BFF, (v >> 3) & 0x3BFF3BFF, v & 0x37FF37FF, 0x3C003C00 ^ (v & 0x03FF03FF));
+  }
+  if (tid == 0) *s_ready = 0;
+  __syncthreads();
+  h8 ra[NK];
+  const h8* rp = rows + ((size_t)(blockIdx.x * WAVES + wave) * NK) * 64 + lane;
+#pragma unroll
+  for (int s = 0; s < NK; ++s) ra[s] = rp[s * 64];
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  float sink = 0.f;
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  if (VAR & 1) {  // halves 0 and 1 are "landed" at the start (the prologue's)
+    if (lane == 0) __hip_atomic_fetch_add(s_ready, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  const int phase = (blockIdx.x & 1) ? PHASE : 0;
+  f32x4 acc[4] = {z, z, z, z};
+  // half h of tile t = h >> 1; its buffer h % 3; during half h the wave issues its pieces of half h + 2
+  auto half = [&](int h, auto rl_c, auto hi_c) __attribute__((always_inline)) {
+    constexpr bool RL = decltype(rl_c)::value;
+    constexpr int HI = decltype(hi_c)::value;  // 0: pieces 0..23, 1: pieces 24..47 (+ the header)
+    const int t = h >> 1;
+    if (VAR & 1) {
+      for (int i = 0; i < (1 << 20); ++i) {
+        if (__hip_atomic_load(s_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= WAVES * (h + 2)) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      asm volatile("" ::: "memory");
+    }
+    const char* bb = smem + (h % 3) * HBUF + lane * 16;
+    char* sbuf = smem + ((h + 2) % 3) * HBUF;
+    const int h2 = h + 2, t2 = h2 >> 1;
+    const int tsrc = (VAR & 16) ? (int)(((blockIdx.x & 7) * 1375 + t2) % src_tiles) : (int)((blockIdx.x + t2) % src_tiles);
+    const v4i sdesc = uniform_desc(src + (size_t)tsrc * (NK + 1) * 1024 + (h2 & 1) * NH * 1024, HBUF);
+    const h8* nr = big_rows + ((size_t)(((long long)blockIdx.x * 7919 + t * 131) % big_items) * WAVES + wave) * NK * 64 + lane;
+    if (HI == 0) {
+      if ((VAR & 8) && (t + phase) % ITEM == 0) __builtin_amdgcn_s_waitcnt(0x0070);
+      acc[0] = z; acc[1] = z; acc[2] = z; acc[3] = z;
+    }
+    h8 b[PD + 1];
+#pragma unroll
+    for (int u = 0; u < PD; ++u) b[u] = *reinterpret_cast<const h8*>(bb + u * 1024);
+#pragma unroll
+    for (int u = 0; u < NH; ++u) {
+      const int s = HI * NH + u;
+      if (u + PD < NH) b[(u + PD) % (PD + 1)] = *reinterpret_cast<const h8*>(bb + (u + PD) * 1024);
+      const int tt = 2 * (s >> 1), qb = s & 1;
+      acc[2 * qb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[tt], b[u % (PD + 1)], acc[2 * qb], 0, 0, 0);
+      acc[2 * qb + 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[tt + 1], b[u % (PD + 1)], acc[2 * qb + 1], 0, 0, 0);
+      if (RL && (s & 1)) {
+        ra[s - 1] = __builtin_nontemporal_load(nr + (s - 1) * 64);
+        ra[s] = __builtin_nontemporal_load(nr + s * 64);
+      }
+      if (VAR & 2) {  // this wave's pieces of half h + 2 (25 pieces over 4 waves: 7 per wave, the last repeats)
+        if (u >= 1 && (u - 1) * WAVES <= NH) {
+          const int p = min((u - 1) * WAVES + wave, NH);
+          dma_b128(sdesc, sbuf + p * 1024, lane * 16, p * 1024);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // signal: done reading half h, and my pieces of half h + 1 (issued during half h - 1) landed: everything but
+    // this half's 7 DMA pieces (and, reloading, the row loads after them) may stay in flight
+    if (VAR & 2) {
+      if (RL) __builtin_amdgcn_s_waitcnt((31 & 15) | (0x7 << 4) | ((31 >> 4) << 14));  // + this half's 24 row loads
+      else __builtin_amdgcn_s_waitcnt((7 & 15) | (0x7 << 4) | ((7 >> 4) << 14));
+    }
+    if (VAR & 1) {
+      asm volatile("" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(s_ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (HI == 1) {
+      if (VAR & 4) {
+        float am0 = fmaxf(acc[0][0], acc[1][0]), am1 = fmaxf(acc[2][0], acc[3][0]);
+#pragma unroll
+        for (int i = 1; i < 4; ++i) {
+          am0 = fmaxf(am0, fmaxf(acc[0][i], acc[1][i]));
+          am1 = fmaxf(am1, fmaxf(acc[2][i], acc[3][i]));
+        }
+        if (__ballot(fmaf(am0, -2.f, 0.5f) < -1e30f || fmaf(am1, -2.f, 0.5f) < -1e30f)) sink += 1.f;
+        sink += am0 * 1e-30f;
+      } else {
+        sink += acc[0][0] + acc[1][1] + acc[2][2] + acc[3][3];
+      }
+    }
+  };
+  for (int t = 0; t < ntiles; ++t) {
+    if ((VAR & 8) && (t + phase) % ITEM == ITEM - 1) {
+      half(2 * t, BoolC<true>{}, IntC<0>{});
+      half(2 * t + 1, BoolC<true>{}, IntC<1>{});
+    } else {
+      half(2 * t, BoolC<false>{}, IntC<0>{});
+      half(2 * t + 1, BoolC<false>{}, IntC<1>{});
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0x0070);
+  const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0 && wave == 0) {
+    clk[2 * blockIdx.x] = t1 - t0;
+    clk[2 * blockIdx.x + 1] = r1 - r0;
+  }
+  out[(size_t)(blockIdx.x * WAVES + wave) * 64 + lane] = sink;
+}
+
 const h8* g_big = nullptr;
 const char* g_q = nullptr;
 long long g_big_items = 1;
@@ -525,6 +642,37 @@ int run_w4(const char* name, const h8* rows, const char* src, int src_tiles, flo
   return 0;
 }
 
+template <int VAR, int PHASE>
+int run_w4h(const char* name, const h8* rows, const char* src, int src_tiles, float* out, unsigned long long* clk,
+            int grid, int ntiles) {
+  const size_t lds = 3 * (NK / 2 * 1024 + 1024) + 64;
+  CHECK(hipFuncSetAttribute((const void*)probe_w4h<VAR, PHASE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  for (int rep = 0; rep < 3; ++rep)
+    hipLaunchKernelGGL((probe_w4h<VAR, PHASE>), dim3(grid), dim3(256), lds, 0, rows, src, src_tiles, ntiles, out, clk, g_big, g_big_items);
+  CHECK(hipEventRecord(e0));
+  hipLaunchKernelGGL((probe_w4h<VAR, PHASE>), dim3(grid), dim3(256), lds, 0, rows, src, src_tiles, ntiles, out, clk, g_big, g_big_items);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  float ms = 0;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  std::vector<unsigned long long> h(2 * grid);
+  CHECK(hipMemcpy(h.data(), clk, sizeof(unsigned long long) * 2 * grid, hipMemcpyDeviceToHost));
+  double ghz = 0;
+  for (int b = 0; b < grid; ++b) ghz += (double)h[2 * b] / (double)h[2 * b + 1] * 0.1;
+  ghz /= grid;
+  const double n_mfma = (double)grid * 4 * ntiles * 2 * NK;
+  const double tf = n_mfma * 16 * 16 * 32 * 2 / (ms * 1e-3) / 1e12;
+  const double pipe = n_mfma / (grid / 2 * 4.0) * 16 / (ms * 1e-3 * ghz * 1e9);
+  printf("%-34s %8.3f ms  %7.1f TF/s  clock %.3f GHz  pipe busy %.3f  frac-of-2.5PF %.3f\n", name, ms, tf, ghz, pipe,
+         tf / 2500.0);
+  CHECK(hipEventDestroy(e0));
+  CHECK(hipEventDestroy(e1));
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const int grid = 256;
   const int ntiles = argc > 1 ? atoi(argv[1]) : 4000;
@@ -570,6 +718,16 @@ int main(int argc, char** argv) {
   }
   printf("grid %d, %d tiles per wave, 16x16x32 f16, 32 rows x 768 dims per wave in registers\n", grid, ntiles);
   const int mode = argc > 2 ? atoi(argv[2]) : 0;
+  if (mode == 2) {  // round 6: K13's shape vs W4H (2 x 4 waves, 32-query tiles in a ring of three half tiles)
+    const int tiles = ntiles - ntiles % 10;
+    for (int rep = 0; rep < 2; ++rep) {
+      run<7 + 8 + 16 + 256, 2, 8>("K13 8w: sync dma epi items hbm", rows, src, big_tiles, out, clk, grid, tiles);
+      run_w4h<7 + 8 + 16, 5>("W4H: sync dma epi items hbm", rows, src, big_tiles, out, clk, 2 * grid, tiles);
+      run_w4h<7 + 8 + 16, 0>("W4H in phase", rows, src, big_tiles, out, clk, 2 * grid, tiles);
+      run_w4h<7 + 16, 0>("W4H: no items (reload-free)", rows, src, big_tiles, out, clk, 2 * grid, tiles);
+    }
+    return 0;
+  }
   if (mode == 1) {  // round 6: K13's shape (8 waves, 32-query tiles, items of 10) vs W4 (2 x 4 waves, 16-query tiles, items of 20)
     // (the same MFMAs: W4 runs twice the tiles of half the size on twice the workgroups)
     const int tiles = ntiles - ntiles % 20;
