@@ -16,6 +16,9 @@
 //   1024 the query pieces gathered straight from a [10k][768] fp16 query array (lane (c, kq) of piece 2 t + qb reads
 //      16 B of query id(16 qb + c) at dims 32 t + 8 kq; ids spread pseudo-randomly over the 15 MB array) instead of
 //      copied from a prebuilt tile image; the header piece still from the image
+//   8192 (with 8) the first PF_P row registers of the next item (PF_P = 7, or 4 with 16384) LDS-DMA'd into a spare
+//      56 KiB of LDS during the item's tiles 1..PF_P, one register per wave per tile, and read from LDS (not HBM) at
+//      the item transition: the transition's HBM intake shrinks by PF_P / 48
 // Reports TF/s, the in-kernel clock (s_memtime / s_memrealtime) and the MFMA pipe's busy fraction.
 // Build: hipcc -O3 --offload-arch=gfx950 -ffp-contract=off tools/k13_probe.hip -o tools/k13_probe
 #include <hip/hip_runtime.h>
@@ -76,6 +79,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void probe(const h8* __restrict__ ro
   constexpr int LANDED_AT = (VAR & 4096) ? 16 : 40;  // (4096: the landed signal early, so waves may lag ~2/3 tile)
   int* s_ready = reinterpret_cast<int*>(smem + NBUF * BUF);
   int* s_done = s_ready + 1;
+  constexpr int PF_P = (VAR & 16384) ? 4 : 7;
+  char* s_pf = smem + NBUF * BUF + 64;  // [WAVES][PF_P] x 1 KiB (VAR & 8192)
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const v4i qdesc = uniform_desc(qarr, kQ * NK * 32);
   for (int i = tid; i < NBUF * BUF / 16; i += WAVES * 64) {
@@ -125,6 +130,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void probe(const h8* __restrict__ ro
     const int gq0 = (int)(((long long)(tsrc * 32 + c) * 7919) % kQ), gq1 = (int)(((long long)(tsrc * 32 + 16 + c) * 7919) % kQ);
     const int qo0 = gq0 * (NK * 32) + (lane >> 4) * 16, qo1 = gq1 * (NK * 32) + (lane >> 4) * 16;
     const h8* nr = big_rows + ((size_t)(((long long)blockIdx.x * 7919 + t * 131) % big_items) * WAVES + wave) * NK * 64 + lane;
+    // VAR & 8192: this item's reload tile t9 and the next item's rows of this wave (the same address as nr there)
+    const int t9 = t - t % 10 + 9;
+    const h8* nr9 = big_rows + ((size_t)(((long long)blockIdx.x * 7919 + t9 * 131) % big_items) * WAVES + wave) * NK * 64;
+    const int pf_p = t % 10 - 1;  // the register prefetched in this tile (tiles 1 .. PF_P of an item)
+    const v4i pdesc = uniform_desc(nr9, NK * 1024);
     if (!(VAR & 32) && (VAR & 8) && t % 10 == 0) __builtin_amdgcn_s_waitcnt(0x0070);
     f32x4 acc[4] = {z, z, z, z};
     h8 b[PD + 1];
@@ -140,6 +150,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void probe(const h8* __restrict__ ro
         if (VAR & 128) {  // (timing only) loads the compiler does not see: no waits for them anywhere
           asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(ra[s - 1]) : "v"(nr + (s - 1) * 64) : "memory");
           asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(ra[s]) : "v"(nr + s * 64) : "memory");
+        } else if ((VAR & 8192) && s - 1 < PF_P) {  // prefetched registers from LDS
+          ra[s - 1] = *reinterpret_cast<const h8*>(s_pf + (wave * PF_P + s - 1) * 1024 + lane * 16);
+          if (s < PF_P) ra[s] = *reinterpret_cast<const h8*>(s_pf + (wave * PF_P + s) * 1024 + lane * 16);
+          else ra[s] = __builtin_nontemporal_load(nr + s * 64);
         } else if (VAR & 256) {  // non-temporal policy (K13's rows: aux = 2)
           ra[s - 1] = __builtin_nontemporal_load(nr + (s - 1) * 64);
           ra[s] = __builtin_nontemporal_load(nr + s * 64);
@@ -167,6 +181,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void probe(const h8* __restrict__ ro
           else dma_b128(sdesc, sbuf + p * 1024, lane * 16, p * 1024);
         }
       }
+      if ((VAR & 8192) && s == 24 && pf_p >= 0 && pf_p < PF_P)
+        dma_b128(pdesc, s_pf + (wave * PF_P + pf_p) * 1024, lane * 16, pf_p * 1024);
       __builtin_amdgcn_sched_barrier(0);
     }
     if (VAR & 32) {
@@ -552,7 +568,7 @@ long long g_big_items = 1;
 template <int VAR, int PD, int WAVES>
 int run(const char* name, const h8* rows, const char* src, int src_tiles, float* out, unsigned long long* clk,
         int grid, int ntiles) {
-  const size_t lds = ((VAR & 2048) ? 3 : 2) * BUF + 64;
+  const size_t lds = ((VAR & 2048) ? 3 : 2) * BUF + 64 + ((VAR & 8192) ? (size_t)WAVES * 7 * 1024 : 0);
   CHECK(hipFuncSetAttribute((const void*)probe<VAR, PD, WAVES>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
@@ -718,6 +734,16 @@ int main(int argc, char** argv) {
   }
   printf("grid %d, %d tiles per wave, 16x16x32 f16, 32 rows x 768 dims per wave in registers\n", grid, ntiles);
   const int mode = argc > 2 ? atoi(argv[2]) : 0;
+  if (mode == 3) {  // round 6: K13's shape with the next item's first rows prefetched into spare LDS
+    const int tiles = ntiles - ntiles % 10;
+    for (int rep = 0; rep < 2; ++rep) {
+      run<7 + 8 + 16 + 256, 2, 8>("K13 8w: sync dma epi items hbm", rows, src, big_tiles, out, clk, grid, tiles);
+      run<7 + 8 + 16 + 256 + 8192, 2, 8>("+ 7 of 48 rows regs via LDS", rows, src, big_tiles, out, clk, grid, tiles);
+      run<7 + 8 + 16 + 256 + 8192 + 16384, 2, 8>("+ 4 of 48 rows regs via LDS", rows, src, big_tiles, out, clk, grid, tiles);
+      run<7 + 16 + 256, 2, 8>("K13 8w: no items (reload-free)", rows, src, big_tiles, out, clk, grid, tiles);
+    }
+    return 0;
+  }
   if (mode == 2) {  // round 6: K13's shape vs W4H (2 x 4 waves, 32-query tiles in a ring of three half tiles)
     const int tiles = ntiles - ntiles % 10;
     for (int rep = 0; rep < 2; ++rep) {
