@@ -981,9 +981,10 @@ void pf_refine_fallback(mivs_index_s* idx, hipStream_t s, const float* q, int64_
 // kth_out: K13's pre-pass -- only the k-th smallest approximate key per query (no refine, no fallback);
 // verify_sel > 0 (with the fp8 scan, f8) makes kth_out the k-th smallest fp32 key of each query's verify_sel
 // best-scored rows
+// raw: K10 leaves each slot as its 16 lane lists (no per-slot merge; K11 / K11v rank every entry)
 void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int k, int np, float* out_d,
                     int64_t* out_i, ProfRec* pr, const int64_t* goff, int n_lists, float* kth_out = nullptr,
-                    int verify_sel = 0, bool f8 = false) {
+                    int verify_sel = 0, bool f8 = false, bool raw = false) {
   Workspace& ws = idx->ws;
   const ListSet& L = idx->lists;
   const int dp = idx->dp;
@@ -997,7 +998,7 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   const std::vector<int64_t>& tcp = idx->pf_top_chunks_prefix;
   const int64_t max_slots = std::max<int64_t>(1, nq * tcp[std::min<int64_t>(np, L.n_lists)]);
   // per-slot candidates: room above k so that a neighbourhood packed into one chunk does not overflow
-  const int slot_k = kPfSlotKMax;
+  const int slot_k = raw ? 16 * kPfLaneK : kPfSlotKMax;
   ws.pf_key.reserve(sizeof(float) * (size_t)max_slots * slot_k);
   ws.pf_pos.reserve(sizeof(int) * (size_t)max_slots * slot_k);
   ws.pf_bound.reserve(sizeof(float) * (size_t)max_slots);
@@ -1043,7 +1044,8 @@ void pf_scan_refine(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq
   a.qtheta = ws.qtheta.as<unsigned>();
   a.k = verify_sel > 0 ? std::min(verify_sel, kPfMaxK) : k;  // (nomination: the slots keep the verify_sel best)
   // (nomination: K11v reads only each slot's verify_sel best keys and their ties, so the slot merge stops there)
-  a.slot_out = verify_sel > 0 ? a.k : 0;
+  a.slot_out = verify_sel > 0 && !raw ? a.k : 0;
+  a.raw_lists = raw ? 1 : 0;
   // K13's pre-pass (kth_out): each list sample is scanned by one tile -- its rows are read once (non-temporal)
   a.rows_nt = kth_out != nullptr;
   a.flags = env_int("MIVS_PF_FLAGS", 0);
@@ -1592,7 +1594,8 @@ void rs_search(mivs_index_s* idx, hipStream_t s, const float* q, int64_t nq, int
                             ws.slot_begin.as<int64_t>(), ws.scan_tmp.p, stb, s));
     ws.pre_kth.reserve(sizeof(float) * nq);
     pf_scan_refine(idx, s, q, nq, k, 1, nullptr, nullptr, nullptr, ws.pre_goff.as<int64_t>(), nl2,
-                   ws.pre_kth.as<float>(), pre_sel, pre_f8);
+                   ws.pre_kth.as<float>(), pre_sel, pre_f8,
+                   engine_setting(kSetPfRawLists, "MIVS_PF_RAW_LISTS", 1) != 0);
   }
   // 2. headers (the pre-pass left the fp16 queries, their scales and residuals in ws.qh / qscale / qres)
   ws.qhdr.reserve(sizeof(float4) * (nq + 1));

@@ -254,6 +254,8 @@ struct PfScanArgs {
   int chunk_stride;           // max chunks per list
   int rows_nt;                // 1: the rows are read once (K13's pre-pass: one tile per list sample) -- load them
                               // with the non-temporal policy (pair mode only)
+  int raw_lists;              // 1: no per-slot merge -- each slot is the query's 16 lane lists as they are (slot_k =
+                              // 16 x kPfLaneK, unsorted, +inf padded) and its bound; K11 / K11v rank every entry
   const uint8_t* groups_f8;   // optional (K13's pre-pass nomination, pair mode): fp8 rows (launch_groups_to_f8);
   const uint8_t* q8;          //   then the fp8 queries (launch_queries_to_f8) and their scales replace groups_h,
   const float* qscale8;       //   qh and qscale
@@ -437,7 +439,7 @@ hipError_t launch_pf_refine(const PfRefineArgs& a, hipStream_t s);
 hipError_t launch_refine(const RefineArgs& a, hipStream_t s);
 // engine switches the kernel launchers read: the environment variable's integer value, read once and
 // kept until mivs_reload_settings (capi.cpp) -- one getenv per process, not per call
-enum EngineSetting { kSetRefineGather = 0, kSetSelectSlotsWave = 1, kSetCount = 2 };
+enum EngineSetting { kSetRefineGather = 0, kSetSelectSlotsWave = 1, kSetPfRawLists = 2, kSetCount = 3 };
 int engine_setting(EngineSetting id, const char* name, int dflt);
 void engine_settings_reset();
 size_t rs_scan_lds_bytes(int dp);

@@ -514,6 +514,35 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
     const unsigned long long pr_d = a.prof ? __builtin_amdgcn_s_memtime() : 0;
     __syncthreads();  // the B image is dead
     const unsigned long long pr_e = a.prof ? __builtin_amdgcn_s_memtime() : 0;
+    if (a.raw_lists) {
+      // raw slots (slot_k = 16 lists x kPfLaneK): every lane's two lists straight into its queries' slots, unsorted --
+      // K11 and K11v rank all of a slot's entries -- and per query the dropped-key bound (as the merge's: the 16 lists'
+      // last entries, +inf where a list is not full, and the theta term), one thread per query from the list ends the
+      // epilogues published in s_l8. No per-query merge rounds (the pre-pass's took ~0.1 of its time, in the three
+      // waves holding a list's ~10 queries while the other five waited).
+      const int64_t sl0 = s_slot[j], sl1 = s_slot[32 + j];
+      if (sl0 >= 0) {
+        float* kd = a.slot_key + sl0 * a.slot_k + src * kPfLaneK;
+        int* pd = a.slot_pos + sl0 * a.slot_k + src * kPfLaneK;
+#pragma unroll
+        for (int i = 0; i < kPfLaneK; ++i) { kd[i] = lk0[i]; pd[i] = lp0[i]; }
+      }
+      if (sl1 >= 0) {
+        float* kd = a.slot_key + sl1 * a.slot_k + src * kPfLaneK;
+        int* pd = a.slot_pos + sl1 * a.slot_k + src * kPfLaneK;
+#pragma unroll
+        for (int i = 0; i < kPfLaneK; ++i) { kd[i] = lk1[i]; pd[i] = lp1[i]; }
+      }
+      if (a.slot_bound && tid < kPfQTile) {
+        const int64_t sl = s_slot[tid];
+        if (sl >= 0) {
+          float bnd = nextafterf(fminf(s_th[tid], pf_theta(s_l8 + tid * 16, s_dl[tid], mth)), INFINITY);
+#pragma unroll
+          for (int i = 0; i < 16; ++i) bnd = fminf(bnd, s_l8[tid * 16 + i]);
+          a.slot_bound[sl] = bnd;
+        }
+      }
+    } else {
     {
 #pragma unroll
       for (int i = 0; i < kPfLaneK; ++i) {
@@ -608,6 +637,7 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
       }
       if (src == 0 && slot >= 0) a.slot_bound[slot] = bnd;
     }
+    }  // (raw_lists)
     __syncthreads();
     if (a.prof) {
       const unsigned long long pr_f = __builtin_amdgcn_s_memtime();
@@ -1647,6 +1677,7 @@ static hipError_t launch_pf_scan_m(const PfScanArgs& a, int grid, size_t lds, hi
 hipError_t launch_pf_scan(const PfScanArgs& a, int grid, size_t lds, hipStream_t s) {
   if (a.dp % 64 != 0 || a.dp > 1024 || lds > 160 * 1024) return hipErrorInvalidValue;
   if (a.k < 1 || a.k > 4 * kPfLaneK || a.k > a.slot_k) return hipErrorInvalidValue;  // (pf_theta: 4 lane lists)
+  if (a.raw_lists && a.slot_k != 16 * kPfLaneK) return hipErrorInvalidValue;          // (a slot = the 16 lane lists)
   return a.metric == kIP ? launch_pf_scan_m<kIP>(a, grid, lds, s) : launch_pf_scan_m<kL2>(a, grid, lds, s);
 }
 

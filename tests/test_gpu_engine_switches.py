@@ -85,6 +85,7 @@ SEARCH_SWITCHES = [
     {"MIVS_FALLBACK_SYNC": "1"},                                      # fallback sized on the host (round 4)
     {"MIVS_FALLBACK_SYNC": "1", "MIVS_RS_QCAP": "4"},
     {"MIVS_FALLBACK_SYNC": "1", "MIVS_RS_WAVE_CAP": "2"},
+    {"MIVS_PF_RAW_LISTS": "0"},                                       # pre-pass slots merged in K10 (round 6)
 ]
 
 
@@ -329,6 +330,49 @@ def test_coarse_probe_equals_oracle(ivf, flat_data, n_probes):
     np.testing.assert_array_equal(p0.cpu().numpy(), op)
     np.testing.assert_array_equal(i0.cpu().numpy(), oi)
     np.testing.assert_array_equal(_bits(d0.cpu().numpy()), _bits(od))
+
+
+@pytest.mark.parametrize("dup", ["exact", "near"])
+def test_coarse_probe_tied_centroids(flat_data, mivs_lib, dup):
+    """centroids 32..63 duplicate 0..31 exactly (every probe key tied, resolved to the lower id) or up to a 1e-6 nudge:
+    the coarse probe (K3w DUMP + K8s above 16 probes) gives the oracle's probes in order, and the search its answer"""
+    from mivs.neighbors import ivf_flat
+
+    x, q = flat_data
+    rng = np.random.default_rng(11)
+    c = x[rng.choice(x.shape[0], 32, replace=False)].copy()
+    c2 = c.copy()
+    if dup == "near":
+        c2 += 1e-6 * rng.standard_normal(c2.shape).astype(np.float32)
+    cents = np.concatenate([c, c2]).astype(np.float32)
+    idx = ivf_flat.build_from_centroids(torch.from_numpy(cents).cuda(), torch.from_numpy(x[:20_000]).cuda())
+    try:
+        qd = torch.from_numpy(q).cuda()
+        for n_probes in (20, 32):
+            p0 = torch.empty((q.shape[0], n_probes), dtype=torch.int32, device="cuda")
+            d0, i0 = ivf_flat.search(ivf_flat.SearchParams(n_probes=n_probes), idx, qd, 10, probes_out=p0)
+            od, oi, op = O.ivf_search(x[:20_000], cents, idx.list_sizes.numpy(), idx.list_ids().cpu().numpy(), q,
+                                      n_probes, 10)
+            np.testing.assert_array_equal(p0.cpu().numpy(), op)
+            np.testing.assert_array_equal(i0.cpu().numpy(), oi)
+            np.testing.assert_array_equal(_bits(d0.cpu().numpy()), _bits(od))
+    finally:
+        idx.close()
+
+
+def test_prepass_raw_lists_same_candidates(ivf, flat_data, monkeypatch):
+    """round 6: the pre-pass's K10 leaves each slot as its 16 lane lists (K11v ranks all of them) instead of merging
+    the best verify_sel in K10: the same nominees, so the same T_q, the same K13 candidates and the same answer"""
+    idx, _ = ivf
+    _, q = flat_data
+    d0, i0 = _search(idx, q)
+    st0 = idx.last_search_stats()
+    _setenv(monkeypatch, "MIVS_PF_RAW_LISTS", "0")
+    d1, i1 = _search(idx, q)
+    st1 = idx.last_search_stats()
+    np.testing.assert_array_equal(i1, i0)
+    np.testing.assert_array_equal(_bits(d1), _bits(d0))
+    assert st0["candidates"] == st1["candidates"] > 0
 
 
 def test_k13_lost_stream_fallback_is_exact_and_reported(ivf, flat_data, monkeypatch):
