@@ -897,11 +897,24 @@ __device__ __forceinline__ int rs_group_hist(const int4* __restrict__ wave_buf, 
                                              int* bins, int* pre) {
   for (int i = threadIdx.x; i < nq; i += blockDim.x) bins[i] = 0;
   const int n = rs_group_prefix(wave_cnt, wave_cap, J, pre);  // (its barrier also orders the zeroing)
-  for (int e = threadIdx.x; e < n; e += blockDim.x) {
-    const RsRec r = rs_rec_load(rs_group_rec(wave_buf, wave_cap, J, pre, e));
-    float xn[8];
-    const unsigned m = rs_rec_hits<METRIC>(r, qhdr[r.q], row_norms, xn);
-    if (m) atomicAdd(bins + r.q, __popc(m));
+  // two records per thread and round, their loads issued together (a record, then its header and row norms: two
+  // dependent memory rounds each)
+  for (int e0 = threadIdx.x; e0 < n; e0 += 2 * blockDim.x) {
+    RsRec r[2];
+    float4 h[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = e0 + u * (int)blockDim.x;
+      r[u] = rs_rec_load(rs_group_rec(wave_buf, wave_cap, J, pre, e < n ? e : e0));
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) h[u] = qhdr[r[u].q];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float xn[8];
+      const unsigned m = rs_rec_hits<METRIC>(r[u], h[u], row_norms, xn);
+      if (m && e0 + u * (int)blockDim.x < n) atomicAdd(bins + r[u].q, __popc(m));
+    }
   }
   __syncthreads();
   return n;
@@ -959,29 +972,52 @@ __global__ __launch_bounds__(1024) void k_rs_bucket_fused(const int4* __restrict
   extern __shared__ int bins[];
   __shared__ int pre[kRsMaxGroupStreams + 1];
   const int n = rs_group_hist<METRIC>(wave_buf, wave_cap, wave_cnt, J, nq, qhdr, row_norms, bins, pre);
-  for (int i = threadIdx.x; i < nq; i += blockDim.x) {
-    const int c = bins[i];
-    if (c) bins[i] = atomicAdd(qcnt + i, c);  // the group's first entry in query i's run
+  // the group's first entry in each query's run: eight returning atomics in flight per thread (one after another,
+  // each waited for its L2 round trip)
+  constexpr int U = 8;
+  for (int i0 = threadIdx.x; i0 < nq; i0 += U * (int)blockDim.x) {
+    int c[U], at[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * (int)blockDim.x;
+      c[u] = i < nq ? bins[i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) at[u] = c[u] ? atomicAdd(qcnt + i0 + u * (int)blockDim.x, c[u]) : 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (c[u]) bins[i0 + u * (int)blockDim.x] = at[u];
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < n; e += blockDim.x) {
-    const RsRec r = rs_rec_load(rs_group_rec(wave_buf, wave_cap, J, pre, e));
-    const float4 h = qhdr[r.q];
-    float xn[8];
-    const unsigned m = rs_rec_hits<METRIC>(r, h, row_norms, xn);
-    if (!m) continue;
-    int at = atomicAdd(bins + r.q, __popc(m));
-    const int64_t base = (int64_t)r.q * cap;
+  for (int e0 = threadIdx.x; e0 < n; e0 += 2 * blockDim.x) {
+    RsRec r[2];
+    float4 h[2];
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-      if (m & (1u << i)) {
-        if (at < cap) {
-          const float c = i < 4 ? r.c0[i] : r.c1[i - 4];
-          key[base + at] = pf_key<METRIC>(c, h.x, xn[i], h.z);
-          pos[base + at] = rs_rec_row(r.pos0, i);
+    for (int u = 0; u < 2; ++u) {
+      const int e = e0 + u * (int)blockDim.x;
+      r[u] = rs_rec_load(rs_group_rec(wave_buf, wave_cap, J, pre, e < n ? e : e0));
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) h[u] = qhdr[r[u].q];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (e0 + u * (int)blockDim.x >= n) continue;
+      float xn[8];
+      const unsigned m = rs_rec_hits<METRIC>(r[u], h[u], row_norms, xn);
+      if (!m) continue;
+      int at = atomicAdd(bins + r[u].q, __popc(m));
+      const int64_t base = (int64_t)r[u].q * cap;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (m & (1u << i)) {
+          if (at < cap) {
+            const float c = i < 4 ? r[u].c0[i] : r[u].c1[i - 4];
+            key[base + at] = pf_key<METRIC>(c, h[u].x, xn[i], h[u].z);
+            pos[base + at] = rs_rec_row(r[u].pos0, i);
+          }
+          ++at;
         }
-        ++at;
-      }
+    }
   }
 }
 
