@@ -658,7 +658,7 @@ __global__ __launch_bounds__(kPfThreads, 1) void k_pf_scan(PfScanArgs a) {
 
 // K11. One wave per query (4 per workgroup; every wave reaches every barrier).
 template <int METRIC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_pf_refine(PfRefineArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_pf_refine(PfRefineArgs a) {
   __shared__ float s_ck[4][kPfCap];
   __shared__ int s_cp[4][kPfCap];
   __shared__ __attribute__((aligned(16))) float s_qv[4][1024];
@@ -789,7 +789,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     const int nB = a.dp >> 6;
     const float* qv = s_qv[wv];
     float* s_dot = s_ck[wv];  // (the window's approximate keys are dead: their slots take the dots)
-    constexpr int CH = 12;    // 64-dim blocks of a pass in flight (d = 768: the whole row)
+    // 64-dim blocks of a pass in flight: 4 (64 VGPRs, 8 waves / SIMD) rather than the whole row at once (CH 12: 128
+    // VGPRs, 4 waves): more queries in flight hide the rows' latency better -- 153-159 vs 175-178 us per 10k-query
+    // refine, CH 6 at 6 waves 158-160 us (alternating runs, profiles/r06x_k11_occupancy.txt)
+    constexpr int CH = 4;
     for (int r0 = 0; r0 < cnt; r0 += 8) {
       const int rj = r0 + j8;
       const float* rowp = a.groups + row_elem(s_cp[wv][rj < cnt ? rj : r0], 0, a.dp) + 8 * p8;
@@ -860,7 +863,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
 // the nominees and the k-th smallest of them (a kernel of its own: inside K11 its code changed how the compiler
 // unrolled K11's exact recompute, 0.18 -> 0.33 ms per final refine)
 template <int METRIC>
-__global__ __launch_bounds__(256) void k_pf_verify(PfRefineArgs a) {
+// (8 waves / SIMD, 64 VGPRs: 82 vs 85-88 us at its own 76-VGPR 6-wave default, profiles/r06x_k11_occupancy.txt)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_pf_verify(PfRefineArgs a) {
   __shared__ int s_cp[4][kPfCap];
   __shared__ __attribute__((aligned(16))) float s_qv[4][1024];
   const int lane = threadIdx.x & 63;
