@@ -167,9 +167,11 @@ __device__ __forceinline__ void rf_raw_cvt(const typename RfRaw<T>::type& r, flo
   }
 }
 
+constexpr int kRfCh = 12;  // K14g: 64-dim blocks of a row in flight per pass (d = 768: the whole row)
+
 template <int METRIC, typename T, bool PF>
 __global__ __launch_bounds__(256) void k_refine_g(RefineArgs a) {
-  constexpr int CH = 12;  // 64-dim blocks of a row in flight per pass (d = 768: the whole row)
+  constexpr int CH = kRfCh;  // (PF loads the next pass's whole rows: valid only for dp <= 64 CH, checked at launch)
   typedef typename RfRaw<T>::type Raw;
   __shared__ __attribute__((aligned(16))) float s_q[4][1024];
   __shared__ float s_key[4][64];
@@ -341,7 +343,7 @@ hipError_t launch_refine(const RefineArgs& a, hipStream_t s) {
   const bool gather = !lane_per_row && (a.d & 7) == 0 && (a.dp & 63) == 0 &&
                       (reinterpret_cast<uintptr_t>(a.data) & 15) == 0;
   if (gather) {
-    const bool pf = a.dp <= 768;  // (fp16 rows: the next pass's 12 blocks fit beside the current pass's)
+    const bool pf = a.dp <= 64 * kRfCh;  // (fp16 rows: the next pass's CH blocks fit beside the current pass's)
     if (a.half && pf) {
       if (a.metric == kIP) hipLaunchKernelGGL((k_refine_g<kIP, _Float16, true>), grid, dim3(256), 0, s, a);
       else hipLaunchKernelGGL((k_refine_g<kL2, _Float16, true>), grid, dim3(256), 0, s, a);
